@@ -1,0 +1,127 @@
+"""Seeded synthetic weights and batches.
+
+There is no network in this environment, so no pretrained HuBERT checkpoint is
+available.  Every parity fixture, test and benchmark therefore uses weights made
+by :func:`seeded_tensor`, a pure function of ``(seed, parameter name, shape)``:
+the golden generator (``tools/gen_golden.py``) fills the *reference* model with
+it, and the tests fill this package's model with it, so both see bit-identical
+fp32 parameters without shipping a checkpoint.
+
+Magnitudes mimic a trained model closely enough that activations stay O(1)
+through 12 post-norm layers (fan-in scaled weights, LN gains near 1).
+HardConcrete ``log_alpha`` follows the reference init
+(wav2vec2/hardconcrete.py:70-74: ``normal(log(1-m) - log(m), 0.01)``).
+"""
+
+import math
+import zlib
+from typing import Dict, Iterable, Tuple
+
+import torch
+
+__all__ = [
+    "HUBERT_BASE_CONFIG",
+    "HUBERT_LARGE_CONFIG",
+    "seeded_tensor",
+    "seeded_state_dict",
+    "synthetic_batch",
+]
+
+# default config of HuBERT Base, as written by convert_hubert_from_hf.py:18-44
+HUBERT_BASE_CONFIG = dict(
+    extractor_mode="group_norm",
+    extractor_conv_layer_config=[(512, 10, 5)] + [(512, 3, 2)] * 4 + [(512, 2, 2)] * 2,
+    extractor_conv_bias=False,
+    encoder_embed_dim=768,
+    encoder_projection_dropout=0.1,
+    encoder_pos_conv_kernel=128,
+    encoder_pos_conv_groups=16,
+    encoder_num_layers=12,
+    encoder_use_attention=[True] * 12,
+    encoder_use_feed_forward=[True] * 12,
+    encoder_num_heads=[12] * 12,
+    encoder_head_dim=64,
+    encoder_attention_dropout=0.1,
+    encoder_ff_interm_features=[3072] * 12,
+    encoder_ff_interm_dropout=0.0,
+    encoder_dropout=0.1,
+    encoder_layer_norm_first=False,
+    encoder_layer_drop=0.05,
+    aux_num_out=None,
+    normalize_waveform=False,
+    extractor_prune_conv_channels=False,
+    encoder_prune_attention_heads=False,
+    encoder_prune_attention_layer=False,
+    encoder_prune_feed_forward_intermediate=False,
+    encoder_prune_feed_forward_layer=False,
+)
+
+# wav2vec2-large teacher of run_large.sh (convert_wav2vec2_large_from_fairseq.py:19-40)
+HUBERT_LARGE_CONFIG = dict(
+    HUBERT_BASE_CONFIG,
+    extractor_mode="layer_norm",
+    extractor_conv_bias=True,
+    encoder_embed_dim=1024,
+    encoder_projection_dropout=0.0,
+    encoder_num_layers=24,
+    encoder_use_attention=[True] * 24,
+    encoder_use_feed_forward=[True] * 24,
+    encoder_num_heads=[16] * 24,
+    encoder_attention_dropout=0.0,
+    encoder_ff_interm_features=[4096] * 24,
+    encoder_dropout=0.0,
+    encoder_layer_norm_first=True,
+    encoder_layer_drop=0.0,
+    normalize_waveform=True,
+)
+
+
+def _gen(seed: int, name: str) -> torch.Generator:
+    g = torch.Generator()
+    g.manual_seed((int(seed) * 1000003 + zlib.crc32(name.encode())) % (2**63 - 1))
+    return g
+
+
+def seeded_tensor(name: str, shape: Tuple[int, ...], seed: int = 0) -> torch.Tensor:
+    """Deterministic fp32 value for parameter ``name`` of ``shape``."""
+    shape = tuple(int(s) for s in shape)
+    g = _gen(seed, name)
+    leaf = name.rsplit(".", 1)[-1]
+    if leaf == "dummy_weight":
+        return torch.ones(shape)
+    if leaf == "log_alpha":
+        # reference init: interm units use init_mean=0.5, everything else 0.01
+        # (components.py:90,370,375,715-722)
+        init_mean = 0.5 if "hard_concrete_for_intermediate" in name else 0.01
+        mean = math.log(1 - init_mean) - math.log(init_mean)
+        return torch.randn(shape, generator=g) * 0.01 + mean
+    if leaf == "weight_g":
+        return 2.4 * (1.0 + 0.1 * torch.randn(shape, generator=g))
+    if leaf == "weight_v":
+        return torch.randn(shape, generator=g)
+    is_norm = ("layer_norm" in name) or ("final_layer_norm" in name)
+    if leaf == "weight" and is_norm:
+        return 1.0 + 0.1 * torch.randn(shape, generator=g)
+    if leaf == "bias":
+        return (0.1 if is_norm else 0.02) * torch.randn(shape, generator=g)
+    if leaf == "weight":
+        fan_in = 1
+        for s in shape[1:]:
+            fan_in *= s
+        return torch.randn(shape, generator=g) / math.sqrt(max(fan_in, 1))
+    if leaf in ("lambda1", "lambda2"):
+        return torch.zeros(shape)
+    return 0.02 * torch.randn(shape, generator=g)
+
+
+def seeded_state_dict(shapes: Iterable[Tuple[str, Tuple[int, ...]]], seed: int = 0) -> Dict[str, torch.Tensor]:
+    return {n: seeded_tensor(n, s, seed) for n, s in shapes}
+
+
+def synthetic_batch(batch: int, samples: int = 160000, seed: int = 2022):
+    """``0.1*randn(B,S)`` waveforms + full lengths."""
+    g = torch.Generator()
+    g.manual_seed(seed)
+    wave = 0.1 * torch.randn(batch, samples, generator=g)
+    lengths = torch.full((batch,), samples, dtype=torch.int64)
+    return wave, lengths

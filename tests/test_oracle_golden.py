@@ -1,0 +1,125 @@
+"""Pin the CPU oracle (oracle/hubert_ref.py) against golden vectors produced by
+importing the reference itself (tools/gen_golden.py).  CPU only."""
+
+import math
+
+import pytest
+import torch
+
+from helpers import ck_close, load_golden, proj_sd_from_recipe, rel_l2, seeded_sd, wave_batch
+from oracle import hubert_ref as ref
+
+
+@pytest.fixture(scope="module")
+def g1():
+    return load_golden("g1_ops.pt")
+
+
+@pytest.mark.parametrize("key", ["hc_12", "hc_64", "hc_1"])
+def test_hardconcrete(g1, key):
+    d = g1[key]
+    m = ref.hc_sample(d["log_alpha"], d["u"])
+    torch.testing.assert_close(m, d["mask"], rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(ref.hc_l0_norm(d["log_alpha"]), d["l0"], rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(ref.hc_eval_mask(d["log_alpha"]), d["eval_mask"], rtol=1e-6, atol=1e-7)
+
+
+def test_distill_loss(g1):
+    keys = [k for k in g1 if k.startswith("loss_")]
+    assert len(keys) == 4
+    for k in keys:
+        d = g1[k]
+        cos_type = k.split("_")[1] if not k.startswith("loss_log_sig") else "log_sig"
+        w = d["w"].tolist()
+        s = d["s"].clone().requires_grad_(True)
+        loss, (mse, l1, cos) = ref.distill_loss(s, d["t"], w[0], w[1], w[2], cos_type)
+        loss.backward()
+        torch.testing.assert_close(loss.detach(), d["loss"], rtol=1e-6, atol=1e-6)
+        torch.testing.assert_close(l1.detach(), d["l1"], rtol=1e-6, atol=1e-6)
+        torch.testing.assert_close(cos.detach(), d["cos"], rtol=1e-6, atol=1e-6)
+        torch.testing.assert_close(s.grad, d["grad"], rtol=1e-5, atol=1e-7)
+
+
+def test_num_params(g1):
+    d = g1["num_params"]
+    sd = seeded_sd(d["cfg"], d["seed"])
+    v = ref.get_num_params(sd, d["cfg"])
+    assert abs(float(v) - float(d["value"])) <= 1e-6 * float(d["value"])
+    base = {k: v for k, v in d["cfg"].items()}
+    for f in ("extractor_prune_conv_channels", "encoder_prune_attention_heads", "encoder_prune_attention_layer",
+              "encoder_prune_feed_forward_intermediate", "encoder_prune_feed_forward_layer"):
+        base[f] = False
+    assert sum(math.prod(s) for _, s in ref.state_dict_shapes(base)) == d["teacher_numel"]
+
+
+def test_lr_schedule_formula():
+    # lightning.py:37-44 restated; spot values
+    assert ref.linear_decay_lr(1, 2e-4, 15000, 50000) == pytest.approx(2e-4 / 15000)
+    assert ref.linear_decay_lr(15000, 2e-4, 15000, 50000) == pytest.approx(2e-4)
+    assert ref.linear_decay_lr(32500, 2e-4, 15000, 50000) == pytest.approx(1e-4)
+    assert ref.linear_decay_lr(50000, 2e-4, 15000, 50000) == 0.0
+
+
+def _run_fixture(fx):
+    tcfg, scfg, seed = fx["tcfg"], fx["scfg"], fx["seed"]
+    tsd = seeded_sd(tcfg, seed)
+    ssd = seeded_sd(scfg, seed)
+    n_proj = max(fx["proj_index"]) + 1
+    psd = proj_sd_from_recipe(n_proj, scfg["encoder_embed_dim"], seed)
+    lengths = fx["lengths"]
+    wave, ln = wave_batch(fx["B"], fx["S"], lengths=None if lengths is None else lengths.tolist())
+    out = ref.distill_step(tsd, tcfg, ssd, scfg, psd, fx["distill_layers"], fx["proj_index"], wave,
+                           ln if lengths is not None else None, fx["u"], fx["lambdas"], fx["global_step"],
+                           l2_weight=fx["l2"], cos_type=fx["cos_type"],
+                           original_num_params=fx["original_num_params"])
+    return out
+
+
+def _check_step(fx, out, tol_loss=1e-5, tol_ck=1e-4):
+    assert abs(out["loss"].item() - fx["loss"].item()) <= tol_loss * max(1.0, abs(fx["loss"].item()))
+    lg = fx["logged"]
+    assert abs(out["loss_distill"].item() - lg["train_loss_distill"].item()) <= tol_loss
+    assert abs(out["loss_l1"].item() - lg["train_loss_l1"].item()) <= tol_loss
+    assert abs(out["loss_cos"].item() - lg["train_loss_cos"].item()) <= tol_loss
+    if fx["lambdas"] is not None:
+        assert abs(out["expected_sparsity"].item() - lg["sparsity_expected"].item()) <= 1e-6
+        assert abs(out["target_sparsity"] - float(lg["sparsity_target"])) <= 1e-7
+        for a, b in zip(out["lambda_grads"], fx["lambda_grads"]):
+            assert abs(a.item() - b.item()) <= 1e-6 + 1e-5 * abs(b.item())
+    for h, ck in zip(out["student_hiddens"], fx["student_hidden_ck"]):
+        e_sample, e_sq = ck_close(h, ck)
+        assert e_sample < tol_ck and e_sq < tol_ck, (e_sample, e_sq)
+    for h, ck in zip(out["teacher_hiddens"], fx["teacher_hidden_ck"]):
+        e_sample, e_sq = ck_close(h, ck)
+        assert e_sample < tol_ck and e_sq < tol_ck, (e_sample, e_sq)
+    for n, g in fx["log_alpha_grads"].items():
+        assert rel_l2(out["grads"][n], g) < 1e-3, n
+    for n, ck in fx["grad_ck"].items():
+        if n.endswith("k_proj.bias"):
+            # softmax is shift-invariant per query row, so d/dk_bias is exactly 0;
+            # both sides hold only rounding noise (~1e-9), nothing to compare.
+            assert out["grads"][n].abs().max().item() < 1e-5
+            continue
+        e_sample, e_sq = ck_close(out["grads"][n], ck)
+        assert e_sq < 1e-3, (n, e_sq)
+
+
+def test_smoke_step_g2():
+    fx = load_golden("g2_smoke_step.pt")
+    out = _run_fixture(fx)
+    _check_step(fx, out)
+    for h, g in zip(out["student_hiddens"], fx["student_hiddens"]):
+        assert rel_l2(h, g) < 1e-5
+
+
+def test_all_units_padded_g2b():
+    fx = load_golden("g2b_all_units_padded.pt")
+    out = _run_fixture(fx)
+    _check_step(fx, out)
+
+
+@pytest.mark.slow
+def test_base12_g3():
+    fx = load_golden("g3_base12.pt")
+    out = _run_fixture(fx)
+    _check_step(fx, out, tol_loss=2e-5, tol_ck=5e-4)

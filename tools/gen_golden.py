@@ -1,0 +1,323 @@
+"""Generate golden parity fixtures by importing the REFERENCE (build container only).
+
+Run:  PYTHONDONTWRITEBYTECODE=1 python tools/gen_golden.py
+
+The reference (/root/reference, read-only) is imported in-process with two
+light stubs injected into sys.modules (pytorch_lightning and torchaudio are not
+installed).  Nothing from the reference is copied: the outputs
+written to tests/golden/*.pt are pure data (inputs, expected outputs,
+checksums) loadable with ``torch.load(..., weights_only=True)``.
+
+Weights come from dphubert_amd.synthetic.seeded_tensor, so the tests rebuild
+the exact same fp32 parameters without shipping a checkpoint.  HardConcrete
+noise ``u`` is recorded by wrapping ``Tensor.uniform_`` while each
+HardConcrete module runs, so the oracle can replay it.
+"""
+
+import copy
+import os
+import sys
+import types
+from pathlib import Path
+
+import torch
+
+REPO = Path(__file__).resolve().parents[1]
+REF = Path("/root/reference")
+OUT = REPO / "tests" / "golden"
+sys.path.insert(0, str(REPO))
+sys.dont_write_bytecode = True
+
+from dphubert_amd.synthetic import HUBERT_BASE_CONFIG, seeded_tensor  # noqa: E402
+
+
+def _install_stubs():
+    pl = types.ModuleType("pytorch_lightning")
+
+    class LightningModule(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.global_step = 0
+            self.logged = {}
+
+        def log_dict(self, d, **kw):
+            self.logged.update({k: (v.detach().clone() if torch.is_tensor(v) else v) for k, v in d.items()})
+
+    pl.LightningModule = LightningModule
+    cb = types.ModuleType("pytorch_lightning.callbacks")
+    cb.ModelCheckpoint = object
+    cb.LearningRateMonitor = object
+    pl.callbacks = cb
+    sys.modules["pytorch_lightning"] = pl
+    sys.modules["pytorch_lightning.callbacks"] = cb
+    ta = types.ModuleType("torchaudio")
+    sys.modules["torchaudio"] = ta
+
+
+_install_stubs()
+sys.path.insert(0, str(REF))
+from wav2vec2.model import wav2vec2_model  # noqa: E402  (reference)
+from wav2vec2.hardconcrete import HardConcrete  # noqa: E402  (reference)
+import lightning as ref_lightning  # noqa: E402  (reference)
+
+
+def checksum(t: torch.Tensor) -> dict:
+    t = t.detach().double().flatten()
+    n = t.numel()
+    idx = torch.linspace(0, n - 1, min(64, n)).long()
+    return {"n": n, "sum": t.sum().item(), "abs": t.abs().sum().item(), "sq": (t * t).sum().item(),
+            "head": t[:16].float().clone(), "sample_idx": idx, "sample": t[idx].float().clone()}
+
+
+def seeded_model(cfg, seed):
+    m = wav2vec2_model(**copy.deepcopy(cfg))
+    sd = {k: seeded_tensor(k, v.shape, seed) for k, v in m.state_dict().items()}
+    m.load_state_dict(sd, strict=True)
+    return m, sd
+
+
+class URecorder:
+    """Record HardConcrete noise u per module (in call order)."""
+
+    def __init__(self, model):
+        self.cur = None
+        self.u = {}
+        self.hooks = []
+        for name, mod in model.named_modules():
+            if isinstance(mod, HardConcrete):
+                self.hooks.append(mod.register_forward_pre_hook(self._pre(name)))
+
+    def _pre(self, name):
+        def f(mod, inp):
+            self.cur = name
+        return f
+
+    def __enter__(self):
+        self._orig = torch.Tensor.uniform_
+        rec = self
+
+        def uniform_(t, *a, **k):
+            r = rec._orig(t, *a, **k)
+            if rec.cur is not None:
+                rec.u[rec.cur] = t.detach().clone()
+                rec.cur = None
+            return r
+
+        torch.Tensor.uniform_ = uniform_
+        return self
+
+    def __exit__(self, *exc):
+        torch.Tensor.uniform_ = self._orig
+        for h in self.hooks:
+            h.remove()
+
+
+def no_dropout(cfg):
+    c = copy.deepcopy(cfg)
+    c.update(encoder_projection_dropout=0.0, encoder_attention_dropout=0.0, encoder_ff_interm_dropout=0.0,
+             encoder_dropout=0.0, encoder_layer_drop=0.0)
+    return c
+
+
+def small_cfg(n_layers, **kw):
+    c = no_dropout(HUBERT_BASE_CONFIG)
+    c.update(encoder_num_layers=n_layers, encoder_use_attention=[True] * n_layers,
+             encoder_use_feed_forward=[True] * n_layers, encoder_num_heads=[12] * n_layers,
+             encoder_ff_interm_features=[3072] * n_layers)
+    c.update(kw)
+    return c
+
+
+def units_flags(units):
+    return dict(extractor_prune_conv_channels="conv" in units, encoder_prune_attention_heads="head" in units,
+                encoder_prune_attention_layer="attlayer" in units,
+                encoder_prune_feed_forward_intermediate="interm" in units,
+                encoder_prune_feed_forward_layer="ffnlayer" in units)
+
+
+def wave_batch(B, S, seed=2022, lengths=None):
+    g = torch.Generator()
+    g.manual_seed(seed)
+    w = 0.1 * torch.randn(B, S, generator=g)
+    if lengths is None:
+        lengths = [S] * B
+    ln = torch.tensor(lengths, dtype=torch.int64)
+    for b, l in enumerate(lengths):
+        w[b, l:] = 0.0
+    return w, ln
+
+
+def run_step(tcfg, scfg, distill_layers_str, B, S, units, lambdas, global_step, seed=0, lengths=None,
+             full=False, cos_type="raw", l2=0.0):
+    """Run the reference DistillModule._step + backward; return a fixture dict."""
+    scfg = dict(scfg, **units_flags(units))
+    teacher, tsd = seeded_model(tcfg, seed)
+    student, ssd = seeded_model(scfg, seed)   # student init = teacher weights (run.sh:20) + seeded log_alpha
+    for p in teacher.parameters():
+        p.requires_grad = False
+    groups = [[int(x) for x in g.split(",")] for g in distill_layers_str.split(".")]
+    layers, projs, proj_index = [], torch.nn.ModuleList(), []
+    D = scfg["encoder_embed_dim"]
+    proj_sd = {}
+    for gi, g in enumerate(groups):
+        lin = torch.nn.Linear(D, tcfg["encoder_embed_dim"])
+        # identity init (distill.py:24-26) perturbed by a seeded delta so grads are non-trivial
+        with torch.no_grad():
+            lin.weight.copy_(torch.eye(D) + seeded_tensor(f"proj{gi}.weight", (D, D), seed) * 0.05)
+            lin.bias.copy_(seeded_tensor(f"proj{gi}.bias", (D,), seed))
+        proj_sd[f"{gi}.weight"] = lin.weight.detach().clone()
+        proj_sd[f"{gi}.bias"] = lin.bias.detach().clone()
+        for l in g:
+            layers.append(l)
+            projs.append(lin)
+            proj_index.append(gi)
+    loss_mod = ref_lightning.DistillLoss(l2_weight=l2, l1_weight=1.0, cos_weight=1.0, cos_type=cos_type)
+    use_reg = lambdas is not None
+    dm = ref_lightning.DistillModule(
+        teacher_model=teacher, student_model=student, distill_mode="layer2layer", distill_layers=layers,
+        distill_linear_projs=projs, distill_loss=loss_mod, learning_rate=2e-4, weight_decay=0.0,
+        warmup_updates=15000, max_updates=50000, use_reg=use_reg, reg_learning_rate=0.02 if use_reg else None,
+        target_sparsity=0.75 if use_reg else None, sparsity_warmup_updates=5000 if use_reg else None,
+        tsv_dir=".", train_subset="train100", seconds_per_batch=160, num_workers=0)
+    if use_reg:
+        with torch.no_grad():
+            dm.lambda1.fill_(lambdas[0])
+            dm.lambda2.fill_(lambdas[1])
+    dm.global_step = global_step
+    dm.train()
+    wave, ln = wave_batch(B, S, lengths=lengths)
+    # capture student hiddens through a wrapper around extract_features
+    cap = {}
+    orig_ef = student.extract_features
+
+    def ef(*a, **k):
+        r = orig_ef(*a, **k)
+        cap["h"] = [x.detach().clone() for x in r[0]]
+        return r
+
+    student.extract_features = ef
+    torch.manual_seed(1234)
+    with URecorder(student) as rec:
+        loss = dm._step((wave, ln if lengths is not None else None), 0, "train")
+    loss.backward()
+    with torch.no_grad():
+        th, _ = teacher.extract_features(wave, ln if lengths is not None else None)
+    fx = {
+        "tcfg": tcfg, "scfg": scfg, "seed": seed, "B": B, "S": S, "lengths": ln if lengths is not None else None,
+        "distill_layers": layers, "proj_index": proj_index,
+        "proj_recipe": "eye(D) + 0.05*seeded_tensor('proj{g}.weight'); bias seeded_tensor('proj{g}.bias')",
+        "lambdas": list(lambdas) if use_reg else None, "global_step": global_step, "cos_type": cos_type, "l2": l2,
+        "u": rec.u, "loss": loss.detach(),
+        "logged": {k: (v if torch.is_tensor(v) else torch.tensor(float(v))) for k, v in dm.logged.items()},
+        "original_num_params": dm.original_num_params,
+        "student_hidden_ck": [checksum(h) for h in cap["h"]],
+        "teacher_hidden_ck": [checksum(h) for h in th],
+        "grad_ck": {n: checksum(p.grad) for n, p in student.named_parameters() if p.grad is not None},
+        "proj_grad_ck": {n: checksum(p.grad) for n, p in projs.named_parameters() if p.grad is not None},
+        "log_alpha_grads": {n: p.grad.detach().clone() for n, p in student.named_parameters()
+                            if n.endswith("log_alpha") and p.grad is not None},
+    }
+    if use_reg:
+        fx["lambda_grads"] = [dm.lambda1.grad.detach().clone(), dm.lambda2.grad.detach().clone()]
+    if full:
+        fx["student_hiddens"] = cap["h"]
+    return fx
+
+
+def gen_ops():
+    """G1: per-op fixtures at small shapes (full tensors)."""
+    torch.manual_seed(7)
+    out = {}
+    # HardConcrete train sample + l0 + eval mask (hardconcrete.py)
+    for n_in, init_mean in [(12, 0.01), (64, 0.5), (1, 0.01)]:
+        hc = HardConcrete(n_in, init_mean=init_mean)
+        with torch.no_grad():
+            hc.log_alpha.copy_(torch.randn(n_in) * 2.0)
+        hc.train()
+        with URecorder(hc) as rec:
+            m = hc()
+        u = rec.u[""]
+        hc.eval()
+        em = hc()
+        out[f"hc_{n_in}"] = {"log_alpha": hc.log_alpha.detach().clone(), "u": u, "mask": m.detach().clone(),
+                             "l0": hc.l0_norm().detach().clone(), "eval_mask": em.detach().clone()}
+    # distill loss (lightning.py:116-139)
+    s = torch.randn(2, 3, 7, 16)
+    t = torch.randn(2, 3, 7, 16)
+    for cos_type in ["raw", "log_sig"]:
+        for w in [(0.0, 1.0, 1.0), (0.5, 1.0, 2.0)]:
+            lm = ref_lightning.DistillLoss(l2_weight=w[0], l1_weight=w[1], cos_weight=w[2], cos_type=cos_type)
+            si = s.clone().requires_grad_(True)
+            loss, (mse, l1, cos) = lm(si, t)
+            loss.backward()
+            out[f"loss_{cos_type}_{w[0]}_{w[2]}"] = {
+                "s": s, "t": t, "w": torch.tensor(w), "loss": loss.detach(), "mse": torch.as_tensor(mse).detach(),
+                "l1": torch.as_tensor(l1).detach(), "cos": torch.as_tensor(cos).detach(), "grad": si.grad.clone()}
+    # expected #params with all five pruning units, seeded log_alpha (model.py:109)
+    cfg = small_cfg(3, **units_flags("conv,head,interm,attlayer,ffnlayer"))
+    m, sd = seeded_model(cfg, 3)
+    out["num_params"] = {"cfg": cfg, "seed": 3, "value": m.get_num_params().detach(),
+                         "teacher_numel": sum(p.numel() for p in seeded_model(small_cfg(3), 3)[0].parameters())}
+    # LR schedule formula (lightning.py:37-44); class itself fails on torch 2.10 (verbose kwarg)
+    return out
+
+
+def gen_prune():
+    """G4: eval-mode prune() round trip (model.py:115-125)."""
+    cfg = small_cfg(2, **units_flags("conv,head,interm,attlayer,ffnlayer"))
+    m, sd = seeded_model(cfg, 5)
+    g = torch.Generator()
+    g.manual_seed(11)
+    la = {}
+    with torch.no_grad():
+        for n, p in m.named_parameters():
+            if n.endswith("log_alpha"):
+                v = torch.randn(p.shape, generator=g) * 3.0 + (1.0 if p.numel() > 1 else 3.0)
+                p.copy_(v)
+                la[n] = v.clone()
+    wave, _ = wave_batch(1, 16000, seed=9)
+    res = m.prune()
+    conv_config, use_attention, use_feed_forward, num_heads, remaining_heads, ff_interm = res
+    # rebuild from the pruned config and reload, as prune.py:62-66,100-105 does
+    pcfg = dict(cfg, extractor_conv_layer_config=conv_config, encoder_use_attention=use_attention,
+                encoder_use_feed_forward=use_feed_forward, encoder_num_heads=num_heads,
+                encoder_ff_interm_features=ff_interm, extractor_prune_conv_channels=False,
+                encoder_prune_attention_heads=False, encoder_prune_attention_layer=False,
+                encoder_prune_feed_forward_intermediate=False, encoder_prune_feed_forward_layer=False)
+    pm = wav2vec2_model(**copy.deepcopy(pcfg))
+    pm.load_state_dict(m.state_dict(), strict=True)
+    pm.eval()
+    with torch.no_grad():
+        h, _ = pm.extract_features(wave)
+    return {"cfg": cfg, "seed": 5, "log_alpha": la, "conv_config": [list(x) for x in conv_config],
+            "use_attention": use_attention, "use_feed_forward": use_feed_forward, "num_heads": num_heads,
+            "ff_interm_features": ff_interm, "pruned_cfg": pcfg, "state_dict_ck": {k: checksum(v) for k, v in m.state_dict().items()},
+            "wave": wave, "pruned_hidden_ck": [checksum(x) for x in h]}
+
+
+def main():
+    OUT.mkdir(parents=True, exist_ok=True)
+    torch.set_num_threads(8)
+    torch.save(gen_ops(), OUT / "g1_ops.pt")
+    print("g1 done")
+    # G2: 2-layer smoke step (BASELINE config 1 shape-reduced to 2 s), units conv,head,interm, reg active
+    g2 = run_step(small_cfg(2), small_cfg(2), "0.1,2", B=2, S=32000, units="conv,head,interm",
+                  lambdas=(0.3, 0.2), global_step=1000, full=True)
+    torch.save(g2, OUT / "g2_smoke_step.pt")
+    print("g2 done", g2["loss"].item())
+    # G2b: all five units, padded batch (lengths), log_sig cosine + l2
+    g2b = run_step(small_cfg(2), small_cfg(2), "0.1,2", B=2, S=24000, units="conv,head,interm,attlayer,ffnlayer",
+                   lambdas=(-0.1, 0.05), global_step=7000, lengths=[24000, 17000], cos_type="log_sig", l2=0.5)
+    torch.save(g2b, OUT / "g2b_all_units_padded.pt")
+    print("g2b done", g2b["loss"].item())
+    # G3: full Base 12 layers, 1 x 10 s, distill layers 0.4,8,12 (checksums only)
+    g3 = run_step(no_dropout(HUBERT_BASE_CONFIG), no_dropout(HUBERT_BASE_CONFIG), "0.4,8,12", B=1, S=160000,
+                  units="conv,head,interm", lambdas=(0.0, 0.0), global_step=5000)
+    torch.save(g3, OUT / "g3_base12.pt")
+    print("g3 done", g3["loss"].item())
+    torch.save(gen_prune(), OUT / "g4_prune.pt")
+    print("g4 done")
+
+
+if __name__ == "__main__":
+    main()
