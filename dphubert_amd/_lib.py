@@ -1,0 +1,139 @@
+"""ctypes binding of the C ABI in include/dphubert_hip.h.
+
+This is the "reference-side binding" of the boundary: plain pointers, sizes
+and the current HIP stream go in, an int status comes back.  There is no
+fallback: if the library is missing or a call fails, a RuntimeError is raised
+(the product path never silently degrades to PyTorch/CPU math).
+"""
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import torch
+
+_HERE = Path(__file__).resolve().parent
+LIB_PATH = _HERE / "libdphubert_hip.so"
+
+vp = C.c_void_p
+i64 = C.c_int64
+i32 = C.c_int32
+f32 = C.c_float
+u64 = C.c_uint64
+
+
+class DphMat(C.Structure):
+    _fields_ = [("ptr", vp), ("rows_per_batch", i64), ("batch_stride", i64), ("row_stride", i64),
+                ("z_div", i64), ("z_outer", i64), ("z_inner", i64)]
+
+
+class DphGemmArgs(C.Structure):
+    _fields_ = [("M", i64), ("N", i64), ("K", i64), ("batch", i32), ("splits", i32), ("a_kcontig", i32),
+                ("b_kcontig", i32), ("A", DphMat), ("B", DphMat), ("C", DphMat), ("c_dtype", i32), ("act", i32),
+                ("alpha", f32), ("dropout_p", f32), ("seed", u64), ("bias", vp), ("colmask", vp), ("smask", vp),
+                ("vec_z_inner", i64), ("pre_out", vp), ("aux_in", vp), ("residual", vp), ("colsum_out", vp),
+                ("colsum_aux", vp), ("row_len", vp), ("len_rows", i64), ("drop_row_offset", i64),
+                ("workspace", vp), ("workspace_bytes", i64)]
+
+
+class DphTensorSlot(C.Structure):
+    _fields_ = [("param", vp), ("grad", vp), ("exp_avg", vp), ("exp_avg_sq", vp), ("n", i64), ("group", i32),
+                ("pad_", i32)]
+
+
+class DphAdamGroup(C.Structure):
+    _fields_ = [("lr", f32), ("weight_decay", f32), ("beta1", f32), ("beta2", f32), ("eps", f32),
+                ("pad_", f32 * 3)]
+
+
+S = vp  # hipStream_t
+
+_SIGS = {
+    "dph_abi_version": ([], C.c_int),
+    "dph_gemm": ([C.POINTER(DphGemmArgs), S], C.c_int),
+    "dph_layernorm_fwd": ([vp, vp, vp, vp, vp, vp, vp, i64, i64, f32, f32, u64, S], C.c_int),
+    "dph_layernorm_bwd": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, f32, u64, vp, f32, u64, vp, vp, vp, vp, S],
+                          C.c_int),
+    "dph_colsum": ([vp, vp, i64, i64, S], C.c_int),
+    "dph_attention_fwd": ([vp, vp, vp, vp, vp, vp, i64, i64, i64, f32, f32, u64, S], C.c_int),
+    "dph_attention_bwd_prep": ([vp, vp, vp, vp, vp, i64, i64, i64, S], C.c_int),
+    "dph_attention_bwd": ([vp, vp, vp, vp, vp, vp, vp, i64, i64, i64, f32, f32, u64, S], C.c_int),
+    "dph_conv0_gn_fwd": ([vp, i64, i64, vp, i64, i64, i64, vp, vp, vp, vp, vp, vp, vp, i64, S], C.c_int),
+    "dph_conv0_gn_bwd": ([vp, i64, i64, vp, i64, i64, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, S],
+                         C.c_int),
+    "dph_conv0_fwd": ([vp, i64, i64, vp, vp, i64, i64, i64, vp, S], C.c_int),
+    "dph_col2im_gelu_bwd": ([vp, i64, i64, i64, i64, i64, i64, vp, vp, vp, vp, S], C.c_int),
+    "dph_gelu_mask_bwd": ([vp, vp, vp, vp, vp, i64, i64, S], C.c_int),
+    "dph_regroup_pad": ([vp, vp, i64, i64, i64, i64, i64, i64, S], C.c_int),
+    "dph_weight_norm_fwd": ([vp, vp, i64, i64, i64, i64, vp, vp, vp, vp, S], C.c_int),
+    "dph_weight_norm_bwd": ([vp, vp, vp, vp, i64, i64, i64, i64, vp, vp, S], C.c_int),
+    "dph_cast_bf16": ([vp, vp, i64, S], C.c_int),
+    "dph_conv_weight_pack": ([vp, vp, i64, i64, i64, S], C.c_int),
+    "dph_conv_weight_unpack_grad": ([vp, vp, i64, i64, i64, C.c_int, S], C.c_int),
+    "dph_add_bf16": ([vp, vp, vp, i64, S], C.c_int),
+    "dph_distill_loss_fwd": ([vp, vp, i64, i64, i64, i64, f32, f32, f32, C.c_int, vp, vp, vp, S], C.c_int),
+    "dph_distill_loss_bwd": ([vp, vp, vp, vp, i64, i64, i64, i64, f32, f32, f32, C.c_int, vp, S], C.c_int),
+    "dph_hc_sample_fwd": ([vp, vp, vp, vp, i64, u64, f32, f32, f32, f32, S], C.c_int),
+    "dph_hc_sample_bwd": ([vp, vp, vp, vp, i64, f32, f32, f32, S], C.c_int),
+    "dph_expected_params_fwd": ([vp, vp, i64, vp, vp, i64, C.c_double, f32, vp, vp, S], C.c_int),
+    "dph_expected_params_bwd": ([vp, vp, vp, i64, vp, vp, i64, vp, vp, f32, S], C.c_int),
+    "dph_grad_sumsq": ([vp, i64, vp, vp, i64, vp, S], C.c_int),
+    "dph_adamw_step": ([vp, i64, vp, vp, i64, vp, i64, i64, vp, f32, S], C.c_int),
+}
+
+_lib = None
+
+
+class DphError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load the kernel library (raises if it is missing: no fallback path)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise DphError(f"{LIB_PATH} not found: run `python -m dphubert_amd.build` (hipcc --offload-arch=gfx950)")
+    L = C.CDLL(str(LIB_PATH))
+    L.dph_last_error.restype = C.c_char_p
+    L.dph_last_error.argtypes = []
+    missing = []
+    for name, (args, res) in _SIGS.items():
+        try:
+            fn = getattr(L, name)
+        except AttributeError:
+            missing.append(name)
+            continue
+        fn.argtypes = args
+        fn.restype = res
+    L.missing_symbols = missing
+    _lib = L
+    return L
+
+
+def exported_symbols():
+    return ["dph_last_error"] + list(_SIGS)
+
+
+def check(rc: int, what: str = ""):
+    if rc != 0:
+        msg = lib().dph_last_error().decode(errors="replace")
+        raise DphError(f"{what or 'dph call'} failed ({rc}): {msg}")
+
+
+def stream_ptr(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def call(name: str, *args):
+    fn = getattr(lib(), name)
+    rc = fn(*args)
+    check(rc, name)

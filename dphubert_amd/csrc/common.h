@@ -1,0 +1,93 @@
+// Shared device helpers for the DPHuBERT gfx950 kernel library.
+//
+// Conventions (see include/dphubert_hip.h):
+//   * activations are bf16 (stored as raw uint16_t), statistics and
+//     accumulation are fp32, master weights / gradients are fp32;
+//   * every entry point takes an explicit hipStream_t and never allocates;
+//   * errors are returned as negative DPH_E* codes with a thread-local
+//     message retrievable through dph_last_error().
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+#include "../../include/dphubert_hip.h"
+
+typedef uint16_t bf16_t;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;
+typedef __attribute__((ext_vector_type(4))) short s16x4_t;
+typedef __attribute__((ext_vector_type(8))) short s16x8_t;
+
+namespace dph {
+
+void set_error(const char* fmt, ...);
+int check_launch(const char* what);
+
+#define DPH_REQUIRE(cond, ...)              \
+  do {                                      \
+    if (!(cond)) {                          \
+      ::dph::set_error(__VA_ARGS__);        \
+      return DPH_EINVAL;                    \
+    }                                       \
+  } while (0)
+
+__device__ __forceinline__ float bf2f(bf16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
+
+// round-to-nearest-even f32 -> bf16 (NaN stays NaN via the hardware cvt)
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  __bf16 h = (__bf16)f;
+  return __builtin_bit_cast(bf16_t, h);
+}
+
+__device__ __forceinline__ uint32_t pack2bf(float a, float b) {
+  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+}
+
+// exact-erf GELU (torch default), components.py:110,331,734
+__device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+
+__device__ __forceinline__ float gelu_grad_f(float x) {
+  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
+  const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+
+// Counter-based RNG: splitmix64 finaliser of (seed, element index).  The same
+// (seed, index) always gives the same bits, so forward and backward kernels
+// regenerate identical dropout / HardConcrete noise without storing masks.
+__device__ __forceinline__ uint32_t rand_u32(uint64_t seed, uint64_t idx) {
+  uint64_t z = seed * 0x9E3779B97F4A7C15ull + idx + 0x632BE59BD9B4E019ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (uint32_t)(z >> 32);
+}
+
+// uniform in [0,1) with 24 random bits
+__device__ __forceinline__ float rand_uniform(uint64_t seed, uint64_t idx) {
+  return (float)(rand_u32(seed, idx) >> 8) * (1.0f / 16777216.0f);
+}
+
+// dropout keep factor: 0 or 1/(1-p); p == 0 -> 1
+__device__ __forceinline__ float dropout_scale(uint64_t seed, uint64_t idx, float p, float inv_keep) {
+  if (p <= 0.f) return 1.0f;
+  return rand_uniform(seed, idx) >= p ? inv_keep : 0.0f;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+__host__ __device__ __forceinline__ int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+}  // namespace dph

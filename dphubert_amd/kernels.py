@@ -1,0 +1,112 @@
+"""Thin tensor-level wrappers over the C ABI (one function per entry point).
+
+Each wrapper validates shapes/dtypes/devices on the host, then passes raw
+device pointers and the current HIP stream to libdphubert_hip.so.  Scratch
+buffers are allocated here through the PyTorch caching allocator, never
+inside the library.
+"""
+
+import ctypes as C
+from typing import Optional, Sequence
+
+import torch
+
+from . import _lib
+from ._lib import DphGemmArgs, DphMat, call, ptr
+
+BF16 = torch.bfloat16
+F32 = torch.float32
+
+ACT_NONE, ACT_GELU, ACT_GELU_BWD = 0, 1, 2
+OUT_BF16, OUT_F32, OUT_F32_ACCUM = 0, 1, 2
+
+
+def _stream():
+    return _lib.stream_ptr()
+
+
+def _chk(t, dtype=None, name="tensor"):
+    if t is None:
+        return
+    if not t.is_cuda:
+        raise ValueError(f"{name} must be a device tensor (no CPU path)")
+    if dtype is not None and t.dtype != dtype:
+        raise ValueError(f"{name}: expected {dtype}, got {t.dtype}")
+
+
+def mat(t: torch.Tensor, row_stride: int, rows_per_batch: int = 0, batch_stride: int = 0, z_div: int = 0,
+        z_outer: int = 0, z_inner: int = 0, offset: int = 0) -> DphMat:
+    """Describe a strided 2-D (optionally batched) view of ``t`` for the GEMM."""
+    return DphMat(t.data_ptr() + offset * t.element_size(), rows_per_batch, batch_stride, row_stride, z_div, z_outer,
+                  z_inner)
+
+
+def dense(t: torch.Tensor, offset: int = 0, row_stride: Optional[int] = None) -> DphMat:
+    return mat(t, t.shape[-1] if row_stride is None else row_stride, offset=offset)
+
+
+def gemm(A: DphMat, B: DphMat, Cm: DphMat, M: int, N: int, K: int, *, a_kcontig: bool, b_kcontig: bool,
+         c_dtype: int = OUT_BF16, act: int = ACT_NONE, alpha: float = 1.0, batch: int = 1, splits: int = 1,
+         bias=None, colmask=None, smask=None, vec_z_inner: int = 0, pre_out=None, aux_in=None, residual=None,
+         colsum_out=None, colsum_aux=None, row_len=None, len_rows: int = 0, dropout_p: float = 0.0, seed: int = 0,
+         drop_row_offset: int = 0, device=None):
+    ws = None
+    ws_bytes = 0
+    if splits > 1:
+        ws_bytes = batch * splits * M * N * 4
+        ws = torch.empty(batch * splits * M * N, dtype=F32, device=device or "cuda")
+    args = DphGemmArgs(M, N, K, batch, splits, int(a_kcontig), int(b_kcontig), A, B, Cm, c_dtype, act, alpha,
+                       dropout_p, seed & 0xFFFFFFFFFFFFFFFF, ptr(bias), ptr(colmask), ptr(smask), vec_z_inner,
+                       ptr(pre_out), ptr(aux_in), ptr(residual), ptr(colsum_out), ptr(colsum_aux), ptr(row_len),
+                       len_rows, drop_row_offset, ptr(ws), ws_bytes)
+    call("dph_gemm", C.byref(args), _stream())
+    return ws  # keep alive until the stream consumes it (caching allocator is stream-ordered)
+
+
+def choose_splits(M: int, N: int, K: int, batch: int = 1, target_blocks: int = 512) -> int:
+    """Split-K factor so that the grid fills the 256 CUs (weight-gradient GEMMs)."""
+    tiles = ((M + 127) // 128) * ((N + 127) // 128) * batch
+    if tiles >= 256:
+        return 1
+    s = max(1, min(target_blocks // max(tiles, 1), K // 256))
+    return int(s)
+
+
+def linear_fwd(x: torch.Tensor, w_bf16: torch.Tensor, bias: Optional[torch.Tensor] = None, *, out=None,
+               out_dtype=BF16, act=ACT_NONE, pre_out=None, colmask=None, smask=None, residual=None,
+               dropout_p=0.0, seed=0, row_len=None, len_rows=0, colsum_out=None):
+    """y = epi(x @ w^T + b); x [M,K] bf16, w [N,K] bf16 (nn.Linear layout)."""
+    _chk(x, BF16, "x")
+    _chk(w_bf16, BF16, "w")
+    M, K = x.shape
+    N = w_bf16.shape[0]
+    if out is None:
+        out = torch.empty(M, N, dtype=out_dtype, device=x.device)
+    c_dtype = OUT_BF16 if out.dtype == BF16 else OUT_F32
+    gemm(dense(x), dense(w_bf16), dense(out), M, N, K, a_kcontig=True, b_kcontig=True, c_dtype=c_dtype, act=act,
+         bias=bias, colmask=colmask, smask=smask, pre_out=pre_out, residual=residual, dropout_p=dropout_p,
+         seed=seed, row_len=row_len, len_rows=len_rows, colsum_out=colsum_out)
+    return out
+
+
+def linear_dgrad(dy: torch.Tensor, w_bf16: torch.Tensor, *, out=None, residual=None, act=ACT_NONE, aux_in=None,
+                 colmask=None, colsum_out=None, colsum_aux=None, dropout_p=0.0, seed=0):
+    """dx = epi(dy @ w); dy [M,N] bf16, w [N,K] bf16 -> [M,K] bf16."""
+    M, N = dy.shape
+    K = w_bf16.shape[1]
+    if out is None:
+        out = torch.empty(M, K, dtype=BF16, device=dy.device)
+    gemm(dense(dy), dense(w_bf16), dense(out), M, K, N, a_kcontig=True, b_kcontig=False, residual=residual, act=act,
+         aux_in=aux_in, colmask=colmask, colsum_out=colsum_out, colsum_aux=colsum_aux, dropout_p=dropout_p,
+         seed=seed)
+    return out
+
+
+def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, accumulate: bool = True):
+    """dw (+)= dy^T @ x; dy [M,N] bf16, x [M,K] bf16, dw [N,K] fp32."""
+    M, N = dy.shape
+    K = x.shape[1]
+    splits = choose_splits(N, K, M)
+    ws = gemm(dense(dy), dense(x), dense(dw), N, K, M, a_kcontig=False, b_kcontig=False,
+              c_dtype=OUT_F32_ACCUM if accumulate else OUT_F32, splits=splits, device=dy.device)
+    return ws

@@ -1,0 +1,260 @@
+/*
+ * dphubert_hip.h — C ABI of the MI355X (gfx950) DPHuBERT distill-step kernels.
+ *
+ * The reference (seas2nada/DPHuBERT) has no FFI: its boundary is the Python
+ * module API.  Every entry point below replaces the ATen /
+ * cuDNN / cuBLAS work behind one reference call site, cited per function.
+ * The Python host mirror (dphubert_amd/_lib.py, ctypes) binds these symbols;
+ * INTEGRATION.md shows the binding.
+ *
+ * Conventions
+ *   - plain pointers + sizes, no torch types; all buffers (incl. workspace) are
+ *     caller-owned device memory; nothing here allocates;
+ *   - every call is stream-ordered on the hipStream_t it is given and
+ *     re-entrant (no mutable global state);
+ *   - bf16 tensors are raw 16-bit storage (uint16_t), row-major;
+ *   - return 0 on success or a negative DPH_E* code; dph_last_error() gives a
+ *     thread-local message for the last failure on the calling thread.
+ */
+#ifndef DPHUBERT_HIP_H
+#define DPHUBERT_HIP_H
+
+#include <stdint.h>
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DPH_OK 0
+#define DPH_EINVAL (-1)
+#define DPH_ELAUNCH (-2)
+#define DPH_EUNSUPPORTED (-3)
+
+const char* dph_last_error(void);
+int dph_abi_version(void);
+
+/* ------------------------------------------------------------------------ *
+ * Generic bf16 MFMA GEMM with fused epilogues.
+ *   C[z][m][n] = epi( alpha * sum_k A[z][m][k] * B[z][k][n] )
+ * Replaces every nn.Linear / conv1d matmul of the hot path (fwd, dgrad,
+ * wgrad): components.py:107 (conv1..6 as implicit GEMM over channels-last
+ * activations), :272 (feature projection), :328 (grouped pos-conv as a
+ * batched GEMM), :406-408/:430 (QKV, out_proj), :733/:741 (FFN),
+ * lightning.py:258 (distill projections).
+ * ------------------------------------------------------------------------ */
+typedef struct DphMat {
+  void* ptr;
+  /* address of row r (elements): rpb > 0 ? (r/rpb)*batch_stride + (r%rpb)*row_stride
+   *                                       : r*row_stride                          */
+  int64_t rows_per_batch;
+  int64_t batch_stride;
+  int64_t row_stride;
+  /* offset of grid batch z: z_div > 0 ? (z/z_div)*z_outer + (z%z_div)*z_inner : z*z_inner */
+  int64_t z_div;
+  int64_t z_outer;
+  int64_t z_inner;
+} DphMat;
+
+#define DPH_ACT_NONE 0
+#define DPH_ACT_GELU 1      /* v = gelu(v), optional pre-activation store        */
+#define DPH_ACT_GELU_BWD 2  /* v = v*drop*colmask*gelu'(aux); colsum_aux += v*drop*gelu(aux) */
+
+#define DPH_OUT_BF16 0
+#define DPH_OUT_F32 1
+#define DPH_OUT_F32_ACCUM 2
+
+typedef struct DphGemmArgs {
+  int64_t M, N, K;
+  int32_t batch;      /* grid batches (z)                                    */
+  int32_t splits;     /* split-K factor; >1 needs workspace M*N*splits*batch fp32 */
+  int32_t a_kcontig;  /* 1: A is [M][K] (k contiguous); 0: A is [K][M]         */
+  int32_t b_kcontig;  /* 1: B is [N][K] (k contiguous); 0: B is [K][N]         */
+  DphMat A, B, C;     /* C layout is shared by pre_out / aux_in / residual     */
+  int32_t c_dtype;    /* DPH_OUT_*                                            */
+  int32_t act;        /* DPH_ACT_*                                            */
+  float alpha;
+  float dropout_p;
+  uint64_t seed;
+  const float* bias;      /* [N], added after alpha                          */
+  const float* colmask;   /* [N], multiplies after the activation             */
+  const float* smask;     /* scalar device pointer (layer mask)               */
+  int64_t vec_z_inner;    /* per-batch offset of bias/colmask/colsum vectors = (z % C.z_div)*vec_z_inner */
+  void* pre_out;          /* bf16, pre-activation (after bias)                */
+  const void* aux_in;     /* bf16, GELU_BWD pre-activation input              */
+  const void* residual;   /* bf16, added last                                 */
+  float* colsum_out;      /* [N] fp32 atomics: column sums of the stored value */
+  float* colsum_aux;      /* [N] fp32 atomics: GELU_BWD mask gradient          */
+  const int64_t* row_len; /* zero rows with (m % len_rows) >= row_len[m / len_rows] */
+  int64_t len_rows;
+  int64_t drop_row_offset;/* dropout element index = (drop_row_offset + m)*N + n (per batch z adds z*M*N) */
+  void* workspace;        /* split-K partials                                  */
+  int64_t workspace_bytes;
+} DphGemmArgs;
+
+int dph_gemm(const DphGemmArgs* args, hipStream_t stream);
+
+/* ------------------------------------------------------------------------ *
+ * LayerNorm over the last dim (rows x D), fp32 statistics, eps=1e-5.
+ * components.py:271, :853, :856, :889 (nn.LayerNorm), :54-61.
+ * y = (x*xscale - mean)*rstd*gamma + beta, then optional dropout.
+ * ------------------------------------------------------------------------ */
+int dph_layernorm_fwd(const void* x, const float* xscale, const float* gamma, const float* beta, void* y,
+                      float* mean, float* rstd, int64_t rows, int64_t D, float eps, float dropout_p,
+                      uint64_t seed, hipStream_t stream);
+/* dx = LN backward; dgamma/dbeta accumulate (atomics).  Optional branch output
+ * (residual sub-branch gradient): branch = dx * drop(branch_p, branch_seed) * (*branch_smask),
+ * branch_colsum += column sums of branch, branch_sdot += sum(dx*drop*branch_pre).
+ * dx_add (optional) is added to dx (other gradient contributions of the LN input). */
+int dph_layernorm_bwd(const void* dy, const void* x, const float* xscale, const float* gamma, const float* mean,
+                      const float* rstd, void* dx, float* dgamma, float* dbeta, int64_t rows, int64_t D,
+                      float dropout_p, uint64_t seed, void* branch, float branch_p, uint64_t branch_seed,
+                      const float* branch_smask, float* branch_colsum, const void* branch_pre,
+                      float* branch_sdot, hipStream_t stream);
+
+/* column sums of a bf16 matrix (bias gradients): out[n] += sum_m x[m][n] */
+int dph_colsum(const void* x, float* out, int64_t rows, int64_t cols, hipStream_t stream);
+
+/* ------------------------------------------------------------------------ *
+ * Fused multi-head self-attention (flash style), head dim 64.
+ * components.py:405-426: q,k,v read from the fused QKV buffer
+ * [B*T][3*H*64] (q | k | v), scores (scale*q)k^T + (-1e4 key padding),
+ * softmax, dropout(p), @v, x head_mask.  Writes o_unmasked and o_masked
+ * ([B*T][H*64] bf16) and the per-row log-sum-exp [B][H][T].
+ * ------------------------------------------------------------------------ */
+int dph_attention_fwd(const void* qkv, void* o_unmasked, void* o_masked, float* lse, const float* head_mask,
+                      const int64_t* key_len, int64_t B, int64_t T, int64_t H, float scale, float dropout_p,
+                      uint64_t seed, hipStream_t stream);
+/* backward prep: rowdot[b][h][t] = sum_d do_m*o_u ; D = head_mask*rowdot ;
+ * dhead_mask[h] += sum rowdot */
+int dph_attention_bwd_prep(const void* do_masked, const void* o_unmasked, const float* head_mask, float* Dvec,
+                           float* dhead_mask, int64_t B, int64_t T, int64_t H, hipStream_t stream);
+/* dq|dk|dv into dqkv [B*T][3*H*64] (bf16) */
+int dph_attention_bwd(const void* qkv, const void* do_masked, const float* head_mask, const float* lse,
+                      const float* Dvec, void* dqkv, const int64_t* key_len, int64_t B, int64_t T, int64_t H,
+                      float scale, float dropout_p, uint64_t seed, hipStream_t stream);
+
+/* ------------------------------------------------------------------------ *
+ * Conv frontend (FeatureExtractor, components.py:94-120, 158-185,
+ * 1071-1076): conv0 (1 -> C, kernel k0, stride s0, no bias) + GroupNorm(C,C)
+ * + GELU + HardConcrete channel mask, output channels-last bf16 [B][L][C].
+ * ------------------------------------------------------------------------ */
+int dph_conv0_gn_fwd(const float* wave, int64_t B, int64_t S, const float* w, int64_t C, int64_t k0, int64_t s0,
+                     const float* gamma, const float* beta, const float* mask, void* y, float* mean, float* rstd,
+                     float* ws, int64_t ws_bytes, hipStream_t stream);
+int dph_conv0_gn_bwd(const float* wave, int64_t B, int64_t S, const float* w, int64_t C, int64_t k0, int64_t s0,
+                     const float* gamma, const float* beta, const float* mask, const float* mean, const float* rstd,
+                     const void* dy, float* dw, float* dgamma, float* dbeta, float* dmask, float* ws,
+                     int64_t ws_bytes, hipStream_t stream);
+/* plain conv0 (no norm, used by layer_norm-mode extractors): y[b][t][c] = sum_j w[c][j]*x[b][s0*t+j] (+bias) */
+int dph_conv0_fwd(const float* wave, int64_t B, int64_t S, const float* w, const float* bias, int64_t C,
+                  int64_t k0, int64_t s0, void* y, hipStream_t stream);
+
+/* Fused col2im + GELU/mask backward for a strided conv layer (k, s):
+ * dy_in[b][t'][c] = sum_{t,j: s*t+j==t'} dcols[b][t][j*C+c]; then, if z_pre != NULL,
+ * out = dy_in*mask[c]*gelu'(z_pre), dmask[c] += dy_in*gelu(z_pre); else out = dy_in. */
+int dph_col2im_gelu_bwd(const void* dcols, int64_t B, int64_t Lout, int64_t Lin, int64_t C, int64_t k, int64_t s,
+                        const void* z_pre, const float* mask, void* out, float* dmask, hipStream_t stream);
+/* GELU/mask backward on a dense [rows][C] tensor (no col2im) */
+int dph_gelu_mask_bwd(const void* dy, const void* z_pre, const float* mask, void* out, float* dmask, int64_t rows,
+                      int64_t C, hipStream_t stream);
+
+/* pos-conv layout helpers: x [B][T][G*Cg] bf16 -> xg [B][G][pad_front + T + pad_back][Cg] zero-padded */
+int dph_regroup_pad(const void* x, void* xg, int64_t B, int64_t T, int64_t G, int64_t Cg, int64_t pad_front,
+                    int64_t pad_back, hipStream_t stream);
+/* weight norm (dim=2): w = g*v/||v||_(dims 0,1), also writes the bf16 GEMM images
+ * wk [G][Cg_out][K*Cg_in] (k-major: index j*Cg_in+c) and its flipped transpose
+ * wt [G][Cg_in][K*Cg_out] (index jj*Cg_out+o, jj=K-1-j) used by the input-gradient GEMM. */
+int dph_weight_norm_fwd(const float* g, const float* v, int64_t Cout, int64_t Cin_g, int64_t K, int64_t G,
+                        float* w, float* norm, void* wk, void* wt, hipStream_t stream);
+/* dW_img [G][Cg_out][K*Cg_in] fp32 (GEMM layout) -> dg [K], dv [Cout][Cin_g][K] */
+int dph_weight_norm_bwd(const float* dw_img, const float* g, const float* v, const float* norm, int64_t Cout,
+                        int64_t Cin_g, int64_t K, int64_t G, float* dg, float* dv, hipStream_t stream);
+
+/* ------------------------------------------------------------------------ *
+ * Casting / layout helpers for the bf16 GEMM images of fp32 master weights.
+ * ------------------------------------------------------------------------ */
+/* dst[r][c] = bf16(src[r][c] * (colscale ? colscale[c] : 1)) */
+int dph_cast_bf16(const float* src, void* dst, int64_t n, hipStream_t stream);
+/* conv weight [O][C][k] fp32 -> bf16 [O][k*C] (index j*C+c) */
+int dph_conv_weight_pack(const float* w, void* dst, int64_t O, int64_t C, int64_t k, hipStream_t stream);
+/* grad of packed conv weight: fp32 [O][k*C] -> [O][C][k] (accumulate if accum) */
+int dph_conv_weight_unpack_grad(const float* g, float* dst, int64_t O, int64_t C, int64_t k, int accum,
+                                hipStream_t stream);
+/* bf16 -> f32 copy / accumulate helpers */
+int dph_add_bf16(const void* a, const void* b, void* out, int64_t n, hipStream_t stream);
+
+/* ------------------------------------------------------------------------ *
+ * Distillation loss (lightning.py:116-139) over student s (fp32) and teacher
+ * layers t_l (bf16), both (B, L, T, D) with the teacher given as L pointers
+ * to [B][T][D] hidden states.
+ * out[0..3] = loss, mse, l1, cos.  rowstats [B*L*T][3] saved for backward.
+ * ------------------------------------------------------------------------ */
+#define DPH_MAX_DISTILL_LAYERS 16
+int dph_distill_loss_fwd(const float* s, const void* const* t_layers, int64_t B, int64_t L, int64_t T, int64_t D,
+                         float l2w, float l1w, float cosw, int cos_logsig, float* rowstats, float* partial,
+                         float* out, hipStream_t stream);
+/* ds (bf16, (B,L,T,D)) = dloss * d loss/ds; dbias[l][D] (fp32 atomics, per layer) optional */
+int dph_distill_loss_bwd(const float* s, const void* const* t_layers, const float* rowstats, const float* dloss,
+                         int64_t B, int64_t L, int64_t T, int64_t D, float l2w, float l1w, float cosw,
+                         int cos_logsig, void* ds, hipStream_t stream);
+
+/* ------------------------------------------------------------------------ *
+ * HardConcrete (hardconcrete.py:85-116) + expected parameter count
+ * (model.py:109-113 and the get_num_params chain).
+ * ------------------------------------------------------------------------ */
+/* mask = clamp(sigmoid((logit(u)+la)/beta)*(r-l)+l, 0, 1); u = uniform(eps, 1-eps) from (seed, i)
+ * unless u_in != NULL.  u_out (optional) receives u. */
+int dph_hc_sample_fwd(const float* log_alpha, const float* u_in, float* u_out, float* mask, int64_t n, uint64_t seed,
+                      float beta, float limit_l, float limit_r, float eps, hipStream_t stream);
+/* dlog_alpha += dmask * dmask/dlog_alpha */
+int dph_hc_sample_bwd(const float* log_alpha, const float* u, const float* dmask, float* dlog_alpha, int64_t n,
+                      float beta, float limit_l, float limit_r, hipStream_t stream);
+
+/* Expected #params as a polynomial in the l0 norms of n_groups HardConcrete
+ * modules: value = const + sum_t coef[t] * prod_{i<3, idx[t][i]>=0} l0[idx[t][i]],
+ * l0[g] = sum sigmoid(la_g + bias).  la_ptrs/la_sizes: device arrays of
+ * per-module pointers / lengths. */
+int dph_expected_params_fwd(const float* const* la_ptrs, const int64_t* la_sizes, int64_t n_groups,
+                            const double* coef, const int32_t* idx, int64_t n_terms, double constant, float hc_bias,
+                            float* l0, float* out, hipStream_t stream);
+int dph_expected_params_bwd(const float* const* la_ptrs, float* const* grad_ptrs, const int64_t* la_sizes,
+                            int64_t n_groups, const double* coef, const int32_t* idx, int64_t n_terms,
+                            const float* l0, const float* dout, float hc_bias, hipStream_t stream);
+
+/* ------------------------------------------------------------------------ *
+ * Optimiser: multi-tensor AdamW (torch.optim.AdamW semantics,
+ * lightning.py:200-228) with global-norm gradient clipping
+ * (Trainer(gradient_clip_val=10), distill.py:48).
+ * ------------------------------------------------------------------------ */
+typedef struct DphTensorSlot {
+  float* param;
+  float* grad;
+  float* exp_avg;
+  float* exp_avg_sq;
+  int64_t n;
+  int32_t group;
+  int32_t pad_;
+} DphTensorSlot;
+
+typedef struct DphAdamGroup {
+  float lr;
+  float weight_decay;
+  float beta1;
+  float beta2;
+  float eps;
+  float pad_[3];
+} DphAdamGroup;
+
+/* sumsq[0] += sum over all slots of grad^2 (fp32 atomics, blocks over chunks) */
+int dph_grad_sumsq(const DphTensorSlot* slots, int64_t n_slots, const int64_t* chunk_slot,
+                   const int64_t* chunk_start, int64_t n_chunks, float* sumsq, hipStream_t stream);
+/* clip coef = min(1, max_norm/(sqrt(sumsq)+1e-6)) applied to grads, then AdamW step `step` (1-based) */
+int dph_adamw_step(const DphTensorSlot* slots, int64_t n_slots, const int64_t* chunk_slot, const int64_t* chunk_start,
+                   int64_t n_chunks, const DphAdamGroup* groups, int64_t n_groups, int64_t step,
+                   const float* sumsq, float max_norm, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DPHUBERT_HIP_H */

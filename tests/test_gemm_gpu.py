@@ -1,0 +1,174 @@
+"""GEMM parity on the GPU: every operand layout and epilogue against a torch fp32
+reference of the same op on the same bf16-rounded inputs."""
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+torch.manual_seed(0)
+
+
+def _k():
+    from dphubert_amd import kernels as K
+    return K
+
+
+def rnd(*shape, scale=1.0):
+    return (torch.randn(*shape, device="cuda") * scale).to(torch.bfloat16)
+
+
+def close(a, b, tol=2e-2):
+    a = a.float()
+    b = b.float()
+    err = (a - b).norm() / b.norm().clamp_min(1e-20)
+    assert err < tol, f"rel err {err}"
+
+
+@pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, True), (False, False)])
+@pytest.mark.parametrize("M,N,K", [(304, 200, 136), (128, 128, 64), (1000, 264, 520)])
+def test_layouts(ak, bk, M, N, K):
+    K_ = _k()
+    A = rnd(M, K) if ak else rnd(K, M)
+    B = rnd(N, K) if bk else rnd(K, N)
+    Af = A.float() if ak else A.float().t()
+    Bf = B.float().t() if bk else B.float()
+    ref = Af @ Bf
+    C = torch.empty(M, N, device="cuda", dtype=torch.float32)
+    K_.gemm(K_.dense(A), K_.dense(B), K_.dense(C), M, N, K, a_kcontig=ak, b_kcontig=bk, c_dtype=K_.OUT_F32)
+    torch.cuda.synchronize()
+    close(C, ref, 1e-5)
+
+
+def test_asymmetric_identity():
+    # A = I with an asymmetric B catches a transposed C write (guide: A=I check)
+    K_ = _k()
+    M = N = K = 128
+    A = torch.eye(M, device="cuda").to(torch.bfloat16)
+    B = (torch.arange(N * K, device="cuda").reshape(N, K) % 251).to(torch.bfloat16)
+    C = torch.empty(M, N, device="cuda")
+    K_.gemm(K_.dense(A), K_.dense(B), K_.dense(C), M, N, K, a_kcontig=True, b_kcontig=True, c_dtype=K_.OUT_F32)
+    torch.cuda.synchronize()
+    assert torch.equal(C, B.float().t())
+
+
+def test_epilogue_gelu_mask_pre():
+    K_ = _k()
+    M, N, K = 513, 384, 256
+    x, w = rnd(M, K), rnd(N, K, scale=0.05)
+    b = torch.randn(N, device="cuda")
+    cm = torch.rand(N, device="cuda")
+    pre = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    y = K_.linear_fwd(x, w, b, act=K_.ACT_GELU, pre_out=pre, colmask=cm)
+    u = x.float() @ w.float().t() + b
+    close(pre, u)
+    close(y, torch.nn.functional.gelu(u) * cm)
+
+
+def test_epilogue_residual_smask_colsum_rowlen():
+    K_ = _k()
+    M, N, K = 400, 256, 128
+    x, w = rnd(M, K), rnd(N, K, scale=0.1)
+    b = torch.randn(N, device="cuda")
+    res = rnd(M, N)
+    sm = torch.tensor([0.7], device="cuda")
+    cs = torch.zeros(N, device="cuda")
+    lens = torch.tensor([150, 200], device="cuda", dtype=torch.int64)
+    y = K_.linear_fwd(x, w, b, smask=sm, residual=res, colsum_out=cs, row_len=lens, len_rows=200)
+    ref = (x.float() @ w.float().t() + b) * 0.7 + res.float()
+    ref[150:200] = 0
+    close(y, ref)
+    close(cs, y.float().sum(0), 1e-2)
+
+
+def test_gelu_bwd_epilogue():
+    K_ = _k()
+    M, N, K = 300, 512, 192   # dF = dY @ W2 ; N = F
+    dy, w2 = rnd(M, K), rnd(K, N, scale=0.05)    # W2 [D=K][F=N]
+    u = rnd(M, N)
+    im = torch.rand(N, device="cuda")
+    dm = torch.zeros(N, device="cuda")
+    db = torch.zeros(N, device="cuda")
+    du = K_.linear_dgrad(dy, w2, act=K_.ACT_GELU_BWD, aux_in=u, colmask=im, colsum_out=db, colsum_aux=dm)
+    df = dy.float() @ w2.float()
+    uf = u.float().requires_grad_(True)
+    g = torch.nn.functional.gelu(uf)
+    gp, = torch.autograd.grad(g.sum(), uf)
+    close(du, df * im * gp)
+    close(dm, (df * g.detach()).sum(0), 1e-2)
+    close(db, du.float().sum(0), 1e-2)
+
+
+@pytest.mark.parametrize("accum", [False, True])
+def test_wgrad_splitk(accum):
+    K_ = _k()
+    M, N, K = 3000, 384, 256
+    dy, x = rnd(M, N), rnd(M, K)
+    dw = torch.randn(N, K, device="cuda")
+    dw0 = dw.clone()
+    K_.linear_wgrad(dy, x, dw, accumulate=accum)
+    ref = dy.float().t() @ x.float() + (dw0 if accum else 0)
+    close(dw, ref, 1e-5)
+
+
+def test_conv_implicit_gemm():
+    # channels-last strided conv (k=3, s=2) as a GEMM with a row-address function
+    K_ = _k()
+    B, Lin, Cc, O, k, s = 2, 101, 64, 96, 3, 2
+    Lout = (Lin - k) // s + 1
+    x = rnd(B, Lin, Cc)
+    w = rnd(O, Cc, k, scale=0.1)
+    wp = w.permute(0, 2, 1).contiguous()       # [O][k][C]
+    y = torch.empty(B * Lout, O, device="cuda", dtype=torch.float32)
+    A = K_.mat(x, row_stride=s * Cc, rows_per_batch=Lout, batch_stride=Lin * Cc)
+    K_.gemm(A, K_.dense(wp.view(O, k * Cc)), K_.dense(y), B * Lout, O, k * Cc, a_kcontig=True, b_kcontig=True,
+            c_dtype=K_.OUT_F32)
+    ref = torch.nn.functional.conv1d(x.float().transpose(1, 2), w.float(), stride=s).transpose(1, 2).reshape(-1, O)
+    close(y, ref, 1e-5)
+
+
+def test_batched_zdiv():
+    # grouped GEMM: z = b*G + g ; B operand depends only on g
+    K_ = _k()
+    Bt, G, M, N, K = 3, 4, 70, 48, 96
+    A = rnd(Bt * G, M, K)
+    W = rnd(G, N, K)
+    out = torch.empty(Bt, M, G * N, device="cuda")
+    K_.gemm(K_.mat(A, K, z_inner=M * K), K_.mat(W, K, z_div=G, z_outer=0, z_inner=N * K),
+            K_.mat(out, G * N, z_div=G, z_outer=M * G * N, z_inner=N), M, N, K, a_kcontig=True, b_kcontig=True,
+            c_dtype=K_.OUT_F32, batch=Bt * G)
+    ref = torch.einsum("bgmk,gnk->bmgn", A.float().view(Bt, G, M, K), W.float()).reshape(Bt, M, G * N)
+    close(out, ref, 1e-5)
+
+
+def test_dropout_epilogue_rate():
+    K_ = _k()
+    M, N, K = 512, 512, 64
+    x, w = rnd(M, K), rnd(N, K)
+    y0 = K_.linear_fwd(x, w, out_dtype=torch.float32)
+    y1 = K_.linear_fwd(x, w, out_dtype=torch.float32, dropout_p=0.25, seed=123)
+    y2 = K_.linear_fwd(x, w, out_dtype=torch.float32, dropout_p=0.25, seed=123)
+    assert torch.equal(y1, y2)
+    keep = y1 != 0
+    rate = 1 - keep.float().mean().item()
+    assert abs(rate - 0.25) < 0.01
+    close(y1[keep], y0[keep] / 0.75, 1e-5)
+
+
+def test_perf_ffn_shape():
+    K_ = _k()
+    M, N, K = 7984, 3072, 768
+    x, w = rnd(M, K), rnd(N, K)
+    b = torch.randn(N, device="cuda")
+    for _ in range(3):
+        K_.linear_fwd(x, w, b, act=K_.ACT_GELU)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(20):
+        K_.linear_fwd(x, w, b, act=K_.ACT_GELU)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / 20
+    tf = 2 * M * N * K / ms / 1e9
+    print(f"\nFFN1 GEMM {M}x{N}x{K}: {ms*1e3:.1f} us, {tf:.0f} TFLOP/s")
