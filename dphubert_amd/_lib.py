@@ -71,12 +71,13 @@ _SIGS = {
     "dph_conv_weight_pack": ([vp, vp, i64, i64, i64, S], C.c_int),
     "dph_conv_weight_unpack_grad": ([vp, vp, i64, i64, i64, C.c_int, S], C.c_int),
     "dph_add_bf16": ([vp, vp, vp, i64, S], C.c_int),
+    "dph_branch_bwd": ([vp, vp, i64, i64, f32, u64, vp, vp, i64, vp, vp, vp, S], C.c_int),
     "dph_distill_loss_fwd": ([vp, vp, i64, i64, i64, i64, f32, f32, f32, C.c_int, vp, vp, vp, S], C.c_int),
     "dph_distill_loss_bwd": ([vp, vp, vp, vp, i64, i64, i64, i64, f32, f32, f32, C.c_int, vp, S], C.c_int),
     "dph_hc_sample_fwd": ([vp, vp, vp, vp, i64, u64, f32, f32, f32, f32, S], C.c_int),
     "dph_hc_sample_bwd": ([vp, vp, vp, vp, i64, f32, f32, f32, S], C.c_int),
     "dph_expected_params_fwd": ([vp, vp, i64, vp, vp, i64, C.c_double, f32, vp, vp, S], C.c_int),
-    "dph_expected_params_bwd": ([vp, vp, vp, i64, vp, vp, i64, vp, vp, f32, S], C.c_int),
+    "dph_expected_params_bwd": ([vp, vp, vp, vp, i64, vp, vp, i64, vp, vp, f32, S], C.c_int),
     "dph_grad_sumsq": ([vp, i64, vp, vp, i64, vp, S], C.c_int),
     "dph_adamw_step": ([vp, i64, vp, vp, i64, vp, i64, i64, vp, f32, S], C.c_int),
 }

@@ -1,0 +1,563 @@
+// Fused multi-head self-attention (head dim 64) for gfx950, forward + backward.
+//
+// Reference: SelfAttention.forward, components.py:405-426:
+//   w = (scaling*q) @ k^T + mask(-1e4 on padded keys); w -= rowmax; softmax;
+//   dropout(p); out = w @ v; out *= head_mask[h].
+// Nothing of size T x T is ever written to HBM: scores live in MFMA
+// accumulators, the forward keeps a running (max, sum) per query row and saves
+// only LSE = max + log(sum); the backward recomputes P from LSE.
+//
+// q, k, v are read straight from the fused QKV projection output
+// [B*T][3*H*64] (q | k | v blocks), gradients are written into the same
+// layout, so no (B,H,T,hd) permute copies exist.
+//
+// MFMA: v_mfma_f32_16x16x32_bf16.  "Swapped" products put the key index in
+// the accumulator rows, so a P/dS tile feeds the next product directly as the
+// B operand (the k permutation of the accumulator rows is matched by the
+// transposed LDS read ds_read_b64_tr_b16 of V / K / dO / Q tiles).
+#include "common.h"
+
+namespace dph {
+namespace {
+
+constexpr int HD = 64;
+constexpr int KT = 64;        // keys per tile (fwd / dQ), keys per block (dKV)
+constexpr int QT = 64;        // query rows per block (fwd / dQ)
+constexpr int QT_BWD = 32;    // query rows per step of the dKV kernel
+constexpr int PADROW = 72;    // padded row (elements) for b128-only tiles
+
+typedef __attribute__((address_space(3))) s16x4_t lds_s16x4;
+
+// 128-byte rows (64 bf16), 32-B units XOR-swizzled by (row>>1)&3: conflict-free
+// for both the 16-B row reads and the 8-row transposed reads.
+__device__ __forceinline__ int swz128(int r, int col) { return r * 128 + ((((col >> 4) ^ (r >> 1)) & 3) * 32) + (col & 15) * 2; }
+
+__device__ __forceinline__ bf16x8_t lds_b128(const char* lds, int byte) {
+  return *reinterpret_cast<const bf16x8_t*>(lds + byte);
+}
+
+// transposed fragment: lane (g=l>>4, i=l&15, q=i>>2, p=i&3) gets X[rows r0(g)+0..3][col c0+i] and
+// X[rows r1(g)+0..3][c0+i] from a swizzled [rows][64] tile
+__device__ __forceinline__ bf16x8_t tr_frag(const char* lds, int r0, int r1, int c0, int lane) {
+  const int i = lane & 15;
+  const int q = i >> 2;
+  const int p = i & 3;
+  s16x4_t v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + swz128(r0 + q, c0 + 4 * p)));
+  s16x4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + swz128(r1 + q, c0 + 4 * p)));
+  s16x8_t v = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
+__device__ __forceinline__ bf16x8_t pack_frag(const f32x4_t& a, const f32x4_t& b) {
+  bf16x8_t r;
+  r[0] = (__bf16)a[0];
+  r[1] = (__bf16)a[1];
+  r[2] = (__bf16)a[2];
+  r[3] = (__bf16)a[3];
+  r[4] = (__bf16)b[0];
+  r[5] = (__bf16)b[1];
+  r[6] = (__bf16)b[2];
+  r[7] = (__bf16)b[3];
+  return r;
+}
+
+__device__ __forceinline__ uint4 scale_bf16x8(uint4 v, float s) {
+  uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) w[k] = pack2bf(__uint_as_float(w[k] << 16) * s, __uint_as_float(w[k] & 0xffff0000u) * s);
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+struct AttnShape {
+  int64_t B, T, H, RS;  // RS = row stride of qkv (3*H*64)
+};
+
+// stage a [rows][64] bf16 tile (rows from row0, clamped to T) from column block col0 into LDS.
+// swizzled: swz128 layout; else padded [rows][72].
+template <int ROWS, bool SWZ>
+__device__ __forceinline__ void stage_load(uint4 (&reg)[ROWS / 32], const bf16_t* base, int64_t row0, int64_t T,
+                                           int64_t RS, float scale, int tid) {
+#pragma unroll
+  for (int i = 0; i < ROWS / 32; ++i) {
+    const int c = tid + 256 * i;
+    const int r = c >> 3;
+    const int c8 = (c & 7) * 8;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (row0 + r < T) v = *reinterpret_cast<const uint4*>(base + (row0 + r) * RS + c8);
+    if (scale != 1.0f) v = scale_bf16x8(v, scale);
+    reg[i] = v;
+  }
+}
+
+template <int ROWS, bool SWZ>
+__device__ __forceinline__ void stage_store(char* lds, const uint4 (&reg)[ROWS / 32], int tid) {
+#pragma unroll
+  for (int i = 0; i < ROWS / 32; ++i) {
+    const int c = tid + 256 * i;
+    const int r = c >> 3;
+    const int c8 = (c & 7) * 8;
+    const int byte = SWZ ? swz128(r, c8) : (r * PADROW + c8) * 2;
+    *reinterpret_cast<uint4*>(lds + byte) = reg[i];
+  }
+}
+
+constexpr int KTILE_PAD_BYTES = KT * PADROW * 2;   // 9216
+constexpr int TILE_SWZ_BYTES = KT * 128;           // 8192
+
+// ---------------------------------------------------------------------------
+// forward: block = (64 query rows, head h, utterance b), 4 waves x 16 rows
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) attn_fwd_kernel(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ o_u,
+                                                       bf16_t* __restrict__ o_m, float* __restrict__ lse,
+                                                       const float* __restrict__ head_mask,
+                                                       const int64_t* __restrict__ key_len, AttnShape sh, float scale,
+                                                       float drop_p, uint64_t seed) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * (KTILE_PAD_BYTES + TILE_SWZ_BYTES)];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int g = lane >> 4;
+  const int64_t b = blockIdx.z;
+  const int64_t h = blockIdx.y;
+  const int64_t T = sh.T, H = sh.H, RS = sh.RS;
+  const int64_t q0 = (int64_t)blockIdx.x * QT + wave * 16;
+  const int64_t qme = q0 + (lane & 15);
+  const bf16_t* rowbase = qkv + b * T * RS;
+  const int64_t klen = key_len ? key_len[b] : T;
+
+  // Q' = scale*q fragments (B operand of S^T = K Q'^T): Q'[q = lane&15][hd = 32ks + 8g + j]
+  bf16x8_t qf[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (qme < T) v = *reinterpret_cast<const uint4*>(rowbase + qme * RS + h * HD + ks * 32 + 8 * g);
+    qf[ks] = __builtin_bit_cast(bf16x8_t, scale_bf16x8(v, scale));
+  }
+
+  f32x4_t oacc[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) oacc[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  float m_run = -INFINITY, l_run = 0.f;
+  const float inv_keep = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
+
+  const int nkt = (int)cdiv(T, KT);
+  uint4 rk[2], rv[2];
+  auto ldsK = [&](int buf) { return smem + buf * (KTILE_PAD_BYTES + TILE_SWZ_BYTES); };
+  auto ldsV = [&](int buf) { return smem + buf * (KTILE_PAD_BYTES + TILE_SWZ_BYTES) + KTILE_PAD_BYTES; };
+  stage_load<KT, false>(rk, rowbase + (H + h) * HD, 0, T, RS, 1.0f, tid);
+  stage_load<KT, true>(rv, rowbase + (2 * H + h) * HD, 0, T, RS, 1.0f, tid);
+  stage_store<KT, false>(ldsK(0), rk, tid);
+  stage_store<KT, true>(ldsV(0), rv, tid);
+  __syncthreads();
+
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int cur = kt & 1;
+    const bool more = kt + 1 < nkt;
+    if (more) {
+      stage_load<KT, false>(rk, rowbase + (H + h) * HD, (int64_t)(kt + 1) * KT, T, RS, 1.0f, tid);
+      stage_load<KT, true>(rv, rowbase + (2 * H + h) * HD, (int64_t)(kt + 1) * KT, T, RS, 1.0f, tid);
+    }
+    const char* K_ = ldsK(cur);
+    const char* V_ = ldsV(cur);
+    // S^T[key = 16s + 4g + i][q = lane&15]
+    f32x4_t sacc[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      sacc[s] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const bf16x8_t kf = lds_b128(K_, ((16 * s + (lane & 15)) * PADROW + ks * 32 + 8 * g) * 2);
+        sacc[s] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[ks], sacc[s], 0, 0, 0);
+      }
+    }
+    float mt = -INFINITY;
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int64_t key = (int64_t)kt * KT + 16 * s + 4 * g + i;
+        float v = sacc[s][i];
+        if (key >= klen) v += -10000.0f;
+        if (key >= T) v = -INFINITY;
+        sacc[s][i] = v;
+        mt = fmaxf(mt, v);
+      }
+    mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    const float m_new = fmaxf(m_run, mt);
+    const float alpha = __expf(m_run - m_new);
+    float ls = 0.f;
+    const uint64_t drow = (((uint64_t)(b * H + h) * T) + (uint64_t)qme) * (uint64_t)T;
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float p = __expf(sacc[s][i] - m_new);
+        ls += p;
+        const int64_t key = (int64_t)kt * KT + 16 * s + 4 * g + i;
+        sacc[s][i] = p * dropout_scale(seed, drow + key, drop_p, inv_keep);
+      }
+    ls += __shfl_xor(ls, 16, 64);
+    ls += __shfl_xor(ls, 32, 64);
+    l_run = l_run * alpha + ls;
+    m_run = m_new;
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) oacc[d][i] *= alpha;
+    // O^T[d][q] += V^T[d][key] P^T[key][q]; k index of step kk: key(g,j) = 16(2kk + j/4) + 4g + j%4
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const bf16x8_t pf = pack_frag(sacc[2 * kk], sacc[2 * kk + 1]);
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const bf16x8_t vf = tr_frag(V_, 32 * kk + 4 * g, 32 * kk + 16 + 4 * g, 16 * d, lane);
+        oacc[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf, oacc[d], 0, 0, 0);
+      }
+    }
+    if (more) {
+      stage_store<KT, false>(ldsK(cur ^ 1), rk, tid);
+      stage_store<KT, true>(ldsV(cur ^ 1), rv, tid);
+    }
+    __syncthreads();
+  }
+
+  if (qme < T) {
+    const float inv_l = 1.0f / l_run;
+    const float hm = head_mask ? head_mask[h] : 1.0f;
+    const int64_t obase = (b * T + qme) * (H * HD) + h * HD;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const int col = 16 * d + 4 * g;
+      float v[4] = {oacc[d][0] * inv_l, oacc[d][1] * inv_l, oacc[d][2] * inv_l, oacc[d][3] * inv_l};
+      *reinterpret_cast<uint2*>(o_u + obase + col) = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
+      *reinterpret_cast<uint2*>(o_m + obase + col) =
+          make_uint2(pack2bf(v[0] * hm, v[1] * hm), pack2bf(v[2] * hm, v[3] * hm));
+    }
+    if (g == 0) lse[(b * H + h) * T + qme] = m_run + __logf(l_run);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// backward prep: rowdot[b][h][t] = sum_d dO_m * O_u ; D = hm * rowdot ; dhm[h] += sum rowdot
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) attn_bwd_prep_kernel(const bf16_t* __restrict__ dom,
+                                                            const bf16_t* __restrict__ ou,
+                                                            const float* __restrict__ head_mask,
+                                                            float* __restrict__ Dv, float* __restrict__ dhm,
+                                                            int64_t B, int64_t T, int64_t H) {
+  __shared__ float red[4];
+  const int64_t h = blockIdx.y;
+  const int64_t bt = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  float rd = 0.f;
+  if (bt < B * T) {
+    const bf16_t* a = dom + bt * H * HD + h * HD;
+    const bf16_t* c = ou + bt * H * HD + h * HD;
+#pragma unroll
+    for (int k = 0; k < HD; k += 8) {
+      uint4 va = *reinterpret_cast<const uint4*>(a + k);
+      uint4 vc = *reinterpret_cast<const uint4*>(c + k);
+      uint32_t wa[4] = {va.x, va.y, va.z, va.w}, wc[4] = {vc.x, vc.y, vc.z, vc.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        rd += __uint_as_float(wa[q] << 16) * __uint_as_float(wc[q] << 16);
+        rd += __uint_as_float(wa[q] & 0xffff0000u) * __uint_as_float(wc[q] & 0xffff0000u);
+      }
+    }
+    const int64_t bb = bt / T, t = bt % T;
+    const float hm = head_mask ? head_mask[h] : 1.0f;
+    Dv[(bb * H + h) * T + t] = rd * hm;
+  }
+  if (!dhm) return;
+  float s = wave_sum(rd);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(dhm + h, red[0] + red[1] + red[2] + red[3]);
+}
+
+// ---------------------------------------------------------------------------
+// backward dK, dV: block = (64 keys, h, b), wave w owns keys k0 = 64*bx + 16w .. +16.
+// Loops over query steps of 32 rows; Q' and dO' (= hm*dO_m) tiles staged in LDS.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) attn_bwd_dkv_kernel(const bf16_t* __restrict__ qkv,
+                                                           const bf16_t* __restrict__ dom,
+                                                           const float* __restrict__ head_mask,
+                                                           const float* __restrict__ lse,
+                                                           const float* __restrict__ Dv, bf16_t* __restrict__ dqkv,
+                                                           const int64_t* __restrict__ key_len, AttnShape sh,
+                                                           float scale, float drop_p, uint64_t seed) {
+  constexpr int TB = QT_BWD * 128;   // 4096 B per tile
+  __shared__ __attribute__((aligned(16))) char smem[2 * (2 * TB) + 2 * 2 * QT_BWD * 4];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int g = lane >> 4;
+  const int64_t b = blockIdx.z;
+  const int64_t h = blockIdx.y;
+  const int64_t T = sh.T, H = sh.H, RS = sh.RS;
+  const int64_t k0 = (int64_t)blockIdx.x * KT + wave * 16;
+  const int64_t kme = k0 + (lane & 15);
+  const bf16_t* rowbase = qkv + b * T * RS;
+  const bf16_t* dobase = dom + b * T * (H * HD) + h * HD;
+  const int64_t klen = key_len ? key_len[b] : T;
+  const float hm = head_mask ? head_mask[h] : 1.0f;
+  const float inv_keep = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
+
+  // K[key = lane&15][hd 32ks+8g+j], V[...]: B operands of S = Q' K^T and dP = dO V^T
+  bf16x8_t kf[2], vf[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    uint4 a = make_uint4(0, 0, 0, 0), c = make_uint4(0, 0, 0, 0);
+    if (kme < T) {
+      a = *reinterpret_cast<const uint4*>(rowbase + kme * RS + (H + h) * HD + ks * 32 + 8 * g);
+      c = *reinterpret_cast<const uint4*>(rowbase + kme * RS + (2 * H + h) * HD + ks * 32 + 8 * g);
+    }
+    kf[ks] = __builtin_bit_cast(bf16x8_t, a);
+    vf[ks] = __builtin_bit_cast(bf16x8_t, c);
+  }
+  f32x4_t dk[4], dv[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    dk[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    dv[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  }
+  auto ldsQ = [&](int buf) { return smem + buf * 2 * TB; };
+  auto ldsO = [&](int buf) { return smem + buf * 2 * TB + TB; };
+  float* lse_s = reinterpret_cast<float*>(smem + 4 * TB);        // [2][32]
+  float* dv_s = reinterpret_cast<float*>(smem + 4 * TB + 2 * QT_BWD * 4);
+
+  const int nqt = (int)cdiv(T, QT_BWD);
+  uint4 rq[1], ro[1];
+  auto load_tiles = [&](int qt) {
+    stage_load<QT_BWD, true>(rq, rowbase + h * HD, (int64_t)qt * QT_BWD, T, RS, scale, tid);
+    stage_load<QT_BWD, true>(ro, dobase, (int64_t)qt * QT_BWD, T, H * HD, hm, tid);
+  };
+  auto store_tiles = [&](int buf, int qt) {
+    stage_store<QT_BWD, true>(ldsQ(buf), rq, tid);
+    stage_store<QT_BWD, true>(ldsO(buf), ro, tid);
+    if (tid < QT_BWD) {
+      const int64_t q = (int64_t)qt * QT_BWD + tid;
+      lse_s[buf * QT_BWD + tid] = q < T ? lse[(b * H + h) * T + q] : 0.f;
+      dv_s[buf * QT_BWD + tid] = q < T ? Dv[(b * H + h) * T + q] : 0.f;
+    }
+  };
+  load_tiles(0);
+  store_tiles(0, 0);
+  __syncthreads();
+  for (int qt = 0; qt < nqt; ++qt) {
+    const int cur = qt & 1;
+    const bool more = qt + 1 < nqt;
+    if (more) load_tiles(qt + 1);
+    const char* Q_ = ldsQ(cur);
+    const char* O_ = ldsO(cur);
+    // S[q = 16u + 4g + i][key = lane&15], dP likewise
+    f32x4_t sacc[2], pacc[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      sacc[u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      pacc[u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const bf16x8_t qa = lds_b128(Q_, swz128(16 * u + (lane & 15), ks * 32 + 8 * g));
+        const bf16x8_t oa = lds_b128(O_, swz128(16 * u + (lane & 15), ks * 32 + 8 * g));
+        sacc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa, kf[ks], sacc[u], 0, 0, 0);
+        pacc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(oa, vf[ks], pacc[u], 0, 0, 0);
+      }
+    }
+    f32x4_t pz[2], ds[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int ql = 16 * u + 4 * g + i;
+        const int64_t q = (int64_t)qt * QT_BWD + ql;
+        float s = sacc[u][i];
+        if (kme >= klen) s += -10000.0f;
+        float p = __expf(s - lse_s[cur * QT_BWD + ql]);
+        if (q >= T || kme >= T) p = 0.f;
+        const float z = dropout_scale(seed, ((((uint64_t)(b * H + h) * T) + (uint64_t)q) * (uint64_t)T) + kme,
+                                      drop_p, inv_keep);
+        pz[u][i] = p * z;
+        ds[u][i] = p * (pacc[u][i] * z - dv_s[cur * QT_BWD + ql]);
+      }
+    // dV[key][d] += sum_q PZ[q][key] dO'[q][d] ; dK[key][d] += sum_q dS[q][key] Q'[q][d]
+    const bf16x8_t pzf = pack_frag(pz[0], pz[1]);
+    const bf16x8_t dsf = pack_frag(ds[0], ds[1]);
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const bf16x8_t of = tr_frag(O_, 4 * g, 16 + 4 * g, 16 * d, lane);
+      const bf16x8_t qf = tr_frag(Q_, 4 * g, 16 + 4 * g, 16 * d, lane);
+      dv[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pzf, of, dv[d], 0, 0, 0);
+      dk[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dsf, qf, dk[d], 0, 0, 0);
+    }
+    if (more) store_tiles(cur ^ 1, qt + 1);
+    __syncthreads();
+  }
+  // lane holds dK[key = k0 + 4g + i][d = 16dd + (lane&15)]
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int64_t key = k0 + 4 * g + i;
+    if (key >= T) continue;
+    bf16_t* rowp = dqkv + (b * T + key) * RS;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      rowp[(H + h) * HD + 16 * d + (lane & 15)] = f2bf(dk[d][i]);
+      rowp[(2 * H + h) * HD + 16 * d + (lane & 15)] = f2bf(dv[d][i]);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// backward dQ: block = (64 query rows, h, b), 4 waves x 16 rows; loops over key tiles.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) attn_bwd_dq_kernel(const bf16_t* __restrict__ qkv,
+                                                          const bf16_t* __restrict__ dom,
+                                                          const float* __restrict__ head_mask,
+                                                          const float* __restrict__ lse,
+                                                          const float* __restrict__ Dv, bf16_t* __restrict__ dqkv,
+                                                          const int64_t* __restrict__ key_len, AttnShape sh,
+                                                          float scale, float drop_p, uint64_t seed) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * (TILE_SWZ_BYTES + KTILE_PAD_BYTES)];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int g = lane >> 4;
+  const int64_t b = blockIdx.z;
+  const int64_t h = blockIdx.y;
+  const int64_t T = sh.T, H = sh.H, RS = sh.RS;
+  const int64_t q0 = (int64_t)blockIdx.x * QT + wave * 16;
+  const int64_t qme = q0 + (lane & 15);
+  const bf16_t* rowbase = qkv + b * T * RS;
+  const int64_t klen = key_len ? key_len[b] : T;
+  const float hm = head_mask ? head_mask[h] : 1.0f;
+  const float inv_keep = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
+
+  bf16x8_t qf[2], of[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    uint4 a = make_uint4(0, 0, 0, 0), c = make_uint4(0, 0, 0, 0);
+    if (qme < T) {
+      a = *reinterpret_cast<const uint4*>(rowbase + qme * RS + h * HD + ks * 32 + 8 * g);
+      c = *reinterpret_cast<const uint4*>(dom + (b * T + qme) * (H * HD) + h * HD + ks * 32 + 8 * g);
+    }
+    qf[ks] = __builtin_bit_cast(bf16x8_t, scale_bf16x8(a, scale));
+    of[ks] = __builtin_bit_cast(bf16x8_t, scale_bf16x8(c, hm));
+  }
+  const float my_lse = qme < T ? lse[(b * H + h) * T + qme] : 0.f;
+  const float my_D = qme < T ? Dv[(b * H + h) * T + qme] : 0.f;
+  f32x4_t dq[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) dq[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  auto ldsK = [&](int buf) { return smem + buf * (TILE_SWZ_BYTES + KTILE_PAD_BYTES); };
+  auto ldsV = [&](int buf) { return smem + buf * (TILE_SWZ_BYTES + KTILE_PAD_BYTES) + TILE_SWZ_BYTES; };
+  const int nkt = (int)cdiv(T, KT);
+  uint4 rk[2], rv[2];
+  stage_load<KT, true>(rk, rowbase + (H + h) * HD, 0, T, RS, 1.0f, tid);
+  stage_load<KT, false>(rv, rowbase + (2 * H + h) * HD, 0, T, RS, 1.0f, tid);
+  stage_store<KT, true>(ldsK(0), rk, tid);
+  stage_store<KT, false>(ldsV(0), rv, tid);
+  __syncthreads();
+  const uint64_t drow = (((uint64_t)(b * H + h) * T) + (uint64_t)qme) * (uint64_t)T;
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int cur = kt & 1;
+    const bool more = kt + 1 < nkt;
+    if (more) {
+      stage_load<KT, true>(rk, rowbase + (H + h) * HD, (int64_t)(kt + 1) * KT, T, RS, 1.0f, tid);
+      stage_load<KT, false>(rv, rowbase + (2 * H + h) * HD, (int64_t)(kt + 1) * KT, T, RS, 1.0f, tid);
+    }
+    const char* K_ = ldsK(cur);
+    const char* V_ = ldsV(cur);
+    f32x4_t ds[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      f32x4_t sa = f32x4_t{0.f, 0.f, 0.f, 0.f}, pa = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const bf16x8_t ka = lds_b128(K_, swz128(16 * s + (lane & 15), ks * 32 + 8 * g));
+        const bf16x8_t va = lds_b128(V_, ((16 * s + (lane & 15)) * PADROW + ks * 32 + 8 * g) * 2);
+        sa = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka, qf[ks], sa, 0, 0, 0);
+        pa = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, of[ks], pa, 0, 0, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int64_t key = (int64_t)kt * KT + 16 * s + 4 * g + i;
+        float sv = sa[i];
+        if (key >= klen) sv += -10000.0f;
+        float p = __expf(sv - my_lse);
+        if (key >= T || qme >= T) p = 0.f;
+        const float z = dropout_scale(seed, drow + key, drop_p, inv_keep);
+        ds[s][i] = p * (pa[i] * z - my_D);
+      }
+    }
+    // dQ'^T[d][q] += K^T[d][key] dS^T[key][q]
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const bf16x8_t dsf = pack_frag(ds[2 * kk], ds[2 * kk + 1]);
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const bf16x8_t kt_f = tr_frag(K_, 32 * kk + 4 * g, 32 * kk + 16 + 4 * g, 16 * d, lane);
+        dq[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kt_f, dsf, dq[d], 0, 0, 0);
+      }
+    }
+    if (more) {
+      stage_store<KT, true>(ldsK(cur ^ 1), rk, tid);
+      stage_store<KT, false>(ldsV(cur ^ 1), rv, tid);
+    }
+    __syncthreads();
+  }
+  if (qme < T) {
+    bf16_t* rowp = dqkv + (b * T + qme) * RS + h * HD;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const int col = 16 * d + 4 * g;
+      *reinterpret_cast<uint2*>(rowp + col) = make_uint2(pack2bf(dq[d][0] * scale, dq[d][1] * scale),
+                                                         pack2bf(dq[d][2] * scale, dq[d][3] * scale));
+    }
+  }
+}
+
+}  // namespace
+}  // namespace dph
+
+using namespace dph;
+
+extern "C" int dph_attention_fwd(const void* qkv, void* o_unmasked, void* o_masked, float* lse,
+                                 const float* head_mask, const int64_t* key_len, int64_t B, int64_t T, int64_t H,
+                                 float scale, float dropout_p, uint64_t seed, hipStream_t stream) {
+  DPH_REQUIRE(qkv && o_unmasked && o_masked && lse && B > 0 && T > 0 && H > 0, "dph_attention_fwd: bad args");
+  AttnShape sh{B, T, H, 3 * H * HD};
+  dim3 grid((unsigned)cdiv(T, QT), (unsigned)H, (unsigned)B);
+  hipLaunchKernelGGL(attn_fwd_kernel, grid, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(qkv),
+                     reinterpret_cast<bf16_t*>(o_unmasked), reinterpret_cast<bf16_t*>(o_masked), lse, head_mask,
+                     key_len, sh, scale, dropout_p, seed);
+  return check_launch("dph_attention_fwd");
+}
+
+extern "C" int dph_attention_bwd_prep(const void* do_masked, const void* o_unmasked, const float* head_mask,
+                                      float* Dvec, float* dhead_mask, int64_t B, int64_t T, int64_t H,
+                                      hipStream_t stream) {
+  DPH_REQUIRE(do_masked && o_unmasked && Dvec && B > 0 && T > 0 && H > 0, "dph_attention_bwd_prep: bad args");
+  dim3 grid((unsigned)cdiv(B * T, 256), (unsigned)H);
+  hipLaunchKernelGGL(attn_bwd_prep_kernel, grid, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(do_masked),
+                     reinterpret_cast<const bf16_t*>(o_unmasked), head_mask, Dvec, dhead_mask, B, T, H);
+  return check_launch("dph_attention_bwd_prep");
+}
+
+extern "C" int dph_attention_bwd(const void* qkv, const void* do_masked, const float* head_mask, const float* lse,
+                                 const float* Dvec, void* dqkv, const int64_t* key_len, int64_t B, int64_t T,
+                                 int64_t H, float scale, float dropout_p, uint64_t seed, hipStream_t stream) {
+  DPH_REQUIRE(qkv && do_masked && lse && Dvec && dqkv && B > 0 && T > 0 && H > 0, "dph_attention_bwd: bad args");
+  AttnShape sh{B, T, H, 3 * H * HD};
+  dim3 grid((unsigned)cdiv(T, KT), (unsigned)H, (unsigned)B);
+  hipLaunchKernelGGL(attn_bwd_dkv_kernel, grid, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(qkv),
+                     reinterpret_cast<const bf16_t*>(do_masked), head_mask, lse, Dvec, reinterpret_cast<bf16_t*>(dqkv),
+                     key_len, sh, scale, dropout_p, seed);
+  int rc = check_launch("dph_attention_bwd dkv");
+  if (rc) return rc;
+  dim3 grid2((unsigned)cdiv(T, QT), (unsigned)H, (unsigned)B);
+  hipLaunchKernelGGL(attn_bwd_dq_kernel, grid2, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(qkv),
+                     reinterpret_cast<const bf16_t*>(do_masked), head_mask, lse, Dvec, reinterpret_cast<bf16_t*>(dqkv),
+                     key_len, sh, scale, dropout_p, seed);
+  return check_launch("dph_attention_bwd dq");
+}

@@ -1,0 +1,304 @@
+// Elementwise / layout kernels of the conv frontend and weight handling.
+//
+//   col2im + GELU/HardConcrete-mask backward of the strided conv layers
+//     (components.py:107-114 backward), GELU/mask backward,
+//   pos-conv regroup + zero padding (components.py:298-306,327-330 as a
+//     batched GEMM over per-group time windows),
+//   fp32 master weight -> bf16 GEMM images.
+#include "common.h"
+
+namespace dph {
+namespace {
+
+// Shared shape: block = 64 x 4 threads; thread handles 8 channels of a row,
+// grid.x over 512-channel chunks, grid.y over row ranges.  Column partials
+// (mask gradients) are reduced across the 4 row-lanes through LDS.
+template <bool COL2IM>
+__global__ void __launch_bounds__(256) gelu_mask_bwd_kernel(const bf16_t* __restrict__ src, int64_t Lout,
+                                                            int64_t Lin, int64_t C, int k, int s,
+                                                            const bf16_t* __restrict__ z_pre,
+                                                            const float* __restrict__ mask, bf16_t* __restrict__ out,
+                                                            float* __restrict__ dmask, int64_t rows,
+                                                            int64_t rows_per_block) {
+  __shared__ float red[4][512];
+  const int tx = threadIdx.x & 63;
+  const int ty = threadIdx.x >> 6;
+  const int64_t c0 = (int64_t)blockIdx.x * 512 + tx * 8;
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per_block;
+  const int64_t r1 = min(rows, r0 + rows_per_block);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float mk[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) mk[i] = (mask && c0 + i < C) ? mask[c0 + i] : 1.0f;
+  if (c0 < C) {
+    for (int64_t r = r0 + ty; r < r1; r += 4) {
+      float dy[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if constexpr (COL2IM) {
+        const int64_t b = r / Lin;
+        const int64_t tp = r % Lin;
+        for (int j = 0; j < k; ++j) {
+          const int64_t d = tp - j;
+          if (d < 0 || d % s) continue;
+          const int64_t t = d / s;
+          if (t >= Lout) continue;
+          const bf16_t* p = src + ((b * Lout + t) * k + j) * C + c0;
+#pragma unroll
+          for (int i = 0; i < 8; ++i)
+            if (c0 + i < C) dy[i] += bf2f(p[i]);
+        }
+      } else {
+        const bf16_t* p = src + r * C + c0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          if (c0 + i < C) dy[i] = bf2f(p[i]);
+      }
+      float o[8];
+      if (z_pre) {
+        const bf16_t* zp = z_pre + r * C + c0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float z = (c0 + i < C) ? bf2f(zp[i]) : 0.f;
+          acc[i] += dy[i] * gelu_f(z);
+          o[i] = dy[i] * mk[i] * gelu_grad_f(z);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = dy[i];
+      }
+      bf16_t* op = out + r * C + c0;
+      if (c0 + 8 <= C && C % 8 == 0) {
+        *reinterpret_cast<uint4*>(op) = make_uint4(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]), pack2bf(o[4], o[5]),
+                                                   pack2bf(o[6], o[7]));
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          if (c0 + i < C) op[i] = f2bf(o[i]);
+      }
+    }
+  }
+  if (!dmask) return;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) red[ty][tx * 8 + i] = acc[i];
+  __syncthreads();
+  for (int c = threadIdx.x; c < 512; c += 256) {
+    const int64_t col = (int64_t)blockIdx.x * 512 + c;
+    if (col < C) atomicAdd(dmask + col, red[0][c] + red[1][c] + red[2][c] + red[3][c]);
+  }
+}
+
+__global__ void regroup_pad_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ xg, int64_t B, int64_t T,
+                                   int64_t G, int64_t Cg, int64_t P, int64_t Q) {
+  // one thread per 8 elements of xg [B][G][P+T+Q][Cg]
+  const int64_t Tp = P + T + Q;
+  const int64_t n8 = B * G * Tp * Cg / 8;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n8) return;
+  const int64_t e = i * 8;
+  const int64_t c = e % Cg;
+  const int64_t tp = (e / Cg) % Tp;
+  const int64_t g = (e / (Cg * Tp)) % G;
+  const int64_t b = e / (Cg * Tp * G);
+  const int64_t t = tp - P;
+  uint4 v = make_uint4(0, 0, 0, 0);
+  if (t >= 0 && t < T) v = *reinterpret_cast<const uint4*>(x + (b * T + t) * (G * Cg) + g * Cg + c);
+  *reinterpret_cast<uint4*>(xg + e) = v;
+}
+
+__global__ void cast_bf16_kernel(const float* __restrict__ src, bf16_t* __restrict__ dst, int64_t n) {
+  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i + 4 <= n) {
+    float4 v = *reinterpret_cast<const float4*>(src + i);
+    *reinterpret_cast<uint2*>(dst + i) = make_uint2(pack2bf(v.x, v.y), pack2bf(v.z, v.w));
+  } else {
+    for (int64_t j = i; j < n; ++j) dst[j] = f2bf(src[j]);
+  }
+}
+
+// w [O][C][k] fp32 -> dst [O][k*C] bf16 (index j*C + c)
+__global__ void conv_pack_kernel(const float* __restrict__ w, bf16_t* __restrict__ dst, int64_t O, int64_t C,
+                                 int64_t k) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= O * C * k) return;
+  const int64_t c = i % C;
+  const int64_t j = (i / C) % k;
+  const int64_t o = i / (C * k);
+  dst[i] = f2bf(w[(o * C + c) * k + j]);
+}
+
+// g [O][k*C] fp32 -> dst [O][C][k]
+__global__ void conv_unpack_kernel(const float* __restrict__ g, float* __restrict__ dst, int64_t O, int64_t C,
+                                   int64_t k, int accum) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= O * C * k) return;
+  const int64_t j = i % k;
+  const int64_t c = (i / k) % C;
+  const int64_t o = i / (C * k);
+  const float v = g[o * k * C + j * C + c];
+  dst[i] = accum ? dst[i] + v : v;
+}
+
+__global__ void add_bf16_kernel(const bf16_t* __restrict__ a, const bf16_t* __restrict__ b, bf16_t* __restrict__ o,
+                                int64_t n) {
+  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8;
+  if (i + 8 <= n) {
+    uint4 va = *reinterpret_cast<const uint4*>(a + i);
+    uint4 vb = *reinterpret_cast<const uint4*>(b + i);
+    uint32_t wa[4] = {va.x, va.y, va.z, va.w}, wb[4] = {vb.x, vb.y, vb.z, vb.w}, wo[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float lo = __uint_as_float(wa[q] << 16) + __uint_as_float(wb[q] << 16);
+      const float hi = __uint_as_float(wa[q] & 0xffff0000u) + __uint_as_float(wb[q] & 0xffff0000u);
+      wo[q] = pack2bf(lo, hi);
+    }
+    *reinterpret_cast<uint4*>(o + i) = make_uint4(wo[0], wo[1], wo[2], wo[3]);
+  } else {
+    for (int64_t j = i; j < n; ++j) o[j] = f2bf(bf2f(a[j]) + bf2f(b[j]));
+  }
+}
+
+// out = dy * drop(p, seed, m*cols+n) * (*smask), rows with (m % len_rows) >= row_len[m / len_rows] zeroed;
+// colsum[n] += out; sdot += sum dy*drop*pre
+__global__ void __launch_bounds__(256) branch_bwd_kernel(const bf16_t* __restrict__ dy, bf16_t* __restrict__ out,
+                                                         int64_t rows, int64_t cols, float p, uint64_t seed,
+                                                         const float* __restrict__ smask,
+                                                         const int64_t* __restrict__ row_len, int64_t len_rows,
+                                                         float* __restrict__ colsum, const bf16_t* __restrict__ pre,
+                                                         float* __restrict__ sdot, int64_t rows_per_block) {
+  __shared__ float red[4][512];
+  __shared__ float sred[4];
+  const int tx = threadIdx.x & 63;
+  const int ty = threadIdx.x >> 6;
+  const int64_t c0 = (int64_t)blockIdx.x * 512 + tx * 8;
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per_block;
+  const int64_t r1 = min(rows, r0 + rows_per_block);
+  const float inv_keep = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  const float sm = smask ? *smask : 1.0f;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float sd = 0.f;
+  if (c0 < cols) {
+    for (int64_t r = r0 + ty; r < r1; r += 4) {
+      const bool zero = row_len && ((r % len_rows) >= row_len[r / len_rows]);
+      float o[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int64_t c = c0 + i;
+        float v = 0.f;
+        if (c < cols && !zero) {
+          v = bf2f(dy[r * cols + c]) * dropout_scale(seed, (uint64_t)r * cols + c, p, inv_keep);
+          if (pre) sd += v * bf2f(pre[r * cols + c]);
+          v *= sm;
+        }
+        o[i] = v;
+        acc[i] += v;
+      }
+      bf16_t* op = out + r * cols + c0;
+      if (c0 + 8 <= cols && cols % 8 == 0) {
+        *reinterpret_cast<uint4*>(op) = make_uint4(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]), pack2bf(o[4], o[5]),
+                                                   pack2bf(o[6], o[7]));
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          if (c0 + i < cols) op[i] = f2bf(o[i]);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) red[ty][tx * 8 + i] = acc[i];
+  sd = wave_sum(sd);
+  if (tx == 0) sred[ty] = sd;
+  __syncthreads();
+  if (colsum) {
+    for (int c = threadIdx.x; c < 512; c += 256) {
+      const int64_t col = (int64_t)blockIdx.x * 512 + c;
+      if (col < cols) atomicAdd(colsum + col, red[0][c] + red[1][c] + red[2][c] + red[3][c]);
+    }
+  }
+  if (sdot && threadIdx.x == 0) atomicAdd(sdot, sred[0] + sred[1] + sred[2] + sred[3]);
+}
+
+int64_t rows_per_block_for(int64_t rows) { return std::max<int64_t>(16, cdiv(cdiv(rows, 4096), 4) * 4); }
+
+}  // namespace
+}  // namespace dph
+
+using namespace dph;
+
+extern "C" int dph_col2im_gelu_bwd(const void* dcols, int64_t B, int64_t Lout, int64_t Lin, int64_t C, int64_t k,
+                                   int64_t s, const void* z_pre, const float* mask, void* out, float* dmask,
+                                   hipStream_t stream) {
+  DPH_REQUIRE(dcols && out && B > 0 && Lout > 0 && Lin >= Lout && C > 0 && k > 0 && s > 0,
+              "dph_col2im_gelu_bwd: bad args");
+  DPH_REQUIRE(!dmask || z_pre, "dph_col2im_gelu_bwd: dmask needs z_pre");
+  const int64_t rows = B * Lin;
+  const int64_t rpb = rows_per_block_for(rows);
+  dim3 grid((unsigned)cdiv(C, 512), (unsigned)cdiv(rows, rpb));
+  hipLaunchKernelGGL(gelu_mask_bwd_kernel<true>, grid, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(dcols),
+                     Lout, Lin, C, (int)k, (int)s, reinterpret_cast<const bf16_t*>(z_pre), mask,
+                     reinterpret_cast<bf16_t*>(out), dmask, rows, rpb);
+  return check_launch("dph_col2im_gelu_bwd");
+}
+
+extern "C" int dph_gelu_mask_bwd(const void* dy, const void* z_pre, const float* mask, void* out, float* dmask,
+                                 int64_t rows, int64_t C, hipStream_t stream) {
+  DPH_REQUIRE(dy && z_pre && out && rows > 0 && C > 0, "dph_gelu_mask_bwd: bad args");
+  const int64_t rpb = rows_per_block_for(rows);
+  dim3 grid((unsigned)cdiv(C, 512), (unsigned)cdiv(rows, rpb));
+  hipLaunchKernelGGL(gelu_mask_bwd_kernel<false>, grid, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(dy),
+                     (int64_t)1, (int64_t)1, C, 1, 1, reinterpret_cast<const bf16_t*>(z_pre), mask,
+                     reinterpret_cast<bf16_t*>(out), dmask, rows, rpb);
+  return check_launch("dph_gelu_mask_bwd");
+}
+
+extern "C" int dph_regroup_pad(const void* x, void* xg, int64_t B, int64_t T, int64_t G, int64_t Cg,
+                               int64_t pad_front, int64_t pad_back, hipStream_t stream) {
+  DPH_REQUIRE(x && xg && Cg % 8 == 0 && B > 0 && T > 0 && G > 0, "dph_regroup_pad: bad args (Cg %% 8 == 0)");
+  const int64_t n8 = B * G * (pad_front + T + pad_back) * Cg / 8;
+  hipLaunchKernelGGL(regroup_pad_kernel, dim3((unsigned)cdiv(n8, 256)), dim3(256), 0, stream,
+                     reinterpret_cast<const bf16_t*>(x), reinterpret_cast<bf16_t*>(xg), B, T, G, Cg, pad_front,
+                     pad_back);
+  return check_launch("dph_regroup_pad");
+}
+
+extern "C" int dph_cast_bf16(const float* src, void* dst, int64_t n, hipStream_t stream) {
+  DPH_REQUIRE(src && dst && n > 0, "dph_cast_bf16: bad args");
+  hipLaunchKernelGGL(cast_bf16_kernel, dim3((unsigned)cdiv(cdiv(n, 4), 256)), dim3(256), 0, stream, src,
+                     reinterpret_cast<bf16_t*>(dst), n);
+  return check_launch("dph_cast_bf16");
+}
+
+extern "C" int dph_conv_weight_pack(const float* w, void* dst, int64_t O, int64_t C, int64_t k, hipStream_t stream) {
+  DPH_REQUIRE(w && dst && O > 0 && C > 0 && k > 0, "dph_conv_weight_pack: bad args");
+  hipLaunchKernelGGL(conv_pack_kernel, dim3((unsigned)cdiv(O * C * k, 256)), dim3(256), 0, stream, w,
+                     reinterpret_cast<bf16_t*>(dst), O, C, k);
+  return check_launch("dph_conv_weight_pack");
+}
+
+extern "C" int dph_conv_weight_unpack_grad(const float* g, float* dst, int64_t O, int64_t C, int64_t k, int accum,
+                                           hipStream_t stream) {
+  DPH_REQUIRE(g && dst && O > 0 && C > 0 && k > 0, "dph_conv_weight_unpack_grad: bad args");
+  hipLaunchKernelGGL(conv_unpack_kernel, dim3((unsigned)cdiv(O * C * k, 256)), dim3(256), 0, stream, g, dst, O, C, k,
+                     accum);
+  return check_launch("dph_conv_weight_unpack_grad");
+}
+
+extern "C" int dph_add_bf16(const void* a, const void* b, void* out, int64_t n, hipStream_t stream) {
+  DPH_REQUIRE(a && b && out && n > 0, "dph_add_bf16: bad args");
+  hipLaunchKernelGGL(add_bf16_kernel, dim3((unsigned)cdiv(cdiv(n, 8), 256)), dim3(256), 0, stream,
+                     reinterpret_cast<const bf16_t*>(a), reinterpret_cast<const bf16_t*>(b),
+                     reinterpret_cast<bf16_t*>(out), n);
+  return check_launch("dph_add_bf16");
+}
+
+extern "C" int dph_branch_bwd(const void* dy, void* out, int64_t rows, int64_t cols, float p, uint64_t seed,
+                              const float* smask, const int64_t* row_len, int64_t len_rows, float* colsum,
+                              const void* pre, float* sdot, hipStream_t stream) {
+  DPH_REQUIRE(dy && out && rows > 0 && cols > 0, "dph_branch_bwd: bad args");
+  DPH_REQUIRE(!row_len || len_rows > 0, "dph_branch_bwd: row_len needs len_rows");
+  DPH_REQUIRE(!sdot || pre, "dph_branch_bwd: sdot needs pre");
+  const int64_t rpb = rows_per_block_for(rows);
+  dim3 grid((unsigned)cdiv(cols, 512), (unsigned)cdiv(rows, rpb));
+  hipLaunchKernelGGL(branch_bwd_kernel, grid, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(dy),
+                     reinterpret_cast<bf16_t*>(out), rows, cols, p, seed, smask, row_len, len_rows, colsum,
+                     reinterpret_cast<const bf16_t*>(pre), sdot, rpb);
+  return check_launch("dph_branch_bwd");
+}

@@ -1,0 +1,443 @@
+// Waveform frontend of the FeatureExtractor and the positional-conv weight norm.
+//
+// conv0 (1 -> C channels, kernel k0, stride s0, no bias) + GroupNorm(C, C) +
+// exact GELU + HardConcrete channel mask  (components.py:81-87,107-114,
+// 1071-1076).  conv0 has a single input channel, so it is NOT a GEMM: each
+// output is a k0-tap FIR of the waveform.  The waveform tile sits in LDS and
+// every tap is an LDS broadcast read; conv0 is recomputed (10 FMAs/output)
+// instead of ever storing its pre-norm output, so the only HBM traffic is the
+// bf16 layer output (and its gradient in backward).
+//
+// Statistics: per (utterance, channel) over L0 = floor((S-k0)/s0)+1 steps,
+// chunk-local two-pass (mean, M2) merged with Chan's formula -> torch
+// group_norm numerics (biased variance, eps=1e-5).
+//
+// Weight norm (components.py:306, dim=2): w = g * v / ||v||_(dims 0,1).
+#include "common.h"
+
+namespace dph {
+namespace {
+
+constexpr int MAXK0 = 10;   // conv0 kernel (512,10,5) of every wav2vec2/HuBERT config
+constexpr int STAT_CH = 256;     // time steps per stats chunk
+constexpr int APPLY_ROWS = 64;   // time steps per apply block
+constexpr int BWD_ROWS = 512;    // time steps per backward block
+
+struct Conv0 {
+  int64_t B, S, C, L0;
+  int k0, s0;
+};
+
+// partial stats: ws[((b*nch + ch)*C + c)*2 + {0,1}] = (mean_chunk, M2_chunk)
+__global__ void __launch_bounds__(256) conv0_stats_kernel(const float* __restrict__ wave, const float* __restrict__ w,
+                                                          Conv0 p, float* __restrict__ ws, int nch) {
+  __shared__ float xs[STAT_CH * 8 + MAXK0];
+  const int64_t b = blockIdx.y;
+  const int ch = blockIdx.x;
+  const int64_t t0 = (int64_t)ch * STAT_CH;
+  const int nt = (int)min<int64_t>(STAT_CH, p.L0 - t0);
+  const int nsamp = (nt - 1) * p.s0 + p.k0;
+  const float* xw = wave + b * p.S + t0 * p.s0;
+  for (int i = threadIdx.x; i < nsamp; i += blockDim.x) xs[i] = xw[i];
+  __syncthreads();
+  for (int64_t c = threadIdx.x; c < p.C; c += blockDim.x) {
+    float wr[MAXK0];
+#pragma unroll
+    for (int j = 0; j < MAXK0; ++j) wr[j] = j < p.k0 ? w[c * p.k0 + j] : 0.f;
+    float s = 0.f;
+    for (int t = 0; t < nt; ++t) {
+      float v = 0.f;
+#pragma unroll
+      for (int j = 0; j < MAXK0; ++j)
+        if (j < p.k0) v += wr[j] * xs[t * p.s0 + j];
+      s += v;
+    }
+    const float m = s / nt;
+    float q = 0.f;
+    for (int t = 0; t < nt; ++t) {
+      float v = 0.f;
+#pragma unroll
+      for (int j = 0; j < MAXK0; ++j)
+        if (j < p.k0) v += wr[j] * xs[t * p.s0 + j];
+      const float d = v - m;
+      q += d * d;
+    }
+    float* o = ws + ((b * nch + ch) * p.C + c) * 2;
+    o[0] = m;
+    o[1] = q;
+  }
+}
+
+__global__ void conv0_stats_finalize(const float* __restrict__ ws, Conv0 p, int nch, float* __restrict__ mean,
+                                     float* __restrict__ rstd, float eps) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= p.B * p.C) return;
+  const int64_t b = i / p.C;
+  const int64_t c = i % p.C;
+  double n = 0.0, m = 0.0, M2 = 0.0;
+  for (int ch = 0; ch < nch; ++ch) {
+    const double nb = (double)min<int64_t>(STAT_CH, p.L0 - (int64_t)ch * STAT_CH);
+    const float* o = ws + ((b * nch + ch) * p.C + c) * 2;
+    const double mb = o[0], M2b = o[1];
+    const double nn = n + nb;
+    const double d = mb - m;
+    m += d * nb / nn;
+    M2 += M2b + d * d * n * nb / nn;
+    n = nn;
+  }
+  mean[i] = (float)m;
+  rstd[i] = (float)(1.0 / sqrt(M2 / n + (double)eps));
+}
+
+// thread layout for apply/backward: TPR threads per time row, 8 channels each
+struct RowLayout {
+  int tpr, rpp;  // threads per row, rows per pass
+  __device__ RowLayout(int64_t C) {
+    tpr = (int)((C + 7) / 8);
+    rpp = max(1, 256 / tpr);
+  }
+};
+
+template <bool GN>
+__global__ void __launch_bounds__(256) conv0_apply_kernel(const float* __restrict__ wave, const float* __restrict__ w,
+                                                          const float* __restrict__ bias, Conv0 p,
+                                                          const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta,
+                                                          const float* __restrict__ mask,
+                                                          const float* __restrict__ mean,
+                                                          const float* __restrict__ rstd, bf16_t* __restrict__ y) {
+  __shared__ float xs[APPLY_ROWS * 8 + MAXK0];
+  const int64_t b = blockIdx.y;
+  const int64_t t0 = (int64_t)blockIdx.x * APPLY_ROWS;
+  const int nt = (int)min<int64_t>(APPLY_ROWS, p.L0 - t0);
+  const int nsamp = (nt - 1) * p.s0 + p.k0;
+  const float* xw = wave + b * p.S + t0 * p.s0;
+  for (int i = threadIdx.x; i < nsamp; i += blockDim.x) xs[i] = xw[i];
+  __syncthreads();
+  RowLayout L(p.C);
+  const int tid = threadIdx.x;
+  if (tid >= L.tpr * L.rpp) return;
+  const int64_t c0 = (int64_t)(tid % L.tpr) * 8;
+  const int r0 = tid / L.tpr;
+  float wr[8][MAXK0], sc[8], sh[8], mk[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int64_t c = c0 + i;
+    const bool ok = c < p.C;
+#pragma unroll
+    for (int j = 0; j < MAXK0; ++j) wr[i][j] = (ok && j < p.k0) ? w[c * p.k0 + j] : 0.f;
+    if (GN) {
+      const float rs = ok ? rstd[b * p.C + c] : 0.f;
+      const float g = ok ? gamma[c] : 0.f;
+      sc[i] = g * rs;
+      sh[i] = ok ? beta[c] - mean[b * p.C + c] * g * rs : 0.f;
+    } else {
+      sc[i] = 1.f;
+      sh[i] = (ok && bias) ? bias[c] : 0.f;
+    }
+    mk[i] = (ok && mask) ? mask[c] : 1.f;
+  }
+  for (int t = r0; t < nt; t += L.rpp) {
+    float o[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float v = 0.f;
+#pragma unroll
+      for (int j = 0; j < MAXK0; ++j)
+        if (j < p.k0) v += wr[i][j] * xs[t * p.s0 + j];
+      v = v * sc[i] + sh[i];
+      o[i] = GN ? gelu_f(v) * mk[i] : v;
+    }
+    bf16_t* yp = y + ((b * p.L0) + t0 + t) * p.C + c0;
+    if (c0 + 8 <= p.C && p.C % 8 == 0) {
+      *reinterpret_cast<uint4*>(yp) = make_uint4(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]), pack2bf(o[4], o[5]),
+                                                 pack2bf(o[6], o[7]));
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        if (c0 + i < p.C) yp[i] = f2bf(o[i]);
+    }
+  }
+}
+
+// Backward pass 1 (PASS=1): per-(b,c) sums A = sum dxh, Bv = sum dxh*xh; per-c dgamma, dbeta, dmask.
+// Backward pass 2 (PASS=2): dconv = rstd*(dxh - A/N - xh*Bv/N); dw[c][j] += sum dconv * x[s0 t + j].
+template <int PASS>
+__global__ void __launch_bounds__(256) conv0_gn_bwd_kernel(const float* __restrict__ wave,
+                                                           const float* __restrict__ w, Conv0 p,
+                                                           const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta,
+                                                           const float* __restrict__ mask,
+                                                           const float* __restrict__ mean,
+                                                           const float* __restrict__ rstd,
+                                                           const bf16_t* __restrict__ dy, float* __restrict__ sums,
+                                                           float* __restrict__ dw, float* __restrict__ dgamma,
+                                                           float* __restrict__ dbeta, float* __restrict__ dmask) {
+  __shared__ float xs[BWD_ROWS * 8 + MAXK0];
+  __shared__ float red[256 * 8];
+  const int64_t b = blockIdx.y;
+  const int64_t t0 = (int64_t)blockIdx.x * BWD_ROWS;
+  const int nt = (int)min<int64_t>(BWD_ROWS, p.L0 - t0);
+  const int nsamp = (nt - 1) * p.s0 + p.k0;
+  const float* xw = wave + b * p.S + t0 * p.s0;
+  for (int i = threadIdx.x; i < nsamp; i += blockDim.x) xs[i] = xw[i];
+  __syncthreads();
+  RowLayout L(p.C);
+  const int tid = threadIdx.x;
+  const bool active = tid < L.tpr * L.rpp;
+  const int64_t c0 = active ? (int64_t)(tid % L.tpr) * 8 : 0;
+  const int r0 = active ? tid / L.tpr : 0;
+  const float invN = 1.0f / (float)p.L0;
+  float wr[8][MAXK0], mu[8], rs[8], ga[8], be[8], mk[8], sA[8], sB[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int64_t c = c0 + i;
+    const bool ok = active && c < p.C;
+#pragma unroll
+    for (int j = 0; j < MAXK0; ++j) wr[i][j] = (ok && j < p.k0) ? w[c * p.k0 + j] : 0.f;
+    mu[i] = ok ? mean[b * p.C + c] : 0.f;
+    rs[i] = ok ? rstd[b * p.C + c] : 0.f;
+    ga[i] = ok ? gamma[c] : 0.f;
+    be[i] = ok ? beta[c] : 0.f;
+    mk[i] = (ok && mask) ? mask[c] : 1.f;
+    if (PASS == 2) {
+      sA[i] = ok ? sums[(b * p.C + c) * 2 + 0] * invN : 0.f;
+      sB[i] = ok ? sums[(b * p.C + c) * 2 + 1] * invN : 0.f;
+    }
+  }
+  float acc[8][MAXK0];   // PASS1: [i][0..4] = A, Bv, dgamma, dbeta, dmask; PASS2: dw taps
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < MAXK0; ++j) acc[i][j] = 0.f;
+  if (active) {
+    for (int t = r0; t < nt; t += L.rpp) {
+      const bf16_t* dyp = dy + ((b * p.L0) + t0 + t) * p.C + c0;
+      float dyv[8];
+      if (c0 + 8 <= p.C && p.C % 8 == 0) {
+        uint4 raw = *reinterpret_cast<const uint4*>(dyp);
+        uint32_t wv[4] = {raw.x, raw.y, raw.z, raw.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          dyv[2 * q] = __uint_as_float(wv[q] << 16);
+          dyv[2 * q + 1] = __uint_as_float(wv[q] & 0xffff0000u);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) dyv[i] = (c0 + i < p.C) ? bf2f(dyp[i]) : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float v = 0.f;
+#pragma unroll
+        for (int j = 0; j < MAXK0; ++j)
+          if (j < p.k0) v += wr[i][j] * xs[t * p.s0 + j];
+        const float xh = (v - mu[i]) * rs[i];
+        const float g = ga[i] * xh + be[i];
+        const float dg = dyv[i] * mk[i] * gelu_grad_f(g);
+        const float dxh = dg * ga[i];
+        if (PASS == 1) {
+          acc[i][0] += dxh;
+          acc[i][1] += dxh * xh;
+          acc[i][2] += dg * xh;
+          acc[i][3] += dg;
+          acc[i][4] += dyv[i] * gelu_f(g);
+        } else {
+          const float dc = rs[i] * (dxh - sA[i] - xh * sB[i]);
+#pragma unroll
+          for (int j = 0; j < MAXK0; ++j)
+            if (j < p.k0) acc[i][j] += dc * xs[t * p.s0 + j];
+        }
+      }
+    }
+  }
+  // reduce over the rpp thread-rows sharing the same channels (static acc index: fully unrolled)
+  const int nacc = PASS == 1 ? 5 : p.k0;
+#pragma unroll
+  for (int a = 0; a < MAXK0; ++a) {
+    if (a < nacc) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) red[tid * 8 + i] = acc[i][a];
+      __syncthreads();
+      if (active && r0 == 0) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          float s = 0.f;
+          for (int r = 0; r < L.rpp; ++r) s += red[(r * L.tpr + (tid % L.tpr)) * 8 + i];
+          const int64_t c = c0 + i;
+          if (c < p.C) {
+            if (PASS == 1) {
+              if (a == 0) atomicAdd(sums + (b * p.C + c) * 2 + 0, s);
+              else if (a == 1) atomicAdd(sums + (b * p.C + c) * 2 + 1, s);
+              else if (a == 2 && dgamma) atomicAdd(dgamma + c, s);
+              else if (a == 3 && dbeta) atomicAdd(dbeta + c, s);
+              else if (a == 4 && dmask) atomicAdd(dmask + c, s);
+            } else {
+              atomicAdd(dw + c * p.k0 + a, s);
+            }
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// ---- weight norm -----------------------------------------------------------
+// sumsq over dims (0,1) per kernel tap j: x [R][K] (R = Cout*Cin_g), out[j] += sum_r a[r][j]*b[r][j]
+__global__ void tap_dot_kernel(const float* __restrict__ a, const float* __restrict__ bb, int64_t R, int64_t K,
+                               float* __restrict__ out, int64_t rows_per_block) {
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = min(R, r0 + rows_per_block);
+  for (int64_t j = threadIdx.x; j < K; j += blockDim.x) {
+    float s = 0.f;
+    for (int64_t r = r0; r < r1; ++r) s += a[r * K + j] * bb[r * K + j];
+    atomicAdd(out + j, s);
+  }
+}
+
+__global__ void weight_norm_apply_kernel(const float* __restrict__ g, const float* __restrict__ v,
+                                         const float* __restrict__ nsq, float* __restrict__ norm_out, int64_t Cout,
+                                         int64_t Cin, int64_t K, int64_t G, float* __restrict__ w,
+                                         bf16_t* __restrict__ wk, bf16_t* __restrict__ wt) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t n = Cout * Cin * K;
+  if (i < K && norm_out) norm_out[i] = sqrtf(nsq[i]);
+  if (i >= n) return;
+  const int64_t j = i % K;
+  const int64_t c = (i / K) % Cin;
+  const int64_t o = i / (K * Cin);
+  const float val = g[j] * v[i] / sqrtf(nsq[j]);
+  if (w) w[i] = val;
+  const int64_t Cg = Cout / G;
+  const int64_t grp = o / Cg;
+  const int64_t oo = o % Cg;
+  if (wk) wk[(grp * Cg + oo) * (K * Cin) + j * Cin + c] = f2bf(val);
+  if (wt) wt[(grp * Cin + c) * (K * Cg) + (K - 1 - j) * Cg + oo] = f2bf(val);
+}
+
+// dw from the GEMM image layout [G][Cg][K*Cin] (index j*Cin + c) into [Cout][Cin][K]
+__global__ void img_to_weight_kernel(const float* __restrict__ img, float* __restrict__ dw, int64_t Cout, int64_t Cin,
+                                     int64_t K, int64_t G) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= Cout * Cin * K) return;
+  const int64_t j = i % K;
+  const int64_t c = (i / K) % Cin;
+  const int64_t o = i / (K * Cin);
+  const int64_t Cg = Cout / G;
+  dw[i] = img[((o / Cg) * Cg + o % Cg) * (K * Cin) + j * Cin + c];
+}
+
+__global__ void weight_norm_bwd_kernel(const float* __restrict__ dw, const float* __restrict__ g,
+                                       const float* __restrict__ v, const float* __restrict__ norm,
+                                       const float* __restrict__ S, int64_t n, int64_t K, float* __restrict__ dg,
+                                       float* __restrict__ dv) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < K && dg) dg[i] = S[i] / norm[i];
+  if (i >= n) return;
+  const int64_t j = i % K;
+  const float nj = norm[j];
+  dv[i] = g[j] / nj * dw[i] - g[j] * S[j] / (nj * nj * nj) * v[i];
+}
+
+}  // namespace
+}  // namespace dph
+
+using namespace dph;
+
+static Conv0 make_conv0(int64_t B, int64_t S, int64_t C, int64_t k0, int64_t s0) {
+  Conv0 p;
+  p.B = B;
+  p.S = S;
+  p.C = C;
+  p.k0 = (int)k0;
+  p.s0 = (int)s0;
+  p.L0 = (S - k0) / s0 + 1;
+  return p;
+}
+
+extern "C" int dph_conv0_gn_fwd(const float* wave, int64_t B, int64_t S, const float* w, int64_t C, int64_t k0,
+                                int64_t s0, const float* gamma, const float* beta, const float* mask, void* y,
+                                float* mean, float* rstd, float* ws, int64_t ws_bytes, hipStream_t stream) {
+  DPH_REQUIRE(wave && w && gamma && beta && y && mean && rstd && ws, "dph_conv0_gn_fwd: null pointer");
+  DPH_REQUIRE(k0 >= 1 && k0 <= MAXK0 && s0 >= 1 && s0 <= 8 && S >= k0 && C <= 2048,
+              "dph_conv0_gn_fwd: unsupported k0=%lld s0=%lld C=%lld", (long long)k0, (long long)s0, (long long)C);
+  Conv0 p = make_conv0(B, S, C, k0, s0);
+  const int nch = (int)cdiv(p.L0, STAT_CH);
+  DPH_REQUIRE(ws_bytes >= (int64_t)B * nch * C * 2 * 4, "dph_conv0_gn_fwd: workspace too small");
+  hipLaunchKernelGGL(conv0_stats_kernel, dim3(nch, (unsigned)B), dim3(256), 0, stream, wave, w, p, ws, nch);
+  hipLaunchKernelGGL(conv0_stats_finalize, dim3((unsigned)cdiv(B * C, 256)), dim3(256), 0, stream, ws, p, nch, mean,
+                     rstd, 1e-5f);
+  hipLaunchKernelGGL(conv0_apply_kernel<true>, dim3((unsigned)cdiv(p.L0, APPLY_ROWS), (unsigned)B), dim3(256), 0,
+                     stream, wave, w, (const float*)nullptr, p, gamma, beta, mask, mean, rstd,
+                     reinterpret_cast<bf16_t*>(y));
+  return check_launch("dph_conv0_gn_fwd");
+}
+
+extern "C" int dph_conv0_fwd(const float* wave, int64_t B, int64_t S, const float* w, const float* bias, int64_t C,
+                             int64_t k0, int64_t s0, void* y, hipStream_t stream) {
+  DPH_REQUIRE(wave && w && y, "dph_conv0_fwd: null pointer");
+  DPH_REQUIRE(k0 >= 1 && k0 <= MAXK0 && s0 >= 1 && s0 <= 8 && S >= k0 && C <= 2048, "dph_conv0_fwd: unsupported");
+  Conv0 p = make_conv0(B, S, C, k0, s0);
+  hipLaunchKernelGGL(conv0_apply_kernel<false>, dim3((unsigned)cdiv(p.L0, APPLY_ROWS), (unsigned)B), dim3(256), 0,
+                     stream, wave, w, bias, p, (const float*)nullptr, (const float*)nullptr, (const float*)nullptr,
+                     (const float*)nullptr, (const float*)nullptr, reinterpret_cast<bf16_t*>(y));
+  return check_launch("dph_conv0_fwd");
+}
+
+extern "C" int dph_conv0_gn_bwd(const float* wave, int64_t B, int64_t S, const float* w, int64_t C, int64_t k0,
+                                int64_t s0, const float* gamma, const float* beta, const float* mask,
+                                const float* mean, const float* rstd, const void* dy, float* dw, float* dgamma,
+                                float* dbeta, float* dmask, float* ws, int64_t ws_bytes, hipStream_t stream) {
+  DPH_REQUIRE(wave && w && gamma && beta && mean && rstd && dy && dw && ws, "dph_conv0_gn_bwd: null pointer");
+  DPH_REQUIRE(k0 >= 1 && k0 <= MAXK0 && s0 >= 1 && s0 <= 8 && S >= k0 && C <= 2048, "dph_conv0_gn_bwd: unsupported");
+  DPH_REQUIRE(ws_bytes >= B * C * 2 * 4, "dph_conv0_gn_bwd: workspace too small");
+  Conv0 p = make_conv0(B, S, C, k0, s0);
+  hipMemsetAsync(ws, 0, B * C * 2 * 4, stream);
+  dim3 grid((unsigned)cdiv(p.L0, BWD_ROWS), (unsigned)B);
+  hipLaunchKernelGGL(conv0_gn_bwd_kernel<1>, grid, dim3(256), 0, stream, wave, w, p, gamma, beta, mask, mean, rstd,
+                     reinterpret_cast<const bf16_t*>(dy), ws, dw, dgamma, dbeta, dmask);
+  hipLaunchKernelGGL(conv0_gn_bwd_kernel<2>, grid, dim3(256), 0, stream, wave, w, p, gamma, beta, mask, mean, rstd,
+                     reinterpret_cast<const bf16_t*>(dy), ws, dw, dgamma, dbeta, dmask);
+  return check_launch("dph_conv0_gn_bwd");
+}
+
+extern "C" int dph_weight_norm_fwd(const float* g, const float* v, int64_t Cout, int64_t Cin_g, int64_t K, int64_t G,
+                                   float* w, float* norm, void* wk, void* wt, hipStream_t stream) {
+  DPH_REQUIRE(g && v && norm && Cout % G == 0 && K <= 4096, "dph_weight_norm_fwd: bad args");
+  // norm doubles as the sum-of-squares accumulator before the sqrt
+  float* nsq = norm;
+  hipMemsetAsync(nsq, 0, K * 4, stream);
+  const int64_t R = Cout * Cin_g;
+  const int64_t rpb = 64;
+  hipLaunchKernelGGL(tap_dot_kernel, dim3((unsigned)cdiv(R, rpb)), dim3(128), 0, stream, v, v, R, K, nsq, rpb);
+  const int64_t n = Cout * Cin_g * K;
+  // apply reads nsq; the sqrt is written back in place by the first K threads AFTER all reads of
+  // that tap?  No: write norms in a separate, final pass to avoid the read/write race.
+  hipLaunchKernelGGL(weight_norm_apply_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, stream, g, v, nsq,
+                     (float*)nullptr, Cout, Cin_g, K, G, w, reinterpret_cast<bf16_t*>(wk),
+                     reinterpret_cast<bf16_t*>(wt));
+  hipLaunchKernelGGL(weight_norm_apply_kernel, dim3((unsigned)cdiv(K, 256)), dim3(256), 0, stream, g, v, nsq, norm,
+                     (int64_t)0, Cin_g, K, G, (float*)nullptr, (bf16_t*)nullptr, (bf16_t*)nullptr);
+  return check_launch("dph_weight_norm_fwd");
+}
+
+extern "C" int dph_weight_norm_bwd(const float* dw_img, const float* g, const float* v, const float* norm,
+                                   int64_t Cout, int64_t Cin_g, int64_t K, int64_t G, float* dg, float* dv,
+                                   hipStream_t stream) {
+  DPH_REQUIRE(dw_img && g && v && norm && dg && dv && Cout % G == 0, "dph_weight_norm_bwd: bad args");
+  const int64_t n = Cout * Cin_g * K;
+  // dv doubles as the [Cout][Cin][K] copy of dw, S (K floats) lives in dg until the final pass
+  hipLaunchKernelGGL(img_to_weight_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, stream, dw_img, dv, Cout, Cin_g,
+                     K, G);
+  hipMemsetAsync(dg, 0, K * 4, stream);
+  const int64_t R = Cout * Cin_g;
+  hipLaunchKernelGGL(tap_dot_kernel, dim3((unsigned)cdiv(R, 64)), dim3(128), 0, stream, dv, v, R, K, dg, (int64_t)64);
+  // dv_out = (g/n) dw - g S/n^3 v  computed in place (each element reads only its own dv)
+  hipLaunchKernelGGL(weight_norm_bwd_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, stream, dv, g, v, norm, dg,
+                     n, K, (float*)nullptr, dv);
+  // dg = S / n  (separate pass: S is read above)
+  hipLaunchKernelGGL(weight_norm_bwd_kernel, dim3((unsigned)cdiv(K, 256)), dim3(256), 0, stream, dv, g, v, norm, dg,
+                     (int64_t)0, K, dg, dv);
+  return check_launch("dph_weight_norm_bwd");
+}

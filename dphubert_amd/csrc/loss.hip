@@ -1,0 +1,170 @@
+// Layer-wise distillation loss (lightning.py:116-139) forward + backward.
+//
+// s: student projections, fp32, layer-major [L][B][T][D] (the rows of
+//    torch.stack(dim=1) of lightning.py:263 in another order; the loss is a
+//    mean over rows, so the order does not matter);
+// t: teacher hidden states, bf16, L separate [B][T][D] buffers
+//    (= torch.stack of lightning.py:250-252 without the copy).
+// loss = l2w*mean((s-t)^2) + l1w*mean|s-t| + cosw*(-mean cos)            (raw)
+//                                          + cosw*(-mean log sigmoid(cos)) (log_sig)
+// cos = s.t / (max(|s|,eps) * max(|t|,eps)), eps = 1e-8 (nn.CosineSimilarity).
+// One wave per (b, l, t) row; row statistics are kept for the backward.
+#include "common.h"
+
+namespace dph {
+namespace {
+
+struct TPtrs {
+  const bf16_t* p[DPH_MAX_DISTILL_LAYERS];
+};
+
+constexpr float COS_EPS = 1e-8f;
+
+__device__ __forceinline__ float log_sigmoid(float x) { return x >= 0.f ? -log1pf(__expf(-x)) : x - log1pf(__expf(x)); }
+
+__global__ void __launch_bounds__(256) loss_fwd_kernel(const float* __restrict__ s, TPtrs tp, int64_t B, int64_t L,
+                                                       int64_t T, int64_t D, int cos_logsig,
+                                                       float* __restrict__ rowstats, float* __restrict__ partial) {
+  __shared__ float red[4][3];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int64_t rows = B * L * T;
+  float l1 = 0.f, l2 = 0.f, cterm = 0.f;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + wave; row < rows; row += (int64_t)gridDim.x * 4) {
+    const int64_t t = row % T;
+    const int64_t b = (row / T) % B;
+    const int64_t l = row / (T * B);
+    const float* sr = s + row * D;
+    const bf16_t* tr = tp.p[l] + (b * T + t) * D;
+    float dot = 0.f, ns = 0.f, nt = 0.f;
+    for (int64_t c = lane * 4; c < D; c += 256) {
+      const float4 sv = *reinterpret_cast<const float4*>(sr + c);
+      const uint2 tv = *reinterpret_cast<const uint2*>(tr + c);
+      const float a[4] = {sv.x, sv.y, sv.z, sv.w};
+      const float bb[4] = {__uint_as_float(tv.x << 16), __uint_as_float(tv.x & 0xffff0000u),
+                           __uint_as_float(tv.y << 16), __uint_as_float(tv.y & 0xffff0000u)};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float d = a[i] - bb[i];
+        l1 += fabsf(d);
+        l2 += d * d;
+        dot += a[i] * bb[i];
+        ns += a[i] * a[i];
+        nt += bb[i] * bb[i];
+      }
+    }
+    dot = wave_sum(dot);
+    ns = wave_sum(ns);
+    nt = wave_sum(nt);
+    const float cs = dot / (fmaxf(sqrtf(ns), COS_EPS) * fmaxf(sqrtf(nt), COS_EPS));
+    cterm += cos_logsig ? log_sigmoid(cs) : cs;
+    if (lane == 0) {
+      rowstats[row * 3 + 0] = dot;
+      rowstats[row * 3 + 1] = ns;
+      rowstats[row * 3 + 2] = nt;
+    }
+  }
+  l1 = wave_sum(l1);
+  l2 = wave_sum(l2);
+  if (lane == 0) {
+    red[wave][0] = l1;
+    red[wave][1] = l2;
+    red[wave][2] = cterm;
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    const float v = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+    atomicAdd(partial + threadIdx.x, v);
+  }
+}
+
+__global__ void loss_finalize_kernel(const float* __restrict__ partial, int64_t rows, int64_t nel, float l2w, float l1w,
+                                     float cosw, float* __restrict__ out) {
+  const float mse = partial[1] / (float)nel;
+  const float l1 = partial[0] / (float)nel;
+  const float cos = -partial[2] / (float)rows;
+  out[1] = l2w != 0.f ? mse : 0.f;
+  out[2] = l1w != 0.f ? l1 : 0.f;
+  out[3] = cosw != 0.f ? cos : 0.f;
+  out[0] = l2w * out[1] + l1w * out[2] + cosw * out[3];
+}
+
+__global__ void __launch_bounds__(256) loss_bwd_kernel(const float* __restrict__ s, TPtrs tp,
+                                                       const float* __restrict__ rowstats,
+                                                       const float* __restrict__ dloss, int64_t B, int64_t L,
+                                                       int64_t T, int64_t D, float l2w, float l1w, float cosw,
+                                                       int cos_logsig, bf16_t* __restrict__ ds) {
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int64_t rows = B * L * T;
+  const int64_t row = (int64_t)blockIdx.x * 4 + wave;
+  if (row >= rows) return;
+  const int64_t t = row % T;
+  const int64_t b = (row / T) % B;
+  const int64_t l = row / (T * B);
+  const float g = dloss ? *dloss : 1.0f;
+  const float nel = (float)(rows * D);
+  const float dot = rowstats[row * 3 + 0];
+  const float ns_ = fmaxf(sqrtf(rowstats[row * 3 + 1]), COS_EPS);
+  const float nt_ = fmaxf(sqrtf(rowstats[row * 3 + 2]), COS_EPS);
+  const float cs = dot / (ns_ * nt_);
+  // d(-mean f(cos))/dcos
+  float fc = -1.0f / (float)rows;
+  if (cos_logsig) fc *= 1.0f / (1.0f + __expf(cs));   // d log sigmoid(x)/dx = sigmoid(-x)
+  fc *= cosw;
+  const float ca = fc / (ns_ * nt_);          // coefficient of t
+  const float cb = fc * cs / (ns_ * ns_);     // coefficient of s
+  const float* sr = s + row * D;
+  const bf16_t* tr = tp.p[l] + (b * T + t) * D;
+  bf16_t* dr = ds + row * D;
+  for (int64_t c = lane * 4; c < D; c += 256) {
+    const float4 sv = *reinterpret_cast<const float4*>(sr + c);
+    const uint2 tv = *reinterpret_cast<const uint2*>(tr + c);
+    const float a[4] = {sv.x, sv.y, sv.z, sv.w};
+    const float bb[4] = {__uint_as_float(tv.x << 16), __uint_as_float(tv.x & 0xffff0000u),
+                         __uint_as_float(tv.y << 16), __uint_as_float(tv.y & 0xffff0000u)};
+    float o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float d = a[i] - bb[i];
+      const float sg = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
+      o[i] = g * (l2w * 2.f * d / nel + l1w * sg / nel + ca * bb[i] - cb * a[i]);
+    }
+    *reinterpret_cast<uint2*>(dr + c) = make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
+  }
+}
+
+}  // namespace
+}  // namespace dph
+
+using namespace dph;
+
+extern "C" int dph_distill_loss_fwd(const float* s, const void* const* t_layers, int64_t B, int64_t L, int64_t T,
+                                    int64_t D, float l2w, float l1w, float cosw, int cos_logsig, float* rowstats,
+                                    float* partial, float* out, hipStream_t stream) {
+  DPH_REQUIRE(s && t_layers && rowstats && partial && out, "dph_distill_loss_fwd: null pointer");
+  DPH_REQUIRE(L >= 1 && L <= DPH_MAX_DISTILL_LAYERS && D % 4 == 0 && B > 0 && T > 0,
+              "dph_distill_loss_fwd: unsupported L=%lld D=%lld", (long long)L, (long long)D);
+  TPtrs tp;
+  for (int i = 0; i < DPH_MAX_DISTILL_LAYERS; ++i) tp.p[i] = i < L ? reinterpret_cast<const bf16_t*>(t_layers[i]) : nullptr;
+  hipMemsetAsync(partial, 0, 3 * sizeof(float), stream);
+  const int64_t rows = B * L * T;
+  hipLaunchKernelGGL(loss_fwd_kernel, dim3((unsigned)std::min<int64_t>(cdiv(rows, 4), 1024)), dim3(256), 0, stream, s,
+                     tp, B, L, T, D,
+                     cos_logsig, rowstats, partial);
+  hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(1), 0, stream, partial, rows, rows * D, l2w, l1w, cosw, out);
+  return check_launch("dph_distill_loss_fwd");
+}
+
+extern "C" int dph_distill_loss_bwd(const float* s, const void* const* t_layers, const float* rowstats,
+                                    const float* dloss, int64_t B, int64_t L, int64_t T, int64_t D, float l2w,
+                                    float l1w, float cosw, int cos_logsig, void* ds, hipStream_t stream) {
+  DPH_REQUIRE(s && t_layers && rowstats && ds, "dph_distill_loss_bwd: null pointer");
+  DPH_REQUIRE(L >= 1 && L <= DPH_MAX_DISTILL_LAYERS && D % 4 == 0, "dph_distill_loss_bwd: unsupported");
+  TPtrs tp;
+  for (int i = 0; i < DPH_MAX_DISTILL_LAYERS; ++i) tp.p[i] = i < L ? reinterpret_cast<const bf16_t*>(t_layers[i]) : nullptr;
+  const int64_t rows = B * L * T;
+  hipLaunchKernelGGL(loss_bwd_kernel, dim3((unsigned)cdiv(rows, 4)), dim3(256), 0, stream, s, tp, rowstats, dloss, B, L,
+                     T, D, l2w, l1w, cosw, cos_logsig, reinterpret_cast<bf16_t*>(ds));
+  return check_launch("dph_distill_loss_bwd");
+}

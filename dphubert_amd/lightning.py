@@ -1,0 +1,209 @@
+"""Distillation + pruning training module (drop-in for lightning.py of the reference).
+
+``DistillModule`` keeps the reference constructor (lightning.py:142-198), the
+``_step`` semantics (lightning.py:245-296: teacher forward under no_grad,
+student forward, per-layer projection, DistillLoss, Lagrangian regulariser
+on the expected sparsity) and ``configure_optimizers`` (3 AdamW groups +
+linear warmup/decay).  It is a plain ``nn.Module`` with the few
+LightningModule hooks the reference uses (``global_step``, ``log_dict``,
+``training_step``); pytorch_lightning is not installed here, and the
+multi-GPU loop lives in ``dphubert_amd.trainer`` (RCCL over xGMI).
+
+On the hot path the projection + loss run fused on the GPU
+(``ops.DistillProjLossFn``: projection GEMMs write straight into the loss
+input, teacher layers are read in place, no ``torch.stack`` copies).
+"""
+
+import math
+import pathlib
+from typing import List, Optional, Union
+
+import torch
+import torch.nn as nn
+
+from . import ops
+from .optim import FusedAdamW, LinearDecayLRScheduler
+from .wav2vec2.model import Wav2Vec2Model
+
+__all__ = ["DistillLoss", "DistillModule", "LinearDecayLRScheduler"]
+
+
+class DistillLoss(nn.Module):
+    """lightning.py:91-139: ``loss = l2*MSE + l1*L1 + cos*(-mean cos)`` (or the ``log_sig`` variant)."""
+
+    def __init__(self, l2_weight, l1_weight, cos_weight, cos_type):
+        super().__init__()
+        self.l2_weight = l2_weight
+        self.l1_weight = l1_weight
+        self.cos_weight = cos_weight
+        self.cos_type = cos_type
+        assert cos_type in ["raw", "log_sig"], cos_type
+
+    def __repr__(self) -> str:
+        return "{}(l2={}, l1={}, {}_cos={})".format(self.__class__.__name__, self.l2_weight, self.l1_weight,
+                                                    self.cos_type, self.cos_weight)
+
+    def cfg(self):
+        return {"l2": float(self.l2_weight), "l1": float(self.l1_weight), "cos": float(self.cos_weight),
+                "cos_type": self.cos_type}
+
+    def forward(self, input: torch.Tensor, target: torch.Tensor):
+        """input/target: (batch, layer, time, feature).  Returns (loss, (mse, l1, cos))."""
+        if input.ndim != 4 or input.shape != target.shape:
+            raise ValueError("DistillLoss expects matching (batch, layer, time, feature) tensors")
+        B, L, T, D = input.shape
+        s = input.float().permute(1, 0, 2, 3).contiguous()          # layer-major rows (loss is row-order free)
+        t_layers = [target[:, l].to(torch.bfloat16).contiguous() for l in range(L)]
+        loss, mse, l1, cos = _LossOnlyFn.apply(self.cfg(), B, T, s, *t_layers)
+        return loss, (mse, l1, cos)
+
+
+class _LossOnlyFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, cfg, B, T, s, *t_layers):
+        from ._lib import C as _C, call, ptr
+        L, D = s.shape[0], s.shape[-1]
+        dev = s.device
+        rowstats = torch.empty(L * B * T * 3, dtype=torch.float32, device=dev)
+        partial = torch.empty(3, dtype=torch.float32, device=dev)
+        out = torch.empty(4, dtype=torch.float32, device=dev)
+        tptrs = (_C.c_void_p * L)(*[t.data_ptr() for t in t_layers])
+        call("dph_distill_loss_fwd", ptr(s), tptrs, B, L, T, D, cfg["l2"], cfg["l1"], cfg["cos"],
+             int(cfg["cos_type"] == "log_sig"), ptr(rowstats), ptr(partial), ptr(out), ops._s())
+        ctx.cfg = (cfg, B, T, L, D)
+        ctx.save_for_backward(s, rowstats, *t_layers)
+        return out[0], out[1], out[2], out[3]
+
+    @staticmethod
+    def backward(ctx, dloss, *_):
+        from ._lib import C as _C, call, ptr
+        cfg, B, T, L, D = ctx.cfg
+        s, rowstats, *t_layers = ctx.saved_tensors
+        ds = torch.empty(s.shape, dtype=torch.bfloat16, device=s.device)
+        tptrs = (_C.c_void_p * L)(*[t.data_ptr() for t in t_layers])
+        call("dph_distill_loss_bwd", ptr(s), tptrs, ptr(rowstats), ptr(dloss.contiguous()), B, L, T, D, cfg["l2"],
+             cfg["l1"], cfg["cos"], int(cfg["cos_type"] == "log_sig"), ptr(ds), ops._s())
+        return (None, None, None, ds.float()) + (None,) * len(t_layers)
+
+
+class DistillModule(nn.Module):
+    """lightning.py:142-342 (training-step math; data loading lives outside the hot path)."""
+
+    def __init__(self, *, teacher_model: Wav2Vec2Model, student_model: Wav2Vec2Model, distill_mode: str,
+                 distill_layers: List[int], distill_linear_projs: nn.ModuleList, distill_loss: DistillLoss,
+                 learning_rate: float, weight_decay: float, warmup_updates: int, max_updates: int, use_reg: bool,
+                 reg_learning_rate: Optional[float], target_sparsity: Optional[float],
+                 sparsity_warmup_updates: Optional[int], tsv_dir: Union[str, pathlib.Path] = ".",
+                 train_subset: str = "train100", seconds_per_batch: float = 160.0, num_workers: int = 0):
+        super().__init__()
+        self.teacher_model = teacher_model
+        self.student_model = student_model
+        self.original_num_params = sum(p.numel() for p in teacher_model.parameters())
+        assert distill_mode in ["layer2layer", "predlayer"], distill_mode
+        assert len(distill_layers) == len(distill_linear_projs)
+        self.distill_mode = distill_mode
+        self.distill_layers = distill_layers
+        self.distill_linear_projs = distill_linear_projs
+        self.distill_loss = distill_loss
+        self.learning_rate = learning_rate
+        self.weight_decay = weight_decay
+        self.warmup_updates = warmup_updates
+        self.max_updates = max_updates
+        self.use_reg = use_reg
+        self.reg_learning_rate = reg_learning_rate
+        self.target_sparsity = target_sparsity
+        self.sparsity_warmup_updates = sparsity_warmup_updates
+        if self.use_reg:
+            self.lambda1 = nn.Parameter(torch.tensor(0.0))
+            self.lambda2 = nn.Parameter(torch.tensor(0.0))
+        self.tsv_dir = tsv_dir
+        self.train_subset = train_subset
+        self.seconds_per_batch = seconds_per_batch
+        self.num_workers = num_workers
+        self.global_step = 0
+        self.logged = {}
+        # distinct projection modules (shared per group, distill.py:94-99) and the per-layer index into them
+        uniq, index = [], []
+        for m in distill_linear_projs:
+            for j, u in enumerate(uniq):
+                if u is m:
+                    index.append(j)
+                    break
+            else:
+                uniq.append(m)
+                index.append(len(uniq) - 1)
+        self._proj_uniq = uniq
+        self._proj_index = index
+
+    # ---- LightningModule surface ------------------------------------------
+    def log_dict(self, d, **kw):
+        self.logged.update(d)
+
+    def configure_optimizers(self, clip_norm: Optional[float] = None):
+        main_params = [p for n, p in self.student_model.named_parameters() if "log_alpha" not in n and p.requires_grad]
+        main_params.extend(list(self.distill_linear_projs.parameters()))
+        seen, mp = set(), []
+        for p in main_params:
+            if id(p) not in seen:
+                seen.add(id(p))
+                mp.append(p)
+        pgs = [{"params": mp, "lr": self.learning_rate, "weight_decay": self.weight_decay, "name": "main_params"}]
+        if self.use_reg:
+            pgs.extend([
+                {"params": [p for n, p in self.student_model.named_parameters() if "log_alpha" in n],
+                 "lr": self.reg_learning_rate, "weight_decay": 0.0, "name": "log_alpha"},
+                {"params": [self.lambda1, self.lambda2], "lr": -self.reg_learning_rate, "weight_decay": 0.0,
+                 "name": "lambda"},
+            ])
+        optimizer = FusedAdamW(pgs, max_grad_norm=clip_norm)
+        lr_scheduler = LinearDecayLRScheduler(optimizer, warmup_updates=self.warmup_updates,
+                                              max_updates=self.max_updates)
+        return {"optimizer": optimizer, "lr_scheduler": {"scheduler": lr_scheduler, "interval": "step"}}
+
+    def _get_target_sparsity(self):
+        if self.global_step >= self.sparsity_warmup_updates:
+            return self.target_sparsity
+        return self.target_sparsity * (self.global_step / self.sparsity_warmup_updates)
+
+    def _step(self, batch, batch_idx, mode):
+        waveforms, lengths = batch
+        self.teacher_model.eval()
+        with torch.no_grad():
+            teacher_hiddens, teacher_lengths = self.teacher_model.extract_features(waveforms, lengths)
+            t_layers = [teacher_hiddens[idx] for idx in self.distill_layers]
+        student_hiddens, student_lengths = self.student_model.extract_features(waveforms, lengths)
+        if self.distill_mode == "layer2layer":
+            s_layers = [student_hiddens[idx] for idx in self.distill_layers]
+        elif self.distill_mode == "predlayer":
+            raise NotImplementedError("predlayer distill mode (Linear+GELU heads) is not on the HIP path yet")
+        else:
+            raise ValueError(f"Invalid distill mode: {self.distill_mode}")
+        B, T, Ds = s_layers[0].shape
+        cfg = dict(self.distill_loss.cfg(), L=len(s_layers), P=len(self._proj_uniq), B=B, T=T,
+                   proj_index=self._proj_index)
+        pw = []
+        for m in self._proj_uniq:
+            pw += [m.weight, m.bias]
+        loss_distill, loss_mse, loss_l1, loss_cos = ops.DistillProjLossFn.apply(
+            cfg, *[h.reshape(B * T, Ds) for h in s_layers], *pw,
+            *[h.reshape(B * T, -1) for h in t_layers])
+        if self.use_reg:
+            cur_target_sparsity = self._get_target_sparsity()
+            cur_expected_sparsity = 1. - self.student_model.get_num_params() / self.original_num_params
+            loss_reg = self.lambda1 * (cur_expected_sparsity - cur_target_sparsity) \
+                + self.lambda2 * (cur_expected_sparsity - cur_target_sparsity) ** 2
+        else:
+            loss_reg = 0
+        loss = loss_distill + loss_reg
+        self.log_dict({f"{mode}_loss": loss, f"{mode}_loss_distill": loss_distill, f"{mode}_loss_mse": loss_mse,
+                       f"{mode}_loss_l1": loss_l1, f"{mode}_loss_cos": loss_cos, f"{mode}_loss_reg": loss_reg})
+        if mode == "train" and self.use_reg:
+            self.log_dict({"sparsity_expected": cur_expected_sparsity, "sparsity_target": cur_target_sparsity,
+                           "lambda1": self.lambda1, "lambda2": self.lambda2})
+        return loss
+
+    def training_step(self, batch, batch_idx):
+        return self._step(batch, batch_idx, mode="train")
+
+    def validation_step(self, batch, batch_idx):
+        return self._step(batch, batch_idx, mode="valid")

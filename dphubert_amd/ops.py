@@ -1,0 +1,709 @@
+"""Autograd layer: one ``torch.autograd.Function`` per reference module.
+
+Each Function's forward/backward is a fixed schedule of HIP kernels from
+libdphubert_hip.so (through ``kernels``): no ATen math runs on the hot path,
+only allocation (caching allocator), views and a few O(channels) glue ops.
+The Functions are coarse (a whole EncoderLayer, the whole conv frontend, ...)
+so that cross-op fusion is possible (GEMM epilogues carry bias, GELU,
+HardConcrete masks, dropout, layer masks and residuals; LayerNorm backward
+emits the residual-branch gradient and its bias column sums in the same
+pass) and Python/autograd overhead stays at a few dozen nodes per step.
+
+Reference semantics followed (file:line of seas2nada/DPHuBERT):
+  FrontendFn           components.py:94-120, 158-185, 1071-1076
+  FeatureProjectionFn  components.py:263-274, 968-984
+  PosConvFn            components.py:319-333, 885-892
+  EncoderLayerFn       components.py:379-436, 726-748, 814-857
+  DistillProjLossFn    lightning.py:250-265, 116-139
+  HardConcreteFn       hardconcrete.py:85-99
+  ExpectedParamsFn     model.py:109-113 + get_num_params chain
+"""
+
+import math
+from typing import List, Optional, Sequence
+
+import torch
+
+from . import _lib
+from . import kernels as K
+from ._lib import call, ptr
+
+BF16 = torch.bfloat16
+F32 = torch.float32
+
+HC_BETA = 2.0 / 3.0
+HC_LIMIT_L = -0.1
+HC_LIMIT_R = 1.1
+HC_EPS = 1e-6
+HC_BIAS = -HC_BETA * math.log(-HC_LIMIT_L / HC_LIMIT_R)
+
+
+def _s():
+    return _lib.stream_ptr()
+
+
+# ---------------------------------------------------------------------------
+# counter-based seeds (dropout / HardConcrete noise)
+# ---------------------------------------------------------------------------
+class SeedSource:
+    """Per-process 64-bit seed stream; reseeded by ``torch.manual_seed``-style calls."""
+
+    def __init__(self, seed: int = 2022):
+        self.reset(seed)
+
+    def reset(self, seed: int):
+        self._state = (int(seed) * 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
+        self._n = 0
+
+    def next(self) -> int:
+        self._n += 1
+        z = (self._state + self._n * 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & 0xFFFFFFFFFFFFFFFF
+        return z ^ (z >> 31)
+
+
+SEEDS = SeedSource()
+
+
+def manual_seed(seed: int):
+    SEEDS.reset(seed)
+
+
+# ---------------------------------------------------------------------------
+# bf16 GEMM images of fp32 master weights (cached per parameter version)
+# ---------------------------------------------------------------------------
+def _version_key(ts):
+    return tuple((id(t), t._version) for t in ts)
+
+
+def bf16_image(*ts: torch.Tensor) -> torch.Tensor:
+    """Concatenate fp32 tensors (along dim 0) into one bf16 image.
+
+    The image is cached ON the first tensor object (attribute), keyed by the identity and
+    version counter of every source tensor, so an optimizer step (in-place update bumps
+    ``_version``) or a different parameter set always rebuilds it, and the cache dies with
+    the parameter.
+    """
+    owner = ts[0]
+    key = ("cat",) + _version_key(ts)
+    hit = getattr(owner, "_dph_img", None)
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    rows = sum(t.shape[0] for t in ts)
+    out = torch.empty((rows,) + tuple(ts[0].shape[1:]), dtype=BF16, device=ts[0].device)
+    off = 0
+    for t in ts:
+        n = t.numel()
+        call("dph_cast_bf16", ptr(t.detach()), out.data_ptr() + off * 2, n, _s())
+        off += n
+    owner._dph_img = (key, out)
+    return out
+
+
+def conv_image(w: torch.Tensor) -> torch.Tensor:
+    """conv weight [O][C][k] fp32 -> bf16 [O][k*C] (k-major, matches channels-last im2col rows)."""
+    key = ("conv",) + _version_key((w,))
+    hit = getattr(w, "_dph_img", None)
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    O, C, kk = w.shape
+    out = torch.empty(O, kk * C, dtype=BF16, device=w.device)
+    call("dph_conv_weight_pack", ptr(w.detach()), ptr(out), O, C, kk, _s())
+    w._dph_img = (key, out)
+    return out
+
+
+def _zeros(n, like_device, dtype=F32):
+    return torch.zeros(n, dtype=dtype, device=like_device)
+
+
+def _dev(t):
+    return t.device
+
+
+# ---------------------------------------------------------------------------
+# HardConcrete sampling (training mode)
+# ---------------------------------------------------------------------------
+class HardConcreteFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, log_alpha, u_in):
+        n = log_alpha.numel()
+        mask = torch.empty_like(log_alpha)
+        u = torch.empty_like(log_alpha) if u_in is None else u_in
+        call("dph_hc_sample_fwd", ptr(log_alpha), ptr(u_in), None if u_in is not None else ptr(u), ptr(mask), n,
+             SEEDS.next(), HC_BETA, HC_LIMIT_L, HC_LIMIT_R, HC_EPS, _s())
+        ctx.save_for_backward(log_alpha, u)
+        return mask
+
+    @staticmethod
+    def backward(ctx, dmask):
+        la, u = ctx.saved_tensors
+        dla = torch.zeros_like(la)
+        call("dph_hc_sample_bwd", ptr(la), ptr(u), ptr(dmask.contiguous()), ptr(dla), la.numel(), HC_BETA,
+             HC_LIMIT_L, HC_LIMIT_R, _s())
+        return dla, None
+
+
+# ---------------------------------------------------------------------------
+# Expected number of parameters (differentiable, from l0 norms)
+# ---------------------------------------------------------------------------
+class ExpectedParamsTable:
+    """Polynomial term table, built once per model config (see wav2vec2/model.py)."""
+
+    def __init__(self, terms, constant, sizes, device):
+        self.n_terms = len(terms)
+        self.constant = float(constant)
+        coef = [c for c, _ in terms] or [0.0]
+        idx = []
+        for _, ix in terms:
+            ix = list(ix) + [-1] * (3 - len(ix))
+            idx.extend(ix)
+        if not idx:
+            idx = [-1, -1, -1]
+        self.coef = torch.tensor(coef, dtype=torch.float64, device=device)
+        self.idx = torch.tensor(idx, dtype=torch.int32, device=device)
+        self.sizes_list = [int(s) for s in sizes]
+        self.sizes = torch.tensor(self.sizes_list or [0], dtype=torch.int64, device=device)
+        offs = [0]
+        for s in self.sizes_list:
+            offs.append(offs[-1] + s)
+        self.offsets = torch.tensor(offs[:-1] or [0], dtype=torch.int64, device=device)
+        self.total = offs[-1]
+        self._ptr_key = None
+        self._ptrs = None
+
+    def ptr_table(self, las):
+        key = tuple(t.data_ptr() for t in las)
+        if key != self._ptr_key:
+            self._ptrs = torch.tensor(list(key) or [0], dtype=torch.int64, device=las[0].device if las else "cuda")
+            self._ptr_key = key
+        return self._ptrs
+
+
+class ExpectedParamsFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, table: ExpectedParamsTable, *las):
+        dev = las[0].device if las else table.coef.device
+        l0 = torch.empty(max(len(las), 1), dtype=F32, device=dev)
+        out = torch.empty((), dtype=F32, device=dev)
+        pt = table.ptr_table(las) if las else None
+        call("dph_expected_params_fwd", ptr(pt), ptr(table.sizes), len(las), ptr(table.coef), ptr(table.idx),
+             table.n_terms, table.constant, HC_BIAS, ptr(l0), ptr(out), _s())
+        ctx.table = table
+        ctx.save_for_backward(l0, *las)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        l0, *las = ctx.saved_tensors
+        table = ctx.table
+        if not las:
+            return (None,)
+        g = torch.zeros(table.total, dtype=F32, device=l0.device)
+        call("dph_expected_params_bwd", ptr(table.ptr_table(las)), ptr(g), ptr(table.offsets), ptr(table.sizes),
+             len(las), ptr(table.coef), ptr(table.idx), table.n_terms, ptr(l0), ptr(dout.contiguous()), HC_BIAS, _s())
+        grads = []
+        for off, n, la in zip(table.offsets.tolist() if False else _offs(table), table.sizes_list, las):
+            grads.append(g[off: off + n].view_as(la))
+        return (None, *grads)
+
+
+def _offs(table):
+    out, o = [], 0
+    for s in table.sizes_list:
+        out.append(o)
+        o += s
+    return out
+
+
+# ---------------------------------------------------------------------------
+# Conv frontend (group_norm extractor)
+# ---------------------------------------------------------------------------
+class FrontendCfg:
+    def __init__(self, layers, B, S, need_grad):
+        self.layers = layers   # list of (out_c, k, s)
+        self.B = B
+        self.S = S
+        self.need_grad = need_grad
+
+
+def conv_lengths(S: int, layers) -> List[int]:
+    out = []
+    L = S
+    for (_, k, s) in layers:
+        L = max((L - k) // s + 1, 0)
+        out.append(L)
+    return out
+
+
+class FrontendFn(torch.autograd.Function):
+    """wave (B,S) fp32 -> channels-last features (B*T, C) bf16 (x dummy_weight).
+
+    inputs: wave, dummy_weight, gn_w, gn_b, then per layer i: conv weight, mask (or None).
+    """
+
+    @staticmethod
+    def forward(ctx, cfg: FrontendCfg, wave, dummy, gn_w, gn_b, *wm):
+        layers = cfg.layers
+        n = len(layers)
+        ws_ = list(wm[0::2])
+        masks = list(wm[1::2])
+        B, S = wave.shape
+        Ls = conv_lengths(S, layers)
+        dev = wave.device
+        need = cfg.need_grad
+        C0, k0, s0 = layers[0]
+        y = torch.empty(B * Ls[0], C0, dtype=BF16, device=dev)
+        mean = torch.empty(B, C0, dtype=F32, device=dev)
+        rstd = torch.empty(B, C0, dtype=F32, device=dev)
+        nch = -(-Ls[0] // 256)
+        ws = torch.empty(B * nch * C0 * 2, dtype=F32, device=dev)
+        call("dph_conv0_gn_fwd", ptr(wave), B, S, ptr(ws_[0]), C0, k0, s0, ptr(gn_w), ptr(gn_b), ptr(masks[0]),
+             ptr(y), ptr(mean), ptr(rstd), ptr(ws), ws.numel() * 4, _s())
+        ys, zs, imgs, cms = [y], [None], [None], [masks[0]]
+        Cin = C0
+        for i in range(1, n):
+            O, k, s = layers[i]
+            img = conv_image(ws_[i])
+            cm = masks[i]
+            if i == n - 1:
+                cm = dummy if cm is None else cm * dummy
+            out = torch.empty(B * Ls[i], O, dtype=BF16, device=dev)
+            z = torch.empty(B * Ls[i], O, dtype=BF16, device=dev) if need else None
+            A = K.mat(ys[-1], row_stride=s * Cin, rows_per_batch=Ls[i], batch_stride=Ls[i - 1] * Cin)
+            K.gemm(A, K.dense(img), K.dense(out), B * Ls[i], O, k * Cin, a_kcontig=True, b_kcontig=True,
+                   act=K.ACT_GELU, pre_out=z, colmask=cm)
+            ys.append(out)
+            zs.append(z)
+            imgs.append(img)
+            cms.append(cm)
+            Cin = O
+        if need:
+            ctx.cfg = cfg
+            ctx.Ls = Ls
+            ctx.cms = cms
+            ctx.has_mask = [m is not None for m in masks]
+            ctx.save_for_backward(wave, dummy, gn_w, gn_b, mean, rstd, *ws_, *[m if m is not None else dummy
+                                                                            for m in masks])
+            ctx.ys = ys[:-1]   # inputs of layers 1..n-1 (the last output is not needed)
+            ctx.zs = zs
+            ctx.imgs = imgs
+        return ys[-1]
+
+    @staticmethod
+    def backward(ctx, dy):
+        cfg = ctx.cfg
+        layers = cfg.layers
+        n = len(layers)
+        saved = ctx.saved_tensors
+        wave, dummy, gn_w, gn_b, mean, rstd = saved[:6]
+        ws_ = list(saved[6:6 + n])
+        masks = [m if h else None for m, h in zip(saved[6 + n:6 + 2 * n], ctx.has_mask)]
+        Ls = ctx.Ls
+        B, S = wave.shape
+        dev = wave.device
+        dy = dy.contiguous()
+        g_w = [None] * n
+        g_m = [None] * n
+        # last layer: GELU / (mask*dummy) backward
+        O = layers[-1][0]
+        dz = torch.empty_like(dy)
+        dm_raw = torch.zeros(O, dtype=F32, device=dev)
+        call("dph_gelu_mask_bwd", ptr(dy), ptr(ctx.zs[-1]), ptr(ctx.cms[-1]), ptr(dz), ptr(dm_raw), B * Ls[-1], O,
+             _s())
+        if masks[-1] is not None:
+            g_m[-1] = dm_raw * dummy
+        keep = []
+        for i in range(n - 1, 0, -1):
+            O, k, s = layers[i]
+            Cin = layers[i - 1][0]
+            M = B * Ls[i]
+            # weight gradient (packed [O][k*Cin]) -> [O][Cin][k]
+            dwp = torch.empty(O, k * Cin, dtype=F32, device=dev)
+            A = K.mat(dz, row_stride=O)
+            Bm = K.mat(ctx.ys[i - 1], row_stride=s * Cin, rows_per_batch=Ls[i], batch_stride=Ls[i - 1] * Cin)
+            splits = K.choose_splits(O, k * Cin, M)
+            keep.append(K.gemm(A, Bm, K.dense(dwp), O, k * Cin, M, a_kcontig=False, b_kcontig=False,
+                               c_dtype=K.OUT_F32, splits=splits, device=dev))
+            dw = torch.empty_like(ws_[i])
+            call("dph_conv_weight_unpack_grad", ptr(dwp), ptr(dw), O, Cin, k, 0, _s())
+            g_w[i] = dw
+            # input gradient columns, then col2im fused with the previous layer's GELU/mask backward
+            dcols = torch.empty(M, k * Cin, dtype=BF16, device=dev)
+            K.gemm(K.dense(dz), K.dense(ctx.imgs[i]), K.dense(dcols), M, k * Cin, O, a_kcontig=True,
+                   b_kcontig=False)
+            nxt = torch.empty(B * Ls[i - 1], Cin, dtype=BF16, device=dev)
+            if i > 1:
+                dmk = torch.zeros(Cin, dtype=F32, device=dev) if masks[i - 1] is not None else None
+                call("dph_col2im_gelu_bwd", ptr(dcols), B, Ls[i], Ls[i - 1], Cin, k, s, ptr(ctx.zs[i - 1]),
+                     ptr(masks[i - 1]), ptr(nxt), ptr(dmk) if dmk is not None else
+                     ptr(torch.zeros(Cin, dtype=F32, device=dev)), _s())
+                g_m[i - 1] = dmk
+            else:
+                call("dph_col2im_gelu_bwd", ptr(dcols), B, Ls[i], Ls[i - 1], Cin, k, s, None, None, ptr(nxt), None,
+                     _s())
+            dz = nxt
+        # layer 0: conv0 + GroupNorm + GELU + mask, recomputed from the waveform
+        C0, k0, s0 = layers[0]
+        dw0 = torch.zeros_like(ws_[0])
+        dgw = torch.zeros(C0, dtype=F32, device=dev)
+        dgb = torch.zeros(C0, dtype=F32, device=dev)
+        dm0 = torch.zeros(C0, dtype=F32, device=dev) if masks[0] is not None else None
+        wsb = torch.empty(B * C0 * 2, dtype=F32, device=dev)
+        call("dph_conv0_gn_bwd", ptr(wave), B, S, ptr(ws_[0]), C0, k0, s0, ptr(gn_w), ptr(gn_b), ptr(masks[0]),
+             ptr(mean), ptr(rstd), ptr(dz), ptr(dw0), ptr(dgw), ptr(dgb), ptr(dm0), ptr(wsb), wsb.numel() * 4, _s())
+        g_w[0] = dw0
+        g_m[0] = dm0
+        grads = [None, None, None, dgw, dgb]
+        for i in range(n):
+            grads += [g_w[i], g_m[i]]
+        return tuple(grads)
+
+
+# ---------------------------------------------------------------------------
+# Feature projection: LN(C) -> Linear(C->D) -> dropout -> zero padded frames
+# ---------------------------------------------------------------------------
+class FeatureProjectionFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, ln_w, ln_b, w, b, cfg):
+        M, C = x.shape
+        dev = x.device
+        xn = torch.empty_like(x)
+        mu = torch.empty(M, dtype=F32, device=dev)
+        rs = torch.empty(M, dtype=F32, device=dev)
+        call("dph_layernorm_fwd", ptr(x), None, ptr(ln_w), ptr(ln_b), ptr(xn), ptr(mu), ptr(rs), M, C, 1e-5, 0.0, 0,
+             _s())
+        img = bf16_image(w)
+        seed = SEEDS.next() if cfg["p"] > 0 else 0
+        out = K.linear_fwd(xn, img, b, dropout_p=cfg["p"], seed=seed, row_len=cfg["lengths"],
+                           len_rows=cfg["T"] if cfg["lengths"] is not None else 0)
+        ctx.cfg = cfg
+        ctx.seed = seed
+        ctx.save_for_backward(x, xn, mu, rs, ln_w, img)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, xn, mu, rs, ln_w, img = ctx.saved_tensors
+        cfg = ctx.cfg
+        M, C = x.shape
+        D = img.shape[0]
+        dev = x.device
+        dout = dout.contiguous()
+        dpre = torch.empty_like(dout)
+        db = torch.zeros(D, dtype=F32, device=dev)
+        lens = cfg["lengths"]
+        call("dph_branch_bwd", ptr(dout), ptr(dpre), M, D, cfg["p"], ctx.seed, None, ptr(lens),
+             cfg["T"] if lens is not None else 0, ptr(db), None, None, _s())
+        dw = torch.empty(D, C, dtype=F32, device=dev)
+        ws = K.linear_wgrad(dpre, xn, dw, accumulate=False)
+        dxn = K.linear_dgrad(dpre, img)
+        dx = torch.empty_like(x)
+        dlw = torch.zeros(C, dtype=F32, device=dev)
+        dlb = torch.zeros(C, dtype=F32, device=dev)
+        call("dph_layernorm_bwd", ptr(dxn), ptr(x), None, ptr(ln_w), ptr(mu), ptr(rs), ptr(dx), ptr(dlw), ptr(dlb), M,
+             C, 0.0, 0, None, 0.0, 0, None, None, None, None, _s())
+        del ws
+        return dx, dlw, dlb, dw, db, None
+
+
+# ---------------------------------------------------------------------------
+# Positional conv embedding + residual + LayerNorm + dropout (Transformer._preprocess)
+# ---------------------------------------------------------------------------
+class PosConvFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, wg, wv, bias, ln_w, ln_b, cfg):
+        B, T, G = cfg["B"], cfg["T"], cfg["G"]
+        M, D = x.shape
+        Kk = wv.shape[2]
+        Cg = D // G
+        dev = x.device
+        # weight norm -> bf16 GEMM images (forward and flipped/transposed for dgrad)
+        norm = torch.empty(Kk, dtype=F32, device=dev)
+        wk = torch.empty(G, Cg, Kk * Cg, dtype=BF16, device=dev)
+        wt = torch.empty(G, Cg, Kk * Cg, dtype=BF16, device=dev)
+        call("dph_weight_norm_fwd", ptr(wg), ptr(wv), D, Cg, Kk, G, None, ptr(norm), ptr(wk), ptr(wt), _s())
+        P = Kk // 2
+        Q = Kk - 1 - P
+        Tp = P + T + Q
+        xg = torch.empty(B * G * Tp * Cg, dtype=BF16, device=dev)
+        call("dph_regroup_pad", ptr(x), ptr(xg), B, T, G, Cg, P, Q, _s())
+        need = cfg["need_grad"]
+        s0 = torch.empty_like(x)
+        z = torch.empty_like(x) if need else None
+        Cm = K.mat(s0, D, z_div=G, z_outer=T * D, z_inner=Cg)
+        K.gemm(K.mat(xg, Cg, z_inner=Tp * Cg), K.mat(wk, Kk * Cg, z_div=G, z_outer=0, z_inner=Cg * Kk * Cg), Cm, T,
+               Cg, Kk * Cg, a_kcontig=True, b_kcontig=True, batch=B * G, act=K.ACT_GELU, bias=bias, vec_z_inner=Cg,
+               pre_out=z, residual=x)
+        h = torch.empty_like(x)
+        mu = torch.empty(M, dtype=F32, device=dev)
+        rs = torch.empty(M, dtype=F32, device=dev)
+        seed = SEEDS.next() if cfg["p"] > 0 else 0
+        call("dph_layernorm_fwd", ptr(s0), None, ptr(ln_w), ptr(ln_b), ptr(h), ptr(mu), ptr(rs), M, D, 1e-5,
+             cfg["p"], seed, _s())
+        if need:
+            ctx.cfg = cfg
+            ctx.seed = seed
+            ctx.save_for_backward(x, wg, wv, norm, wt, xg, s0, z, mu, rs, ln_w)
+        return h
+
+    @staticmethod
+    def backward(ctx, dh):
+        x, wg, wv, norm, wt, xg, s0, z, mu, rs, ln_w = ctx.saved_tensors
+        cfg = ctx.cfg
+        B, T, G = cfg["B"], cfg["T"], cfg["G"]
+        M, D = x.shape
+        Kk = wv.shape[2]
+        Cg = D // G
+        dev = x.device
+        dh = dh.contiguous()
+        ds0 = torch.empty_like(dh)
+        dlw = torch.zeros(D, dtype=F32, device=dev)
+        dlb = torch.zeros(D, dtype=F32, device=dev)
+        call("dph_layernorm_bwd", ptr(dh), ptr(s0), None, ptr(ln_w), ptr(mu), ptr(rs), ptr(ds0), ptr(dlw), ptr(dlb),
+             M, D, cfg["p"], ctx.seed, None, 0.0, 0, None, None, None, None, _s())
+        dz = torch.empty_like(ds0)
+        call("dph_gelu_mask_bwd", ptr(ds0), ptr(z), None, ptr(dz), None, M, D, _s())
+        db = torch.zeros(D, dtype=F32, device=dev)
+        call("dph_colsum", ptr(dz), ptr(db), M, D, _s())
+        # input gradient: transposed conv = same batched GEMM over a re-padded dz with flipped weights
+        P = Kk // 2
+        Q = Kk - 1 - P
+        P2, Q2 = Kk - 1 - P, Kk - 1 - Q
+        Tp2 = P2 + T + Q2
+        dzg = torch.empty(B * G * Tp2 * Cg, dtype=BF16, device=dev)
+        call("dph_regroup_pad", ptr(dz), ptr(dzg), B, T, G, Cg, P2, Q2, _s())
+        dx = torch.empty_like(x)
+        K.gemm(K.mat(dzg, Cg, z_inner=Tp2 * Cg), K.mat(wt, Kk * Cg, z_div=G, z_outer=0, z_inner=Cg * Kk * Cg),
+               K.mat(dx, D, z_div=G, z_outer=T * D, z_inner=Cg), T, Cg, Kk * Cg, a_kcontig=True, b_kcontig=True,
+               batch=B * G, residual=ds0)
+        # weight gradient in GEMM image layout [G][Cg_out][K*Cg_in]
+        Tp = P + T + Q
+        dimg = torch.empty(G, Cg, Kk * Cg, dtype=F32, device=dev)
+        A = K.mat(dz, D, z_inner=Cg)
+        Bm = K.mat(xg, Cg, rows_per_batch=T, batch_stride=G * Tp * Cg, z_inner=Tp * Cg)
+        splits = K.choose_splits(Cg, Kk * Cg, B * T, batch=G)
+        ws = K.gemm(A, Bm, K.mat(dimg, Kk * Cg, z_inner=Cg * Kk * Cg), Cg, Kk * Cg, B * T, a_kcontig=False,
+                    b_kcontig=False, c_dtype=K.OUT_F32, batch=G, splits=splits, device=dev)
+        dg = torch.empty_like(norm)
+        dv = torch.empty_like(wv)
+        call("dph_weight_norm_bwd", ptr(dimg), ptr(wg), ptr(wv), ptr(norm), D, Cg, Kk, G, ptr(dg), ptr(dv), _s())
+        del ws
+        return dx, dg.view_as(wg), dv, db, dlw, dlb, None
+
+
+# ---------------------------------------------------------------------------
+# Encoder layer (post-norm; HuBERT/wav2vec2 Base)
+# ---------------------------------------------------------------------------
+class EncoderLayerFn(torch.autograd.Function):
+    """h (B*T, D) bf16 -> layer output (B*T, D) bf16.
+
+    tensors: h, wq, wk, wv, bq, bk, bv, wo, bo, ln1_w, ln1_b, w1, b1, w2, b2, ln2_w, ln2_b,
+             head_mask, att_lmask, interm_mask, ff_lmask   (masks may be None; attention /
+             FFN weights may be None when the sub-layer is pruned away)
+    """
+
+    @staticmethod
+    def forward(ctx, cfg, h, wq, wk, wv, bq, bk, bv, wo, bo, ln1_w, ln1_b, w1, b1, w2, b2, ln2_w, ln2_b, hm, lma,
+                im, lmf):
+        M, D = h.shape
+        dev = h.device
+        need = cfg["need_grad"]
+        B, T, H = cfg["B"], cfg["T"], cfg["H"]
+        use_att = wq is not None
+        use_ff = w1 is not None
+        sv = {}
+        # ---------------- attention block ----------------
+        if use_att:
+            Dh = wq.shape[0]
+            Wqkv = bf16_image(wq, wk, wv)
+            bqkv = torch.cat([bq, bk, bv])
+            qkv = K.linear_fwd(h, Wqkv, bqkv)
+            o_u = torch.empty(M, Dh, dtype=BF16, device=dev)
+            o_m = torch.empty(M, Dh, dtype=BF16, device=dev)
+            lse = torch.empty(B * H * T, dtype=F32, device=dev)
+            seed_a = SEEDS.next() if cfg["p_attn"] > 0 else 0
+            call("dph_attention_fwd", ptr(qkv), ptr(o_u), ptr(o_m), ptr(lse), ptr(hm), ptr(cfg["lengths"]), B, T, H,
+                 cfg["head_dim"] ** -0.5, cfg["p_attn"], seed_a, _s())
+            Wo = bf16_image(wo)
+            seed_d = SEEDS.next() if cfg["p_drop"] > 0 else 0
+            a_pre = torch.empty(M, D, dtype=BF16, device=dev) if (need and lma is not None) else None
+            s1 = K.linear_fwd(o_m, Wo, bo, smask=lma, residual=h, dropout_p=cfg["p_drop"], seed=seed_d,
+                              pre_out=a_pre)
+            sv.update(Wqkv=Wqkv, qkv=qkv, o_u=o_u, o_m=o_m, lse=lse, Wo=Wo, a_pre=a_pre, seed_a=seed_a, seed_d=seed_d)
+        else:
+            s1 = h
+        h1 = torch.empty_like(h)
+        mu1 = torch.empty(M, dtype=F32, device=dev)
+        rs1 = torch.empty(M, dtype=F32, device=dev)
+        call("dph_layernorm_fwd", ptr(s1), None, ptr(ln1_w), ptr(ln1_b), ptr(h1), ptr(mu1), ptr(rs1), M, D, 1e-5, 0.0,
+             0, _s())
+        # ---------------- feed-forward block ----------------
+        if use_ff:
+            F_ = w1.shape[0]
+            W1 = bf16_image(w1)
+            W2 = bf16_image(w2)
+            seed_i = SEEDS.next() if cfg["p_interm"] > 0 else 0
+            u = torch.empty(M, F_, dtype=BF16, device=dev) if need else None
+            f = K.linear_fwd(h1, W1, b1, act=K.ACT_GELU, pre_out=u, colmask=im, dropout_p=cfg["p_interm"],
+                             seed=seed_i)
+            seed_o = SEEDS.next() if cfg["p_drop"] > 0 else 0
+            y_pre = torch.empty(M, D, dtype=BF16, device=dev) if (need and lmf is not None) else None
+            s2 = K.linear_fwd(f, W2, b2, smask=lmf, residual=h1, dropout_p=cfg["p_drop"], seed=seed_o, pre_out=y_pre)
+            sv.update(W1=W1, W2=W2, u=u, f=f, y_pre=y_pre, seed_i=seed_i, seed_o=seed_o)
+        else:
+            s2 = h1
+        out = torch.empty_like(h)
+        mu2 = torch.empty(M, dtype=F32, device=dev)
+        rs2 = torch.empty(M, dtype=F32, device=dev)
+        call("dph_layernorm_fwd", ptr(s2), None, ptr(ln2_w), ptr(ln2_b), ptr(out), ptr(mu2), ptr(rs2), M, D, 1e-5,
+             0.0, 0, _s())
+        if need:
+            ctx.cfg = cfg
+            ctx.sv = sv
+            ctx.flags = (use_att, use_ff, hm is not None, lma is not None, im is not None, lmf is not None)
+            ctx.save_for_backward(h, s1, mu1, rs1, h1, s2, mu2, rs2, ln1_w, ln2_w, hm, lma, im, lmf)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        h, s1, mu1, rs1, h1, s2, mu2, rs2, ln1_w, ln2_w, hm, lma, im, lmf = ctx.saved_tensors
+        cfg = ctx.cfg
+        sv = ctx.sv
+        use_att, use_ff, has_hm, has_lma, has_im, has_lmf = ctx.flags
+        B, T, H = cfg["B"], cfg["T"], cfg["H"]
+        M, D = h.shape
+        dev = h.device
+        dout = dout.contiguous()
+        z = lambda n: torch.zeros(n, dtype=F32, device=dev)  # noqa: E731
+        g = {}
+        # ---- LN2 backward (+ FFN branch gradient) ----
+        ds2 = torch.empty_like(dout)
+        g["ln2_w"], g["ln2_b"] = z(D), z(D)
+        if use_ff:
+            dy = torch.empty_like(dout)
+            g["b2"] = z(D)
+            g["lmf"] = z(1) if has_lmf else None
+            call("dph_layernorm_bwd", ptr(dout), ptr(s2), None, ptr(ln2_w), ptr(mu2), ptr(rs2), ptr(ds2),
+                 ptr(g["ln2_w"]), ptr(g["ln2_b"]), M, D, 0.0, 0, ptr(dy), cfg["p_drop"], sv["seed_o"], ptr(lmf),
+                 ptr(g["b2"]), ptr(sv["y_pre"]), ptr(g["lmf"]), _s())
+            F_ = sv["W1"].shape[0]
+            g["w2"] = torch.empty(D, F_, dtype=F32, device=dev)
+            k1 = K.linear_wgrad(dy, sv["f"], g["w2"], accumulate=False)
+            g["b1"] = z(F_)
+            g["im"] = z(F_) if has_im else None
+            du = K.linear_dgrad(dy, sv["W2"], act=K.ACT_GELU_BWD, aux_in=sv["u"], colmask=im, colsum_out=g["b1"],
+                                colsum_aux=g["im"] if has_im else z(F_), dropout_p=cfg["p_interm"],
+                                seed=sv["seed_i"])
+            g["w1"] = torch.empty(F_, D, dtype=F32, device=dev)
+            k2 = K.linear_wgrad(du, h1, g["w1"], accumulate=False)
+            dh1 = K.linear_dgrad(du, sv["W1"], residual=ds2)
+            del k1, k2
+        else:
+            call("dph_layernorm_bwd", ptr(dout), ptr(s2), None, ptr(ln2_w), ptr(mu2), ptr(rs2), ptr(ds2),
+                 ptr(g["ln2_w"]), ptr(g["ln2_b"]), M, D, 0.0, 0, None, 0.0, 0, None, None, None, None, _s())
+            dh1 = ds2
+        # ---- LN1 backward (+ attention branch gradient) ----
+        ds1 = torch.empty_like(dout)
+        g["ln1_w"], g["ln1_b"] = z(D), z(D)
+        if use_att:
+            da = torch.empty_like(dout)
+            g["bo"] = z(D)
+            g["lma"] = z(1) if has_lma else None
+            call("dph_layernorm_bwd", ptr(dh1), ptr(s1), None, ptr(ln1_w), ptr(mu1), ptr(rs1), ptr(ds1),
+                 ptr(g["ln1_w"]), ptr(g["ln1_b"]), M, D, 0.0, 0, ptr(da), cfg["p_drop"], sv["seed_d"], ptr(lma),
+                 ptr(g["bo"]), ptr(sv["a_pre"]), ptr(g["lma"]), _s())
+            Dh = sv["Wo"].shape[1]
+            g["wo"] = torch.empty(D, Dh, dtype=F32, device=dev)
+            k3 = K.linear_wgrad(da, sv["o_m"], g["wo"], accumulate=False)
+            do_m = K.linear_dgrad(da, sv["Wo"])
+            Dvec = torch.empty(B * H * T, dtype=F32, device=dev)
+            g["hm"] = z(H) if has_hm else None
+            call("dph_attention_bwd_prep", ptr(do_m), ptr(sv["o_u"]), ptr(hm), ptr(Dvec), ptr(g["hm"]), B, T, H, _s())
+            dqkv = torch.empty_like(sv["qkv"])
+            call("dph_attention_bwd", ptr(sv["qkv"]), ptr(do_m), ptr(hm), ptr(sv["lse"]), ptr(Dvec), ptr(dqkv),
+                 ptr(cfg["lengths"]), B, T, H, cfg["head_dim"] ** -0.5, cfg["p_attn"], sv["seed_a"], _s())
+            dbqkv = z(3 * Dh)
+            call("dph_colsum", ptr(dqkv), ptr(dbqkv), M, 3 * Dh, _s())
+            dWqkv = torch.empty(3 * Dh, D, dtype=F32, device=dev)
+            k4 = K.linear_wgrad(dqkv, h, dWqkv, accumulate=False)
+            dh = K.linear_dgrad(dqkv, sv["Wqkv"], residual=ds1)
+            g["wq"], g["wk"], g["wv"] = dWqkv[:Dh], dWqkv[Dh:2 * Dh], dWqkv[2 * Dh:]
+            g["bq"], g["bk"], g["bv"] = dbqkv[:Dh], dbqkv[Dh:2 * Dh], dbqkv[2 * Dh:]
+            del k3, k4
+        else:
+            call("dph_layernorm_bwd", ptr(dh1), ptr(s1), None, ptr(ln1_w), ptr(mu1), ptr(rs1), ptr(ds1),
+                 ptr(g["ln1_w"]), ptr(g["ln1_b"]), M, D, 0.0, 0, None, 0.0, 0, None, None, None, None, _s())
+            dh = ds1
+        order = ["wq", "wk", "wv", "bq", "bk", "bv", "wo", "bo", "ln1_w", "ln1_b", "w1", "b1", "w2", "b2", "ln2_w",
+                 "ln2_b", "hm", "lma", "im", "lmf"]
+        return (None, dh) + tuple(g.get(k) for k in order)
+
+
+# ---------------------------------------------------------------------------
+# Distill projections + DistillLoss (fused)
+# ---------------------------------------------------------------------------
+class DistillProjLossFn(torch.autograd.Function):
+    """student hidden list -> per-layer Linear (shared per group) -> loss terms.
+
+    args: cfg, then L student hiddens (B*T, Ds) bf16, then P projection (weight, bias) pairs,
+    then L teacher hiddens (B*T, Dt) bf16.  Returns (loss, mse, l1, cos) 0-d fp32.
+    """
+
+    @staticmethod
+    def forward(ctx, cfg, *args):
+        L, P = cfg["L"], cfg["P"]
+        sh = args[:L]
+        pw = args[L:L + 2 * P]
+        th = args[L + 2 * P:L + 2 * P + L]
+        B, T = cfg["B"], cfg["T"]
+        M, Ds = sh[0].shape
+        Dt = pw[0].shape[0]
+        dev = sh[0].device
+        s = torch.empty(L, M, Dt, dtype=F32, device=dev)
+        imgs = [bf16_image(pw[2 * p]) for p in range(P)]
+        for l in range(L):
+            p = cfg["proj_index"][l]
+            K.linear_fwd(sh[l], imgs[p], pw[2 * p + 1], out=s[l])
+        rowstats = torch.empty(L * M * 3, dtype=F32, device=dev)
+        partial = torch.empty(3, dtype=F32, device=dev)
+        out = torch.empty(4, dtype=F32, device=dev)
+        tptrs = (_lib.C.c_void_p * L)(*[t.data_ptr() for t in th])
+        call("dph_distill_loss_fwd", ptr(s), tptrs, B, L, T, Dt, cfg["l2"], cfg["l1"], cfg["cos"],
+             int(cfg["cos_type"] == "log_sig"), ptr(rowstats), ptr(partial), ptr(out), _s())
+        ctx.cfg = cfg
+        ctx.save_for_backward(s, rowstats, *sh, *imgs, *th)
+        return out[0], out[1], out[2], out[3]
+
+    @staticmethod
+    def backward(ctx, dloss, dmse, dl1, dcos):
+        cfg = ctx.cfg
+        L, P = cfg["L"], cfg["P"]
+        s, rowstats, *rest = ctx.saved_tensors
+        sh = rest[:L]
+        imgs = rest[L:L + P]
+        th = rest[L + P:]
+        B, T = cfg["B"], cfg["T"]
+        M, Ds = sh[0].shape
+        Dt = s.shape[2]
+        dev = s.device
+        ds = torch.empty(L, M, Dt, dtype=BF16, device=dev)
+        tptrs = (_lib.C.c_void_p * L)(*[t.data_ptr() for t in th])
+        dl = dloss.contiguous() if dloss is not None else torch.ones((), dtype=F32, device=dev)
+        call("dph_distill_loss_bwd", ptr(s), tptrs, ptr(rowstats), ptr(dl), B, L, T, Dt, cfg["l2"], cfg["l1"],
+             cfg["cos"], int(cfg["cos_type"] == "log_sig"), ptr(ds), _s())
+        dW = [torch.zeros(Dt, Ds, dtype=F32, device=dev) for _ in range(P)]
+        db = [torch.zeros(Dt, dtype=F32, device=dev) for _ in range(P)]
+        dh = []
+        keep = []
+        for l in range(L):
+            p = cfg["proj_index"][l]
+            keep.append(K.linear_wgrad(ds[l], sh[l], dW[p], accumulate=True))
+            call("dph_colsum", ptr(ds[l]), ptr(db[p]), M, Dt, _s())
+            dh.append(K.linear_dgrad(ds[l], imgs[p]))
+        grads = [None] + dh
+        for p in range(P):
+            grads += [dW[p], db[p]]
+        grads += [None] * L
+        return tuple(grads)

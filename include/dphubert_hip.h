@@ -181,13 +181,21 @@ int dph_conv_weight_pack(const float* w, void* dst, int64_t O, int64_t C, int64_
 /* grad of packed conv weight: fp32 [O][k*C] -> [O][C][k] (accumulate if accum) */
 int dph_conv_weight_unpack_grad(const float* g, float* dst, int64_t O, int64_t C, int64_t k, int accum,
                                 hipStream_t stream);
+/* residual-branch gradient: out = dy*drop(p,seed)*(*smask), padded rows zeroed
+ * ((m % len_rows) >= row_len[m/len_rows]); colsum += out; sdot += sum(dy*drop*pre).
+ * Backward of components.py:273,845 (dropout), :432-434,:744-746 (layer masks), :980 (pad zeroing). */
+int dph_branch_bwd(const void* dy, void* out, int64_t rows, int64_t cols, float p, uint64_t seed, const float* smask,
+                   const int64_t* row_len, int64_t len_rows, float* colsum, const void* pre, float* sdot,
+                   hipStream_t stream);
 /* bf16 -> f32 copy / accumulate helpers */
 int dph_add_bf16(const void* a, const void* b, void* out, int64_t n, hipStream_t stream);
 
 /* ------------------------------------------------------------------------ *
- * Distillation loss (lightning.py:116-139) over student s (fp32) and teacher
- * layers t_l (bf16), both (B, L, T, D) with the teacher given as L pointers
- * to [B][T][D] hidden states.
+ * Distillation loss (lightning.py:116-139) over student s (fp32, layer-major
+ * [L][B][T][D]: each distill layer's projection is one dense GEMM output) and
+ * teacher layers t_l (bf16), given as L pointers to [B][T][D] hidden states.
+ * The loss is a mean over all (l,b,t) rows, so the layer-major order is
+ * equivalent to the reference's torch.stack(dim=1) (B,L,T,D).
  * out[0..3] = loss, mse, l1, cos.  rowstats [B*L*T][3] saved for backward.
  * ------------------------------------------------------------------------ */
 #define DPH_MAX_DISTILL_LAYERS 16
@@ -218,9 +226,10 @@ int dph_hc_sample_bwd(const float* log_alpha, const float* u, const float* dmask
 int dph_expected_params_fwd(const float* const* la_ptrs, const int64_t* la_sizes, int64_t n_groups,
                             const double* coef, const int32_t* idx, int64_t n_terms, double constant, float hc_bias,
                             float* l0, float* out, hipStream_t stream);
-int dph_expected_params_bwd(const float* const* la_ptrs, float* const* grad_ptrs, const int64_t* la_sizes,
-                            int64_t n_groups, const double* coef, const int32_t* idx, int64_t n_terms,
-                            const float* l0, const float* dout, float hc_bias, hipStream_t stream);
+/* grad_flat[grad_offsets[g] + i] += dout * dE/dl0[g] * sigmoid'(la_g[i] + bias) */
+int dph_expected_params_bwd(const float* const* la_ptrs, float* grad_flat, const int64_t* grad_offsets,
+                            const int64_t* la_sizes, int64_t n_groups, const double* coef, const int32_t* idx,
+                            int64_t n_terms, const float* l0, const float* dout, float hc_bias, hipStream_t stream);
 
 /* ------------------------------------------------------------------------ *
  * Optimiser: multi-tensor AdamW (torch.optim.AdamW semantics,
