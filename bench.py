@@ -1,0 +1,177 @@
+"""DPHuBERT distill-step benchmark on MI355X (see BASELINE.json / SURVEY.md 8(d)).
+
+One step = the reference's distill.py training step (lightning.py:245-296 + the
+Lightning loop): frozen teacher forward (eval), student forward in training mode
+(dropout, HardConcrete conv/head/interm masks sampled), per-group projections,
+L1 + cosine distillation loss, Lagrangian expected-sparsity regulariser,
+backward, RCCL gradient all-reduce (N > 1), grad-norm clip (10) and AdamW,
+on synthetic 10 s / 16 kHz waveforms, B utterances per GPU (default 16 =
+run.sh's 160 s per GPU), HuBERT-Base teacher+student with seeded weights.
+
+Prints ONE JSON line on rank 0.  Launch N > 1 with
+  python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \\
+      --master-port P bench.py --gpus N
+"""
+
+import argparse
+import copy
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+FLOP_PER_UTT_BASE = 599.6e9      # teacher fwd + 3 x (student fwd + projections), 10 s utterance
+MFMA_PEAK_TFLOPS = 2500.0        # MI355X dense bf16 (MI355X_MICROARCH.md)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(batch: int = 1, steps: int = 2, seconds: float = 10.0):
+    """Time the fp32 CPU oracle (oracle/hubert_ref.py) on a bounded sample of the same step."""
+    from dphubert_amd.synthetic import HUBERT_BASE_CONFIG, seeded_state_dict, synthetic_batch
+    from oracle import hubert_ref as ref
+    threads = min(os.cpu_count() or 1, 16)
+    torch.set_num_threads(threads)
+    cfg = copy.deepcopy(HUBERT_BASE_CONFIG)
+    scfg = dict(cfg, extractor_prune_conv_channels=True, encoder_prune_attention_heads=True,
+                encoder_prune_feed_forward_intermediate=True)
+    tsd = seeded_state_dict(ref.state_dict_shapes(cfg), 0)
+    ssd = seeded_state_dict(ref.state_dict_shapes(scfg), 0)
+    psd = {"0.weight": torch.eye(768), "0.bias": torch.zeros(768), "1.weight": torch.eye(768),
+           "1.bias": torch.zeros(768)}
+    wave, lengths = synthetic_batch(batch, int(seconds * 16000))
+    g = torch.Generator().manual_seed(0)
+    u = {n[:-len(".log_alpha")]: torch.rand(v.shape, generator=g) * 0.98 + 0.01 for n, v in ssd.items()
+         if n.endswith(".log_alpha")}
+    kw = dict(teacher_sd=tsd, teacher_cfg=cfg, student_sd=ssd, student_cfg=scfg, proj_sd=psd,
+              distill_layers=[0, 4, 8, 12], proj_index=[0, 1, 1, 1], wave=wave, lengths=lengths, u=u,
+              lambdas=(0.0, 0.0), global_step=5000, original_num_params=94371456)
+    ref.distill_step(**kw)                      # warm-up
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ref.distill_step(**kw)
+    dt = time.perf_counter() - t0
+    return {"value": round(batch * seconds * steps / dt, 3), "unit": "audio-seconds/sec", "cores": threads,
+            "kind": "port",
+            "sample": f"oracle/hubert_ref.py distill_step (teacher fwd + student fwd/bwd + loss + reg, fp32, no "
+                      f"optimizer), HuBERT-Base 12 layers, B={batch} x {seconds:.0f} s, {steps} timed steps after 1 "
+                      f"warm-up, torch CPU {threads} threads"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=16, help="utterances per GPU (run.sh: 160 s per GPU)")
+    ap.add_argument("--seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-roofline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    from dphubert_amd import ops
+    from dphubert_amd.kernels import LaunchProfiler
+    from dphubert_amd.synthetic import HUBERT_BASE_CONFIG, synthetic_batch
+    from dphubert_amd.trainer import Trainer, build_distill_module
+
+    ops.manual_seed(2022 + rank)
+    module = build_distill_module(HUBERT_BASE_CONFIG, pruning_units="conv,head,interm", distill_layers="0.4,8,12",
+                                  use_reg=True)
+    module.global_step = 5000            # target sparsity reached (0.75)
+    module = module.to(dev)
+    trainer = Trainer(module, clip_norm=10.0)
+    samples = int(args.seconds * 16000)
+    wave, lengths = synthetic_batch(args.batch, samples, seed=2022 + rank)
+    batch = (wave.to(dev), lengths.to(dev))
+
+    for i in range(args.warmup):
+        loss = trainer.step(batch)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = trainer.step(batch)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = t.item()
+    ms = dt / args.steps * 1e3
+    audio_s = world * args.batch * args.seconds * args.steps
+    value = audio_s / dt
+    log(f"loss {loss.item():.5f}  step {ms:.2f} ms  {value:.1f} audio-s/s  "
+        f"({FLOP_PER_UTT_BASE * args.batch * args.seconds / 10 / (ms / 1e3) / 1e12:.0f} TFLOP/s algorithmic/GPU)")
+
+    out = {
+        "metric": "audio-seconds/sec/node (HuBERT-Base distill step, 10s utts)",
+        "value": round(value, 2),
+        "unit": "audio-seconds/sec",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic (0.1*randn 16 kHz waveforms, seeded random-init HuBERT-Base weights)",
+        "config": {"workload": "distill.py step: HuBERT-Base teacher (eval) + student (train, HardConcrete "
+                               "conv,head,interm, dropout) + L1/cos distill loss + sparsity Lagrangian + AdamW",
+                   "utterances_per_gpu": args.batch, "seconds_per_utt": args.seconds,
+                   "global_batch_audio_s": world * args.batch * args.seconds, "distill_layers": "0.4,8,12",
+                   "parallelism": f"dp{world}"},
+    }
+    if rank == 0 and not args.no_roofline:
+        with LaunchProfiler() as prof:
+            trainer.step(batch)
+        summ = prof.summary()
+        top = max(summ.items(), key=lambda kv: kv[1]["ms"])
+        name, d = top
+        avg_ms = d["ms"] / d["launches"]
+        flops_per_launch = d["flops"] / d["launches"]
+        achieved = flops_per_launch / (avg_ms / 1e3) / 1e12
+        all_ms = sum(v["ms"] for v in summ.values())
+        all_fl = sum(v["flops"] for v in summ.values())
+        out["roofline"] = {"bound": "mfma", "kernel": name, "achieved": round(achieved, 1),
+                           "peak": MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / MFMA_PEAK_TFLOPS, 4),
+                           "traffic": None, "launches_per_step": d["launches"],
+                           "avg_launch_us": round(avg_ms * 1e3, 2), "flop_per_launch": flops_per_launch,
+                           "all_gemm_tflops": round(all_fl / (all_ms / 1e3) / 1e12, 1),
+                           "gemm_ms_per_step": round(all_ms, 3)}
+        log(json.dumps({k: v for k, v in summ.items()}))
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            out["cpu_baseline"] = cpu_baseline()
+        except Exception as e:  # noqa: BLE001 -- baseline is informational
+            out["cpu_baseline"] = {"value": None, "error": repr(e)}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,122 @@
+"""Data-parallel gradient reduction over RCCL (xGMI), overlapped with backward.
+
+Replaces PyTorch-Lightning ``strategy="ddp"`` (distill.py:41 -> torch DDP over
+NCCL).  Design for one 8x MI355X node:
+
+* gradients of the trainable parameters (student + HardConcrete log_alpha +
+  distill projections + Lagrange multipliers, ~95.6 M fp32 = 382 MB for
+  HuBERT-Base) live in a few large flat buckets; each ``p.grad`` is a view
+  into its bucket, so the all-reduce needs no pack/unpack copies;
+* buckets are filled in reverse registration order (= backward order), and a
+  bucket's ``all_reduce`` is launched asynchronously from the
+  post-accumulate-grad hook of its last parameter, so RCCL traffic over the
+  point-to-point xGMI links overlaps the remaining backward kernels;
+* bucket size defaults to 64 MB: the ring all-reduce on xGMI is per-link
+  bound, so few large collectives beat DDP's 25 MB default;
+* the average is applied in the collective (``ReduceOp.AVG``) on RCCL, or by
+  a scale after SUM on gloo (CPU tests).
+"""
+
+from typing import Iterable, List, Optional
+
+import torch
+import torch.distributed as dist
+
+
+class GradReducer:
+    def __init__(self, params: Iterable[torch.nn.Parameter], bucket_mb: float = 64.0, process_group=None):
+        self.group = process_group
+        self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
+        ps: List[torch.nn.Parameter] = []
+        seen = set()
+        for p in params:
+            if p.requires_grad and id(p) not in seen:
+                seen.add(id(p))
+                ps.append(p)
+        ps = list(reversed(ps))        # backward produces gradients roughly in reverse order
+        self.params = ps
+        cap = int(bucket_mb * 1024 * 1024 / 4)
+        self.buckets: List[List[torch.nn.Parameter]] = []
+        cur, n = [], 0
+        for p in ps:
+            if cur and n + p.numel() > cap:
+                self.buckets.append(cur)
+                cur, n = [], 0
+            cur.append(p)
+            n += p.numel()
+        if cur:
+            self.buckets.append(cur)
+        self.flat = []
+        self.bucket_of = {}
+        for bi, b in enumerate(self.buckets):
+            dev = b[0].device
+            dt = b[0].dtype
+            self.flat.append(torch.zeros(sum(p.numel() for p in b), dtype=dt, device=dev))
+            for p in b:
+                self.bucket_of[id(p)] = bi
+        self.views = {}
+        for bi, b in enumerate(self.buckets):
+            off = 0
+            for p in b:
+                self.views[id(p)] = self.flat[bi][off:off + p.numel()].view_as(p)
+                off += p.numel()
+        self._pending = [0] * len(self.buckets)
+        self._handles = [None] * len(self.buckets)
+        self._hooks = [p.register_post_accumulate_grad_hook(self._hook) for p in ps]
+        self.backend = dist.get_backend(process_group) if dist.is_initialized() else None
+        self.enabled = self.world > 1
+
+    def prepare(self, zero: bool = True, sync: bool = True):
+        """Point every .grad at its bucket view (zeroed when ``zero``) before a backward.
+
+        ``sync=False`` for the non-final micro-batches of gradient accumulation: gradients
+        accumulate locally and no collective is launched until the final micro-batch.
+        """
+        if zero:
+            for f in self.flat:
+                f.zero_()
+        for p in self.params:
+            p.grad = self.views[id(p)]
+        self.sync = sync
+        self._pending = [len(b) for b in self.buckets]
+        self._handles = [None] * len(self.buckets)
+
+    def _hook(self, p):
+        bi = self.bucket_of[id(p)]
+        if not getattr(self, "sync", True):
+            if p.grad.data_ptr() != self.views[id(p)].data_ptr():
+                self.views[id(p)].copy_(p.grad)
+                p.grad = self.views[id(p)]
+            return
+        if p.grad is not self.views[id(p)] and p.grad.data_ptr() != self.views[id(p)].data_ptr():
+            # autograd replaced the grad tensor (e.g. prepare() not called): copy into the bucket
+            self.views[id(p)].copy_(p.grad)
+            p.grad = self.views[id(p)]
+        self._pending[bi] -= 1
+        if self._pending[bi] == 0 and self.enabled:
+            self._launch(bi)
+
+    def _launch(self, bi):
+        f = self.flat[bi]
+        if self.backend == "nccl":
+            self._handles[bi] = dist.all_reduce(f, op=dist.ReduceOp.AVG, group=self.group, async_op=True)
+        else:
+            self._handles[bi] = dist.all_reduce(f, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+
+    def finish(self):
+        """Wait for every bucket (launch the ones whose params got no gradient) and average."""
+        if not self.enabled:
+            return
+        for bi in range(len(self.buckets)):
+            if self._handles[bi] is None:
+                self._launch(bi)
+        for bi, h in enumerate(self._handles):
+            h.wait()
+            if self.backend != "nccl":
+                self.flat[bi].div_(self.world)
+        for p in self.params:
+            p.grad = self.views[id(p)]
+
+    def remove(self):
+        for h in self._hooks:
+            h.remove()

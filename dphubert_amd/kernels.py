@@ -45,6 +45,38 @@ def dense(t: torch.Tensor, offset: int = 0, row_stride: Optional[int] = None) ->
     return mat(t, t.shape[-1] if row_stride is None else row_stride, offset=offset)
 
 
+class LaunchProfiler:
+    """Brackets every GEMM launch with HIP events on the launch stream (used by bench.py to
+    measure per-kernel average durations live; off by default)."""
+
+    active = None
+
+    def __init__(self):
+        self.records = []
+
+    def __enter__(self):
+        LaunchProfiler.active = self
+        return self
+
+    def __exit__(self, *exc):
+        LaunchProfiler.active = None
+
+    def summary(self):
+        torch.cuda.synchronize()
+        out = {}
+        for name, flops, e0, e1 in self.records:
+            ms = e0.elapsed_time(e1)
+            d = out.setdefault(name, {"launches": 0, "ms": 0.0, "flops": 0.0})
+            d["launches"] += 1
+            d["ms"] += ms
+            d["flops"] += flops
+        return out
+
+
+def _variant(a_kcontig, b_kcontig):
+    return f"gemm_kernel<{str(bool(a_kcontig)).lower()}, {str(bool(b_kcontig)).lower()}>"
+
+
 def gemm(A: DphMat, B: DphMat, Cm: DphMat, M: int, N: int, K: int, *, a_kcontig: bool, b_kcontig: bool,
          c_dtype: int = OUT_BF16, act: int = ACT_NONE, alpha: float = 1.0, batch: int = 1, splits: int = 1,
          bias=None, colmask=None, smask=None, vec_z_inner: int = 0, pre_out=None, aux_in=None, residual=None,
@@ -59,7 +91,15 @@ def gemm(A: DphMat, B: DphMat, Cm: DphMat, M: int, N: int, K: int, *, a_kcontig:
                        dropout_p, seed & 0xFFFFFFFFFFFFFFFF, ptr(bias), ptr(colmask), ptr(smask), vec_z_inner,
                        ptr(pre_out), ptr(aux_in), ptr(residual), ptr(colsum_out), ptr(colsum_aux), ptr(row_len),
                        len_rows, drop_row_offset, ptr(ws), ws_bytes)
+    prof = LaunchProfiler.active
+    if prof is not None:
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
     call("dph_gemm", C.byref(args), _stream())
+    if prof is not None:
+        e1.record()
+        prof.records.append((_variant(a_kcontig, b_kcontig), 2.0 * M * N * K * batch, e0, e1))
     return ws  # keep alive until the stream consumes it (caching allocator is stream-ordered)
 
 
