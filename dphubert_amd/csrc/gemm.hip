@@ -33,7 +33,10 @@ namespace {
 constexpr int BM = 128;
 constexpr int BN = 128;
 constexpr int BK = 64;
-constexpr int NTHREADS = 256;
+constexpr int NTHREADS = 256;                 // 4 waves: 2 (M) x 2 (N), each a 64x64 output tile
+constexpr int CHUNKS = (128 * BK / 8) / NTHREADS;   // 16-B chunks per thread per operand tile
+constexpr int WTN = 64;                       // wave tile width (N)
+constexpr int NJ = WTN / 16;                  // accumulator tiles per wave along N
 constexpr int KROW = BK + 8;                  // k-contig LDS row (elements)
 constexpr int LDS_KC = 128 * KROW * 2;        // bytes, k-contig tile
 constexpr int LDS_MN = BK * 128 * 2;          // bytes, mn-contig tile
@@ -59,8 +62,8 @@ __device__ __forceinline__ int swz(int k) { return (k & 3) | (((k >> 3) & 1) << 
 template <bool KC>
 struct Stager {
   const bf16_t* base;   // operand base incl. batch offset
-  int64_t roff[4];      // k-contig: per-chunk row offsets (fixed per block)
-  bool rvalid[4];
+  int64_t roff[CHUNKS];  // k-contig: per-chunk row offsets (fixed per block)
+  bool rvalid[CHUNKS];
   int64_t r0;           // first row/col of the tile (M or N index)
   int64_t R;            // rows (M or N)
   DphMat d;
@@ -72,46 +75,49 @@ struct Stager {
     R = Rn;
     if constexpr (KC) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < CHUNKS; ++i) {
         int c = tid + NTHREADS * i;
         int64_t r = tile0 + (c >> 3);
         rvalid[i] = r < Rn;
-        roff[i] = rvalid[i] ? row_addr(dm, r) : 0;
+        roff[i] = row_addr(dm, rvalid[i] ? r : Rn - 1);
       }
     }
   }
 
-  __device__ void load(uint4 (&reg)[4], int64_t k0, int64_t kend, int tid) const {
+  // Loads are unconditional (addresses clamped into the operand) so hipcc can keep several
+  // tiles in flight with counted vmcnt; out-of-range chunks are zeroed at store time.
+  __device__ void load(uint4 (&reg)[CHUNKS], int64_t k0, int64_t kend, int tid) const {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < CHUNKS; ++i) {
       int c = tid + NTHREADS * i;
-      uint4 v = make_uint4(0, 0, 0, 0);
       if constexpr (KC) {
-        int64_t k = k0 + (c & 7) * 8;
-        if (rvalid[i] && k < kend) v = *reinterpret_cast<const uint4*>(base + roff[i] + k);
+        int64_t k = min(k0 + (c & 7) * 8, kend - 8);
+        reg[i] = *reinterpret_cast<const uint4*>(base + roff[i] + k);
       } else {
-        int64_t k = k0 + (c >> 4);
-        int64_t col = r0 + (c & 15) * 8;
-        if (k < kend && col < R) v = *reinterpret_cast<const uint4*>(base + row_addr(d, k) + col);
+        int64_t k = min(k0 + (c >> 4), kend - 1);
+        int64_t col = min(r0 + (c & 15) * 8, R - 8);
+        reg[i] = *reinterpret_cast<const uint4*>(base + row_addr(d, k) + col);
       }
-      reg[i] = v;
     }
   }
 
-  __device__ void store(char* lds, const uint4 (&reg)[4], int tid) const {
+  __device__ void store(char* lds, const uint4 (&reg)[CHUNKS], int64_t k0, int64_t kend, int tid) const {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < CHUNKS; ++i) {
       int c = tid + NTHREADS * i;
       int byte;
+      bool ok;
       if constexpr (KC) {
         byte = ((c >> 3) * KROW + (c & 7) * 8) * 2;
+        ok = rvalid[i] && (k0 + (c & 7) * 8 < kend);
       } else {
         int kr = c >> 4;
         int col8 = c & 15;
         int u = (col8 >> 1) ^ swz(kr);
         byte = kr * 256 + u * 32 + (col8 & 1) * 16;
+        ok = (k0 + kr < kend) && (r0 + col8 * 8 < R);
       }
-      *reinterpret_cast<uint4*>(lds + byte) = reg[i];
+      *reinterpret_cast<uint4*>(lds + byte) = ok ? reg[i] : make_uint4(0, 0, 0, 0);
     }
   }
 };
@@ -144,108 +150,132 @@ __device__ __forceinline__ bf16x8_t frag(const char* lds, int rb, int ks, int la
 }
 
 // ---- epilogue ---------------------------------------------------------------
-struct EpiAcc {
-  float out[4];
-  float aux[4];
+// Row-contiguous epilogue: one thread handles 8 consecutive columns [n, n+8) of row m, so
+// every global access (bias / mask vectors, residual / aux inputs, pre-activation and C
+// outputs) is a 16-byte vector access and a wave covers whole 256-B row segments.
+struct Cs8 {
+  float out[8];
+  float aux[8];
 };
 
-// Apply the epilogue to 4 consecutive columns [n, n+4) of row m (batch z).
-// Returns the stored values (for column sums) in acc.out / acc.aux.
-__device__ __forceinline__ void epilogue4(const DphGemmArgs& a, int64_t z, int64_t m, int64_t n, float (&v)[4],
-                                          EpiAcc& cs) {
+__device__ __forceinline__ void load8_bf16(const bf16_t* p, bool vec, int nv, float (&o)[8]) {
+  if (vec) {
+    const uint4 r = *reinterpret_cast<const uint4*>(p);
+    const uint32_t w[4] = {r.x, r.y, r.z, r.w};
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+    for (int q = 0; q < 4; ++q) {
+      o[2 * q] = __uint_as_float(w[q] << 16);
+      o[2 * q + 1] = __uint_as_float(w[q] & 0xffff0000u);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = (i < nv) ? bf2f(p[i]) : 0.f;
+  }
+}
+
+__device__ __forceinline__ void load8_f32(const float* p, bool vec, int nv, float (&o)[8]) {
+  if (vec) {
+    const float4 a = *reinterpret_cast<const float4*>(p);
+    const float4 b = *reinterpret_cast<const float4*>(p + 4);
+    o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w;
+    o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = (i < nv) ? p[i] : 0.f;
+  }
+}
+
+__device__ __forceinline__ void store8_bf16(bf16_t* p, bool vec, int nv, const float (&v)[8]) {
+  if (vec) {
+    *reinterpret_cast<uint4*>(p) = make_uint4(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]),
+                                              pack2bf(v[6], v[7]));
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      if (i < nv) p[i] = f2bf(v[i]);
+  }
+}
+
+__device__ __forceinline__ void epilogue8(const DphGemmArgs& a, int64_t z, int64_t m, int64_t n, float (&v)[8],
+                                          Cs8& cs) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
     cs.out[i] = 0.f;
     cs.aux[i] = 0.f;
   }
   if (m >= a.M || n >= a.N) return;
   const int64_t voff = (a.C.z_div > 0 ? (z % a.C.z_div) : z) * a.vec_z_inner;
   const int64_t coff = z_addr(a.C, z) + row_addr(a.C, m) + n;
-  const bool full = (n + 4 <= a.N);
-  const int nv = full ? 4 : (int)(a.N - n);
+  const int nv = (int)min<int64_t>(8, a.N - n);
+  // 16-B vector path needs 8 valid columns and 16-B aligned rows (all strides multiples of 8)
+  const bool vec = (nv == 8) && ((coff & 7) == 0);
+  const bool vvec = (nv == 8) && (((voff + n) & 3) == 0);
   const float inv_keep = a.dropout_p > 0.f ? 1.0f / (1.0f - a.dropout_p) : 1.0f;
   const uint64_t drow = ((uint64_t)(z * a.M + a.drop_row_offset + m)) * (uint64_t)a.N;
   bool zero_row = false;
-  if (a.row_len) {
-    int64_t b = m / a.len_rows;
-    zero_row = (m % a.len_rows) >= a.row_len[b];
-  }
-  float pre[4], aux[4] = {0.f, 0.f, 0.f, 0.f}, res[4] = {0.f, 0.f, 0.f, 0.f};
-  if (a.aux_in) {
-    const bf16_t* p = reinterpret_cast<const bf16_t*>(a.aux_in) + coff;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      if (i < nv) aux[i] = bf2f(p[i]);
-  }
-  if (a.residual) {
-    const bf16_t* p = reinterpret_cast<const bf16_t*>(a.residual) + coff;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      if (i < nv) res[i] = bf2f(p[i]);
-  }
+  if (a.row_len) zero_row = (m % a.len_rows) >= a.row_len[m / a.len_rows];
+  float bias[8], cm[8], aux[8], res[8];
+  if (a.bias) load8_f32(a.bias + voff + n, vvec, nv, bias);
+  if (a.colmask) load8_f32(a.colmask + voff + n, vvec, nv, cm);
+  if (a.aux_in) load8_bf16(reinterpret_cast<const bf16_t*>(a.aux_in) + coff, vec, nv, aux);
+  if (a.residual) load8_bf16(reinterpret_cast<const bf16_t*>(a.residual) + coff, vec, nv, res);
   const float sm = a.smask ? *a.smask : 1.0f;
+  float pre[8];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int64_t nn = (i < nv) ? n + i : n;
+  for (int i = 0; i < 8; ++i) {
     float x = v[i] * a.alpha;
-    if (a.bias) x += a.bias[voff + nn];
+    if (a.bias) x += bias[i];
     pre[i] = x;
-    const float dz = dropout_scale(a.seed, drow + nn, a.dropout_p, inv_keep);
-    float cm = a.colmask ? a.colmask[voff + nn] : 1.0f;
+    const float dz = dropout_scale(a.seed, drow + n + i, a.dropout_p, inv_keep);
+    const float c = a.colmask ? cm[i] : 1.0f;
     float ax = 0.f;
     if (a.act == DPH_ACT_GELU) {
-      x = gelu_f(x) * dz * cm;
+      x = gelu_f(x) * dz * c;
     } else if (a.act == DPH_ACT_GELU_BWD) {
       const float gz = x * dz;
       ax = gz * gelu_f(aux[i]);
-      x = gz * gelu_grad_f(aux[i]) * cm;
+      x = gz * gelu_grad_f(aux[i]) * c;
     } else {
-      x = x * dz * cm;
+      x = x * dz * c;
     }
-    x = x * sm + res[i];
+    x = x * sm;
+    if (a.residual) x += res[i];
     if (zero_row) x = 0.f;
     v[i] = x;
     cs.out[i] = (i < nv) ? x : 0.f;
     cs.aux[i] = (i < nv) ? ax : 0.f;
   }
-  if (a.pre_out) {
-    bf16_t* p = reinterpret_cast<bf16_t*>(a.pre_out) + coff;
-    if (full) {
-      *reinterpret_cast<uint2*>(p) = make_uint2(pack2bf(pre[0], pre[1]), pack2bf(pre[2], pre[3]));
-    } else {
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if (i < nv) p[i] = f2bf(pre[i]);
-    }
-  }
+  if (a.pre_out) store8_bf16(reinterpret_cast<bf16_t*>(a.pre_out) + coff, vec, nv, pre);
   if (a.c_dtype == DPH_OUT_BF16) {
-    bf16_t* p = reinterpret_cast<bf16_t*>(a.C.ptr) + coff;
-    if (full) {
-      *reinterpret_cast<uint2*>(p) = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
-    } else {
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if (i < nv) p[i] = f2bf(v[i]);
-    }
+    store8_bf16(reinterpret_cast<bf16_t*>(a.C.ptr) + coff, vec, nv, v);
   } else {
     float* p = reinterpret_cast<float*>(a.C.ptr) + coff;
+    const bool fvec = (nv == 8) && ((coff & 3) == 0);
     if (a.c_dtype == DPH_OUT_F32_ACCUM) {
+      float old[8];
+      load8_f32(p, fvec, nv, old);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if (i < nv) p[i] += v[i];
-    } else if (full) {
+      for (int i = 0; i < 8; ++i) v[i] += old[i];
+    }
+    if (fvec) {
       *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+      *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
     } else {
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < 8; ++i)
         if (i < nv) p[i] = v[i];
     }
   }
 }
 
+// LDS staging of the fp32 accumulator tile for the row-contiguous epilogue
+constexpr int CROW = BN + 4;                       // padded fp32 row
+constexpr int LDS_C = BM * CROW * 4;               // 67,584 B
+
 template <bool AK, bool BKc>
 __global__ void __launch_bounds__(NTHREADS, 2) gemm_kernel(const DphGemmArgs a, int64_t kchunk) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * (TileBytes<AK>::v + TileBytes<BKc>::v)];
+  constexpr int PIPE = 2 * (TileBytes<AK>::v + TileBytes<BKc>::v);
+  __shared__ __attribute__((aligned(16))) char smem[PIPE > LDS_C ? PIPE : LDS_C];
   char* const ldsA0 = smem;
   char* const ldsB0 = smem + 2 * TileBytes<AK>::v;
 #define LDSA(buf) (ldsA0 + (buf) * TileBytes<AK>::v)
@@ -254,14 +284,35 @@ __global__ void __launch_bounds__(NTHREADS, 2) gemm_kernel(const DphGemmArgs a, 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const int wm = wave >> 1;
-  const int wn = wave & 1;
+  const int wm = wave >> 1;   // 0..1 -> rows wm*64 .. +64
+  const int wn = wave & 1;    // 0..1 -> cols wn*64 .. +64
 
   const int64_t zz = blockIdx.z;
   const int64_t split = zz % a.splits;
   const int64_t z = zz / a.splits;
-  const int64_t m0 = (int64_t)blockIdx.y * BM;
-  const int64_t n0 = (int64_t)blockIdx.x * BN;
+  // XCD-aware grouped tile order (guide T1): blocks are dealt round-robin over the 8 XCDs, so
+  // give every XCD a contiguous range of tiles, and walk that range in GROUP_M-tall column
+  // strips so the ~64 co-resident blocks of an XCD cover an 8x8 tile square and share their
+  // A/B panels in that XCD's private L2.
+  int64_t tm, tn;
+  {
+    const int64_t ntm = gridDim.y, ntn = gridDim.x;
+    const int64_t nt = ntm * ntn;
+    const int64_t bid = (int64_t)blockIdx.y * ntn + blockIdx.x;
+    const int64_t q = nt / 8, r = nt % 8;
+    const int64_t xcd = bid % 8, loc = bid / 8;
+    const int64_t t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+    constexpr int64_t GM = 8;
+    const int64_t gsz = GM * ntn;
+    const int64_t grp = t / gsz;
+    const int64_t gm0 = grp * GM;
+    const int64_t gh = min(GM, ntm - gm0);
+    const int64_t l = t % gsz;
+    tm = gm0 + l % gh;
+    tn = l / gh;
+  }
+  const int64_t m0 = tm * BM;
+  const int64_t n0 = tn * BN;
   const int64_t kbeg = split * kchunk;
   const int64_t kend = min(a.K, kbeg + kchunk);
 
@@ -270,134 +321,171 @@ __global__ void __launch_bounds__(NTHREADS, 2) gemm_kernel(const DphGemmArgs a, 
   sa.init(a.A, reinterpret_cast<const bf16_t*>(a.A.ptr) + z_addr(a.A, z), m0, a.M, tid);
   sb.init(a.B, reinterpret_cast<const bf16_t*>(a.B.ptr) + z_addr(a.B, z), n0, a.N, tid);
 
-  f32x4_t acc[4][4];
+  f32x4_t acc[4][NJ];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  uint4 ra[4], rb[4];
+  // Pipeline: LDS double buffer + one register stage.  Tile t+1 is issued into registers at the
+  // top of step t (unconditional loads: counted vmcnt), tile t is computed from LDS, then tile
+  // t+1 is written to the other LDS buffer behind one barrier.  Two co-resident blocks per CU
+  // (73 KB LDS, <=256 VGPR) overlap each other's load latency.
+  uint4 ra[CHUNKS], rb[CHUNKS];
   const int nk = (int)cdiv(max<int64_t>(kend - kbeg, 0), BK);
+  auto kof = [&](int t) { return kbeg + (int64_t)t * BK; };
   if (nk > 0) {
-    sa.load(ra, kbeg, kend, tid);
-    sb.load(rb, kbeg, kend, tid);
-    sa.store(LDSA(0), ra, tid);
-    sb.store(LDSB(0), rb, tid);
+    sa.load(ra, kof(0), kend, tid);
+    sb.load(rb, kof(0), kend, tid);
+    sa.store(LDSA(0), ra, kof(0), kend, tid);
+    sb.store(LDSB(0), rb, kof(0), kend, tid);
   }
   __syncthreads();
   for (int t = 0; t < nk; ++t) {
     const int cur = t & 1;
     const bool more = (t + 1) < nk;
     if (more) {
-      sa.load(ra, kbeg + (int64_t)(t + 1) * BK, kend, tid);
-      sb.load(rb, kbeg + (int64_t)(t + 1) * BK, kend, tid);
+      sa.load(ra, kof(t + 1), kend, tid);
+      sb.load(rb, kof(t + 1), kend, tid);
     }
+    const char* LA = LDSA(cur);
+    const char* LB = LDSB(cur);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      bf16x8_t af[4], bfr[4];
+      bf16x8_t af[4], bfr[NJ];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = frag<AK>(LDSA(cur), wm * 64 + 16 * i, ks, lane);
+      for (int i = 0; i < 4; ++i) af[i] = frag<AK>(LA, wm * 64 + 16 * i, ks, lane);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bfr[j] = frag<BKc>(LDSB(cur), wn * 64 + 16 * j, ks, lane);
+      for (int j = 0; j < NJ; ++j) bfr[j] = frag<BKc>(LB, wn * WTN + 16 * j, ks, lane);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < NJ; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
     }
     if (more) {
-      sa.store(LDSA(cur ^ 1), ra, tid);
-      sb.store(LDSB(cur ^ 1), rb, tid);
+      sa.store(LDSA(cur ^ 1), ra, kof(t + 1), kend, tid);
+      sb.store(LDSB(cur ^ 1), rb, kof(t + 1), kend, tid);
     }
     __syncthreads();
   }
 
 #undef LDSA
 #undef LDSB
-  // lane holds C[m = rowbase + (lane&15)][n = colbase + 4*(lane>>4) + r]
+  // ---- accumulators -> LDS (lane holds C[rowbase + (lane&15)][colbase + 4*(lane>>4) + r]) ----
+  float* ct = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = wm * 64 + 16 * i + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int c = wn * WTN + 16 * j + 4 * (lane >> 4);
+      *reinterpret_cast<float4*>(ct + r * CROW + c) = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2],
+                                                                   acc[i][j][3]);
+    }
+  }
+  __syncthreads();
+  // ---- row-contiguous epilogue: thread = 8 columns x 8 rows (rows r0 + 16 p) ----
+  const int c8 = (tid & 15) * 8;
+  const int r0 = tid >> 4;
   if (a.splits > 1) {
     float* ws = reinterpret_cast<float*>(a.workspace) + (zz * a.M) * a.N;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int64_t m = m0 + wm * 64 + 16 * i + (lane & 15);
-      if (m >= a.M) continue;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int64_t n = n0 + wn * 64 + 16 * j + 4 * (lane >> 4);
-        if (n + 4 <= a.N) {
-          *reinterpret_cast<float4*>(ws + m * a.N + n) = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2],
-                                                                      acc[i][j][3]);
-        } else {
-          for (int r = 0; r < 4 && n + r < a.N; ++r) ws[m * a.N + n + r] = acc[i][j][r];
-        }
+#pragma unroll 2
+    for (int p = 0; p < BM * BN / 8 / NTHREADS; ++p) {
+      const int r = r0 + (NTHREADS / 16) * p;
+      const int64_t m = m0 + r;
+      const int64_t n = n0 + c8;
+      if (m >= a.M || n >= a.N) continue;
+      const float* src = ct + r * CROW + c8;
+      float* dst = ws + m * a.N + n;
+      if (n + 8 <= a.N && (a.N & 3) == 0) {
+        *reinterpret_cast<float4*>(dst) = *reinterpret_cast<const float4*>(src);
+        *reinterpret_cast<float4*>(dst + 4) = *reinterpret_cast<const float4*>(src + 4);
+      } else {
+        for (int q = 0; q < 8 && n + q < a.N; ++q) dst[q] = src[q];
       }
     }
     return;
   }
-
-  const bool want_cs = (a.colsum_out != nullptr) || (a.colsum_aux != nullptr);
-  float cso[4][4], csa[4][4];
+  float cso[8], csa[8];
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
+  for (int q = 0; q < 8; ++q) {
+    cso[q] = 0.f;
+    csa[q] = 0.f;
+  }
+#pragma unroll 1
+  for (int p = 0; p < BM * BN / 8 / NTHREADS; ++p) {
+    const int r = r0 + (NTHREADS / 16) * p;
+    const float* src = ct + r * CROW + c8;
+    float v[8];
+    const float4 x0 = *reinterpret_cast<const float4*>(src);
+    const float4 x1 = *reinterpret_cast<const float4*>(src + 4);
+    v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w;
+    v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
+    Cs8 cs;
+    epilogue8(a, z, m0 + r, n0 + c8, v, cs);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      cso[j][r] = 0.f;
-      csa[j][r] = 0.f;
-    }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int64_t m = m0 + wm * 64 + 16 * i + (lane & 15);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int64_t n = n0 + wn * 64 + 16 * j + 4 * (lane >> 4);
-      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      EpiAcc cs;
-      epilogue4(a, z, m, n, v, cs);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        cso[j][r] += cs.out[r];
-        csa[j][r] += cs.aux[r];
-      }
+    for (int q = 0; q < 8; ++q) {
+      cso[q] += cs.out[q];
+      csa[q] += cs.aux[q];
     }
   }
-  if (want_cs) {
-    const int64_t voff = (a.C.z_div > 0 ? (z % a.C.z_div) : z) * a.vec_z_inner;
+  if ((a.colsum_out != nullptr) || (a.colsum_aux != nullptr)) {
+    // lanes l, l^16, l^32, l^48 share columns inside a wave; then 4 waves through LDS
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int q = 0; q < 8; ++q) {
+      cso[q] += __shfl_xor(cso[q], 16, 64);
+      cso[q] += __shfl_xor(cso[q], 32, 64);
+      csa[q] += __shfl_xor(csa[q], 16, 64);
+      csa[q] += __shfl_xor(csa[q], 32, 64);
+    }
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);   // [waves][2][128]
+    if (lane < 16) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float so = cso[j][r], sx = csa[j][r];
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-          so += __shfl_xor(so, o, 64);
-          sx += __shfl_xor(sx, o, 64);
-        }
-        const int64_t n = n0 + wn * 64 + 16 * j + 4 * (lane >> 4) + r;
-        if ((lane & 15) == 0 && n < a.N) {
-          if (a.colsum_out) atomicAdd(a.colsum_out + voff + n, so);
-          if (a.colsum_aux) atomicAdd(a.colsum_aux + voff + n, sx);
-        }
+      for (int q = 0; q < 8; ++q) {
+        red[(wave * 2 + 0) * 128 + c8 + q] = cso[q];
+        red[(wave * 2 + 1) * 128 + c8 + q] = csa[q];
       }
+    }
+    __syncthreads();
+    if (tid < 128) {
+      const int64_t n = n0 + tid;
+      if (n < a.N) {
+        const int64_t voff = (a.C.z_div > 0 ? (z % a.C.z_div) : z) * a.vec_z_inner;
+        float so = 0.f, sx = 0.f;
+#pragma unroll
+        for (int w = 0; w < NTHREADS / 64; ++w) {
+          so += red[(w * 2 + 0) * 128 + tid];
+          sx += red[(w * 2 + 1) * 128 + tid];
+        }
+        if (a.colsum_out) atomicAdd(a.colsum_out + voff + n, so);
+        if (a.colsum_aux) atomicAdd(a.colsum_aux + voff + n, sx);
+      }
+    }
   }
 }
 
-// split-K reduction + epilogue: one thread per 4 columns
+// split-K reduction + epilogue: one thread per 8 columns of a row
 __global__ void splitk_reduce_kernel(const DphGemmArgs a) {
   const int64_t z = blockIdx.z;
-  const int64_t n4 = (a.N + 3) / 4;
+  const int64_t n8 = (a.N + 7) / 8;
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= a.M * n4) return;
-  const int64_t m = idx / n4;
-  const int64_t n = (idx % n4) * 4;
+  if (idx >= a.M * n8) return;
+  const int64_t m = idx / n8;
+  const int64_t n = (idx % n8) * 8;
   const float* ws = reinterpret_cast<const float*>(a.workspace);
-  float v[4] = {0.f, 0.f, 0.f, 0.f};
+  float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const bool vec = (n + 8 <= a.N) && ((a.N & 3) == 0);
   for (int s = 0; s < a.splits; ++s) {
     const float* p = ws + ((z * a.splits + s) * a.M + m) * a.N + n;
-    for (int r = 0; r < 4; ++r)
-      if (n + r < a.N) v[r] += p[r];
+    float t[8];
+    load8_f32(p, vec, (int)min<int64_t>(8, a.N - n), t);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] += t[q];
   }
-  EpiAcc cs;
-  epilogue4(a, z, m, n, v, cs);
+  Cs8 cs;
+  epilogue8(a, z, m, n, v, cs);
 }
 
 }  // namespace
@@ -440,7 +528,7 @@ extern "C" int dph_gemm(const DphGemmArgs* args, hipStream_t stream) {
   int rc = check_launch("dph_gemm");
   if (rc) return rc;
   if (a.splits > 1) {
-    const int64_t work = a.M * cdiv(a.N, 4);
+    const int64_t work = a.M * cdiv(a.N, 8);
     dim3 g2((unsigned)cdiv(work, 256), 1, (unsigned)a.batch);
     hipLaunchKernelGGL(splitk_reduce_kernel, g2, dim3(256), 0, stream, a);
     rc = check_launch("dph_gemm splitk_reduce");
