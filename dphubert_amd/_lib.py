@@ -13,7 +13,8 @@ from pathlib import Path
 import torch
 
 _HERE = Path(__file__).resolve().parent
-LIB_PATH = _HERE / "libdphubert_hip.so"
+# DPH_LIB_PATH selects another build of the same library (A/B measurements)
+LIB_PATH = Path(os.environ.get("DPH_LIB_PATH", str(_HERE / "libdphubert_hip.so")))
 
 vp = C.c_void_p
 i64 = C.c_int64
@@ -65,8 +66,8 @@ _SIGS = {
     "dph_col2im_gelu_bwd": ([vp, i64, i64, i64, i64, i64, i64, vp, vp, vp, vp, S], C.c_int),
     "dph_gelu_mask_bwd": ([vp, vp, vp, vp, vp, i64, i64, S], C.c_int),
     "dph_regroup_pad": ([vp, vp, i64, i64, i64, i64, i64, i64, S], C.c_int),
-    "dph_weight_norm_fwd": ([vp, vp, i64, i64, i64, i64, vp, vp, vp, vp, S], C.c_int),
-    "dph_weight_norm_bwd": ([vp, vp, vp, vp, i64, i64, i64, i64, vp, vp, S], C.c_int),
+    "dph_weight_norm_fwd": ([vp, vp, i64, i64, i64, i64, vp, vp, vp, vp, vp, i64, S], C.c_int),
+    "dph_weight_norm_bwd": ([vp, vp, vp, vp, i64, i64, i64, i64, vp, vp, vp, i64, S], C.c_int),
     "dph_cast_bf16": ([vp, vp, i64, S], C.c_int),
     "dph_conv_weight_pack": ([vp, vp, i64, i64, i64, S], C.c_int),
     "dph_conv_weight_unpack_grad": ([vp, vp, i64, i64, i64, C.c_int, S], C.c_int),

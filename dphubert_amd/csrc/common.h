@@ -45,13 +45,61 @@ __device__ __forceinline__ uint32_t pack2bf(float a, float b) {
   return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
 }
 
-// exact-erf GELU (torch default), components.py:110,331,734
-__device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+// 8 consecutive bf16 -> fp32 (16-B vector load when the row is 8-aligned; masked tail otherwise)
+__device__ __forceinline__ void load_bf16x8(const bf16_t* p, int64_t c0, int64_t C, float (&v)[8]) {
+  if (c0 + 8 <= C && (C & 7) == 0) {
+    const uint4 r = *reinterpret_cast<const uint4*>(p);
+    const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] = __uint_as_float(w[i] << 16);
+      v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = (c0 + i < C) ? bf2f(p[i]) : 0.f;
+  }
+}
+
+// Exact-erf GELU (torch default, components.py:110,331,734).  Phi(x) is evaluated through
+// erfc with the Chebyshev-fitted form of Numerical Recipes (6.2), fractional error < 1.2e-7
+// over the whole real line: branch-free, ~13 VALU ops instead of the libm erff, and more
+// accurate than 1 + erf(x) for negative x (no cancellation).  Outputs are stored in bf16
+// (relative step 3.9e-3), so the approximation error is invisible.
+__device__ __forceinline__ float erfc_pos(float z, float& e_minus_z2) {
+  // z >= 0; returns erfc(z) and exp(-z^2)
+  const float t = 1.0f / (1.0f + 0.5f * z);
+  const float p = -1.26551223f + t * (1.00002368f + t * (0.37409196f + t * (0.09678418f +
+                  t * (-0.18628806f + t * (0.27886807f + t * (-1.13520398f + t * (1.48851587f +
+                  t * (-0.82215223f + t * 0.17087277f))))))));
+  e_minus_z2 = __expf(-z * z);
+  return t * e_minus_z2 * __expf(p);
+}
+
+__device__ __forceinline__ float norm_cdf(float x, float& pdf) {
+  float e;
+  const float r = erfc_pos(fabsf(x) * 0.70710678118654752f, e);
+  pdf = 0.39894228040143268f * e;   // phi(x) = exp(-x^2/2)/sqrt(2 pi)
+  return x >= 0.f ? 1.0f - 0.5f * r : 0.5f * r;
+}
+
+__device__ __forceinline__ float gelu_f(float x) {
+  float pdf;
+  return x * norm_cdf(x, pdf);
+}
 
 __device__ __forceinline__ float gelu_grad_f(float x) {
-  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
-  const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
+  float pdf;
+  const float cdf = norm_cdf(x, pdf);
   return cdf + x * pdf;
+}
+
+// gelu and gelu' together (one erfc evaluation)
+__device__ __forceinline__ void gelu_and_grad(float x, float& g, float& dg) {
+  float pdf;
+  const float cdf = norm_cdf(x, pdf);
+  g = x * cdf;
+  dg = cdf + x * pdf;
 }
 
 // Counter-based RNG: splitmix64 finaliser of (seed, element index).  The same

@@ -41,25 +41,24 @@ __global__ void __launch_bounds__(256) gelu_mask_bwd_kernel(const bf16_t* __rest
           if (d < 0 || d % s) continue;
           const int64_t t = d / s;
           if (t >= Lout) continue;
-          const bf16_t* p = src + ((b * Lout + t) * k + j) * C + c0;
+          float v[8];
+          load_bf16x8(src + ((b * Lout + t) * k + j) * C + c0, c0, C, v);
 #pragma unroll
-          for (int i = 0; i < 8; ++i)
-            if (c0 + i < C) dy[i] += bf2f(p[i]);
+          for (int i = 0; i < 8; ++i) dy[i] += v[i];
         }
       } else {
-        const bf16_t* p = src + r * C + c0;
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-          if (c0 + i < C) dy[i] = bf2f(p[i]);
+        load_bf16x8(src + r * C + c0, c0, C, dy);
       }
       float o[8];
       if (z_pre) {
-        const bf16_t* zp = z_pre + r * C + c0;
+        float z[8];
+        load_bf16x8(z_pre + r * C + c0, c0, C, z);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-          const float z = (c0 + i < C) ? bf2f(zp[i]) : 0.f;
-          acc[i] += dy[i] * gelu_f(z);
-          o[i] = dy[i] * mk[i] * gelu_grad_f(z);
+          float g, dg;
+          gelu_and_grad(z[i], g, dg);
+          acc[i] += dy[i] * g;
+          o[i] = dy[i] * mk[i] * dg;
         }
       } else {
 #pragma unroll

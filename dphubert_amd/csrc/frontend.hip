@@ -28,10 +28,39 @@ struct Conv0 {
   int k0, s0;
 };
 
-// partial stats: ws[((b*nch + ch)*C + c)*2 + {0,1}] = (mean_chunk, M2_chunk)
+// thread layout shared by the conv0 kernels: TPR threads per time row, CPT channels each,
+// RPP rows in flight per pass (a wave covers whole rows -> the waveform taps are LDS broadcasts)
+template <int CPT>
+struct RowLayout {
+  int tpr, rpp;
+  __device__ RowLayout(int64_t C) {
+    tpr = (int)((C + CPT - 1) / CPT);
+    rpp = max(1, 256 / tpr);
+  }
+};
+
+template <int CPT>
+__device__ __forceinline__ void conv_taps(const float (&wr)[CPT][MAXK0], const float* xs, int k0, float (&v)[CPT]) {
+#pragma unroll
+  for (int i = 0; i < CPT; ++i) v[i] = 0.f;
+#pragma unroll
+  for (int j = 0; j < MAXK0; ++j) {
+    if (j < k0) {
+      const float x = xs[j];
+#pragma unroll
+      for (int i = 0; i < CPT; ++i) v[i] = fmaf(wr[i][j], x, v[i]);
+    }
+  }
+}
+
+// Partial statistics per (utterance, chunk of STAT_CH steps, channel): shifted sums around the
+// chunk's first conv value (stable), written as (chunk mean, M2) for a Chan merge.
+// ws[((b*nch + ch)*C + c)*2 + {0,1}]
 __global__ void __launch_bounds__(256) conv0_stats_kernel(const float* __restrict__ wave, const float* __restrict__ w,
                                                           Conv0 p, float* __restrict__ ws, int nch) {
+  constexpr int CPT = 8;
   __shared__ float xs[STAT_CH * 8 + MAXK0];
+  __shared__ float red[256 * CPT * 2];
   const int64_t b = blockIdx.y;
   const int ch = blockIdx.x;
   const int64_t t0 = (int64_t)ch * STAT_CH;
@@ -40,31 +69,55 @@ __global__ void __launch_bounds__(256) conv0_stats_kernel(const float* __restric
   const float* xw = wave + b * p.S + t0 * p.s0;
   for (int i = threadIdx.x; i < nsamp; i += blockDim.x) xs[i] = xw[i];
   __syncthreads();
-  for (int64_t c = threadIdx.x; c < p.C; c += blockDim.x) {
-    float wr[MAXK0];
+  RowLayout<CPT> L(p.C);
+  const int tid = threadIdx.x;
+  const bool active = tid < L.tpr * L.rpp;
+  const int64_t c0 = active ? (int64_t)(tid % L.tpr) * CPT : 0;
+  const int r0 = active ? tid / L.tpr : 0;
+  float wr[CPT][MAXK0];
 #pragma unroll
-    for (int j = 0; j < MAXK0; ++j) wr[j] = j < p.k0 ? w[c * p.k0 + j] : 0.f;
-    float s = 0.f;
-    for (int t = 0; t < nt; ++t) {
-      float v = 0.f;
+  for (int i = 0; i < CPT; ++i)
 #pragma unroll
-      for (int j = 0; j < MAXK0; ++j)
-        if (j < p.k0) v += wr[j] * xs[t * p.s0 + j];
-      s += v;
+    for (int j = 0; j < MAXK0; ++j) wr[i][j] = (active && c0 + i < p.C && j < p.k0) ? w[(c0 + i) * p.k0 + j] : 0.f;
+  float sh[CPT], s1[CPT], s2[CPT];
+  conv_taps<CPT>(wr, xs, p.k0, sh);          // shift = conv value at the chunk's first step
+#pragma unroll
+  for (int i = 0; i < CPT; ++i) s1[i] = s2[i] = 0.f;
+  if (active) {
+    for (int t = r0; t < nt; t += L.rpp) {
+      float v[CPT];
+      conv_taps<CPT>(wr, xs + t * p.s0, p.k0, v);
+#pragma unroll
+      for (int i = 0; i < CPT; ++i) {
+        const float d = v[i] - sh[i];
+        s1[i] += d;
+        s2[i] = fmaf(d, d, s2[i]);
+      }
     }
-    const float m = s / nt;
-    float q = 0.f;
-    for (int t = 0; t < nt; ++t) {
-      float v = 0.f;
+  }
 #pragma unroll
-      for (int j = 0; j < MAXK0; ++j)
-        if (j < p.k0) v += wr[j] * xs[t * p.s0 + j];
-      const float d = v - m;
-      q += d * d;
+  for (int i = 0; i < CPT; ++i) {
+    red[(tid * CPT + i) * 2 + 0] = s1[i];
+    red[(tid * CPT + i) * 2 + 1] = s2[i];
+  }
+  __syncthreads();
+  if (active && r0 == 0) {
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      float a = 0.f, q = 0.f;
+      for (int r = 0; r < L.rpp; ++r) {
+        const int tt = r * L.tpr + (tid % L.tpr);
+        a += red[(tt * CPT + i) * 2 + 0];
+        q += red[(tt * CPT + i) * 2 + 1];
+      }
+      const int64_t c = c0 + i;
+      if (c < p.C) {
+        const float m = a / nt;
+        float* o = ws + ((b * nch + ch) * p.C + c) * 2;
+        o[0] = sh[i] + m;
+        o[1] = fmaxf(q - a * m, 0.f);
+      }
     }
-    float* o = ws + ((b * nch + ch) * p.C + c) * 2;
-    o[0] = m;
-    o[1] = q;
   }
 }
 
@@ -89,15 +142,6 @@ __global__ void conv0_stats_finalize(const float* __restrict__ ws, Conv0 p, int 
   rstd[i] = (float)(1.0 / sqrt(M2 / n + (double)eps));
 }
 
-// thread layout for apply/backward: TPR threads per time row, 8 channels each
-struct RowLayout {
-  int tpr, rpp;  // threads per row, rows per pass
-  __device__ RowLayout(int64_t C) {
-    tpr = (int)((C + 7) / 8);
-    rpp = max(1, 256 / tpr);
-  }
-};
-
 template <bool GN>
 __global__ void __launch_bounds__(256) conv0_apply_kernel(const float* __restrict__ wave, const float* __restrict__ w,
                                                           const float* __restrict__ bias, Conv0 p,
@@ -106,6 +150,7 @@ __global__ void __launch_bounds__(256) conv0_apply_kernel(const float* __restric
                                                           const float* __restrict__ mask,
                                                           const float* __restrict__ mean,
                                                           const float* __restrict__ rstd, bf16_t* __restrict__ y) {
+  constexpr int CPT = 8;
   __shared__ float xs[APPLY_ROWS * 8 + MAXK0];
   const int64_t b = blockIdx.y;
   const int64_t t0 = (int64_t)blockIdx.x * APPLY_ROWS;
@@ -114,14 +159,14 @@ __global__ void __launch_bounds__(256) conv0_apply_kernel(const float* __restric
   const float* xw = wave + b * p.S + t0 * p.s0;
   for (int i = threadIdx.x; i < nsamp; i += blockDim.x) xs[i] = xw[i];
   __syncthreads();
-  RowLayout L(p.C);
+  RowLayout<CPT> L(p.C);
   const int tid = threadIdx.x;
   if (tid >= L.tpr * L.rpp) return;
-  const int64_t c0 = (int64_t)(tid % L.tpr) * 8;
+  const int64_t c0 = (int64_t)(tid % L.tpr) * CPT;
   const int r0 = tid / L.tpr;
-  float wr[8][MAXK0], sc[8], sh[8], mk[8];
+  float wr[CPT][MAXK0], sc[CPT], sh[CPT], mk[CPT];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
+  for (int i = 0; i < CPT; ++i) {
     const int64_t c = c0 + i;
     const bool ok = c < p.C;
 #pragma unroll
@@ -138,14 +183,11 @@ __global__ void __launch_bounds__(256) conv0_apply_kernel(const float* __restric
     mk[i] = (ok && mask) ? mask[c] : 1.f;
   }
   for (int t = r0; t < nt; t += L.rpp) {
-    float o[8];
+    float o[CPT];
+    conv_taps<CPT>(wr, xs + t * p.s0, p.k0, o);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      float v = 0.f;
-#pragma unroll
-      for (int j = 0; j < MAXK0; ++j)
-        if (j < p.k0) v += wr[i][j] * xs[t * p.s0 + j];
-      v = v * sc[i] + sh[i];
+    for (int i = 0; i < CPT; ++i) {
+      const float v = fmaf(o[i], sc[i], sh[i]);
       o[i] = GN ? gelu_f(v) * mk[i] : v;
     }
     bf16_t* yp = y + ((b * p.L0) + t0 + t) * p.C + c0;
@@ -154,7 +196,7 @@ __global__ void __launch_bounds__(256) conv0_apply_kernel(const float* __restric
                                                  pack2bf(o[6], o[7]));
     } else {
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
+      for (int i = 0; i < CPT; ++i)
         if (c0 + i < p.C) yp[i] = f2bf(o[i]);
     }
   }
@@ -162,6 +204,7 @@ __global__ void __launch_bounds__(256) conv0_apply_kernel(const float* __restric
 
 // Backward pass 1 (PASS=1): per-(b,c) sums A = sum dxh, Bv = sum dxh*xh; per-c dgamma, dbeta, dmask.
 // Backward pass 2 (PASS=2): dconv = rstd*(dxh - A/N - xh*Bv/N); dw[c][j] += sum dconv * x[s0 t + j].
+// 4 channels per thread keeps the tap weights + tap accumulators at ~80 VGPRs.
 template <int PASS>
 __global__ void __launch_bounds__(256) conv0_gn_bwd_kernel(const float* __restrict__ wave,
                                                            const float* __restrict__ w, Conv0 p,
@@ -173,8 +216,9 @@ __global__ void __launch_bounds__(256) conv0_gn_bwd_kernel(const float* __restri
                                                            const bf16_t* __restrict__ dy, float* __restrict__ sums,
                                                            float* __restrict__ dw, float* __restrict__ dgamma,
                                                            float* __restrict__ dbeta, float* __restrict__ dmask) {
+  constexpr int CPT = 4;
   __shared__ float xs[BWD_ROWS * 8 + MAXK0];
-  __shared__ float red[256 * 8];
+  __shared__ float red[256 * CPT];
   const int64_t b = blockIdx.y;
   const int64_t t0 = (int64_t)blockIdx.x * BWD_ROWS;
   const int nt = (int)min<int64_t>(BWD_ROWS, p.L0 - t0);
@@ -182,15 +226,15 @@ __global__ void __launch_bounds__(256) conv0_gn_bwd_kernel(const float* __restri
   const float* xw = wave + b * p.S + t0 * p.s0;
   for (int i = threadIdx.x; i < nsamp; i += blockDim.x) xs[i] = xw[i];
   __syncthreads();
-  RowLayout L(p.C);
+  RowLayout<CPT> L(p.C);
   const int tid = threadIdx.x;
   const bool active = tid < L.tpr * L.rpp;
-  const int64_t c0 = active ? (int64_t)(tid % L.tpr) * 8 : 0;
+  const int64_t c0 = active ? (int64_t)(tid % L.tpr) * CPT : 0;
   const int r0 = active ? tid / L.tpr : 0;
   const float invN = 1.0f / (float)p.L0;
-  float wr[8][MAXK0], mu[8], rs[8], ga[8], be[8], mk[8], sA[8], sB[8];
+  float wr[CPT][MAXK0], mu[CPT], rs[CPT], ga[CPT], be[CPT], mk[CPT], sA[CPT], sB[CPT];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
+  for (int i = 0; i < CPT; ++i) {
     const int64_t c = c0 + i;
     const bool ok = active && c < p.C;
 #pragma unroll
@@ -200,53 +244,52 @@ __global__ void __launch_bounds__(256) conv0_gn_bwd_kernel(const float* __restri
     ga[i] = ok ? gamma[c] : 0.f;
     be[i] = ok ? beta[c] : 0.f;
     mk[i] = (ok && mask) ? mask[c] : 1.f;
-    if (PASS == 2) {
-      sA[i] = ok ? sums[(b * p.C + c) * 2 + 0] * invN : 0.f;
-      sB[i] = ok ? sums[(b * p.C + c) * 2 + 1] * invN : 0.f;
+    sA[i] = sB[i] = 0.f;
+    if (PASS == 2 && ok) {
+      sA[i] = sums[(b * p.C + c) * 2 + 0] * invN;
+      sB[i] = sums[(b * p.C + c) * 2 + 1] * invN;
     }
   }
-  float acc[8][MAXK0];   // PASS1: [i][0..4] = A, Bv, dgamma, dbeta, dmask; PASS2: dw taps
+  float acc[CPT][MAXK0];   // PASS1: [i][0..4] = A, Bv, dgamma, dbeta, dmask; PASS2: dw taps
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < CPT; ++i)
 #pragma unroll
     for (int j = 0; j < MAXK0; ++j) acc[i][j] = 0.f;
   if (active) {
     for (int t = r0; t < nt; t += L.rpp) {
       const bf16_t* dyp = dy + ((b * p.L0) + t0 + t) * p.C + c0;
-      float dyv[8];
-      if (c0 + 8 <= p.C && p.C % 8 == 0) {
-        uint4 raw = *reinterpret_cast<const uint4*>(dyp);
-        uint32_t wv[4] = {raw.x, raw.y, raw.z, raw.w};
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          dyv[2 * q] = __uint_as_float(wv[q] << 16);
-          dyv[2 * q + 1] = __uint_as_float(wv[q] & 0xffff0000u);
-        }
+      float dyv[CPT];
+      if (c0 + CPT <= p.C && p.C % CPT == 0) {
+        const uint2 raw = *reinterpret_cast<const uint2*>(dyp);
+        dyv[0] = __uint_as_float(raw.x << 16);
+        dyv[1] = __uint_as_float(raw.x & 0xffff0000u);
+        dyv[2] = __uint_as_float(raw.y << 16);
+        dyv[3] = __uint_as_float(raw.y & 0xffff0000u);
       } else {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) dyv[i] = (c0 + i < p.C) ? bf2f(dyp[i]) : 0.f;
+        for (int i = 0; i < CPT; ++i) dyv[i] = (c0 + i < p.C) ? bf2f(dyp[i]) : 0.f;
       }
+      float v[CPT];
+      conv_taps<CPT>(wr, xs + t * p.s0, p.k0, v);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        float v = 0.f;
-#pragma unroll
-        for (int j = 0; j < MAXK0; ++j)
-          if (j < p.k0) v += wr[i][j] * xs[t * p.s0 + j];
-        const float xh = (v - mu[i]) * rs[i];
-        const float g = ga[i] * xh + be[i];
-        const float dg = dyv[i] * mk[i] * gelu_grad_f(g);
+      for (int i = 0; i < CPT; ++i) {
+        const float xh = (v[i] - mu[i]) * rs[i];
+        const float g = fmaf(ga[i], xh, be[i]);
+        float gl, gd;
+        gelu_and_grad(g, gl, gd);
+        const float dg = dyv[i] * mk[i] * gd;
         const float dxh = dg * ga[i];
         if (PASS == 1) {
           acc[i][0] += dxh;
-          acc[i][1] += dxh * xh;
-          acc[i][2] += dg * xh;
+          acc[i][1] = fmaf(dxh, xh, acc[i][1]);
+          acc[i][2] = fmaf(dg, xh, acc[i][2]);
           acc[i][3] += dg;
-          acc[i][4] += dyv[i] * gelu_f(g);
+          acc[i][4] = fmaf(dyv[i], gl, acc[i][4]);
         } else {
           const float dc = rs[i] * (dxh - sA[i] - xh * sB[i]);
 #pragma unroll
           for (int j = 0; j < MAXK0; ++j)
-            if (j < p.k0) acc[i][j] += dc * xs[t * p.s0 + j];
+            if (j < p.k0) acc[i][j] = fmaf(dc, xs[t * p.s0 + j], acc[i][j]);
         }
       }
     }
@@ -257,13 +300,13 @@ __global__ void __launch_bounds__(256) conv0_gn_bwd_kernel(const float* __restri
   for (int a = 0; a < MAXK0; ++a) {
     if (a < nacc) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) red[tid * 8 + i] = acc[i][a];
+      for (int i = 0; i < CPT; ++i) red[tid * CPT + i] = acc[i][a];
       __syncthreads();
       if (active && r0 == 0) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
+        for (int i = 0; i < CPT; ++i) {
           float s = 0.f;
-          for (int r = 0; r < L.rpp; ++r) s += red[(r * L.tpr + (tid % L.tpr)) * 8 + i];
+          for (int r = 0; r < L.rpp; ++r) s += red[(r * L.tpr + (tid % L.tpr)) * CPT + i];
           const int64_t c = c0 + i;
           if (c < p.C) {
             if (PASS == 1) {
@@ -284,16 +327,28 @@ __global__ void __launch_bounds__(256) conv0_gn_bwd_kernel(const float* __restri
 }
 
 // ---- weight norm -----------------------------------------------------------
-// sumsq over dims (0,1) per kernel tap j: x [R][K] (R = Cout*Cin_g), out[j] += sum_r a[r][j]*b[r][j]
-__global__ void tap_dot_kernel(const float* __restrict__ a, const float* __restrict__ bb, int64_t R, int64_t K,
-                               float* __restrict__ out, int64_t rows_per_block) {
+// per-tap dot products over dims (0,1), deterministic two-stage reduction (no atomics, so the
+// forward pass is bitwise reproducible): x [R][K] (R = Cout*Cin_g)
+//   stage 1: part[blk][j] = sum_{r in blk} a[r][j]*b[r][j]
+//   stage 2: out[j] = sum_blk part[blk][j]  (fixed order)
+__global__ void tap_dot_partial_kernel(const float* __restrict__ a, const float* __restrict__ bb, int64_t R,
+                                       int64_t K, float* __restrict__ part, int64_t rows_per_block) {
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
   const int64_t r1 = min(R, r0 + rows_per_block);
   for (int64_t j = threadIdx.x; j < K; j += blockDim.x) {
     float s = 0.f;
-    for (int64_t r = r0; r < r1; ++r) s += a[r * K + j] * bb[r * K + j];
-    atomicAdd(out + j, s);
+    for (int64_t r = r0; r < r1; ++r) s = fmaf(a[r * K + j], bb[r * K + j], s);
+    part[(int64_t)blockIdx.x * K + j] = s;
   }
+}
+
+__global__ void tap_dot_finalize_kernel(const float* __restrict__ part, int64_t nblk, int64_t K,
+                                        float* __restrict__ out) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= K) return;
+  float s = 0.f;
+  for (int64_t b = 0; b < nblk; ++b) s += part[b * K + j];
+  out[j] = s;
 }
 
 __global__ void weight_norm_apply_kernel(const float* __restrict__ g, const float* __restrict__ v,
@@ -402,18 +457,29 @@ extern "C" int dph_conv0_gn_bwd(const float* wave, int64_t B, int64_t S, const f
   return check_launch("dph_conv0_gn_bwd");
 }
 
+static constexpr int64_t TAP_ROWS = 64;
+
+static int tap_dot(const float* a, const float* b, int64_t R, int64_t K, float* out, float* ws, int64_t ws_bytes,
+                   hipStream_t stream) {
+  const int64_t nblk = cdiv(R, TAP_ROWS);
+  DPH_REQUIRE(ws && ws_bytes >= nblk * K * 4, "weight norm: workspace too small (%lld bytes needed)",
+              (long long)(nblk * K * 4));
+  hipLaunchKernelGGL(tap_dot_partial_kernel, dim3((unsigned)nblk), dim3(128), 0, stream, a, b, R, K, ws, TAP_ROWS);
+  hipLaunchKernelGGL(tap_dot_finalize_kernel, dim3((unsigned)cdiv(K, 128)), dim3(128), 0, stream, ws, nblk, K, out);
+  return DPH_OK;
+}
+
 extern "C" int dph_weight_norm_fwd(const float* g, const float* v, int64_t Cout, int64_t Cin_g, int64_t K, int64_t G,
-                                   float* w, float* norm, void* wk, void* wt, hipStream_t stream) {
+                                   float* w, float* norm, void* wk, void* wt, float* ws, int64_t ws_bytes,
+                                   hipStream_t stream) {
   DPH_REQUIRE(g && v && norm && Cout % G == 0 && K <= 4096, "dph_weight_norm_fwd: bad args");
-  // norm doubles as the sum-of-squares accumulator before the sqrt
+  // norm holds the per-tap sum of squares until the final pass takes the sqrt
   float* nsq = norm;
-  hipMemsetAsync(nsq, 0, K * 4, stream);
   const int64_t R = Cout * Cin_g;
-  const int64_t rpb = 64;
-  hipLaunchKernelGGL(tap_dot_kernel, dim3((unsigned)cdiv(R, rpb)), dim3(128), 0, stream, v, v, R, K, nsq, rpb);
+  int rc = tap_dot(v, v, R, K, nsq, ws, ws_bytes, stream);
+  if (rc != DPH_OK) return rc;
   const int64_t n = Cout * Cin_g * K;
-  // apply reads nsq; the sqrt is written back in place by the first K threads AFTER all reads of
-  // that tap?  No: write norms in a separate, final pass to avoid the read/write race.
+  // apply reads nsq; the norms are written in a separate, final pass (no read/write race)
   hipLaunchKernelGGL(weight_norm_apply_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, stream, g, v, nsq,
                      (float*)nullptr, Cout, Cin_g, K, G, w, reinterpret_cast<bf16_t*>(wk),
                      reinterpret_cast<bf16_t*>(wt));
@@ -423,16 +489,15 @@ extern "C" int dph_weight_norm_fwd(const float* g, const float* v, int64_t Cout,
 }
 
 extern "C" int dph_weight_norm_bwd(const float* dw_img, const float* g, const float* v, const float* norm,
-                                   int64_t Cout, int64_t Cin_g, int64_t K, int64_t G, float* dg, float* dv,
-                                   hipStream_t stream) {
+                                   int64_t Cout, int64_t Cin_g, int64_t K, int64_t G, float* dg, float* dv, float* ws,
+                                   int64_t ws_bytes, hipStream_t stream) {
   DPH_REQUIRE(dw_img && g && v && norm && dg && dv && Cout % G == 0, "dph_weight_norm_bwd: bad args");
   const int64_t n = Cout * Cin_g * K;
   // dv doubles as the [Cout][Cin][K] copy of dw, S (K floats) lives in dg until the final pass
   hipLaunchKernelGGL(img_to_weight_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, stream, dw_img, dv, Cout, Cin_g,
                      K, G);
-  hipMemsetAsync(dg, 0, K * 4, stream);
-  const int64_t R = Cout * Cin_g;
-  hipLaunchKernelGGL(tap_dot_kernel, dim3((unsigned)cdiv(R, 64)), dim3(128), 0, stream, dv, v, R, K, dg, (int64_t)64);
+  int rc = tap_dot(dv, v, Cout * Cin_g, K, dg, ws, ws_bytes, stream);
+  if (rc != DPH_OK) return rc;
   // dv_out = (g/n) dw - g S/n^3 v  computed in place (each element reads only its own dv)
   hipLaunchKernelGGL(weight_norm_bwd_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, stream, dv, g, v, norm, dg,
                      n, K, (float*)nullptr, dv);

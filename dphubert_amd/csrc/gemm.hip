@@ -233,8 +233,10 @@ __device__ __forceinline__ void epilogue8(const DphGemmArgs& a, int64_t z, int64
       x = gelu_f(x) * dz * c;
     } else if (a.act == DPH_ACT_GELU_BWD) {
       const float gz = x * dz;
-      ax = gz * gelu_f(aux[i]);
-      x = gz * gelu_grad_f(aux[i]) * c;
+      float g, dg;
+      gelu_and_grad(aux[i], g, dg);
+      ax = gz * g;
+      x = gz * dg * c;
     } else {
       x = x * dz * c;
     }

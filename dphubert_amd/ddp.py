@@ -17,14 +17,24 @@ NCCL).  Design for one 8x MI355X node:
   a scale after SUM on gloo (CPU tests).
 """
 
-from typing import Iterable, List, Optional
+from typing import Iterable, List, Optional, Sequence
 
 import torch
 import torch.distributed as dist
 
 
 class GradReducer:
-    def __init__(self, params: Iterable[torch.nn.Parameter], bucket_mb: float = 64.0, process_group=None):
+    """Flat-bucket gradient all-reduce, launched from gradient-ready notifications.
+
+    ``groups``: tuples of parameters whose gradients must be laid out back-to-back, in the given
+    order (e.g. q/k/v projection weights, produced by one fused weight-gradient GEMM).
+    ``direct``: arm gradient sinks (``p._dph_sink``) so the HIP backward kernels accumulate
+    straight into the bucket storage (ops.GradOut); autograd then never zero-fills or adds those
+    gradients, and the Function notifies readiness through ``p._dph_sink_ready``.
+    """
+
+    def __init__(self, params: Iterable[torch.nn.Parameter], bucket_mb: float = 64.0, process_group=None,
+                 groups: Optional[Sequence[Sequence[torch.nn.Parameter]]] = None, direct: bool = True):
         self.group = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
         ps: List[torch.nn.Parameter] = []
@@ -34,16 +44,30 @@ class GradReducer:
                 seen.add(id(p))
                 ps.append(p)
         ps = list(reversed(ps))        # backward produces gradients roughly in reverse order
-        self.params = ps
+        group_of = {}
+        for gi, grp in enumerate(groups or []):
+            if all(id(p) in seen for p in grp):
+                for p in grp:
+                    group_of[id(p)] = gi
+        units: List[List[torch.nn.Parameter]] = []
+        placed = set()
+        for p in ps:
+            if id(p) in placed:
+                continue
+            unit = list(groups[group_of[id(p)]]) if id(p) in group_of else [p]
+            placed.update(id(q) for q in unit)
+            units.append(unit)
+        self.params = [p for u in units for p in u]
         cap = int(bucket_mb * 1024 * 1024 / 4)
         self.buckets: List[List[torch.nn.Parameter]] = []
         cur, n = [], 0
-        for p in ps:
-            if cur and n + p.numel() > cap:
+        for u in units:
+            un = sum(p.numel() for p in u)
+            if cur and n + un > cap:
                 self.buckets.append(cur)
                 cur, n = [], 0
-            cur.append(p)
-            n += p.numel()
+            cur.extend(u)
+            n += un
         if cur:
             self.buckets.append(cur)
         self.flat = []
@@ -55,16 +79,21 @@ class GradReducer:
             for p in b:
                 self.bucket_of[id(p)] = bi
         self.views = {}
+        self.offsets = {}
         for bi, b in enumerate(self.buckets):
             off = 0
             for p in b:
                 self.views[id(p)] = self.flat[bi][off:off + p.numel()].view_as(p)
+                self.offsets[id(p)] = off
                 off += p.numel()
+        self.direct = direct
         self._pending = [0] * len(self.buckets)
         self._handles = [None] * len(self.buckets)
-        self._hooks = [p.register_post_accumulate_grad_hook(self._hook) for p in ps]
+        self._hooks = [p.register_post_accumulate_grad_hook(self._hook) for p in self.params]
         self.backend = dist.get_backend(process_group) if dist.is_initialized() else None
         self.enabled = self.world > 1
+        self.sync = True
+        self._seen = set()
 
     def prepare(self, zero: bool = True, sync: bool = True):
         """Point every .grad at its bucket view (zeroed when ``zero``) before a backward.
@@ -77,21 +106,28 @@ class GradReducer:
                 f.zero_()
         for p in self.params:
             p.grad = self.views[id(p)]
+            if self.direct:
+                p._dph_sink = (self.flat[self.bucket_of[id(p)]], self.offsets[id(p)], tuple(p.shape))
+                p._dph_sink_ready = self._ready
         self.sync = sync
+        self._seen = set()
         self._pending = [len(b) for b in self.buckets]
         self._handles = [None] * len(self.buckets)
 
     def _hook(self, p):
-        bi = self.bucket_of[id(p)]
-        if not getattr(self, "sync", True):
-            if p.grad.data_ptr() != self.views[id(p)].data_ptr():
-                self.views[id(p)].copy_(p.grad)
-                p.grad = self.views[id(p)]
-            return
+        # also fires (with the bucket view untouched) for a parameter whose Function returned None
+        # after writing through its sink; _ready() counts each parameter once per backward
         if p.grad is not self.views[id(p)] and p.grad.data_ptr() != self.views[id(p)].data_ptr():
             # autograd replaced the grad tensor (e.g. prepare() not called): copy into the bucket
             self.views[id(p)].copy_(p.grad)
             p.grad = self.views[id(p)]
+        self._ready(p)
+
+    def _ready(self, p):
+        if not self.sync or id(p) in self._seen:
+            return
+        self._seen.add(id(p))
+        bi = self.bucket_of[id(p)]
         self._pending[bi] -= 1
         if self._pending[bi] == 0 and self.enabled:
             self._launch(bi)
@@ -120,3 +156,7 @@ class GradReducer:
     def remove(self):
         for h in self._hooks:
             h.remove()
+        for p in self.params:
+            for a in ("_dph_sink", "_dph_sink_ready"):
+                if hasattr(p, a):
+                    delattr(p, a)

@@ -118,6 +118,68 @@ def _zeros(n, like_device, dtype=F32):
     return torch.zeros(n, dtype=dtype, device=like_device)
 
 
+# ---------------------------------------------------------------------------
+# gradient sinks: weight gradients written straight into the data-parallel buckets
+# ---------------------------------------------------------------------------
+def _sink_view(params) -> Optional[torch.Tensor]:
+    """Bucket storage of ``params`` (back-to-back, as one tensor over the concatenated rows) when
+    a GradReducer has armed sinks on all of them, else None (see ddp.GradReducer.prepare)."""
+    sinks = [getattr(p, "_dph_sink", None) if p is not None else None for p in params]
+    if any(s is None for s in sinks):
+        return None
+    flat, off = sinks[0][0], sinks[0][1]
+    n = 0
+    for (f, o, _), p in zip(sinks, params):
+        if f is not flat or o != off + n:
+            return None
+        n += p.numel()
+    rows = sum(p.shape[0] for p in params)
+    return flat[off:off + n].view((rows,) + tuple(params[0].shape[1:]))
+
+
+class GradOut:
+    """Hands out gradient buffers inside a Function's backward.
+
+    ``buf(*params)`` returns ``(tensor, direct)``: with ``direct`` the tensor IS the parameters'
+    bucket storage (kernels must accumulate into it, and autograd gets ``None`` for them, so no
+    zero-fill / AccumulateGrad add ever runs for these gradients); otherwise a fresh fp32 tensor
+    (zero-filled when ``zero``).  ``ret(*params)`` is what backward returns for the same params,
+    and ``done()`` tells the reducer those gradients are complete (stream-ordered).
+    """
+
+    def __init__(self, dev):
+        self.dev = dev
+        self.sunk = set()
+        self.sunk_params = []
+        self.bufs = {}
+
+    def buf(self, *params, zero: bool = True):
+        t = _sink_view(params)
+        direct = t is not None
+        if direct:
+            self.sunk.update(id(p) for p in params)
+            self.sunk_params.extend(params)
+        else:
+            rows = sum(p.shape[0] for p in params)
+            shape = (rows,) + tuple(params[0].shape[1:])
+            t = torch.zeros(shape, dtype=F32, device=self.dev) if zero else torch.empty(shape, dtype=F32,
+                                                                                         device=self.dev)
+        off = 0
+        for p in params:
+            self.bufs[id(p)] = t[off:off + p.shape[0]]
+            off += p.shape[0]
+        return t, direct
+
+    def ret(self, p):
+        if p is None or id(p) in self.sunk:
+            return None
+        return self.bufs.get(id(p))
+
+    def done(self):
+        for p in self.sunk_params:
+            p._dph_sink_ready(p)
+
+
 def _dev(t):
     return t.device
 
@@ -204,7 +266,7 @@ class ExpectedParamsFn(torch.autograd.Function):
         call("dph_expected_params_bwd", ptr(table.ptr_table(las)), ptr(g), ptr(table.offsets), ptr(table.sizes),
              len(las), ptr(table.coef), ptr(table.idx), table.n_terms, ptr(l0), ptr(dout.contiguous()), HC_BIAS, _s())
         grads = []
-        for off, n, la in zip(table.offsets.tolist() if False else _offs(table), table.sizes_list, las):
+        for off, n, la in zip(_offs(table), table.sizes_list, las):
             grads.append(g[off: off + n].view_as(la))
         return (None, *grads)
 
@@ -281,6 +343,7 @@ class FrontendFn(torch.autograd.Function):
             Cin = O
         if need:
             ctx.cfg = cfg
+            ctx.params = (gn_w, gn_b, *ws_)
             ctx.Ls = Ls
             ctx.cms = cms
             ctx.has_mask = [m is not None for m in masks]
@@ -304,7 +367,8 @@ class FrontendFn(torch.autograd.Function):
         B, S = wave.shape
         dev = wave.device
         dy = dy.contiguous()
-        g_w = [None] * n
+        pgn_w, pgn_b, *pws = ctx.params
+        go = GradOut(dev)
         g_m = [None] * n
         # last layer: GELU / (mask*dummy) backward
         O = layers[-1][0]
@@ -326,9 +390,8 @@ class FrontendFn(torch.autograd.Function):
             splits = K.choose_splits(O, k * Cin, M)
             keep.append(K.gemm(A, Bm, K.dense(dwp), O, k * Cin, M, a_kcontig=False, b_kcontig=False,
                                c_dtype=K.OUT_F32, splits=splits, device=dev))
-            dw = torch.empty_like(ws_[i])
-            call("dph_conv_weight_unpack_grad", ptr(dwp), ptr(dw), O, Cin, k, 0, _s())
-            g_w[i] = dw
+            dw, direct = go.buf(pws[i], zero=False)
+            call("dph_conv_weight_unpack_grad", ptr(dwp), ptr(dw), O, Cin, k, int(direct), _s())
             # input gradient columns, then col2im fused with the previous layer's GELU/mask backward
             dcols = torch.empty(M, k * Cin, dtype=BF16, device=dev)
             K.gemm(K.dense(dz), K.dense(ctx.imgs[i]), K.dense(dcols), M, k * Cin, O, a_kcontig=True,
@@ -346,18 +409,18 @@ class FrontendFn(torch.autograd.Function):
             dz = nxt
         # layer 0: conv0 + GroupNorm + GELU + mask, recomputed from the waveform
         C0, k0, s0 = layers[0]
-        dw0 = torch.zeros_like(ws_[0])
-        dgw = torch.zeros(C0, dtype=F32, device=dev)
-        dgb = torch.zeros(C0, dtype=F32, device=dev)
+        dw0, _ = go.buf(pws[0])
+        dgw, _ = go.buf(pgn_w)
+        dgb, _ = go.buf(pgn_b)
         dm0 = torch.zeros(C0, dtype=F32, device=dev) if masks[0] is not None else None
         wsb = torch.empty(B * C0 * 2, dtype=F32, device=dev)
         call("dph_conv0_gn_bwd", ptr(wave), B, S, ptr(ws_[0]), C0, k0, s0, ptr(gn_w), ptr(gn_b), ptr(masks[0]),
              ptr(mean), ptr(rstd), ptr(dz), ptr(dw0), ptr(dgw), ptr(dgb), ptr(dm0), ptr(wsb), wsb.numel() * 4, _s())
-        g_w[0] = dw0
         g_m[0] = dm0
-        grads = [None, None, None, dgw, dgb]
+        go.done()
+        grads = [None, None, None, go.ret(pgn_w), go.ret(pgn_b)]
         for i in range(n):
-            grads += [g_w[i], g_m[i]]
+            grads += [go.ret(pws[i]), g_m[i]]
         return tuple(grads)
 
 
@@ -380,6 +443,7 @@ class FeatureProjectionFn(torch.autograd.Function):
                            len_rows=cfg["T"] if cfg["lengths"] is not None else 0)
         ctx.cfg = cfg
         ctx.seed = seed
+        ctx.params = (ln_w, ln_b, w, b)
         ctx.save_for_backward(x, xn, mu, rs, ln_w, img)
         return out
 
@@ -392,25 +456,33 @@ class FeatureProjectionFn(torch.autograd.Function):
         dev = x.device
         dout = dout.contiguous()
         dpre = torch.empty_like(dout)
-        db = torch.zeros(D, dtype=F32, device=dev)
+        p_lw, p_lb, p_w, p_b = ctx.params
+        go = GradOut(dev)
+        db, _ = go.buf(p_b)
         lens = cfg["lengths"]
         call("dph_branch_bwd", ptr(dout), ptr(dpre), M, D, cfg["p"], ctx.seed, None, ptr(lens),
              cfg["T"] if lens is not None else 0, ptr(db), None, None, _s())
-        dw = torch.empty(D, C, dtype=F32, device=dev)
-        ws = K.linear_wgrad(dpre, xn, dw, accumulate=False)
+        dw, direct = go.buf(p_w, zero=False)
+        ws = K.linear_wgrad(dpre, xn, dw, accumulate=direct)
         dxn = K.linear_dgrad(dpre, img)
         dx = torch.empty_like(x)
-        dlw = torch.zeros(C, dtype=F32, device=dev)
-        dlb = torch.zeros(C, dtype=F32, device=dev)
+        dlw, _ = go.buf(p_lw)
+        dlb, _ = go.buf(p_lb)
         call("dph_layernorm_bwd", ptr(dxn), ptr(x), None, ptr(ln_w), ptr(mu), ptr(rs), ptr(dx), ptr(dlw), ptr(dlb), M,
              C, 0.0, 0, None, 0.0, 0, None, None, None, None, _s())
         del ws
-        return dx, dlw, dlb, dw, db, None
+        go.done()
+        return dx, go.ret(p_lw), go.ret(p_lb), go.ret(p_w), go.ret(p_b), None
 
 
 # ---------------------------------------------------------------------------
 # Positional conv embedding + residual + LayerNorm + dropout (Transformer._preprocess)
 # ---------------------------------------------------------------------------
+def _weight_norm_ws(R: int, K: int, dev):
+    """Workspace of the deterministic per-tap reduction in dph_weight_norm_{fwd,bwd} (64 rows/block)."""
+    return torch.empty(-(-R // 64) * K, dtype=F32, device=dev)
+
+
 class PosConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, wg, wv, bias, ln_w, ln_b, cfg):
@@ -423,7 +495,9 @@ class PosConvFn(torch.autograd.Function):
         norm = torch.empty(Kk, dtype=F32, device=dev)
         wk = torch.empty(G, Cg, Kk * Cg, dtype=BF16, device=dev)
         wt = torch.empty(G, Cg, Kk * Cg, dtype=BF16, device=dev)
-        call("dph_weight_norm_fwd", ptr(wg), ptr(wv), D, Cg, Kk, G, None, ptr(norm), ptr(wk), ptr(wt), _s())
+        wn_ws = _weight_norm_ws(D * Cg, Kk, dev)
+        call("dph_weight_norm_fwd", ptr(wg), ptr(wv), D, Cg, Kk, G, None, ptr(norm), ptr(wk), ptr(wt), ptr(wn_ws),
+             wn_ws.numel() * 4, _s())
         P = Kk // 2
         Q = Kk - 1 - P
         Tp = P + T + Q
@@ -445,6 +519,7 @@ class PosConvFn(torch.autograd.Function):
         if need:
             ctx.cfg = cfg
             ctx.seed = seed
+            ctx.params = (bias, ln_w, ln_b)
             ctx.save_for_backward(x, wg, wv, norm, wt, xg, s0, z, mu, rs, ln_w)
         return h
 
@@ -459,13 +534,15 @@ class PosConvFn(torch.autograd.Function):
         dev = x.device
         dh = dh.contiguous()
         ds0 = torch.empty_like(dh)
-        dlw = torch.zeros(D, dtype=F32, device=dev)
-        dlb = torch.zeros(D, dtype=F32, device=dev)
+        p_bias, p_lw, p_lb = ctx.params
+        go = GradOut(dev)
+        dlw, _ = go.buf(p_lw)
+        dlb, _ = go.buf(p_lb)
         call("dph_layernorm_bwd", ptr(dh), ptr(s0), None, ptr(ln_w), ptr(mu), ptr(rs), ptr(ds0), ptr(dlw), ptr(dlb),
              M, D, cfg["p"], ctx.seed, None, 0.0, 0, None, None, None, None, _s())
         dz = torch.empty_like(ds0)
         call("dph_gelu_mask_bwd", ptr(ds0), ptr(z), None, ptr(dz), None, M, D, _s())
-        db = torch.zeros(D, dtype=F32, device=dev)
+        db, _ = go.buf(p_bias)
         call("dph_colsum", ptr(dz), ptr(db), M, D, _s())
         # input gradient: transposed conv = same batched GEMM over a re-padded dz with flipped weights
         P = Kk // 2
@@ -488,9 +565,12 @@ class PosConvFn(torch.autograd.Function):
                     b_kcontig=False, c_dtype=K.OUT_F32, batch=G, splits=splits, device=dev)
         dg = torch.empty_like(norm)
         dv = torch.empty_like(wv)
-        call("dph_weight_norm_bwd", ptr(dimg), ptr(wg), ptr(wv), ptr(norm), D, Cg, Kk, G, ptr(dg), ptr(dv), _s())
+        wn_ws = _weight_norm_ws(D * Cg, Kk, dev)
+        call("dph_weight_norm_bwd", ptr(dimg), ptr(wg), ptr(wv), ptr(norm), D, Cg, Kk, G, ptr(dg), ptr(dv), ptr(wn_ws),
+             wn_ws.numel() * 4, _s())
         del ws
-        return dx, dg.view_as(wg), dv, db, dlw, dlb, None
+        go.done()
+        return dx, dg.view_as(wg), dv, go.ret(p_bias), go.ret(p_lw), go.ret(p_lb), None
 
 
 # ---------------------------------------------------------------------------
@@ -562,6 +642,8 @@ class EncoderLayerFn(torch.autograd.Function):
         if need:
             ctx.cfg = cfg
             ctx.sv = sv
+            ctx.params = dict(wq=wq, wk=wk, wv=wv, bq=bq, bk=bk, bv=bv, wo=wo, bo=bo, ln1_w=ln1_w, ln1_b=ln1_b, w1=w1,
+                              b1=b1, w2=w2, b2=b2, ln2_w=ln2_w, ln2_b=ln2_b)
             ctx.flags = (use_att, use_ff, hm is not None, lma is not None, im is not None, lmf is not None)
             ctx.save_for_backward(h, s1, mu1, rs1, h1, s2, mu2, rs2, ln1_w, ln2_w, hm, lma, im, lmf)
         return out
@@ -577,46 +659,49 @@ class EncoderLayerFn(torch.autograd.Function):
         dev = h.device
         dout = dout.contiguous()
         z = lambda n: torch.zeros(n, dtype=F32, device=dev)  # noqa: E731
+        pr = ctx.params
+        go = GradOut(dev)
         g = {}
         # ---- LN2 backward (+ FFN branch gradient) ----
         ds2 = torch.empty_like(dout)
-        g["ln2_w"], g["ln2_b"] = z(D), z(D)
+        dln2w, _ = go.buf(pr["ln2_w"])
+        dln2b, _ = go.buf(pr["ln2_b"])
         if use_ff:
             dy = torch.empty_like(dout)
-            g["b2"] = z(D)
+            db2, _ = go.buf(pr["b2"])
             g["lmf"] = z(1) if has_lmf else None
             call("dph_layernorm_bwd", ptr(dout), ptr(s2), None, ptr(ln2_w), ptr(mu2), ptr(rs2), ptr(ds2),
-                 ptr(g["ln2_w"]), ptr(g["ln2_b"]), M, D, 0.0, 0, ptr(dy), cfg["p_drop"], sv["seed_o"], ptr(lmf),
-                 ptr(g["b2"]), ptr(sv["y_pre"]), ptr(g["lmf"]), _s())
+                 ptr(dln2w), ptr(dln2b), M, D, 0.0, 0, ptr(dy), cfg["p_drop"], sv["seed_o"], ptr(lmf), ptr(db2),
+                 ptr(sv["y_pre"]), ptr(g["lmf"]), _s())
             F_ = sv["W1"].shape[0]
-            g["w2"] = torch.empty(D, F_, dtype=F32, device=dev)
-            k1 = K.linear_wgrad(dy, sv["f"], g["w2"], accumulate=False)
-            g["b1"] = z(F_)
+            dw2, direct = go.buf(pr["w2"], zero=False)
+            k1 = K.linear_wgrad(dy, sv["f"], dw2, accumulate=direct)
+            db1, _ = go.buf(pr["b1"])
             g["im"] = z(F_) if has_im else None
-            du = K.linear_dgrad(dy, sv["W2"], act=K.ACT_GELU_BWD, aux_in=sv["u"], colmask=im, colsum_out=g["b1"],
+            du = K.linear_dgrad(dy, sv["W2"], act=K.ACT_GELU_BWD, aux_in=sv["u"], colmask=im, colsum_out=db1,
                                 colsum_aux=g["im"] if has_im else z(F_), dropout_p=cfg["p_interm"],
                                 seed=sv["seed_i"])
-            g["w1"] = torch.empty(F_, D, dtype=F32, device=dev)
-            k2 = K.linear_wgrad(du, h1, g["w1"], accumulate=False)
+            dw1, direct = go.buf(pr["w1"], zero=False)
+            k2 = K.linear_wgrad(du, h1, dw1, accumulate=direct)
             dh1 = K.linear_dgrad(du, sv["W1"], residual=ds2)
             del k1, k2
         else:
             call("dph_layernorm_bwd", ptr(dout), ptr(s2), None, ptr(ln2_w), ptr(mu2), ptr(rs2), ptr(ds2),
-                 ptr(g["ln2_w"]), ptr(g["ln2_b"]), M, D, 0.0, 0, None, 0.0, 0, None, None, None, None, _s())
+                 ptr(dln2w), ptr(dln2b), M, D, 0.0, 0, None, 0.0, 0, None, None, None, None, _s())
             dh1 = ds2
         # ---- LN1 backward (+ attention branch gradient) ----
         ds1 = torch.empty_like(dout)
-        g["ln1_w"], g["ln1_b"] = z(D), z(D)
+        dln1w, _ = go.buf(pr["ln1_w"])
+        dln1b, _ = go.buf(pr["ln1_b"])
         if use_att:
             da = torch.empty_like(dout)
-            g["bo"] = z(D)
+            dbo, _ = go.buf(pr["bo"])
             g["lma"] = z(1) if has_lma else None
             call("dph_layernorm_bwd", ptr(dh1), ptr(s1), None, ptr(ln1_w), ptr(mu1), ptr(rs1), ptr(ds1),
-                 ptr(g["ln1_w"]), ptr(g["ln1_b"]), M, D, 0.0, 0, ptr(da), cfg["p_drop"], sv["seed_d"], ptr(lma),
-                 ptr(g["bo"]), ptr(sv["a_pre"]), ptr(g["lma"]), _s())
-            Dh = sv["Wo"].shape[1]
-            g["wo"] = torch.empty(D, Dh, dtype=F32, device=dev)
-            k3 = K.linear_wgrad(da, sv["o_m"], g["wo"], accumulate=False)
+                 ptr(dln1w), ptr(dln1b), M, D, 0.0, 0, ptr(da), cfg["p_drop"], sv["seed_d"], ptr(lma), ptr(dbo),
+                 ptr(sv["a_pre"]), ptr(g["lma"]), _s())
+            dwo, direct = go.buf(pr["wo"], zero=False)
+            k3 = K.linear_wgrad(da, sv["o_m"], dwo, accumulate=direct)
             do_m = K.linear_dgrad(da, sv["Wo"])
             Dvec = torch.empty(B * H * T, dtype=F32, device=dev)
             g["hm"] = z(H) if has_hm else None
@@ -624,21 +709,21 @@ class EncoderLayerFn(torch.autograd.Function):
             dqkv = torch.empty_like(sv["qkv"])
             call("dph_attention_bwd", ptr(sv["qkv"]), ptr(do_m), ptr(hm), ptr(sv["lse"]), ptr(Dvec), ptr(dqkv),
                  ptr(cfg["lengths"]), B, T, H, cfg["head_dim"] ** -0.5, cfg["p_attn"], sv["seed_a"], _s())
-            dbqkv = z(3 * Dh)
-            call("dph_colsum", ptr(dqkv), ptr(dbqkv), M, 3 * Dh, _s())
-            dWqkv = torch.empty(3 * Dh, D, dtype=F32, device=dev)
-            k4 = K.linear_wgrad(dqkv, h, dWqkv, accumulate=False)
+            dbqkv, _ = go.buf(pr["bq"], pr["bk"], pr["bv"])
+            call("dph_colsum", ptr(dqkv), ptr(dbqkv), M, dqkv.shape[1], _s())
+            dwqkv, direct = go.buf(pr["wq"], pr["wk"], pr["wv"], zero=False)
+            k4 = K.linear_wgrad(dqkv, h, dwqkv, accumulate=direct)
             dh = K.linear_dgrad(dqkv, sv["Wqkv"], residual=ds1)
-            g["wq"], g["wk"], g["wv"] = dWqkv[:Dh], dWqkv[Dh:2 * Dh], dWqkv[2 * Dh:]
-            g["bq"], g["bk"], g["bv"] = dbqkv[:Dh], dbqkv[Dh:2 * Dh], dbqkv[2 * Dh:]
             del k3, k4
         else:
             call("dph_layernorm_bwd", ptr(dh1), ptr(s1), None, ptr(ln1_w), ptr(mu1), ptr(rs1), ptr(ds1),
-                 ptr(g["ln1_w"]), ptr(g["ln1_b"]), M, D, 0.0, 0, None, 0.0, 0, None, None, None, None, _s())
+                 ptr(dln1w), ptr(dln1b), M, D, 0.0, 0, None, 0.0, 0, None, None, None, None, _s())
             dh = ds1
+        go.done()
         order = ["wq", "wk", "wv", "bq", "bk", "bv", "wo", "bo", "ln1_w", "ln1_b", "w1", "b1", "w2", "b2", "ln2_w",
-                 "ln2_b", "hm", "lma", "im", "lmf"]
-        return (None, dh) + tuple(g.get(k) for k in order)
+                 "ln2_b"]
+        return (None, dh) + tuple(go.ret(pr[k]) for k in order) + (g.get("hm"), g.get("lma"), g.get("im"),
+                                                                    g.get("lmf"))
 
 
 # ---------------------------------------------------------------------------
@@ -673,6 +758,7 @@ class DistillProjLossFn(torch.autograd.Function):
         call("dph_distill_loss_fwd", ptr(s), tptrs, B, L, T, Dt, cfg["l2"], cfg["l1"], cfg["cos"],
              int(cfg["cos_type"] == "log_sig"), ptr(rowstats), ptr(partial), ptr(out), _s())
         ctx.cfg = cfg
+        ctx.params = pw
         ctx.save_for_backward(s, rowstats, *sh, *imgs, *th)
         return out[0], out[1], out[2], out[3]
 
@@ -693,8 +779,10 @@ class DistillProjLossFn(torch.autograd.Function):
         dl = dloss.contiguous() if dloss is not None else torch.ones((), dtype=F32, device=dev)
         call("dph_distill_loss_bwd", ptr(s), tptrs, ptr(rowstats), ptr(dl), B, L, T, Dt, cfg["l2"], cfg["l1"],
              cfg["cos"], int(cfg["cos_type"] == "log_sig"), ptr(ds), _s())
-        dW = [torch.zeros(Dt, Ds, dtype=F32, device=dev) for _ in range(P)]
-        db = [torch.zeros(Dt, dtype=F32, device=dev) for _ in range(P)]
+        go = GradOut(dev)
+        pw = ctx.params
+        dW = [go.buf(pw[2 * p])[0] for p in range(P)]
+        db = [go.buf(pw[2 * p + 1])[0] for p in range(P)]
         dh = []
         keep = []
         for l in range(L):
@@ -702,8 +790,9 @@ class DistillProjLossFn(torch.autograd.Function):
             keep.append(K.linear_wgrad(ds[l], sh[l], dW[p], accumulate=True))
             call("dph_colsum", ptr(ds[l]), ptr(db[p]), M, Dt, _s())
             dh.append(K.linear_dgrad(ds[l], imgs[p]))
+        go.done()
         grads = [None] + dh
         for p in range(P):
-            grads += [dW[p], db[p]]
+            grads += [go.ret(pw[2 * p]), go.ret(pw[2 * p + 1])]
         grads += [None] * L
         return tuple(grads)

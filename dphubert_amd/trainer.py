@@ -94,6 +94,18 @@ def build_distill_module(teacher_config: dict, student_config: Optional[dict] = 
                          sparsity_warmup_updates=sparsity_warmup_updates if use_reg else None)
 
 
+def fused_grad_groups(model) -> List[tuple]:
+    """Parameters whose gradients one fused kernel produces together (q/k/v weight and bias
+    gradients come out of a single [3*Dh, D] weight-gradient GEMM / column sum)."""
+    groups = []
+    for layer in model.encoder.transformer.layers:
+        a = layer.attention
+        if a is not None:
+            groups.append((a.q_proj.weight, a.k_proj.weight, a.v_proj.weight))
+            groups.append((a.q_proj.bias, a.k_proj.bias, a.v_proj.bias))
+    return groups
+
+
 class Trainer:
     """One process per GPU; call ``step(batch)`` per optimizer update (accum_grad=1)."""
 
@@ -104,7 +116,7 @@ class Trainer:
         self.optimizer = opt["optimizer"]
         self.scheduler = opt["lr_scheduler"]["scheduler"]
         params = [p for g in self.optimizer.param_groups for p in g["params"]]
-        self.reducer = GradReducer(params, bucket_mb=bucket_mb)
+        self.reducer = GradReducer(params, bucket_mb=bucket_mb, groups=fused_grad_groups(module.student_model))
         self.accum_grad = accum_grad
         self._micro = 0
 

@@ -162,14 +162,16 @@ int dph_gelu_mask_bwd(const void* dy, const void* z_pre, const float* mask, void
 /* pos-conv layout helpers: x [B][T][G*Cg] bf16 -> xg [B][G][pad_front + T + pad_back][Cg] zero-padded */
 int dph_regroup_pad(const void* x, void* xg, int64_t B, int64_t T, int64_t G, int64_t Cg, int64_t pad_front,
                     int64_t pad_back, hipStream_t stream);
-/* weight norm (dim=2): w = g*v/||v||_(dims 0,1), also writes the bf16 GEMM images
+/* weight norm (dim=2): w = g*v/||v||_(dims 0,1) (deterministic reduction: workspace of
+ * ceil(Cout*Cin_g/64)*K floats), also writes the bf16 GEMM images
  * wk [G][Cg_out][K*Cg_in] (k-major: index j*Cg_in+c) and its flipped transpose
  * wt [G][Cg_in][K*Cg_out] (index jj*Cg_out+o, jj=K-1-j) used by the input-gradient GEMM. */
 int dph_weight_norm_fwd(const float* g, const float* v, int64_t Cout, int64_t Cin_g, int64_t K, int64_t G,
-                        float* w, float* norm, void* wk, void* wt, hipStream_t stream);
+                        float* w, float* norm, void* wk, void* wt, float* ws, int64_t ws_bytes, hipStream_t stream);
 /* dW_img [G][Cg_out][K*Cg_in] fp32 (GEMM layout) -> dg [K], dv [Cout][Cin_g][K] */
 int dph_weight_norm_bwd(const float* dw_img, const float* g, const float* v, const float* norm, int64_t Cout,
-                        int64_t Cin_g, int64_t K, int64_t G, float* dg, float* dv, hipStream_t stream);
+                        int64_t Cin_g, int64_t K, int64_t G, float* dg, float* dv, float* ws, int64_t ws_bytes,
+                        hipStream_t stream);
 
 /* ------------------------------------------------------------------------ *
  * Casting / layout helpers for the bf16 GEMM images of fp32 master weights.

@@ -1,0 +1,137 @@
+"""Data-parallel gradient path on CPU (gloo, world_size 2): GradReducer bucketing, fused-group
+layout, direct gradient sinks (ops.GradOut) and gradient accumulation.
+
+The RCCL path on the GPU is the same code with backend "nccl" (ReduceOp.AVG); here the reduction
+is SUM + divide on gloo.  Reference: distill.py:41 (strategy="ddp"), SURVEY 8(e).
+"""
+
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from dphubert_amd.ddp import GradReducer
+from dphubert_amd.ops import GradOut
+
+
+class SinkLinear(torch.autograd.Function):
+    """y = x @ w^T + b whose weight/bias gradients go through GradOut (as the HIP Functions do)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x)
+        ctx.params = (w, b)
+        return x @ w.t() + b
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        w, b = ctx.params
+        go = GradOut(x.device)
+        dw, direct = go.buf(w, zero=False)
+        if direct:
+            dw.add_(dy.t() @ x)
+        else:
+            dw.copy_(dy.t() @ x)
+        db, _ = go.buf(b)
+        db.add_(dy.sum(0))
+        go.done()
+        return dy @ w, go.ret(w), go.ret(b)
+
+
+class Net(torch.nn.Module):
+    def __init__(self, sink: bool):
+        super().__init__()
+        g = torch.Generator().manual_seed(0)
+        self.q = torch.nn.Linear(6, 4)
+        self.k = torch.nn.Linear(6, 4)
+        self.v = torch.nn.Linear(6, 4)
+        self.o = torch.nn.Linear(12, 3)
+        for p in self.parameters():
+            with torch.no_grad():
+                p.copy_(torch.randn(p.shape, generator=g))
+        self.sink = sink
+
+    def lin(self, m, x):
+        return SinkLinear.apply(x, m.weight, m.bias) if self.sink else m(x)
+
+    def forward(self, x):
+        h = torch.cat([self.lin(self.q, x), self.lin(self.k, x), self.lin(self.v, x)], dim=1)
+        return (self.lin(self.o, torch.tanh(h)) ** 2).mean()
+
+    def groups(self):
+        return [(self.q.weight, self.k.weight, self.v.weight), (self.q.bias, self.k.bias, self.v.bias)]
+
+
+def _inputs(rank, micro):
+    g = torch.Generator().manual_seed(100 + 10 * rank + micro)
+    return torch.randn(5, 6, generator=g)
+
+
+def _reference_grads(world, accum):
+    net = Net(sink=False)
+    for r in range(world):
+        for m in range(accum):
+            (net(_inputs(r, m)) / accum).backward()
+    return {n: p.grad / world for n, p in net.named_parameters()}
+
+
+def _worker(rank, world, port, sink, accum, bucket_mb, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        net = Net(sink=sink)
+        red = GradReducer(list(net.parameters()), bucket_mb=bucket_mb, groups=net.groups())
+        for m in range(accum):
+            red.prepare(zero=m == 0, sync=m + 1 == accum)
+            (net(_inputs(rank, m)) / accum).backward()
+        red.finish()
+        # fused groups are laid out back-to-back in one bucket
+        for grp in net.groups():
+            ptrs = [p.grad.data_ptr() for p in grp]
+            sizes = [p.numel() * 4 for p in grp]
+            assert all(ptrs[i] + sizes[i] == ptrs[i + 1] for i in range(len(grp) - 1))
+        q.put((rank, {n: p.grad.detach().numpy().copy() for n, p in net.named_parameters()}))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("sink,accum,bucket_mb", [(False, 1, 64.0), (True, 1, 64.0), (True, 2, 1e-4),
+                                                  (False, 3, 1e-4)])
+def test_grad_reducer_gloo_ws2(sink, accum, bucket_mb):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, sink, accum, bucket_mb, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = _reference_grads(world, accum)
+    for r in range(world):
+        for n, g in want.items():
+            assert torch.allclose(torch.from_numpy(got[r][n]), g, rtol=1e-5, atol=1e-6), (r, n)
+
+
+def test_grad_out_fallback_without_reducer():
+    """No reducer armed: GradOut hands out fresh tensors and autograd accumulates as usual."""
+    net = Net(sink=True)
+    ref = Net(sink=False)
+    x = _inputs(0, 0)
+    net(x).backward()
+    ref(x).backward()
+    for (n, p), (_, r) in zip(net.named_parameters(), ref.named_parameters()):
+        assert torch.allclose(p.grad, r.grad, rtol=1e-5, atol=1e-6), n
