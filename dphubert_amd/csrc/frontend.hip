@@ -342,13 +342,17 @@ __global__ void tap_dot_partial_kernel(const float* __restrict__ a, const float*
   }
 }
 
-__global__ void tap_dot_finalize_kernel(const float* __restrict__ part, int64_t nblk, int64_t K,
-                                        float* __restrict__ out) {
-  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= K) return;
+// one block per tap; fixed strided partition + fixed-shape tree (deterministic)
+__global__ void __launch_bounds__(256) tap_dot_finalize_kernel(const float* __restrict__ part, int64_t nblk,
+                                                               int64_t K, float* __restrict__ out) {
+  __shared__ float red[4];
+  const int64_t j = blockIdx.x;
   float s = 0.f;
-  for (int64_t b = 0; b < nblk; ++b) s += part[b * K + j];
-  out[j] = s;
+  for (int64_t b = threadIdx.x; b < nblk; b += 256) s += part[b * K + j];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) out[j] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
 __global__ void weight_norm_apply_kernel(const float* __restrict__ g, const float* __restrict__ v,
@@ -465,7 +469,7 @@ static int tap_dot(const float* a, const float* b, int64_t R, int64_t K, float* 
   DPH_REQUIRE(ws && ws_bytes >= nblk * K * 4, "weight norm: workspace too small (%lld bytes needed)",
               (long long)(nblk * K * 4));
   hipLaunchKernelGGL(tap_dot_partial_kernel, dim3((unsigned)nblk), dim3(128), 0, stream, a, b, R, K, ws, TAP_ROWS);
-  hipLaunchKernelGGL(tap_dot_finalize_kernel, dim3((unsigned)cdiv(K, 128)), dim3(128), 0, stream, ws, nblk, K, out);
+  hipLaunchKernelGGL(tap_dot_finalize_kernel, dim3((unsigned)K), dim3(256), 0, stream, ws, nblk, K, out);
   return DPH_OK;
 }
 

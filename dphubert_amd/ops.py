@@ -101,6 +101,18 @@ def bf16_image(*ts: torch.Tensor) -> torch.Tensor:
     return out
 
 
+def f32_cat(*ts: torch.Tensor) -> torch.Tensor:
+    """torch.cat of fp32 parameters (e.g. the q/k/v biases), cached like bf16_image."""
+    owner = ts[0]
+    key = ("f32cat",) + _version_key(ts)
+    hit = getattr(owner, "_dph_cat", None)
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    out = torch.cat([t.detach() for t in ts])
+    owner._dph_cat = (key, out)
+    return out
+
+
 def conv_image(w: torch.Tensor) -> torch.Tensor:
     """conv weight [O][C][k] fp32 -> bf16 [O][k*C] (k-major, matches channels-last im2col rows)."""
     key = ("conv",) + _version_key((w,))
@@ -114,8 +126,44 @@ def conv_image(w: torch.Tensor) -> torch.Tensor:
     return out
 
 
+class _ZeroArena:
+    """Zero-filled fp32 slices carved from 4 MB chunks: one fill per chunk instead of one fill
+    kernel per small gradient / accumulator buffer (~100 per step).  Slices are never reused
+    (the offset only grows); a chunk is freed by the caching allocator once every slice is dead."""
+
+    CHUNK = 1 << 20
+
+    def __init__(self):
+        self.buf = None
+        self.off = 0
+
+    def take(self, n: int, dev) -> torch.Tensor:
+        n_al = (n + 63) // 64 * 64
+        if n_al > self.CHUNK // 4:
+            return torch.zeros(n, dtype=F32, device=dev)
+        if self.buf is None or self.off + n_al > self.CHUNK or self.buf.device != torch.device(dev):
+            self.buf = torch.zeros(self.CHUNK, dtype=F32, device=dev)
+            self.off = 0
+        t = self.buf[self.off:self.off + n]
+        self.off += n_al
+        return t
+
+
+_ZEROS = _ZeroArena()
+
+
+def zeros_f32(shape, dev) -> torch.Tensor:
+    """Zero-filled fp32 tensor (small ones come from the arena, no fill kernel of their own)."""
+    if isinstance(shape, int):
+        shape = (shape,)
+    n = 1
+    for d in shape:
+        n *= d
+    return _ZEROS.take(n, dev).view(shape)
+
+
 def _zeros(n, like_device, dtype=F32):
-    return torch.zeros(n, dtype=dtype, device=like_device)
+    return zeros_f32(n, like_device) if dtype == F32 else torch.zeros(n, dtype=dtype, device=like_device)
 
 
 # ---------------------------------------------------------------------------
@@ -162,8 +210,7 @@ class GradOut:
         else:
             rows = sum(p.shape[0] for p in params)
             shape = (rows,) + tuple(params[0].shape[1:])
-            t = torch.zeros(shape, dtype=F32, device=self.dev) if zero else torch.empty(shape, dtype=F32,
-                                                                                         device=self.dev)
+            t = zeros_f32(shape, self.dev) if zero else torch.empty(shape, dtype=F32, device=self.dev)
         off = 0
         for p in params:
             self.bufs[id(p)] = t[off:off + p.shape[0]]
@@ -201,7 +248,7 @@ class HardConcreteFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dmask):
         la, u = ctx.saved_tensors
-        dla = torch.zeros_like(la)
+        dla = zeros_f32(tuple(la.shape), la.device)
         call("dph_hc_sample_bwd", ptr(la), ptr(u), ptr(dmask.contiguous()), ptr(dla), la.numel(), HC_BETA,
              HC_LIMIT_L, HC_LIMIT_R, _s())
         return dla, None
@@ -262,7 +309,7 @@ class ExpectedParamsFn(torch.autograd.Function):
         table = ctx.table
         if not las:
             return (None,)
-        g = torch.zeros(table.total, dtype=F32, device=l0.device)
+        g = zeros_f32(table.total, l0.device)
         call("dph_expected_params_bwd", ptr(table.ptr_table(las)), ptr(g), ptr(table.offsets), ptr(table.sizes),
              len(las), ptr(table.coef), ptr(table.idx), table.n_terms, ptr(l0), ptr(dout.contiguous()), HC_BIAS, _s())
         grads = []
@@ -373,7 +420,7 @@ class FrontendFn(torch.autograd.Function):
         # last layer: GELU / (mask*dummy) backward
         O = layers[-1][0]
         dz = torch.empty_like(dy)
-        dm_raw = torch.zeros(O, dtype=F32, device=dev)
+        dm_raw = zeros_f32(O, dev)
         call("dph_gelu_mask_bwd", ptr(dy), ptr(ctx.zs[-1]), ptr(ctx.cms[-1]), ptr(dz), ptr(dm_raw), B * Ls[-1], O,
              _s())
         if masks[-1] is not None:
@@ -398,10 +445,10 @@ class FrontendFn(torch.autograd.Function):
                    b_kcontig=False)
             nxt = torch.empty(B * Ls[i - 1], Cin, dtype=BF16, device=dev)
             if i > 1:
-                dmk = torch.zeros(Cin, dtype=F32, device=dev) if masks[i - 1] is not None else None
+                dmk = zeros_f32(Cin, dev) if masks[i - 1] is not None else None
                 call("dph_col2im_gelu_bwd", ptr(dcols), B, Ls[i], Ls[i - 1], Cin, k, s, ptr(ctx.zs[i - 1]),
                      ptr(masks[i - 1]), ptr(nxt), ptr(dmk) if dmk is not None else
-                     ptr(torch.zeros(Cin, dtype=F32, device=dev)), _s())
+                     ptr(zeros_f32(Cin, dev)), _s())
                 g_m[i - 1] = dmk
             else:
                 call("dph_col2im_gelu_bwd", ptr(dcols), B, Ls[i], Ls[i - 1], Cin, k, s, None, None, ptr(nxt), None,
@@ -412,7 +459,7 @@ class FrontendFn(torch.autograd.Function):
         dw0, _ = go.buf(pws[0])
         dgw, _ = go.buf(pgn_w)
         dgb, _ = go.buf(pgn_b)
-        dm0 = torch.zeros(C0, dtype=F32, device=dev) if masks[0] is not None else None
+        dm0 = zeros_f32(C0, dev) if masks[0] is not None else None
         wsb = torch.empty(B * C0 * 2, dtype=F32, device=dev)
         call("dph_conv0_gn_bwd", ptr(wave), B, S, ptr(ws_[0]), C0, k0, s0, ptr(gn_w), ptr(gn_b), ptr(masks[0]),
              ptr(mean), ptr(rstd), ptr(dz), ptr(dw0), ptr(dgw), ptr(dgb), ptr(dm0), ptr(wsb), wsb.numel() * 4, _s())
@@ -598,7 +645,7 @@ class EncoderLayerFn(torch.autograd.Function):
         if use_att:
             Dh = wq.shape[0]
             Wqkv = bf16_image(wq, wk, wv)
-            bqkv = torch.cat([bq, bk, bv])
+            bqkv = f32_cat(bq, bk, bv)
             qkv = K.linear_fwd(h, Wqkv, bqkv)
             o_u = torch.empty(M, Dh, dtype=BF16, device=dev)
             o_m = torch.empty(M, Dh, dtype=BF16, device=dev)
@@ -658,7 +705,7 @@ class EncoderLayerFn(torch.autograd.Function):
         M, D = h.shape
         dev = h.device
         dout = dout.contiguous()
-        z = lambda n: torch.zeros(n, dtype=F32, device=dev)  # noqa: E731
+        z = lambda n: zeros_f32(n, dev)  # noqa: E731
         pr = ctx.params
         go = GradOut(dev)
         g = {}
