@@ -15,9 +15,13 @@ Prints ONE JSON line on rank 0.  Launch N > 1 with
 
 import argparse
 import copy
+import csv
 import json
 import os
+import shutil
+import subprocess
 import sys
+import tempfile
 import time
 
 import torch
@@ -63,6 +67,48 @@ def cpu_baseline(batch: int = 1, steps: int = 2, seconds: float = 10.0):
                       f"warm-up, torch CPU {threads} threads"}
 
 
+def pmc_traffic(args):
+    """HBM bytes per launch of every GEMM variant from rocprofv3 PMC counters.
+
+    Two child runs of this script (1 warm-up + 1 step, same workload), one counter per pass
+    (FETCH_SIZE and WRITE_SIZE do not fit one TCC pass), started before this process touches the
+    GPU.  gfx950 corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE is in KiB and reports
+    half the bytes of wide coalesced reads -> bytes = 2 * 1024 * FETCH_SIZE; WRITE_SIZE is exact
+    for 16-B stores -> bytes = 1024 * WRITE_SIZE.  Returns {kernel name: bytes per launch}.
+    """
+    exe = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(exe):
+        raise RuntimeError("rocprofv3 not found")
+    here = os.path.dirname(os.path.abspath(__file__))
+    out = {}
+    with tempfile.TemporaryDirectory(dir="/tmp") as td:
+        for counter, scale in (("FETCH_SIZE", 2 * 1024.0), ("WRITE_SIZE", 1024.0)):
+            d = os.path.join(td, counter)
+            cmd = [exe, "--pmc", counter, "--kernel-include-regex", "gemm_kernel", "-f", "csv", "-d", d, "-o", "run",
+                   "--", sys.executable, os.path.join(here, "bench.py"), "--steps", "1", "--warmup", "1",
+                   "--no-cpu-baseline", "--no-roofline", "--traffic", "off", "--batch", str(args.batch),
+                   "--seconds", str(args.seconds)]
+            env = dict(os.environ, TMPDIR="/tmp")
+            r = subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                               timeout=400)
+            if r.returncode != 0:
+                raise RuntimeError(f"rocprofv3 {counter} pass failed ({r.returncode}): {r.stdout[-400:]!r}")
+            files = [os.path.join(dp, f) for dp, _, fs in os.walk(d) for f in fs
+                     if f.endswith("counter_collection.csv")]
+            if not files:
+                raise RuntimeError(f"rocprofv3 {counter}: no counter_collection.csv")
+            sums = {}
+            for row in csv.DictReader(open(files[0])):
+                if row["Counter_Name"] != counter:
+                    continue
+                v = sums.setdefault(row["Kernel_Name"], [0.0, 0])
+                v[0] += float(row["Counter_Value"]) * scale
+                v[1] += 1
+            for k, (tot, n) in sums.items():
+                out[k] = out.get(k, 0.0) + tot / n
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -72,11 +118,20 @@ def main():
     ap.add_argument("--seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--traffic", choices=["auto", "off"], default="auto",
+                    help="auto: measure per-launch HBM bytes of the GEMMs with rocprofv3 PMC passes (rank 0, N=1)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    traffic, traffic_err = None, None
+    if world == 1 and not args.no_roofline and args.traffic == "auto":
+        # before this process initialises the GPU (the profiled children own it meanwhile)
+        try:
+            traffic = pmc_traffic(args)
+        except Exception as e:  # noqa: BLE001 -- traffic is informational
+            traffic_err = repr(e)[:300]
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local_rank)
@@ -106,9 +161,15 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    # GEMM launches of the LAST timed step are bracketed by HIP events on their launch stream (an
+    # event marker costs ~3 us of GPU time, so bracketing every step would tax the headline number)
+    prof = LaunchProfiler() if (rank == 0 and not args.no_roofline) else None
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
+        if prof is not None and i == args.steps - 1:
+            prof.__enter__()
         loss = trainer.step(batch)
+    t_host = time.perf_counter() - t0          # host enqueue time (GPU may still be running)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -121,6 +182,7 @@ def main():
     ms = dt / args.steps * 1e3
     audio_s = world * args.batch * args.seconds * args.steps
     value = audio_s / dt
+    log(f"host enqueue {t_host / args.steps * 1e3:.2f} ms/step")
     log(f"loss {loss.item():.5f}  step {ms:.2f} ms  {value:.1f} audio-s/s  "
         f"({FLOP_PER_UTT_BASE * args.batch * args.seconds / 10 / (ms / 1e3) / 1e12:.0f} TFLOP/s algorithmic/GPU)")
 
@@ -142,10 +204,10 @@ def main():
                    "utterances_per_gpu": args.batch, "seconds_per_utt": args.seconds,
                    "global_batch_audio_s": world * args.batch * args.seconds, "distill_layers": "0.4,8,12",
                    "parallelism": f"dp{world}"},
+        "peak_hbm_gib": round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 2),
     }
-    if rank == 0 and not args.no_roofline:
-        with LaunchProfiler() as prof:
-            trainer.step(batch)
+    if prof is not None:
+        prof.__exit__(None, None, None)
         summ = prof.summary()
         top = max(summ.items(), key=lambda kv: kv[1]["ms"])
         name, d = top
@@ -154,12 +216,19 @@ def main():
         achieved = flops_per_launch / (avg_ms / 1e3) / 1e12
         all_ms = sum(v["ms"] for v in summ.values())
         all_fl = sum(v["flops"] for v in summ.values())
+        tr = None
+        if traffic:
+            hits = [v for k, v in traffic.items() if name in k]
+            tr = round(hits[0]) if hits else None
         out["roofline"] = {"bound": "mfma", "kernel": name, "achieved": round(achieved, 1),
                            "peak": MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / MFMA_PEAK_TFLOPS, 4),
-                           "traffic": None, "launches_per_step": d["launches"],
+                           "traffic": tr, "traffic_unit": "bytes/launch (HBM, PMC FETCH_SIZE*2 + WRITE_SIZE)",
+                           "launches_per_step": d["launches"],
                            "avg_launch_us": round(avg_ms * 1e3, 2), "flop_per_launch": flops_per_launch,
                            "all_gemm_tflops": round(all_fl / (all_ms / 1e3) / 1e12, 1),
                            "gemm_ms_per_step": round(all_ms, 3)}
+        if traffic_err:
+            out["roofline"]["traffic_error"] = traffic_err
         log(json.dumps({k: v for k, v in summ.items()}))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:

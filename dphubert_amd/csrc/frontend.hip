@@ -18,18 +18,22 @@
 namespace dph {
 namespace {
 
-constexpr int MAXK0 = 10;   // conv0 kernel (512,10,5) of every wav2vec2/HuBERT config
+// conv0 of every wav2vec2 / HuBERT / WavLM config is (512, 10, 5): compile-time taps and stride let
+// each thread keep a sliding window of the waveform in registers (k0 = 2*s0: consecutive rows share
+// half their taps), so a row costs s0 LDS broadcast reads instead of k0.
+constexpr int K0 = 10;
+constexpr int S0 = 5;
+static_assert(K0 == 2 * S0, "sliding window assumes k0 = 2*s0");
 constexpr int STAT_CH = 256;     // time steps per stats chunk
-constexpr int APPLY_ROWS = 64;   // time steps per apply block
+constexpr int APPLY_ROWS = 256;  // time steps per apply block
 constexpr int BWD_ROWS = 512;    // time steps per backward block
 
 struct Conv0 {
   int64_t B, S, C, L0;
-  int k0, s0;
 };
 
-// thread layout shared by the conv0 kernels: TPR threads per time row, CPT channels each,
-// RPP rows in flight per pass (a wave covers whole rows -> the waveform taps are LDS broadcasts)
+// thread layout shared by the conv0 kernels: TPR threads per time row (CPT channels each), RPP
+// thread-rows per block, each owning a CONTIGUOUS range of nper time steps (sliding window)
 template <int CPT>
 struct RowLayout {
   int tpr, rpp;
@@ -39,18 +43,46 @@ struct RowLayout {
   }
 };
 
+__device__ __forceinline__ void win_load(float (&x)[K0], const float* xs, int t) {
+#pragma unroll
+  for (int j = 0; j < K0; ++j) x[j] = xs[t * S0 + j];
+}
+
+// window of row t -> window of row t+1
+__device__ __forceinline__ void win_advance(float (&x)[K0], const float* xs, int t) {
+#pragma unroll
+  for (int j = 0; j < S0; ++j) x[j] = x[j + S0];
+#pragma unroll
+  for (int j = 0; j < S0; ++j) x[S0 + j] = xs[(t + 1) * S0 + S0 + j];
+}
+
 template <int CPT>
-__device__ __forceinline__ void conv_taps(const float (&wr)[CPT][MAXK0], const float* xs, int k0, float (&v)[CPT]) {
+__device__ __forceinline__ void fir(const float (&wr)[CPT][K0], const float (&x)[K0], float (&v)[CPT]) {
 #pragma unroll
-  for (int i = 0; i < CPT; ++i) v[i] = 0.f;
+  for (int i = 0; i < CPT; ++i) {
+    float a = 0.f;
 #pragma unroll
-  for (int j = 0; j < MAXK0; ++j) {
-    if (j < k0) {
-      const float x = xs[j];
-#pragma unroll
-      for (int i = 0; i < CPT; ++i) v[i] = fmaf(wr[i][j], x, v[i]);
-    }
+    for (int j = 0; j < K0; ++j) a = fmaf(wr[i][j], x[j], a);
+    v[i] = a;
   }
+}
+
+template <int CPT>
+__device__ __forceinline__ void load_taps(float (&wr)[CPT][K0], const float* w, int64_t c0, int64_t C, bool active) {
+#pragma unroll
+  for (int i = 0; i < CPT; ++i)
+#pragma unroll
+    for (int j = 0; j < K0; ++j) wr[i][j] = (active && c0 + i < C) ? w[(c0 + i) * K0 + j] : 0.f;
+}
+
+// stage the waveform samples of time steps [t0, t0+nt) in LDS
+__device__ __forceinline__ int stage_wave(float* xs, const float* wave, const Conv0& p, int64_t b, int64_t t0,
+                                          int nt) {
+  const int nsamp = (nt - 1) * S0 + K0;
+  const float* xw = wave + b * p.S + t0 * S0;
+  for (int i = threadIdx.x; i < nsamp; i += blockDim.x) xs[i] = xw[i];
+  __syncthreads();
+  return nsamp;
 }
 
 // Partial statistics per (utterance, chunk of STAT_CH steps, channel): shifted sums around the
@@ -59,40 +91,40 @@ __device__ __forceinline__ void conv_taps(const float (&wr)[CPT][MAXK0], const f
 __global__ void __launch_bounds__(256) conv0_stats_kernel(const float* __restrict__ wave, const float* __restrict__ w,
                                                           Conv0 p, float* __restrict__ ws, int nch) {
   constexpr int CPT = 8;
-  __shared__ float xs[STAT_CH * 8 + MAXK0];
+  __shared__ float xs[STAT_CH * S0 + K0];
   __shared__ float red[256 * CPT * 2];
   const int64_t b = blockIdx.y;
   const int ch = blockIdx.x;
   const int64_t t0 = (int64_t)ch * STAT_CH;
   const int nt = (int)min<int64_t>(STAT_CH, p.L0 - t0);
-  const int nsamp = (nt - 1) * p.s0 + p.k0;
-  const float* xw = wave + b * p.S + t0 * p.s0;
-  for (int i = threadIdx.x; i < nsamp; i += blockDim.x) xs[i] = xw[i];
-  __syncthreads();
+  stage_wave(xs, wave, p, b, t0, nt);
   RowLayout<CPT> L(p.C);
   const int tid = threadIdx.x;
   const bool active = tid < L.tpr * L.rpp;
   const int64_t c0 = active ? (int64_t)(tid % L.tpr) * CPT : 0;
   const int r0 = active ? tid / L.tpr : 0;
-  float wr[CPT][MAXK0];
-#pragma unroll
-  for (int i = 0; i < CPT; ++i)
-#pragma unroll
-    for (int j = 0; j < MAXK0; ++j) wr[i][j] = (active && c0 + i < p.C && j < p.k0) ? w[(c0 + i) * p.k0 + j] : 0.f;
-  float sh[CPT], s1[CPT], s2[CPT];
-  conv_taps<CPT>(wr, xs, p.k0, sh);          // shift = conv value at the chunk's first step
+  float wr[CPT][K0];
+  load_taps<CPT>(wr, w, c0, p.C, active);
+  float x[K0], sh[CPT], s1[CPT], s2[CPT];
+  win_load(x, xs, 0);
+  fir<CPT>(wr, x, sh);          // shift = conv value at the chunk's first step
 #pragma unroll
   for (int i = 0; i < CPT; ++i) s1[i] = s2[i] = 0.f;
-  if (active) {
-    for (int t = r0; t < nt; t += L.rpp) {
+  const int nper = (nt + L.rpp - 1) / L.rpp;
+  const int ta = r0 * nper;
+  const int tb = min(nt, ta + nper);
+  if (active && ta < tb) {
+    win_load(x, xs, ta);
+    for (int t = ta; t < tb; ++t) {
       float v[CPT];
-      conv_taps<CPT>(wr, xs + t * p.s0, p.k0, v);
+      fir<CPT>(wr, x, v);
 #pragma unroll
       for (int i = 0; i < CPT; ++i) {
         const float d = v[i] - sh[i];
         s1[i] += d;
         s2[i] = fmaf(d, d, s2[i]);
       }
+      if (t + 1 < tb) win_advance(x, xs, t);
     }
   }
 #pragma unroll
@@ -151,26 +183,22 @@ __global__ void __launch_bounds__(256) conv0_apply_kernel(const float* __restric
                                                           const float* __restrict__ mean,
                                                           const float* __restrict__ rstd, bf16_t* __restrict__ y) {
   constexpr int CPT = 8;
-  __shared__ float xs[APPLY_ROWS * 8 + MAXK0];
+  __shared__ float xs[APPLY_ROWS * S0 + K0];
   const int64_t b = blockIdx.y;
   const int64_t t0 = (int64_t)blockIdx.x * APPLY_ROWS;
   const int nt = (int)min<int64_t>(APPLY_ROWS, p.L0 - t0);
-  const int nsamp = (nt - 1) * p.s0 + p.k0;
-  const float* xw = wave + b * p.S + t0 * p.s0;
-  for (int i = threadIdx.x; i < nsamp; i += blockDim.x) xs[i] = xw[i];
-  __syncthreads();
+  stage_wave(xs, wave, p, b, t0, nt);
   RowLayout<CPT> L(p.C);
   const int tid = threadIdx.x;
   if (tid >= L.tpr * L.rpp) return;
   const int64_t c0 = (int64_t)(tid % L.tpr) * CPT;
   const int r0 = tid / L.tpr;
-  float wr[CPT][MAXK0], sc[CPT], sh[CPT], mk[CPT];
+  float wr[CPT][K0], sc[CPT], sh[CPT], mk[CPT];
+  load_taps<CPT>(wr, w, c0, p.C, true);
 #pragma unroll
   for (int i = 0; i < CPT; ++i) {
     const int64_t c = c0 + i;
     const bool ok = c < p.C;
-#pragma unroll
-    for (int j = 0; j < MAXK0; ++j) wr[i][j] = (ok && j < p.k0) ? w[c * p.k0 + j] : 0.f;
     if (GN) {
       const float rs = ok ? rstd[b * p.C + c] : 0.f;
       const float g = ok ? gamma[c] : 0.f;
@@ -182,16 +210,23 @@ __global__ void __launch_bounds__(256) conv0_apply_kernel(const float* __restric
     }
     mk[i] = (ok && mask) ? mask[c] : 1.f;
   }
-  for (int t = r0; t < nt; t += L.rpp) {
+  const int nper = (nt + L.rpp - 1) / L.rpp;
+  const int ta = r0 * nper;
+  const int tb = min(nt, ta + nper);
+  if (ta >= tb) return;
+  float x[K0];
+  win_load(x, xs, ta);
+  const bool vec = c0 + 8 <= p.C && p.C % 8 == 0;
+  for (int t = ta; t < tb; ++t) {
     float o[CPT];
-    conv_taps<CPT>(wr, xs + t * p.s0, p.k0, o);
+    fir<CPT>(wr, x, o);
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
       const float v = fmaf(o[i], sc[i], sh[i]);
       o[i] = GN ? gelu_f(v) * mk[i] : v;
     }
     bf16_t* yp = y + ((b * p.L0) + t0 + t) * p.C + c0;
-    if (c0 + 8 <= p.C && p.C % 8 == 0) {
+    if (vec) {
       *reinterpret_cast<uint4*>(yp) = make_uint4(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]), pack2bf(o[4], o[5]),
                                                  pack2bf(o[6], o[7]));
     } else {
@@ -199,12 +234,27 @@ __global__ void __launch_bounds__(256) conv0_apply_kernel(const float* __restric
       for (int i = 0; i < CPT; ++i)
         if (c0 + i < p.C) yp[i] = f2bf(o[i]);
     }
+    if (t + 1 < tb) win_advance(x, xs, t);
+  }
+}
+
+__device__ __forceinline__ void load_dy4(const bf16_t* dyp, int64_t c0, int64_t C, float (&d)[4]) {
+  if (c0 + 4 <= C && (C & 3) == 0) {
+    const uint2 raw = *reinterpret_cast<const uint2*>(dyp);
+    d[0] = __uint_as_float(raw.x << 16);
+    d[1] = __uint_as_float(raw.x & 0xffff0000u);
+    d[2] = __uint_as_float(raw.y << 16);
+    d[3] = __uint_as_float(raw.y & 0xffff0000u);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) d[i] = (c0 + i < C) ? bf2f(dyp[i]) : 0.f;
   }
 }
 
 // Backward pass 1 (PASS=1): per-(b,c) sums A = sum dxh, Bv = sum dxh*xh; per-c dgamma, dbeta, dmask.
 // Backward pass 2 (PASS=2): dconv = rstd*(dxh - A/N - xh*Bv/N); dw[c][j] += sum dconv * x[s0 t + j].
-// 4 channels per thread keeps the tap weights + tap accumulators at ~80 VGPRs.
+// 4 channels per thread keeps the tap weights + tap accumulators at ~80 VGPRs; the next row's dy
+// is loaded one iteration ahead.
 template <int PASS>
 __global__ void __launch_bounds__(256) conv0_gn_bwd_kernel(const float* __restrict__ wave,
                                                            const float* __restrict__ w, Conv0 p,
@@ -217,28 +267,24 @@ __global__ void __launch_bounds__(256) conv0_gn_bwd_kernel(const float* __restri
                                                            float* __restrict__ dw, float* __restrict__ dgamma,
                                                            float* __restrict__ dbeta, float* __restrict__ dmask) {
   constexpr int CPT = 4;
-  __shared__ float xs[BWD_ROWS * 8 + MAXK0];
+  __shared__ float xs[BWD_ROWS * S0 + K0];
   __shared__ float red[256 * CPT];
   const int64_t b = blockIdx.y;
   const int64_t t0 = (int64_t)blockIdx.x * BWD_ROWS;
   const int nt = (int)min<int64_t>(BWD_ROWS, p.L0 - t0);
-  const int nsamp = (nt - 1) * p.s0 + p.k0;
-  const float* xw = wave + b * p.S + t0 * p.s0;
-  for (int i = threadIdx.x; i < nsamp; i += blockDim.x) xs[i] = xw[i];
-  __syncthreads();
+  stage_wave(xs, wave, p, b, t0, nt);
   RowLayout<CPT> L(p.C);
   const int tid = threadIdx.x;
   const bool active = tid < L.tpr * L.rpp;
   const int64_t c0 = active ? (int64_t)(tid % L.tpr) * CPT : 0;
   const int r0 = active ? tid / L.tpr : 0;
   const float invN = 1.0f / (float)p.L0;
-  float wr[CPT][MAXK0], mu[CPT], rs[CPT], ga[CPT], be[CPT], mk[CPT], sA[CPT], sB[CPT];
+  float wr[CPT][K0], mu[CPT], rs[CPT], ga[CPT], be[CPT], mk[CPT], sA[CPT], sB[CPT];
+  load_taps<CPT>(wr, w, c0, p.C, active);
 #pragma unroll
   for (int i = 0; i < CPT; ++i) {
     const int64_t c = c0 + i;
     const bool ok = active && c < p.C;
-#pragma unroll
-    for (int j = 0; j < MAXK0; ++j) wr[i][j] = (ok && j < p.k0) ? w[c * p.k0 + j] : 0.f;
     mu[i] = ok ? mean[b * p.C + c] : 0.f;
     rs[i] = ok ? rstd[b * p.C + c] : 0.f;
     ga[i] = ok ? gamma[c] : 0.f;
@@ -250,27 +296,26 @@ __global__ void __launch_bounds__(256) conv0_gn_bwd_kernel(const float* __restri
       sB[i] = sums[(b * p.C + c) * 2 + 1] * invN;
     }
   }
-  float acc[CPT][MAXK0];   // PASS1: [i][0..4] = A, Bv, dgamma, dbeta, dmask; PASS2: dw taps
+  float acc[CPT][K0];   // PASS1: [i][0..4] = A, Bv, dgamma, dbeta, dmask; PASS2: dw taps
 #pragma unroll
   for (int i = 0; i < CPT; ++i)
 #pragma unroll
-    for (int j = 0; j < MAXK0; ++j) acc[i][j] = 0.f;
-  if (active) {
-    for (int t = r0; t < nt; t += L.rpp) {
-      const bf16_t* dyp = dy + ((b * p.L0) + t0 + t) * p.C + c0;
+    for (int j = 0; j < K0; ++j) acc[i][j] = 0.f;
+  const int nper = (nt + L.rpp - 1) / L.rpp;
+  const int ta = r0 * nper;
+  const int tb = min(nt, ta + nper);
+  if (active && ta < tb) {
+    const bf16_t* dyrow = dy + ((b * p.L0) + t0) * p.C + c0;
+    float x[K0], dn[CPT];
+    win_load(x, xs, ta);
+    load_dy4(dyrow + (int64_t)ta * p.C, c0, p.C, dn);
+    for (int t = ta; t < tb; ++t) {
       float dyv[CPT];
-      if (c0 + CPT <= p.C && p.C % CPT == 0) {
-        const uint2 raw = *reinterpret_cast<const uint2*>(dyp);
-        dyv[0] = __uint_as_float(raw.x << 16);
-        dyv[1] = __uint_as_float(raw.x & 0xffff0000u);
-        dyv[2] = __uint_as_float(raw.y << 16);
-        dyv[3] = __uint_as_float(raw.y & 0xffff0000u);
-      } else {
 #pragma unroll
-        for (int i = 0; i < CPT; ++i) dyv[i] = (c0 + i < p.C) ? bf2f(dyp[i]) : 0.f;
-      }
+      for (int i = 0; i < CPT; ++i) dyv[i] = dn[i];
+      if (t + 1 < tb) load_dy4(dyrow + (int64_t)(t + 1) * p.C, c0, p.C, dn);
       float v[CPT];
-      conv_taps<CPT>(wr, xs + t * p.s0, p.k0, v);
+      fir<CPT>(wr, x, v);
 #pragma unroll
       for (int i = 0; i < CPT; ++i) {
         const float xh = (v[i] - mu[i]) * rs[i];
@@ -288,41 +333,39 @@ __global__ void __launch_bounds__(256) conv0_gn_bwd_kernel(const float* __restri
         } else {
           const float dc = rs[i] * (dxh - sA[i] - xh * sB[i]);
 #pragma unroll
-          for (int j = 0; j < MAXK0; ++j)
-            if (j < p.k0) acc[i][j] = fmaf(dc, xs[t * p.s0 + j], acc[i][j]);
+          for (int j = 0; j < K0; ++j) acc[i][j] = fmaf(dc, x[j], acc[i][j]);
         }
       }
+      if (t + 1 < tb) win_advance(x, xs, t);
     }
   }
   // reduce over the rpp thread-rows sharing the same channels (static acc index: fully unrolled)
-  const int nacc = PASS == 1 ? 5 : p.k0;
+  constexpr int NACC = PASS == 1 ? 5 : K0;
 #pragma unroll
-  for (int a = 0; a < MAXK0; ++a) {
-    if (a < nacc) {
+  for (int a = 0; a < NACC; ++a) {
 #pragma unroll
-      for (int i = 0; i < CPT; ++i) red[tid * CPT + i] = acc[i][a];
-      __syncthreads();
-      if (active && r0 == 0) {
+    for (int i = 0; i < CPT; ++i) red[tid * CPT + i] = acc[i][a];
+    __syncthreads();
+    if (active && r0 == 0) {
 #pragma unroll
-        for (int i = 0; i < CPT; ++i) {
-          float s = 0.f;
-          for (int r = 0; r < L.rpp; ++r) s += red[(r * L.tpr + (tid % L.tpr)) * CPT + i];
-          const int64_t c = c0 + i;
-          if (c < p.C) {
-            if (PASS == 1) {
-              if (a == 0) atomicAdd(sums + (b * p.C + c) * 2 + 0, s);
-              else if (a == 1) atomicAdd(sums + (b * p.C + c) * 2 + 1, s);
-              else if (a == 2 && dgamma) atomicAdd(dgamma + c, s);
-              else if (a == 3 && dbeta) atomicAdd(dbeta + c, s);
-              else if (a == 4 && dmask) atomicAdd(dmask + c, s);
-            } else {
-              atomicAdd(dw + c * p.k0 + a, s);
-            }
+      for (int i = 0; i < CPT; ++i) {
+        float s = 0.f;
+        for (int r = 0; r < L.rpp; ++r) s += red[(r * L.tpr + (tid % L.tpr)) * CPT + i];
+        const int64_t c = c0 + i;
+        if (c < p.C) {
+          if (PASS == 1) {
+            if (a == 0) atomicAdd(sums + (b * p.C + c) * 2 + 0, s);
+            else if (a == 1) atomicAdd(sums + (b * p.C + c) * 2 + 1, s);
+            else if (a == 2 && dgamma) atomicAdd(dgamma + c, s);
+            else if (a == 3 && dbeta) atomicAdd(dbeta + c, s);
+            else if (a == 4 && dmask) atomicAdd(dmask + c, s);
+          } else {
+            atomicAdd(dw + c * K0 + a, s);
           }
         }
       }
-      __syncthreads();
     }
+    __syncthreads();
   }
 }
 
@@ -404,14 +447,12 @@ __global__ void weight_norm_bwd_kernel(const float* __restrict__ dw, const float
 
 using namespace dph;
 
-static Conv0 make_conv0(int64_t B, int64_t S, int64_t C, int64_t k0, int64_t s0) {
+static Conv0 make_conv0(int64_t B, int64_t S, int64_t C) {
   Conv0 p;
   p.B = B;
   p.S = S;
   p.C = C;
-  p.k0 = (int)k0;
-  p.s0 = (int)s0;
-  p.L0 = (S - k0) / s0 + 1;
+  p.L0 = (S - K0) / S0 + 1;
   return p;
 }
 
@@ -419,9 +460,13 @@ extern "C" int dph_conv0_gn_fwd(const float* wave, int64_t B, int64_t S, const f
                                 int64_t s0, const float* gamma, const float* beta, const float* mask, void* y,
                                 float* mean, float* rstd, float* ws, int64_t ws_bytes, hipStream_t stream) {
   DPH_REQUIRE(wave && w && gamma && beta && y && mean && rstd && ws, "dph_conv0_gn_fwd: null pointer");
-  DPH_REQUIRE(k0 >= 1 && k0 <= MAXK0 && s0 >= 1 && s0 <= 8 && S >= k0 && C <= 2048,
-              "dph_conv0_gn_fwd: unsupported k0=%lld s0=%lld C=%lld", (long long)k0, (long long)s0, (long long)C);
-  Conv0 p = make_conv0(B, S, C, k0, s0);
+  if (k0 != K0 || s0 != S0) {
+    set_error("dph_conv0_gn_fwd: conv0 kernel/stride (%lld,%lld) unsupported (only (10,5))", (long long)k0,
+              (long long)s0);
+    return DPH_EUNSUPPORTED;
+  }
+  DPH_REQUIRE(S >= K0 && C <= 2048, "dph_conv0_gn_fwd: unsupported S=%lld C=%lld", (long long)S, (long long)C);
+  Conv0 p = make_conv0(B, S, C);
   const int nch = (int)cdiv(p.L0, STAT_CH);
   DPH_REQUIRE(ws_bytes >= (int64_t)B * nch * C * 2 * 4, "dph_conv0_gn_fwd: workspace too small");
   hipLaunchKernelGGL(conv0_stats_kernel, dim3(nch, (unsigned)B), dim3(256), 0, stream, wave, w, p, ws, nch);
@@ -436,8 +481,13 @@ extern "C" int dph_conv0_gn_fwd(const float* wave, int64_t B, int64_t S, const f
 extern "C" int dph_conv0_fwd(const float* wave, int64_t B, int64_t S, const float* w, const float* bias, int64_t C,
                              int64_t k0, int64_t s0, void* y, hipStream_t stream) {
   DPH_REQUIRE(wave && w && y, "dph_conv0_fwd: null pointer");
-  DPH_REQUIRE(k0 >= 1 && k0 <= MAXK0 && s0 >= 1 && s0 <= 8 && S >= k0 && C <= 2048, "dph_conv0_fwd: unsupported");
-  Conv0 p = make_conv0(B, S, C, k0, s0);
+  if (k0 != K0 || s0 != S0) {
+    set_error("dph_conv0_fwd: conv0 kernel/stride (%lld,%lld) unsupported (only (10,5))", (long long)k0,
+              (long long)s0);
+    return DPH_EUNSUPPORTED;
+  }
+  DPH_REQUIRE(S >= K0 && C <= 2048, "dph_conv0_fwd: unsupported");
+  Conv0 p = make_conv0(B, S, C);
   hipLaunchKernelGGL(conv0_apply_kernel<false>, dim3((unsigned)cdiv(p.L0, APPLY_ROWS), (unsigned)B), dim3(256), 0,
                      stream, wave, w, bias, p, (const float*)nullptr, (const float*)nullptr, (const float*)nullptr,
                      (const float*)nullptr, (const float*)nullptr, reinterpret_cast<bf16_t*>(y));
@@ -449,9 +499,14 @@ extern "C" int dph_conv0_gn_bwd(const float* wave, int64_t B, int64_t S, const f
                                 const float* mean, const float* rstd, const void* dy, float* dw, float* dgamma,
                                 float* dbeta, float* dmask, float* ws, int64_t ws_bytes, hipStream_t stream) {
   DPH_REQUIRE(wave && w && gamma && beta && mean && rstd && dy && dw && ws, "dph_conv0_gn_bwd: null pointer");
-  DPH_REQUIRE(k0 >= 1 && k0 <= MAXK0 && s0 >= 1 && s0 <= 8 && S >= k0 && C <= 2048, "dph_conv0_gn_bwd: unsupported");
+  if (k0 != K0 || s0 != S0) {
+    set_error("dph_conv0_gn_bwd: conv0 kernel/stride (%lld,%lld) unsupported (only (10,5))", (long long)k0,
+              (long long)s0);
+    return DPH_EUNSUPPORTED;
+  }
+  DPH_REQUIRE(S >= K0 && C <= 2048, "dph_conv0_gn_bwd: unsupported");
   DPH_REQUIRE(ws_bytes >= B * C * 2 * 4, "dph_conv0_gn_bwd: workspace too small");
-  Conv0 p = make_conv0(B, S, C, k0, s0);
+  Conv0 p = make_conv0(B, S, C);
   hipMemsetAsync(ws, 0, B * C * 2 * 4, stream);
   dim3 grid((unsigned)cdiv(p.L0, BWD_ROWS), (unsigned)B);
   hipLaunchKernelGGL(conv0_gn_bwd_kernel<1>, grid, dim3(256), 0, stream, wave, w, p, gamma, beta, mask, mean, rstd,
