@@ -1,0 +1,368 @@
+"""Command-line entry points with the reference's flags (distill.py:147-331, final_distill.py:131-287,
+prune.py:76-107, save_final_ckpt.py:8-49).  The repo-root scripts of the same names call these.
+
+Differences from the reference, all in the plumbing around the hot path:
+  * one process per GPU launched by ``torch.distributed.run`` (``--gpus N`` on a single node
+    relaunches this script under it as child processes); the Lightning Trainer is replaced by
+    ``dphubert_amd.trainer.Trainer`` (RCCL all-reduce, clip, fused AdamW, LR schedule);
+  * checkpoints keep Lightning's layout where prune.py / save_final_ckpt.py read it:
+    ``{"state_dict": {"student_model.*", "distill_linear_projs.*", ...}, "global_step", ...}``
+    under ``exp_dir/ckpts/last.ckpt``; every load uses ``weights_only=True``;
+  * ``--synthetic_utterances`` replaces the LibriSpeech feed by seeded 0.1*randn waveforms
+    (no dataset is available offline); otherwise ``--tsv_dir`` manifests of WAV files are read
+    (``dphubert_amd.data``).
+"""
+
+import argparse
+import copy
+import json
+import logging
+import os
+import pathlib
+import subprocess
+import sys
+import time
+
+import torch
+import torch.nn as nn
+
+_LG = logging.getLogger("dphubert_amd")
+
+
+# ---------------------------------------------------------------------------------------------
+# argument parsers (names, defaults and choices of the reference)
+# ---------------------------------------------------------------------------------------------
+def _common_args(p: argparse.ArgumentParser, lr: float, warmup: int, max_updates: int):
+    p.add_argument("--tsv_dir", type=pathlib.Path, default=None, help="Directory with the tsv manifests.")
+    p.add_argument("--train_subset", default="train100", choices=["train100", "train960"], type=str)
+    p.add_argument("--seconds_per_batch", default=87.5, type=float)
+    p.add_argument("--num_workers", default=1, type=int)
+    p.add_argument("--resume_checkpoint", type=pathlib.Path, default=None)
+    p.add_argument("--exp_dir", default=pathlib.Path("./exp"), type=pathlib.Path)
+    p.add_argument("--log_interval", default=50, type=int)
+    p.add_argument("--learning_rate", default=lr, type=float)
+    p.add_argument("--weight_decay", default=0.0, type=float)
+    p.add_argument("--warmup_updates", default=warmup, type=int)
+    p.add_argument("--max_updates", default=max_updates, type=int)
+    p.add_argument("--clip_norm", default=10.0, type=float)
+    p.add_argument("--num_nodes", default=1, type=int)
+    p.add_argument("--gpus", default=4, type=int)
+    p.add_argument("--accum_grad", default=1, type=int)
+    p.add_argument("--precision", default=32, type=int,
+                   help="accepted for compatibility: the HIP path always computes bf16 x bf16 -> fp32")
+    p.add_argument("--teacher_ckpt", default=pathlib.Path("pretrained_ckpts/hubert-base-ls960.pth"), type=pathlib.Path)
+    p.add_argument("--student_ckpt", default=pathlib.Path("pretrained_ckpts/hubert-base-ls960.pth"), type=pathlib.Path)
+    p.add_argument("--distill_layers", default="0.4,8,12", type=str)
+    p.add_argument("--distill_mode", type=str, default="layer2layer", choices=["layer2layer", "predlayer"])
+    p.add_argument("--l2_weight", default=0.0, type=float)
+    p.add_argument("--l1_weight", default=1.0, type=float)
+    p.add_argument("--cos_weight", default=1.0, type=float)
+    p.add_argument("--cos_type", default="raw", type=str, choices=["raw", "log_sig"])
+    # build-specific
+    p.add_argument("--synthetic_utterances", default=0, type=int,
+                   help="train on this many seeded synthetic utterances per GPU per step instead of --tsv_dir")
+    p.add_argument("--synthetic_seconds", default=10.0, type=float)
+    p.add_argument("--save_interval", default=0, type=int, help="also checkpoint every N updates (0: at the end)")
+
+
+def distill_parser():
+    p = argparse.ArgumentParser(description="Joint distillation and pruning of HuBERT (MI355X)")
+    _common_args(p, lr=2e-4, warmup=15000, max_updates=50000)
+    p.add_argument("--pruning_units", default="conv,head,interm,attlayer,ffnlayer", type=str)
+    p.add_argument("--reg_learning_rate", default=0.02, type=float)
+    p.add_argument("--target_sparsity", default=0.75, type=float)
+    p.add_argument("--sparsity_warmup_updates", default=5000, type=int)
+    return p
+
+
+def final_distill_parser():
+    p = argparse.ArgumentParser(description="Final distillation of a pruned student (MI355X)")
+    _common_args(p, lr=1e-4, warmup=5000, max_updates=25000)
+    return p
+
+
+# ---------------------------------------------------------------------------------------------
+# launch helpers
+# ---------------------------------------------------------------------------------------------
+def _maybe_relaunch(args, argv):
+    """Single node, --gpus N > 1, not yet under torch.distributed.run: start it as a child process
+    (never exec: nothing has touched the GPU yet, and the parent only waits)."""
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        if args.num_nodes != 1:
+            raise SystemExit("multi-node: launch with torch.distributed.run on every node")
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+               "--master-addr", "127.0.0.1", "--master-port", os.environ.get("MASTER_PORT", "29531"),
+               sys.argv[0]] + list(argv)
+        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+        raise SystemExit(subprocess.call(cmd, env=env))
+
+
+def _init_dist():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if not torch.cuda.is_available():
+        raise SystemExit("the distill step runs on the GPU only (no CPU path)")
+    torch.cuda.set_device(local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank, torch.device("cuda", local)
+
+
+def _load(path):
+    return torch.load(path, map_location="cpu", weights_only=True)
+
+
+def _split_groups(distill_layers: str):
+    groups = [[int(x) for x in g.split(",")] for g in distill_layers.split(".")]
+    return groups, [l for g in groups for l in g]
+
+
+def _projections(groups, d_s, d_t, identity: bool):
+    projs = nn.ModuleList()
+    for g in groups:
+        lin = nn.Linear(d_s, d_t)
+        if identity:     # distill.py:24-26
+            with torch.no_grad():
+                lin.weight.copy_(torch.eye(len(lin.weight)))
+                lin.bias.fill_(0)
+        for _ in g:
+            projs.append(lin)
+    return projs
+
+
+def _batches(args, rank, world, dev):
+    """Yields (waveforms, lengths) on the device, forever."""
+    if args.synthetic_utterances > 0:
+        from .synthetic import synthetic_batch
+        step = 0
+        while True:
+            w, ln = synthetic_batch(args.synthetic_utterances, int(args.synthetic_seconds * 16000),
+                                    seed=2022 + 7919 * step + rank)
+            yield w.to(dev, non_blocking=True), ln.to(dev, non_blocking=True)
+            step += 1
+    if args.tsv_dir is None:
+        raise SystemExit("--tsv_dir is required (or --synthetic_utterances N)")
+    from .data import train_loader
+    epoch = 0
+    while True:
+        for w, ln in train_loader(args.tsv_dir, args.train_subset, args.seconds_per_batch, args.num_workers,
+                                  seed=epoch, rank=rank, world=world):
+            yield w.to(dev, non_blocking=True), ln.to(dev, non_blocking=True)
+        epoch += 1
+
+
+def _train(args, module, world, rank, dev):
+    from .trainer import Trainer
+    torch.manual_seed(2022)            # pl.seed_everything(2022)
+    from . import ops
+    ops.manual_seed(2022 + rank)
+    module = module.to(dev)
+    trainer = Trainer(module, clip_norm=args.clip_norm, accum_grad=args.accum_grad)
+    ckpt_dir = args.exp_dir / "ckpts"
+    if args.resume_checkpoint is not None:
+        ck = _load(args.resume_checkpoint)
+        module.load_state_dict(ck["state_dict"], strict=False)
+        if "optimizer" in ck:
+            trainer.optimizer.load_state_dict(ck["optimizer"])
+        module.global_step = int(ck.get("global_step", 0))
+        for _ in range(module.global_step):
+            trainer.scheduler.step()
+    if rank == 0:
+        ckpt_dir.mkdir(parents=True, exist_ok=True)
+    log_f = open(args.exp_dir / "log.jsonl", "a") if rank == 0 else None
+    feed = _batches(args, rank, world, dev)
+    t0 = time.time()
+    audio = 0.0
+    while module.global_step < args.max_updates:
+        for _ in range(args.accum_grad):
+            batch = next(feed)
+            audio += batch[0].shape[0] * batch[0].shape[1] / 16000.0
+            loss = trainer.step(batch)
+        gs = module.global_step
+        if rank == 0 and (gs % args.log_interval == 0 or gs == args.max_updates):
+            rec = {"step": gs, "audio_s_per_s": round(audio * world / max(time.time() - t0, 1e-9), 1),
+                   "lr": trainer.scheduler.get_last_lr()[0]}
+            rec.update({k: float(v) for k, v in module.logged.items()})
+            line = json.dumps(rec)
+            print(line, flush=True)
+            log_f.write(line + "\n")
+            log_f.flush()
+        if rank == 0 and args.save_interval and gs % args.save_interval == 0:
+            _save(module, trainer, ckpt_dir / f"step{gs}.ckpt")
+    if rank == 0:
+        _save(module, trainer, ckpt_dir / "last.ckpt")
+        log_f.close()
+    return module
+
+
+def _save(module, trainer, path):
+    sd = {k: v.detach().cpu() for k, v in module.state_dict().items()}
+    torch.save({"state_dict": sd, "global_step": module.global_step,
+                "optimizer": trainer.optimizer.state_dict()}, path)
+    _LG.info("saved %s", path)
+
+
+def _init_logger(rank):
+    logging.basicConfig(format="%(asctime)s - %(levelname)s - %(name)s - %(message)s", datefmt="%Y-%m-%d %H:%M:%S",
+                        level=logging.INFO if rank == 0 else logging.WARN)
+
+
+# ---------------------------------------------------------------------------------------------
+# distill.py
+# ---------------------------------------------------------------------------------------------
+def distill_main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = distill_parser().parse_args(argv)
+    _maybe_relaunch(args, argv)
+    world, rank, dev = _init_dist()
+    _init_logger(rank)
+    from .lightning import DistillLoss, DistillModule
+    from .trainer import units_flags
+    from .wav2vec2.model import wav2vec2_model
+    tck = _load(args.teacher_ckpt)
+    teacher = wav2vec2_model(**tck["config"])
+    res = teacher.load_state_dict(tck["state_dict"], strict=False)
+    _LG.info("teacher: missing %s, unexpected %s", res.missing_keys, res.unexpected_keys)
+    for p in teacher.parameters():
+        p.requires_grad = False
+    teacher.eval()
+    sck = _load(args.student_ckpt)
+    scfg = dict(sck["config"])
+    scfg.update(units_flags(args.pruning_units))
+    student = wav2vec2_model(**scfg)
+    res = student.load_state_dict(sck["state_dict"], strict=False)
+    _LG.info("student: missing %s, unexpected %s", res.missing_keys, res.unexpected_keys)
+    groups, layers = _split_groups(args.distill_layers)
+    if args.distill_mode != "layer2layer":
+        raise NotImplementedError("predlayer distill mode is not on the HIP path")
+    projs = _projections(groups, student.encoder.feature_projection.projection.out_features,
+                         teacher.encoder.feature_projection.projection.out_features, identity=True)
+    module = DistillModule(teacher_model=teacher, student_model=student, distill_mode=args.distill_mode,
+                           distill_layers=layers, distill_linear_projs=projs,
+                           distill_loss=DistillLoss(args.l2_weight, args.l1_weight, args.cos_weight, args.cos_type),
+                           learning_rate=args.learning_rate, weight_decay=args.weight_decay,
+                           warmup_updates=args.warmup_updates, max_updates=args.max_updates, use_reg=True,
+                           reg_learning_rate=args.reg_learning_rate, target_sparsity=args.target_sparsity,
+                           sparsity_warmup_updates=args.sparsity_warmup_updates, tsv_dir=args.tsv_dir or ".",
+                           train_subset=args.train_subset, seconds_per_batch=args.seconds_per_batch,
+                           num_workers=args.num_workers)
+    _train(args, module, world, rank, dev)
+
+
+# ---------------------------------------------------------------------------------------------
+# final_distill.py
+# ---------------------------------------------------------------------------------------------
+def final_distill_main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = final_distill_parser().parse_args(argv)
+    _maybe_relaunch(args, argv)
+    world, rank, dev = _init_dist()
+    _init_logger(rank)
+    from .lightning import DistillLoss, DistillModule
+    from .wav2vec2.model import wav2vec2_model
+    tck = _load(args.teacher_ckpt)
+    teacher = wav2vec2_model(**tck["config"])
+    teacher.load_state_dict(tck["state_dict"], strict=False)
+    for p in teacher.parameters():
+        p.requires_grad = False
+    teacher.eval()
+    sck = _load(args.student_ckpt)
+    student = wav2vec2_model(**sck["config"])
+    student.load_state_dict(sck["state_dict"], strict=False)
+    groups, layers = _split_groups(args.distill_layers)
+    if args.distill_mode != "layer2layer":
+        raise NotImplementedError("predlayer distill mode is not on the HIP path")
+    projs = _projections(groups, student.encoder.feature_projection.projection.out_features,
+                         teacher.encoder.feature_projection.projection.out_features, identity=False)
+    projs.load_state_dict(sck["distill_linear_projs"])
+    module = DistillModule(teacher_model=teacher, student_model=student, distill_mode=args.distill_mode,
+                           distill_layers=layers, distill_linear_projs=projs,
+                           distill_loss=DistillLoss(args.l2_weight, args.l1_weight, args.cos_weight, args.cos_type),
+                           learning_rate=args.learning_rate, weight_decay=args.weight_decay,
+                           warmup_updates=args.warmup_updates, max_updates=args.max_updates, use_reg=False,
+                           reg_learning_rate=None, target_sparsity=None, sparsity_warmup_updates=None)
+    _train(args, module, world, rank, dev)
+
+
+# ---------------------------------------------------------------------------------------------
+# prune.py / save_final_ckpt.py
+# ---------------------------------------------------------------------------------------------
+def _sub_state(state_dict, prefix):
+    return {k[len(prefix):]: v for k, v in state_dict.items() if k.startswith(prefix)}
+
+
+def prune_from_ckpt(distilled_ckpt, original_ckpt):
+    """prune.py:13-73: rebuild the student from the distilled checkpoint, run prune(), return the
+    pruned {"state_dict", "config", "distill_linear_projs"}."""
+    from .wav2vec2.model import wav2vec2_model
+    ck = _load(distilled_ckpt)
+    ssd = _sub_state(ck["state_dict"], "student_model.")
+    psd = _sub_state(ck["state_dict"], "distill_linear_projs.")
+    config = dict(_load(original_ckpt)["config"])
+    probe = {
+        "extractor_prune_conv_channels": "feature_extractor.conv_layers.0.hard_concrete.log_alpha",
+        "encoder_prune_attention_heads": "encoder.transformer.layers.0.attention.hard_concrete_for_heads.log_alpha",
+        "encoder_prune_attention_layer": "encoder.transformer.layers.0.attention.hard_concrete_for_layer.log_alpha",
+        "encoder_prune_feed_forward_intermediate":
+            "encoder.transformer.layers.0.feed_forward.hard_concrete_for_intermediate.log_alpha",
+        "encoder_prune_feed_forward_layer": "encoder.transformer.layers.0.feed_forward.hard_concrete_for_layer.log_alpha",
+    }
+    config.update({flag: key in ssd for flag, key in probe.items()})
+    model = wav2vec2_model(**config)
+    model.load_state_dict(ssd, strict=True)
+    pruned_config = prune_config(model, config)
+    print(json.dumps(pruned_config, indent=4))
+    return {"state_dict": model.state_dict(), "config": pruned_config, "distill_linear_projs": psd}
+
+
+def prune_config(model, config):
+    """Call model.prune() (in place) and return the config of the pruned architecture."""
+    model.eval()
+    conv_config, use_attention, use_feed_forward, num_heads, remaining_heads, ff_interm = model.prune()
+    pruned = copy.deepcopy(config)
+    if len(num_heads) == 0:
+        pruned["encoder_remaining_heads"] = remaining_heads
+    else:
+        pruned["encoder_num_heads"] = num_heads
+    pruned.update({"extractor_conv_layer_config": conv_config, "encoder_use_attention": use_attention,
+                   "encoder_use_feed_forward": use_feed_forward, "encoder_ff_interm_features": ff_interm,
+                   "extractor_prune_conv_channels": False, "encoder_prune_attention_heads": False,
+                   "encoder_prune_attention_layer": False, "encoder_prune_feed_forward_intermediate": False,
+                   "encoder_prune_feed_forward_layer": False})
+    return pruned
+
+
+def load_pruned_model(ckpt_path):
+    from .wav2vec2.model import wav2vec2_model
+    ck = _load(ckpt_path)
+    model = wav2vec2_model(**ck["config"])
+    model.load_state_dict(ck["state_dict"], strict=True)
+    return model
+
+
+def prune_main(argv=None):
+    p = argparse.ArgumentParser(description="Prune and save distilled model.")
+    p.add_argument("--distilled_ckpt", type=pathlib.Path)
+    p.add_argument("--original_ckpt", type=pathlib.Path)
+    args = p.parse_args(argv)
+    out = args.distilled_ckpt.parent / "pruned_hubert_base.pth"
+    torch.save(prune_from_ckpt(args.distilled_ckpt, args.original_ckpt), out)
+    load_pruned_model(out)
+    print(f"Successfully saved pruned model weights and config to: {out}")
+
+
+def save_final_ckpt_main(argv=None):
+    p = argparse.ArgumentParser(description="Save ckpt and config after final distill.")
+    p.add_argument("--config_path", type=pathlib.Path)
+    p.add_argument("--ckpt_after_final_distill", type=pathlib.Path)
+    args = p.parse_args(argv)
+    config = _load(args.config_path)["config"]
+    print(json.dumps(config, indent=4))
+    ck = _load(args.ckpt_after_final_distill)
+    out = args.ckpt_after_final_distill.parent / "pruned_hubert_base.pth"
+    torch.save({"state_dict": _sub_state(ck["state_dict"], "student_model."), "config": config,
+                "distill_linear_projs": _sub_state(ck["state_dict"], "distill_linear_projs.")}, out)
+    load_pruned_model(out)
+    print(f"Successfully saved pruned model weights and config to: {out}")

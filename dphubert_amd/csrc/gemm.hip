@@ -11,9 +11,11 @@
 // 64x64 output tile = 4x4 v_mfma_f32_16x16x32_bf16 accumulators.  Both
 // operands are staged global -> registers -> LDS with a double-buffered LDS
 // ring and ONE barrier per K-step.  Operand layouts:
-//   k-contiguous  ([rows][K]): LDS image [128][64+8] (16-B row pad, conflict
-//                 free for the 16-lane ds_read_b128 groups), fragments by
-//                 ds_read_b128.
+//   k-contiguous  ([rows][K]): LDS image [128][64], 16-B chunk p of row r holds
+//                 k-chunk p ^ ((r>>1)&7) (conflict free for the 16-lane
+//                 ds_read_b128 groups and the 2-row ds_write_b128 groups; the
+//                 padded [128][72] image measured 33 % bank-conflict cycles),
+//                 fragments by ds_read_b128.
 //   mn-contiguous ([K][rows]): LDS image [64][128] with a 32-B XOR swizzle
 //                 (unit ^= (k&3)|((k>>3)&1)<<2, conflict free for the two
 //                 8-row halves of a transposed read), fragments by the gfx950
@@ -26,6 +28,8 @@
 
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
 
 namespace dph {
 
@@ -37,8 +41,7 @@ constexpr int NTHREADS = 256;                 // 4 waves: 2 (M) x 2 (N), each a 
 constexpr int CHUNKS = (128 * BK / 8) / NTHREADS;   // 16-B chunks per thread per operand tile
 constexpr int WTN = 64;                       // wave tile width (N)
 constexpr int NJ = WTN / 16;                  // accumulator tiles per wave along N
-constexpr int KROW = BK + 8;                  // k-contig LDS row (elements)
-constexpr int LDS_KC = 128 * KROW * 2;        // bytes, k-contig tile
+constexpr int LDS_KC = 128 * BK * 2;          // bytes, k-contig tile [128][64], 16-B chunk XOR swizzle
 constexpr int LDS_MN = BK * 128 * 2;          // bytes, mn-contig tile
 
 template <bool KC>
@@ -108,7 +111,7 @@ struct Stager {
       int byte;
       bool ok;
       if constexpr (KC) {
-        byte = ((c >> 3) * KROW + (c & 7) * 8) * 2;
+        byte = (c >> 3) * 128 + (((c & 7) ^ (((c >> 3) >> 1) & 7)) * 16);
         ok = rvalid[i] && (k0 + (c & 7) * 8 < kend);
       } else {
         int kr = c >> 4;
@@ -128,9 +131,9 @@ struct Stager {
 template <bool KC>
 __device__ __forceinline__ bf16x8_t frag(const char* lds, int rb, int ks, int lane) {
   if constexpr (KC) {
-    int row = rb + (lane & 15);
-    int col = ks * 32 + 8 * (lane >> 4);
-    return *reinterpret_cast<const bf16x8_t*>(lds + (row * KROW + col) * 2);
+    const int row = rb + (lane & 15);
+    const int phys = (ks * 4 + (lane >> 4)) ^ ((row >> 1) & 7);
+    return *reinterpret_cast<const bf16x8_t*>(lds + row * 128 + phys * 16);
   } else {
     const int g = lane >> 4;
     const int i = lane & 15;
@@ -468,6 +471,313 @@ __global__ void __launch_bounds__(NTHREADS, 2) gemm_kernel(const DphGemmArgs a, 
   }
 }
 
+// =============================================================================================
+// LDS-DMA ring kernels (both operands k-contiguous, K % 32 == 0), one template, two shapes:
+//   RingCfg<256,256,128,64>: 256x256 tile, 8 waves (2 M x 4 N) of 128x64, one block per CU;
+//   RingCfg<128,128,64,64>:  128x128 tile, 4 waves (2 x 2) of 64x64, two blocks per CU.
+//
+// Staging: a ring of 4 LDS slots, each one 32-deep k-slice of both operands ([rows][32 k] bf16),
+// filled by the LDS-DMA (global_load_lds_dwordx4: no VGPR round trip, no ds_write, which at
+// ~79 B/clk/CU would cost more LDS time than the ds_read_b128 fragment reads at 256 B/clk).
+// k-slice i+4 is issued into slot i%4 as soon as slice i is in registers, so three slices (96 k)
+// are always in flight behind the one being multiplied; waits are counted (`s_waitcnt vmcnt(8)`:
+// 2 slices x 4 DMA per thread may stay pending) behind a raw s_barrier -- never vmcnt(0) in the
+// loop.  Within a wave, the fragments of slice i+1 are read while the MFMAs of slice i run (two
+// fragment register sets).  One barrier per slice certifies both that slice i+1 landed for every
+// wave (RAW) and that every wave finished reading the slot being restaged (WAR).
+//
+// LDS image of an operand slice: 64-B rows; 16-B chunk p of row r holds logical k-chunk
+// p ^ swz_chunk(r), conflict free for the real ds_read_b128 lane groups (each 16-lane group spans
+// 16 rows and two k-chunks; the naive (r>>2)&3 measured 50 % bank-conflict cycles).  The swizzle
+// is applied on the DMA SOURCE address since an LDS-DMA writes its 1 KB lane-linearly.
+// =============================================================================================
+namespace ring {
+constexpr int KS = 32;      // k per slice
+constexpr int NSLOT = 4;
+
+// found by exhaustive search over 2-bit XOR swizzles of the row bits
+__device__ __forceinline__ int swz_chunk(int r) { return ((r & 1) * 3) ^ (((r >> 2) & 1) << 1); }
+
+__device__ __forceinline__ void dma16(const bf16_t* src, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+
+// MFMA operand fragment: rows rb..rb+15 of a [rows][32] slice image; lane l gets
+// X[rb + (l&15)][k = 8*(l>>4) .. +7]
+__device__ __forceinline__ bf16x8_t frag(const char* lds, int rb, int lane) {
+  const int row = rb + (lane & 15);
+  const int phys = (lane >> 4) ^ swz_chunk(row);
+  return *reinterpret_cast<const bf16x8_t*>(lds + row * 64 + phys * 16);
+}
+
+template <int BM_, int BN_, int WTM_, int WTN_>
+struct Cfg {
+  static constexpr int BM = BM_, BN = BN_, WTM = WTM_, WTN = WTN_;
+  static constexpr int WGM = BM / WTM, WGN = BN / WTN;     // wave grid
+  static constexpr int NW = WGM * WGN;
+  static constexpr int NT = 64 * NW;
+  static constexpr int FM = WTM / 16, FN = WTN / 16;       // accumulator tiles per wave
+  static constexpr int HALF_A = BM * KS * 2, HALF_B = BN * KS * 2;
+  static constexpr int SLOT = HALF_A + HALF_B;
+  static constexpr int PIPE = NSLOT * SLOT;
+  static constexpr int DMA_A = BM * 64 / (NT * 16);          // DMA instructions per thread per slice
+  static constexpr int DMA_B = BN * 64 / (NT * 16);
+  static_assert(DMA_A + DMA_B == 4, "vmcnt counts assume 4 DMA per thread per slice");
+  static constexpr int EROWS = BM > 128 ? 128 : BM;          // epilogue staging rows per pass
+  static constexpr int CROW = BN + 4;
+  static constexpr int EPI = EROWS * CROW * 4;
+  static constexpr int LDS = PIPE > EPI ? PIPE : EPI;
+  static constexpr int MINB = NW >= 8 ? 1 : 2;               // blocks per CU
+};
+using Big = Cfg<256, 256, 128, 64>;
+using Mid = Cfg<128, 128, 64, 64>;
+
+template <class C>
+struct Frags {
+  bf16x8_t a[C::FM];
+  bf16x8_t b[C::FN];
+};
+
+template <class C>
+__device__ __forceinline__ void read_frags(Frags<C>& f, const char* slot, int wr, int wc, int lane) {
+#pragma unroll
+  for (int j = 0; j < C::FN; ++j) f.b[j] = frag(slot + C::HALF_A, wc * C::WTN + 16 * j, lane);
+#pragma unroll
+  for (int i = 0; i < C::FM; ++i) f.a[i] = frag(slot, wr * C::WTM + 16 * i, lane);
+}
+
+template <class C>
+__device__ __forceinline__ void mfma_slice(f32x4_t (&acc)[C::FM][C::FN], const Frags<C>& f) {
+#pragma unroll
+  for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+    for (int j = 0; j < C::FN; ++j)
+      acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.b[j], f.a[i], acc[i][j], 0, 0, 0);
+}
+}  // namespace ring
+
+template <class C>
+__global__ void __launch_bounds__(C::NT, C::MINB) ring_gemm_kernel(const DphGemmArgs a, int64_t kchunk) {
+  __shared__ __attribute__((aligned(1024))) char smem[C::LDS];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wr = wave / C::WGN;
+  const int wc = wave % C::WGN;
+
+  const int64_t zz = blockIdx.z;
+  const int64_t split = zz % a.splits;
+  const int64_t z = zz / a.splits;
+  int64_t tm, tn;
+  {
+    const int64_t ntm = gridDim.y, ntn = gridDim.x;
+    const int64_t nt = ntm * ntn;
+    const int64_t bid = (int64_t)blockIdx.y * ntn + blockIdx.x;
+    const int64_t q = nt / 8, r = nt % 8;
+    const int64_t xcd = bid % 8, loc = bid / 8;
+    const int64_t t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+    constexpr int64_t GM = C::BM > 128 ? 4 : 8;
+    const int64_t gsz = GM * ntn;
+    const int64_t grp = t / gsz;
+    const int64_t gm0 = grp * GM;
+    const int64_t gh = min(GM, ntm - gm0);
+    const int64_t l = t % gsz;
+    tm = gm0 + l % gh;
+    tn = l / gh;
+  }
+  const int64_t m0 = tm * C::BM;
+  const int64_t n0 = tn * C::BN;
+  const int64_t kbeg = split * kchunk;
+  const int64_t kend = min(a.K, kbeg + kchunk);
+  const int H = (int)(max<int64_t>(kend - kbeg, 0) / ring::KS);   // k-slices
+
+  // DMA sources: instruction j of wave w covers slice rows (j*NW+w)*16 .. +16; this lane loads
+  // row r = (j*NW+w)*16 + lane/4 into physical chunk lane%4 <- logical chunk (lane%4) ^ swz(r)
+  const bf16_t* Ab = reinterpret_cast<const bf16_t*>(a.A.ptr) + z_addr(a.A, z);
+  const bf16_t* Bb = reinterpret_cast<const bf16_t*>(a.B.ptr) + z_addr(a.B, z);
+  int64_t aoff[C::DMA_A], boff[C::DMA_B];
+#pragma unroll
+  for (int j = 0; j < C::DMA_A; ++j) {
+    const int r = (j * C::NW + wave) * 16 + (lane >> 2);
+    aoff[j] = row_addr(a.A, min(m0 + r, a.M - 1)) + ((lane & 3) ^ ring::swz_chunk(r)) * 8 + kbeg;
+  }
+#pragma unroll
+  for (int j = 0; j < C::DMA_B; ++j) {
+    const int r = (j * C::NW + wave) * 16 + (lane >> 2);
+    boff[j] = row_addr(a.B, min(n0 + r, a.N - 1)) + ((lane & 3) ^ ring::swz_chunk(r)) * 8 + kbeg;
+  }
+  auto issue = [&](int i) {   // k-slice i -> slot i % 4
+    char* la = smem + (i & (ring::NSLOT - 1)) * C::SLOT;
+    char* lb = la + C::HALF_A;
+    const int64_t ko = (int64_t)i * ring::KS;
+#pragma unroll
+    for (int j = 0; j < C::DMA_A; ++j) ring::dma16(Ab + aoff[j] + ko, la + (j * C::NW + wave) * 1024);
+#pragma unroll
+    for (int j = 0; j < C::DMA_B; ++j) ring::dma16(Bb + boff[j] + ko, lb + (j * C::NW + wave) * 1024);
+  };
+  auto slot = [&](int i) -> const char* { return smem + (i & (ring::NSLOT - 1)) * C::SLOT; };
+
+  f32x4_t acc[C::FM][C::FN];
+#pragma unroll
+  for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+    for (int j = 0; j < C::FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  // one pipeline step: slice i is in registers (cur); wait for slice i+1, restage slot i%4 with
+  // slice i+4, read slice i+1 into nxt while multiplying cur
+  auto step = [&](int i, ring::Frags<C>& cur, ring::Frags<C>& nxt) {
+    if (i + 3 < H) {
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    } else if (i + 2 < H) {
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (i + 4 < H) issue(i + 4);
+    if (i + 1 < H) ring::read_frags<C>(nxt, slot(i + 1), wr, wc, lane);
+    __builtin_amdgcn_sched_barrier(0);
+    ring::mfma_slice<C>(acc, cur);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): nxt landed (and slot i+1 reads retired)
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  if (H > 0) {
+#pragma unroll
+    for (int i = 0; i < ring::NSLOT; ++i)
+      if (i < H) issue(i);
+    // slice 0: wait until at most the later slices' DMAs remain
+    if (H >= 4) {
+      asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    } else if (H == 3) {
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    } else if (H == 2) {
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    ring::Frags<C> f0, f1;
+    ring::read_frags<C>(f0, slot(0), wr, wc, lane);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_sched_barrier(0);
+    int i = 0;
+    for (; i + 1 < H; i += 2) {
+      step(i, f0, f1);
+      step(i + 1, f1, f0);
+    }
+    if (i < H) step(i, f0, f1);
+  }
+
+  // ---- epilogue, EROWS rows at a time: accumulators -> LDS fp32 -> row-contiguous ----
+  constexpr int TPR = C::BN / 8;              // threads per output row (8 columns each)
+  constexpr int RPP = C::NT / TPR;            // rows per pass
+  float* ct = reinterpret_cast<float*>(smem);
+  const int c8 = (tid % TPR) * 8;
+  const int r0 = tid / TPR;
+  float cso[8], csa[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    cso[q] = 0.f;
+    csa[q] = 0.f;
+  }
+#pragma unroll 1
+  for (int h = 0; h < C::BM / C::EROWS; ++h) {
+    __syncthreads();
+    // waves whose rows fall in this pass stage their accumulators
+    if (wr * C::WTM / C::EROWS == h) {
+#pragma unroll
+      for (int i = 0; i < C::FM; ++i) {
+        const int r = (wr * C::WTM) % C::EROWS + 16 * i + (lane & 15);
+#pragma unroll
+        for (int j = 0; j < C::FN; ++j) {
+          const int c = wc * C::WTN + 16 * j + 4 * (lane >> 4);
+          *reinterpret_cast<float4*>(ct + r * C::CROW + c) =
+              make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+        }
+      }
+    }
+    __syncthreads();
+    if (a.splits > 1) {
+      float* ws = reinterpret_cast<float*>(a.workspace) + (zz * a.M) * a.N;
+#pragma unroll 2
+      for (int p = 0; p < C::EROWS / RPP; ++p) {
+        const int r = r0 + RPP * p;
+        const int64_t m = m0 + h * C::EROWS + r;
+        const int64_t n = n0 + c8;
+        if (m >= a.M || n >= a.N) continue;
+        const float* src = ct + r * C::CROW + c8;
+        float* dst = ws + m * a.N + n;
+        if (n + 8 <= a.N && (a.N & 3) == 0) {
+          *reinterpret_cast<float4*>(dst) = *reinterpret_cast<const float4*>(src);
+          *reinterpret_cast<float4*>(dst + 4) = *reinterpret_cast<const float4*>(src + 4);
+        } else {
+          for (int q = 0; q < 8 && n + q < a.N; ++q) dst[q] = src[q];
+        }
+      }
+      continue;
+    }
+#pragma unroll 1
+    for (int p = 0; p < C::EROWS / RPP; ++p) {
+      const int r = r0 + RPP * p;
+      const float* src = ct + r * C::CROW + c8;
+      float v[8];
+      const float4 x0 = *reinterpret_cast<const float4*>(src);
+      const float4 x1 = *reinterpret_cast<const float4*>(src + 4);
+      v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w;
+      v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
+      Cs8 cs;
+      epilogue8(a, z, m0 + h * C::EROWS + r, n0 + c8, v, cs);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        cso[q] += cs.out[q];
+        csa[q] += cs.aux[q];
+      }
+    }
+  }
+  if (a.splits == 1 && ((a.colsum_out != nullptr) || (a.colsum_aux != nullptr))) {
+    // lanes sharing columns inside a wave (lane ^ TPR, ...), then the waves through LDS
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+#pragma unroll
+      for (int o = TPR; o < 64; o <<= 1) {
+        cso[q] += __shfl_xor(cso[q], o, 64);
+        csa[q] += __shfl_xor(csa[q], o, 64);
+      }
+    }
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);   // [NW][2][BN]
+    if (lane < TPR) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        red[(wave * 2 + 0) * C::BN + c8 + q] = cso[q];
+        red[(wave * 2 + 1) * C::BN + c8 + q] = csa[q];
+      }
+    }
+    __syncthreads();
+    if (tid < C::BN) {
+      const int64_t n = n0 + tid;
+      if (n < a.N) {
+        const int64_t voff = (a.C.z_div > 0 ? (z % a.C.z_div) : z) * a.vec_z_inner;
+        float so = 0.f, sx = 0.f;
+#pragma unroll
+        for (int w = 0; w < C::NW; ++w) {
+          so += red[(w * 2 + 0) * C::BN + tid];
+          sx += red[(w * 2 + 1) * C::BN + tid];
+        }
+        if (a.colsum_out) atomicAdd(a.colsum_out + voff + n, so);
+        if (a.colsum_aux) atomicAdd(a.colsum_aux + voff + n, sx);
+      }
+    }
+  }
+}
+
 // split-K reduction + epilogue: one thread per 8 columns of a row
 __global__ void splitk_reduce_kernel(const DphGemmArgs a) {
   const int64_t z = blockIdx.z;
@@ -496,6 +806,13 @@ __global__ void splitk_reduce_kernel(const DphGemmArgs a) {
 
 using namespace dph;
 
+// DPH_GEMM_PATH: unset/auto = size-based choice, "small" = 128x128 kernel only, "big" = large-tile
+// kernel wherever its layout constraints allow (tests exercise both paths in one process)
+static int gemm_path_override() {
+  const char* e = getenv("DPH_GEMM_PATH");
+  return (e && !strcmp(e, "small")) ? 1 : (e && !strcmp(e, "big")) ? 2 : (e && !strcmp(e, "mid")) ? 3 : 0;
+}
+
 extern "C" int dph_gemm(const DphGemmArgs* args, hipStream_t stream) {
   DPH_REQUIRE(args != nullptr, "dph_gemm: null args");
   const DphGemmArgs& a = *args;
@@ -517,6 +834,25 @@ extern "C" int dph_gemm(const DphGemmArgs* args, hipStream_t stream) {
     DPH_REQUIRE(a.workspace && a.workspace_bytes >= need, "dph_gemm: split-K workspace too small (%lld < %lld)",
                 (long long)a.workspace_bytes, (long long)need);
   }
+  // LDS-DMA ring kernels for k-contiguous A and B with whole 32-deep k-slices: the 256x256 tile
+  // when there are >= ~2 full rounds of tiles over the 256 CUs at one block per CU, else the
+  // 128x128 tile (DPH_GEMM_PATH=small|big|mid forces a path, for tests)
+  const bool ring_ok = a.a_kcontig && a.b_kcontig && a.K % ring::KS == 0 && kchunk % ring::KS == 0;
+  const int64_t tiles256 = cdiv(a.M, ring::Big::BM) * cdiv(a.N, ring::Big::BN) * a.batch * a.splits;
+  int kind = !ring_ok ? 0 : (tiles256 >= 480 ? 2 : 1);   // 0 small, 1 mid ring, 2 big ring
+  const int path = gemm_path_override();
+  if (path == 1) kind = 0;
+  if (path == 2 && ring_ok) kind = 2;
+  if (path == 3 && ring_ok) kind = 1;
+  if (kind == 2) {
+    dim3 gb((unsigned)cdiv(a.N, ring::Big::BN), (unsigned)cdiv(a.M, ring::Big::BM), (unsigned)(a.batch * a.splits));
+    DPH_REQUIRE(gb.y < 65536 && gb.z < 65536, "dph_gemm: grid too large");
+    hipLaunchKernelGGL(ring_gemm_kernel<ring::Big>, gb, dim3(ring::Big::NT), 0, stream, a, kchunk);
+  } else if (kind == 1) {
+    dim3 gm((unsigned)cdiv(a.N, ring::Mid::BN), (unsigned)cdiv(a.M, ring::Mid::BM), (unsigned)(a.batch * a.splits));
+    DPH_REQUIRE(gm.y < 65536 && gm.z < 65536, "dph_gemm: grid too large");
+    hipLaunchKernelGGL(ring_gemm_kernel<ring::Mid>, gm, dim3(ring::Mid::NT), 0, stream, a, kchunk);
+  } else {
   dim3 grid((unsigned)cdiv(a.N, BN), (unsigned)cdiv(a.M, BM), (unsigned)(a.batch * a.splits));
   DPH_REQUIRE(grid.y < 65536 && grid.z < 65536, "dph_gemm: grid too large");
   if (a.a_kcontig && a.b_kcontig)
@@ -527,6 +863,7 @@ extern "C" int dph_gemm(const DphGemmArgs* args, hipStream_t stream) {
     hipLaunchKernelGGL((gemm_kernel<false, true>), grid, dim3(NTHREADS), 0, stream, a, kchunk);
   else
     hipLaunchKernelGGL((gemm_kernel<false, false>), grid, dim3(NTHREADS), 0, stream, a, kchunk);
+  }
   int rc = check_launch("dph_gemm");
   if (rc) return rc;
   if (a.splits > 1) {

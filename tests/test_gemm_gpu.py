@@ -9,6 +9,15 @@ pytestmark = pytest.mark.gpu
 torch.manual_seed(0)
 
 
+@pytest.fixture(autouse=True, params=["small", "mid", "big"])
+def gemm_path(request, monkeypatch):
+    """Run every test on each GEMM path: the 128x128 register-staged kernel and the 128x128 /
+    256x256 LDS-DMA ring kernels (taken where their constraints hold: both operands k-contiguous,
+    K % 32 == 0)."""
+    monkeypatch.setenv("DPH_GEMM_PATH", request.param)
+    return request.param
+
+
 def _k():
     from dphubert_amd import kernels as K
     return K
@@ -26,7 +35,8 @@ def close(a, b, tol=2e-2):
 
 
 @pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, True), (False, False)])
-@pytest.mark.parametrize("M,N,K", [(304, 200, 136), (128, 128, 64), (1000, 264, 520)])
+@pytest.mark.parametrize("M,N,K", [(304, 200, 136), (128, 128, 64), (1000, 264, 520), (1000, 264, 512),
+                                   (2056, 520, 768), (256, 256, 64), (7984, 768, 192)])
 def test_layouts(ak, bk, M, N, K):
     K_ = _k()
     A = rnd(M, K) if ak else rnd(K, M)
@@ -127,10 +137,11 @@ def test_conv_implicit_gemm():
     close(y, ref, 1e-5)
 
 
-def test_batched_zdiv():
+@pytest.mark.parametrize("M,N,K", [(70, 48, 96), (300, 264, 128)])
+def test_batched_zdiv(M, N, K):
     # grouped GEMM: z = b*G + g ; B operand depends only on g
     K_ = _k()
-    Bt, G, M, N, K = 3, 4, 70, 48, 96
+    Bt, G = 3, 4
     A = rnd(Bt * G, M, K)
     W = rnd(G, N, K)
     out = torch.empty(Bt, M, G * N, device="cuda")

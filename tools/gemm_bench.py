@@ -14,11 +14,15 @@ SHAPES = [  # (name, M, N, K, a_kcontig, b_kcontig)
     ("ffn2 fwd", M, 768, 3072, True, True),
     ("oproj fwd", M, 768, 768, True, True),
     ("conv1 fwd", 16 * 15999, 512, 1536, True, True),
+    ("conv1 dgrad", 16 * 15999, 1536, 512, True, False),
+    ("conv1 wgrad", 512, 1536, 16 * 15999, False, False),
     ("ffn2 dgrad", M, 3072, 768, True, False),
     ("ffn1 dgrad", M, 768, 3072, True, False),
     ("qkv dgrad", M, 768, 2304, True, False),
     ("ffn1 wgrad", 3072, 768, M, False, False),
     ("qkv wgrad", 2304, 768, M, False, False),
+    ("sq 4096", 4096, 4096, 4096, True, True),
+    ("sq 8192", 8192, 8192, 8192, True, True),
 ]
 
 
@@ -44,7 +48,19 @@ def run(name, M, N, Kd, ak, bk, iters=20):
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / iters
     tf = 2 * M * N * Kd / ms / 1e9
-    print(f"{name:16s} M={M:6d} N={N:5d} K={Kd:5d} splits={splits:2d}  {ms*1e3:8.1f} us  {tf:6.0f} TF/s", flush=True)
+    # library reference point: torch.matmul (hipBLASLt) on the same operands, plain bf16 output
+    At = A if ak else A.t()
+    Bt = B.t() if bk else B
+    for _ in range(3):
+        torch.matmul(At, Bt)
+    e0.record()
+    for _ in range(iters):
+        torch.matmul(At, Bt)
+    e1.record()
+    torch.cuda.synchronize()
+    ms_lib = e0.elapsed_time(e1) / iters
+    print(f"{name:16s} M={M:6d} N={N:5d} K={Kd:5d} splits={splits:2d}  {ms*1e3:8.1f} us  {tf:6.0f} TF/s   "
+          f"torch.matmul {ms_lib*1e3:8.1f} us {2 * M * N * Kd / ms_lib / 1e9:6.0f} TF/s", flush=True)
     return ms
 
 

@@ -295,9 +295,45 @@ def gen_prune():
             "wave": wave, "pruned_hidden_ck": [checksum(x) for x in h]}
 
 
+def gen_data():
+    """G5: data-pipeline fixtures -- the reference's samplers and collate on synthetic lengths."""
+    from dataset.audio_dataset import BucketizeBatchSampler, CollateFnAudio, DistributedBatchSampler  # reference
+    g = torch.Generator().manual_seed(5)
+    lengths = torch.randint(20000, 260000, (600,), generator=g).tolist()
+    out = {"lengths": torch.tensor(lengths)}
+    bs = BucketizeBatchSampler(lengths, num_buckets=50, max_token_count=900000, min_len=32000, max_len=250000,
+                               shuffle=False)
+    out["token_batches"] = [torch.tensor(b) for b in bs.iter_list]
+    bs2 = BucketizeBatchSampler(lengths, num_buckets=20, batch_size=7, min_len=32000, max_len=250000,
+                                shuffle=False, drop_last=True)
+    out["size_batches"] = [torch.tensor(b) for b in bs2.iter_list]
+    torch.manual_seed(11)
+    bs3 = BucketizeBatchSampler(lengths, num_buckets=50, max_token_count=900000, min_len=32000, max_len=250000,
+                                shuffle=True)
+    out["shuffled_token_batches"] = [torch.tensor(b) for b in bs3.iter_list]
+    for world in (2, 3):
+        for drop in (False, True):
+            for r in range(world):
+                ds = DistributedBatchSampler(bs, num_replicas=world, rank=r, shuffle=True, seed=3, drop_last=drop)
+                out[f"dist_w{world}_d{int(drop)}_r{r}"] = [torch.tensor(b) for b in ds.subset]
+    waves = [torch.randn(1, n, generator=g) for n in (4000, 3500, 5123)]
+    batch = [(w, w.shape[1]) for w in waves]
+    out["collate_in"] = waves
+    torch.manual_seed(13)
+    out["collate_crop"] = CollateFnAudio(pad=False, rand_crop=True)(batch)
+    out["collate_pad"] = CollateFnAudio(pad=True, rand_crop=False)(batch)
+    return out
+
+
 def main():
     OUT.mkdir(parents=True, exist_ok=True)
     torch.set_num_threads(8)
+    if "--only-data" in sys.argv:
+        torch.save(gen_data(), OUT / "g5_data.pt")
+        print("g5 done")
+        return
+    torch.save(gen_data(), OUT / "g5_data.pt")
+    print("g5 done")
     torch.save(gen_ops(), OUT / "g1_ops.pt")
     print("g1 done")
     # G2: 2-layer smoke step (BASELINE config 1 shape-reduced to 2 s), units conv,head,interm, reg active
