@@ -34,7 +34,7 @@ class DphGemmArgs(C.Structure):
                 ("alpha", f32), ("dropout_p", f32), ("seed", u64), ("bias", vp), ("colmask", vp), ("smask", vp),
                 ("vec_z_inner", i64), ("pre_out", vp), ("aux_in", vp), ("residual", vp), ("colsum_out", vp),
                 ("colsum_aux", vp), ("row_len", vp), ("len_rows", i64), ("drop_row_offset", i64),
-                ("workspace", vp), ("workspace_bytes", i64)]
+                ("workspace", vp), ("workspace_bytes", i64), ("colsum_n", i64)]
 
 
 class DphTensorSlot(C.Structure):
@@ -55,6 +55,9 @@ _SIGS = {
     "dph_layernorm_fwd": ([vp, vp, vp, vp, vp, vp, vp, i64, i64, f32, f32, u64, S], C.c_int),
     "dph_layernorm_bwd": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, f32, u64, vp, f32, u64, vp, vp, vp, vp, S],
                           C.c_int),
+    "dph_layernorm_fwd_ld": ([vp, vp, vp, vp, vp, vp, vp, i64, i64, i64, f32, f32, u64, S], C.c_int),
+    "dph_layernorm_bwd_ld": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, i64, f32, u64, vp, f32, u64, vp, vp, vp,
+                              vp, S], C.c_int),
     "dph_colsum": ([vp, vp, i64, i64, S], C.c_int),
     "dph_attention_fwd": ([vp, vp, vp, vp, vp, vp, i64, i64, i64, f32, f32, u64, S], C.c_int),
     "dph_attention_bwd_prep": ([vp, vp, vp, vp, vp, i64, i64, i64, S], C.c_int),
@@ -69,8 +72,8 @@ _SIGS = {
     "dph_weight_norm_fwd": ([vp, vp, i64, i64, i64, i64, vp, vp, vp, vp, vp, i64, S], C.c_int),
     "dph_weight_norm_bwd": ([vp, vp, vp, vp, i64, i64, i64, i64, vp, vp, vp, i64, S], C.c_int),
     "dph_cast_bf16": ([vp, vp, i64, S], C.c_int),
-    "dph_conv_weight_pack": ([vp, vp, i64, i64, i64, S], C.c_int),
-    "dph_conv_weight_unpack_grad": ([vp, vp, i64, i64, i64, C.c_int, S], C.c_int),
+    "dph_conv_weight_pack": ([vp, vp, i64, i64, i64, i64, i64, S], C.c_int),
+    "dph_conv_weight_unpack_grad": ([vp, vp, i64, i64, i64, i64, C.c_int, S], C.c_int),
     "dph_add_bf16": ([vp, vp, vp, i64, S], C.c_int),
     "dph_branch_bwd": ([vp, vp, i64, i64, f32, u64, vp, vp, i64, vp, vp, vp, S], C.c_int),
     "dph_distill_loss_fwd": ([vp, vp, i64, i64, i64, i64, f32, f32, f32, C.c_int, vp, vp, vp, S], C.c_int),
@@ -84,6 +87,7 @@ _SIGS = {
 }
 
 _lib = None
+ABI_VERSION = 2     # include/dphubert_hip.h layout (DphGemmArgs.colsum_n, padded conv packing, strided LN)
 
 
 class DphError(RuntimeError):
@@ -110,6 +114,8 @@ def lib():
         fn.argtypes = args
         fn.restype = res
     L.missing_symbols = missing
+    if "dph_abi_version" not in missing and L.dph_abi_version() != ABI_VERSION:
+        raise DphError(f"{LIB_PATH}: ABI {L.dph_abi_version()} != {ABI_VERSION}; rebuild (python -m dphubert_amd.build)")
     _lib = L
     return L
 

@@ -113,26 +113,26 @@ __global__ void cast_bf16_kernel(const float* __restrict__ src, bf16_t* __restri
   }
 }
 
-// w [O][C][k] fp32 -> dst [O][k*C] bf16 (index j*C + c)
+// w [O][C][k] fp32 -> dst [Op][k*Cp] bf16 (index j*Cp + c); zero padding rows / channels
 __global__ void conv_pack_kernel(const float* __restrict__ w, bf16_t* __restrict__ dst, int64_t O, int64_t C,
-                                 int64_t k) {
+                                 int64_t k, int64_t Op, int64_t Cp) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= O * C * k) return;
-  const int64_t c = i % C;
-  const int64_t j = (i / C) % k;
-  const int64_t o = i / (C * k);
-  dst[i] = f2bf(w[(o * C + c) * k + j]);
+  if (i >= Op * Cp * k) return;
+  const int64_t c = i % Cp;
+  const int64_t j = (i / Cp) % k;
+  const int64_t o = i / (Cp * k);
+  dst[i] = (o < O && c < C) ? f2bf(w[(o * C + c) * k + j]) : (bf16_t)0;
 }
 
-// g [O][k*C] fp32 -> dst [O][C][k]
+// g [>=O][k*Cp] fp32 -> dst [O][C][k]
 __global__ void conv_unpack_kernel(const float* __restrict__ g, float* __restrict__ dst, int64_t O, int64_t C,
-                                   int64_t k, int accum) {
+                                   int64_t k, int64_t Cp, int accum) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= O * C * k) return;
   const int64_t j = i % k;
   const int64_t c = (i / k) % C;
   const int64_t o = i / (C * k);
-  const float v = g[o * k * C + j * C + c];
+  const float v = g[o * k * Cp + j * Cp + c];
   dst[i] = accum ? dst[i] + v : v;
 }
 
@@ -265,18 +265,19 @@ extern "C" int dph_cast_bf16(const float* src, void* dst, int64_t n, hipStream_t
   return check_launch("dph_cast_bf16");
 }
 
-extern "C" int dph_conv_weight_pack(const float* w, void* dst, int64_t O, int64_t C, int64_t k, hipStream_t stream) {
-  DPH_REQUIRE(w && dst && O > 0 && C > 0 && k > 0, "dph_conv_weight_pack: bad args");
-  hipLaunchKernelGGL(conv_pack_kernel, dim3((unsigned)cdiv(O * C * k, 256)), dim3(256), 0, stream, w,
-                     reinterpret_cast<bf16_t*>(dst), O, C, k);
+extern "C" int dph_conv_weight_pack(const float* w, void* dst, int64_t O, int64_t C, int64_t k, int64_t Op,
+                                    int64_t Cp, hipStream_t stream) {
+  DPH_REQUIRE(w && dst && O > 0 && C > 0 && k > 0 && Op >= O && Cp >= C, "dph_conv_weight_pack: bad args");
+  hipLaunchKernelGGL(conv_pack_kernel, dim3((unsigned)cdiv(Op * Cp * k, 256)), dim3(256), 0, stream, w,
+                     reinterpret_cast<bf16_t*>(dst), O, C, k, Op, Cp);
   return check_launch("dph_conv_weight_pack");
 }
 
-extern "C" int dph_conv_weight_unpack_grad(const float* g, float* dst, int64_t O, int64_t C, int64_t k, int accum,
-                                           hipStream_t stream) {
-  DPH_REQUIRE(g && dst && O > 0 && C > 0 && k > 0, "dph_conv_weight_unpack_grad: bad args");
+extern "C" int dph_conv_weight_unpack_grad(const float* g, float* dst, int64_t O, int64_t C, int64_t k, int64_t Cp,
+                                           int accum, hipStream_t stream) {
+  DPH_REQUIRE(g && dst && O > 0 && C > 0 && k > 0 && Cp >= C, "dph_conv_weight_unpack_grad: bad args");
   hipLaunchKernelGGL(conv_unpack_kernel, dim3((unsigned)cdiv(O * C * k, 256)), dim3(256), 0, stream, g, dst, O, C, k,
-                     accum);
+                     Cp, accum);
   return check_launch("dph_conv_weight_unpack_grad");
 }
 

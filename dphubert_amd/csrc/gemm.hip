@@ -98,7 +98,7 @@ struct Stager {
         reg[i] = *reinterpret_cast<const uint4*>(base + roff[i] + k);
       } else {
         int64_t k = min(k0 + (c >> 4), kend - 1);
-        int64_t col = min(r0 + (c & 15) * 8, R - 8);
+        int64_t col = min(r0 + (c & 15) * 8, ((R + 7) & ~(int64_t)7) - 8);   // padded rows: see dph_gemm
         reg[i] = *reinterpret_cast<const uint4*>(base + row_addr(d, k) + col);
       }
     }
@@ -458,14 +458,15 @@ __global__ void __launch_bounds__(NTHREADS, 2) gemm_kernel(const DphGemmArgs a, 
       const int64_t n = n0 + tid;
       if (n < a.N) {
         const int64_t voff = (a.C.z_div > 0 ? (z % a.C.z_div) : z) * a.vec_z_inner;
+        const int64_t csn = a.colsum_n > 0 ? a.colsum_n : a.N;
         float so = 0.f, sx = 0.f;
 #pragma unroll
         for (int w = 0; w < NTHREADS / 64; ++w) {
           so += red[(w * 2 + 0) * 128 + tid];
           sx += red[(w * 2 + 1) * 128 + tid];
         }
-        if (a.colsum_out) atomicAdd(a.colsum_out + voff + n, so);
-        if (a.colsum_aux) atomicAdd(a.colsum_aux + voff + n, sx);
+        if (a.colsum_out && n < csn) atomicAdd(a.colsum_out + voff + n, so);
+        if (a.colsum_aux && n < csn) atomicAdd(a.colsum_aux + voff + n, sx);
       }
     }
   }
@@ -765,14 +766,15 @@ __global__ void __launch_bounds__(C::NT, C::MINB) ring_gemm_kernel(const DphGemm
       const int64_t n = n0 + tid;
       if (n < a.N) {
         const int64_t voff = (a.C.z_div > 0 ? (z % a.C.z_div) : z) * a.vec_z_inner;
+        const int64_t csn = a.colsum_n > 0 ? a.colsum_n : a.N;
         float so = 0.f, sx = 0.f;
 #pragma unroll
         for (int w = 0; w < C::NW; ++w) {
           so += red[(w * 2 + 0) * C::BN + tid];
           sx += red[(w * 2 + 1) * C::BN + tid];
         }
-        if (a.colsum_out) atomicAdd(a.colsum_out + voff + n, so);
-        if (a.colsum_aux) atomicAdd(a.colsum_aux + voff + n, sx);
+        if (a.colsum_out && n < csn) atomicAdd(a.colsum_out + voff + n, so);
+        if (a.colsum_aux && n < csn) atomicAdd(a.colsum_aux + voff + n, sx);
       }
     }
   }
@@ -822,8 +824,13 @@ extern "C" int dph_gemm(const DphGemmArgs* args, hipStream_t stream) {
   DPH_REQUIRE(a.A.ptr && a.B.ptr && a.C.ptr, "dph_gemm: null operand");
   DPH_REQUIRE(a.K % 8 == 0 || !a.a_kcontig, "dph_gemm: k-contiguous A needs K %% 8 == 0 (K=%lld)", (long long)a.K);
   DPH_REQUIRE(a.K % 8 == 0 || !a.b_kcontig, "dph_gemm: k-contiguous B needs K %% 8 == 0 (K=%lld)", (long long)a.K);
-  DPH_REQUIRE(a.a_kcontig || a.M % 8 == 0, "dph_gemm: mn-contiguous A needs M %% 8 == 0");
-  DPH_REQUIRE(a.b_kcontig || a.N % 8 == 0, "dph_gemm: mn-contiguous B needs N %% 8 == 0");
+  // an mn-contiguous operand is read in 8-wide 16-B chunks: its extent must be a multiple of 8, or
+  // its rows padded to one (row stride % 8 == 0 and >= the rounded-up extent; the padding columns
+  // only feed outputs that are never stored)
+  DPH_REQUIRE(a.a_kcontig || a.M % 8 == 0 || (a.A.row_stride % 8 == 0 && a.A.row_stride >= (a.M + 7) / 8 * 8),
+              "dph_gemm: mn-contiguous A needs M %% 8 == 0 or 8-padded rows");
+  DPH_REQUIRE(a.b_kcontig || a.N % 8 == 0 || (a.B.row_stride % 8 == 0 && a.B.row_stride >= (a.N + 7) / 8 * 8),
+              "dph_gemm: mn-contiguous B needs N %% 8 == 0 or 8-padded rows");
   DPH_REQUIRE(a.act != DPH_ACT_GELU_BWD || a.aux_in, "dph_gemm: GELU_BWD needs aux_in");
   DPH_REQUIRE(!a.row_len || a.len_rows > 0, "dph_gemm: row_len needs len_rows");
   int64_t kchunk = a.K;

@@ -15,12 +15,13 @@ constexpr int LN_MAXV = 4;   // up to 4 x (64 lanes x 4 elements) = 1024 columns
 __global__ void __launch_bounds__(256) ln_fwd_kernel(const bf16_t* __restrict__ x, const float* __restrict__ xscale,
                                                      const float* __restrict__ gamma, const float* __restrict__ beta,
                                                      bf16_t* __restrict__ y, float* __restrict__ mean_out,
-                                                     float* __restrict__ rstd_out, int64_t rows, int D, float eps,
-                                                     float drop_p, uint64_t seed) {
+                                                     float* __restrict__ rstd_out, int64_t rows, int D, int ld,
+                                                     float eps, float drop_p, uint64_t seed) {
+  // rows have stride ld >= D (ld % 4 == 0); columns [D, ld) are row padding: read as 0, written as 0
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
-  const bf16_t* xr = x + row * D;
+  const bf16_t* xr = x + row * ld;
   float v[LN_MAXV][4];
   float s = 0.f;
 #pragma unroll
@@ -32,9 +33,10 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const bf16_t* __restrict__ 
       v[c][1] = __uint_as_float(raw.x & 0xffff0000u);
       v[c][2] = __uint_as_float(raw.y << 16);
       v[c][3] = __uint_as_float(raw.y & 0xffff0000u);
-      if (xscale) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) v[c][i] *= xscale[col + i];
+      for (int i = 0; i < 4; ++i) {
+        if (col + i >= D) v[c][i] = 0.f;
+        else if (xscale) v[c][i] *= xscale[col + i];
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) s += v[c][i];
@@ -52,7 +54,7 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const bf16_t* __restrict__ 
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const float d = v[c][i] - mean;
-        q += d * d;
+        if (col + i < D) q += d * d;
       }
     }
   }
@@ -62,14 +64,18 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const bf16_t* __restrict__ 
 #pragma unroll
   for (int c = 0; c < LN_MAXV; ++c) {
     const int col = (c * 64 + lane) * 4;
-    if (col < D) {
+    if (col < ld) {
       float o[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        o[i] = (v[c][i] - mean) * rstd * gamma[col + i] + beta[col + i];
-        o[i] *= dropout_scale(seed, (uint64_t)row * D + col + i, drop_p, inv_keep);
+        if (col + i < D) {
+          o[i] = (v[c][i] - mean) * rstd * gamma[col + i] + beta[col + i];
+          o[i] *= dropout_scale(seed, (uint64_t)row * D + col + i, drop_p, inv_keep);
+        } else {
+          o[i] = 0.f;
+        }
       }
-      *reinterpret_cast<uint2*>(y + row * D + col) = make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
+      *reinterpret_cast<uint2*>(y + row * ld + col) = make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
     }
   }
   if (lane == 0) {
@@ -84,7 +90,8 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const bf16_t* __restrict__ 
 __global__ void __launch_bounds__(256) ln_bwd_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const float* __restrict__ xscale,
     const float* __restrict__ gamma, const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
-    bf16_t* __restrict__ dx, float* __restrict__ dgamma, float* __restrict__ dbeta, int64_t rows, int D, float drop_p,
+    bf16_t* __restrict__ dx, float* __restrict__ dgamma, float* __restrict__ dbeta, int64_t rows, int D, int ld,
+    float drop_p,
     uint64_t seed, bf16_t* __restrict__ branch, float branch_p, uint64_t branch_seed,
     const float* __restrict__ branch_smask, float* __restrict__ branch_colsum, const bf16_t* __restrict__ branch_pre,
     float* __restrict__ branch_sdot) {
@@ -110,18 +117,19 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(
     for (int c = 0; c < LN_MAXV; ++c) {
       const int col = (c * 64 + lane) * 4;
       if (col < D) {
-        uint2 rx = *reinterpret_cast<const uint2*>(x + row * D + col);
-        uint2 rd = *reinterpret_cast<const uint2*>(dy + row * D + col);
+        uint2 rx = *reinterpret_cast<const uint2*>(x + row * ld + col);
+        uint2 rd = *reinterpret_cast<const uint2*>(dy + row * ld + col);
         float xv[4] = {__uint_as_float(rx.x << 16), __uint_as_float(rx.x & 0xffff0000u),
                        __uint_as_float(rx.y << 16), __uint_as_float(rx.y & 0xffff0000u)};
         float dv[4] = {__uint_as_float(rd.x << 16), __uint_as_float(rd.x & 0xffff0000u),
                        __uint_as_float(rd.y << 16), __uint_as_float(rd.y & 0xffff0000u)};
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          float xs = xscale ? xv[i] * xscale[col + i] : xv[i];
-          xh[c][i] = (xs - mean) * rstd;
-          dyv[c][i] = dv[i] * dropout_scale(seed, (uint64_t)row * D + col + i, drop_p, inv_keep);
-          g[c][i] = dyv[c][i] * gamma[col + i];
+          const bool ok = col + i < D;
+          float xs = (xscale && ok) ? xv[i] * xscale[col + i] : xv[i];
+          xh[c][i] = ok ? (xs - mean) * rstd : 0.f;
+          dyv[c][i] = ok ? dv[i] * dropout_scale(seed, (uint64_t)row * D + col + i, drop_p, inv_keep) : 0.f;
+          g[c][i] = ok ? dyv[c][i] * gamma[col + i] : 0.f;
           s1 += g[c][i];
           s2 += g[c][i] * xh[c][i];
           pg[c][i] += dyv[c][i] * xh[c][i];
@@ -134,19 +142,20 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(
 #pragma unroll
     for (int c = 0; c < LN_MAXV; ++c) {
       const int col = (c * 64 + lane) * 4;
-      if (col < D) {
+      if (col < ld) {
         float o[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          o[i] = rstd * (g[c][i] - s1 - xh[c][i] * s2);
-          if (xscale) o[i] *= xscale[col + i];
+          const bool ok = col + i < D;
+          o[i] = ok ? rstd * (g[c][i] - s1 - xh[c][i] * s2) : 0.f;
+          if (xscale && ok) o[i] *= xscale[col + i];
         }
-        *reinterpret_cast<uint2*>(dx + row * D + col) = make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
+        *reinterpret_cast<uint2*>(dx + row * ld + col) = make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
         if (branch) {
           float bo[4];
           float pre[4] = {0.f, 0.f, 0.f, 0.f};
           if (branch_sdot) {
-            uint2 rp = *reinterpret_cast<const uint2*>(branch_pre + row * D + col);
+            uint2 rp = *reinterpret_cast<const uint2*>(branch_pre + row * ld + col);
             pre[0] = __uint_as_float(rp.x << 16);
             pre[1] = __uint_as_float(rp.x & 0xffff0000u);
             pre[2] = __uint_as_float(rp.y << 16);
@@ -154,12 +163,13 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(
           }
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const float z = o[i] * dropout_scale(branch_seed, (uint64_t)row * D + col + i, branch_p, binv_keep);
+            const float z = (col + i < D) ? o[i] * dropout_scale(branch_seed, (uint64_t)row * D + col + i, branch_p,
+                                                                 binv_keep) : 0.f;
             sdot += z * pre[i];
             bo[i] = z * bsm;
             pc[c][i] += bo[i];
           }
-          *reinterpret_cast<uint2*>(branch + row * D + col) = make_uint2(pack2bf(bo[0], bo[1]),
+          *reinterpret_cast<uint2*>(branch + row * ld + col) = make_uint2(pack2bf(bo[0], bo[1]),
                                                                          pack2bf(bo[2], bo[3]));
         }
       }
@@ -235,15 +245,44 @@ __global__ void __launch_bounds__(256) colsum_kernel(const bf16_t* __restrict__ 
 
 using namespace dph;
 
+extern "C" int dph_layernorm_fwd_ld(const void* x, const float* xscale, const float* gamma, const float* beta,
+                                    void* y, float* mean, float* rstd, int64_t rows, int64_t D, int64_t ld, float eps,
+                                    float dropout_p, uint64_t seed, hipStream_t stream) {
+  DPH_REQUIRE(x && gamma && beta && y && mean && rstd, "dph_layernorm_fwd: null pointer");
+  if (ld == 0) ld = D;
+  DPH_REQUIRE(D >= 1 && ld >= D && ld % 4 == 0 && ld <= LN_MAXV * 256 && rows > 0,
+              "dph_layernorm_fwd: unsupported D=%lld ld=%lld", (long long)D, (long long)ld);
+  hipLaunchKernelGGL(ln_fwd_kernel, dim3((unsigned)cdiv(rows, 4)), dim3(256), 0, stream,
+                     reinterpret_cast<const bf16_t*>(x), xscale, gamma, beta, reinterpret_cast<bf16_t*>(y), mean, rstd,
+                     rows, (int)D, (int)ld, eps, dropout_p, seed);
+  return check_launch("dph_layernorm_fwd");
+}
+
 extern "C" int dph_layernorm_fwd(const void* x, const float* xscale, const float* gamma, const float* beta, void* y,
                                  float* mean, float* rstd, int64_t rows, int64_t D, float eps, float dropout_p,
                                  uint64_t seed, hipStream_t stream) {
-  DPH_REQUIRE(x && gamma && beta && y && mean && rstd, "dph_layernorm_fwd: null pointer");
-  DPH_REQUIRE(D % 4 == 0 && D <= LN_MAXV * 256 && rows > 0, "dph_layernorm_fwd: unsupported D=%lld", (long long)D);
-  hipLaunchKernelGGL(ln_fwd_kernel, dim3((unsigned)cdiv(rows, 4)), dim3(256), 0, stream,
-                     reinterpret_cast<const bf16_t*>(x), xscale, gamma, beta, reinterpret_cast<bf16_t*>(y), mean, rstd,
-                     rows, (int)D, eps, dropout_p, seed);
-  return check_launch("dph_layernorm_fwd");
+  return dph_layernorm_fwd_ld(x, xscale, gamma, beta, y, mean, rstd, rows, D, D, eps, dropout_p, seed, stream);
+}
+
+extern "C" int dph_layernorm_bwd_ld(const void* dy, const void* x, const float* xscale, const float* gamma,
+                                    const float* mean, const float* rstd, void* dx, float* dgamma, float* dbeta,
+                                    int64_t rows, int64_t D, int64_t ld, float dropout_p, uint64_t seed, void* branch,
+                                    float branch_p, uint64_t branch_seed, const float* branch_smask,
+                                    float* branch_colsum, const void* branch_pre, float* branch_sdot,
+                                    hipStream_t stream) {
+  DPH_REQUIRE(dy && x && gamma && mean && rstd && dx, "dph_layernorm_bwd: null pointer");
+  if (ld == 0) ld = D;
+  DPH_REQUIRE(D >= 1 && ld >= D && ld % 4 == 0 && ld <= LN_MAXV * 256 && rows > 0,
+              "dph_layernorm_bwd: unsupported D=%lld ld=%lld", (long long)D, (long long)ld);
+  DPH_REQUIRE(!branch_sdot || branch_pre, "dph_layernorm_bwd: branch_sdot needs branch_pre");
+  DPH_REQUIRE(!(branch_colsum || branch_sdot) || branch, "dph_layernorm_bwd: branch sums need branch output");
+  const int64_t blocks = std::min<int64_t>(cdiv(rows, 4 * 8), 1024);
+  hipLaunchKernelGGL(ln_bwd_kernel, dim3((unsigned)blocks), dim3(256), 0, stream,
+                     reinterpret_cast<const bf16_t*>(dy), reinterpret_cast<const bf16_t*>(x), xscale, gamma, mean,
+                     rstd, reinterpret_cast<bf16_t*>(dx), dgamma, dbeta, rows, (int)D, (int)ld, dropout_p, seed,
+                     reinterpret_cast<bf16_t*>(branch), branch_p, branch_seed, branch_smask, branch_colsum,
+                     reinterpret_cast<const bf16_t*>(branch_pre), branch_sdot);
+  return check_launch("dph_layernorm_bwd");
 }
 
 extern "C" int dph_layernorm_bwd(const void* dy, const void* x, const float* xscale, const float* gamma,
@@ -252,17 +291,9 @@ extern "C" int dph_layernorm_bwd(const void* dy, const void* x, const float* xsc
                                  float branch_p, uint64_t branch_seed, const float* branch_smask,
                                  float* branch_colsum, const void* branch_pre, float* branch_sdot,
                                  hipStream_t stream) {
-  DPH_REQUIRE(dy && x && gamma && mean && rstd && dx, "dph_layernorm_bwd: null pointer");
-  DPH_REQUIRE(D % 4 == 0 && D <= LN_MAXV * 256 && rows > 0, "dph_layernorm_bwd: unsupported D=%lld", (long long)D);
-  DPH_REQUIRE(!branch_sdot || branch_pre, "dph_layernorm_bwd: branch_sdot needs branch_pre");
-  DPH_REQUIRE(!(branch_colsum || branch_sdot) || branch, "dph_layernorm_bwd: branch sums need branch output");
-  const int64_t blocks = std::min<int64_t>(cdiv(rows, 4 * 8), 1024);
-  hipLaunchKernelGGL(ln_bwd_kernel, dim3((unsigned)blocks), dim3(256), 0, stream,
-                     reinterpret_cast<const bf16_t*>(dy), reinterpret_cast<const bf16_t*>(x), xscale, gamma, mean,
-                     rstd, reinterpret_cast<bf16_t*>(dx), dgamma, dbeta, rows, (int)D, dropout_p, seed,
-                     reinterpret_cast<bf16_t*>(branch), branch_p, branch_seed, branch_smask, branch_colsum,
-                     reinterpret_cast<const bf16_t*>(branch_pre), branch_sdot);
-  return check_launch("dph_layernorm_bwd");
+  return dph_layernorm_bwd_ld(dy, x, xscale, gamma, mean, rstd, dx, dgamma, dbeta, rows, D, D, dropout_p, seed,
+                              branch, branch_p, branch_seed, branch_smask, branch_colsum, branch_pre, branch_sdot,
+                              stream);
 }
 
 extern "C" int dph_colsum(const void* x, float* out, int64_t rows, int64_t cols, hipStream_t stream) {

@@ -27,4 +27,4 @@ int check_launch(const char* what) {
 }  // namespace dph
 
 extern "C" const char* dph_last_error(void) { return dph::g_err; }
-extern "C" int dph_abi_version(void) { return 1; }
+extern "C" int dph_abi_version(void) { return 2; }

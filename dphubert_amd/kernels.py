@@ -81,7 +81,7 @@ def gemm(A: DphMat, B: DphMat, Cm: DphMat, M: int, N: int, K: int, *, a_kcontig:
          c_dtype: int = OUT_BF16, act: int = ACT_NONE, alpha: float = 1.0, batch: int = 1, splits: int = 1,
          bias=None, colmask=None, smask=None, vec_z_inner: int = 0, pre_out=None, aux_in=None, residual=None,
          colsum_out=None, colsum_aux=None, row_len=None, len_rows: int = 0, dropout_p: float = 0.0, seed: int = 0,
-         drop_row_offset: int = 0, device=None):
+         drop_row_offset: int = 0, colsum_n: int = 0, device=None):
     ws = None
     ws_bytes = 0
     if splits > 1:
@@ -90,7 +90,7 @@ def gemm(A: DphMat, B: DphMat, Cm: DphMat, M: int, N: int, K: int, *, a_kcontig:
     args = DphGemmArgs(M, N, K, batch, splits, int(a_kcontig), int(b_kcontig), A, B, Cm, c_dtype, act, alpha,
                        dropout_p, seed & 0xFFFFFFFFFFFFFFFF, ptr(bias), ptr(colmask), ptr(smask), vec_z_inner,
                        ptr(pre_out), ptr(aux_in), ptr(residual), ptr(colsum_out), ptr(colsum_aux), ptr(row_len),
-                       len_rows, drop_row_offset, ptr(ws), ws_bytes)
+                       len_rows, drop_row_offset, ptr(ws), ws_bytes, colsum_n)
     prof = LaunchProfiler.active
     if prof is not None:
         e0 = torch.cuda.Event(enable_timing=True)
@@ -130,7 +130,7 @@ def linear_fwd(x: torch.Tensor, w_bf16: torch.Tensor, bias: Optional[torch.Tenso
 
 
 def linear_dgrad(dy: torch.Tensor, w_bf16: torch.Tensor, *, out=None, residual=None, act=ACT_NONE, aux_in=None,
-                 colmask=None, colsum_out=None, colsum_aux=None, dropout_p=0.0, seed=0):
+                 colmask=None, colsum_out=None, colsum_aux=None, dropout_p=0.0, seed=0, colsum_n=0):
     """dx = epi(dy @ w); dy [M,N] bf16, w [N,K] bf16 -> [M,K] bf16."""
     M, N = dy.shape
     K = w_bf16.shape[1]
@@ -138,15 +138,20 @@ def linear_dgrad(dy: torch.Tensor, w_bf16: torch.Tensor, *, out=None, residual=N
         out = torch.empty(M, K, dtype=BF16, device=dy.device)
     gemm(dense(dy), dense(w_bf16), dense(out), M, K, N, a_kcontig=True, b_kcontig=False, residual=residual, act=act,
          aux_in=aux_in, colmask=colmask, colsum_out=colsum_out, colsum_aux=colsum_aux, dropout_p=dropout_p,
-         seed=seed)
+         seed=seed, colsum_n=colsum_n)
     return out
 
 
-def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, accumulate: bool = True):
-    """dw (+)= dy^T @ x; dy [M,N] bf16, x [M,K] bf16, dw [N,K] fp32."""
+def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, accumulate: bool = True, n_out: int = 0,
+                 k_in: int = 0):
+    """dw (+)= dy^T @ x; dy [M,N] bf16, x [M,K] bf16, dw [N,K] fp32.
+
+    ``n_out`` / ``k_in`` < the operands' widths: only the first n_out x k_in block is produced
+    (dy / x rows padded to multiples of 8 for pruned students; dw stays dense [n_out][k_in])."""
     M, N = dy.shape
     K = x.shape[1]
-    splits = choose_splits(N, K, M)
-    ws = gemm(dense(dy), dense(x), dense(dw), N, K, M, a_kcontig=False, b_kcontig=False,
+    Nw, Kw = (n_out or N), (k_in or K)
+    splits = choose_splits(Nw, Kw, M)
+    ws = gemm(dense(dy), dense(x), mat(dw, Kw), Nw, Kw, M, a_kcontig=False, b_kcontig=False,
               c_dtype=OUT_F32_ACCUM if accumulate else OUT_F32, splits=splits, device=dy.device)
     return ws

@@ -113,16 +113,49 @@ def f32_cat(*ts: torch.Tensor) -> torch.Tensor:
     return out
 
 
-def conv_image(w: torch.Tensor) -> torch.Tensor:
-    """conv weight [O][C][k] fp32 -> bf16 [O][k*C] (k-major, matches channels-last im2col rows)."""
-    key = ("conv",) + _version_key((w,))
+def pad8(n: int) -> int:
+    """Storage width of a channel / feature dimension: pruned students have ragged widths, the
+    bf16 kernels read 16-B chunks, so rows are padded to a multiple of 8 with zero columns."""
+    return (int(n) + 7) // 8 * 8
+
+
+def conv_image(w: torch.Tensor, Op: Optional[int] = None, Cp: Optional[int] = None) -> torch.Tensor:
+    """conv weight [O][C][k] fp32 -> bf16 [Op][k*Cp] (k-major, matches channels-last im2col rows;
+    zero rows / channels for the 8-padding of pruned widths)."""
+    O, C, kk = w.shape
+    Op = Op or O
+    Cp = Cp or C
+    key = ("conv", Op, Cp) + _version_key((w,))
     hit = getattr(w, "_dph_img", None)
     if hit is not None and hit[0] == key:
         return hit[1]
-    O, C, kk = w.shape
-    out = torch.empty(O, kk * C, dtype=BF16, device=w.device)
-    call("dph_conv_weight_pack", ptr(w.detach()), ptr(out), O, C, kk, _s())
+    out = torch.empty(Op, kk * Cp, dtype=BF16, device=w.device)
+    call("dph_conv_weight_pack", ptr(w.detach()), ptr(out), O, C, kk, Op, Cp, _s())
     w._dph_img = (key, out)
+    return out
+
+
+def padded_image(w: torch.Tensor, rows_p: int, cols_p: int) -> torch.Tensor:
+    """bf16 image of a 2-D fp32 weight zero-padded to [rows_p][cols_p] (pruned widths), cached
+    like bf16_image; the padding glue is plain torch and runs once per optimizer step."""
+    if tuple(w.shape) == (rows_p, cols_p):
+        return bf16_image(w)
+    key = ("pad", rows_p, cols_p) + _version_key((w,))
+    hit = getattr(w, "_dph_img", None)
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    out = torch.zeros(rows_p, cols_p, dtype=BF16, device=w.device)
+    out[:w.shape[0], :w.shape[1]] = w.detach().to(BF16)
+    w._dph_img = (key, out)
+    return out
+
+
+def padded_vec(v: Optional[torch.Tensor], n_p: int) -> Optional[torch.Tensor]:
+    """fp32 vector zero-padded to n_p (bias / mask of a pruned width); the same tensor if no padding."""
+    if v is None or v.numel() == n_p:
+        return v
+    out = torch.zeros(n_p, dtype=v.dtype, device=v.device)
+    out[:v.numel()] = v
     return out
 
 
@@ -363,37 +396,49 @@ class FrontendFn(torch.autograd.Function):
         dev = wave.device
         need = cfg.need_grad
         C0, k0, s0 = layers[0]
-        y = torch.empty(B * Ls[0], C0, dtype=BF16, device=dev)
-        mean = torch.empty(B, C0, dtype=F32, device=dev)
-        rstd = torch.empty(B, C0, dtype=F32, device=dev)
+        C0p = pad8(C0)
+        # conv0 of a pruned student (ragged C0) runs over C0p channels with zero weights / affine /
+        # mask in the padding: those channels come out exactly 0
+        w0, g0, b0, m0 = ws_[0], gn_w, gn_b, masks[0]
+        if C0p != C0:
+            w0 = torch.zeros(C0p, *ws_[0].shape[1:], dtype=F32, device=dev)
+            w0[:C0] = ws_[0].detach()
+            g0, b0 = padded_vec(gn_w.detach(), C0p), padded_vec(gn_b.detach(), C0p)
+            m0 = padded_vec(masks[0] if masks[0] is not None else torch.ones(C0, device=dev), C0p)
+        y = torch.empty(B * Ls[0], C0p, dtype=BF16, device=dev)
+        mean = torch.empty(B, C0p, dtype=F32, device=dev)
+        rstd = torch.empty(B, C0p, dtype=F32, device=dev)
         nch = -(-Ls[0] // 256)
-        ws = torch.empty(B * nch * C0 * 2, dtype=F32, device=dev)
-        call("dph_conv0_gn_fwd", ptr(wave), B, S, ptr(ws_[0]), C0, k0, s0, ptr(gn_w), ptr(gn_b), ptr(masks[0]),
+        ws = torch.empty(B * nch * C0p * 2, dtype=F32, device=dev)
+        call("dph_conv0_gn_fwd", ptr(wave), B, S, ptr(w0), C0p, k0, s0, ptr(g0), ptr(b0), ptr(m0),
              ptr(y), ptr(mean), ptr(rstd), ptr(ws), ws.numel() * 4, _s())
-        ys, zs, imgs, cms = [y], [None], [None], [masks[0]]
-        Cin = C0
+        ys, zs, imgs, cms = [y], [None], [None], [m0]
+        Cin, Cinp = C0, C0p
         for i in range(1, n):
             O, k, s = layers[i]
-            img = conv_image(ws_[i])
+            Op = pad8(O)
+            img = conv_image(ws_[i], Op, Cinp)
             cm = masks[i]
             if i == n - 1:
                 cm = dummy if cm is None else cm * dummy
-            out = torch.empty(B * Ls[i], O, dtype=BF16, device=dev)
-            z = torch.empty(B * Ls[i], O, dtype=BF16, device=dev) if need else None
-            A = K.mat(ys[-1], row_stride=s * Cin, rows_per_batch=Ls[i], batch_stride=Ls[i - 1] * Cin)
-            K.gemm(A, K.dense(img), K.dense(out), B * Ls[i], O, k * Cin, a_kcontig=True, b_kcontig=True,
+            cm = padded_vec(cm, Op)
+            out = torch.empty(B * Ls[i], Op, dtype=BF16, device=dev)
+            z = torch.empty(B * Ls[i], Op, dtype=BF16, device=dev) if need else None
+            A = K.mat(ys[-1], row_stride=s * Cinp, rows_per_batch=Ls[i], batch_stride=Ls[i - 1] * Cinp)
+            K.gemm(A, K.dense(img), K.dense(out), B * Ls[i], Op, k * Cinp, a_kcontig=True, b_kcontig=True,
                    act=K.ACT_GELU, pre_out=z, colmask=cm)
             ys.append(out)
             zs.append(z)
             imgs.append(img)
             cms.append(cm)
-            Cin = O
+            Cin, Cinp = O, Op
         if need:
             ctx.cfg = cfg
             ctx.params = (gn_w, gn_b, *ws_)
             ctx.Ls = Ls
             ctx.cms = cms
             ctx.has_mask = [m is not None for m in masks]
+            ctx.padded0 = (w0, g0, b0, m0) if C0p != C0 else None
             ctx.save_for_backward(wave, dummy, gn_w, gn_b, mean, rstd, *ws_, *[m if m is not None else dummy
                                                                             for m in masks])
             ctx.ys = ys[:-1]   # inputs of layers 1..n-1 (the last output is not needed)
@@ -417,53 +462,63 @@ class FrontendFn(torch.autograd.Function):
         pgn_w, pgn_b, *pws = ctx.params
         go = GradOut(dev)
         g_m = [None] * n
-        # last layer: GELU / (mask*dummy) backward
+        # last layer: GELU / (mask*dummy) backward (widths are the 8-padded storage widths)
         O = layers[-1][0]
+        Op = pad8(O)
         dz = torch.empty_like(dy)
-        dm_raw = zeros_f32(O, dev)
-        call("dph_gelu_mask_bwd", ptr(dy), ptr(ctx.zs[-1]), ptr(ctx.cms[-1]), ptr(dz), ptr(dm_raw), B * Ls[-1], O,
+        dm_raw = zeros_f32(Op, dev)
+        call("dph_gelu_mask_bwd", ptr(dy), ptr(ctx.zs[-1]), ptr(ctx.cms[-1]), ptr(dz), ptr(dm_raw), B * Ls[-1], Op,
              _s())
         if masks[-1] is not None:
-            g_m[-1] = dm_raw * dummy
+            g_m[-1] = dm_raw[:O] * dummy
         keep = []
         for i in range(n - 1, 0, -1):
             O, k, s = layers[i]
+            Op = pad8(O)
             Cin = layers[i - 1][0]
+            Cinp = pad8(Cin)
             M = B * Ls[i]
-            # weight gradient (packed [O][k*Cin]) -> [O][Cin][k]
-            dwp = torch.empty(O, k * Cin, dtype=F32, device=dev)
-            A = K.mat(dz, row_stride=O)
-            Bm = K.mat(ctx.ys[i - 1], row_stride=s * Cin, rows_per_batch=Ls[i], batch_stride=Ls[i - 1] * Cin)
-            splits = K.choose_splits(O, k * Cin, M)
-            keep.append(K.gemm(A, Bm, K.dense(dwp), O, k * Cin, M, a_kcontig=False, b_kcontig=False,
+            # weight gradient (packed [O][k*Cinp]) -> [O][Cin][k]
+            dwp = torch.empty(O, k * Cinp, dtype=F32, device=dev)
+            A = K.mat(dz, row_stride=Op)
+            Bm = K.mat(ctx.ys[i - 1], row_stride=s * Cinp, rows_per_batch=Ls[i], batch_stride=Ls[i - 1] * Cinp)
+            splits = K.choose_splits(O, k * Cinp, M)
+            keep.append(K.gemm(A, Bm, K.dense(dwp), O, k * Cinp, M, a_kcontig=False, b_kcontig=False,
                                c_dtype=K.OUT_F32, splits=splits, device=dev))
             dw, direct = go.buf(pws[i], zero=False)
-            call("dph_conv_weight_unpack_grad", ptr(dwp), ptr(dw), O, Cin, k, int(direct), _s())
+            call("dph_conv_weight_unpack_grad", ptr(dwp), ptr(dw), O, Cin, k, Cinp, int(direct), _s())
             # input gradient columns, then col2im fused with the previous layer's GELU/mask backward
-            dcols = torch.empty(M, k * Cin, dtype=BF16, device=dev)
-            K.gemm(K.dense(dz), K.dense(ctx.imgs[i]), K.dense(dcols), M, k * Cin, O, a_kcontig=True,
+            dcols = torch.empty(M, k * Cinp, dtype=BF16, device=dev)
+            K.gemm(K.dense(dz), K.dense(ctx.imgs[i]), K.dense(dcols), M, k * Cinp, Op, a_kcontig=True,
                    b_kcontig=False)
-            nxt = torch.empty(B * Ls[i - 1], Cin, dtype=BF16, device=dev)
+            nxt = torch.empty(B * Ls[i - 1], Cinp, dtype=BF16, device=dev)
             if i > 1:
-                dmk = zeros_f32(Cin, dev) if masks[i - 1] is not None else None
-                call("dph_col2im_gelu_bwd", ptr(dcols), B, Ls[i], Ls[i - 1], Cin, k, s, ptr(ctx.zs[i - 1]),
-                     ptr(masks[i - 1]), ptr(nxt), ptr(dmk) if dmk is not None else
-                     ptr(zeros_f32(Cin, dev)), _s())
-                g_m[i - 1] = dmk
+                dmk = zeros_f32(Cinp, dev) if masks[i - 1] is not None else None
+                call("dph_col2im_gelu_bwd", ptr(dcols), B, Ls[i], Ls[i - 1], Cinp, k, s, ptr(ctx.zs[i - 1]),
+                     ptr(ctx.cms[i - 1]), ptr(nxt), ptr(dmk) if dmk is not None else
+                     ptr(zeros_f32(Cinp, dev)), _s())
+                g_m[i - 1] = dmk[:Cin] if dmk is not None else None
             else:
-                call("dph_col2im_gelu_bwd", ptr(dcols), B, Ls[i], Ls[i - 1], Cin, k, s, None, None, ptr(nxt), None,
+                call("dph_col2im_gelu_bwd", ptr(dcols), B, Ls[i], Ls[i - 1], Cinp, k, s, None, None, ptr(nxt), None,
                      _s())
             dz = nxt
         # layer 0: conv0 + GroupNorm + GELU + mask, recomputed from the waveform
         C0, k0, s0 = layers[0]
-        dw0, _ = go.buf(pws[0])
-        dgw, _ = go.buf(pgn_w)
-        dgb, _ = go.buf(pgn_b)
-        dm0 = zeros_f32(C0, dev) if masks[0] is not None else None
-        wsb = torch.empty(B * C0 * 2, dtype=F32, device=dev)
-        call("dph_conv0_gn_bwd", ptr(wave), B, S, ptr(ws_[0]), C0, k0, s0, ptr(gn_w), ptr(gn_b), ptr(masks[0]),
+        C0p = pad8(C0)
+        if ctx.padded0 is None:
+            dw0, _ = go.buf(pws[0])
+            dgw, _ = go.buf(pgn_w)
+            dgb, _ = go.buf(pgn_b)
+            w0, g0, b0, m0 = ws_[0], gn_w, gn_b, masks[0]
+        else:   # pruned (ragged) conv0: padded scratch gradients, returned sliced to autograd
+            w0, g0, b0, m0 = ctx.padded0
+            dw0, dgw, dgb = zeros_f32((C0p,) + tuple(ws_[0].shape[1:]), dev), zeros_f32(C0p, dev), zeros_f32(C0p, dev)
+            go.bufs[id(pws[0])], go.bufs[id(pgn_w)], go.bufs[id(pgn_b)] = dw0[:C0], dgw[:C0], dgb[:C0]
+        dm0 = zeros_f32(C0p, dev) if masks[0] is not None else None
+        wsb = torch.empty(B * C0p * 2, dtype=F32, device=dev)
+        call("dph_conv0_gn_bwd", ptr(wave), B, S, ptr(w0), C0p, k0, s0, ptr(g0), ptr(b0), ptr(m0),
              ptr(mean), ptr(rstd), ptr(dz), ptr(dw0), ptr(dgw), ptr(dgb), ptr(dm0), ptr(wsb), wsb.numel() * 4, _s())
-        g_m[0] = dm0
+        g_m[0] = dm0[:C0] if dm0 is not None else None
         go.done()
         grads = [None, None, None, go.ret(pgn_w), go.ret(pgn_b)]
         for i in range(n):
@@ -477,14 +532,17 @@ class FrontendFn(torch.autograd.Function):
 class FeatureProjectionFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, ln_w, ln_b, w, b, cfg):
-        M, C = x.shape
+        # x: [M][Cp] with the true channel count C = cfg["C"] <= Cp (8-padded rows of a pruned
+        # frontend; the padding columns are zero and stay zero through LN)
+        M, Cp = x.shape
+        C = cfg.get("C") or Cp
         dev = x.device
         xn = torch.empty_like(x)
         mu = torch.empty(M, dtype=F32, device=dev)
         rs = torch.empty(M, dtype=F32, device=dev)
-        call("dph_layernorm_fwd", ptr(x), None, ptr(ln_w), ptr(ln_b), ptr(xn), ptr(mu), ptr(rs), M, C, 1e-5, 0.0, 0,
-             _s())
-        img = bf16_image(w)
+        call("dph_layernorm_fwd_ld", ptr(x), None, ptr(ln_w), ptr(ln_b), ptr(xn), ptr(mu), ptr(rs), M, C, Cp, 1e-5,
+             0.0, 0, _s())
+        img = padded_image(w, w.shape[0], Cp)
         seed = SEEDS.next() if cfg["p"] > 0 else 0
         out = K.linear_fwd(xn, img, b, dropout_p=cfg["p"], seed=seed, row_len=cfg["lengths"],
                            len_rows=cfg["T"] if cfg["lengths"] is not None else 0)
@@ -498,7 +556,8 @@ class FeatureProjectionFn(torch.autograd.Function):
     def backward(ctx, dout):
         x, xn, mu, rs, ln_w, img = ctx.saved_tensors
         cfg = ctx.cfg
-        M, C = x.shape
+        M, Cp = x.shape
+        C = cfg.get("C") or Cp
         D = img.shape[0]
         dev = x.device
         dout = dout.contiguous()
@@ -510,13 +569,13 @@ class FeatureProjectionFn(torch.autograd.Function):
         call("dph_branch_bwd", ptr(dout), ptr(dpre), M, D, cfg["p"], ctx.seed, None, ptr(lens),
              cfg["T"] if lens is not None else 0, ptr(db), None, None, _s())
         dw, direct = go.buf(p_w, zero=False)
-        ws = K.linear_wgrad(dpre, xn, dw, accumulate=direct)
+        ws = K.linear_wgrad(dpre, xn, dw, accumulate=direct, k_in=C)
         dxn = K.linear_dgrad(dpre, img)
         dx = torch.empty_like(x)
         dlw, _ = go.buf(p_lw)
         dlb, _ = go.buf(p_lb)
-        call("dph_layernorm_bwd", ptr(dxn), ptr(x), None, ptr(ln_w), ptr(mu), ptr(rs), ptr(dx), ptr(dlw), ptr(dlb), M,
-             C, 0.0, 0, None, 0.0, 0, None, None, None, None, _s())
+        call("dph_layernorm_bwd_ld", ptr(dxn), ptr(x), None, ptr(ln_w), ptr(mu), ptr(rs), ptr(dx), ptr(dlw), ptr(dlb),
+             M, C, Cp, 0.0, 0, None, 0.0, 0, None, None, None, None, _s())
         del ws
         go.done()
         return dx, go.ret(p_lw), go.ret(p_lb), go.ret(p_w), go.ret(p_b), None
@@ -668,17 +727,21 @@ class EncoderLayerFn(torch.autograd.Function):
              0, _s())
         # ---------------- feed-forward block ----------------
         if use_ff:
+            # intermediate width F of a pruned student is ragged: stored 8-padded (zero weight rows /
+            # columns, bias and mask padding 0 -> the padding columns of u and f are exactly 0)
             F_ = w1.shape[0]
-            W1 = bf16_image(w1)
-            W2 = bf16_image(w2)
+            Fp = pad8(F_)
+            W1 = padded_image(w1, Fp, D)
+            W2 = padded_image(w2, D, Fp)
+            b1p, imp = padded_vec(b1, Fp), padded_vec(im, Fp)
             seed_i = SEEDS.next() if cfg["p_interm"] > 0 else 0
-            u = torch.empty(M, F_, dtype=BF16, device=dev) if need else None
-            f = K.linear_fwd(h1, W1, b1, act=K.ACT_GELU, pre_out=u, colmask=im, dropout_p=cfg["p_interm"],
+            u = torch.empty(M, Fp, dtype=BF16, device=dev) if need else None
+            f = K.linear_fwd(h1, W1, b1p, act=K.ACT_GELU, pre_out=u, colmask=imp, dropout_p=cfg["p_interm"],
                              seed=seed_i)
             seed_o = SEEDS.next() if cfg["p_drop"] > 0 else 0
             y_pre = torch.empty(M, D, dtype=BF16, device=dev) if (need and lmf is not None) else None
             s2 = K.linear_fwd(f, W2, b2, smask=lmf, residual=h1, dropout_p=cfg["p_drop"], seed=seed_o, pre_out=y_pre)
-            sv.update(W1=W1, W2=W2, u=u, f=f, y_pre=y_pre, seed_i=seed_i, seed_o=seed_o)
+            sv.update(W1=W1, W2=W2, u=u, f=f, y_pre=y_pre, seed_i=seed_i, seed_o=seed_o, F=F_, imp=imp)
         else:
             s2 = h1
         out = torch.empty_like(h)
@@ -720,16 +783,16 @@ class EncoderLayerFn(torch.autograd.Function):
             call("dph_layernorm_bwd", ptr(dout), ptr(s2), None, ptr(ln2_w), ptr(mu2), ptr(rs2), ptr(ds2),
                  ptr(dln2w), ptr(dln2b), M, D, 0.0, 0, ptr(dy), cfg["p_drop"], sv["seed_o"], ptr(lmf), ptr(db2),
                  ptr(sv["y_pre"]), ptr(g["lmf"]), _s())
-            F_ = sv["W1"].shape[0]
+            F_ = sv["F"]
             dw2, direct = go.buf(pr["w2"], zero=False)
-            k1 = K.linear_wgrad(dy, sv["f"], dw2, accumulate=direct)
+            k1 = K.linear_wgrad(dy, sv["f"], dw2, accumulate=direct, k_in=F_)
             db1, _ = go.buf(pr["b1"])
             g["im"] = z(F_) if has_im else None
-            du = K.linear_dgrad(dy, sv["W2"], act=K.ACT_GELU_BWD, aux_in=sv["u"], colmask=im, colsum_out=db1,
+            du = K.linear_dgrad(dy, sv["W2"], act=K.ACT_GELU_BWD, aux_in=sv["u"], colmask=sv["imp"], colsum_out=db1,
                                 colsum_aux=g["im"] if has_im else z(F_), dropout_p=cfg["p_interm"],
-                                seed=sv["seed_i"])
+                                seed=sv["seed_i"], colsum_n=F_)
             dw1, direct = go.buf(pr["w1"], zero=False)
-            k2 = K.linear_wgrad(du, h1, dw1, accumulate=direct)
+            k2 = K.linear_wgrad(du, h1, dw1, accumulate=direct, n_out=F_)
             dh1 = K.linear_dgrad(du, sv["W1"], residual=ds2)
             del k1, k2
         else:

@@ -165,7 +165,16 @@ class FeatureExtractor(Module):
         y = ops.FrontendFn.apply(cfg, x.contiguous().float(), self.dummy_weight, l0.layer_norm.weight,
                                  l0.layer_norm.bias, *flat)
         T = ops.conv_lengths(S, layers)[-1]
-        y = y.view(B, T, layers[-1][0])
+        C = layers[-1][0]
+        Cp = ops.pad8(C)
+        if Cp != C:
+            # pruned (ragged) width: the HIP path keeps 8-padded rows; expose the reference's
+            # (B, T, C) as a view and hand the padded storage to FeatureProjection
+            yp = y
+            y = yp.view(B, T, Cp)[:, :, :C]
+            y._dph_padded = yp
+        else:
+            y = y.view(B, T, C)
         if length is not None:
             for (_, k, s) in layers:
                 length = torch.div(length - k, s, rounding_mode="floor") + 1
@@ -237,7 +246,14 @@ class FeatureProjection(Module):
         p = self.dropout.p if self.training else 0.0
         cfg = {"p": p, "lengths": lengths.to(x.device, torch.int64).contiguous() if lengths is not None else None,
                "T": T}
-        y = ops.FeatureProjectionFn.apply(x.reshape(B * T, C), self.layer_norm.weight, self.layer_norm.bias,
+        xp = getattr(x, "_dph_padded", None)
+        if xp is not None:
+            cfg["C"] = C
+        else:
+            xp = x.reshape(B * T, C)
+            if C % 4:
+                raise NotImplementedError("FeatureProjection: ragged widths need the 8-padded frontend output")
+        y = ops.FeatureProjectionFn.apply(xp, self.layer_norm.weight, self.layer_norm.bias,
                                           self.projection.weight, self.projection.bias, cfg)
         return y.view(B, T, -1)
 

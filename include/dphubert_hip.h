@@ -90,6 +90,7 @@ typedef struct DphGemmArgs {
   int64_t drop_row_offset;/* dropout element index = (drop_row_offset + m)*N + n (per batch z adds z*M*N) */
   void* workspace;        /* split-K partials                                  */
   int64_t workspace_bytes;
+  int64_t colsum_n;       /* column sums only for n < colsum_n (0: all N); padded-width operands */
 } DphGemmArgs;
 
 int dph_gemm(const DphGemmArgs* args, hipStream_t stream);
@@ -111,6 +112,17 @@ int dph_layernorm_bwd(const void* dy, const void* x, const float* xscale, const 
                       float dropout_p, uint64_t seed, void* branch, float branch_p, uint64_t branch_seed,
                       const float* branch_smask, float* branch_colsum, const void* branch_pre,
                       float* branch_sdot, hipStream_t stream);
+
+/* the same over rows of stride ld >= D (ld % 4 == 0): columns [D, ld) are row padding (pruned
+ * students' channel counts padded to multiples of 8), read as 0 and written as 0 */
+int dph_layernorm_fwd_ld(const void* x, const float* xscale, const float* gamma, const float* beta, void* y,
+                         float* mean, float* rstd, int64_t rows, int64_t D, int64_t ld, float eps, float dropout_p,
+                         uint64_t seed, hipStream_t stream);
+int dph_layernorm_bwd_ld(const void* dy, const void* x, const float* xscale, const float* gamma, const float* mean,
+                         const float* rstd, void* dx, float* dgamma, float* dbeta, int64_t rows, int64_t D, int64_t ld,
+                         float dropout_p, uint64_t seed, void* branch, float branch_p, uint64_t branch_seed,
+                         const float* branch_smask, float* branch_colsum, const void* branch_pre, float* branch_sdot,
+                         hipStream_t stream);
 
 /* column sums of a bf16 matrix (bias gradients): out[n] += sum_m x[m][n] */
 int dph_colsum(const void* x, float* out, int64_t rows, int64_t cols, hipStream_t stream);
@@ -178,10 +190,12 @@ int dph_weight_norm_bwd(const float* dw_img, const float* g, const float* v, con
  * ------------------------------------------------------------------------ */
 /* dst[r][c] = bf16(src[r][c] * (colscale ? colscale[c] : 1)) */
 int dph_cast_bf16(const float* src, void* dst, int64_t n, hipStream_t stream);
-/* conv weight [O][C][k] fp32 -> bf16 [O][k*C] (index j*C+c) */
-int dph_conv_weight_pack(const float* w, void* dst, int64_t O, int64_t C, int64_t k, hipStream_t stream);
-/* grad of packed conv weight: fp32 [O][k*C] -> [O][C][k] (accumulate if accum) */
-int dph_conv_weight_unpack_grad(const float* g, float* dst, int64_t O, int64_t C, int64_t k, int accum,
+/* conv weight [O][C][k] fp32 -> bf16 [Op][k*Cp] (index j*Cp+c), zero for o >= O or c >= C
+ * (channel counts of pruned students padded to multiples of 8) */
+int dph_conv_weight_pack(const float* w, void* dst, int64_t O, int64_t C, int64_t k, int64_t Op, int64_t Cp,
+                         hipStream_t stream);
+/* grad of packed conv weight: fp32 [>=O][k*Cp] -> [O][C][k] (accumulate if accum) */
+int dph_conv_weight_unpack_grad(const float* g, float* dst, int64_t O, int64_t C, int64_t k, int64_t Cp, int accum,
                                 hipStream_t stream);
 /* residual-branch gradient: out = dy*drop(p,seed)*(*smask), padded rows zeroed
  * ((m % len_rows) >= row_len[m/len_rows]); colsum += out; sdot += sum(dy*drop*pre).

@@ -71,7 +71,7 @@ def test_library_loads_and_exports_every_symbol():
     from dphubert_amd import _lib
     L = _lib.lib()
     assert L.missing_symbols == []
-    assert L.dph_abi_version() == 1
+    assert L.dph_abi_version() == _lib.ABI_VERSION
     # every symbol declared in include/dphubert_hip.h is exported
     import re
     from pathlib import Path

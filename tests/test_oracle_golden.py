@@ -123,3 +123,23 @@ def test_base12_g3():
     fx = load_golden("g3_base12.pt")
     out = _run_fixture(fx)
     _check_step(fx, out, tol_loss=2e-5, tol_ck=5e-4)
+
+
+def test_oracle_pruned_forward_matches_reference():
+    """The oracle restatement on the reference's pruned architecture (ragged widths) -- g4."""
+    import copy as _copy
+    from dphubert_amd.cli import prune_config
+    from dphubert_amd.wav2vec2.model import wav2vec2_model
+    from helpers import ck_close, seeded_sd
+    fx = load_golden("g4_prune.pt")
+    m = wav2vec2_model(**_copy.deepcopy(fx["cfg"]))
+    sd = seeded_sd(fx["cfg"], fx["seed"])
+    sd.update(fx["log_alpha"])
+    m.load_state_dict(sd)
+    pcfg = prune_config(m, fx["cfg"])
+    psd = {k: v.detach() for k, v in m.state_dict().items()}
+    with torch.no_grad():
+        hs, _ = ref.extract_features(psd, pcfg, fx["wave"])
+    for h, ck in zip(hs, fx["pruned_hidden_ck"]):
+        e_sample, e_sq = ck_close(h, ck)
+        assert e_sample < 1e-4 and e_sq < 1e-5, (e_sample, e_sq)
