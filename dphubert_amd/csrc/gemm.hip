@@ -492,6 +492,9 @@ __global__ void __launch_bounds__(NTHREADS, 2) gemm_kernel(const DphGemmArgs a, 
 // 16 rows and two k-chunks; the naive (r>>2)&3 measured 50 % bank-conflict cycles).  The swizzle
 // is applied on the DMA SOURCE address since an LDS-DMA writes its 1 KB lane-linearly.
 // =============================================================================================
+#ifndef DPH_ABLATE
+#define DPH_ABLATE 0        // timing ablations of the ring loop (tools/ablate_gemm.py); 0 = production
+#endif
 namespace ring {
 constexpr int KS = 32;      // k per slice
 constexpr int NSLOT = 4;
@@ -524,7 +527,8 @@ struct Cfg {
   static constexpr int PIPE = NSLOT * SLOT;
   static constexpr int DMA_A = BM * 64 / (NT * 16);          // DMA instructions per thread per slice
   static constexpr int DMA_B = BN * 64 / (NT * 16);
-  static_assert(DMA_A + DMA_B == 4, "vmcnt counts assume 4 DMA per thread per slice");
+  static constexpr int DMA = DMA_A + DMA_B;                   // per thread per slice
+  static_assert(DMA == 4 || DMA == 8, "vmcnt immediates exist for 4 or 8 DMA per thread per slice");
   static constexpr int EROWS = BM > 128 ? 128 : BM;          // epilogue staging rows per pass
   static constexpr int CROW = BN + 4;
   static constexpr int EPI = EROWS * CROW * 4;
@@ -533,6 +537,18 @@ struct Cfg {
 };
 using Big = Cfg<256, 256, 128, 64>;
 using Mid = Cfg<128, 128, 64, 64>;
+
+// s_waitcnt vmcnt(n * DMA): at most n slices' DMAs still in flight
+template <int DMA, int n>
+__device__ __forceinline__ void wait_slices() {
+  if constexpr (DMA * n == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (DMA * n == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (DMA * n == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (DMA * n == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else if constexpr (DMA * n == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else if constexpr (DMA * n == 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+  else static_assert(DMA * n < 0, "no vmcnt immediate");
+}
 
 template <class C>
 struct Frags {
@@ -629,19 +645,26 @@ __global__ void __launch_bounds__(C::NT, C::MINB) ring_gemm_kernel(const DphGemm
   // slice i+4, read slice i+1 into nxt while multiplying cur
   auto step = [&](int i, ring::Frags<C>& cur, ring::Frags<C>& nxt) {
     if (i + 3 < H) {
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      ring::wait_slices<C::DMA, 2>();
     } else if (i + 2 < H) {
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      ring::wait_slices<C::DMA, 1>();
     } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      ring::wait_slices<C::DMA, 0>();
     }
     __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
+    if (DPH_ABLATE != 3) __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if (i + 4 < H) issue(i + 4);
-    if (i + 1 < H) ring::read_frags<C>(nxt, slot(i + 1), wr, wc, lane);
+    if (i + 4 < H && DPH_ABLATE != 1) issue(i + 4);
+    if (i + 1 < H && DPH_ABLATE != 4) ring::read_frags<C>(nxt, slot(i + 1), wr, wc, lane);
     __builtin_amdgcn_sched_barrier(0);
-    ring::mfma_slice<C>(acc, cur);
+    if (DPH_ABLATE != 2) {
+      ring::mfma_slice<C>(acc, cur);
+    } else {
+#pragma unroll
+      for (int q = 0; q < C::FM; ++q) asm volatile("" ::"v"(cur.a[q]));
+#pragma unroll
+      for (int q = 0; q < C::FN; ++q) asm volatile("" ::"v"(cur.b[q]));
+    }
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): nxt landed (and slot i+1 reads retired)
     __builtin_amdgcn_sched_barrier(0);
@@ -653,13 +676,13 @@ __global__ void __launch_bounds__(C::NT, C::MINB) ring_gemm_kernel(const DphGemm
       if (i < H) issue(i);
     // slice 0: wait until at most the later slices' DMAs remain
     if (H >= 4) {
-      asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+      ring::wait_slices<C::DMA, 3>();
     } else if (H == 3) {
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      ring::wait_slices<C::DMA, 2>();
     } else if (H == 2) {
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      ring::wait_slices<C::DMA, 1>();
     } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      ring::wait_slices<C::DMA, 0>();
     }
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
@@ -812,7 +835,8 @@ using namespace dph;
 // kernel wherever its layout constraints allow (tests exercise both paths in one process)
 static int gemm_path_override() {
   const char* e = getenv("DPH_GEMM_PATH");
-  return (e && !strcmp(e, "small")) ? 1 : (e && !strcmp(e, "big")) ? 2 : (e && !strcmp(e, "mid")) ? 3 : 0;
+  if (!e) return 0;
+  return !strcmp(e, "small") ? 1 : !strcmp(e, "big") ? 2 : !strcmp(e, "mid") ? 3 : 0;
 }
 
 extern "C" int dph_gemm(const DphGemmArgs* args, hipStream_t stream) {
