@@ -57,7 +57,8 @@ _SIGS = {
                           C.c_int),
     "dph_layernorm_fwd_ld": ([vp, vp, vp, vp, vp, vp, vp, i64, i64, i64, f32, f32, u64, S], C.c_int),
     "dph_layernorm_bwd_ld": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, i64, f32, u64, vp, f32, u64, vp, vp, vp,
-                              vp, S], C.c_int),
+                              vp, vp, S], C.c_int),
+    "dph_wave_layernorm": ([vp, vp, i64, i64, f32, vp, S], C.c_int),
     "dph_colsum": ([vp, vp, i64, i64, S], C.c_int),
     "dph_attention_fwd": ([vp, vp, vp, vp, vp, vp, i64, i64, i64, f32, f32, u64, S], C.c_int),
     "dph_attention_bwd_prep": ([vp, vp, vp, vp, vp, i64, i64, i64, S], C.c_int),

@@ -94,7 +94,7 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(
     float drop_p,
     uint64_t seed, bf16_t* __restrict__ branch, float branch_p, uint64_t branch_seed,
     const float* __restrict__ branch_smask, float* __restrict__ branch_colsum, const bf16_t* __restrict__ branch_pre,
-    float* __restrict__ branch_sdot) {
+    float* __restrict__ branch_sdot, const bf16_t* __restrict__ dx_add) {
   __shared__ float red[4][3][LN_MAXV * 256];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -150,7 +150,17 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(
           o[i] = ok ? rstd * (g[c][i] - s1 - xh[c][i] * s2) : 0.f;
           if (xscale && ok) o[i] *= xscale[col + i];
         }
-        *reinterpret_cast<uint2*>(dx + row * ld + col) = make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
+        if (dx_add) {
+          // other gradient paths into the LN input (pre-norm residual); the branch output below
+          // stays the LN-path gradient only
+          const uint2 ra = *reinterpret_cast<const uint2*>(dx_add + row * ld + col);
+          const float ad[4] = {__uint_as_float(ra.x << 16), __uint_as_float(ra.x & 0xffff0000u),
+                               __uint_as_float(ra.y << 16), __uint_as_float(ra.y & 0xffff0000u)};
+          *reinterpret_cast<uint2*>(dx + row * ld + col) =
+              make_uint2(pack2bf(o[0] + ad[0], o[1] + ad[1]), pack2bf(o[2] + ad[2], o[3] + ad[3]));
+        } else {
+          *reinterpret_cast<uint2*>(dx + row * ld + col) = make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
+        }
         if (branch) {
           float bo[4];
           float pre[4] = {0.f, 0.f, 0.f, 0.f};
@@ -202,6 +212,47 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(
     sdot = wave_sum(sdot);
     if (lane == 0) atomicAdd(branch_sdot, sdot);
   }
+}
+
+// Per-utterance waveform LayerNorm (model.py:96-103, wav2vec2-Large normalize_waveform): each
+// row's first len samples -> (x - mean) * rsqrt(var + eps) (no affine, biased variance), the
+// rest -> 0.  One 1024-thread block per utterance; fp64 sums (S = 160 000 samples).
+__global__ void __launch_bounds__(1024) wave_norm_kernel(const float* __restrict__ x,
+                                                         const int64_t* __restrict__ lengths, int64_t S, float eps,
+                                                         float* __restrict__ y) {
+  __shared__ double red[2][16];
+  const int64_t b = blockIdx.x;
+  const int64_t L = lengths ? min<int64_t>(max<int64_t>(lengths[b], 0), S) : S;
+  const float* xr = x + b * S;
+  double s1 = 0.0, s2 = 0.0;
+  for (int64_t i = threadIdx.x; i < L; i += blockDim.x) {
+    const double v = xr[i];
+    s1 += v;
+    s2 += v * v;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    s1 += __shfl_xor(s1, o, 64);
+    s2 += __shfl_xor(s2, o, 64);
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red[0][w] = s1;
+    red[1][w] = s2;
+  }
+  __syncthreads();
+  double t1 = 0.0, t2 = 0.0;
+  for (int i = 0; i < (int)(blockDim.x >> 6); ++i) {
+    t1 += red[0][i];
+    t2 += red[1][i];
+  }
+  const double n = L > 0 ? (double)L : 1.0;
+  const double mean = t1 / n;
+  const double var = max(t2 / n - mean * mean, 0.0);
+  const float m = (float)mean;
+  const float r = (float)(1.0 / sqrt(var + (double)eps));
+  float* yr = y + b * S;
+  for (int64_t i = threadIdx.x; i < S; i += blockDim.x) yr[i] = i < L ? (xr[i] - m) * r : 0.f;
 }
 
 // out[n] += sum_m x[m][n]; block = 64 x 4 threads, 8 columns per thread
@@ -269,7 +320,7 @@ extern "C" int dph_layernorm_bwd_ld(const void* dy, const void* x, const float* 
                                     int64_t rows, int64_t D, int64_t ld, float dropout_p, uint64_t seed, void* branch,
                                     float branch_p, uint64_t branch_seed, const float* branch_smask,
                                     float* branch_colsum, const void* branch_pre, float* branch_sdot,
-                                    hipStream_t stream) {
+                                    const void* dx_add, hipStream_t stream) {
   DPH_REQUIRE(dy && x && gamma && mean && rstd && dx, "dph_layernorm_bwd: null pointer");
   if (ld == 0) ld = D;
   DPH_REQUIRE(D >= 1 && ld >= D && ld % 4 == 0 && ld <= LN_MAXV * 256 && rows > 0,
@@ -281,8 +332,16 @@ extern "C" int dph_layernorm_bwd_ld(const void* dy, const void* x, const float* 
                      reinterpret_cast<const bf16_t*>(dy), reinterpret_cast<const bf16_t*>(x), xscale, gamma, mean,
                      rstd, reinterpret_cast<bf16_t*>(dx), dgamma, dbeta, rows, (int)D, (int)ld, dropout_p, seed,
                      reinterpret_cast<bf16_t*>(branch), branch_p, branch_seed, branch_smask, branch_colsum,
-                     reinterpret_cast<const bf16_t*>(branch_pre), branch_sdot);
+                     reinterpret_cast<const bf16_t*>(branch_pre), branch_sdot,
+                     reinterpret_cast<const bf16_t*>(dx_add));
   return check_launch("dph_layernorm_bwd");
+}
+
+extern "C" int dph_wave_layernorm(const float* x, const int64_t* lengths, int64_t B, int64_t S, float eps, float* y,
+                                  hipStream_t stream) {
+  DPH_REQUIRE(x && y && B > 0 && S > 0, "dph_wave_layernorm: bad args");
+  hipLaunchKernelGGL(wave_norm_kernel, dim3((unsigned)B), dim3(1024), 0, stream, x, lengths, S, eps, y);
+  return check_launch("dph_wave_layernorm");
 }
 
 extern "C" int dph_layernorm_bwd(const void* dy, const void* x, const float* xscale, const float* gamma,
@@ -293,7 +352,7 @@ extern "C" int dph_layernorm_bwd(const void* dy, const void* x, const float* xsc
                                  hipStream_t stream) {
   return dph_layernorm_bwd_ld(dy, x, xscale, gamma, mean, rstd, dx, dgamma, dbeta, rows, D, D, dropout_p, seed,
                               branch, branch_p, branch_seed, branch_smask, branch_colsum, branch_pre, branch_sdot,
-                              stream);
+                              nullptr, stream);
 }
 
 extern "C" int dph_colsum(const void* x, float* out, int64_t rows, int64_t cols, hipStream_t stream) {

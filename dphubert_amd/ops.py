@@ -575,7 +575,7 @@ class FeatureProjectionFn(torch.autograd.Function):
         dlw, _ = go.buf(p_lw)
         dlb, _ = go.buf(p_lb)
         call("dph_layernorm_bwd_ld", ptr(dxn), ptr(x), None, ptr(ln_w), ptr(mu), ptr(rs), ptr(dx), ptr(dlw), ptr(dlb),
-             M, C, Cp, 0.0, 0, None, 0.0, 0, None, None, None, None, _s())
+             M, C, Cp, 0.0, 0, None, 0.0, 0, None, None, None, None, None, _s())
         del ws
         go.done()
         return dx, go.ret(p_lw), go.ret(p_lb), go.ret(p_w), go.ret(p_b), None
@@ -587,6 +587,32 @@ class FeatureProjectionFn(torch.autograd.Function):
 def _weight_norm_ws(R: int, K: int, dev):
     """Workspace of the deterministic per-tap reduction in dph_weight_norm_{fwd,bwd} (64 rows/block)."""
     return torch.empty(-(-R // 64) * K, dtype=F32, device=dev)
+
+
+class LayerNormFn(torch.autograd.Function):
+    """Plain nn.LayerNorm over the last dim of (rows, D) bf16 (the final LN of a pre-norm
+    Transformer.forward, components.py:903-904)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        M, D = x.shape
+        y = torch.empty_like(x)
+        mu = torch.empty(M, dtype=F32, device=x.device)
+        rs = torch.empty(M, dtype=F32, device=x.device)
+        call("dph_layernorm_fwd", ptr(x), None, ptr(w), ptr(b), ptr(y), ptr(mu), ptr(rs), M, D, 1e-5, 0.0, 0, _s())
+        ctx.save_for_backward(x, w, mu, rs)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, mu, rs = ctx.saved_tensors
+        M, D = x.shape
+        dx = torch.empty_like(x)
+        dw = zeros_f32(D, x.device)
+        db = zeros_f32(D, x.device)
+        call("dph_layernorm_bwd", ptr(dy.contiguous()), ptr(x), None, ptr(w), ptr(mu), ptr(rs), ptr(dx), ptr(dw),
+             ptr(db), M, D, 0.0, 0, None, 0.0, 0, None, None, None, None, _s())
+        return dx, dw, db
 
 
 class PosConvFn(torch.autograd.Function):
@@ -620,8 +646,11 @@ class PosConvFn(torch.autograd.Function):
         mu = torch.empty(M, dtype=F32, device=dev)
         rs = torch.empty(M, dtype=F32, device=dev)
         seed = SEEDS.next() if cfg["p"] > 0 else 0
-        call("dph_layernorm_fwd", ptr(s0), None, ptr(ln_w), ptr(ln_b), ptr(h), ptr(mu), ptr(rs), M, D, 1e-5,
-             cfg["p"], seed, _s())
+        if cfg.get("ln", True):
+            call("dph_layernorm_fwd", ptr(s0), None, ptr(ln_w), ptr(ln_b), ptr(h), ptr(mu), ptr(rs), M, D, 1e-5,
+                 cfg["p"], seed, _s())
+        else:   # pre-norm Transformer (components.py:1283 flag): no LayerNorm here, dropout only
+            call("dph_branch_bwd", ptr(s0), ptr(h), M, D, cfg["p"], seed, None, None, 0, None, None, None, _s())
         if need:
             ctx.cfg = cfg
             ctx.seed = seed
@@ -642,10 +671,13 @@ class PosConvFn(torch.autograd.Function):
         ds0 = torch.empty_like(dh)
         p_bias, p_lw, p_lb = ctx.params
         go = GradOut(dev)
-        dlw, _ = go.buf(p_lw)
-        dlb, _ = go.buf(p_lb)
-        call("dph_layernorm_bwd", ptr(dh), ptr(s0), None, ptr(ln_w), ptr(mu), ptr(rs), ptr(ds0), ptr(dlw), ptr(dlb),
-             M, D, cfg["p"], ctx.seed, None, 0.0, 0, None, None, None, None, _s())
+        if cfg.get("ln", True):
+            dlw, _ = go.buf(p_lw)
+            dlb, _ = go.buf(p_lb)
+            call("dph_layernorm_bwd", ptr(dh), ptr(s0), None, ptr(ln_w), ptr(mu), ptr(rs), ptr(ds0), ptr(dlw),
+                 ptr(dlb), M, D, cfg["p"], ctx.seed, None, 0.0, 0, None, None, None, None, _s())
+        else:
+            call("dph_branch_bwd", ptr(dh), ptr(ds0), M, D, cfg["p"], ctx.seed, None, None, 0, None, None, None, _s())
         dz = torch.empty_like(ds0)
         call("dph_gelu_mask_bwd", ptr(ds0), ptr(z), None, ptr(dz), None, M, D, _s())
         db, _ = go.buf(p_bias)
@@ -693,6 +725,10 @@ class EncoderLayerFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, cfg, h, wq, wk, wv, bq, bk, bv, wo, bo, ln1_w, ln1_b, w1, b1, w2, b2, ln2_w, ln2_b, hm, lma,
                 im, lmf):
+        if cfg.get("pre_norm"):
+            return EncoderLayerFn._forward_pre(ctx, cfg, h, wq, wk, wv, bq, bk, bv, wo, bo, ln1_w, ln1_b, w1, b1, w2,
+                                               b2, ln2_w, ln2_b, hm, lma, im, lmf)
+        ctx.pre = False
         M, D = h.shape
         dev = h.device
         need = cfg["need_grad"]
@@ -758,8 +794,154 @@ class EncoderLayerFn(torch.autograd.Function):
             ctx.save_for_backward(h, s1, mu1, rs1, h1, s2, mu2, rs2, ln1_w, ln2_w, hm, lma, im, lmf)
         return out
 
+    # ---------------- pre-norm (wav2vec2 / HuBERT Large, components.py:835-845) ----------------
+    #   s1  = h + drop(attn(LN1(h))) * layer_mask_att
+    #   out = s1 + FFN(LN2(s1)) * layer_mask_ffn        (no LayerNorm after the block)
+    @staticmethod
+    def _forward_pre(ctx, cfg, h, wq, wk, wv, bq, bk, bv, wo, bo, ln1_w, ln1_b, w1, b1, w2, b2, ln2_w, ln2_b, hm,
+                     lma, im, lmf):
+        M, D = h.shape
+        dev = h.device
+        need = cfg["need_grad"]
+        B, T, H = cfg["B"], cfg["T"], cfg["H"]
+        use_att = wq is not None
+        use_ff = w1 is not None
+        sv = {}
+        xn1 = mu1 = rs1 = xn2 = mu2 = rs2 = None
+        if use_att:
+            xn1 = torch.empty_like(h)
+            mu1 = torch.empty(M, dtype=F32, device=dev)
+            rs1 = torch.empty(M, dtype=F32, device=dev)
+            call("dph_layernorm_fwd", ptr(h), None, ptr(ln1_w), ptr(ln1_b), ptr(xn1), ptr(mu1), ptr(rs1), M, D, 1e-5,
+                 0.0, 0, _s())
+            Dh = wq.shape[0]
+            Wqkv = bf16_image(wq, wk, wv)
+            qkv = K.linear_fwd(xn1, Wqkv, f32_cat(bq, bk, bv))
+            o_u = torch.empty(M, Dh, dtype=BF16, device=dev)
+            o_m = torch.empty(M, Dh, dtype=BF16, device=dev)
+            lse = torch.empty(B * H * T, dtype=F32, device=dev)
+            seed_a = SEEDS.next() if cfg["p_attn"] > 0 else 0
+            call("dph_attention_fwd", ptr(qkv), ptr(o_u), ptr(o_m), ptr(lse), ptr(hm), ptr(cfg["lengths"]), B, T, H,
+                 cfg["head_dim"] ** -0.5, cfg["p_attn"], seed_a, _s())
+            Wo = bf16_image(wo)
+            seed_d = SEEDS.next() if cfg["p_drop"] > 0 else 0
+            a_pre = torch.empty(M, D, dtype=BF16, device=dev) if (need and lma is not None) else None
+            s1 = K.linear_fwd(o_m, Wo, bo, smask=lma, residual=h, dropout_p=cfg["p_drop"], seed=seed_d,
+                              pre_out=a_pre)
+            sv.update(Wqkv=Wqkv, qkv=qkv, o_u=o_u, o_m=o_m, lse=lse, Wo=Wo, a_pre=a_pre, seed_a=seed_a, seed_d=seed_d)
+        else:
+            s1 = h
+        if use_ff:
+            xn2 = torch.empty_like(h)
+            mu2 = torch.empty(M, dtype=F32, device=dev)
+            rs2 = torch.empty(M, dtype=F32, device=dev)
+            call("dph_layernorm_fwd", ptr(s1), None, ptr(ln2_w), ptr(ln2_b), ptr(xn2), ptr(mu2), ptr(rs2), M, D,
+                 1e-5, 0.0, 0, _s())
+            F_ = w1.shape[0]
+            Fp = pad8(F_)
+            W1 = padded_image(w1, Fp, D)
+            W2 = padded_image(w2, D, Fp)
+            b1p, imp = padded_vec(b1, Fp), padded_vec(im, Fp)
+            seed_i = SEEDS.next() if cfg["p_interm"] > 0 else 0
+            u = torch.empty(M, Fp, dtype=BF16, device=dev) if need else None
+            f = K.linear_fwd(xn2, W1, b1p, act=K.ACT_GELU, pre_out=u, colmask=imp, dropout_p=cfg["p_interm"],
+                             seed=seed_i)
+            seed_o = SEEDS.next() if cfg["p_drop"] > 0 else 0
+            y_pre = torch.empty(M, D, dtype=BF16, device=dev) if (need and lmf is not None) else None
+            out = K.linear_fwd(f, W2, b2, smask=lmf, residual=s1, dropout_p=cfg["p_drop"], seed=seed_o,
+                               pre_out=y_pre)
+            sv.update(W1=W1, W2=W2, u=u, f=f, y_pre=y_pre, seed_i=seed_i, seed_o=seed_o, F=F_, imp=imp)
+        else:
+            out = s1.clone() if s1 is h else s1
+        if need:
+            ctx.pre = True
+            ctx.cfg = cfg
+            ctx.sv = sv
+            ctx.params = dict(wq=wq, wk=wk, wv=wv, bq=bq, bk=bk, bv=bv, wo=wo, bo=bo, ln1_w=ln1_w, ln1_b=ln1_b, w1=w1,
+                              b1=b1, w2=w2, b2=b2, ln2_w=ln2_w, ln2_b=ln2_b)
+            ctx.flags = (use_att, use_ff, hm is not None, lma is not None, im is not None, lmf is not None)
+            ctx.save_for_backward(h, xn1, mu1, rs1, s1, xn2, mu2, rs2, ln1_w, ln2_w, hm, lma, im, lmf)
+        return out
+
+    @staticmethod
+    def _backward_pre(ctx, dout):
+        h, xn1, mu1, rs1, s1, xn2, mu2, rs2, ln1_w, ln2_w, hm, lma, im, lmf = ctx.saved_tensors
+        cfg = ctx.cfg
+        sv = ctx.sv
+        use_att, use_ff, has_hm, has_lma, has_im, has_lmf = ctx.flags
+        B, T, H = cfg["B"], cfg["T"], cfg["H"]
+        M, D = h.shape
+        dev = h.device
+        dout = dout.contiguous()
+        z = lambda n: zeros_f32(n, dev)  # noqa: E731
+        pr = ctx.params
+        go = GradOut(dev)
+        g = {}
+        # ---- FFN branch: out = s1 + drop(FFN(LN2(s1))) * lmf ----
+        if use_ff:
+            dy = torch.empty_like(dout)
+            db2, _ = go.buf(pr["b2"])
+            g["lmf"] = z(1) if has_lmf else None
+            call("dph_branch_bwd", ptr(dout), ptr(dy), M, D, cfg["p_drop"], sv["seed_o"], ptr(lmf), None, 0, ptr(db2),
+                 ptr(sv["y_pre"]) if has_lmf else None, ptr(g["lmf"]), _s())
+            F_ = sv["F"]
+            dw2, direct = go.buf(pr["w2"], zero=False)
+            k1 = K.linear_wgrad(dy, sv["f"], dw2, accumulate=direct, k_in=F_)
+            db1, _ = go.buf(pr["b1"])
+            g["im"] = z(F_) if has_im else None
+            du = K.linear_dgrad(dy, sv["W2"], act=K.ACT_GELU_BWD, aux_in=sv["u"], colmask=sv["imp"], colsum_out=db1,
+                                colsum_aux=g["im"] if has_im else z(F_), dropout_p=cfg["p_interm"],
+                                seed=sv["seed_i"], colsum_n=F_)
+            dw1, direct = go.buf(pr["w1"], zero=False)
+            k2 = K.linear_wgrad(du, xn2, dw1, accumulate=direct, n_out=F_)
+            dxn2 = K.linear_dgrad(du, sv["W1"])
+            ds1 = torch.empty_like(dout)
+            dln2w, _ = go.buf(pr["ln2_w"])
+            dln2b, _ = go.buf(pr["ln2_b"])
+            call("dph_layernorm_bwd_ld", ptr(dxn2), ptr(s1), None, ptr(ln2_w), ptr(mu2), ptr(rs2), ptr(ds1),
+                 ptr(dln2w), ptr(dln2b), M, D, D, 0.0, 0, None, 0.0, 0, None, None, None, None, ptr(dout), _s())
+            del k1, k2
+        else:
+            ds1 = dout
+        # ---- attention branch: s1 = h + drop(attn(LN1(h))) * lma ----
+        if use_att:
+            da = torch.empty_like(dout)
+            dbo, _ = go.buf(pr["bo"])
+            g["lma"] = z(1) if has_lma else None
+            call("dph_branch_bwd", ptr(ds1), ptr(da), M, D, cfg["p_drop"], sv["seed_d"], ptr(lma), None, 0, ptr(dbo),
+                 ptr(sv["a_pre"]) if has_lma else None, ptr(g["lma"]), _s())
+            dwo, direct = go.buf(pr["wo"], zero=False)
+            k3 = K.linear_wgrad(da, sv["o_m"], dwo, accumulate=direct)
+            do_m = K.linear_dgrad(da, sv["Wo"])
+            Dvec = torch.empty(B * H * T, dtype=F32, device=dev)
+            g["hm"] = z(H) if has_hm else None
+            call("dph_attention_bwd_prep", ptr(do_m), ptr(sv["o_u"]), ptr(hm), ptr(Dvec), ptr(g["hm"]), B, T, H, _s())
+            dqkv = torch.empty_like(sv["qkv"])
+            call("dph_attention_bwd", ptr(sv["qkv"]), ptr(do_m), ptr(hm), ptr(sv["lse"]), ptr(Dvec), ptr(dqkv),
+                 ptr(cfg["lengths"]), B, T, H, cfg["head_dim"] ** -0.5, cfg["p_attn"], sv["seed_a"], _s())
+            dbqkv, _ = go.buf(pr["bq"], pr["bk"], pr["bv"])
+            call("dph_colsum", ptr(dqkv), ptr(dbqkv), M, dqkv.shape[1], _s())
+            dwqkv, direct = go.buf(pr["wq"], pr["wk"], pr["wv"], zero=False)
+            k4 = K.linear_wgrad(dqkv, xn1, dwqkv, accumulate=direct)
+            dxn1 = K.linear_dgrad(dqkv, sv["Wqkv"])
+            dh = torch.empty_like(dout)
+            dln1w, _ = go.buf(pr["ln1_w"])
+            dln1b, _ = go.buf(pr["ln1_b"])
+            call("dph_layernorm_bwd_ld", ptr(dxn1), ptr(h), None, ptr(ln1_w), ptr(mu1), ptr(rs1), ptr(dh),
+                 ptr(dln1w), ptr(dln1b), M, D, D, 0.0, 0, None, 0.0, 0, None, None, None, None, ptr(ds1), _s())
+            del k3, k4
+        else:
+            dh = ds1
+        go.done()
+        order = ["wq", "wk", "wv", "bq", "bk", "bv", "wo", "bo", "ln1_w", "ln1_b", "w1", "b1", "w2", "b2", "ln2_w",
+                 "ln2_b"]
+        return (None, dh) + tuple(go.ret(pr[k]) for k in order) + (g.get("hm"), g.get("lma"), g.get("im"),
+                                                                    g.get("lmf"))
+
     @staticmethod
     def backward(ctx, dout):
+        if ctx.pre:
+            return EncoderLayerFn._backward_pre(ctx, dout)
         h, s1, mu1, rs1, h1, s2, mu2, rs2, ln1_w, ln2_w, hm, lma, im, lmf = ctx.saved_tensors
         cfg = ctx.cfg
         sv = ctx.sv

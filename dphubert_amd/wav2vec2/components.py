@@ -393,7 +393,7 @@ class FeedForward(Module):
 
 
 class EncoderLayer(Module):
-    """Attention + FFN block, post-norm (Base) (components.py:794-865)."""
+    """Attention + FFN block, post-norm (Base) or pre-norm (Large) (components.py:794-865)."""
 
     def __init__(self, attention: Optional[Module], dropout: float, layer_norm_first: bool,
                  feed_forward: Optional[Module], embed_dim: int):
@@ -408,8 +408,6 @@ class EncoderLayer(Module):
 
     def forward(self, x: Tensor, attention_mask=None, position_bias: Optional[Tensor] = None,
                 key_padding_mask: Optional[Tensor] = None, key_len: Optional[Tensor] = None):
-        if self.layer_norm_first:
-            raise NotImplementedError("pre-norm encoder layers (Large) are not on the HIP path yet")
         B, T, D = x.shape
         att, ff = self.attention, self.feed_forward
         tr = self.training
@@ -430,6 +428,7 @@ class EncoderLayer(Module):
             "p_drop": self.dropout.p if tr else 0.0,
             "p_interm": ff.intermediate_dropout.p if (tr and ff is not None) else 0.0,
             "lengths": key_len,
+            "pre_norm": bool(self.layer_norm_first),
         }
         if ff is not None and tr and ff.output_dropout.p != self.dropout.p:
             raise NotImplementedError("FFN output dropout != layer dropout")
@@ -474,13 +473,13 @@ class Transformer(Module):
         self.layers = layers
 
     def _preprocess(self, x: Tensor):
-        """x + pos_conv(x) -> LayerNorm -> dropout (components.py:885-892; Base has the LN)."""
-        if not self.layer_norm_first:
-            raise NotImplementedError("Transformer without the preprocess LayerNorm (Large) is not on the HIP path yet")
+        """x + pos_conv(x) -> [LayerNorm] -> dropout (components.py:885-892): the LN runs for post-norm
+        (Base) encoders only -- the flag is inverted at construction (components.py:1283)."""
         B, T, D = x.shape
         pc = self.pos_conv_embed
         need = torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
-        cfg = {"B": B, "T": T, "G": pc.groups, "p": self.dropout.p if self.training else 0.0, "need_grad": need}
+        cfg = {"B": B, "T": T, "G": pc.groups, "p": self.dropout.p if self.training else 0.0, "need_grad": need,
+               "ln": bool(self.layer_norm_first)}
         h = ops.PosConvFn.apply(x.reshape(B * T, D), pc.conv.weight_g, pc.conv.weight_v, pc.conv.bias,
                                 self.layer_norm.weight, self.layer_norm.bias, cfg)
         return h.view(B, T, D)
@@ -491,6 +490,9 @@ class Transformer(Module):
         for layer in self.layers:
             if not (self.training and random.random() <= self.layer_drop):
                 x, position_bias = layer(x, attention_mask, position_bias=position_bias, key_len=key_len)
+        if not self.layer_norm_first:
+            B, T, D = x.shape
+            x = ops.LayerNormFn.apply(x.reshape(B * T, D), self.layer_norm.weight, self.layer_norm.bias).view(B, T, D)
         return x
 
     def get_intermediate_outputs(self, x: Tensor, attention_mask=None, num_layers: Optional[int] = None,

@@ -31,11 +31,20 @@ class Wav2Vec2Model(Module):
         self._np_key = None
 
     def _normalize(self, waveforms, lengths):
-        # model.py:96-103 (per-utterance layer norm); host loop as in the reference (Large configs only)
-        if lengths is not None:
-            waves = [F.layer_norm(w[:l], (int(l),)) for w, l in zip(waveforms, lengths)]
-            return torch.nn.utils.rnn.pad_sequence(waves, batch_first=True)
-        return F.layer_norm(waveforms, waveforms.shape[-1:])
+        """model.py:96-103: per-utterance LayerNorm over each waveform's valid samples (HIP kernel),
+        zero padding after; like the reference's pad_sequence, the batch is cut to max(lengths)."""
+        if not waveforms.is_cuda:
+            raise ValueError("normalize_waveform runs on the HIP path only: pass a device tensor")
+        x = waveforms.contiguous().float()
+        B, S = x.shape
+        ln = lengths.to(x.device, torch.int64).contiguous() if lengths is not None else None
+        y = torch.empty_like(x)
+        ops.call("dph_wave_layernorm", ops.ptr(x), ops.ptr(ln), B, S, 1e-5, ops.ptr(y), ops._s())
+        if ln is not None:
+            lmax = int(ln.max())
+            if lmax < S:
+                y = y[:, :lmax].contiguous()
+        return y
 
     def extract_features(self, waveforms: Tensor, lengths: Optional[Tensor] = None,
                          num_layers: Optional[int] = None) -> Tuple[List[Tensor], Optional[Tensor]]:

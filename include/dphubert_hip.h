@@ -118,11 +118,18 @@ int dph_layernorm_bwd(const void* dy, const void* x, const float* xscale, const 
 int dph_layernorm_fwd_ld(const void* x, const float* xscale, const float* gamma, const float* beta, void* y,
                          float* mean, float* rstd, int64_t rows, int64_t D, int64_t ld, float eps, float dropout_p,
                          uint64_t seed, hipStream_t stream);
+/* dx_add (optional, bf16 with the same stride): added to dx -- the pre-norm residual path
+ * (components.py:835-850: x + f(LN(x))); the branch output stays the LN-path gradient */
 int dph_layernorm_bwd_ld(const void* dy, const void* x, const float* xscale, const float* gamma, const float* mean,
                          const float* rstd, void* dx, float* dgamma, float* dbeta, int64_t rows, int64_t D, int64_t ld,
                          float dropout_p, uint64_t seed, void* branch, float branch_p, uint64_t branch_seed,
                          const float* branch_smask, float* branch_colsum, const void* branch_pre, float* branch_sdot,
-                         hipStream_t stream);
+                         const void* dx_add, hipStream_t stream);
+/* per-utterance waveform LayerNorm, model.py:96-103 (normalize_waveform, wav2vec2-Large):
+ * y[b][:len_b] = (x - mean) / sqrt(var + eps) over the first len_b samples, y[b][len_b:] = 0
+ * (lengths == NULL: full rows) */
+int dph_wave_layernorm(const float* x, const int64_t* lengths, int64_t B, int64_t S, float eps, float* y,
+                       hipStream_t stream);
 
 /* column sums of a bf16 matrix (bias gradients): out[n] += sum_m x[m][n] */
 int dph_colsum(const void* x, float* out, int64_t rows, int64_t cols, hipStream_t stream);

@@ -300,3 +300,26 @@ def test_hardconcrete_and_expected_params():
     mk.backward(gm.to(DEV))
     mr.backward(gm)
     assert rel_l2(hc.log_alpha.grad.cpu(), la.grad) < 1e-4
+
+
+@pytest.mark.parametrize("lengths", [None, [16000, 9001, 12000]])
+def test_wave_layernorm_vs_reference_semantics(lengths):
+    """normalize_waveform (model.py:96-103): per-utterance LN over the valid samples, zero pad,
+    batch cut to max(lengths) like pad_sequence."""
+    import torch.nn.functional as F
+    from dphubert_amd.wav2vec2.model import wav2vec2_model
+    from dphubert_amd.synthetic import HUBERT_BASE_CONFIG
+    cfg = dict(HUBERT_BASE_CONFIG, normalize_waveform=True, encoder_num_layers=1, encoder_use_attention=[True],
+               encoder_use_feed_forward=[True], encoder_num_heads=[12], encoder_ff_interm_features=[3072])
+    m = wav2vec2_model(**cfg)
+    torch.manual_seed(3)
+    w = torch.randn(3, 16000) * 0.3 + 0.05
+    ln = torch.tensor(lengths) if lengths is not None else None
+    got = m._normalize(w.to(DEV), ln.to(DEV) if ln is not None else None).cpu()
+    if ln is None:
+        want = F.layer_norm(w, w.shape[-1:])
+    else:
+        want = torch.nn.utils.rnn.pad_sequence([F.layer_norm(x[:l], (int(l),)) for x, l in zip(w, ln)],
+                                               batch_first=True)
+    assert got.shape == want.shape
+    assert torch.allclose(got, want, atol=2e-5, rtol=1e-5)

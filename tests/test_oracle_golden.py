@@ -143,3 +143,12 @@ def test_oracle_pruned_forward_matches_reference():
     for h, ck in zip(hs, fx["pruned_hidden_ck"]):
         e_sample, e_sq = ck_close(h, ck)
         assert e_sample < 1e-4 and e_sq < 1e-5, (e_sample, e_sq)
+
+
+def test_prenorm_normalize_waveform_g6():
+    """wav2vec2-Large-style layers: pre-norm encoder + per-utterance waveform LayerNorm."""
+    fx = load_golden("g6_prenorm_normwave.pt")
+    out = _run_fixture(fx)
+    _check_step(fx, out)
+    for h, g in zip(out["student_hiddens"], fx["student_hiddens"]):
+        assert rel_l2(h, g) < 1e-5

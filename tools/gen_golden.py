@@ -325,6 +325,14 @@ def gen_data():
     return out
 
 
+def gen_prenorm():
+    """G6: wav2vec2-Large-style layers (pre-norm, normalize_waveform=True; run_large.sh:11 teacher
+    family) on the 2-layer shape, padded batch, all five pruning units, regulariser active."""
+    cfg = small_cfg(2, encoder_layer_norm_first=True, normalize_waveform=True)
+    return run_step(cfg, cfg, "0.1,2", B=2, S=24000, units="conv,head,interm,attlayer,ffnlayer",
+                    lambdas=(0.2, 0.1), global_step=2500, lengths=[24000, 18000], full=True)
+
+
 def main():
     OUT.mkdir(parents=True, exist_ok=True)
     torch.set_num_threads(8)
@@ -332,8 +340,14 @@ def main():
         torch.save(gen_data(), OUT / "g5_data.pt")
         print("g5 done")
         return
+    if "--only-prenorm" in sys.argv:
+        torch.save(gen_prenorm(), OUT / "g6_prenorm_normwave.pt")
+        print("g6 done")
+        return
     torch.save(gen_data(), OUT / "g5_data.pt")
     print("g5 done")
+    torch.save(gen_prenorm(), OUT / "g6_prenorm_normwave.pt")
+    print("g6 done")
     torch.save(gen_ops(), OUT / "g1_ops.pt")
     print("g1 done")
     # G2: 2-layer smoke step (BASELINE config 1 shape-reduced to 2 s), units conv,head,interm, reg active
