@@ -105,6 +105,9 @@ def lib():
     L = C.CDLL(str(LIB_PATH))
     L.dph_last_error.restype = C.c_char_p
     L.dph_last_error.argtypes = []
+    if hasattr(L, "dph_gemm_variant"):
+        L.dph_gemm_variant.restype = C.c_char_p
+        L.dph_gemm_variant.argtypes = [C.POINTER(DphGemmArgs)]
     missing = []
     for name, (args, res) in _SIGS.items():
         try:
@@ -122,7 +125,7 @@ def lib():
 
 
 def exported_symbols():
-    return ["dph_last_error"] + list(_SIGS)
+    return ["dph_last_error", "dph_gemm_variant"] + list(_SIGS)
 
 
 def check(rc: int, what: str = ""):

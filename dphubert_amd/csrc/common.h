@@ -102,15 +102,24 @@ __device__ __forceinline__ void gelu_and_grad(float x, float& g, float& dg) {
   dg = cdf + x * pdf;
 }
 
-// Counter-based RNG: splitmix64 finaliser of (seed, element index).  The same
-// (seed, index) always gives the same bits, so forward and backward kernels
-// regenerate identical dropout / HardConcrete noise without storing masks.
+// Counter-based RNG: two rounds of a 32-bit avalanche hash (Wellons' low-bias constants) over the
+// folded (seed, element index).  The same (seed, index) always gives the same bits, so forward
+// and backward kernels regenerate identical dropout / HardConcrete noise without storing masks.
+// 32-bit arithmetic only: the previous splitmix64 finaliser (3 64-bit multiplies per element)
+// cost 60 % of the attention forward at p = 0.1, where every score element draws a number.
+__device__ __forceinline__ uint32_t hash32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x21f0aaadu;
+  x ^= x >> 15;
+  x *= 0x735a2d97u;
+  x ^= x >> 15;
+  return x;
+}
+
 __device__ __forceinline__ uint32_t rand_u32(uint64_t seed, uint64_t idx) {
-  uint64_t z = seed * 0x9E3779B97F4A7C15ull + idx + 0x632BE59BD9B4E019ull;
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  z ^= z >> 31;
-  return (uint32_t)(z >> 32);
+  uint32_t x = (uint32_t)idx ^ ((uint32_t)(idx >> 32) * 0x9E3779B9u) ^ (uint32_t)seed;
+  x = hash32(x);
+  return hash32(x ^ (uint32_t)(seed >> 32));
 }
 
 // uniform in [0,1) with 24 random bits

@@ -839,6 +839,36 @@ static int gemm_path_override() {
   return !strcmp(e, "small") ? 1 : !strcmp(e, "big") ? 2 : !strcmp(e, "mid") ? 3 : 0;
 }
 
+// 0: 128x128 register-staged kernel, 1: ring Mid (128x128), 2: ring Big (256x256)
+static int gemm_kind(const DphGemmArgs& a, int64_t kchunk) {
+  const bool ring_ok = a.a_kcontig && a.b_kcontig && a.K % ring::KS == 0 && kchunk % ring::KS == 0;
+  const int64_t tiles256 = cdiv(a.M, ring::Big::BM) * cdiv(a.N, ring::Big::BN) * a.batch * a.splits;
+  int kind = !ring_ok ? 0 : (tiles256 >= 480 ? 2 : 1);
+  const int path = gemm_path_override();
+  if (path == 1) kind = 0;
+  if (path == 2 && ring_ok) kind = 2;
+  if (path == 3 && ring_ok) kind = 1;
+  return kind;
+}
+
+static int64_t gemm_kchunk(const DphGemmArgs& a) {
+  return a.splits > 1 ? cdiv(cdiv(a.K, a.splits), BK) * BK : a.K;
+}
+
+extern "C" const char* dph_gemm_variant(const DphGemmArgs* args) {
+  if (!args) return "";
+  const DphGemmArgs& a = *args;
+  switch (gemm_kind(a, gemm_kchunk(a))) {
+    case 2: return "ring::Cfg<256, 256, 128, 64>";
+    case 1: return "ring::Cfg<128, 128, 64, 64>";
+    default:
+      if (a.a_kcontig && a.b_kcontig) return "gemm_kernel<true, true>";
+      if (a.a_kcontig) return "gemm_kernel<true, false>";
+      if (a.b_kcontig) return "gemm_kernel<false, true>";
+      return "gemm_kernel<false, false>";
+  }
+}
+
 extern "C" int dph_gemm(const DphGemmArgs* args, hipStream_t stream) {
   DPH_REQUIRE(args != nullptr, "dph_gemm: null args");
   const DphGemmArgs& a = *args;
@@ -868,13 +898,7 @@ extern "C" int dph_gemm(const DphGemmArgs* args, hipStream_t stream) {
   // LDS-DMA ring kernels for k-contiguous A and B with whole 32-deep k-slices: the 256x256 tile
   // when there are >= ~2 full rounds of tiles over the 256 CUs at one block per CU, else the
   // 128x128 tile (DPH_GEMM_PATH=small|big|mid forces a path, for tests)
-  const bool ring_ok = a.a_kcontig && a.b_kcontig && a.K % ring::KS == 0 && kchunk % ring::KS == 0;
-  const int64_t tiles256 = cdiv(a.M, ring::Big::BM) * cdiv(a.N, ring::Big::BN) * a.batch * a.splits;
-  int kind = !ring_ok ? 0 : (tiles256 >= 480 ? 2 : 1);   // 0 small, 1 mid ring, 2 big ring
-  const int path = gemm_path_override();
-  if (path == 1) kind = 0;
-  if (path == 2 && ring_ok) kind = 2;
-  if (path == 3 && ring_ok) kind = 1;
+  const int kind = gemm_kind(a, kchunk);
   if (kind == 2) {
     dim3 gb((unsigned)cdiv(a.N, ring::Big::BN), (unsigned)cdiv(a.M, ring::Big::BM), (unsigned)(a.batch * a.splits));
     DPH_REQUIRE(gb.y < 65536 && gb.z < 65536, "dph_gemm: grid too large");

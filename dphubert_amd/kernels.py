@@ -73,8 +73,9 @@ class LaunchProfiler:
         return out
 
 
-def _variant(a_kcontig, b_kcontig):
-    return f"gemm_kernel<{str(bool(a_kcontig)).lower()}, {str(bool(b_kcontig)).lower()}>"
+def _variant(args):
+    """Name of the kernel dph_gemm launches for these args (matches rocprof kernel names)."""
+    return _lib.lib().dph_gemm_variant(C.byref(args)).decode()
 
 
 def gemm(A: DphMat, B: DphMat, Cm: DphMat, M: int, N: int, K: int, *, a_kcontig: bool, b_kcontig: bool,
@@ -99,7 +100,7 @@ def gemm(A: DphMat, B: DphMat, Cm: DphMat, M: int, N: int, K: int, *, a_kcontig:
     call("dph_gemm", C.byref(args), _stream())
     if prof is not None:
         e1.record()
-        prof.records.append((_variant(a_kcontig, b_kcontig), 2.0 * M * N * K * batch, e0, e1))
+        prof.records.append((_variant(args), 2.0 * M * N * K * batch, e0, e1))
     return ws  # keep alive until the stream consumes it (caching allocator is stream-ordered)
 
 

@@ -94,6 +94,8 @@ typedef struct DphGemmArgs {
 } DphGemmArgs;
 
 int dph_gemm(const DphGemmArgs* args, hipStream_t stream);
+/* name (as it appears in rocprof kernel names) of the kernel dph_gemm launches for these args */
+const char* dph_gemm_variant(const DphGemmArgs* args);
 
 /* ------------------------------------------------------------------------ *
  * LayerNorm over the last dim (rows x D), fp32 statistics, eps=1e-5.
