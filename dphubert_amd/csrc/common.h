@@ -127,10 +127,23 @@ __device__ __forceinline__ float rand_uniform(uint64_t seed, uint64_t idx) {
   return (float)(rand_u32(seed, idx) >> 8) * (1.0f / 16777216.0f);
 }
 
+// Dropout bits: ONE hash32 per PAIR of consecutive elements (element idx uses the low / high 16
+// bits of pair idx >> 1), compared against a 16-bit threshold.  Half the hash work of a per-element
+// draw and a quarter of rand_u32's (v_mul_lo_u32 is a quarter-rate op: the per-element double
+// hash cost ~64 cycles per element in the GEMM epilogues).  p is quantised to 1/65536.
+__device__ __forceinline__ uint32_t drop_thr(float p) { return (uint32_t)(p * 65536.0f + 0.5f); }
+
+__device__ __forceinline__ uint32_t drop_bits2(uint64_t seed, uint64_t pair) {
+  const uint32_t hi = (uint32_t)(pair >> 32) * 0x9E3779B9u + (uint32_t)(seed >> 32) * 0x85EBCA6Bu;
+  return hash32((uint32_t)pair ^ (uint32_t)seed ^ hi);
+}
+
 // dropout keep factor: 0 or 1/(1-p); p == 0 -> 1
 __device__ __forceinline__ float dropout_scale(uint64_t seed, uint64_t idx, float p, float inv_keep) {
   if (p <= 0.f) return 1.0f;
-  return rand_uniform(seed, idx) >= p ? inv_keep : 0.0f;
+  const uint32_t bits = drop_bits2(seed, idx >> 1);
+  const uint32_t u = (idx & 1) ? (bits >> 16) : (bits & 0xffffu);
+  return u >= drop_thr(p) ? inv_keep : 0.0f;
 }
 
 __device__ __forceinline__ float wave_sum(float v) {

@@ -71,7 +71,7 @@ struct Stager {
   int64_t R;            // rows (M or N)
   DphMat d;
 
-  __device__ void init(const DphMat& dm, const bf16_t* b, int64_t tile0, int64_t Rn, int tid) {
+  __device__ __forceinline__ void init(const DphMat& dm, const bf16_t* b, int64_t tile0, int64_t Rn, int tid) {
     d = dm;
     base = b;
     r0 = tile0;
@@ -89,7 +89,7 @@ struct Stager {
 
   // Loads are unconditional (addresses clamped into the operand) so hipcc can keep several
   // tiles in flight with counted vmcnt; out-of-range chunks are zeroed at store time.
-  __device__ void load(uint4 (&reg)[CHUNKS], int64_t k0, int64_t kend, int tid) const {
+  __device__ __forceinline__ void load(uint4 (&reg)[CHUNKS], int64_t k0, int64_t kend, int tid) const {
 #pragma unroll
     for (int i = 0; i < CHUNKS; ++i) {
       int c = tid + NTHREADS * i;
@@ -104,7 +104,7 @@ struct Stager {
     }
   }
 
-  __device__ void store(char* lds, const uint4 (&reg)[CHUNKS], int64_t k0, int64_t kend, int tid) const {
+  __device__ __forceinline__ void store(char* lds, const uint4 (&reg)[CHUNKS], int64_t k0, int64_t kend, int tid) const {
 #pragma unroll
     for (int i = 0; i < CHUNKS; ++i) {
       int c = tid + NTHREADS * i;
@@ -273,6 +273,170 @@ __device__ __forceinline__ void epilogue8(const DphGemmArgs& a, int64_t z, int64
   }
 }
 
+// ---- fast tile epilogue ----------------------------------------------------------------------
+// A thread owns the 8 columns [n, n+8) of the P rows m = mrow0 + RPP*p + (p/JP)*JUMP of a staged
+// fp32 tile (LDS row mrow0-relative RPP*p).
+// gfx9 counts stores in vmcnt, so a global load issued after a store makes its s_waitcnt wait
+// for that store's write acknowledgement: the per-row generic epilogue8 (conditional loads
+// between stores, each behind an s_waitcnt vmcnt(0)) measured 15 us per round of 128x128 tiles,
+// as long as the whole K=768 main loop.  Here every global input (bias / colmask once, then the
+// per-row aux / residual / old-C / row-length values of all P rows) is issued first, retired by
+// one wait, and the stores follow with no load behind them.  Preconditions (tile_epi_ok): full
+// 8-column groups and 16-B aligned rows of C and of the vectors.
+__device__ __forceinline__ bool tile_epi_ok(const DphGemmArgs& a, int64_t n) {
+  const int64_t calign = a.C.row_stride | a.C.batch_stride | a.C.z_outer | a.C.z_inner;
+  const uintptr_t palign = reinterpret_cast<uintptr_t>(a.C.ptr) | reinterpret_cast<uintptr_t>(a.pre_out) |
+                           reinterpret_cast<uintptr_t>(a.aux_in) | reinterpret_cast<uintptr_t>(a.residual);
+  const uintptr_t valign = reinterpret_cast<uintptr_t>(a.bias) | reinterpret_cast<uintptr_t>(a.colmask);
+  // one per-row bf16 input (aux_in OR residual) and a plain (non-accumulating) output
+  return n + 8 <= a.N && (calign & 7) == 0 && (palign & 15) == 0 && (valign & 15) == 0 &&
+         (a.vec_z_inner & 3) == 0 && !(a.aux_in && a.residual) && a.c_dtype != DPH_OUT_F32_ACCUM &&
+         (a.N & 1) == 0;
+}
+
+__device__ __forceinline__ void unpack_bf16x8(const uint4 r, float (&o)[8]) {
+  const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    o[2 * q] = __uint_as_float(w[q] << 16);
+    o[2 * q + 1] = __uint_as_float(w[q] & 0xffff0000u);
+  }
+}
+
+__device__ __forceinline__ void load_f32x8(const float* p, float (&o)[8]) {
+  const float4 u = *reinterpret_cast<const float4*>(p);
+  const float4 v = *reinterpret_cast<const float4*>(p + 4);
+  o[0] = u.x; o[1] = u.y; o[2] = u.z; o[3] = u.w;
+  o[4] = v.x; o[5] = v.y; o[6] = v.z; o[7] = v.w;
+}
+
+// Rolled row loop (small code: the executed epilogue is fetched once into the instruction cache;
+// fully unrolled variants measured 1.6x slower per tile purely with code size), the row-dependent
+// input of row p+1 is loaded before row p's stores, so its wait never covers a store.
+template <int P, int RPP, int JP, int JUMP, int ACT, bool DROP>
+__device__ __forceinline__ void tile_epi_rows(const DphGemmArgs& a, int64_t z, int64_t mrow0, int64_t n,
+                                              const float* lds, int lds_stride, float (&cso)[8], float (&csa)[8]) {
+  const int64_t voff = (a.C.z_div > 0 ? (z % a.C.z_div) : z) * a.vec_z_inner + n;
+  const int64_t cz = z_addr(a.C, z) + n;
+  // (arithmetic select of the two pointer VALUES: a `?:` over the fields becomes a select of field
+  // addresses, which forces the whole kernel-argument struct into scratch)
+  const uintptr_t ax_p = reinterpret_cast<uintptr_t>(a.aux_in), rs_p = reinterpret_cast<uintptr_t>(a.residual);
+  const bf16_t* inp = reinterpret_cast<const bf16_t*>(ax_p | (rs_p & (uintptr_t)(-(intptr_t)(ax_p == 0))));
+  const bool has_in = inp != nullptr, has_res = has_in && ax_p == 0;
+  const bool has_len = a.row_len != nullptr, has_pre = a.pre_out != nullptr, out_bf16 = a.c_dtype == DPH_OUT_BF16;
+  const bool colsum = a.colsum_out || a.colsum_aux;
+  float bias[8], csm[8], kc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    bias[i] = 0.f;
+    csm[i] = 1.f;
+  }
+  if (a.bias) load_f32x8(a.bias + voff, bias);
+  if (a.colmask) load_f32x8(a.colmask + voff, csm);
+  // per-column factors fixed for the thread: csm = colmask * layer mask, kc = csm / (1 - p)
+  const float sm = a.smask ? *a.smask : 1.0f;
+  const float inv_keep = DROP ? 1.0f / (1.0f - a.dropout_p) : 1.0f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    csm[i] *= sm;
+    kc[i] = csm[i] * inv_keep;
+  }
+  const uint32_t thr = DROP ? drop_thr(a.dropout_p) : 0u;
+  const uint32_t lr = has_len ? (uint32_t)a.len_rows : 1u;
+  auto row_of = [&](int p) -> int64_t { return mrow0 + RPP * p + (p / JP) * JUMP; };
+  uint4 nxt = make_uint4(0, 0, 0, 0);
+  if (has_in && row_of(0) < a.M) nxt = *reinterpret_cast<const uint4*>(inp + cz + row_addr(a.C, row_of(0)));
+#pragma unroll 1
+  for (int p = 0; p < P; ++p) {
+    const int64_t m = row_of(p);
+    const uint4 cur = nxt;
+    if (has_in && p + 1 < P && row_of(p + 1) < a.M)
+      nxt = *reinterpret_cast<const uint4*>(inp + cz + row_addr(a.C, row_of(p + 1)));
+    if (m >= a.M) continue;
+    const int64_t coff = cz + row_addr(a.C, m);
+    bool zero_row = false;
+    if (has_len) {
+      const uint32_t seg = (uint32_t)m / lr;
+      zero_row = (uint32_t)m >= (uint32_t)a.row_len[seg] + seg * lr;
+    }
+    float v[8], in[8], pre[8], ax[8];
+    load_f32x8(lds + p * RPP * lds_stride, v);
+    unpack_bf16x8(cur, in);
+    uint32_t keep = 0xffu;                     // bit i: element i kept
+    if constexpr (DROP) {
+      const uint64_t pair0 = (((uint64_t)(z * a.M + a.drop_row_offset + m)) * (uint64_t)a.N + (uint64_t)n) >> 1;
+      keep = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t bits = drop_bits2(a.seed, pair0 + j);
+        keep |= ((bits & 0xffffu) >= thr ? 1u : 0u) << (2 * j);
+        keep |= ((bits >> 16) >= thr ? 1u : 0u) << (2 * j + 1);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      pre[i] = fmaf(v[i], a.alpha, bias[i]);
+      const bool k = (keep >> i) & 1u;
+      if constexpr (ACT == DPH_ACT_GELU) {
+        v[i] = k ? gelu_f(pre[i]) * kc[i] : 0.f;
+      } else if constexpr (ACT == DPH_ACT_GELU_BWD) {
+        const float gz = DROP ? (k ? pre[i] * inv_keep : 0.f) : pre[i];
+        float g, dg;
+        gelu_and_grad(in[i], g, dg);
+        ax[i] = gz * g;
+        v[i] = gz * dg * csm[i];
+      } else {
+        v[i] = DROP ? (k ? pre[i] * kc[i] : 0.f) : pre[i] * csm[i];
+      }
+    }
+    if (has_res) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] += in[i];
+    }
+    if (zero_row) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = 0.f;
+    }
+    if (colsum) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        cso[i] += v[i];
+        if constexpr (ACT == DPH_ACT_GELU_BWD) csa[i] += ax[i];
+      }
+    }
+    if (has_pre)
+      *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(a.pre_out) + coff) =
+          make_uint4(pack2bf(pre[0], pre[1]), pack2bf(pre[2], pre[3]), pack2bf(pre[4], pre[5]), pack2bf(pre[6], pre[7]));
+    if (out_bf16) {
+      *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(a.C.ptr) + coff) =
+          make_uint4(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]), pack2bf(v[6], v[7]));
+    } else {
+      float* q = reinterpret_cast<float*>(a.C.ptr) + coff;
+      *reinterpret_cast<float4*>(q) = make_float4(v[0], v[1], v[2], v[3]);
+      *reinterpret_cast<float4*>(q + 4) = make_float4(v[4], v[5], v[6], v[7]);
+    }
+  }
+}
+
+// The activation and dropout are template parameters: with runtime switches hipcc if-converts the
+// branches and evaluates BOTH erfc-GELU forms and the dropout hash for every element (measured
+// 32k cycles per 128x128 tile with every feature off, vs 2.5k for a bare copy-out).
+template <int P, int RPP, int JP = P, int JUMP = 0>
+__device__ __forceinline__ void tile_epi(const DphGemmArgs& a, int64_t z, int64_t mrow0, int64_t n, const float* lds,
+                                         int lds_stride, float (&cso)[8], float (&csa)[8]) {
+  const bool drop = a.dropout_p > 0.f;
+  if (a.act == DPH_ACT_GELU) {
+    if (drop) tile_epi_rows<P, RPP, JP, JUMP, DPH_ACT_GELU, true>(a, z, mrow0, n, lds, lds_stride, cso, csa);
+    else tile_epi_rows<P, RPP, JP, JUMP, DPH_ACT_GELU, false>(a, z, mrow0, n, lds, lds_stride, cso, csa);
+  } else if (a.act == DPH_ACT_GELU_BWD) {
+    if (drop) tile_epi_rows<P, RPP, JP, JUMP, DPH_ACT_GELU_BWD, true>(a, z, mrow0, n, lds, lds_stride, cso, csa);
+    else tile_epi_rows<P, RPP, JP, JUMP, DPH_ACT_GELU_BWD, false>(a, z, mrow0, n, lds, lds_stride, cso, csa);
+  } else {
+    if (drop) tile_epi_rows<P, RPP, JP, JUMP, DPH_ACT_NONE, true>(a, z, mrow0, n, lds, lds_stride, cso, csa);
+    else tile_epi_rows<P, RPP, JP, JUMP, DPH_ACT_NONE, false>(a, z, mrow0, n, lds, lds_stride, cso, csa);
+  }
+}
+
 // LDS staging of the fp32 accumulator tile for the row-contiguous epilogue
 constexpr int CROW = BN + 4;                       // padded fp32 row
 constexpr int LDS_C = BM * CROW * 4;               // 67,584 B
@@ -418,6 +582,9 @@ __global__ void __launch_bounds__(NTHREADS, 2) gemm_kernel(const DphGemmArgs a, 
     cso[q] = 0.f;
     csa[q] = 0.f;
   }
+  if (tile_epi_ok(a, n0 + c8)) {
+    tile_epi<BM * BN / 8 / NTHREADS, NTHREADS / 16>(a, z, m0 + r0, n0 + c8, ct + r0 * CROW + c8, CROW, cso, csa);
+  } else {
 #pragma unroll 1
   for (int p = 0; p < BM * BN / 8 / NTHREADS; ++p) {
     const int r = r0 + (NTHREADS / 16) * p;
@@ -434,6 +601,7 @@ __global__ void __launch_bounds__(NTHREADS, 2) gemm_kernel(const DphGemmArgs a, 
       cso[q] += cs.out[q];
       csa[q] += cs.aux[q];
     }
+  }
   }
   if ((a.colsum_out != nullptr) || (a.colsum_aux != nullptr)) {
     // lanes l, l^16, l^32, l^48 share columns inside a wave; then 4 waves through LDS
@@ -492,6 +660,17 @@ __global__ void __launch_bounds__(NTHREADS, 2) gemm_kernel(const DphGemmArgs a, 
 // 16 rows and two k-chunks; the naive (r>>2)&3 measured 50 % bank-conflict cycles).  The swizzle
 // is applied on the DMA SOURCE address since an LDS-DMA writes its 1 KB lane-linearly.
 // =============================================================================================
+#ifndef DPH_STAMP
+#define DPH_STAMP 0         // diagnostic build: per-block s_memtime stamps into a.workspace (tools/stamp_gemm.py)
+#endif
+#define DPH_TSTAMP(v)                                                                     \
+  do {                                                                                    \
+    if (DPH_STAMP) {                                                                      \
+      __builtin_amdgcn_sched_barrier(0);                                                  \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory");            \
+      __builtin_amdgcn_sched_barrier(0);                                                  \
+    }                                                                                     \
+  } while (0)
 #ifndef DPH_ABLATE
 #define DPH_ABLATE 0        // timing ablations of the ring loop (tools/ablate_gemm.py); 0 = production
 #endif
@@ -607,7 +786,9 @@ __global__ void __launch_bounds__(C::NT, C::MINB) ring_gemm_kernel(const DphGemm
   const int64_t n0 = tn * C::BN;
   const int64_t kbeg = split * kchunk;
   const int64_t kend = min(a.K, kbeg + kchunk);
-  const int H = (int)(max<int64_t>(kend - kbeg, 0) / ring::KS);   // k-slices
+  const int H = DPH_ABLATE == 6 ? 0 : (int)(max<int64_t>(kend - kbeg, 0) / ring::KS);   // k-slices
+  unsigned long long st0 = 0, st1 = 0, st2 = 0, st3 = 0, sA = 0, sB = 0, sC = 0;
+  DPH_TSTAMP(st0);
 
   // DMA sources: instruction j of wave w covers slice rows (j*NW+w)*16 .. +16; this lane loads
   // row r = (j*NW+w)*16 + lane/4 into physical chunk lane%4 <- logical chunk (lane%4) ^ swz(r)
@@ -691,6 +872,7 @@ __global__ void __launch_bounds__(C::NT, C::MINB) ring_gemm_kernel(const DphGemm
     ring::read_frags<C>(f0, slot(0), wr, wc, lane);
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_sched_barrier(0);
+    DPH_TSTAMP(st1);
     int i = 0;
     for (; i + 1 < H; i += 2) {
       step(i, f0, f1);
@@ -698,7 +880,15 @@ __global__ void __launch_bounds__(C::NT, C::MINB) ring_gemm_kernel(const DphGemm
     }
     if (i < H) step(i, f0, f1);
   }
+  DPH_TSTAMP(st2);
 
+  if (DPH_ABLATE == 5) {   // timing ablation: no epilogue (accumulators kept live)
+#pragma unroll
+    for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+      for (int j = 0; j < C::FN; ++j) asm volatile("" ::"v"(acc[i][j]));
+    return;
+  }
   // ---- epilogue, EROWS rows at a time: accumulators -> LDS fp32 -> row-contiguous ----
   constexpr int TPR = C::BN / 8;              // threads per output row (8 columns each)
   constexpr int RPP = C::NT / TPR;            // rows per pass
@@ -711,29 +901,39 @@ __global__ void __launch_bounds__(C::NT, C::MINB) ring_gemm_kernel(const DphGemm
     cso[q] = 0.f;
     csa[q] = 0.f;
   }
-#pragma unroll 1
-  for (int h = 0; h < C::BM / C::EROWS; ++h) {
+  // Pass h stages accumulator rows i in [h*FMH, (h+1)*FMH) of every wave, so the registers of
+  // the staged rows die before the next pass (the Big tile cannot hold its 128 accumulator VGPRs
+  // and the epilogue's prefetched inputs at once).  LDS row r holds tile row
+  // (r / SEG) * WTM + h * SEG + r % SEG.
+  constexpr int NPASS = C::BM / C::EROWS;
+  constexpr int FMH = C::FM / NPASS;
+  constexpr int SEG = C::WTM / NPASS;
+  constexpr int JP = SEG / RPP;                // passes p per SEG run of rows
+  static_assert(SEG % RPP == 0 && C::FM % NPASS == 0, "epilogue row map");
+  auto trow = [&](int h, int r) { return (r / SEG) * C::WTM + h * SEG + r % SEG; };
+#pragma unroll
+  for (int h = 0; h < NPASS; ++h) {
     __syncthreads();
-    // waves whose rows fall in this pass stage their accumulators
-    if (wr * C::WTM / C::EROWS == h) {
+    if (h == 0) DPH_TSTAMP(sA);
 #pragma unroll
-      for (int i = 0; i < C::FM; ++i) {
-        const int r = (wr * C::WTM) % C::EROWS + 16 * i + (lane & 15);
+    for (int ii = 0; ii < FMH; ++ii) {
+      const int i = h * FMH + ii;
+      const int r = wr * SEG + 16 * ii + (lane & 15);
 #pragma unroll
-        for (int j = 0; j < C::FN; ++j) {
-          const int c = wc * C::WTN + 16 * j + 4 * (lane >> 4);
-          *reinterpret_cast<float4*>(ct + r * C::CROW + c) =
-              make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
-        }
+      for (int j = 0; j < C::FN; ++j) {
+        const int c = wc * C::WTN + 16 * j + 4 * (lane >> 4);
+        *reinterpret_cast<float4*>(ct + r * C::CROW + c) =
+            make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
       }
     }
     __syncthreads();
+    if (h == 0) DPH_TSTAMP(sB);
     if (a.splits > 1) {
       float* ws = reinterpret_cast<float*>(a.workspace) + (zz * a.M) * a.N;
 #pragma unroll 2
       for (int p = 0; p < C::EROWS / RPP; ++p) {
         const int r = r0 + RPP * p;
-        const int64_t m = m0 + h * C::EROWS + r;
+        const int64_t m = m0 + trow(h, r);
         const int64_t n = n0 + c8;
         if (m >= a.M || n >= a.N) continue;
         const float* src = ct + r * C::CROW + c8;
@@ -747,6 +947,16 @@ __global__ void __launch_bounds__(C::NT, C::MINB) ring_gemm_kernel(const DphGemm
       }
       continue;
     }
+    // (the Big tile keeps the per-row epilogue: the prefetching one pushes its main loop into
+    // scratch spills at the 256-VGPR cap)
+    if constexpr (C::BM <= 128) {
+      if (tile_epi_ok(a, n0 + c8)) {
+        tile_epi<C::EROWS / RPP, RPP, JP, C::WTM - SEG>(a, z, m0 + trow(h, r0), n0 + c8, ct + r0 * C::CROW + c8,
+                                                        C::CROW, cso, csa);
+        if (h == 0) DPH_TSTAMP(sC);
+        continue;
+      }
+    }
 #pragma unroll 1
     for (int p = 0; p < C::EROWS / RPP; ++p) {
       const int r = r0 + RPP * p;
@@ -757,13 +967,26 @@ __global__ void __launch_bounds__(C::NT, C::MINB) ring_gemm_kernel(const DphGemm
       v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w;
       v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
       Cs8 cs;
-      epilogue8(a, z, m0 + h * C::EROWS + r, n0 + c8, v, cs);
+      epilogue8(a, z, m0 + trow(h, r), n0 + c8, v, cs);
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         cso[q] += cs.out[q];
         csa[q] += cs.aux[q];
       }
     }
+  }
+  if (DPH_STAMP) {
+    __syncthreads();
+    DPH_TSTAMP(st3);
+    if (tid == 0) {
+      unsigned hw, xcc;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+      unsigned long long* o = reinterpret_cast<unsigned long long*>(a.workspace) +
+                              16 * ((int64_t)blockIdx.y * gridDim.x + blockIdx.x);
+      o[0] = st0; o[1] = st1; o[2] = st2; o[3] = st3; o[4] = hw; o[5] = xcc; o[6] = sA; o[7] = sB; o[8] = sC;
+    }
+    return;
   }
   if (a.splits == 1 && ((a.colsum_out != nullptr) || (a.colsum_aux != nullptr))) {
     // lanes sharing columns inside a wave (lane ^ TPR, ...), then the waves through LDS

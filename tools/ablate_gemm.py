@@ -1,10 +1,11 @@
 """Build timing-ablation variants of the ring GEMM into ab/abl<N>.so (build container), or time one
 shape with whatever library DPH_LIB_PATH selects (GPU box).
 
-  python tools/ablate_gemm.py build            # ab/abl0.so .. ab/abl4.so
+  python tools/ablate_gemm.py build            # ab/abl0.so .. ab/abl6.so
   DPH_LIB_PATH=ab/abl1.so DPH_GEMM_PATH=big python tools/ablate_gemm.py time M N K
 Variants: 0 production, 1 no DMA in the loop, 2 no MFMA, 3 no barrier, 4 no fragment reads
-(outputs are wrong for 1-4; only their timing is meaningful).
+5 no epilogue, 6 no k-loop
+(outputs are wrong for 1-6; only their timing is meaningful).
 """
 import os
 import subprocess
@@ -19,7 +20,7 @@ if sys.argv[1] == "build":
     b.build()
     objs = [o for o in (REPO / "dphubert_amd" / "csrc" / "build").glob("*.o") if o.stem != "gemm"]
     (REPO / "ab").mkdir(exist_ok=True)
-    for n in range(5):
+    for n in range(7):
         obj = REPO / "ab" / f"gemm_abl{n}.o"
         subprocess.run([b.HIPCC] + b.FLAGS + [f"-DDPH_ABLATE={n}", "-c", str(b.CSRC / "gemm.hip"), "-o", str(obj)],
                        check=True)
