@@ -86,7 +86,7 @@ def pmc_traffic(args):
             d = os.path.join(td, counter)
             cmd = [exe, "--pmc", counter, "--kernel-include-regex", "gemm_kernel", "-f", "csv", "-d", d, "-o", "run",
                    "--", sys.executable, os.path.join(here, "bench.py"), "--steps", "1", "--warmup", "1",
-                   "--no-cpu-baseline", "--no-roofline", "--traffic", "off", "--batch", str(args.batch),
+                   "--no-cpu-baseline", "--no-roofline", "--traffic", "off", "--graphs", "off", "--batch", str(args.batch),
                    "--seconds", str(args.seconds)]
             env = dict(os.environ, TMPDIR="/tmp")
             r = subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
@@ -120,6 +120,8 @@ def main():
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--traffic", choices=["auto", "off"], default="auto",
                     help="auto: measure per-launch HBM bytes of the GEMMs with rocprofv3 PMC passes (rank 0, N=1)")
+    ap.add_argument("--graphs", choices=["on", "off"], default="on",
+                    help="on: replay the whole step as one captured HIP graph after the eager warm-up steps")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -150,25 +152,41 @@ def main():
                                   use_reg=True)
     module.global_step = 5000            # target sparsity reached (0.75)
     module = module.to(dev)
-    trainer = Trainer(module, clip_norm=10.0)
+    graphs = args.graphs == "on"
+    trainer = Trainer(module, clip_norm=10.0, graphs=graphs, graph_warmup=2)
     samples = int(args.seconds * 16000)
     wave, lengths = synthetic_batch(args.batch, samples, seed=2022 + rank)
     batch = (wave.to(dev), lengths.to(dev))
 
-    for i in range(args.warmup):
+    # warm-up: 2 eager steps, then (graphs) the capture + first replay
+    for i in range(max(args.warmup, 3 if graphs else 1)):
         loss = trainer.step(batch)
     torch.cuda.synchronize()
+    graphed = trainer._graph is not None
+    log(f"step mode: {'HIP graph replay' if graphed else 'eager'}")
+    # GEMM launches of the LAST timed step are bracketed by HIP events on their launch stream (an
+    # event marker costs ~3 us of GPU time, so bracketing every step would tax the headline number).
+    # With graphs, that step replays a second capture of the same step whose GEMMs carry event nodes.
+    prof = LaunchProfiler() if (rank == 0 and not args.no_roofline) else None
+    prof_mode = "timed step" if prof is not None else None
+    if prof is not None and graphed:
+        try:
+            trainer.prepare_profiled_step(prof)
+            prof_mode = "last timed step (graph replay with event nodes)"
+        except Exception as e:  # noqa: BLE001 -- event nodes not capturable: profile an eager step after timing
+            log(f"profiled capture unavailable ({e!r}); GEMMs are timed on an eager step after the timed region")
+            prof = LaunchProfiler()
+            prof_mode = "eager step right after the timed region (same kernels)"
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    # GEMM launches of the LAST timed step are bracketed by HIP events on their launch stream (an
-    # event marker costs ~3 us of GPU time, so bracketing every step would tax the headline number)
-    prof = LaunchProfiler() if (rank == 0 and not args.no_roofline) else None
     t0 = time.perf_counter()
+    in_loop = prof is not None and prof_mode != "eager step right after the timed region (same kernels)"
     for i in range(args.steps):
-        if prof is not None and i == args.steps - 1:
+        last = in_loop and i == args.steps - 1
+        if last and not graphed:
             prof.__enter__()
-        loss = trainer.step(batch)
+        loss = trainer.step(batch, profiled=last)
     t_host = time.perf_counter() - t0          # host enqueue time (GPU may still be running)
     torch.cuda.synchronize()
     if world > 1:
@@ -205,7 +223,16 @@ def main():
                    "global_batch_audio_s": world * args.batch * args.seconds, "distill_layers": "0.4,8,12",
                    "parallelism": f"dp{world}"},
         "peak_hbm_gib": round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 2),
+        "step_mode": "hip_graph" if graphed else "eager",
     }
+    if prof is not None and not in_loop:
+        torch.cuda.synchronize()
+        trainer._graph, saved = None, trainer._graph      # one eager step with the profiler on
+        g_on = trainer.graphs
+        trainer.graphs = False
+        with prof:
+            trainer.step(batch)
+        trainer.graphs, trainer._graph = g_on, saved
     if prof is not None:
         prof.__exit__(None, None, None)
         summ = prof.summary()
@@ -226,7 +253,7 @@ def main():
                            "launches_per_step": d["launches"],
                            "avg_launch_us": round(avg_ms * 1e3, 2), "flop_per_launch": flops_per_launch,
                            "all_gemm_tflops": round(all_fl / (all_ms / 1e3) / 1e12, 1),
-                           "gemm_ms_per_step": round(all_ms, 3)}
+                           "gemm_ms_per_step": round(all_ms, 3), "timed_on": prof_mode}
         if traffic_err:
             out["roofline"]["traffic_error"] = traffic_err
         log(json.dumps({k: v for k, v in summ.items()}))

@@ -47,6 +47,10 @@ class DphAdamGroup(C.Structure):
                 ("pad_", f32 * 3)]
 
 
+class DphAdamDyn(C.Structure):
+    _fields_ = [("g", DphAdamGroup * 4), ("step", f32), ("pad_", f32 * 3)]
+
+
 S = vp  # hipStream_t
 
 _SIGS = {
@@ -85,10 +89,16 @@ _SIGS = {
     "dph_expected_params_bwd": ([vp, vp, vp, vp, i64, vp, vp, i64, vp, vp, f32, S], C.c_int),
     "dph_grad_sumsq": ([vp, i64, vp, vp, i64, vp, S], C.c_int),
     "dph_adamw_step": ([vp, i64, vp, vp, i64, vp, i64, i64, vp, f32, S], C.c_int),
+    "dph_adamw_step_dev": ([vp, i64, vp, vp, i64, vp, vp, f32, S], C.c_int),
+    "dph_set_rng_epoch": ([vp], C.c_int),
+    "dph_event_create": ([C.POINTER(vp)], C.c_int),
+    "dph_event_record": ([vp, S], C.c_int),
+    "dph_event_elapsed_ms": ([vp, vp, C.POINTER(f32)], C.c_int),
+    "dph_event_destroy": ([vp], C.c_int),
 }
 
 _lib = None
-ABI_VERSION = 2     # include/dphubert_hip.h layout (DphGemmArgs.colsum_n, padded conv packing, strided LN)
+ABI_VERSION = 4     # include/dphubert_hip.h layout (3: dph_adamw_step_dev + DphAdamDyn, dph_set_rng_epoch; 4: dph_event_*)
 
 
 class DphError(RuntimeError):

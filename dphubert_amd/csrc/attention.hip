@@ -112,6 +112,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const bf16_t* __restrict_
                                                        const float* __restrict__ head_mask,
                                                        const int64_t* __restrict__ key_len, AttnShape sh, float scale,
                                                        float drop_p, uint64_t seed) {
+  seed = epoch_seed(seed);   // per-step RNG epoch (graph replays)
   __shared__ __attribute__((aligned(16))) char smem[2 * (KTILE_PAD_BYTES + TILE_SWZ_BYTES)];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -286,6 +287,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dkv_kernel(const bf16_t* __restr
                                                            const float* __restrict__ Dv, bf16_t* __restrict__ dqkv,
                                                            const int64_t* __restrict__ key_len, AttnShape sh,
                                                            float scale, float drop_p, uint64_t seed) {
+  seed = epoch_seed(seed);   // per-step RNG epoch (graph replays)
   constexpr int TB = QT_BWD * 128;   // 4096 B per tile
   __shared__ __attribute__((aligned(16))) char smem[2 * (2 * TB) + 2 * 2 * QT_BWD * 4];
   const int tid = threadIdx.x;
@@ -417,6 +419,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(const bf16_t* __restri
                                                           const float* __restrict__ Dv, bf16_t* __restrict__ dqkv,
                                                           const int64_t* __restrict__ key_len, AttnShape sh,
                                                           float scale, float drop_p, uint64_t seed) {
+  seed = epoch_seed(seed);   // per-step RNG epoch (graph replays)
   __shared__ __attribute__((aligned(16))) char smem[2 * (TILE_SWZ_BYTES + KTILE_PAD_BYTES)];
   const int tid = threadIdx.x;
   const int lane = tid & 63;

@@ -160,4 +160,27 @@ __device__ __forceinline__ float wave_max(float v) {
 
 __host__ __device__ __forceinline__ int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// ---- per-step RNG epoch ---------------------------------------------------------------------
+// Every kernel that draws dropout / HardConcrete noise mixes a device-resident epoch word into
+// its seed at entry.  The trainer advances that word with a stream-ordered op once per step, so a
+// captured HIP graph (fixed kernel arguments) still draws fresh noise on every replay, and the
+// backward kernels of a step regenerate exactly the forward's masks.  Each translation unit has
+// its own pointer variable (no -fgpu-rdc); dph_set_rng_epoch() sets all of them.
+void register_epoch_setter(int (*fn)(const uint64_t*));
+namespace {
+__device__ const uint64_t* g_rng_epoch = nullptr;
+int set_epoch_tu(const uint64_t* p) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_rng_epoch), &p, sizeof(p)) == hipSuccess ? 0 : -1;
+}
+struct EpochReg {
+  EpochReg() { register_epoch_setter(&set_epoch_tu); }
+};
+EpochReg g_epoch_reg;
+}  // namespace
+
+__device__ __forceinline__ uint64_t epoch_seed(uint64_t seed) {
+  const uint64_t* e = g_rng_epoch;
+  return e ? seed + (*e) * 0x9E3779B97F4A7C15ull : seed;
+}
+
 }  // namespace dph

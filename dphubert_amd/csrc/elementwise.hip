@@ -163,6 +163,7 @@ __global__ void __launch_bounds__(256) branch_bwd_kernel(const bf16_t* __restric
                                                          const int64_t* __restrict__ row_len, int64_t len_rows,
                                                          float* __restrict__ colsum, const bf16_t* __restrict__ pre,
                                                          float* __restrict__ sdot, int64_t rows_per_block) {
+  seed = epoch_seed(seed);   // per-step RNG epoch (graph replays)
   __shared__ float red[4][512];
   __shared__ float sred[4];
   const int tx = threadIdx.x & 63;

@@ -214,6 +214,7 @@ __device__ __forceinline__ void epilogue8(const DphGemmArgs& a, int64_t z, int64
   const bool vec = (nv == 8) && ((coff & 7) == 0);
   const bool vvec = (nv == 8) && (((voff + n) & 3) == 0);
   const float inv_keep = a.dropout_p > 0.f ? 1.0f / (1.0f - a.dropout_p) : 1.0f;
+  const uint64_t seed = a.dropout_p > 0.f ? epoch_seed(a.seed) : 0;
   const uint64_t drow = ((uint64_t)(z * a.M + a.drop_row_offset + m)) * (uint64_t)a.N;
   bool zero_row = false;
   if (a.row_len) zero_row = (m % a.len_rows) >= a.row_len[m / a.len_rows];
@@ -229,7 +230,7 @@ __device__ __forceinline__ void epilogue8(const DphGemmArgs& a, int64_t z, int64
     float x = v[i] * a.alpha;
     if (a.bias) x += bias[i];
     pre[i] = x;
-    const float dz = dropout_scale(a.seed, drow + n + i, a.dropout_p, inv_keep);
+    const float dz = dropout_scale(seed, drow + n + i, a.dropout_p, inv_keep);
     const float c = a.colmask ? cm[i] : 1.0f;
     float ax = 0.f;
     if (a.act == DPH_ACT_GELU) {
@@ -342,6 +343,7 @@ __device__ __forceinline__ void tile_epi_rows(const DphGemmArgs& a, int64_t z, i
     kc[i] = csm[i] * inv_keep;
   }
   const uint32_t thr = DROP ? drop_thr(a.dropout_p) : 0u;
+  const uint64_t seed = DROP ? epoch_seed(a.seed) : 0;
   const uint32_t lr = has_len ? (uint32_t)a.len_rows : 1u;
   auto row_of = [&](int p) -> int64_t { return mrow0 + RPP * p + (p / JP) * JUMP; };
   uint4 nxt = make_uint4(0, 0, 0, 0);
@@ -368,7 +370,7 @@ __device__ __forceinline__ void tile_epi_rows(const DphGemmArgs& a, int64_t z, i
       keep = 0;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const uint32_t bits = drop_bits2(a.seed, pair0 + j);
+        const uint32_t bits = drop_bits2(seed, pair0 + j);
         keep |= ((bits & 0xffffu) >= thr ? 1u : 0u) << (2 * j);
         keep |= ((bits >> 16) >= thr ? 1u : 0u) << (2 * j + 1);
       }

@@ -15,6 +15,7 @@ namespace {
 __global__ void hc_fwd_kernel(const float* __restrict__ la, const float* __restrict__ u_in, float* __restrict__ u_out,
                               float* __restrict__ mask, int64_t n, uint64_t seed, float beta, float lo, float hi,
                               float eps) {
+  seed = epoch_seed(seed);   // per-step RNG epoch (graph replays)
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   // u ~ U(eps, 1-eps)   (hardconcrete.py:96)

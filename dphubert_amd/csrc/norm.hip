@@ -17,6 +17,7 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const bf16_t* __restrict__ 
                                                      bf16_t* __restrict__ y, float* __restrict__ mean_out,
                                                      float* __restrict__ rstd_out, int64_t rows, int D, int ld,
                                                      float eps, float drop_p, uint64_t seed) {
+  seed = epoch_seed(seed);   // per-step RNG epoch (graph replays)
   // rows have stride ld >= D (ld % 4 == 0); columns [D, ld) are row padding: read as 0, written as 0
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -95,6 +96,7 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(
     uint64_t seed, bf16_t* __restrict__ branch, float branch_p, uint64_t branch_seed,
     const float* __restrict__ branch_smask, float* __restrict__ branch_colsum, const bf16_t* __restrict__ branch_pre,
     float* __restrict__ branch_sdot, const bf16_t* __restrict__ dx_add) {
+  seed = epoch_seed(seed); branch_seed = epoch_seed(branch_seed);   // per-step RNG epoch (graph replays)
   __shared__ float red[4][3][LN_MAXV * 256];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;

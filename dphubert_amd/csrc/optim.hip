@@ -39,16 +39,19 @@ __global__ void __launch_bounds__(256) sumsq_kernel(const DphTensorSlot* __restr
 
 __global__ void __launch_bounds__(256) adamw_kernel(const DphTensorSlot* __restrict__ slots,
                                                     const int64_t* __restrict__ cslot,
-                                                    const int64_t* __restrict__ cstart, Groups G, int64_t step,
+                                                    const int64_t* __restrict__ cstart, Groups G, float step,
+                                                    const DphAdamDyn* __restrict__ dyn,
                                                     const float* __restrict__ sumsq, float max_norm) {
   const int64_t c = blockIdx.x;
   const DphTensorSlot sl = slots[cslot[c]];
   if (!sl.grad) return;
-  const DphAdamGroup gr = G.g[sl.group];
+  // device-resident lr / step (HIP-graph replays) or the launch-time values
+  const DphAdamGroup gr = dyn ? dyn->g[sl.group] : G.g[sl.group];
+  if (dyn) step = dyn->step;
   float clip = 1.0f;
   if (sumsq && max_norm > 0.f) clip = fminf(max_norm / (sqrtf(*sumsq) + 1e-6f), 1.0f);
-  const float bc1 = 1.0f - powf(gr.beta1, (float)step);
-  const float bc2 = 1.0f - powf(gr.beta2, (float)step);
+  const float bc1 = 1.0f - powf(gr.beta1, step);
+  const float bc2 = 1.0f - powf(gr.beta2, step);
   const float step_size = gr.lr / bc1;
   const float bc2_sqrt = sqrtf(bc2);
   const float decay = 1.0f - gr.lr * gr.weight_decay;
@@ -93,6 +96,16 @@ extern "C" int dph_adamw_step(const DphTensorSlot* slots, int64_t n_slots, const
   Groups G;
   for (int i = 0; i < MAX_GROUPS; ++i) G.g[i] = groups[i < n_groups ? i : 0];
   hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)n_chunks), dim3(256), 0, stream, slots, chunk_slot, chunk_start, G,
-                     step, sumsq, max_norm);
+                     (float)step, (const DphAdamDyn*)nullptr, sumsq, max_norm);
   return check_launch("dph_adamw_step");
+}
+
+extern "C" int dph_adamw_step_dev(const DphTensorSlot* slots, int64_t n_slots, const int64_t* chunk_slot,
+                                  const int64_t* chunk_start, int64_t n_chunks, const DphAdamDyn* dyn,
+                                  const float* sumsq, float max_norm, hipStream_t stream) {
+  DPH_REQUIRE(slots && chunk_slot && chunk_start && dyn && n_chunks > 0, "dph_adamw_step_dev: bad args");
+  Groups G = {};
+  hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)n_chunks), dim3(256), 0, stream, slots, chunk_slot, chunk_start, G,
+                     1.0f, dyn, sumsq, max_norm);
+  return check_launch("dph_adamw_step_dev");
 }

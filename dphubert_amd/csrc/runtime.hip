@@ -7,6 +7,13 @@
 namespace dph {
 namespace {
 thread_local char g_err[1024] = {0};
+constexpr int MAX_TU = 32;
+int (*g_epoch_setters[MAX_TU])(const uint64_t*);
+int g_n_epoch_setters = 0;
+}
+
+void register_epoch_setter(int (*fn)(const uint64_t*)) {
+  if (g_n_epoch_setters < MAX_TU) g_epoch_setters[g_n_epoch_setters++] = fn;
 }
 
 void set_error(const char* fmt, ...) {
@@ -27,4 +34,67 @@ int check_launch(const char* what) {
 }  // namespace dph
 
 extern "C" const char* dph_last_error(void) { return dph::g_err; }
-extern "C" int dph_abi_version(void) { return 2; }
+extern "C" int dph_abi_version(void) { return 4; }
+
+// Point every kernel's RNG epoch at the device word `epoch` (uint64, device memory) on the current
+// device, or detach it (NULL: seeds are used as passed).  Not stream-ordered: call outside any
+// capture, before the kernels that should see it.
+extern "C" int dph_set_rng_epoch(const uint64_t* epoch) {
+  for (int i = 0; i < dph::g_n_epoch_setters; ++i)
+    if (dph::g_epoch_setters[i](epoch) != 0) {
+      dph::set_error("dph_set_rng_epoch: hipMemcpyToSymbol failed");
+      return DPH_ELAUNCH;
+    }
+  return DPH_OK;
+}
+
+// ---- timing events (bench.py's live per-kernel timing) ----------------------------------------
+// Recorded with hipEventRecordExternal so that, inside a stream capture, they become event-record
+// nodes of the graph whose timestamps are readable after each replay (torch refuses external
+// events on ROCm).  Outside a capture the flag is a plain record.
+extern "C" int dph_event_create(void** ev) {
+  hipEvent_t e = nullptr;
+  if (!ev || hipEventCreateWithFlags(&e, hipEventDefault) != hipSuccess) {
+    dph::set_error("dph_event_create failed");
+    return DPH_ELAUNCH;
+  }
+  *ev = reinterpret_cast<void*>(e);
+  return DPH_OK;
+}
+
+extern "C" int dph_event_record(void* ev, hipStream_t stream) {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  unsigned long long cid = 0;
+  hipGraph_t graph = nullptr;
+  const hipGraphNode_t* deps = nullptr;
+  size_t ndeps = 0;
+  hipError_t e = hipStreamGetCaptureInfo_v2(stream, &st, &cid, &graph, &deps, &ndeps);
+  if (e == hipSuccess && st == hipStreamCaptureStatusActive) {
+    // capturing: append an event-record node after the stream's current capture frontier and make
+    // it the new frontier (hipEventRecordWithFlags(external) is rejected by this ROCm)
+    hipGraphNode_t node = nullptr;
+    e = hipGraphAddEventRecordNode(&node, graph, deps, ndeps, reinterpret_cast<hipEvent_t>(ev));
+    if (e == hipSuccess) e = hipStreamUpdateCaptureDependencies(stream, &node, 1, hipStreamSetCaptureDependencies);
+  } else if (e == hipSuccess) {
+    e = hipEventRecord(reinterpret_cast<hipEvent_t>(ev), stream);
+  }
+  if (e != hipSuccess) {
+    dph::set_error("dph_event_record (capturing=%d): %s", (int)(st == hipStreamCaptureStatusActive),
+                   hipGetErrorString(e));
+    return DPH_ELAUNCH;
+  }
+  return DPH_OK;
+}
+
+extern "C" int dph_event_elapsed_ms(void* start, void* stop, float* ms) {
+  if (hipEventSynchronize(reinterpret_cast<hipEvent_t>(stop)) != hipSuccess ||
+      hipEventElapsedTime(ms, reinterpret_cast<hipEvent_t>(start), reinterpret_cast<hipEvent_t>(stop)) != hipSuccess) {
+    dph::set_error("dph_event_elapsed_ms failed");
+    return DPH_ELAUNCH;
+  }
+  return DPH_OK;
+}
+
+extern "C" int dph_event_destroy(void* ev) {
+  return hipEventDestroy(reinterpret_cast<hipEvent_t>(ev)) == hipSuccess ? DPH_OK : DPH_ELAUNCH;
+}

@@ -45,9 +45,34 @@ def dense(t: torch.Tensor, offset: int = 0, row_stride: Optional[int] = None) ->
     return mat(t, t.shape[-1] if row_stride is None else row_stride, offset=offset)
 
 
+class _Event:
+    """A hipEvent_t from the kernel library: recorded as an external event node when the launch
+    stream is being captured (torch refuses external events on ROCm)."""
+
+    def __init__(self):
+        h = C.c_void_p()
+        call("dph_event_create", C.byref(h))
+        self.h = h.value
+
+    def record(self):
+        call("dph_event_record", self.h, _stream())
+
+    def elapsed_time(self, end: "_Event") -> float:
+        ms = C.c_float()
+        call("dph_event_elapsed_ms", self.h, end.h, C.byref(ms))
+        return ms.value
+
+    def __del__(self):
+        try:
+            _lib.lib().dph_event_destroy(self.h)
+        except Exception:  # noqa: BLE001 -- interpreter shutdown
+            pass
+
+
 class LaunchProfiler:
     """Brackets every GEMM launch with HIP events on the launch stream (used by bench.py to
-    measure per-kernel average durations live; off by default)."""
+    measure per-kernel average durations live; off by default).  Works eagerly and inside a HIP
+    graph capture (the events become event-record nodes, read after the replay)."""
 
     active = None
 
@@ -94,8 +119,7 @@ def gemm(A: DphMat, B: DphMat, Cm: DphMat, M: int, N: int, K: int, *, a_kcontig:
                        len_rows, drop_row_offset, ptr(ws), ws_bytes, colsum_n)
     prof = LaunchProfiler.active
     if prof is not None:
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
+        e0, e1 = _Event(), _Event()
         e0.record()
     call("dph_gemm", C.byref(args), _stream())
     if prof is not None:

@@ -121,6 +121,7 @@ class DistillModule(nn.Module):
         self.seconds_per_batch = seconds_per_batch
         self.num_workers = num_workers
         self.global_step = 0
+        self.target_sparsity_dev = None    # 0-d device view set by trainer.Trainer (stepstate block)
         self.logged = {}
         # distinct projection modules (shared per group, distill.py:94-99) and the per-layer index into them
         uniq, index = [], []
@@ -137,7 +138,9 @@ class DistillModule(nn.Module):
 
     # ---- LightningModule surface ------------------------------------------
     def log_dict(self, d, **kw):
-        self.logged.update(d)
+        # detached: a logged loss must not keep the step's autograd graph (and its AccumulateGrad
+        # nodes, bound to the stream they were created on) alive into the next step / a graph capture
+        self.logged.update({k: v.detach() if torch.is_tensor(v) else v for k, v in d.items()})
 
     def configure_optimizers(self, clip_norm: Optional[float] = None):
         main_params = [p for n, p in self.student_model.named_parameters() if "log_alpha" not in n and p.requires_grad]
@@ -189,9 +192,12 @@ class DistillModule(nn.Module):
             *[h.reshape(B * T, -1) for h in t_layers])
         if self.use_reg:
             cur_target_sparsity = self._get_target_sparsity()
+            # the trainer keeps the target in its per-step device block (HIP-graph replays read it there)
+            tgt = cur_target_sparsity if self.target_sparsity_dev is None else self.target_sparsity_dev
             cur_expected_sparsity = 1. - self.student_model.get_num_params() / self.original_num_params
-            loss_reg = self.lambda1 * (cur_expected_sparsity - cur_target_sparsity) \
-                + self.lambda2 * (cur_expected_sparsity - cur_target_sparsity) ** 2
+            loss_reg = self.lambda1 * (cur_expected_sparsity - tgt) \
+                + self.lambda2 * (cur_expected_sparsity - tgt) ** 2
+            cur_target_sparsity = tgt
         else:
             loss_reg = 0
         loss = loss_distill + loss_reg

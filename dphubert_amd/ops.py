@@ -185,6 +185,13 @@ class _ZeroArena:
 _ZEROS = _ZeroArena()
 
 
+def reset_zero_arena():
+    """Start a fresh arena chunk on the next request (around a HIP-graph capture: slices handed out
+    inside the capture must come from a chunk whose zero fill is itself part of the graph)."""
+    _ZEROS.buf = None
+    _ZEROS.off = 0
+
+
 def zeros_f32(shape, dev) -> torch.Tensor:
     """Zero-filled fp32 tensor (small ones come from the arena, no fill kernel of their own)."""
     if isinstance(shape, int):

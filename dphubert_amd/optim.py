@@ -11,6 +11,7 @@ import math
 from typing import Iterable, List, Optional
 
 import torch
+from torch.autograd.graph import increment_version
 
 from . import _lib
 from ._lib import DphAdamGroup, DphTensorSlot, call, ptr
@@ -30,7 +31,10 @@ class FusedAdamW(torch.optim.Optimizer):
         self._pinned = None
         self._slots_dev = None
         self._event = None
+        self._slot_key = None
         self._step = 0
+        self._step_t = torch.zeros((), dtype=torch.float32)   # one counter shared by every param's state
+        self.dyn_ptr = None          # device DphAdamDyn (stepstate.StepScalars) -> dph_adamw_step_dev
 
     def _params(self):
         out = []
@@ -59,56 +63,95 @@ class FusedAdamW(torch.optim.Optimizer):
         self._sumsq = torch.zeros(1, dtype=torch.float32, device=dev)
         self._chunk_key = key
 
+    def _slot_table(self, plist):
+        """Upload the (param, grad, exp_avg, exp_avg_sq) pointer table when any pointer changed.
+        With a GradReducer the gradients are fixed bucket views, so this runs once."""
+        key = []
+        for gi, p in plist:
+            st = self.state[p]
+            if len(st) == 0:
+                st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["step"] = self._step_t
+            elif st.get("step") is not self._step_t:
+                # loaded state (load_state_dict): adopt its step count, then share one counter
+                self._step = max(self._step, int(st["step"]))
+                self._step_t.fill_(self._step)
+                st["step"] = self._step_t
+            if p.grad is not None and not p.grad.is_contiguous():
+                p.grad = p.grad.contiguous()
+            if p.grad is not None and p.grad.dtype != torch.float32:
+                raise TypeError("FusedAdamW expects fp32 gradients")
+            key.append((p.data_ptr(), p.grad.data_ptr() if p.grad is not None else 0, st["exp_avg"].data_ptr(),
+                        st["exp_avg_sq"].data_ptr(), p.numel(), gi))
+        key = tuple(key)
+        if key == self._slot_key:
+            return
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("FusedAdamW: parameter/gradient storage changed inside a HIP graph capture")
+        if self._event is not None:
+            self._event.synchronize()     # previous H2D copy of the pinned table is done
+        slots = (DphTensorSlot * len(plist)).from_address(self._pinned.data_ptr())
+        for i, (pp, gp, ma, va, n, gi) in enumerate(key):
+            slots[i].param, slots[i].grad, slots[i].exp_avg, slots[i].exp_avg_sq = pp, gp, ma, va
+            slots[i].n = n
+            slots[i].group = gi
+        self._slots_dev.copy_(self._pinned, non_blocking=True)
+        self._event = torch.cuda.Event()
+        self._event.record()
+        self._slot_key = key
+
+    def begin_step(self) -> int:
+        """Host half of a step: advance the step counter; returns the 1-based AdamW step that a
+        device-resident DphAdamDyn must carry together with the current ``param_groups`` values."""
+        self._step += 1
+        self._step_t.fill_(self._step)
+        self._opt_called = True       # what torch's LRScheduler checks for "optimizer.step() ran first"
+        return self._step
+
+    @torch.no_grad()
+    def launch(self):
+        """Device half of a step: clip + AdamW over every parameter (2 launches), stream-ordered and
+        capturable.  Reads lr / step from ``self.dyn_ptr`` (a DphAdamDyn in device memory) when set,
+        else from ``param_groups`` at launch time."""
+        plist = self._params()
+        if not plist:
+            return
+        self._ensure_chunks(plist)
+        self._slot_table(plist)
+        s = _lib.stream_ptr()
+        clip = self.max_grad_norm is not None and self.max_grad_norm > 0
+        if clip:
+            call("dph_grad_sumsq", ptr(self._slots_dev), len(plist), ptr(self._cslot), ptr(self._cstart),
+                 self._nchunks, ptr(self._sumsq), s)
+        if self.dyn_ptr is not None:
+            call("dph_adamw_step_dev", ptr(self._slots_dev), len(plist), ptr(self._cslot), ptr(self._cstart),
+                 self._nchunks, self.dyn_ptr, ptr(self._sumsq) if clip else None, float(self.max_grad_norm or 0.0), s)
+        else:
+            groups = (DphAdamGroup * 4)()
+            for gi, g in enumerate(self.param_groups):
+                groups[gi].lr = g["lr"]
+                groups[gi].weight_decay = g["weight_decay"]
+                groups[gi].beta1 = g["betas"][0]
+                groups[gi].beta2 = g["betas"][1]
+                groups[gi].eps = g["eps"]
+            call("dph_adamw_step", ptr(self._slots_dev), len(plist), ptr(self._cslot), ptr(self._cstart),
+                 self._nchunks, groups, len(self.param_groups), self._step, ptr(self._sumsq) if clip else None,
+                 float(self.max_grad_norm or 0.0), s)
+        # the kernel wrote the masters behind autograd's back: bump their version counters so every
+        # cached bf16 GEMM image of them (ops.bf16_image & co.) is rebuilt before its next use
+        increment_version([p for _, p in plist])
+
     @torch.no_grad()
     def step(self, closure=None):
         loss = None
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
-        plist = self._params()
-        if not plist:
+        if not self._params():
             return loss
-        self._ensure_chunks(plist)
-        # per-param state and the slot table (grad pointers change every step)
-        if self._event is not None:
-            self._event.synchronize()     # previous H2D copy of the pinned table is done
-        slots = (DphTensorSlot * len(plist)).from_address(self._pinned.data_ptr())
-        for i, (gi, p) in enumerate(plist):
-            st = self.state[p]
-            if len(st) == 0:
-                st["step"] = torch.zeros((), dtype=torch.float32)
-                st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-                st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-            if p.grad is not None and not p.grad.is_contiguous():
-                p.grad = p.grad.contiguous()
-            if p.grad is not None and p.grad.dtype != torch.float32:
-                raise TypeError("FusedAdamW expects fp32 gradients")
-            slots[i].param = p.data_ptr()
-            slots[i].grad = p.grad.data_ptr() if p.grad is not None else 0
-            slots[i].exp_avg = st["exp_avg"].data_ptr()
-            slots[i].exp_avg_sq = st["exp_avg_sq"].data_ptr()
-            slots[i].n = p.numel()
-            slots[i].group = gi
-            st["step"] += 1
-        self._slots_dev.copy_(self._pinned, non_blocking=True)
-        self._event = torch.cuda.Event()
-        self._event.record()
-        self._step += 1
-        groups = (DphAdamGroup * 4)()
-        for gi, g in enumerate(self.param_groups):
-            groups[gi].lr = g["lr"]
-            groups[gi].weight_decay = g["weight_decay"]
-            groups[gi].beta1 = g["betas"][0]
-            groups[gi].beta2 = g["betas"][1]
-            groups[gi].eps = g["eps"]
-        s = _lib.stream_ptr()
-        clip = self.max_grad_norm is not None and self.max_grad_norm > 0
-        if clip:
-            call("dph_grad_sumsq", ptr(self._slots_dev), len(plist), ptr(self._cslot), ptr(self._cstart),
-                 self._nchunks, ptr(self._sumsq), s)
-        call("dph_adamw_step", ptr(self._slots_dev), len(plist), ptr(self._cslot), ptr(self._cstart), self._nchunks,
-             groups, len(self.param_groups), self._step, ptr(self._sumsq) if clip else None,
-             float(self.max_grad_norm or 0.0), s)
+        self.begin_step()
+        self.launch()
         return loss
 
 

@@ -7,9 +7,17 @@ seeded weights, identity-initialised per-group distill projections
 (distill.py:24-26, 86-99), ``configure_optimizers`` (AdamW groups +
 LinearDecayLR), gradient clipping, and the data-parallel all-reduce
 (``dphubert_amd.ddp.GradReducer`` over RCCL).
+
+``Trainer(graphs=True)`` replays the whole optimizer step (teacher + student forward, backward, the
+gradient all-reduce, clip + AdamW) as ONE captured HIP graph after ``graph_warmup`` eager steps:
+the per-step scalars (RNG epoch, learning rates, AdamW step, target sparsity) live in a device block
+that the host refreshes before every step (``stepstate.StepScalars``), so replays follow the
+reference schedule exactly while the host does ~50 us of work per step instead of enqueuing
+~1000 kernels through Python.
 """
 
 import copy
+import warnings
 from typing import List, Optional
 
 import torch
@@ -18,6 +26,7 @@ import torch.nn as nn
 from . import ops
 from .ddp import GradReducer
 from .lightning import DistillLoss, DistillModule
+from .stepstate import step_scalars
 from .synthetic import seeded_state_dict
 from .wav2vec2.model import wav2vec2_model
 
@@ -107,10 +116,18 @@ def fused_grad_groups(model) -> List[tuple]:
 
 
 class Trainer:
-    """One process per GPU; call ``step(batch)`` per optimizer update (accum_grad=1)."""
+    """One process per GPU; call ``step(batch)`` per micro-batch (optimizer update every
+    ``accum_grad`` calls).
+
+    ``graphs=True``: the first ``graph_warmup`` steps run eagerly (they build the optimizer state,
+    the gradient buckets and every cached GEMM image), the next one captures the whole step into a
+    HIP graph, and every later step copies its batch into the graph's static input buffers and
+    replays it.  Batches must keep one shape; ``accum_grad`` must be 1.  If the capture fails (an
+    op on the path that cannot be captured) the trainer warns and stays eager.
+    """
 
     def __init__(self, module: DistillModule, clip_norm: float = 10.0, bucket_mb: float = 64.0,
-                 accum_grad: int = 1):
+                 accum_grad: int = 1, graphs: bool = False, graph_warmup: int = 2):
         self.module = module
         opt = module.configure_optimizers(clip_norm=clip_norm)
         self.optimizer = opt["optimizer"]
@@ -119,22 +136,116 @@ class Trainer:
         self.reducer = GradReducer(params, bucket_mb=bucket_mb, groups=fused_grad_groups(module.student_model))
         self.accum_grad = accum_grad
         self._micro = 0
+        if graphs and accum_grad != 1:
+            raise ValueError("Trainer(graphs=True) replays whole optimizer steps: accum_grad must be 1")
+        self.graphs = bool(graphs)
+        self.graph_warmup = max(1, int(graph_warmup))
+        self._n_eager = 0
+        self._graph = None
+        self._prof_graph = None
+        self._static = None
+        self._static_loss = None
+        self._prof_loss = None
+        self.scalars = None
 
-    def step(self, batch):
+    # ---- per-step device scalars -------------------------------------------------------------
+    def _bind_scalars(self, device):
+        if self.scalars is None:
+            self.scalars = step_scalars(device)
+            self.optimizer.dyn_ptr = self.scalars.adam_dyn_ptr
+            self.module.target_sparsity_dev = self.scalars.target_sparsity
+        return self.scalars
+
+    def _upload(self, device, adam_step: int):
         m = self.module
-        m.train()
-        self.reducer.prepare(zero=self._micro == 0, sync=self._micro + 1 == self.accum_grad)
+        tgt = m._get_target_sparsity() if m.use_reg else 0.0
+        self._bind_scalars(device).upload(target_sparsity=tgt, adam_groups=self.optimizer.param_groups,
+                                          adam_step=adam_step)
+
+    # ---- the GPU half of one (micro-)step: no host sync, capturable ---------------------------
+    def _gpu_step(self, batch, final: bool):
+        m = self.module
+        self.reducer.prepare(zero=self._micro == 0, sync=final)
         loss = m.training_step(batch, 0)
         (loss / self.accum_grad if self.accum_grad > 1 else loss).backward()
-        self._micro += 1
-        if self._micro < self.accum_grad:
-            return loss
+        if final:
+            self.reducer.finish()
+            self.optimizer.launch()
+        return loss
+
+    def _capture(self, prof=None):
+        """Record one whole step into a HIP graph (nothing executes during capture)."""
+        from .kernels import LaunchProfiler
+        ops.reset_zero_arena()           # zero-filled scratch must be allocated (and filled) inside the graph
+        g = torch.cuda.CUDAGraph()
+        try:
+            if prof is not None:
+                LaunchProfiler.active = prof
+            with torch.cuda.graph(g):
+                loss = self._gpu_step(self._static, True)
+        finally:
+            LaunchProfiler.active = None
+            ops.reset_zero_arena()
+        return g, loss
+
+    def _set_static(self, batch):
+        wave, lengths = batch
+        if self._static is None:
+            self._static = (wave.detach().clone(), lengths.detach().clone() if lengths is not None else None)
+            return
+        sw, sl = self._static
+        if wave.shape != sw.shape or (lengths is None) != (sl is None):
+            raise ValueError("Trainer(graphs=True): every batch must have the captured shape "
+                             f"{tuple(sw.shape)} (got {tuple(wave.shape)})")
+        sw.copy_(wave)
+        if lengths is not None:
+            sl.copy_(lengths)
+
+    def prepare_profiled_step(self, prof):
+        """Capture a second graph of the step whose GEMM launches are bracketed by timing events
+        (bench.py's live roofline); ``step(batch, profiled=True)`` replays it."""
+        if self._graph is None:
+            raise RuntimeError("prepare_profiled_step needs the main graph (run the warm-up steps first)")
+        self._prof_graph, self._prof_loss = self._capture(prof)
+
+    # ---- one step ----------------------------------------------------------------------------
+    def step(self, batch, profiled: bool = False):
+        m = self.module
+        m.train()
+        dev = batch[0].device
+        final = self._micro + 1 == self.accum_grad
+        adam_step = self.optimizer.begin_step() if final else self.optimizer._step + 1
+        self._upload(dev, adam_step)
+        if self.graphs and self._n_eager >= self.graph_warmup:
+            self._set_static(batch)
+            if self._graph is None:
+                try:
+                    self._graph, self._static_loss = self._capture()
+                except Exception as e:  # noqa: BLE001 -- uncapturable op: stay eager
+                    warnings.warn(f"HIP graph capture failed, running eagerly: {e!r}")
+                    self.graphs = False
+                    self._graph = None
+            if self._graph is not None:
+                if profiled and self._prof_graph is not None:
+                    self._prof_graph.replay()
+                    loss = self._prof_loss
+                else:
+                    self._graph.replay()
+                    loss = self._static_loss
+            else:
+                loss = self._gpu_step(batch, final)
+        else:
+            loss = self._gpu_step(batch, final)
+            self._n_eager += 1
+        if not final:
+            self._micro += 1
+            return loss.detach()
         self._micro = 0
-        self.reducer.finish()
-        self.optimizer.step()
+        loss = loss.detach()
         self.scheduler.step()
-        for g in self.optimizer.param_groups:
-            for p in g["params"]:
-                p.grad = None
+        if self._graph is None:
+            for g in self.optimizer.param_groups:
+                for p in g["params"]:
+                    p.grad = None
         m.global_step += 1
         return loss

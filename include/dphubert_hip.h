@@ -287,6 +287,33 @@ int dph_grad_sumsq(const DphTensorSlot* slots, int64_t n_slots, const int64_t* c
 int dph_adamw_step(const DphTensorSlot* slots, int64_t n_slots, const int64_t* chunk_slot, const int64_t* chunk_start,
                    int64_t n_chunks, const DphAdamGroup* groups, int64_t n_groups, int64_t step,
                    const float* sumsq, float max_norm, hipStream_t stream);
+/* the same with the per-group hyper-parameters and the (1-based) step read from DEVICE memory at
+ * run time, so a captured HIP graph replays a changing LR schedule (lightning.py:22-44) */
+typedef struct DphAdamDyn {
+  DphAdamGroup g[4];
+  float step;
+  float pad_[3];
+} DphAdamDyn;
+int dph_adamw_step_dev(const DphTensorSlot* slots, int64_t n_slots, const int64_t* chunk_slot,
+                       const int64_t* chunk_start, int64_t n_chunks, const DphAdamDyn* dyn, const float* sumsq,
+                       float max_norm, hipStream_t stream);
+
+/* ------------------------------------------------------------------------ *
+ * Per-step RNG epoch: every dropout / HardConcrete kernel adds (*epoch) * 0x9E3779B97F4A7C15 to
+ * its seed at entry (device word, uint64).  The trainer bumps the word with a stream-ordered op
+ * once per step, so HIP-graph replays draw fresh noise and a step's backward regenerates its
+ * forward's masks.  NULL detaches (seeds as passed).  Not stream-ordered; call outside capture.
+ * ------------------------------------------------------------------------ */
+int dph_set_rng_epoch(const uint64_t* epoch);
+
+/* ------------------------------------------------------------------------ *
+ * Timing events for live per-kernel durations (bench.py roofline): recorded as external
+ * event-record nodes when the stream is being captured into a HIP graph.  ev is a hipEvent_t.
+ * ------------------------------------------------------------------------ */
+int dph_event_create(void** ev);
+int dph_event_record(void* ev, hipStream_t stream);
+int dph_event_elapsed_ms(void* start, void* stop, float* ms);
+int dph_event_destroy(void* ev);
 
 #ifdef __cplusplus
 }
