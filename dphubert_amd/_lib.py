@@ -57,13 +57,16 @@ _SIGS = {
     "dph_abi_version": ([], C.c_int),
     "dph_gemm": ([C.POINTER(DphGemmArgs), S], C.c_int),
     "dph_layernorm_fwd": ([vp, vp, vp, vp, vp, vp, vp, i64, i64, f32, f32, u64, S], C.c_int),
-    "dph_layernorm_bwd": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, f32, u64, vp, f32, u64, vp, vp, vp, vp, S],
+    "dph_layernorm_bwd": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, f32, u64, vp, f32, u64, vp, vp, vp, vp, vp, i64,
+                           S],
                           C.c_int),
     "dph_layernorm_fwd_ld": ([vp, vp, vp, vp, vp, vp, vp, i64, i64, i64, f32, f32, u64, S], C.c_int),
     "dph_layernorm_bwd_ld": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, i64, f32, u64, vp, f32, u64, vp, vp, vp,
-                              vp, vp, S], C.c_int),
+                              vp, vp, vp, i64, S], C.c_int),
     "dph_wave_layernorm": ([vp, vp, i64, i64, f32, vp, S], C.c_int),
-    "dph_colsum": ([vp, vp, i64, i64, S], C.c_int),
+    "dph_colsum": ([vp, vp, i64, i64, vp, i64, S], C.c_int),
+    "dph_colsum_workspace": ([i64, i64], i64),
+    "dph_layernorm_bwd_workspace": ([i64, i64], i64),
     "dph_attention_fwd": ([vp, vp, vp, vp, vp, vp, i64, i64, i64, f32, f32, u64, S], C.c_int),
     "dph_attention_bwd_prep": ([vp, vp, vp, vp, vp, i64, i64, i64, S], C.c_int),
     "dph_attention_bwd": ([vp, vp, vp, vp, vp, vp, vp, i64, i64, i64, f32, f32, u64, S], C.c_int),
@@ -98,7 +101,7 @@ _SIGS = {
 }
 
 _lib = None
-ABI_VERSION = 4     # include/dphubert_hip.h layout (3: dph_adamw_step_dev + DphAdamDyn, dph_set_rng_epoch; 4: dph_event_*)
+ABI_VERSION = 5     # include/dphubert_hip.h layout (3: dph_adamw_step_dev, dph_set_rng_epoch; 4: dph_event_*; 5: LN bwd / colsum workspaces)
 
 
 class DphError(RuntimeError):

@@ -72,6 +72,18 @@ struct AttnShape {
   int64_t B, T, H, RS;  // RS = row stride of qkv (3*H*64)
 };
 
+// Dropout of the attention probabilities: element (row = (b*H+h)*T + q, key) draws 16 bits from ONE
+// 32-bit hash per (row, key pair) -- rows padded to an even key count, so the 4 consecutive keys a
+// lane holds in the forward / dQ kernels cost 2 hashes, and in the dK/dV kernel (4 queries of one
+// key per lane) neighbouring lanes (keys 2m, 2m+1) split the hashing and swap halves.
+__device__ __forceinline__ uint32_t attn_hash(uint64_t seed, uint64_t row, int64_t key, uint64_t half_tp) {
+  return drop_bits2(seed, row * half_tp + (uint64_t)(key >> 1));
+}
+
+__device__ __forceinline__ float attn_keep(uint32_t bits, bool odd_key, uint32_t thr, float inv_keep) {
+  return ((odd_key ? (bits >> 16) : (bits & 0xffffu)) >= thr) ? inv_keep : 0.f;
+}
+
 // stage a [rows][64] bf16 tile (rows from row0, clamped to T) from column block col0 into LDS.
 // swizzled: swz128 layout; else padded [rows][72].
 template <int ROWS, bool SWZ>
@@ -140,6 +152,8 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const bf16_t* __restrict_
   for (int d = 0; d < 4; ++d) oacc[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   float m_run = -INFINITY, l_run = 0.f;
   const float inv_keep = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
+  const uint32_t thr = drop_thr(drop_p);
+  const uint64_t half_tp = (uint64_t)(T + 1) >> 1;
 
   const int nkt = (int)cdiv(T, KT);
   uint4 rk[2], rv[2];
@@ -188,16 +202,22 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const bf16_t* __restrict_
     const float m_new = fmaxf(m_run, mt);
     const float alpha = __expf(m_run - m_new);
     float ls = 0.f;
-    const uint64_t drow = (((uint64_t)(b * H + h) * T) + (uint64_t)qme) * (uint64_t)T;
+    const uint64_t arow = (uint64_t)(b * H + h) * T + (uint64_t)qme;
 #pragma unroll
-    for (int s = 0; s < 4; ++s)
+    for (int s = 0; s < 4; ++s) {
+      uint32_t hb[2] = {0u, 0u};
+      if (drop_p > 0.f) {
+        const int64_t key0 = (int64_t)kt * KT + 16 * s + 4 * g;
+        hb[0] = attn_hash(seed, arow, key0, half_tp);
+        hb[1] = attn_hash(seed, arow, key0 + 2, half_tp);
+      }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const float p = __expf(sacc[s][i] - m_new);
         ls += p;
-        const int64_t key = (int64_t)kt * KT + 16 * s + 4 * g + i;
-        sacc[s][i] = p * dropout_scale(seed, drow + key, drop_p, inv_keep);
+        sacc[s][i] = drop_p > 0.f ? p * attn_keep(hb[i >> 1], i & 1, thr, inv_keep) : p;
       }
+    }
     ls += __shfl_xor(ls, 16, 64);
     ls += __shfl_xor(ls, 32, 64);
     l_run = l_run * alpha + ls;
@@ -304,6 +324,9 @@ __global__ void __launch_bounds__(256) attn_bwd_dkv_kernel(const bf16_t* __restr
   const int64_t klen = key_len ? key_len[b] : T;
   const float hm = head_mask ? head_mask[h] : 1.0f;
   const float inv_keep = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
+  const uint32_t thr = drop_thr(drop_p);
+  const uint64_t half_tp = (uint64_t)(T + 1) >> 1;
+  const bool odd_key = (kme & 1) != 0;
 
   // K[key = lane&15][hd 32ks+8g+j], V[...]: B operands of S = Q' K^T and dP = dO V^T
   bf16x8_t kf[2], vf[2];
@@ -368,7 +391,21 @@ __global__ void __launch_bounds__(256) attn_bwd_dkv_kernel(const bf16_t* __restr
     }
     f32x4_t pz[2], ds[2];
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
+    for (int u = 0; u < 2; ++u) {
+      // this lane hashes queries ia, ia+1 of its key pair; the neighbour (key ^ 1) the other two
+      uint32_t hb[4] = {0u, 0u, 0u, 0u};
+      if (drop_p > 0.f) {
+        const int ia = odd_key ? 2 : 0;
+        const uint64_t qa = (uint64_t)(b * H + h) * T + (uint64_t)(qt * QT_BWD + 16 * u + 4 * g + ia);
+        const uint32_t h0 = attn_hash(seed, qa, kme, half_tp);
+        const uint32_t h1 = attn_hash(seed, qa + 1, kme, half_tp);
+        const uint32_t o0 = (uint32_t)__shfl_xor((int)h0, 1, 64);
+        const uint32_t o1 = (uint32_t)__shfl_xor((int)h1, 1, 64);
+        hb[0] = odd_key ? o0 : h0;
+        hb[1] = odd_key ? o1 : h1;
+        hb[2] = odd_key ? h0 : o0;
+        hb[3] = odd_key ? h1 : o1;
+      }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int ql = 16 * u + 4 * g + i;
@@ -377,11 +414,11 @@ __global__ void __launch_bounds__(256) attn_bwd_dkv_kernel(const bf16_t* __restr
         if (kme >= klen) s += -10000.0f;
         float p = __expf(s - lse_s[cur * QT_BWD + ql]);
         if (q >= T || kme >= T) p = 0.f;
-        const float z = dropout_scale(seed, ((((uint64_t)(b * H + h) * T) + (uint64_t)q) * (uint64_t)T) + kme,
-                                      drop_p, inv_keep);
+        const float z = drop_p > 0.f ? attn_keep(hb[i], odd_key, thr, inv_keep) : 1.f;
         pz[u][i] = p * z;
         ds[u][i] = p * (pacc[u][i] * z - dv_s[cur * QT_BWD + ql]);
       }
+    }
     // dV[key][d] += sum_q PZ[q][key] dO'[q][d] ; dK[key][d] += sum_q dS[q][key] Q'[q][d]
     const bf16x8_t pzf = pack_frag(pz[0], pz[1]);
     const bf16x8_t dsf = pack_frag(ds[0], ds[1]);
@@ -461,7 +498,9 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(const bf16_t* __restri
   stage_store<KT, true>(ldsK(0), rk, tid);
   stage_store<KT, false>(ldsV(0), rv, tid);
   __syncthreads();
-  const uint64_t drow = (((uint64_t)(b * H + h) * T) + (uint64_t)qme) * (uint64_t)T;
+  const uint64_t arow = (uint64_t)(b * H + h) * T + (uint64_t)qme;
+  const uint32_t thr = drop_thr(drop_p);
+  const uint64_t half_tp = (uint64_t)(T + 1) >> 1;
   for (int kt = 0; kt < nkt; ++kt) {
     const int cur = kt & 1;
     const bool more = kt + 1 < nkt;
@@ -482,6 +521,12 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(const bf16_t* __restri
         sa = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka, qf[ks], sa, 0, 0, 0);
         pa = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, of[ks], pa, 0, 0, 0);
       }
+      uint32_t hb[2] = {0u, 0u};
+      if (drop_p > 0.f) {
+        const int64_t key0 = (int64_t)kt * KT + 16 * s + 4 * g;
+        hb[0] = attn_hash(seed, arow, key0, half_tp);
+        hb[1] = attn_hash(seed, arow, key0 + 2, half_tp);
+      }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int64_t key = (int64_t)kt * KT + 16 * s + 4 * g + i;
@@ -489,7 +534,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(const bf16_t* __restri
         if (key >= klen) sv += -10000.0f;
         float p = __expf(sv - my_lse);
         if (key >= T || qme >= T) p = 0.f;
-        const float z = dropout_scale(seed, drow + key, drop_p, inv_keep);
+        const float z = drop_p > 0.f ? attn_keep(hb[i >> 1], i & 1, thr, inv_keep) : 1.f;
         ds[s][i] = p * (pa[i] * z - my_D);
       }
     }

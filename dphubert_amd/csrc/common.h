@@ -146,6 +146,28 @@ __device__ __forceinline__ float dropout_scale(uint64_t seed, uint64_t idx, floa
   return u >= drop_thr(p) ? inv_keep : 0.0f;
 }
 
+// keep factors (0 or 1/(1-p)) of the 4 consecutive elements idx0..idx0+3: the same bits as four
+// dropout_scale calls, from 2 hashes (idx0 even) or 3 (odd)
+__device__ __forceinline__ void dropout_scale4(uint64_t seed, uint64_t idx0, float p, float inv_keep, float (&z)[4]) {
+  if (p <= 0.f) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) z[i] = 1.0f;
+    return;
+  }
+  const uint32_t thr = drop_thr(p);
+  const uint64_t pr = idx0 >> 1;
+  const uint32_t b0 = drop_bits2(seed, pr), b1 = drop_bits2(seed, pr + 1);
+  uint32_t u[4];
+  if ((idx0 & 1) == 0) {
+    u[0] = b0 & 0xffffu; u[1] = b0 >> 16; u[2] = b1 & 0xffffu; u[3] = b1 >> 16;
+  } else {
+    const uint32_t b2 = drop_bits2(seed, pr + 2);
+    u[0] = b0 >> 16; u[1] = b1 & 0xffffu; u[2] = b1 >> 16; u[3] = b2 & 0xffffu;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) z[i] = u[i] >= thr ? inv_keep : 0.0f;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

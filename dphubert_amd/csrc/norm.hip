@@ -11,204 +11,239 @@ namespace dph {
 namespace {
 
 constexpr int LN_MAXV = 4;   // up to 4 x (64 lanes x 4 elements) = 1024 columns
+constexpr int LN_FWD_RPW = 2;   // rows per wave, forward (both rows' loads issued before any math)
+constexpr int LN_BWD_RPW = 2;   // rows per wave, backward
+constexpr int LN_BWD_WAVES = 8; // 512-thread backward blocks: 16 rows share one LDS column reduction
 
+__device__ __forceinline__ void unpack4(uint2 r, float (&o)[4]) {
+  o[0] = __uint_as_float(r.x << 16);
+  o[1] = __uint_as_float(r.x & 0xffff0000u);
+  o[2] = __uint_as_float(r.y << 16);
+  o[3] = __uint_as_float(r.y & 0xffff0000u);
+}
+
+// per-column vector (gamma / beta / scale) for the NV 4-column chunks a lane owns; 0 past D
+template <int NV>
+__device__ __forceinline__ void load_cols(const float* __restrict__ v, int D, int lane, float fill, float (&o)[NV][4]) {
+#pragma unroll
+  for (int c = 0; c < NV; ++c) {
+    const int col = (c * 64 + lane) * 4;
+    if (v && col + 4 <= D && (D & 3) == 0) {
+      const float4 t = *reinterpret_cast<const float4*>(v + col);
+      o[c][0] = t.x; o[c][1] = t.y; o[c][2] = t.z; o[c][3] = t.w;
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o[c][i] = (col + i < D) ? (v ? v[col + i] : fill) : 0.f;
+    }
+  }
+}
+
+// Forward: one wave owns LN_FWD_RPW rows; gamma/beta live in registers, all row loads are issued
+// first (latency of the HBM reads overlaps across rows), fp32 two-pass statistics in registers.
+// Rows have stride ld >= D (ld % 4 == 0); columns [D, ld) are row padding: read as 0, written as 0.
+template <int NV>
 __global__ void __launch_bounds__(256) ln_fwd_kernel(const bf16_t* __restrict__ x, const float* __restrict__ xscale,
                                                      const float* __restrict__ gamma, const float* __restrict__ beta,
                                                      bf16_t* __restrict__ y, float* __restrict__ mean_out,
                                                      float* __restrict__ rstd_out, int64_t rows, int D, int ld,
                                                      float eps, float drop_p, uint64_t seed) {
   seed = epoch_seed(seed);   // per-step RNG epoch (graph replays)
-  // rows have stride ld >= D (ld % 4 == 0); columns [D, ld) are row padding: read as 0, written as 0
   const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= rows) return;
-  const bf16_t* xr = x + row * ld;
-  float v[LN_MAXV][4];
-  float s = 0.f;
+  const int64_t r0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * LN_FWD_RPW;
+  if (r0 >= rows) return;
+  uint2 raw[LN_FWD_RPW][NV];
 #pragma unroll
-  for (int c = 0; c < LN_MAXV; ++c) {
-    const int col = (c * 64 + lane) * 4;
-    if (col < D) {
-      uint2 raw = *reinterpret_cast<const uint2*>(xr + col);
-      v[c][0] = __uint_as_float(raw.x << 16);
-      v[c][1] = __uint_as_float(raw.x & 0xffff0000u);
-      v[c][2] = __uint_as_float(raw.y << 16);
-      v[c][3] = __uint_as_float(raw.y & 0xffff0000u);
+  for (int r = 0; r < LN_FWD_RPW; ++r)
+#pragma unroll
+    for (int c = 0; c < NV; ++c) {
+      const int col = (c * 64 + lane) * 4;
+      raw[r][c] = (r0 + r < rows && col < D) ? *reinterpret_cast<const uint2*>(x + (r0 + r) * ld + col)
+                                              : make_uint2(0, 0);
+    }
+  float ga[NV][4], be[NV][4], xs[NV][4];
+  load_cols<NV>(gamma, D, lane, 1.f, ga);
+  load_cols<NV>(beta, D, lane, 0.f, be);
+  load_cols<NV>(xscale, D, lane, 1.f, xs);
+  const float inv_keep = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
+  const float invD = 1.0f / (float)D;
+#pragma unroll
+  for (int r = 0; r < LN_FWD_RPW; ++r) {
+    const int64_t row = r0 + r;
+    if (row >= rows) break;
+    float v[NV][4];
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < NV; ++c) {
+      const int col = (c * 64 + lane) * 4;
+      unpack4(raw[r][c], v[c]);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        if (col + i >= D) v[c][i] = 0.f;
-        else if (xscale) v[c][i] *= xscale[col + i];
+        v[c][i] = (col + i < D) ? v[c][i] * xs[c][i] : 0.f;
+        s += v[c][i];
       }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) s += v[c][i];
-    } else {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) v[c][i] = 0.f;
     }
-  }
-  const float mean = wave_sum(s) / D;
-  float q = 0.f;
+    const float mean = wave_sum(s) * invD;
+    float q = 0.f;
 #pragma unroll
-  for (int c = 0; c < LN_MAXV; ++c) {
-    const int col = (c * 64 + lane) * 4;
-    if (col < D) {
+    for (int c = 0; c < NV; ++c) {
+      const int col = (c * 64 + lane) * 4;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const float d = v[c][i] - mean;
-        if (col + i < D) q += d * d;
+        q += (col + i < D) ? d * d : 0.f;
       }
     }
-  }
-  const float var = wave_sum(q) / D;
-  const float rstd = rsqrtf(var + eps);
-  const float inv_keep = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
+    const float rstd = rsqrtf(wave_sum(q) * invD + eps);
 #pragma unroll
-  for (int c = 0; c < LN_MAXV; ++c) {
-    const int col = (c * 64 + lane) * 4;
-    if (col < ld) {
-      float o[4];
+    for (int c = 0; c < NV; ++c) {
+      const int col = (c * 64 + lane) * 4;
+      if (col < ld) {
+        float z[4];
+        dropout_scale4(seed, (uint64_t)row * D + col, drop_p, inv_keep, z);
+        float o[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        if (col + i < D) {
-          o[i] = (v[c][i] - mean) * rstd * gamma[col + i] + beta[col + i];
-          o[i] *= dropout_scale(seed, (uint64_t)row * D + col + i, drop_p, inv_keep);
-        } else {
-          o[i] = 0.f;
-        }
+        for (int i = 0; i < 4; ++i) o[i] = (col + i < D) ? ((v[c][i] - mean) * rstd * ga[c][i] + be[c][i]) * z[i] : 0.f;
+        *reinterpret_cast<uint2*>(y + row * ld + col) = make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
       }
-      *reinterpret_cast<uint2*>(y + row * ld + col) = make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
     }
-  }
-  if (lane == 0) {
-    mean_out[row] = mean;
-    rstd_out[row] = rstd;
+    if (lane == 0) {
+      mean_out[row] = mean;
+      rstd_out[row] = rstd;
+    }
   }
 }
 
-// Backward.  Each wave walks rows with a grid stride; per-column partials
-// (dgamma, dbeta, branch column sums) stay in registers, are reduced across
-// the block's 4 waves through LDS and land with one atomic per column.
-__global__ void __launch_bounds__(256) ln_bwd_kernel(
+// Backward: 8 waves x LN_BWD_RPW rows per block, every row load issued before the math.  Per-column
+// partials (dgamma, dbeta, branch column sums) are summed in registers over the wave's rows, then
+// across the block's waves with LDS atomics, and written as one slab row per block; slab_reduce
+// adds the columns into the outputs.  (One global atomic per column per block -- ~500 blocks onto
+// the same 2304 addresses -- measured 0.09 TB/s: same-address atomics serialise at the memory side.)
+template <int NV>
+__global__ void __launch_bounds__(64 * LN_BWD_WAVES) ln_bwd_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const float* __restrict__ xscale,
     const float* __restrict__ gamma, const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
     bf16_t* __restrict__ dx, float* __restrict__ dgamma, float* __restrict__ dbeta, int64_t rows, int D, int ld,
-    float drop_p,
-    uint64_t seed, bf16_t* __restrict__ branch, float branch_p, uint64_t branch_seed,
+    float drop_p, uint64_t seed, bf16_t* __restrict__ branch, float branch_p, uint64_t branch_seed,
     const float* __restrict__ branch_smask, float* __restrict__ branch_colsum, const bf16_t* __restrict__ branch_pre,
-    float* __restrict__ branch_sdot, const bf16_t* __restrict__ dx_add) {
+    float* __restrict__ branch_sdot, const bf16_t* __restrict__ dx_add, float* __restrict__ ws) {
   seed = epoch_seed(seed); branch_seed = epoch_seed(branch_seed);   // per-step RNG epoch (graph replays)
-  __shared__ float red[4][3][LN_MAXV * 256];
+  __shared__ float4 red[LN_BWD_WAVES][NV * 64];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
+  const int64_t r0 = ((int64_t)blockIdx.x * LN_BWD_WAVES + wave) * LN_BWD_RPW;
+  uint2 rx[LN_BWD_RPW][NV], rd[LN_BWD_RPW][NV];
+#pragma unroll
+  for (int r = 0; r < LN_BWD_RPW; ++r)
+#pragma unroll
+    for (int c = 0; c < NV; ++c) {
+      const int col = (c * 64 + lane) * 4;
+      const bool ok = r0 + r < rows && col < D;
+      rx[r][c] = ok ? *reinterpret_cast<const uint2*>(x + (r0 + r) * ld + col) : make_uint2(0, 0);
+      rd[r][c] = ok ? *reinterpret_cast<const uint2*>(dy + (r0 + r) * ld + col) : make_uint2(0, 0);
+    }
+  float ga[NV][4], xs[NV][4];
+  load_cols<NV>(gamma, D, lane, 1.f, ga);
+  load_cols<NV>(xscale, D, lane, 1.f, xs);
   const float inv_keep = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
   const float binv_keep = branch_p > 0.f ? 1.f / (1.f - branch_p) : 1.f;
   const float bsm = branch_smask ? *branch_smask : 1.0f;
-  float pg[LN_MAXV][4], pb[LN_MAXV][4], pc[LN_MAXV][4];
+  const float invD = 1.0f / (float)D;
+  float pg[NV][4], pb[NV][4], pc[NV][4];
 #pragma unroll
-  for (int c = 0; c < LN_MAXV; ++c)
+  for (int c = 0; c < NV; ++c)
 #pragma unroll
     for (int i = 0; i < 4; ++i) pg[c][i] = pb[c][i] = pc[c][i] = 0.f;
   float sdot = 0.f;
-
-  for (int64_t row = (int64_t)blockIdx.x * 4 + wave; row < rows; row += (int64_t)gridDim.x * 4) {
+#pragma unroll
+  for (int r = 0; r < LN_BWD_RPW; ++r) {
+    const int64_t row = r0 + r;
+    if (row >= rows) break;
     const float mean = mean_in[row];
     const float rstd = rstd_in[row];
-    float xh[LN_MAXV][4], g[LN_MAXV][4], dyv[LN_MAXV][4];
+    float xh[NV][4], g[NV][4], dyv[NV][4];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-    for (int c = 0; c < LN_MAXV; ++c) {
+    for (int c = 0; c < NV; ++c) {
       const int col = (c * 64 + lane) * 4;
-      if (col < D) {
-        uint2 rx = *reinterpret_cast<const uint2*>(x + row * ld + col);
-        uint2 rd = *reinterpret_cast<const uint2*>(dy + row * ld + col);
-        float xv[4] = {__uint_as_float(rx.x << 16), __uint_as_float(rx.x & 0xffff0000u),
-                       __uint_as_float(rx.y << 16), __uint_as_float(rx.y & 0xffff0000u)};
-        float dv[4] = {__uint_as_float(rd.x << 16), __uint_as_float(rd.x & 0xffff0000u),
-                       __uint_as_float(rd.y << 16), __uint_as_float(rd.y & 0xffff0000u)};
+      float xv[4], dv[4], z[4];
+      unpack4(rx[r][c], xv);
+      unpack4(rd[r][c], dv);
+      dropout_scale4(seed, (uint64_t)row * D + col, drop_p, inv_keep, z);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const bool ok = col + i < D;
-          float xs = (xscale && ok) ? xv[i] * xscale[col + i] : xv[i];
-          xh[c][i] = ok ? (xs - mean) * rstd : 0.f;
-          dyv[c][i] = ok ? dv[i] * dropout_scale(seed, (uint64_t)row * D + col + i, drop_p, inv_keep) : 0.f;
-          g[c][i] = ok ? dyv[c][i] * gamma[col + i] : 0.f;
-          s1 += g[c][i];
-          s2 += g[c][i] * xh[c][i];
-          pg[c][i] += dyv[c][i] * xh[c][i];
-          pb[c][i] += dyv[c][i];
-        }
+      for (int i = 0; i < 4; ++i) {
+        const bool ok = col + i < D;
+        xh[c][i] = ok ? (xv[i] * xs[c][i] - mean) * rstd : 0.f;
+        dyv[c][i] = ok ? dv[i] * z[i] : 0.f;
+        g[c][i] = dyv[c][i] * ga[c][i];
+        s1 += g[c][i];
+        s2 += g[c][i] * xh[c][i];
+        pg[c][i] += dyv[c][i] * xh[c][i];
+        pb[c][i] += dyv[c][i];
       }
     }
-    s1 = wave_sum(s1) / D;
-    s2 = wave_sum(s2) / D;
+    s1 = wave_sum(s1) * invD;
+    s2 = wave_sum(s2) * invD;
 #pragma unroll
-    for (int c = 0; c < LN_MAXV; ++c) {
+    for (int c = 0; c < NV; ++c) {
       const int col = (c * 64 + lane) * 4;
-      if (col < ld) {
-        float o[4];
+      if (col >= ld) continue;
+      float o[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o[i] = (col + i < D) ? rstd * (g[c][i] - s1 - xh[c][i] * s2) * xs[c][i] : 0.f;
+      if (dx_add) {
+        // other gradient paths into the LN input (pre-norm residual); the branch output below
+        // stays the LN-path gradient only
+        float ad[4];
+        unpack4(*reinterpret_cast<const uint2*>(dx_add + row * ld + col), ad);
+        *reinterpret_cast<uint2*>(dx + row * ld + col) =
+            make_uint2(pack2bf(o[0] + ad[0], o[1] + ad[1]), pack2bf(o[2] + ad[2], o[3] + ad[3]));
+      } else {
+        *reinterpret_cast<uint2*>(dx + row * ld + col) = make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
+      }
+      if (branch) {
+        float pre[4] = {0.f, 0.f, 0.f, 0.f}, z[4], bo[4];
+        if (branch_sdot) unpack4(*reinterpret_cast<const uint2*>(branch_pre + row * ld + col), pre);
+        dropout_scale4(branch_seed, (uint64_t)row * D + col, branch_p, binv_keep, z);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const bool ok = col + i < D;
-          o[i] = ok ? rstd * (g[c][i] - s1 - xh[c][i] * s2) : 0.f;
-          if (xscale && ok) o[i] *= xscale[col + i];
+          const float zz = (col + i < D) ? o[i] * z[i] : 0.f;
+          sdot += zz * pre[i];
+          bo[i] = zz * bsm;
+          pc[c][i] += bo[i];
         }
-        if (dx_add) {
-          // other gradient paths into the LN input (pre-norm residual); the branch output below
-          // stays the LN-path gradient only
-          const uint2 ra = *reinterpret_cast<const uint2*>(dx_add + row * ld + col);
-          const float ad[4] = {__uint_as_float(ra.x << 16), __uint_as_float(ra.x & 0xffff0000u),
-                               __uint_as_float(ra.y << 16), __uint_as_float(ra.y & 0xffff0000u)};
-          *reinterpret_cast<uint2*>(dx + row * ld + col) =
-              make_uint2(pack2bf(o[0] + ad[0], o[1] + ad[1]), pack2bf(o[2] + ad[2], o[3] + ad[3]));
-        } else {
-          *reinterpret_cast<uint2*>(dx + row * ld + col) = make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
-        }
-        if (branch) {
-          float bo[4];
-          float pre[4] = {0.f, 0.f, 0.f, 0.f};
-          if (branch_sdot) {
-            uint2 rp = *reinterpret_cast<const uint2*>(branch_pre + row * ld + col);
-            pre[0] = __uint_as_float(rp.x << 16);
-            pre[1] = __uint_as_float(rp.x & 0xffff0000u);
-            pre[2] = __uint_as_float(rp.y << 16);
-            pre[3] = __uint_as_float(rp.y & 0xffff0000u);
-          }
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const float z = (col + i < D) ? o[i] * dropout_scale(branch_seed, (uint64_t)row * D + col + i, branch_p,
-                                                                 binv_keep) : 0.f;
-            sdot += z * pre[i];
-            bo[i] = z * bsm;
-            pc[c][i] += bo[i];
-          }
-          *reinterpret_cast<uint2*>(branch + row * ld + col) = make_uint2(pack2bf(bo[0], bo[1]),
-                                                                         pack2bf(bo[2], bo[3]));
-        }
+        *reinterpret_cast<uint2*>(branch + row * ld + col) = make_uint2(pack2bf(bo[0], bo[1]), pack2bf(bo[2], bo[3]));
       }
     }
   }
-  // block reduction of the column partials
+  // cross-wave column reduction, one quantity at a time: plain float4 LDS stores of every wave's
+  // partials, then each thread sums the 8 waves for its column quads and writes the block's slab
+  // row ws[block][3][D] (LDS float atomics with the 16-B lane stride ran 4-way bank-conflicted:
+  // +35 us per launch)
+  float* wrow = ws + (int64_t)blockIdx.x * 3 * D;
 #pragma unroll
-  for (int c = 0; c < LN_MAXV; ++c)
+  for (int q = 0; q < 3; ++q) {
+    const bool want = q == 0 ? dgamma != nullptr : (q == 1 ? dbeta != nullptr : branch_colsum != nullptr);
+    if (!want) continue;
+    __syncthreads();
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int col = (c * 64 + lane) * 4 + i;
-      red[wave][0][col] = pg[c][i];
-      red[wave][1][col] = pb[c][i];
-      red[wave][2][col] = pc[c][i];
+    for (int c = 0; c < NV; ++c) {
+      const float(&pq)[NV][4] = q == 0 ? pg : (q == 1 ? pb : pc);
+      red[wave][c * 64 + lane] = make_float4(pq[c][0], pq[c][1], pq[c][2], pq[c][3]);
     }
-  __syncthreads();
-  for (int col = threadIdx.x; col < D; col += 256) {
-    float a = 0.f, b = 0.f, cc = 0.f;
+    __syncthreads();
+    for (int j = threadIdx.x; j < NV * 64; j += 64 * LN_BWD_WAVES) {
+      float4 t = red[0][j];
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      a += red[w][0][col];
-      b += red[w][1][col];
-      cc += red[w][2][col];
+      for (int w = 1; w < LN_BWD_WAVES; ++w) {
+        const float4 u = red[w][j];
+        t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+      }
+      const int col = j * 4;
+      const float tv[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (col + i < D) wrow[q * D + col + i] = tv[i];
     }
-    if (dgamma) atomicAdd(dgamma + col, a);
-    if (dbeta) atomicAdd(dbeta + col, b);
-    if (branch_colsum) atomicAdd(branch_colsum + col, cc);
   }
   if (branch_sdot) {
     sdot = wave_sum(sdot);
@@ -257,8 +292,9 @@ __global__ void __launch_bounds__(1024) wave_norm_kernel(const float* __restrict
   for (int64_t i = threadIdx.x; i < S; i += blockDim.x) yr[i] = i < L ? (xr[i] - m) * r : 0.f;
 }
 
-// out[n] += sum_m x[m][n]; block = 64 x 4 threads, 8 columns per thread
-__global__ void __launch_bounds__(256) colsum_kernel(const bf16_t* __restrict__ x, float* __restrict__ out,
+// column partial sums of x [rows][cols] bf16: block (blockIdx.x: 512-column chunk, blockIdx.y: range of
+// rows_per_block rows) = 64 x 4 threads, 8 columns per thread -> ws[blockIdx.y][cols]
+__global__ void __launch_bounds__(256) colsum_kernel(const bf16_t* __restrict__ x, float* __restrict__ ws,
                                                      int64_t rows, int64_t cols, int64_t rows_per_block) {
   __shared__ float red[4][512];
   const int tx = threadIdx.x & 63;
@@ -289,9 +325,44 @@ __global__ void __launch_bounds__(256) colsum_kernel(const bf16_t* __restrict__ 
   __syncthreads();
   for (int c = threadIdx.x; c < 512; c += 256) {
     const int64_t col = (int64_t)blockIdx.x * 512 + c;
-    if (col < cols) atomicAdd(out + col, red[0][c] + red[1][c] + red[2][c] + red[3][c]);
+    if (col < cols) ws[(int64_t)blockIdx.y * cols + col] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
   }
 }
+
+// out_q[c] += sum_r ws[r][q * seg + c] for the (up to 3) column segments q of width seg (null outputs
+// skipped).  Block = 64 columns x 4 row phases over one of gridDim.y row groups; one atomic per column
+// per group (a handful of adders per address).
+__global__ void __launch_bounds__(256) slab_reduce_kernel(const float* __restrict__ ws, int64_t nrows, int64_t ncols,
+                                                          int64_t seg, float* __restrict__ o0, float* __restrict__ o1,
+                                                          float* __restrict__ o2) {
+  __shared__ float red[4][64];
+  const int tx = threadIdx.x & 63;
+  const int ty = threadIdx.x >> 6;
+  const int64_t col = (int64_t)blockIdx.x * 64 + tx;
+  const int64_t per = cdiv(nrows, (int64_t)gridDim.y);
+  const int64_t ra = (int64_t)blockIdx.y * per;
+  const int64_t rb = min(nrows, ra + per);
+  const int q = col < ncols ? (int)(col / seg) : 0;
+  float* out = q == 0 ? o0 : (q == 1 ? o1 : o2);
+  float s = 0.f;
+  if (col < ncols && out) {
+    int64_t r = ra + ty;
+    float s1 = 0.f;
+    for (; r + 4 < rb; r += 8) {
+      s += ws[r * ncols + col];
+      s1 += ws[(r + 4) * ncols + col];
+    }
+    if (r < rb) s += ws[r * ncols + col];
+    s += s1;
+  }
+  red[ty][tx] = s;
+  __syncthreads();
+  if (ty == 0 && col < ncols && out) atomicAdd(out + (col - (int64_t)q * seg), red[0][tx] + red[1][tx] + red[2][tx] + red[3][tx]);
+}
+
+int64_t slab_groups(int64_t nrows) { return std::max<int64_t>(1, std::min<int64_t>(8, cdiv(nrows, 64))); }
+
+int64_t colsum_rpb(int64_t rows) { return std::max<int64_t>(64, cdiv(cdiv(rows, 8192), 4) * 4); }
 
 }  // namespace
 }  // namespace dph
@@ -305,9 +376,17 @@ extern "C" int dph_layernorm_fwd_ld(const void* x, const float* xscale, const fl
   if (ld == 0) ld = D;
   DPH_REQUIRE(D >= 1 && ld >= D && ld % 4 == 0 && ld <= LN_MAXV * 256 && rows > 0,
               "dph_layernorm_fwd: unsupported D=%lld ld=%lld", (long long)D, (long long)ld);
-  hipLaunchKernelGGL(ln_fwd_kernel, dim3((unsigned)cdiv(rows, 4)), dim3(256), 0, stream,
-                     reinterpret_cast<const bf16_t*>(x), xscale, gamma, beta, reinterpret_cast<bf16_t*>(y), mean, rstd,
-                     rows, (int)D, (int)ld, eps, dropout_p, seed);
+  const dim3 grid((unsigned)cdiv(rows, 4 * LN_FWD_RPW));
+#define LN_FWD_LAUNCH(NV)                                                                                    \
+  hipLaunchKernelGGL(ln_fwd_kernel<NV>, grid, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(x), xscale, \
+                     gamma, beta, reinterpret_cast<bf16_t*>(y), mean, rstd, rows, (int)D, (int)ld, eps, dropout_p, seed)
+  switch (cdiv(ld, 256)) {
+    case 1: LN_FWD_LAUNCH(1); break;
+    case 2: LN_FWD_LAUNCH(2); break;
+    case 3: LN_FWD_LAUNCH(3); break;
+    default: LN_FWD_LAUNCH(4); break;
+  }
+#undef LN_FWD_LAUNCH
   return check_launch("dph_layernorm_fwd");
 }
 
@@ -317,25 +396,46 @@ extern "C" int dph_layernorm_fwd(const void* x, const float* xscale, const float
   return dph_layernorm_fwd_ld(x, xscale, gamma, beta, y, mean, rstd, rows, D, D, eps, dropout_p, seed, stream);
 }
 
+extern "C" int64_t dph_layernorm_bwd_workspace(int64_t rows, int64_t D) {
+  return cdiv(rows, (int64_t)LN_BWD_WAVES * LN_BWD_RPW) * 3 * D * 4;
+}
+
 extern "C" int dph_layernorm_bwd_ld(const void* dy, const void* x, const float* xscale, const float* gamma,
                                     const float* mean, const float* rstd, void* dx, float* dgamma, float* dbeta,
                                     int64_t rows, int64_t D, int64_t ld, float dropout_p, uint64_t seed, void* branch,
                                     float branch_p, uint64_t branch_seed, const float* branch_smask,
                                     float* branch_colsum, const void* branch_pre, float* branch_sdot,
-                                    const void* dx_add, hipStream_t stream) {
+                                    const void* dx_add, float* ws, int64_t ws_bytes, hipStream_t stream) {
   DPH_REQUIRE(dy && x && gamma && mean && rstd && dx, "dph_layernorm_bwd: null pointer");
   if (ld == 0) ld = D;
   DPH_REQUIRE(D >= 1 && ld >= D && ld % 4 == 0 && ld <= LN_MAXV * 256 && rows > 0,
               "dph_layernorm_bwd: unsupported D=%lld ld=%lld", (long long)D, (long long)ld);
   DPH_REQUIRE(!branch_sdot || branch_pre, "dph_layernorm_bwd: branch_sdot needs branch_pre");
   DPH_REQUIRE(!(branch_colsum || branch_sdot) || branch, "dph_layernorm_bwd: branch sums need branch output");
-  const int64_t blocks = std::min<int64_t>(cdiv(rows, 4 * 8), 1024);
-  hipLaunchKernelGGL(ln_bwd_kernel, dim3((unsigned)blocks), dim3(256), 0, stream,
-                     reinterpret_cast<const bf16_t*>(dy), reinterpret_cast<const bf16_t*>(x), xscale, gamma, mean,
-                     rstd, reinterpret_cast<bf16_t*>(dx), dgamma, dbeta, rows, (int)D, (int)ld, dropout_p, seed,
-                     reinterpret_cast<bf16_t*>(branch), branch_p, branch_seed, branch_smask, branch_colsum,
-                     reinterpret_cast<const bf16_t*>(branch_pre), branch_sdot,
-                     reinterpret_cast<const bf16_t*>(dx_add));
+  const bool sums = dgamma || dbeta || branch_colsum;
+  DPH_REQUIRE(!sums || (ws && ws_bytes >= dph_layernorm_bwd_workspace(rows, D)),
+              "dph_layernorm_bwd: workspace too small (%lld < %lld bytes)", (long long)ws_bytes,
+              (long long)dph_layernorm_bwd_workspace(rows, D));
+  const dim3 grid((unsigned)cdiv(rows, LN_BWD_WAVES * LN_BWD_RPW));
+#define LN_BWD_LAUNCH(NV)                                                                                        \
+  hipLaunchKernelGGL(ln_bwd_kernel<NV>, grid, dim3(64 * LN_BWD_WAVES), 0, stream,                                \
+                     reinterpret_cast<const bf16_t*>(dy), reinterpret_cast<const bf16_t*>(x), xscale, gamma, mean, \
+                     rstd, reinterpret_cast<bf16_t*>(dx), dgamma, dbeta, rows, (int)D, (int)ld, dropout_p, seed,  \
+                     reinterpret_cast<bf16_t*>(branch), branch_p, branch_seed, branch_smask, branch_colsum,       \
+                     reinterpret_cast<const bf16_t*>(branch_pre), branch_sdot, reinterpret_cast<const bf16_t*>(dx_add), \
+                     ws)
+  switch (cdiv(ld, 256)) {
+    case 1: LN_BWD_LAUNCH(1); break;
+    case 2: LN_BWD_LAUNCH(2); break;
+    case 3: LN_BWD_LAUNCH(3); break;
+    default: LN_BWD_LAUNCH(4); break;
+  }
+#undef LN_BWD_LAUNCH
+  if (sums) {
+    const int64_t nblk = grid.x;
+    hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)cdiv(3 * D, 64), (unsigned)slab_groups(nblk)), dim3(256),
+                       0, stream, ws, nblk, 3 * D, D, dgamma, dbeta, branch_colsum);
+  }
   return check_launch("dph_layernorm_bwd");
 }
 
@@ -350,18 +450,27 @@ extern "C" int dph_layernorm_bwd(const void* dy, const void* x, const float* xsc
                                  const float* mean, const float* rstd, void* dx, float* dgamma, float* dbeta,
                                  int64_t rows, int64_t D, float dropout_p, uint64_t seed, void* branch,
                                  float branch_p, uint64_t branch_seed, const float* branch_smask,
-                                 float* branch_colsum, const void* branch_pre, float* branch_sdot,
-                                 hipStream_t stream) {
+                                 float* branch_colsum, const void* branch_pre, float* branch_sdot, float* ws,
+                                 int64_t ws_bytes, hipStream_t stream) {
   return dph_layernorm_bwd_ld(dy, x, xscale, gamma, mean, rstd, dx, dgamma, dbeta, rows, D, D, dropout_p, seed,
                               branch, branch_p, branch_seed, branch_smask, branch_colsum, branch_pre, branch_sdot,
-                              nullptr, stream);
+                              nullptr, ws, ws_bytes, stream);
 }
 
-extern "C" int dph_colsum(const void* x, float* out, int64_t rows, int64_t cols, hipStream_t stream) {
+extern "C" int64_t dph_colsum_workspace(int64_t rows, int64_t cols) {
+  return cdiv(rows, colsum_rpb(rows)) * cols * 4;
+}
+
+extern "C" int dph_colsum(const void* x, float* out, int64_t rows, int64_t cols, float* ws, int64_t ws_bytes,
+                          hipStream_t stream) {
   DPH_REQUIRE(x && out && rows > 0 && cols > 0, "dph_colsum: bad args");
-  const int64_t rpb = std::max<int64_t>(64, cdiv(cdiv(rows, 8192), 4) * 4);
-  dim3 grid((unsigned)cdiv(cols, 512), (unsigned)cdiv(rows, rpb));
-  hipLaunchKernelGGL(colsum_kernel, grid, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(x), out, rows, cols,
+  DPH_REQUIRE(ws && ws_bytes >= dph_colsum_workspace(rows, cols), "dph_colsum: workspace too small");
+  const int64_t rpb = colsum_rpb(rows);
+  const int64_t nrb = cdiv(rows, rpb);
+  dim3 grid((unsigned)cdiv(cols, 512), (unsigned)nrb);
+  hipLaunchKernelGGL(colsum_kernel, grid, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(x), ws, rows, cols,
                      rpb);
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)cdiv(cols, 64), (unsigned)slab_groups(nrb)), dim3(256), 0,
+                     stream, ws, nrb, cols, cols, out, (float*)nullptr, (float*)nullptr);
   return check_launch("dph_colsum");
 }

@@ -42,6 +42,21 @@ def _s():
     return _lib.stream_ptr()
 
 
+def _ws(nbytes: int, dev):
+    """Scratch for a column-partial slab (stream-ordered caching allocator: the block is reused only
+    by work queued after the kernel that consumes it)."""
+    t = torch.empty(max(int(nbytes), 4) // 4, dtype=F32, device=dev)
+    return ptr(t), t.numel() * 4
+
+
+def ln_ws(rows: int, D: int, dev):
+    return _ws(_lib.lib().dph_layernorm_bwd_workspace(rows, D), dev)
+
+
+def colsum_ws(rows: int, cols: int, dev):
+    return _ws(_lib.lib().dph_colsum_workspace(rows, cols), dev)
+
+
 # ---------------------------------------------------------------------------
 # counter-based seeds (dropout / HardConcrete noise)
 # ---------------------------------------------------------------------------
@@ -582,7 +597,7 @@ class FeatureProjectionFn(torch.autograd.Function):
         dlw, _ = go.buf(p_lw)
         dlb, _ = go.buf(p_lb)
         call("dph_layernorm_bwd_ld", ptr(dxn), ptr(x), None, ptr(ln_w), ptr(mu), ptr(rs), ptr(dx), ptr(dlw), ptr(dlb),
-             M, C, Cp, 0.0, 0, None, 0.0, 0, None, None, None, None, None, _s())
+             M, C, Cp, 0.0, 0, None, 0.0, 0, None, None, None, None, None, *ln_ws(M, C, dev), _s())
         del ws
         go.done()
         return dx, go.ret(p_lw), go.ret(p_lb), go.ret(p_w), go.ret(p_b), None
@@ -618,7 +633,7 @@ class LayerNormFn(torch.autograd.Function):
         dw = zeros_f32(D, x.device)
         db = zeros_f32(D, x.device)
         call("dph_layernorm_bwd", ptr(dy.contiguous()), ptr(x), None, ptr(w), ptr(mu), ptr(rs), ptr(dx), ptr(dw),
-             ptr(db), M, D, 0.0, 0, None, 0.0, 0, None, None, None, None, _s())
+             ptr(db), M, D, 0.0, 0, None, 0.0, 0, None, None, None, None, *ln_ws(M, D, x.device), _s())
         return dx, dw, db
 
 
@@ -682,13 +697,13 @@ class PosConvFn(torch.autograd.Function):
             dlw, _ = go.buf(p_lw)
             dlb, _ = go.buf(p_lb)
             call("dph_layernorm_bwd", ptr(dh), ptr(s0), None, ptr(ln_w), ptr(mu), ptr(rs), ptr(ds0), ptr(dlw),
-                 ptr(dlb), M, D, cfg["p"], ctx.seed, None, 0.0, 0, None, None, None, None, _s())
+                 ptr(dlb), M, D, cfg["p"], ctx.seed, None, 0.0, 0, None, None, None, None, *ln_ws(M, D, dev), _s())
         else:
             call("dph_branch_bwd", ptr(dh), ptr(ds0), M, D, cfg["p"], ctx.seed, None, None, 0, None, None, None, _s())
         dz = torch.empty_like(ds0)
         call("dph_gelu_mask_bwd", ptr(ds0), ptr(z), None, ptr(dz), None, M, D, _s())
         db, _ = go.buf(p_bias)
-        call("dph_colsum", ptr(dz), ptr(db), M, D, _s())
+        call("dph_colsum", ptr(dz), ptr(db), M, D, *colsum_ws(M, D, dev), _s())
         # input gradient: transposed conv = same batched GEMM over a re-padded dz with flipped weights
         P = Kk // 2
         Q = Kk - 1 - P
@@ -906,7 +921,8 @@ class EncoderLayerFn(torch.autograd.Function):
             dln2w, _ = go.buf(pr["ln2_w"])
             dln2b, _ = go.buf(pr["ln2_b"])
             call("dph_layernorm_bwd_ld", ptr(dxn2), ptr(s1), None, ptr(ln2_w), ptr(mu2), ptr(rs2), ptr(ds1),
-                 ptr(dln2w), ptr(dln2b), M, D, D, 0.0, 0, None, 0.0, 0, None, None, None, None, ptr(dout), _s())
+                 ptr(dln2w), ptr(dln2b), M, D, D, 0.0, 0, None, 0.0, 0, None, None, None, None, ptr(dout),
+                 *ln_ws(M, D, dev), _s())
             del k1, k2
         else:
             ds1 = dout
@@ -927,7 +943,7 @@ class EncoderLayerFn(torch.autograd.Function):
             call("dph_attention_bwd", ptr(sv["qkv"]), ptr(do_m), ptr(hm), ptr(sv["lse"]), ptr(Dvec), ptr(dqkv),
                  ptr(cfg["lengths"]), B, T, H, cfg["head_dim"] ** -0.5, cfg["p_attn"], sv["seed_a"], _s())
             dbqkv, _ = go.buf(pr["bq"], pr["bk"], pr["bv"])
-            call("dph_colsum", ptr(dqkv), ptr(dbqkv), M, dqkv.shape[1], _s())
+            call("dph_colsum", ptr(dqkv), ptr(dbqkv), M, dqkv.shape[1], *colsum_ws(M, dqkv.shape[1], dev), _s())
             dwqkv, direct = go.buf(pr["wq"], pr["wk"], pr["wv"], zero=False)
             k4 = K.linear_wgrad(dqkv, xn1, dwqkv, accumulate=direct)
             dxn1 = K.linear_dgrad(dqkv, sv["Wqkv"])
@@ -935,7 +951,8 @@ class EncoderLayerFn(torch.autograd.Function):
             dln1w, _ = go.buf(pr["ln1_w"])
             dln1b, _ = go.buf(pr["ln1_b"])
             call("dph_layernorm_bwd_ld", ptr(dxn1), ptr(h), None, ptr(ln1_w), ptr(mu1), ptr(rs1), ptr(dh),
-                 ptr(dln1w), ptr(dln1b), M, D, D, 0.0, 0, None, 0.0, 0, None, None, None, None, ptr(ds1), _s())
+                 ptr(dln1w), ptr(dln1b), M, D, D, 0.0, 0, None, 0.0, 0, None, None, None, None, ptr(ds1),
+                 *ln_ws(M, D, dev), _s())
             del k3, k4
         else:
             dh = ds1
@@ -971,7 +988,7 @@ class EncoderLayerFn(torch.autograd.Function):
             g["lmf"] = z(1) if has_lmf else None
             call("dph_layernorm_bwd", ptr(dout), ptr(s2), None, ptr(ln2_w), ptr(mu2), ptr(rs2), ptr(ds2),
                  ptr(dln2w), ptr(dln2b), M, D, 0.0, 0, ptr(dy), cfg["p_drop"], sv["seed_o"], ptr(lmf), ptr(db2),
-                 ptr(sv["y_pre"]), ptr(g["lmf"]), _s())
+                 ptr(sv["y_pre"]), ptr(g["lmf"]), *ln_ws(M, D, dev), _s())
             F_ = sv["F"]
             dw2, direct = go.buf(pr["w2"], zero=False)
             k1 = K.linear_wgrad(dy, sv["f"], dw2, accumulate=direct, k_in=F_)
@@ -986,7 +1003,8 @@ class EncoderLayerFn(torch.autograd.Function):
             del k1, k2
         else:
             call("dph_layernorm_bwd", ptr(dout), ptr(s2), None, ptr(ln2_w), ptr(mu2), ptr(rs2), ptr(ds2),
-                 ptr(dln2w), ptr(dln2b), M, D, 0.0, 0, None, 0.0, 0, None, None, None, None, _s())
+                 ptr(dln2w), ptr(dln2b), M, D, 0.0, 0, None, 0.0, 0, None, None, None, None, *ln_ws(M, D, dev),
+                 _s())
             dh1 = ds2
         # ---- LN1 backward (+ attention branch gradient) ----
         ds1 = torch.empty_like(dout)
@@ -998,7 +1016,7 @@ class EncoderLayerFn(torch.autograd.Function):
             g["lma"] = z(1) if has_lma else None
             call("dph_layernorm_bwd", ptr(dh1), ptr(s1), None, ptr(ln1_w), ptr(mu1), ptr(rs1), ptr(ds1),
                  ptr(dln1w), ptr(dln1b), M, D, 0.0, 0, ptr(da), cfg["p_drop"], sv["seed_d"], ptr(lma), ptr(dbo),
-                 ptr(sv["a_pre"]), ptr(g["lma"]), _s())
+                 ptr(sv["a_pre"]), ptr(g["lma"]), *ln_ws(M, D, dev), _s())
             dwo, direct = go.buf(pr["wo"], zero=False)
             k3 = K.linear_wgrad(da, sv["o_m"], dwo, accumulate=direct)
             do_m = K.linear_dgrad(da, sv["Wo"])
@@ -1009,14 +1027,15 @@ class EncoderLayerFn(torch.autograd.Function):
             call("dph_attention_bwd", ptr(sv["qkv"]), ptr(do_m), ptr(hm), ptr(sv["lse"]), ptr(Dvec), ptr(dqkv),
                  ptr(cfg["lengths"]), B, T, H, cfg["head_dim"] ** -0.5, cfg["p_attn"], sv["seed_a"], _s())
             dbqkv, _ = go.buf(pr["bq"], pr["bk"], pr["bv"])
-            call("dph_colsum", ptr(dqkv), ptr(dbqkv), M, dqkv.shape[1], _s())
+            call("dph_colsum", ptr(dqkv), ptr(dbqkv), M, dqkv.shape[1], *colsum_ws(M, dqkv.shape[1], dev), _s())
             dwqkv, direct = go.buf(pr["wq"], pr["wk"], pr["wv"], zero=False)
             k4 = K.linear_wgrad(dqkv, h, dwqkv, accumulate=direct)
             dh = K.linear_dgrad(dqkv, sv["Wqkv"], residual=ds1)
             del k3, k4
         else:
             call("dph_layernorm_bwd", ptr(dh1), ptr(s1), None, ptr(ln1_w), ptr(mu1), ptr(rs1), ptr(ds1),
-                 ptr(dln1w), ptr(dln1b), M, D, 0.0, 0, None, 0.0, 0, None, None, None, None, _s())
+                 ptr(dln1w), ptr(dln1b), M, D, 0.0, 0, None, 0.0, 0, None, None, None, None, *ln_ws(M, D, dev),
+                 _s())
             dh = ds1
         go.done()
         order = ["wq", "wk", "wv", "bq", "bk", "bv", "wo", "bo", "ln1_w", "ln1_b", "w1", "b1", "w2", "b2", "ln2_w",
@@ -1087,7 +1106,7 @@ class DistillProjLossFn(torch.autograd.Function):
         for l in range(L):
             p = cfg["proj_index"][l]
             keep.append(K.linear_wgrad(ds[l], sh[l], dW[p], accumulate=True))
-            call("dph_colsum", ptr(ds[l]), ptr(db[p]), M, Dt, _s())
+            call("dph_colsum", ptr(ds[l]), ptr(db[p]), M, Dt, *colsum_ws(M, Dt, dev), _s())
             dh.append(K.linear_dgrad(ds[l], imgs[p]))
         go.done()
         grads = [None] + dh

@@ -113,7 +113,10 @@ int dph_layernorm_bwd(const void* dy, const void* x, const float* xscale, const 
                       const float* rstd, void* dx, float* dgamma, float* dbeta, int64_t rows, int64_t D,
                       float dropout_p, uint64_t seed, void* branch, float branch_p, uint64_t branch_seed,
                       const float* branch_smask, float* branch_colsum, const void* branch_pre,
-                      float* branch_sdot, hipStream_t stream);
+                      float* branch_sdot, float* ws, int64_t ws_bytes, hipStream_t stream);
+/* workspace (bytes) of dph_layernorm_bwd(_ld): per-block column-partial slab, reduced by a second
+ * kernel (same-address atomics from hundreds of blocks serialise at the memory side) */
+int64_t dph_layernorm_bwd_workspace(int64_t rows, int64_t D);
 
 /* the same over rows of stride ld >= D (ld % 4 == 0): columns [D, ld) are row padding (pruned
  * students' channel counts padded to multiples of 8), read as 0 and written as 0 */
@@ -126,15 +129,17 @@ int dph_layernorm_bwd_ld(const void* dy, const void* x, const float* xscale, con
                          const float* rstd, void* dx, float* dgamma, float* dbeta, int64_t rows, int64_t D, int64_t ld,
                          float dropout_p, uint64_t seed, void* branch, float branch_p, uint64_t branch_seed,
                          const float* branch_smask, float* branch_colsum, const void* branch_pre, float* branch_sdot,
-                         const void* dx_add, hipStream_t stream);
+                         const void* dx_add, float* ws, int64_t ws_bytes, hipStream_t stream);
 /* per-utterance waveform LayerNorm, model.py:96-103 (normalize_waveform, wav2vec2-Large):
  * y[b][:len_b] = (x - mean) / sqrt(var + eps) over the first len_b samples, y[b][len_b:] = 0
  * (lengths == NULL: full rows) */
 int dph_wave_layernorm(const float* x, const int64_t* lengths, int64_t B, int64_t S, float eps, float* y,
                        hipStream_t stream);
 
-/* column sums of a bf16 matrix (bias gradients): out[n] += sum_m x[m][n] */
-int dph_colsum(const void* x, float* out, int64_t rows, int64_t cols, hipStream_t stream);
+/* column sums of a bf16 matrix (bias gradients): out[n] += sum_m x[m][n]; ws: per-row-block partial
+ * slab of dph_colsum_workspace(rows, cols) bytes */
+int dph_colsum(const void* x, float* out, int64_t rows, int64_t cols, float* ws, int64_t ws_bytes, hipStream_t stream);
+int64_t dph_colsum_workspace(int64_t rows, int64_t cols);
 
 /* ------------------------------------------------------------------------ *
  * Fused multi-head self-attention (flash style), head dim 64.
