@@ -696,6 +696,27 @@ __device__ __forceinline__ bf16x8_t frag(const char* lds, int rb, int lane) {
   return *reinterpret_cast<const bf16x8_t*>(lds + row * 64 + phys * 16);
 }
 
+// mn-contiguous slice image: [KS k-rows][R] bf16 (rows of R*2 bytes); the 32-B unit u of k-row k holds
+// logical unit u ^ swz(k) (the register-staged kernel's swizzle, conflict free for the transposed
+// reads of a half-wave: k-rows {0..3, 8..11} + 16h).  Fragment: lane l gets X[rb + (l&15)][k = 8(l>>4)+j]
+// by two hardware-transposed ds_read_b64_tr_b16.
+__device__ __forceinline__ bf16x8_t frag_mn(const char* lds, int rb, int lane, int rbytes) {
+  const int g = lane >> 4;
+  const int i = lane & 15;
+  const int q = i >> 2;
+  const int p = i & 3;
+  const int k0 = 8 * g + q;
+  const int u = rb >> 4;
+  const int b0 = k0 * rbytes + ((u ^ swz(k0)) * 32) + 8 * p;
+  const int k1 = k0 + 4;
+  const int b1 = k1 * rbytes + ((u ^ swz(k1)) * 32) + 8 * p;
+  typedef __attribute__((address_space(3))) s16x4_t lds_s16x4;
+  s16x4_t v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + b0));
+  s16x4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + b1));
+  s16x8_t v = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
 template <int BM_, int BN_, int WTM_, int WTN_>
 struct Cfg {
   static constexpr int BM = BM_, BN = BN_, WTM = WTM_, WTN = WTN_;
@@ -737,13 +758,56 @@ struct Frags {
   bf16x8_t b[C::FN];
 };
 
-template <class C>
+template <class C, bool AK, bool BK>
 __device__ __forceinline__ void read_frags(Frags<C>& f, const char* slot, int wr, int wc, int lane) {
 #pragma unroll
-  for (int j = 0; j < C::FN; ++j) f.b[j] = frag(slot + C::HALF_A, wc * C::WTN + 16 * j, lane);
+  for (int j = 0; j < C::FN; ++j)
+    f.b[j] = BK ? frag(slot + C::HALF_A, wc * C::WTN + 16 * j, lane)
+                : frag_mn(slot + C::HALF_A, wc * C::WTN + 16 * j, lane, C::BN * 2);
 #pragma unroll
-  for (int i = 0; i < C::FM; ++i) f.a[i] = frag(slot, wr * C::WTM + 16 * i, lane);
+  for (int i = 0; i < C::FM; ++i)
+    f.a[i] = AK ? frag(slot, wr * C::WTM + 16 * i, lane) : frag_mn(slot, wr * C::WTM + 16 * i, lane, C::BM * 2);
 }
+
+// LDS-DMA source of one 16-B chunk per lane for an operand slice.
+//   k-contiguous ([rows][K]): row fixed per DMA, k advances by KS per slice (precomputed offset).
+//   mn-contiguous ([K][rows]): k-row kl of the slice fixed per DMA, the operand row index
+//     k = kbeg + KS*i + kl advances by KS per slice: tracked as (batch, row-in-batch) for
+//     rows_per_batch layouts (rpb >= KS: at most one carry per slice); rows past kend read row
+//     kend-1 (finite data; the A operand's tail rows are zeroed in LDS before use).
+template <bool KC, int DMAN>
+struct DmaSrc {
+  int64_t off[DMAN];   // KC: element offset incl. kbeg; MN: column offset within a row
+  int32_t kb[DMAN], kr[DMAN], kk[DMAN];   // MN: k-row as (batch, row in batch) and its absolute index
+};
+
+template <bool KC, int N, int NW, int R>
+__device__ __forceinline__ void dma_setup(DmaSrc<KC, N>& ds, const DphMat& d, int64_t r0, int64_t Rtot, int64_t kbeg,
+                                          int wave, int lane) {
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    const int c = (j * NW + wave) * 64 + lane;
+    if constexpr (KC) {
+      const int r = c >> 2;
+      ds.off[j] = row_addr(d, min(r0 + r, Rtot - 1)) + ((c & 3) ^ swz_chunk(r)) * 8 + kbeg;
+    } else {
+      constexpr int CPR = R / 8;                      // 16-B chunks per k-row
+      const int kl = c / CPR, pc = c % CPR;
+      const int lu = (pc >> 1) ^ swz(kl);
+      ds.off[j] = min(r0 + lu * 16 + (pc & 1) * 8, ((Rtot + 7) & ~(int64_t)7) - 8);
+      const int64_t k = kbeg + kl;
+      ds.kk[j] = (int32_t)k;
+      if (d.rows_per_batch > 0) {
+        ds.kb[j] = (int32_t)(k / d.rows_per_batch);
+        ds.kr[j] = (int32_t)(k % d.rows_per_batch);
+      } else {
+        ds.kb[j] = 0;
+        ds.kr[j] = (int32_t)k;
+      }
+    }
+  }
+}
+
 
 template <class C>
 __device__ __forceinline__ void mfma_slice(f32x4_t (&acc)[C::FM][C::FN], const Frags<C>& f) {
@@ -755,7 +819,7 @@ __device__ __forceinline__ void mfma_slice(f32x4_t (&acc)[C::FM][C::FN], const F
 }
 }  // namespace ring
 
-template <class C>
+template <class C, bool AK, bool BK>
 __global__ void __launch_bounds__(C::NT, C::MINB) ring_gemm_kernel(const DphGemmArgs a, int64_t kchunk) {
   __shared__ __attribute__((aligned(1024))) char smem[C::LDS];
   const int tid = threadIdx.x;
@@ -788,34 +852,61 @@ __global__ void __launch_bounds__(C::NT, C::MINB) ring_gemm_kernel(const DphGemm
   const int64_t n0 = tn * C::BN;
   const int64_t kbeg = split * kchunk;
   const int64_t kend = min(a.K, kbeg + kchunk);
-  const int H = DPH_ABLATE == 6 ? 0 : (int)(max<int64_t>(kend - kbeg, 0) / ring::KS);   // k-slices
+  // k-slices (whole slices unless both operands are mn-contiguous: then the last one may be partial)
+  const int H = DPH_ABLATE == 6 ? 0 : (int)cdiv(max<int64_t>(kend - kbeg, 0), ring::KS);
+  const int ktail = (int)((kend - kbeg) - (int64_t)(H - 1) * ring::KS);   // valid k-rows of slice H-1
   unsigned long long st0 = 0, st1 = 0, st2 = 0, st3 = 0, sA = 0, sB = 0, sC = 0;
   DPH_TSTAMP(st0);
 
-  // DMA sources: instruction j of wave w covers slice rows (j*NW+w)*16 .. +16; this lane loads
-  // row r = (j*NW+w)*16 + lane/4 into physical chunk lane%4 <- logical chunk (lane%4) ^ swz(r)
+  // DMA sources: instruction j of wave w fills bytes [(j*NW+w)*1024, +1024) of the operand's slot
+  // half (lane-linear), i.e. chunk c = (j*NW+w)*64 + lane.  k-contiguous: slice row c/4, physical
+  // chunk c%4 <- logical chunk (c%4) ^ swz(row).  mn-contiguous: k-row c/(R/8), physical chunk
+  // c%(R/8) of that k-row <- logical 32-B unit ((c%(R/8))>>1) ^ swz(k-row).
   const bf16_t* Ab = reinterpret_cast<const bf16_t*>(a.A.ptr) + z_addr(a.A, z);
   const bf16_t* Bb = reinterpret_cast<const bf16_t*>(a.B.ptr) + z_addr(a.B, z);
-  int64_t aoff[C::DMA_A], boff[C::DMA_B];
-#pragma unroll
-  for (int j = 0; j < C::DMA_A; ++j) {
-    const int r = (j * C::NW + wave) * 16 + (lane >> 2);
-    aoff[j] = row_addr(a.A, min(m0 + r, a.M - 1)) + ((lane & 3) ^ ring::swz_chunk(r)) * 8 + kbeg;
-  }
-#pragma unroll
-  for (int j = 0; j < C::DMA_B; ++j) {
-    const int r = (j * C::NW + wave) * 16 + (lane >> 2);
-    boff[j] = row_addr(a.B, min(n0 + r, a.N - 1)) + ((lane & 3) ^ ring::swz_chunk(r)) * 8 + kbeg;
-  }
-  auto issue = [&](int i) {   // k-slice i -> slot i % 4
+  ring::DmaSrc<AK, C::DMA_A> da;
+  ring::DmaSrc<BK, C::DMA_B> db;
+  ring::dma_setup<AK, C::DMA_A, C::NW, C::BM>(da, a.A, m0, a.M, kbeg, wave, lane);
+  ring::dma_setup<BK, C::DMA_B, C::NW, C::BN>(db, a.B, n0, a.N, kbeg, wave, lane);
+  const int64_t a_tail = AK ? 0 : row_addr(a.A, max<int64_t>(kend - 1, 0));
+  const int64_t b_tail = BK ? 0 : row_addr(a.B, max<int64_t>(kend - 1, 0));
+  // source element offset of DMA j for slice i (mn: advances the k-row state by KS)
+  auto src_mn = [&](auto& ds, const DphMat& d, int64_t tail, int j) -> int64_t {
+    const int64_t o = ds.kk[j] < kend ? (int64_t)ds.kb[j] * d.batch_stride + (int64_t)ds.kr[j] * d.row_stride + ds.off[j]
+                                      : tail + ds.off[j];
+    ds.kk[j] += ring::KS;
+    ds.kr[j] += ring::KS;
+    if (d.rows_per_batch > 0 && ds.kr[j] >= d.rows_per_batch) {
+      ds.kr[j] -= d.rows_per_batch;
+      ds.kb[j] += 1;
+    }
+    return o;
+  };
+  auto issue = [&](int i) {   // k-slice i -> slot i % 4 (called for i = 0, 1, 2, ... in order)
     char* la = smem + (i & (ring::NSLOT - 1)) * C::SLOT;
     char* lb = la + C::HALF_A;
     const int64_t ko = (int64_t)i * ring::KS;
 #pragma unroll
-    for (int j = 0; j < C::DMA_A; ++j) ring::dma16(Ab + aoff[j] + ko, la + (j * C::NW + wave) * 1024);
+    for (int j = 0; j < C::DMA_A; ++j)
+      ring::dma16(Ab + (AK ? da.off[j] + ko : src_mn(da, a.A, a_tail, j)), la + (j * C::NW + wave) * 1024);
 #pragma unroll
-    for (int j = 0; j < C::DMA_B; ++j) ring::dma16(Bb + boff[j] + ko, lb + (j * C::NW + wave) * 1024);
+    for (int j = 0; j < C::DMA_B; ++j)
+      ring::dma16(Bb + (BK ? db.off[j] + ko : src_mn(db, a.B, b_tail, j)), lb + (j * C::NW + wave) * 1024);
   };
+  // both operands mn-contiguous and K not a multiple of KS: zero the A operand's k-rows past kend in
+  // the last slice (its B rows repeat row kend-1: finite, multiplied by 0).  Runs after the slice's
+  // DMA landed for every wave (vmcnt(0) + barrier) and before any fragment read of it.
+  auto zero_tail = [&](int i) {
+    char* la = smem + (i & (ring::NSLOT - 1)) * C::SLOT;
+    const int nb = (ring::KS - ktail) * C::BM * 2;
+    for (int o = tid * 16; o < nb; o += C::NT * 16)
+      *reinterpret_cast<uint4*>(la + ktail * C::BM * 2 + o) = make_uint4(0, 0, 0, 0);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  const bool has_tail = !AK && ktail < ring::KS;
   auto slot = [&](int i) -> const char* { return smem + (i & (ring::NSLOT - 1)) * C::SLOT; };
 
   f32x4_t acc[C::FM][C::FN];
@@ -838,7 +929,8 @@ __global__ void __launch_bounds__(C::NT, C::MINB) ring_gemm_kernel(const DphGemm
     if (DPH_ABLATE != 3) __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     if (i + 4 < H && DPH_ABLATE != 1) issue(i + 4);
-    if (i + 1 < H && DPH_ABLATE != 4) ring::read_frags<C>(nxt, slot(i + 1), wr, wc, lane);
+    if (has_tail && i + 2 == H) zero_tail(i + 1);
+    if (i + 1 < H && DPH_ABLATE != 4) ring::read_frags<C, AK, BK>(nxt, slot(i + 1), wr, wc, lane);
     __builtin_amdgcn_sched_barrier(0);
     if (DPH_ABLATE != 2) {
       ring::mfma_slice<C>(acc, cur);
@@ -871,7 +963,8 @@ __global__ void __launch_bounds__(C::NT, C::MINB) ring_gemm_kernel(const DphGemm
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     ring::Frags<C> f0, f1;
-    ring::read_frags<C>(f0, slot(0), wr, wc, lane);
+    if (has_tail && H == 1) zero_tail(0);
+    ring::read_frags<C, AK, BK>(f0, slot(0), wr, wc, lane);
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_sched_barrier(0);
     DPH_TSTAMP(st1);
@@ -1064,14 +1157,34 @@ static int gemm_path_override() {
   return !strcmp(e, "small") ? 1 : !strcmp(e, "big") ? 2 : !strcmp(e, "mid") ? 3 : 0;
 }
 
-// 0: 128x128 register-staged kernel, 1: ring Mid (128x128), 2: ring Big (256x256)
+// an operand the ring kernels can stage: k-contiguous with whole 32-deep k-slices, or mn-contiguous
+// (any K: a partial last slice is zero-filled) whose batched row layout carries at most once per slice
+static bool ring_operand_ok(bool kcontig, const DphMat& d, int64_t K) {
+  if (kcontig) return K % ring::KS == 0;
+  if (K >= ((int64_t)1 << 31) - 2 * ring::KS) return false;   // 32-bit k-row state
+  return d.rows_per_batch == 0 || d.rows_per_batch >= ring::KS;
+}
+
+// 0: 128x128 register-staged kernel, 1: ring Mid (128x128), 2: ring Big (256x256).  The ring kernels
+// take (k, k), (k, mn) and (mn, mn) operand layouts; (mn, k) and K-tails beside a k-contiguous
+// operand stay on the register-staged kernel.
 static int gemm_kind(const DphGemmArgs& a, int64_t kchunk) {
-  const bool ring_ok = a.a_kcontig && a.b_kcontig && a.K % ring::KS == 0 && kchunk % ring::KS == 0;
+  // mn-contiguous operands on the ring measured slower than the register-staged kernel on every
+  // step shape (dgrad 7984x768x3072: 80 vs 73 us, conv1 wgrad 862 vs 642 us: two transposed reads per
+  // fragment and a barrier per 32-k slice), so by default they stay there; DPH_GEMM_PATH=mid/big
+  // forces the ring (tests cover both)
+  const int path0 = gemm_path_override();
+  const bool layouts = (a.a_kcontig && a.b_kcontig) || (path0 == 3 && !((!a.a_kcontig) && a.b_kcontig));
+  const bool ring_ok = layouts && ring_operand_ok(a.a_kcontig, a.A, a.K) && ring_operand_ok(a.b_kcontig, a.B, a.K) &&
+                       (a.splits == 1 || kchunk % ring::KS == 0);
+  // the 256x256 tile is k-contiguous only: its 128 accumulators leave no registers for the
+  // mn-contiguous k-row state (it spilled 28-100 VGPRs)
+  const bool big_ok = ring_ok && a.a_kcontig && a.b_kcontig;
   const int64_t tiles256 = cdiv(a.M, ring::Big::BM) * cdiv(a.N, ring::Big::BN) * a.batch * a.splits;
-  int kind = !ring_ok ? 0 : (tiles256 >= 480 ? 2 : 1);
+  int kind = !ring_ok ? 0 : ((big_ok && tiles256 >= 480) ? 2 : 1);
   const int path = gemm_path_override();
   if (path == 1) kind = 0;
-  if (path == 2 && ring_ok) kind = 2;
+  if (path == 2 && big_ok) kind = 2;
   if (path == 3 && ring_ok) kind = 1;
   return kind;
 }
@@ -1083,14 +1196,29 @@ static int64_t gemm_kchunk(const DphGemmArgs& a) {
 extern "C" const char* dph_gemm_variant(const DphGemmArgs* args) {
   if (!args) return "";
   const DphGemmArgs& a = *args;
-  switch (gemm_kind(a, gemm_kchunk(a))) {
-    case 2: return "ring::Cfg<256, 256, 128, 64>";
-    case 1: return "ring::Cfg<128, 128, 64, 64>";
-    default:
-      if (a.a_kcontig && a.b_kcontig) return "gemm_kernel<true, true>";
-      if (a.a_kcontig) return "gemm_kernel<true, false>";
-      if (a.b_kcontig) return "gemm_kernel<false, true>";
-      return "gemm_kernel<false, false>";
+  const int kind = gemm_kind(a, gemm_kchunk(a));
+  if (kind == 2) return "ring::Cfg<256, 256, 128, 64>, true, true>";
+  if (kind == 1) {
+    if (a.a_kcontig && a.b_kcontig) return "ring::Cfg<128, 128, 64, 64>, true, true>";
+    if (a.a_kcontig) return "ring::Cfg<128, 128, 64, 64>, true, false>";
+    return "ring::Cfg<128, 128, 64, 64>, false, false>";
+  }
+  if (a.a_kcontig && a.b_kcontig) return "gemm_kernel<true, true>";
+  if (a.a_kcontig) return "gemm_kernel<true, false>";
+  if (a.b_kcontig) return "gemm_kernel<false, true>";
+  return "gemm_kernel<false, false>";
+}
+
+template <class Cf, bool MN>
+static void launch_ring(const DphGemmArgs& a, int64_t kchunk, hipStream_t stream) {
+  dim3 g((unsigned)cdiv(a.N, Cf::BN), (unsigned)cdiv(a.M, Cf::BM), (unsigned)(a.batch * a.splits));
+  if constexpr (MN) {
+    if (a.a_kcontig)
+      hipLaunchKernelGGL((ring_gemm_kernel<Cf, true, false>), g, dim3(Cf::NT), 0, stream, a, kchunk);
+    else
+      hipLaunchKernelGGL((ring_gemm_kernel<Cf, false, false>), g, dim3(Cf::NT), 0, stream, a, kchunk);
+  } else {
+    hipLaunchKernelGGL((ring_gemm_kernel<Cf, true, true>), g, dim3(Cf::NT), 0, stream, a, kchunk);
   }
 }
 
@@ -1125,13 +1253,12 @@ extern "C" int dph_gemm(const DphGemmArgs* args, hipStream_t stream) {
   // 128x128 tile (DPH_GEMM_PATH=small|big|mid forces a path, for tests)
   const int kind = gemm_kind(a, kchunk);
   if (kind == 2) {
-    dim3 gb((unsigned)cdiv(a.N, ring::Big::BN), (unsigned)cdiv(a.M, ring::Big::BM), (unsigned)(a.batch * a.splits));
-    DPH_REQUIRE(gb.y < 65536 && gb.z < 65536, "dph_gemm: grid too large");
-    hipLaunchKernelGGL(ring_gemm_kernel<ring::Big>, gb, dim3(ring::Big::NT), 0, stream, a, kchunk);
+    DPH_REQUIRE(cdiv(a.M, ring::Big::BM) < 65536 && a.batch * a.splits < 65536, "dph_gemm: grid too large");
+    launch_ring<ring::Big, false>(a, kchunk, stream);
   } else if (kind == 1) {
-    dim3 gm((unsigned)cdiv(a.N, ring::Mid::BN), (unsigned)cdiv(a.M, ring::Mid::BM), (unsigned)(a.batch * a.splits));
-    DPH_REQUIRE(gm.y < 65536 && gm.z < 65536, "dph_gemm: grid too large");
-    hipLaunchKernelGGL(ring_gemm_kernel<ring::Mid>, gm, dim3(ring::Mid::NT), 0, stream, a, kchunk);
+    DPH_REQUIRE(cdiv(a.M, ring::Mid::BM) < 65536 && a.batch * a.splits < 65536, "dph_gemm: grid too large");
+    if (a.a_kcontig && a.b_kcontig) launch_ring<ring::Mid, false>(a, kchunk, stream);
+    else launch_ring<ring::Mid, true>(a, kchunk, stream);
   } else {
   dim3 grid((unsigned)cdiv(a.N, BN), (unsigned)cdiv(a.M, BM), (unsigned)(a.batch * a.splits));
   DPH_REQUIRE(grid.y < 65536 && grid.z < 65536, "dph_gemm: grid too large");
