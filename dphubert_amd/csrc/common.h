@@ -68,7 +68,7 @@ __device__ __forceinline__ void load_bf16x8(const bf16_t* p, int64_t c0, int64_t
 // (relative step 3.9e-3), so the approximation error is invisible.
 __device__ __forceinline__ float erfc_pos(float z, float& e_minus_z2) {
   // z >= 0; returns erfc(z) and exp(-z^2)
-  const float t = 1.0f / (1.0f + 0.5f * z);
+  const float t = __builtin_amdgcn_rcpf(1.0f + 0.5f * z);   // 1 ulp, no IEEE divide sequence
   const float p = -1.26551223f + t * (1.00002368f + t * (0.37409196f + t * (0.09678418f +
                   t * (-0.18628806f + t * (0.27886807f + t * (-1.13520398f + t * (1.48851587f +
                   t * (-0.82215223f + t * 0.17087277f))))))));

@@ -238,24 +238,46 @@ __global__ void __launch_bounds__(256) conv0_apply_kernel(const float* __restric
   }
 }
 
-__device__ __forceinline__ void load_dy4(const bf16_t* dyp, int64_t c0, int64_t C, float (&d)[4]) {
-  if (c0 + 4 <= C && (C & 3) == 0) {
-    const uint2 raw = *reinterpret_cast<const uint2*>(dyp);
-    d[0] = __uint_as_float(raw.x << 16);
-    d[1] = __uint_as_float(raw.x & 0xffff0000u);
-    d[2] = __uint_as_float(raw.y << 16);
-    d[3] = __uint_as_float(raw.y & 0xffff0000u);
+// CPT consecutive bf16 channels of one dy row -> fp32 (one 4/8/16-byte load when aligned)
+template <int CPT>
+__device__ __forceinline__ void load_dyc(const bf16_t* dyp, int64_t c0, int64_t C, float (&d)[CPT]) {
+  if (c0 + CPT <= C && (C % CPT) == 0) {
+    uint32_t r[CPT / 2];
+    if constexpr (CPT == 2) {
+      r[0] = *reinterpret_cast<const uint32_t*>(dyp);
+    } else if constexpr (CPT == 4) {
+      const uint2 v = *reinterpret_cast<const uint2*>(dyp);
+      r[0] = v.x; r[1] = v.y;
+    } else {
+      static_assert(CPT == 8, "CPT");
+      const uint4 v = *reinterpret_cast<const uint4*>(dyp);
+      r[0] = v.x; r[1] = v.y; r[2] = v.z; r[3] = v.w;
+    }
+#pragma unroll
+    for (int i = 0; i < CPT / 2; ++i) {
+      d[2 * i] = __uint_as_float(r[i] << 16);
+      d[2 * i + 1] = __uint_as_float(r[i] & 0xffff0000u);
+    }
   } else {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) d[i] = (c0 + i < C) ? bf2f(dyp[i]) : 0.f;
+    for (int i = 0; i < CPT; ++i) d[i] = (c0 + i < C) ? bf2f(dyp[i]) : 0.f;
   }
 }
 
-// Backward pass 1 (PASS=1): per-(b,c) sums A = sum dxh, Bv = sum dxh*xh; per-c dgamma, dbeta, dmask.
-// Backward pass 2 (PASS=2): dconv = rstd*(dxh - A/N - xh*Bv/N); dw[c][j] += sum dconv * x[s0 t + j].
-// 4 channels per thread keeps the tap weights + tap accumulators at ~80 VGPRs; the next row's dy
-// is loaded one iteration ahead.
-template <int PASS>
+// Backward in ONE pass over dy (components.py:107-114 backward: GroupNorm(C groups) + GELU + mask).
+// With g = gamma*xh + beta, dg = dy*mask*GELU'(g), dxh = dg*gamma, the GroupNorm input gradient is
+// dconv = rstd*(dxh - A/N - xh*Bv/N) (A = sum_t dxh, Bv = sum_t dxh*xh), and the conv0 weight
+// gradient dw[c][j] = sum_t dconv[t]*x_j[t] (x_j[t] = wave[s0*t+j]) is LINEAR in per-(b,c) sums:
+//   dw[c][j] = sum_b rstd*(P_j - (A/N)*S_j - (Bv/N)*Q_j),
+//   P_j = sum_t dxh*x_j (accumulated here), S_j = sum_t x_j and
+//   Q_j = sum_t xh*x_j = rstd*(sum_k w[c][k]*G[k][j] - mean*S_j) from the per-utterance Gram matrix
+//   G[k][j] = sum_t x_k*x_j of the waveform (conv0_gram_kernel).
+// So the old second pass (recompute conv0 + GELU' + dconv) disappears.  Per (b, c) the blocks add
+// their 15 partial sums (P[10], A, Bv, dgamma, dbeta, dmask) into ws with fp32 atomics (63 time
+// blocks per address), conv0_bwd_finalize combines them.  dy is prefetched 4 time steps ahead.
+constexpr int NQ = 15;
+
+template <int CPT, int PF>
 __global__ void __launch_bounds__(256) conv0_gn_bwd_kernel(const float* __restrict__ wave,
                                                            const float* __restrict__ w, Conv0 p,
                                                            const float* __restrict__ gamma,
@@ -264,22 +286,19 @@ __global__ void __launch_bounds__(256) conv0_gn_bwd_kernel(const float* __restri
                                                            const float* __restrict__ mean,
                                                            const float* __restrict__ rstd,
                                                            const bf16_t* __restrict__ dy, float* __restrict__ sums,
-                                                           float* __restrict__ dw, float* __restrict__ dgamma,
-                                                           float* __restrict__ dbeta, float* __restrict__ dmask) {
-  constexpr int CPT = 4;
+                                                           int rows) {
   __shared__ float xs[BWD_ROWS * S0 + K0];
   __shared__ float red[256 * CPT];
   const int64_t b = blockIdx.y;
-  const int64_t t0 = (int64_t)blockIdx.x * BWD_ROWS;
-  const int nt = (int)min<int64_t>(BWD_ROWS, p.L0 - t0);
+  const int64_t t0 = (int64_t)blockIdx.x * rows;
+  const int nt = (int)min<int64_t>(rows, p.L0 - t0);
   stage_wave(xs, wave, p, b, t0, nt);
   RowLayout<CPT> L(p.C);
   const int tid = threadIdx.x;
   const bool active = tid < L.tpr * L.rpp;
   const int64_t c0 = active ? (int64_t)(tid % L.tpr) * CPT : 0;
   const int r0 = active ? tid / L.tpr : 0;
-  const float invN = 1.0f / (float)p.L0;
-  float wr[CPT][K0], mu[CPT], rs[CPT], ga[CPT], be[CPT], mk[CPT], sA[CPT], sB[CPT];
+  float wr[CPT][K0], mu[CPT], rs[CPT], ga[CPT], be[CPT], mk[CPT];
   load_taps<CPT>(wr, w, c0, p.C, active);
 #pragma unroll
   for (int i = 0; i < CPT; ++i) {
@@ -290,61 +309,71 @@ __global__ void __launch_bounds__(256) conv0_gn_bwd_kernel(const float* __restri
     ga[i] = ok ? gamma[c] : 0.f;
     be[i] = ok ? beta[c] : 0.f;
     mk[i] = (ok && mask) ? mask[c] : 1.f;
-    sA[i] = sB[i] = 0.f;
-    if (PASS == 2 && ok) {
-      sA[i] = sums[(b * p.C + c) * 2 + 0] * invN;
-      sB[i] = sums[(b * p.C + c) * 2 + 1] * invN;
-    }
   }
-  float acc[CPT][K0];   // PASS1: [i][0..4] = A, Bv, dgamma, dbeta, dmask; PASS2: dw taps
+  float acc[CPT][NQ];
 #pragma unroll
   for (int i = 0; i < CPT; ++i)
 #pragma unroll
-    for (int j = 0; j < K0; ++j) acc[i][j] = 0.f;
+    for (int q = 0; q < NQ; ++q) acc[i][q] = 0.f;
   const int nper = (nt + L.rpp - 1) / L.rpp;
   const int ta = r0 * nper;
   const int tb = min(nt, ta + nper);
   if (active && ta < tb) {
     const bf16_t* dyrow = dy + ((b * p.L0) + t0) * p.C + c0;
-    float x[K0], dn[CPT];
+    float x[K0];
     win_load(x, xs, ta);
-    load_dy4(dyrow + (int64_t)ta * p.C, c0, p.C, dn);
-    for (int t = ta; t < tb; ++t) {
-      float dyv[CPT];
+    float cur[PF][CPT], nxt[PF][CPT];
 #pragma unroll
-      for (int i = 0; i < CPT; ++i) dyv[i] = dn[i];
-      if (t + 1 < tb) load_dy4(dyrow + (int64_t)(t + 1) * p.C, c0, p.C, dn);
-      float v[CPT];
-      fir<CPT>(wr, x, v);
+    for (int u = 0; u < PF; ++u) {
+      if (ta + u < tb) load_dyc<CPT>(dyrow + (int64_t)(ta + u) * p.C, c0, p.C, cur[u]);
+      else
 #pragma unroll
-      for (int i = 0; i < CPT; ++i) {
-        const float xh = (v[i] - mu[i]) * rs[i];
-        const float g = fmaf(ga[i], xh, be[i]);
-        float gl, gd;
-        gelu_and_grad(g, gl, gd);
-        const float dg = dyv[i] * mk[i] * gd;
-        const float dxh = dg * ga[i];
-        if (PASS == 1) {
-          acc[i][0] += dxh;
-          acc[i][1] = fmaf(dxh, xh, acc[i][1]);
-          acc[i][2] = fmaf(dg, xh, acc[i][2]);
-          acc[i][3] += dg;
-          acc[i][4] = fmaf(dyv[i], gl, acc[i][4]);
-        } else {
-          const float dc = rs[i] * (dxh - sA[i] - xh * sB[i]);
+        for (int i = 0; i < CPT; ++i) cur[u][i] = 0.f;
+    }
+    for (int tg = ta; tg < tb; tg += PF) {
 #pragma unroll
-          for (int j = 0; j < K0; ++j) acc[i][j] = fmaf(dc, x[j], acc[i][j]);
+      for (int u = 0; u < PF; ++u) {
+        if (tg + PF + u < tb) load_dyc<CPT>(dyrow + (int64_t)(tg + PF + u) * p.C, c0, p.C, nxt[u]);
+        else
+#pragma unroll
+          for (int i = 0; i < CPT; ++i) nxt[u][i] = 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < PF; ++u) {
+        const int t = tg + u;
+        if (t < tb) {
+          float v[CPT];
+          fir<CPT>(wr, x, v);
+#pragma unroll
+          for (int i = 0; i < CPT; ++i) {
+            const float xh = (v[i] - mu[i]) * rs[i];
+            const float g = fmaf(ga[i], xh, be[i]);
+            float gl, gd;
+            gelu_and_grad(g, gl, gd);
+            const float dg = cur[u][i] * mk[i] * gd;
+            const float dxh = dg * ga[i];
+#pragma unroll
+            for (int j = 0; j < K0; ++j) acc[i][j] = fmaf(dxh, x[j], acc[i][j]);
+            acc[i][10] += dxh;
+            acc[i][11] = fmaf(dxh, xh, acc[i][11]);
+            acc[i][12] = fmaf(dg, xh, acc[i][12]);
+            acc[i][13] += dg;
+            acc[i][14] = fmaf(cur[u][i], gl, acc[i][14]);
+          }
+          if (t + 1 < tb) win_advance(x, xs, t);
         }
       }
-      if (t + 1 < tb) win_advance(x, xs, t);
+#pragma unroll
+      for (int u = 0; u < PF; ++u)
+#pragma unroll
+        for (int i = 0; i < CPT; ++i) cur[u][i] = nxt[u][i];
     }
   }
-  // reduce over the rpp thread-rows sharing the same channels (static acc index: fully unrolled)
-  constexpr int NACC = PASS == 1 ? 5 : K0;
+  // reduce over the rpp thread-rows sharing the same channels, then one atomic per (b, c, q) per block
 #pragma unroll
-  for (int a = 0; a < NACC; ++a) {
+  for (int q = 0; q < NQ; ++q) {
 #pragma unroll
-    for (int i = 0; i < CPT; ++i) red[tid * CPT + i] = acc[i][a];
+    for (int i = 0; i < CPT; ++i) red[tid * CPT + i] = acc[i][q];
     __syncthreads();
     if (active && r0 == 0) {
 #pragma unroll
@@ -352,21 +381,92 @@ __global__ void __launch_bounds__(256) conv0_gn_bwd_kernel(const float* __restri
         float s = 0.f;
         for (int r = 0; r < L.rpp; ++r) s += red[(r * L.tpr + (tid % L.tpr)) * CPT + i];
         const int64_t c = c0 + i;
-        if (c < p.C) {
-          if (PASS == 1) {
-            if (a == 0) atomicAdd(sums + (b * p.C + c) * 2 + 0, s);
-            else if (a == 1) atomicAdd(sums + (b * p.C + c) * 2 + 1, s);
-            else if (a == 2 && dgamma) atomicAdd(dgamma + c, s);
-            else if (a == 3 && dbeta) atomicAdd(dbeta + c, s);
-            else if (a == 4 && dmask) atomicAdd(dmask + c, s);
-          } else {
-            atomicAdd(dw + c * K0 + a, s);
-          }
-        }
+        if (c < p.C) atomicAdd(sums + (b * p.C + c) * NQ + q, s);
       }
     }
     __syncthreads();
   }
+}
+
+// per utterance: S[j] = sum_t x_j[t], G[k][j] = sum_t x_k[t] x_j[t] (x_j[t] = wave[s0*t + j], t < L0),
+// fp64, packed: gram[b][0..9] = S, gram[b][10 + j*(j+1)/2 + k] = G[k][j] (k <= j).  Grid (chunks of
+// GRAM_ROWS time steps, B); blocks add their partial sums with fp64 atomics (gram zeroed first).
+constexpr int NG = K0 + K0 * (K0 + 1) / 2;   // 65
+constexpr int GRAM_ROWS = 2048;
+
+__device__ __forceinline__ int gram_idx(int k, int j) {   // symmetric
+  return k <= j ? K0 + j * (j + 1) / 2 + k : K0 + k * (k + 1) / 2 + j;
+}
+
+__global__ void __launch_bounds__(256) conv0_gram_kernel(const float* __restrict__ wave, Conv0 p,
+                                                         double* __restrict__ gram) {
+  __shared__ double red[4][NG];
+  const int64_t b = blockIdx.y;
+  const float* xw = wave + b * p.S;
+  const int64_t t1 = min<int64_t>(p.L0, (int64_t)(blockIdx.x + 1) * GRAM_ROWS);
+  double acc[NG];
+#pragma unroll
+  for (int q = 0; q < NG; ++q) acc[q] = 0.0;
+  for (int64_t t = (int64_t)blockIdx.x * GRAM_ROWS + threadIdx.x; t < t1; t += 256) {
+    float x[K0];
+#pragma unroll
+    for (int j = 0; j < K0; ++j) x[j] = xw[t * S0 + j];
+#pragma unroll
+    for (int j = 0; j < K0; ++j) {
+      acc[j] += x[j];
+#pragma unroll
+      for (int k = 0; k <= j; ++k) acc[K0 + j * (j + 1) / 2 + k] += (double)x[k] * (double)x[j];
+    }
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int q = 0; q < NG; ++q) {
+    double v = acc[q];
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (lane == 0) red[wv][q] = v;
+  }
+  __syncthreads();
+  for (int q = threadIdx.x; q < NG; q += 256)
+    atomicAdd(gram + b * NG + q, (red[0][q] + red[1][q]) + (red[2][q] + red[3][q]));
+}
+
+// one thread per channel: combine the per-(b,c) sums into dw[c][j], dgamma, dbeta, dmask (accumulate)
+__global__ void conv0_bwd_finalize(const float* __restrict__ sums, const double* __restrict__ gram,
+                                   const float* __restrict__ w, const float* __restrict__ mean,
+                                   const float* __restrict__ rstd, Conv0 p, float* __restrict__ dw,
+                                   float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ dmask) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= p.C) return;
+  const double N = (double)p.L0;
+  double wc[K0], dwc[K0];
+#pragma unroll
+  for (int j = 0; j < K0; ++j) {
+    wc[j] = w[c * K0 + j];
+    dwc[j] = 0.0;
+  }
+  double dga = 0.0, dbe = 0.0, dma = 0.0;
+  for (int64_t b = 0; b < p.B; ++b) {
+    const float* sm = sums + (b * p.C + c) * NQ;
+    const double* gb = gram + b * NG;
+    const double mu = mean[b * p.C + c], r = rstd[b * p.C + c];
+    const double A = sm[10], Bv = sm[11];
+#pragma unroll
+    for (int j = 0; j < K0; ++j) {
+      double cg = 0.0;
+#pragma unroll
+      for (int k = 0; k < K0; ++k) cg += wc[k] * gb[gram_idx(k, j)];
+      const double Q = r * (cg - mu * gb[j]);
+      dwc[j] += r * ((double)sm[j] - (A / N) * gb[j] - (Bv / N) * Q);
+    }
+    dga += sm[12];
+    dbe += sm[13];
+    dma += sm[14];
+  }
+#pragma unroll
+  for (int j = 0; j < K0; ++j) dw[c * K0 + j] += (float)dwc[j];
+  if (dgamma) dgamma[c] += (float)dga;
+  if (dbeta) dbeta[c] += (float)dbe;
+  if (dmask) dmask[c] += (float)dma;
 }
 
 // ---- weight norm -----------------------------------------------------------
@@ -494,6 +594,10 @@ extern "C" int dph_conv0_fwd(const float* wave, int64_t B, int64_t S, const floa
   return check_launch("dph_conv0_fwd");
 }
 
+extern "C" int64_t dph_conv0_gn_bwd_workspace(int64_t B, int64_t C) {
+  return cdiv(B * C * NQ * 4, 64) * 64 + B * NG * 8;
+}
+
 extern "C" int dph_conv0_gn_bwd(const float* wave, int64_t B, int64_t S, const float* w, int64_t C, int64_t k0,
                                 int64_t s0, const float* gamma, const float* beta, const float* mask,
                                 const float* mean, const float* rstd, const void* dy, float* dw, float* dgamma,
@@ -504,15 +608,36 @@ extern "C" int dph_conv0_gn_bwd(const float* wave, int64_t B, int64_t S, const f
               (long long)s0);
     return DPH_EUNSUPPORTED;
   }
-  DPH_REQUIRE(S >= K0 && C <= 2048, "dph_conv0_gn_bwd: unsupported");
-  DPH_REQUIRE(ws_bytes >= B * C * 2 * 4, "dph_conv0_gn_bwd: workspace too small");
+  DPH_REQUIRE(S >= K0 && C <= 1024, "dph_conv0_gn_bwd: unsupported (C > 1024)");   // 256 threads x 4 channels
+  DPH_REQUIRE(ws_bytes >= dph_conv0_gn_bwd_workspace(B, C), "dph_conv0_gn_bwd: workspace too small (%lld < %lld)",
+              (long long)ws_bytes, (long long)dph_conv0_gn_bwd_workspace(B, C));
   Conv0 p = make_conv0(B, S, C);
-  hipMemsetAsync(ws, 0, B * C * 2 * 4, stream);
-  dim3 grid((unsigned)cdiv(p.L0, BWD_ROWS), (unsigned)B);
-  hipLaunchKernelGGL(conv0_gn_bwd_kernel<1>, grid, dim3(256), 0, stream, wave, w, p, gamma, beta, mask, mean, rstd,
-                     reinterpret_cast<const bf16_t*>(dy), ws, dw, dgamma, dbeta, dmask);
-  hipLaunchKernelGGL(conv0_gn_bwd_kernel<2>, grid, dim3(256), 0, stream, wave, w, p, gamma, beta, mask, mean, rstd,
-                     reinterpret_cast<const bf16_t*>(dy), ws, dw, dgamma, dbeta, dmask);
+  float* sums = ws;
+  const int64_t sums_bytes = cdiv(B * C * NQ * 4, 64) * 64;
+  double* gram = reinterpret_cast<double*>(reinterpret_cast<char*>(ws) + sums_bytes);
+  hipMemsetAsync(ws, 0, sums_bytes + B * NG * 8, stream);
+  hipLaunchKernelGGL(conv0_gram_kernel, dim3((unsigned)cdiv(p.L0, GRAM_ROWS), (unsigned)B), dim3(256), 0, stream,
+                     wave, p, gram);
+  // DPH_C0B_VARIANT (tuning knob): 0 = 4 channels/thread, 4-row dy prefetch, 512 rows/block;
+  // 1 = 2 ch/thread; 2 = 4 ch, 1-row prefetch; 3 = 4 ch, 256 rows/block
+  static const int var = [] {
+    const char* e = getenv("DPH_C0B_VARIANT");
+    return e ? atoi(e) : 0;
+  }();
+  const int rows = var == 3 ? BWD_ROWS / 2 : BWD_ROWS;
+  dim3 grid((unsigned)cdiv(p.L0, rows), (unsigned)B);
+  const bf16_t* dyb = reinterpret_cast<const bf16_t*>(dy);
+  if (var == 1 && C <= 512)
+    hipLaunchKernelGGL((conv0_gn_bwd_kernel<2, 4>), grid, dim3(256), 0, stream, wave, w, p, gamma, beta, mask, mean,
+                       rstd, dyb, sums, rows);
+  else if (var == 2)
+    hipLaunchKernelGGL((conv0_gn_bwd_kernel<4, 1>), grid, dim3(256), 0, stream, wave, w, p, gamma, beta, mask, mean,
+                       rstd, dyb, sums, rows);
+  else
+    hipLaunchKernelGGL((conv0_gn_bwd_kernel<4, 4>), grid, dim3(256), 0, stream, wave, w, p, gamma, beta, mask, mean,
+                       rstd, dyb, sums, rows);
+  hipLaunchKernelGGL(conv0_bwd_finalize, dim3((unsigned)cdiv(C, 64)), dim3(64), 0, stream, sums, gram, w, mean, rstd,
+                     p, dw, dgamma, dbeta, dmask);
   return check_launch("dph_conv0_gn_bwd");
 }
 

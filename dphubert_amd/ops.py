@@ -537,7 +537,7 @@ class FrontendFn(torch.autograd.Function):
             dw0, dgw, dgb = zeros_f32((C0p,) + tuple(ws_[0].shape[1:]), dev), zeros_f32(C0p, dev), zeros_f32(C0p, dev)
             go.bufs[id(pws[0])], go.bufs[id(pgn_w)], go.bufs[id(pgn_b)] = dw0[:C0], dgw[:C0], dgb[:C0]
         dm0 = zeros_f32(C0p, dev) if masks[0] is not None else None
-        wsb = torch.empty(B * C0p * 2, dtype=F32, device=dev)
+        wsb = torch.empty((_lib.lib().dph_conv0_gn_bwd_workspace(B, C0p) + 3) // 4, dtype=F32, device=dev)
         call("dph_conv0_gn_bwd", ptr(wave), B, S, ptr(w0), C0p, k0, s0, ptr(g0), ptr(b0), ptr(m0),
              ptr(mean), ptr(rstd), ptr(dz), ptr(dw0), ptr(dgw), ptr(dgb), ptr(dm0), ptr(wsb), wsb.numel() * 4, _s())
         g_m[0] = dm0[:C0] if dm0 is not None else None

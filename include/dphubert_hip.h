@@ -168,6 +168,8 @@ int dph_attention_bwd(const void* qkv, const void* do_masked, const float* head_
 int dph_conv0_gn_fwd(const float* wave, int64_t B, int64_t S, const float* w, int64_t C, int64_t k0, int64_t s0,
                      const float* gamma, const float* beta, const float* mask, void* y, float* mean, float* rstd,
                      float* ws, int64_t ws_bytes, hipStream_t stream);
+/* backward scratch: per-(b,c) partial sums (fp32) + per-utterance waveform Gram matrix (fp64) */
+int64_t dph_conv0_gn_bwd_workspace(int64_t B, int64_t C);
 int dph_conv0_gn_bwd(const float* wave, int64_t B, int64_t S, const float* w, int64_t C, int64_t k0, int64_t s0,
                      const float* gamma, const float* beta, const float* mask, const float* mean, const float* rstd,
                      const void* dy, float* dw, float* dgamma, float* dbeta, float* dmask, float* ws,

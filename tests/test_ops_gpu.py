@@ -323,3 +323,53 @@ def test_wave_layernorm_vs_reference_semantics(lengths):
                                                batch_first=True)
     assert got.shape == want.shape
     assert torch.allclose(got, want, atol=2e-5, rtol=1e-5)
+
+
+def _conv0_gn(wave, w, C, gamma, beta, mask, dy=None):
+    """conv0 + GroupNorm(C, C) + GELU + mask through the C ABI (forward, optional backward)."""
+    from dphubert_amd import _lib
+    from dphubert_amd._lib import call, ptr
+    B, S = wave.shape
+    L0 = (S - 10) // 5 + 1
+    y = torch.empty(B * L0, C, dtype=torch.bfloat16, device=DEV)
+    mean = torch.empty(B, C, device=DEV)
+    rstd = torch.empty(B, C, device=DEV)
+    ws = torch.empty(B * (-(-L0 // 256)) * C * 2, device=DEV)
+    st = _lib.stream_ptr()
+    call("dph_conv0_gn_fwd", ptr(wave), B, S, ptr(w), C, 10, 5, ptr(gamma), ptr(beta), ptr(mask), ptr(y),
+         ptr(mean), ptr(rstd), ptr(ws), ws.numel() * 4, st)
+    if dy is None:
+        return y
+    dw = torch.zeros(C, 10, device=DEV)
+    dg, db, dm = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+    wsb = torch.empty((_lib.lib().dph_conv0_gn_bwd_workspace(B, C) + 3) // 4, device=DEV)
+    call("dph_conv0_gn_bwd", ptr(wave), B, S, ptr(w), C, 10, 5, ptr(gamma), ptr(beta), ptr(mask), ptr(mean),
+         ptr(rstd), ptr(dy), ptr(dw), ptr(dg), ptr(db), ptr(dm), ptr(wsb), wsb.numel() * 4, st)
+    torch.cuda.synchronize()
+    return y, dw, dg, db, dm
+
+
+@pytest.mark.parametrize("B,S,C", [(3, 16000, 512), (2, 5003, 200), (1, 47, 36)])
+def test_conv0_gn_bwd_fp32_reference(B, S, C):
+    """Single-pass conv0/GroupNorm backward (per-(b,c) sums + waveform Gram matrix) against fp32 torch
+    autograd of conv1d -> group_norm -> gelu -> *mask (components.py:81-87,107-114); the kernel's only
+    bf16 input is dy, fed identically to both.  Tolerance 2e-3 rel-L2 (fp32 atomics over ~10^4 terms)."""
+    g = torch.Generator().manual_seed(B * 1000 + C)
+    wave = 0.1 * torch.randn(B, S, generator=g)
+    wave[:, : S // 3] += 0.05      # DC offset: exercises the mean-subtraction terms of the Gram form
+    w = torch.randn(C, 10, generator=g) * 0.3
+    gamma = 1 + 0.2 * torch.randn(C, generator=g)
+    beta = 0.1 * torch.randn(C, generator=g)
+    mask = torch.rand(C, generator=g)
+    L0 = (S - 10) // 5 + 1
+    dy = torch.randn(B, L0, C, generator=g).to(torch.bfloat16)
+    _, dw, dg, db, dm = _conv0_gn(wave.to(DEV), w.to(DEV), C, gamma.to(DEV), beta.to(DEV), mask.to(DEV),
+                                  dy.to(DEV))
+    pr = {k: v.clone().double().requires_grad_(True) for k, v in dict(w=w, gamma=gamma, beta=beta, mask=mask).items()}
+    z = F.conv1d(wave.double()[:, None], pr["w"][:, None, :], stride=5)
+    z = F.group_norm(z, C, pr["gamma"], pr["beta"], eps=1e-5)
+    y = F.gelu(z) * pr["mask"][None, :, None]
+    y.backward(dy.double().transpose(1, 2))
+    for name, got in (("w", dw), ("gamma", dg), ("beta", db), ("mask", dm)):
+        e = rel_l2(got.cpu().double(), pr[name].grad)
+        assert e < 2e-3, (name, e)
