@@ -730,7 +730,7 @@ struct Cfg {
   static constexpr int DMA_A = BM * 64 / (NT * 16);          // DMA instructions per thread per slice
   static constexpr int DMA_B = BN * 64 / (NT * 16);
   static constexpr int DMA = DMA_A + DMA_B;                   // per thread per slice
-  static_assert(DMA == 4 || DMA == 8, "vmcnt immediates exist for 4 or 8 DMA per thread per slice");
+  static_assert(DMA == 4 || DMA == 5 || DMA == 8, "vmcnt immediates exist for 4, 5 or 8 DMA per thread per slice");
   static constexpr int EROWS = BM > 128 ? 128 : BM;          // epilogue staging rows per pass
   static constexpr int CROW = BN + 4;
   static constexpr int EPI = EROWS * CROW * 4;
@@ -739,12 +739,18 @@ struct Cfg {
 };
 using Big = Cfg<256, 256, 128, 64>;
 using Mid = Cfg<128, 128, 64, 64>;
+// narrow-N shapes (the grouped positional conv: N = 48 output channels per group, M = T, K = 6144):
+// 256 x 64 tile, 4 waves of 128 x 32, two blocks per CU (2 x 80 KB LDS)
+using Tall = Cfg<256, 64, 128, 32>;
 
 // s_waitcnt vmcnt(n * DMA): at most n slices' DMAs still in flight
 template <int DMA, int n>
 __device__ __forceinline__ void wait_slices() {
   if constexpr (DMA * n == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   else if constexpr (DMA * n == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (DMA * n == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+  else if constexpr (DMA * n == 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+  else if constexpr (DMA * n == 15) asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
   else if constexpr (DMA * n == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
   else if constexpr (DMA * n == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
   else if constexpr (DMA * n == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
@@ -1042,9 +1048,9 @@ __global__ void __launch_bounds__(C::NT, C::MINB) ring_gemm_kernel(const DphGemm
       }
       continue;
     }
-    // (the Big tile keeps the per-row epilogue: the prefetching one pushes its main loop into
+    // (the 8-wave Big tile keeps the per-row epilogue: the prefetching one pushes its main loop into
     // scratch spills at the 256-VGPR cap)
-    if constexpr (C::BM <= 128) {
+    if constexpr (C::NW < 8) {
       if (tile_epi_ok(a, n0 + c8)) {
         tile_epi<C::EROWS / RPP, RPP, JP, C::WTM - SEG>(a, z, m0 + trow(h, r0), n0 + c8, ct + r0 * C::CROW + c8,
                                                         C::CROW, cso, csa);
@@ -1154,7 +1160,7 @@ using namespace dph;
 static int gemm_path_override() {
   const char* e = getenv("DPH_GEMM_PATH");
   if (!e) return 0;
-  return !strcmp(e, "small") ? 1 : !strcmp(e, "big") ? 2 : !strcmp(e, "mid") ? 3 : 0;
+  return !strcmp(e, "small") ? 1 : !strcmp(e, "big") ? 2 : !strcmp(e, "mid") ? 3 : !strcmp(e, "tall") ? 4 : 0;
 }
 
 // an operand the ring kernels can stage: k-contiguous with whole 32-deep k-slices, or mn-contiguous
@@ -1182,10 +1188,13 @@ static int gemm_kind(const DphGemmArgs& a, int64_t kchunk) {
   const bool big_ok = ring_ok && a.a_kcontig && a.b_kcontig;
   const int64_t tiles256 = cdiv(a.M, ring::Big::BM) * cdiv(a.N, ring::Big::BN) * a.batch * a.splits;
   int kind = !ring_ok ? 0 : ((big_ok && tiles256 >= 480) ? 2 : 1);
+  // N <= 64 (<= 1/4 of a 256 tile, 1/2 of a 128 tile): the 256 x 64 tile
+  if (big_ok && a.N <= ring::Tall::BN && a.M > 128) kind = 3;
   const int path = gemm_path_override();
   if (path == 1) kind = 0;
   if (path == 2 && big_ok) kind = 2;
   if (path == 3 && ring_ok) kind = 1;
+  if (path == 4 && big_ok) kind = 3;
   return kind;
 }
 
@@ -1197,6 +1206,7 @@ extern "C" const char* dph_gemm_variant(const DphGemmArgs* args) {
   if (!args) return "";
   const DphGemmArgs& a = *args;
   const int kind = gemm_kind(a, gemm_kchunk(a));
+  if (kind == 3) return "ring::Cfg<256, 64, 128, 32>, true, true>";
   if (kind == 2) return "ring::Cfg<256, 256, 128, 64>, true, true>";
   if (kind == 1) {
     if (a.a_kcontig && a.b_kcontig) return "ring::Cfg<128, 128, 64, 64>, true, true>";
@@ -1252,7 +1262,10 @@ extern "C" int dph_gemm(const DphGemmArgs* args, hipStream_t stream) {
   // when there are >= ~2 full rounds of tiles over the 256 CUs at one block per CU, else the
   // 128x128 tile (DPH_GEMM_PATH=small|big|mid forces a path, for tests)
   const int kind = gemm_kind(a, kchunk);
-  if (kind == 2) {
+  if (kind == 3) {
+    DPH_REQUIRE(cdiv(a.M, ring::Tall::BM) < 65536 && a.batch * a.splits < 65536, "dph_gemm: grid too large");
+    launch_ring<ring::Tall, false>(a, kchunk, stream);
+  } else if (kind == 2) {
     DPH_REQUIRE(cdiv(a.M, ring::Big::BM) < 65536 && a.batch * a.splits < 65536, "dph_gemm: grid too large");
     launch_ring<ring::Big, false>(a, kchunk, stream);
   } else if (kind == 1) {

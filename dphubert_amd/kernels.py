@@ -76,8 +76,9 @@ class LaunchProfiler:
 
     active = None
 
-    def __init__(self):
+    def __init__(self, by_shape: bool = False):
         self.records = []
+        self.by_shape = by_shape   # key the summary by (kernel, M, N, K, batch, splits) -- diagnostics
 
     def __enter__(self):
         LaunchProfiler.active = self
@@ -124,7 +125,10 @@ def gemm(A: DphMat, B: DphMat, Cm: DphMat, M: int, N: int, K: int, *, a_kcontig:
     call("dph_gemm", C.byref(args), _stream())
     if prof is not None:
         e1.record()
-        prof.records.append((_variant(args), 2.0 * M * N * K * batch, e0, e1))
+        name = _variant(args)
+        if prof.by_shape:
+            name = f"{name} M={M} N={N} K={K} b={batch} s={splits} {int(a_kcontig)}{int(b_kcontig)}"
+        prof.records.append((name, 2.0 * M * N * K * batch, e0, e1))
     return ws  # keep alive until the stream consumes it (caching allocator is stream-ordered)
 
 

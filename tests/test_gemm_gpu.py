@@ -9,11 +9,11 @@ pytestmark = pytest.mark.gpu
 torch.manual_seed(0)
 
 
-@pytest.fixture(autouse=True, params=["small", "mid", "big", "wide"])
+@pytest.fixture(autouse=True, params=["small", "mid", "big", "wide", "tall"])
 def gemm_path(request, monkeypatch):
     """Run every test on each GEMM path: the 128x128 register-staged kernel and the 128x128 /
-    256x256 LDS-DMA ring kernels (taken where their constraints hold: both operands k-contiguous,
-    K % 32 == 0)."""
+    256x256 / 256x64 LDS-DMA ring kernels (taken where their constraints hold: both operands
+    k-contiguous, K % 32 == 0)."""
     monkeypatch.setenv("DPH_GEMM_PATH", request.param)
     return request.param
 
@@ -36,7 +36,8 @@ def close(a, b, tol=2e-2):
 
 @pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, True), (False, False)])
 @pytest.mark.parametrize("M,N,K", [(304, 200, 136), (128, 128, 64), (1000, 264, 520), (1000, 264, 512),
-                                   (2056, 520, 768), (256, 256, 64), (7984, 768, 192)])
+                                   (2056, 520, 768), (256, 256, 64), (7984, 768, 192),
+                                   (504, 48, 1536)])
 def test_layouts(ak, bk, M, N, K):
     K_ = _k()
     A = rnd(M, K) if ak else rnd(K, M)
