@@ -259,6 +259,52 @@ extern "C" int dph_regroup_pad(const void* x, void* xg, int64_t B, int64_t T, in
   return check_launch("dph_regroup_pad");
 }
 
+namespace dph {
+namespace {
+// bf16 [R][C] -> [C][R] through a 64x64 LDS tile (16-B loads and stores; R, C multiples of 8).
+// Makes the k-contiguous image W^T of a weight for the input-gradient GEMM dx = dy @ W, so that
+// GEMM stages both operands with the LDS-DMA ring instead of hardware-transposed LDS reads.
+__global__ void __launch_bounds__(256) transpose_bf16_kernel(const bf16_t* __restrict__ src, int64_t R, int64_t C,
+                                                             bf16_t* __restrict__ dst) {
+  __shared__ uint16_t t[64][72];
+  const int64_t r0 = (int64_t)blockIdx.y * 64, c0 = (int64_t)blockIdx.x * 64;
+  const int tid = threadIdx.x;
+  const int c8 = (tid & 7) * 8;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int r = (tid >> 3) + 32 * h;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (r0 + r < R && c0 + c8 < C) v = *reinterpret_cast<const uint4*>(src + (r0 + r) * C + c0 + c8);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      t[r][c8 + 2 * q] = (uint16_t)(w[q] & 0xffffu);
+      t[r][c8 + 2 * q + 1] = (uint16_t)(w[q] >> 16);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int c = (tid >> 3) + 32 * h;      // output row (source column)
+    if (c0 + c >= C || r0 + c8 >= R) continue;
+    uint32_t w[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) w[q] = (uint32_t)t[c8 + 2 * q][c] | ((uint32_t)t[c8 + 2 * q + 1][c] << 16);
+    *reinterpret_cast<uint4*>(dst + (c0 + c) * R + r0 + c8) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+}  // namespace
+}  // namespace dph
+
+extern "C" int dph_transpose_bf16(const void* src, int64_t R, int64_t C, void* dst, hipStream_t stream) {
+  DPH_REQUIRE(src && dst && R > 0 && C > 0 && R % 8 == 0 && C % 8 == 0,
+              "dph_transpose_bf16: bad args (R=%lld C=%lld must be multiples of 8)", (long long)R, (long long)C);
+  DPH_REQUIRE(cdiv(R, 64) < 65536, "dph_transpose_bf16: too many rows");
+  hipLaunchKernelGGL(dph::transpose_bf16_kernel, dim3((unsigned)cdiv(C, 64), (unsigned)cdiv(R, 64)), dim3(256), 0,
+                     stream, reinterpret_cast<const bf16_t*>(src), R, C, reinterpret_cast<bf16_t*>(dst));
+  return check_launch("dph_transpose_bf16");
+}
+
 extern "C" int dph_cast_bf16(const float* src, void* dst, int64_t n, hipStream_t stream) {
   DPH_REQUIRE(src && dst && n > 0, "dph_cast_bf16: bad args");
   hipLaunchKernelGGL(cast_bf16_kernel, dim3((unsigned)cdiv(cdiv(n, 4), 256)), dim3(256), 0, stream, src,

@@ -724,29 +724,35 @@ struct Cfg {
   static constexpr int NW = WGM * WGN;
   static constexpr int NT = 64 * NW;
   static constexpr int FM = WTM / 16, FN = WTN / 16;       // accumulator tiles per wave
+  static_assert(FM >= FN, "the ring step deals fragment reads over FM chunks");
   static constexpr int HALF_A = BM * KS * 2, HALF_B = BN * KS * 2;
   static constexpr int SLOT = HALF_A + HALF_B;
   static constexpr int PIPE = NSLOT * SLOT;
   static constexpr int DMA_A = BM * 64 / (NT * 16);          // DMA instructions per thread per slice
   static constexpr int DMA_B = BN * 64 / (NT * 16);
   static constexpr int DMA = DMA_A + DMA_B;                   // per thread per slice
-  static_assert(DMA == 4 || DMA == 5 || DMA == 8, "vmcnt immediates exist for 4, 5 or 8 DMA per thread per slice");
+  static_assert(DMA == 3 || DMA == 4 || DMA == 5 || DMA == 8, "vmcnt immediates exist for 3, 4, 5 or 8 DMA per thread per slice");
   static constexpr int EROWS = BM > 128 ? 128 : BM;          // epilogue staging rows per pass
   static constexpr int CROW = BN + 4;
   static constexpr int EPI = EROWS * CROW * 4;
   static constexpr int LDS = PIPE > EPI ? PIPE : EPI;
-  static constexpr int MINB = NW >= 8 ? 1 : 2;               // blocks per CU
+  static constexpr int MINB = NW >= 8 ? 1 : (BM * BN <= 128 * 64 ? 3 : 2);   // blocks per CU
 };
 using Big = Cfg<256, 256, 128, 64>;
 using Mid = Cfg<128, 128, 64, 64>;
 // narrow-N shapes (the grouped positional conv: N = 48 output channels per group, M = T, K = 6144):
 // 256 x 64 tile, 4 waves of 128 x 32, two blocks per CU (2 x 80 KB LDS)
 using Tall = Cfg<256, 64, 128, 32>;
+// N = 768 shapes with few 128x128 tiles (< 2 per CU): 128 x 64 tile, 4 waves of 64 x 32, 48 KB LDS
+using Half = Cfg<128, 64, 64, 32>;
 
 // s_waitcnt vmcnt(n * DMA): at most n slices' DMAs still in flight
 template <int DMA, int n>
 __device__ __forceinline__ void wait_slices() {
   if constexpr (DMA * n == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (DMA * n == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+  else if constexpr (DMA * n == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if constexpr (DMA * n == 9) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
   else if constexpr (DMA * n == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   else if constexpr (DMA * n == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
   else if constexpr (DMA * n == 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
@@ -828,6 +834,16 @@ __device__ __forceinline__ void mfma_slice(f32x4_t (&acc)[C::FM][C::FN], const F
 template <class C, bool AK, bool BK>
 __global__ void __launch_bounds__(C::NT, C::MINB) ring_gemm_kernel(const DphGemmArgs a, int64_t kchunk) {
   __shared__ __attribute__((aligned(1024))) char smem[C::LDS];
+#ifdef DPH_STAGGER
+  // timing experiment: the second block of each CU in the first dispatch round (linear ids 256..511,
+  // placed breadth-first) starts late, so co-resident blocks run out of phase
+  if (C::MINB >= 2) {
+    const int64_t nb = (int64_t)gridDim.x * gridDim.y * gridDim.z;
+    const int64_t lb = ((int64_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    if (nb >= 768 && lb >= 256 && lb < 512)
+      for (int r = 0; r < DPH_STAGGER; ++r) __builtin_amdgcn_s_sleep(127);
+  }
+#endif
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
@@ -888,16 +904,21 @@ __global__ void __launch_bounds__(C::NT, C::MINB) ring_gemm_kernel(const DphGemm
     }
     return o;
   };
-  auto issue = [&](int i) {   // k-slice i -> slot i % 4 (called for i = 0, 1, 2, ... in order)
+  // DMA j of k-slice i -> slot i % 4 (j < DMA_A: operand A, else B); slices are issued in order
+  auto issue_one = [&](int i, int j) {
     char* la = smem + (i & (ring::NSLOT - 1)) * C::SLOT;
-    char* lb = la + C::HALF_A;
     const int64_t ko = (int64_t)i * ring::KS;
-#pragma unroll
-    for (int j = 0; j < C::DMA_A; ++j)
+    if (j < C::DMA_A) {
       ring::dma16(Ab + (AK ? da.off[j] + ko : src_mn(da, a.A, a_tail, j)), la + (j * C::NW + wave) * 1024);
+    } else {
+      const int jb = j - C::DMA_A;
+      ring::dma16(Bb + (BK ? db.off[jb] + ko : src_mn(db, a.B, b_tail, jb)),
+                  la + C::HALF_A + (jb * C::NW + wave) * 1024);
+    }
+  };
+  auto issue = [&](int i) {
 #pragma unroll
-    for (int j = 0; j < C::DMA_B; ++j)
-      ring::dma16(Bb + (BK ? db.off[j] + ko : src_mn(db, a.B, b_tail, j)), lb + (j * C::NW + wave) * 1024);
+    for (int j = 0; j < C::DMA; ++j) issue_one(i, j);
   };
   // both operands mn-contiguous and K not a multiple of KS: zero the A operand's k-rows past kend in
   // the last slice (its B rows repeat row kend-1: finite, multiplied by 0).  Runs after the slice's
@@ -922,7 +943,11 @@ __global__ void __launch_bounds__(C::NT, C::MINB) ring_gemm_kernel(const DphGemm
     for (int j = 0; j < C::FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   // one pipeline step: slice i is in registers (cur); wait for slice i+1, restage slot i%4 with
-  // slice i+4, read slice i+1 into nxt while multiplying cur
+  // slice i+4, read slice i+1 into nxt while multiplying cur.  The step is cut into FM chunks
+  // (one accumulator row of MFMAs each) and the DMAs and fragment reads are dealt over them: an
+  // LDS-DMA costs its wave ~60-180 issue cycles, which hide behind the MFMAs of the chunk instead
+  // of stalling the wave in front of them (measured: the loop spent ~3x its MFMA time per slice
+  // with the DMAs issued as one block after the barrier).
   auto step = [&](int i, ring::Frags<C>& cur, ring::Frags<C>& nxt) {
     if (i + 3 < H) {
       ring::wait_slices<C::DMA, 2>();
@@ -934,19 +959,34 @@ __global__ void __launch_bounds__(C::NT, C::MINB) ring_gemm_kernel(const DphGemm
     __builtin_amdgcn_sched_barrier(0);
     if (DPH_ABLATE != 3) __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if (i + 4 < H && DPH_ABLATE != 1) issue(i + 4);
+    const bool restage = i + 4 < H && DPH_ABLATE != 1;
+    const bool rd = i + 1 < H && DPH_ABLATE != 4;
     if (has_tail && i + 2 == H) zero_tail(i + 1);
-    if (i + 1 < H && DPH_ABLATE != 4) ring::read_frags<C, AK, BK>(nxt, slot(i + 1), wr, wc, lane);
-    __builtin_amdgcn_sched_barrier(0);
-    if (DPH_ABLATE != 2) {
-      ring::mfma_slice<C>(acc, cur);
-    } else {
+    const char* sn = slot(i + 1);
 #pragma unroll
-      for (int q = 0; q < C::FM; ++q) asm volatile("" ::"v"(cur.a[q]));
+    for (int q = 0; q < C::FM; ++q) {
+#pragma unroll
+      for (int j = q; j < C::DMA; j += C::FM)
+        if (restage) issue_one(i + 4, j);
+      if (rd) {
+        if (q < C::FN)
+          nxt.b[q] = BK ? ring::frag(sn + C::HALF_A, wc * C::WTN + 16 * q, lane)
+                        : ring::frag_mn(sn + C::HALF_A, wc * C::WTN + 16 * q, lane, C::BN * 2);
+        nxt.a[q] = AK ? ring::frag(sn, wr * C::WTM + 16 * q, lane) : ring::frag_mn(sn, wr * C::WTM + 16 * q, lane, C::BM * 2);
+      }
+      if (DPH_ABLATE != 2) {
+#pragma unroll
+        for (int jj = 0; jj < C::FN; ++jj)
+          acc[q][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur.b[jj], cur.a[q], acc[q][jj], 0, 0, 0);
+      } else {
+        asm volatile("" ::"v"(cur.a[q]));
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (DPH_ABLATE == 2) {
 #pragma unroll
       for (int q = 0; q < C::FN; ++q) asm volatile("" ::"v"(cur.b[q]));
     }
-    __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): nxt landed (and slot i+1 reads retired)
     __builtin_amdgcn_sched_barrier(0);
   };
@@ -1160,7 +1200,7 @@ using namespace dph;
 static int gemm_path_override() {
   const char* e = getenv("DPH_GEMM_PATH");
   if (!e) return 0;
-  return !strcmp(e, "small") ? 1 : !strcmp(e, "big") ? 2 : !strcmp(e, "mid") ? 3 : !strcmp(e, "tall") ? 4 : 0;
+  return !strcmp(e, "small") ? 1 : !strcmp(e, "big") ? 2 : !strcmp(e, "mid") ? 3 : !strcmp(e, "tall") ? 4 : !strcmp(e, "half") ? 5 : 0;
 }
 
 // an operand the ring kernels can stage: k-contiguous with whole 32-deep k-slices, or mn-contiguous
@@ -1195,6 +1235,7 @@ static int gemm_kind(const DphGemmArgs& a, int64_t kchunk) {
   if (path == 2 && big_ok) kind = 2;
   if (path == 3 && ring_ok) kind = 1;
   if (path == 4 && big_ok) kind = 3;
+  if (path == 5 && big_ok) kind = 4;
   return kind;
 }
 
@@ -1206,6 +1247,7 @@ extern "C" const char* dph_gemm_variant(const DphGemmArgs* args) {
   if (!args) return "";
   const DphGemmArgs& a = *args;
   const int kind = gemm_kind(a, gemm_kchunk(a));
+  if (kind == 4) return "ring::Cfg<128, 64, 64, 32>, true, true>";
   if (kind == 3) return "ring::Cfg<256, 64, 128, 32>, true, true>";
   if (kind == 2) return "ring::Cfg<256, 256, 128, 64>, true, true>";
   if (kind == 1) {
@@ -1262,7 +1304,10 @@ extern "C" int dph_gemm(const DphGemmArgs* args, hipStream_t stream) {
   // when there are >= ~2 full rounds of tiles over the 256 CUs at one block per CU, else the
   // 128x128 tile (DPH_GEMM_PATH=small|big|mid forces a path, for tests)
   const int kind = gemm_kind(a, kchunk);
-  if (kind == 3) {
+  if (kind == 4) {
+    DPH_REQUIRE(cdiv(a.M, ring::Half::BM) < 65536 && a.batch * a.splits < 65536, "dph_gemm: grid too large");
+    launch_ring<ring::Half, false>(a, kchunk, stream);
+  } else if (kind == 3) {
     DPH_REQUIRE(cdiv(a.M, ring::Tall::BM) < 65536 && a.batch * a.splits < 65536, "dph_gemm: grid too large");
     launch_ring<ring::Tall, false>(a, kchunk, stream);
   } else if (kind == 2) {

@@ -159,13 +159,22 @@ def linear_fwd(x: torch.Tensor, w_bf16: torch.Tensor, bias: Optional[torch.Tenso
 
 
 def linear_dgrad(dy: torch.Tensor, w_bf16: torch.Tensor, *, out=None, residual=None, act=ACT_NONE, aux_in=None,
-                 colmask=None, colsum_out=None, colsum_aux=None, dropout_p=0.0, seed=0, colsum_n=0):
-    """dx = epi(dy @ w); dy [M,N] bf16, w [N,K] bf16 -> [M,K] bf16."""
+                 colmask=None, colsum_out=None, colsum_aux=None, dropout_p=0.0, seed=0, colsum_n=0, w_t=None):
+    """dx = epi(dy @ w); dy [M,N] bf16, w [N,K] bf16 -> [M,K] bf16.
+
+    ``w_t``: the [K,N] transposed image of w (ops.t_image): both GEMM operands are then
+    k-contiguous and the LDS-DMA ring kernels take the GEMM."""
     M, N = dy.shape
     K = w_bf16.shape[1]
     if out is None:
         out = torch.empty(M, K, dtype=BF16, device=dy.device)
-    gemm(dense(dy), dense(w_bf16), dense(out), M, K, N, a_kcontig=True, b_kcontig=False, residual=residual, act=act,
+    if w_t is not None:
+        if tuple(w_t.shape) != (K, N):
+            raise ValueError(f"w_t must be [{K},{N}], got {tuple(w_t.shape)}")
+        B, bk = dense(w_t), True
+    else:
+        B, bk = dense(w_bf16), False
+    gemm(dense(dy), B, dense(out), M, K, N, a_kcontig=True, b_kcontig=bk, residual=residual, act=act,
          aux_in=aux_in, colmask=colmask, colsum_out=colsum_out, colsum_aux=colsum_aux, dropout_p=dropout_p,
          seed=seed, colsum_n=colsum_n)
     return out

@@ -20,6 +20,7 @@ Reference semantics followed (file:line of seas2nada/DPHuBERT):
 """
 
 import math
+import os
 from typing import List, Optional, Sequence
 
 import torch
@@ -162,6 +163,26 @@ def padded_image(w: torch.Tensor, rows_p: int, cols_p: int) -> torch.Tensor:
     out = torch.zeros(rows_p, cols_p, dtype=BF16, device=w.device)
     out[:w.shape[0], :w.shape[1]] = w.detach().to(BF16)
     w._dph_img = (key, out)
+    return out
+
+
+# input-gradient GEMMs take the transposed weight image (k-contiguous B: ring kernels); DPH_DGRAD_T=0
+# keeps the mn-contiguous B operand (register-staged kernel) for A/B timing
+_DGRAD_T = os.environ.get("DPH_DGRAD_T", "1") != "0"
+
+
+def t_image(img: torch.Tensor) -> Optional[torch.Tensor]:
+    """[C][R] transpose of a bf16 weight image [R][C], cached on the image tensor (an image is
+    rebuilt whenever its fp32 master changes, so the transpose follows it); None when disabled or
+    the widths are not multiples of 8."""
+    if not _DGRAD_T or img.dim() != 2 or img.shape[0] % 8 or img.shape[1] % 8:
+        return None
+    hit = getattr(img, "_dph_t", None)
+    if hit is not None:
+        return hit
+    out = torch.empty(img.shape[1], img.shape[0], dtype=BF16, device=img.device)
+    call("dph_transpose_bf16", ptr(img), img.shape[0], img.shape[1], ptr(out), _s())
+    img._dph_t = out
     return out
 
 
@@ -592,7 +613,7 @@ class FeatureProjectionFn(torch.autograd.Function):
              cfg["T"] if lens is not None else 0, ptr(db), None, None, _s())
         dw, direct = go.buf(p_w, zero=False)
         ws = K.linear_wgrad(dpre, xn, dw, accumulate=direct, k_in=C)
-        dxn = K.linear_dgrad(dpre, img)
+        dxn = K.linear_dgrad(dpre, img, w_t=t_image(img))
         dx = torch.empty_like(x)
         dlw, _ = go.buf(p_lw)
         dlb, _ = go.buf(p_lb)
@@ -911,12 +932,12 @@ class EncoderLayerFn(torch.autograd.Function):
             k1 = K.linear_wgrad(dy, sv["f"], dw2, accumulate=direct, k_in=F_)
             db1, _ = go.buf(pr["b1"])
             g["im"] = z(F_) if has_im else None
-            du = K.linear_dgrad(dy, sv["W2"], act=K.ACT_GELU_BWD, aux_in=sv["u"], colmask=sv["imp"], colsum_out=db1,
+            du = K.linear_dgrad(dy, sv["W2"], w_t=t_image(sv["W2"]), act=K.ACT_GELU_BWD, aux_in=sv["u"], colmask=sv["imp"], colsum_out=db1,
                                 colsum_aux=g["im"] if has_im else z(F_), dropout_p=cfg["p_interm"],
                                 seed=sv["seed_i"], colsum_n=F_)
             dw1, direct = go.buf(pr["w1"], zero=False)
             k2 = K.linear_wgrad(du, xn2, dw1, accumulate=direct, n_out=F_)
-            dxn2 = K.linear_dgrad(du, sv["W1"])
+            dxn2 = K.linear_dgrad(du, sv["W1"], w_t=t_image(sv["W1"]))
             ds1 = torch.empty_like(dout)
             dln2w, _ = go.buf(pr["ln2_w"])
             dln2b, _ = go.buf(pr["ln2_b"])
@@ -935,7 +956,7 @@ class EncoderLayerFn(torch.autograd.Function):
                  ptr(sv["a_pre"]) if has_lma else None, ptr(g["lma"]), _s())
             dwo, direct = go.buf(pr["wo"], zero=False)
             k3 = K.linear_wgrad(da, sv["o_m"], dwo, accumulate=direct)
-            do_m = K.linear_dgrad(da, sv["Wo"])
+            do_m = K.linear_dgrad(da, sv["Wo"], w_t=t_image(sv["Wo"]))
             Dvec = torch.empty(B * H * T, dtype=F32, device=dev)
             g["hm"] = z(H) if has_hm else None
             call("dph_attention_bwd_prep", ptr(do_m), ptr(sv["o_u"]), ptr(hm), ptr(Dvec), ptr(g["hm"]), B, T, H, _s())
@@ -946,7 +967,7 @@ class EncoderLayerFn(torch.autograd.Function):
             call("dph_colsum", ptr(dqkv), ptr(dbqkv), M, dqkv.shape[1], *colsum_ws(M, dqkv.shape[1], dev), _s())
             dwqkv, direct = go.buf(pr["wq"], pr["wk"], pr["wv"], zero=False)
             k4 = K.linear_wgrad(dqkv, xn1, dwqkv, accumulate=direct)
-            dxn1 = K.linear_dgrad(dqkv, sv["Wqkv"])
+            dxn1 = K.linear_dgrad(dqkv, sv["Wqkv"], w_t=t_image(sv["Wqkv"]))
             dh = torch.empty_like(dout)
             dln1w, _ = go.buf(pr["ln1_w"])
             dln1b, _ = go.buf(pr["ln1_b"])
@@ -994,12 +1015,12 @@ class EncoderLayerFn(torch.autograd.Function):
             k1 = K.linear_wgrad(dy, sv["f"], dw2, accumulate=direct, k_in=F_)
             db1, _ = go.buf(pr["b1"])
             g["im"] = z(F_) if has_im else None
-            du = K.linear_dgrad(dy, sv["W2"], act=K.ACT_GELU_BWD, aux_in=sv["u"], colmask=sv["imp"], colsum_out=db1,
+            du = K.linear_dgrad(dy, sv["W2"], w_t=t_image(sv["W2"]), act=K.ACT_GELU_BWD, aux_in=sv["u"], colmask=sv["imp"], colsum_out=db1,
                                 colsum_aux=g["im"] if has_im else z(F_), dropout_p=cfg["p_interm"],
                                 seed=sv["seed_i"], colsum_n=F_)
             dw1, direct = go.buf(pr["w1"], zero=False)
             k2 = K.linear_wgrad(du, h1, dw1, accumulate=direct, n_out=F_)
-            dh1 = K.linear_dgrad(du, sv["W1"], residual=ds2)
+            dh1 = K.linear_dgrad(du, sv["W1"], w_t=t_image(sv["W1"]), residual=ds2)
             del k1, k2
         else:
             call("dph_layernorm_bwd", ptr(dout), ptr(s2), None, ptr(ln2_w), ptr(mu2), ptr(rs2), ptr(ds2),
@@ -1019,7 +1040,7 @@ class EncoderLayerFn(torch.autograd.Function):
                  ptr(sv["a_pre"]), ptr(g["lma"]), *ln_ws(M, D, dev), _s())
             dwo, direct = go.buf(pr["wo"], zero=False)
             k3 = K.linear_wgrad(da, sv["o_m"], dwo, accumulate=direct)
-            do_m = K.linear_dgrad(da, sv["Wo"])
+            do_m = K.linear_dgrad(da, sv["Wo"], w_t=t_image(sv["Wo"]))
             Dvec = torch.empty(B * H * T, dtype=F32, device=dev)
             g["hm"] = z(H) if has_hm else None
             call("dph_attention_bwd_prep", ptr(do_m), ptr(sv["o_u"]), ptr(hm), ptr(Dvec), ptr(g["hm"]), B, T, H, _s())
@@ -1030,7 +1051,7 @@ class EncoderLayerFn(torch.autograd.Function):
             call("dph_colsum", ptr(dqkv), ptr(dbqkv), M, dqkv.shape[1], *colsum_ws(M, dqkv.shape[1], dev), _s())
             dwqkv, direct = go.buf(pr["wq"], pr["wk"], pr["wv"], zero=False)
             k4 = K.linear_wgrad(dqkv, h, dwqkv, accumulate=direct)
-            dh = K.linear_dgrad(dqkv, sv["Wqkv"], residual=ds1)
+            dh = K.linear_dgrad(dqkv, sv["Wqkv"], w_t=t_image(sv["Wqkv"]), residual=ds1)
             del k3, k4
         else:
             call("dph_layernorm_bwd", ptr(dh1), ptr(s1), None, ptr(ln1_w), ptr(mu1), ptr(rs1), ptr(ds1),
@@ -1107,7 +1128,7 @@ class DistillProjLossFn(torch.autograd.Function):
             p = cfg["proj_index"][l]
             keep.append(K.linear_wgrad(ds[l], sh[l], dW[p], accumulate=True))
             call("dph_colsum", ptr(ds[l]), ptr(db[p]), M, Dt, *colsum_ws(M, Dt, dev), _s())
-            dh.append(K.linear_dgrad(ds[l], imgs[p]))
+            dh.append(K.linear_dgrad(ds[l], imgs[p], w_t=t_image(imgs[p])))
         go.done()
         grads = [None] + dh
         for p in range(P):

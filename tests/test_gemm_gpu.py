@@ -9,7 +9,7 @@ pytestmark = pytest.mark.gpu
 torch.manual_seed(0)
 
 
-@pytest.fixture(autouse=True, params=["small", "mid", "big", "wide", "tall"])
+@pytest.fixture(autouse=True, params=["small", "mid", "big", "wide", "tall", "half"])
 def gemm_path(request, monkeypatch):
     """Run every test on each GEMM path: the 128x128 register-staged kernel and the 128x128 /
     256x256 / 256x64 LDS-DMA ring kernels (taken where their constraints hold: both operands
@@ -184,3 +184,22 @@ def test_perf_ffn_shape():
     ms = e0.elapsed_time(e1) / 20
     tf = 2 * M * N * K / ms / 1e9
     print(f"\nFFN1 GEMM {M}x{N}x{K}: {ms*1e3:.1f} us, {tf:.0f} TFLOP/s")
+
+
+@pytest.mark.parametrize("R,C", [(768, 3072), (2304, 768), (40, 136)])
+def test_transposed_image_dgrad(R, C):
+    """ops.t_image is an exact transpose, and the input-gradient GEMM on it (both operands
+    k-contiguous) matches the mn-contiguous form."""
+    from dphubert_amd import ops
+    K_ = _k()
+    img = rnd(R, C)
+    wt = ops.t_image(img)
+    assert wt is not None and torch.equal(wt, img.t().contiguous())
+    assert ops.t_image(img) is wt            # cached on the image
+    dy = rnd(520, R)
+    a = K_.linear_dgrad(dy, img)
+    b = K_.linear_dgrad(dy, img, w_t=wt)
+    torch.cuda.synchronize()
+    ref = dy.float() @ img.float()
+    close(a, ref, 1e-2)
+    close(b, ref, 1e-2)

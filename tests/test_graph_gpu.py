@@ -96,14 +96,20 @@ def test_graph_replay_matches_eager():
     assert len(set(round(x, 6) for x in lg)) > 1, "replayed steps did not train"
     pa = dict(ea.module.named_parameters())
     pb = dict(eb.module.named_parameters())
-    for n, p in gr.module.named_parameters():
-        # k_proj.bias has an exactly-zero gradient (softmax shift invariance): Adam turns the fp32
-        # atomic-order noise of that zero into +-lr steps, so it is not comparable run to run
-        if not p.requires_grad or n.endswith("k_proj.bias"):
-            continue
-        e = rel_l2(p.detach().cpu(), pa[n].detach().cpu())
+    names = [n for n, p in gr.module.named_parameters() if p.requires_grad and not n.endswith("k_proj.bias")]
+    # k_proj.bias has an exactly-zero gradient (softmax shift invariance): Adam turns the fp32
+    # atomic-order noise of that zero into +-lr steps, so it is not comparable run to run.
+    # Per parameter: within 4x the eager-vs-eager drift of the same parameter or 5e-3 (small-gradient
+    # biases drift ~2e-3 between two EAGER runs after 5 Adam steps); all parameters together: within
+    # 4x the eager-vs-eager drift of the whole parameter vector.
+    pg = dict(gr.module.named_parameters())
+    for n in names:
+        e = rel_l2(pg[n].detach().cpu(), pa[n].detach().cpu())
         base = rel_l2(pb[n].detach().cpu(), pa[n].detach().cpu())
-        assert e < max(1e-3, 4 * base), (n, e, base)
+        assert e < max(5e-3, 4 * base), (n, e, base)
+    cat = lambda d: torch.cat([d[n].detach().float().flatten().cpu() for n in names])  # noqa: E731
+    e_all, base_all = rel_l2(cat(pg), cat(pa)), rel_l2(cat(pb), cat(pa))
+    assert e_all < max(1e-5, 4 * base_all), (e_all, base_all)
     # the graph replays follow the LR schedule: optimizer and scheduler state agree
     assert ea.optimizer._step == gr.optimizer._step
     for g1, g2 in zip(ea.optimizer.param_groups, gr.optimizer.param_groups):

@@ -20,13 +20,16 @@ if sys.argv[1] == "build":
     b.build()
     objs = [o for o in (REPO / "dphubert_amd" / "csrc" / "build").glob("*.o") if o.stem != "gemm"]
     (REPO / "ab").mkdir(exist_ok=True)
-    for n in range(7):
-        obj = REPO / "ab" / f"gemm_abl{n}.o"
-        subprocess.run([b.HIPCC] + b.FLAGS + [f"-DDPH_ABLATE={n}", "-c", str(b.CSRC / "gemm.hip"), "-o", str(obj)],
-                       check=True)
-        subprocess.run([b.HIPCC, f"--offload-arch={b.ARCH}", "-shared", "-fPIC", "-o", str(REPO / "ab" / f"abl{n}.so"),
+    # abl0..abl6: DPH_ABLATE variants; extra args "stgN" build ab/stgN.so with DPH_STAGGER=N
+    variants = sys.argv[2:] or [str(n) for n in range(7)]
+    for n in variants:
+        flag = f"-DDPH_STAGGER={n[3:]}" if n.startswith("stg") else f"-DDPH_ABLATE={n}"
+        name = n if n.startswith("stg") else f"abl{n}"
+        obj = REPO / "ab" / f"gemm_{name}.o"
+        subprocess.run([b.HIPCC] + b.FLAGS + [flag, "-c", str(b.CSRC / "gemm.hip"), "-o", str(obj)], check=True)
+        subprocess.run([b.HIPCC, f"--offload-arch={b.ARCH}", "-shared", "-fPIC", "-o", str(REPO / "ab" / f"{name}.so"),
                         str(obj)] + [str(o) for o in objs], check=True)
-        print("built", n)
+        print("built", name)
 else:
     import torch
     from dphubert_amd import kernels as K
