@@ -116,14 +116,24 @@ __device__ __forceinline__ void stage_store(char* lds, const uint4 (&reg)[ROWS /
 constexpr int KTILE_PAD_BYTES = KT * PADROW * 2;   // 9216
 constexpr int TILE_SWZ_BYTES = KT * 128;           // 8192
 
+// Each wave owns NG = 2 groups of 16 rows (queries in the forward / dQ kernels, keys in dK/dV), so
+// every K / V (resp. Q / dO) fragment read from LDS feeds NG MFMAs: with one group per wave the
+// fragment reads alone filled the CU's LDS bandwidth (~1 KB per 16-cycle MFMA per wave).
+constexpr int NG = 2;
+constexpr int RB = 4 * 16 * NG;   // rows per block: 128
+
 // ---------------------------------------------------------------------------
-// forward: block = (64 query rows, head h, utterance b), 4 waves x 16 rows
+// forward: block = (128 query rows, head h, utterance b), 4 waves x 2 x 16 rows.
+// DROP is a template parameter and the key masks are selects on 32-bit key indices, so a tile is
+// one basic block (runtime `if`s split it and kept hipcc from overlapping one query group's
+// softmax with the other group's MFMAs).
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) attn_fwd_kernel(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ o_u,
-                                                       bf16_t* __restrict__ o_m, float* __restrict__ lse,
-                                                       const float* __restrict__ head_mask,
-                                                       const int64_t* __restrict__ key_len, AttnShape sh, float scale,
-                                                       float drop_p, uint64_t seed) {
+template <bool DROP>
+__global__ void __launch_bounds__(256, 2) attn_fwd_kernel(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ o_u,
+                                                          bf16_t* __restrict__ o_m, float* __restrict__ lse,
+                                                          const float* __restrict__ head_mask,
+                                                          const int64_t* __restrict__ key_len, AttnShape sh,
+                                                          float scale, float drop_p, uint64_t seed) {
   seed = epoch_seed(seed);   // per-step RNG epoch (graph replays)
   __shared__ __attribute__((aligned(16))) char smem[2 * (KTILE_PAD_BYTES + TILE_SWZ_BYTES)];
   const int tid = threadIdx.x;
@@ -133,27 +143,41 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const bf16_t* __restrict_
   const int64_t b = blockIdx.z;
   const int64_t h = blockIdx.y;
   const int64_t T = sh.T, H = sh.H, RS = sh.RS;
-  const int64_t q0 = (int64_t)blockIdx.x * QT + wave * 16;
-  const int64_t qme = q0 + (lane & 15);
+  const int T32 = (int)T;
+  const int64_t q0 = (int64_t)blockIdx.x * RB + wave * 16 * NG;
   const bf16_t* rowbase = qkv + b * T * RS;
-  const int64_t klen = key_len ? key_len[b] : T;
-
-  // Q' = scale*q fragments (B operand of S^T = K Q'^T): Q'[q = lane&15][hd = 32ks + 8g + j]
-  bf16x8_t qf[2];
+  const int klen = (int)(key_len ? key_len[b] : T);
+  const uint64_t half_tp = (uint64_t)(T + 1) >> 1;
+  int64_t qme[NG];
+  uint64_t hrow[NG];   // dropout pair index of (row, key 0)
 #pragma unroll
-  for (int ks = 0; ks < 2; ++ks) {
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (qme < T) v = *reinterpret_cast<const uint4*>(rowbase + qme * RS + h * HD + ks * 32 + 8 * g);
-    qf[ks] = __builtin_bit_cast(bf16x8_t, scale_bf16x8(v, scale));
+  for (int u = 0; u < NG; ++u) {
+    qme[u] = q0 + 16 * u + (lane & 15);
+    hrow[u] = ((uint64_t)(b * H + h) * T + (uint64_t)qme[u]) * half_tp;
   }
 
-  f32x4_t oacc[4];
+  // Q' = scale*q fragments (B operand of S^T = K Q'^T): Q'[q = lane&15][hd = 32ks + 8g + j]
+  bf16x8_t qf[NG][2];
 #pragma unroll
-  for (int d = 0; d < 4; ++d) oacc[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  float m_run = -INFINITY, l_run = 0.f;
-  const float inv_keep = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
+  for (int u = 0; u < NG; ++u)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (qme[u] < T) v = *reinterpret_cast<const uint4*>(rowbase + qme[u] * RS + h * HD + ks * 32 + 8 * g);
+      qf[u][ks] = __builtin_bit_cast(bf16x8_t, scale_bf16x8(v, scale));
+    }
+
+  f32x4_t oacc[NG][4];
+  float m_run[NG], l_run[NG];
+#pragma unroll
+  for (int u = 0; u < NG; ++u) {
+    m_run[u] = -INFINITY;
+    l_run[u] = 0.f;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) oacc[u][d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  }
+  const float inv_keep = DROP ? 1.f / (1.f - drop_p) : 1.f;
   const uint32_t thr = drop_thr(drop_p);
-  const uint64_t half_tp = (uint64_t)(T + 1) >> 1;
 
   const int nkt = (int)cdiv(T, KT);
   uint4 rk[2], rv[2];
@@ -174,66 +198,71 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const bf16_t* __restrict_
     }
     const char* K_ = ldsK(cur);
     const char* V_ = ldsV(cur);
-    // S^T[key = 16s + 4g + i][q = lane&15]
-    f32x4_t sacc[4];
+    // S^T[key = 16s + 4g + i][q = lane&15] per query group
+    f32x4_t sacc[NG][4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      sacc[s] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < NG; ++u) sacc[u][s] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         const bf16x8_t kf = lds_b128(K_, ((16 * s + (lane & 15)) * PADROW + ks * 32 + 8 * g) * 2);
-        sacc[s] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[ks], sacc[s], 0, 0, 0);
+#pragma unroll
+        for (int u = 0; u < NG; ++u) sacc[u][s] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[u][ks], sacc[u][s], 0, 0, 0);
       }
     }
-    float mt = -INFINITY;
+    const int kb = kt * KT + 4 * g;   // key of (s = 0, i = 0) for this lane
 #pragma unroll
-    for (int s = 0; s < 4; ++s)
+    for (int u = 0; u < NG; ++u) {
+      float mt = -INFINITY;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int64_t key = (int64_t)kt * KT + 16 * s + 4 * g + i;
-        float v = sacc[s][i];
-        if (key >= klen) v += -10000.0f;
-        if (key >= T) v = -INFINITY;
-        sacc[s][i] = v;
-        mt = fmaxf(mt, v);
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int key = kb + 16 * s + i;
+          float v = sacc[u][s][i];
+          v = key >= klen ? v - 10000.0f : v;
+          v = key >= T32 ? -INFINITY : v;
+          sacc[u][s][i] = v;
+          mt = fmaxf(mt, v);
+        }
+      mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
+      mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+      const float m_new = fmaxf(m_run[u], mt);
+      const float alpha = __expf(m_run[u] - m_new);
+      float ls = 0.f;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        uint32_t hb[2] = {0u, 0u};
+        if constexpr (DROP) {
+          const uint64_t pr = hrow[u] + (uint64_t)((kb + 16 * s) >> 1);
+          hb[0] = drop_bits2(seed, pr);
+          hb[1] = drop_bits2(seed, pr + 1);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float p = __expf(sacc[u][s][i] - m_new);
+          ls += p;
+          sacc[u][s][i] = DROP ? p * attn_keep(hb[i >> 1], i & 1, thr, inv_keep) : p;
+        }
       }
-    mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
-    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-    const float m_new = fmaxf(m_run, mt);
-    const float alpha = __expf(m_run - m_new);
-    float ls = 0.f;
-    const uint64_t arow = (uint64_t)(b * H + h) * T + (uint64_t)qme;
+      ls += __shfl_xor(ls, 16, 64);
+      ls += __shfl_xor(ls, 32, 64);
+      l_run[u] = l_run[u] * alpha + ls;
+      m_run[u] = m_new;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      uint32_t hb[2] = {0u, 0u};
-      if (drop_p > 0.f) {
-        const int64_t key0 = (int64_t)kt * KT + 16 * s + 4 * g;
-        hb[0] = attn_hash(seed, arow, key0, half_tp);
-        hb[1] = attn_hash(seed, arow, key0 + 2, half_tp);
-      }
+      for (int d = 0; d < 4; ++d)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float p = __expf(sacc[s][i] - m_new);
-        ls += p;
-        sacc[s][i] = drop_p > 0.f ? p * attn_keep(hb[i >> 1], i & 1, thr, inv_keep) : p;
-      }
-    }
-    ls += __shfl_xor(ls, 16, 64);
-    ls += __shfl_xor(ls, 32, 64);
-    l_run = l_run * alpha + ls;
-    m_run = m_new;
+        for (int i = 0; i < 4; ++i) oacc[u][d][i] *= alpha;
+      // O^T[d][q] += V^T[d][key] P^T[key][q]; k index of step kk: key(g,j) = 16(2kk + j/4) + 4g + j%4
 #pragma unroll
-    for (int d = 0; d < 4; ++d)
+      for (int kk = 0; kk < 2; ++kk) {
+        const bf16x8_t pf = pack_frag(sacc[u][2 * kk], sacc[u][2 * kk + 1]);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) oacc[d][i] *= alpha;
-    // O^T[d][q] += V^T[d][key] P^T[key][q]; k index of step kk: key(g,j) = 16(2kk + j/4) + 4g + j%4
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const bf16x8_t pf = pack_frag(sacc[2 * kk], sacc[2 * kk + 1]);
-#pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        const bf16x8_t vf = tr_frag(V_, 32 * kk + 4 * g, 32 * kk + 16 + 4 * g, 16 * d, lane);
-        oacc[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf, oacc[d], 0, 0, 0);
+        for (int d = 0; d < 4; ++d) {
+          const bf16x8_t vf = tr_frag(V_, 32 * kk + 4 * g, 32 * kk + 16 + 4 * g, 16 * d, lane);
+          oacc[u][d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf, oacc[u][d], 0, 0, 0);
+        }
       }
     }
     if (more) {
@@ -243,19 +272,21 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const bf16_t* __restrict_
     __syncthreads();
   }
 
-  if (qme < T) {
-    const float inv_l = 1.0f / l_run;
-    const float hm = head_mask ? head_mask[h] : 1.0f;
-    const int64_t obase = (b * T + qme) * (H * HD) + h * HD;
+  const float hm = head_mask ? head_mask[h] : 1.0f;
+#pragma unroll
+  for (int u = 0; u < NG; ++u) {
+    if (qme[u] >= T) continue;
+    const float inv_l = 1.0f / l_run[u];
+    const int64_t obase = (b * T + qme[u]) * (H * HD) + h * HD;
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
       const int col = 16 * d + 4 * g;
-      float v[4] = {oacc[d][0] * inv_l, oacc[d][1] * inv_l, oacc[d][2] * inv_l, oacc[d][3] * inv_l};
+      float v[4] = {oacc[u][d][0] * inv_l, oacc[u][d][1] * inv_l, oacc[u][d][2] * inv_l, oacc[u][d][3] * inv_l};
       *reinterpret_cast<uint2*>(o_u + obase + col) = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
       *reinterpret_cast<uint2*>(o_m + obase + col) =
           make_uint2(pack2bf(v[0] * hm, v[1] * hm), pack2bf(v[2] * hm, v[3] * hm));
     }
-    if (g == 0) lse[(b * H + h) * T + qme] = m_run + __logf(l_run);
+    if (g == 0) lse[(b * H + h) * T + qme[u]] = m_run[u] + __logf(l_run[u]);
   }
 }
 
@@ -297,10 +328,11 @@ __global__ void __launch_bounds__(256) attn_bwd_prep_kernel(const bf16_t* __rest
 }
 
 // ---------------------------------------------------------------------------
-// backward dK, dV: block = (64 keys, h, b), wave w owns keys k0 = 64*bx + 16w .. +16.
-// Loops over query steps of 32 rows; Q' and dO' (= hm*dO_m) tiles staged in LDS.
+// backward dK, dV: block = (128 keys, h, b), wave w owns keys k0 = 128*bx + 32w + 16u + (0..15),
+// u < NG.  Loops over query steps of 32 rows; Q' and dO' (= hm*dO_m) tiles staged in LDS.
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) attn_bwd_dkv_kernel(const bf16_t* __restrict__ qkv,
+template <bool DROP>
+__global__ void __launch_bounds__(256, 2) attn_bwd_dkv_kernel(const bf16_t* __restrict__ qkv,
                                                            const bf16_t* __restrict__ dom,
                                                            const float* __restrict__ head_mask,
                                                            const float* __restrict__ lse,
@@ -317,8 +349,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dkv_kernel(const bf16_t* __restr
   const int64_t b = blockIdx.z;
   const int64_t h = blockIdx.y;
   const int64_t T = sh.T, H = sh.H, RS = sh.RS;
-  const int64_t k0 = (int64_t)blockIdx.x * KT + wave * 16;
-  const int64_t kme = k0 + (lane & 15);
+  const int64_t k0 = (int64_t)blockIdx.x * RB + wave * 16 * NG;
   const bf16_t* rowbase = qkv + b * T * RS;
   const bf16_t* dobase = dom + b * T * (H * HD) + h * HD;
   const int64_t klen = key_len ? key_len[b] : T;
@@ -326,26 +357,39 @@ __global__ void __launch_bounds__(256) attn_bwd_dkv_kernel(const bf16_t* __restr
   const float inv_keep = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
   const uint32_t thr = drop_thr(drop_p);
   const uint64_t half_tp = (uint64_t)(T + 1) >> 1;
-  const bool odd_key = (kme & 1) != 0;
+  const bool odd_key = (lane & 1) != 0;     // key parity (k0 is a multiple of 16)
+  int64_t kme[NG];
+  bool kpad[NG], kout[NG];   // key padded (masked -1e4) / past T
+  const int T32 = (int)T;
+#pragma unroll
+  for (int u = 0; u < NG; ++u) {
+    kme[u] = k0 + 16 * u + (lane & 15);
+    kpad[u] = kme[u] >= klen;
+    kout[u] = kme[u] >= T;
+  }
 
   // K[key = lane&15][hd 32ks+8g+j], V[...]: B operands of S = Q' K^T and dP = dO V^T
-  bf16x8_t kf[2], vf[2];
+  bf16x8_t kf[NG][2], vf[NG][2];
 #pragma unroll
-  for (int ks = 0; ks < 2; ++ks) {
-    uint4 a = make_uint4(0, 0, 0, 0), c = make_uint4(0, 0, 0, 0);
-    if (kme < T) {
-      a = *reinterpret_cast<const uint4*>(rowbase + kme * RS + (H + h) * HD + ks * 32 + 8 * g);
-      c = *reinterpret_cast<const uint4*>(rowbase + kme * RS + (2 * H + h) * HD + ks * 32 + 8 * g);
+  for (int u = 0; u < NG; ++u)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      uint4 x = make_uint4(0, 0, 0, 0), c = make_uint4(0, 0, 0, 0);
+      if (kme[u] < T) {
+        x = *reinterpret_cast<const uint4*>(rowbase + kme[u] * RS + (H + h) * HD + ks * 32 + 8 * g);
+        c = *reinterpret_cast<const uint4*>(rowbase + kme[u] * RS + (2 * H + h) * HD + ks * 32 + 8 * g);
+      }
+      kf[u][ks] = __builtin_bit_cast(bf16x8_t, x);
+      vf[u][ks] = __builtin_bit_cast(bf16x8_t, c);
     }
-    kf[ks] = __builtin_bit_cast(bf16x8_t, a);
-    vf[ks] = __builtin_bit_cast(bf16x8_t, c);
-  }
-  f32x4_t dk[4], dv[4];
+  f32x4_t dk[NG][4], dv[NG][4];
 #pragma unroll
-  for (int d = 0; d < 4; ++d) {
-    dk[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    dv[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  }
+  for (int u = 0; u < NG; ++u)
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      dk[u][d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      dv[u][d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    }
   auto ldsQ = [&](int buf) { return smem + buf * 2 * TB; };
   auto ldsO = [&](int buf) { return smem + buf * 2 * TB + TB; };
   float* lse_s = reinterpret_cast<float*>(smem + 4 * TB);        // [2][32]
@@ -375,81 +419,97 @@ __global__ void __launch_bounds__(256) attn_bwd_dkv_kernel(const bf16_t* __restr
     if (more) load_tiles(qt + 1);
     const char* Q_ = ldsQ(cur);
     const char* O_ = ldsO(cur);
-    // S[q = 16u + 4g + i][key = lane&15], dP likewise
-    f32x4_t sacc[2], pacc[2];
+    // S[q = 16w + 4g + i][key = lane&15], dP likewise (w: query sub-step, u: key group)
+    f32x4_t sacc[NG][2], pacc[NG][2];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      sacc[u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-      pacc[u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int w = 0; w < 2; ++w) {
+#pragma unroll
+      for (int u = 0; u < NG; ++u) {
+        sacc[u][w] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        pacc[u][w] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      }
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        const bf16x8_t qa = lds_b128(Q_, swz128(16 * u + (lane & 15), ks * 32 + 8 * g));
-        const bf16x8_t oa = lds_b128(O_, swz128(16 * u + (lane & 15), ks * 32 + 8 * g));
-        sacc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa, kf[ks], sacc[u], 0, 0, 0);
-        pacc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(oa, vf[ks], pacc[u], 0, 0, 0);
+        const bf16x8_t qa = lds_b128(Q_, swz128(16 * w + (lane & 15), ks * 32 + 8 * g));
+        const bf16x8_t oa = lds_b128(O_, swz128(16 * w + (lane & 15), ks * 32 + 8 * g));
+#pragma unroll
+        for (int u = 0; u < NG; ++u) {
+          sacc[u][w] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa, kf[u][ks], sacc[u][w], 0, 0, 0);
+          pacc[u][w] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(oa, vf[u][ks], pacc[u][w], 0, 0, 0);
+        }
       }
     }
-    f32x4_t pz[2], ds[2];
+    bf16x8_t pzf[NG], dsf[NG];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      // this lane hashes queries ia, ia+1 of its key pair; the neighbour (key ^ 1) the other two
-      uint32_t hb[4] = {0u, 0u, 0u, 0u};
-      if (drop_p > 0.f) {
-        const int ia = odd_key ? 2 : 0;
-        const uint64_t qa = (uint64_t)(b * H + h) * T + (uint64_t)(qt * QT_BWD + 16 * u + 4 * g + ia);
-        const uint32_t h0 = attn_hash(seed, qa, kme, half_tp);
-        const uint32_t h1 = attn_hash(seed, qa + 1, kme, half_tp);
-        const uint32_t o0 = (uint32_t)__shfl_xor((int)h0, 1, 64);
-        const uint32_t o1 = (uint32_t)__shfl_xor((int)h1, 1, 64);
-        hb[0] = odd_key ? o0 : h0;
-        hb[1] = odd_key ? o1 : h1;
-        hb[2] = odd_key ? h0 : o0;
-        hb[3] = odd_key ? h1 : o1;
-      }
+    for (int u = 0; u < NG; ++u) {
+      f32x4_t pz[2], ds[2];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int ql = 16 * u + 4 * g + i;
-        const int64_t q = (int64_t)qt * QT_BWD + ql;
-        float s = sacc[u][i];
-        if (kme >= klen) s += -10000.0f;
-        float p = __expf(s - lse_s[cur * QT_BWD + ql]);
-        if (q >= T || kme >= T) p = 0.f;
-        const float z = drop_p > 0.f ? attn_keep(hb[i], odd_key, thr, inv_keep) : 1.f;
-        pz[u][i] = p * z;
-        ds[u][i] = p * (pacc[u][i] * z - dv_s[cur * QT_BWD + ql]);
+      for (int w = 0; w < 2; ++w) {
+        // this lane hashes queries ia, ia+1 of its key pair; the neighbour (key ^ 1) the other two
+        uint32_t hb[4] = {0u, 0u, 0u, 0u};
+        if constexpr (DROP) {
+          const int ia = odd_key ? 2 : 0;
+          const uint64_t qa = (uint64_t)(b * H + h) * T + (uint64_t)(qt * QT_BWD + 16 * w + 4 * g + ia);
+          const uint32_t h0 = attn_hash(seed, qa, kme[u], half_tp);
+          const uint32_t h1 = attn_hash(seed, qa + 1, kme[u], half_tp);
+          const uint32_t o0 = (uint32_t)__shfl_xor((int)h0, 1, 64);
+          const uint32_t o1 = (uint32_t)__shfl_xor((int)h1, 1, 64);
+          hb[0] = odd_key ? o0 : h0;
+          hb[1] = odd_key ? o1 : h1;
+          hb[2] = odd_key ? h0 : o0;
+          hb[3] = odd_key ? h1 : o1;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int ql = 16 * w + 4 * g + i;
+          const int q = qt * QT_BWD + ql;
+          float sv = sacc[u][w][i];
+          sv = kpad[u] ? sv - 10000.0f : sv;
+          float p = __expf(sv - lse_s[cur * QT_BWD + ql]);
+          p = (q >= T32 || kout[u]) ? 0.f : p;
+          const float z = DROP ? attn_keep(hb[i], odd_key, thr, inv_keep) : 1.f;
+          pz[w][i] = p * z;
+          ds[w][i] = p * (pacc[u][w][i] * z - dv_s[cur * QT_BWD + ql]);
+        }
       }
+      pzf[u] = pack_frag(pz[0], pz[1]);
+      dsf[u] = pack_frag(ds[0], ds[1]);
     }
     // dV[key][d] += sum_q PZ[q][key] dO'[q][d] ; dK[key][d] += sum_q dS[q][key] Q'[q][d]
-    const bf16x8_t pzf = pack_frag(pz[0], pz[1]);
-    const bf16x8_t dsf = pack_frag(ds[0], ds[1]);
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
       const bf16x8_t of = tr_frag(O_, 4 * g, 16 + 4 * g, 16 * d, lane);
       const bf16x8_t qf = tr_frag(Q_, 4 * g, 16 + 4 * g, 16 * d, lane);
-      dv[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pzf, of, dv[d], 0, 0, 0);
-      dk[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dsf, qf, dk[d], 0, 0, 0);
+#pragma unroll
+      for (int u = 0; u < NG; ++u) {
+        dv[u][d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pzf[u], of, dv[u][d], 0, 0, 0);
+        dk[u][d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dsf[u], qf, dk[u][d], 0, 0, 0);
+      }
     }
     if (more) store_tiles(cur ^ 1, qt + 1);
     __syncthreads();
   }
-  // lane holds dK[key = k0 + 4g + i][d = 16dd + (lane&15)]
+  // lane holds dK[key = k0 + 16u + 4g + i][d = 16dd + (lane&15)]
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int64_t key = k0 + 4 * g + i;
-    if (key >= T) continue;
-    bf16_t* rowp = dqkv + (b * T + key) * RS;
+  for (int u = 0; u < NG; ++u)
 #pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      rowp[(H + h) * HD + 16 * d + (lane & 15)] = f2bf(dk[d][i]);
-      rowp[(2 * H + h) * HD + 16 * d + (lane & 15)] = f2bf(dv[d][i]);
+    for (int i = 0; i < 4; ++i) {
+      const int64_t key = k0 + 16 * u + 4 * g + i;
+      if (key >= T) continue;
+      bf16_t* rowp = dqkv + (b * T + key) * RS;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        rowp[(H + h) * HD + 16 * d + (lane & 15)] = f2bf(dk[u][d][i]);
+        rowp[(2 * H + h) * HD + 16 * d + (lane & 15)] = f2bf(dv[u][d][i]);
+      }
     }
-  }
 }
 
 // ---------------------------------------------------------------------------
-// backward dQ: block = (64 query rows, h, b), 4 waves x 16 rows; loops over key tiles.
+// backward dQ: block = (128 query rows, h, b), 4 waves x 2 x 16 rows; loops over key tiles.
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) attn_bwd_dq_kernel(const bf16_t* __restrict__ qkv,
+template <bool DROP>
+__global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(const bf16_t* __restrict__ qkv,
                                                           const bf16_t* __restrict__ dom,
                                                           const float* __restrict__ head_mask,
                                                           const float* __restrict__ lse,
@@ -465,29 +525,39 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(const bf16_t* __restri
   const int64_t b = blockIdx.z;
   const int64_t h = blockIdx.y;
   const int64_t T = sh.T, H = sh.H, RS = sh.RS;
-  const int64_t q0 = (int64_t)blockIdx.x * QT + wave * 16;
-  const int64_t qme = q0 + (lane & 15);
+  const int64_t q0 = (int64_t)blockIdx.x * RB + wave * 16 * NG;
   const bf16_t* rowbase = qkv + b * T * RS;
   const int64_t klen = key_len ? key_len[b] : T;
   const float hm = head_mask ? head_mask[h] : 1.0f;
   const float inv_keep = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
-
-  bf16x8_t qf[2], of[2];
+  int64_t qme[NG];
+  uint64_t hrow[NG];
+  bool qout[NG];
+  bf16x8_t qf[NG][2], of[NG][2];
+  float my_lse[NG], my_D[NG];
+  f32x4_t dq[NG][4];
+  const int T32 = (int)T, klen32 = (int)klen;
+  const uint64_t half_tp0 = (uint64_t)(T + 1) >> 1;
 #pragma unroll
-  for (int ks = 0; ks < 2; ++ks) {
-    uint4 a = make_uint4(0, 0, 0, 0), c = make_uint4(0, 0, 0, 0);
-    if (qme < T) {
-      a = *reinterpret_cast<const uint4*>(rowbase + qme * RS + h * HD + ks * 32 + 8 * g);
-      c = *reinterpret_cast<const uint4*>(dom + (b * T + qme) * (H * HD) + h * HD + ks * 32 + 8 * g);
+  for (int u = 0; u < NG; ++u) {
+    qme[u] = q0 + 16 * u + (lane & 15);
+    qout[u] = qme[u] >= T;
+    hrow[u] = ((uint64_t)(b * H + h) * T + (uint64_t)qme[u]) * half_tp0;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      uint4 x = make_uint4(0, 0, 0, 0), c = make_uint4(0, 0, 0, 0);
+      if (qme[u] < T) {
+        x = *reinterpret_cast<const uint4*>(rowbase + qme[u] * RS + h * HD + ks * 32 + 8 * g);
+        c = *reinterpret_cast<const uint4*>(dom + (b * T + qme[u]) * (H * HD) + h * HD + ks * 32 + 8 * g);
+      }
+      qf[u][ks] = __builtin_bit_cast(bf16x8_t, scale_bf16x8(x, scale));
+      of[u][ks] = __builtin_bit_cast(bf16x8_t, scale_bf16x8(c, hm));
     }
-    qf[ks] = __builtin_bit_cast(bf16x8_t, scale_bf16x8(a, scale));
-    of[ks] = __builtin_bit_cast(bf16x8_t, scale_bf16x8(c, hm));
-  }
-  const float my_lse = qme < T ? lse[(b * H + h) * T + qme] : 0.f;
-  const float my_D = qme < T ? Dv[(b * H + h) * T + qme] : 0.f;
-  f32x4_t dq[4];
+    my_lse[u] = qme[u] < T ? lse[(b * H + h) * T + qme[u]] : 0.f;
+    my_D[u] = qme[u] < T ? Dv[(b * H + h) * T + qme[u]] : 0.f;
 #pragma unroll
-  for (int d = 0; d < 4; ++d) dq[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int d = 0; d < 4; ++d) dq[u][d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  }
 
   auto ldsK = [&](int buf) { return smem + buf * (TILE_SWZ_BYTES + KTILE_PAD_BYTES); };
   auto ldsV = [&](int buf) { return smem + buf * (TILE_SWZ_BYTES + KTILE_PAD_BYTES) + TILE_SWZ_BYTES; };
@@ -498,7 +568,6 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(const bf16_t* __restri
   stage_store<KT, true>(ldsK(0), rk, tid);
   stage_store<KT, false>(ldsV(0), rv, tid);
   __syncthreads();
-  const uint64_t arow = (uint64_t)(b * H + h) * T + (uint64_t)qme;
   const uint32_t thr = drop_thr(drop_p);
   const uint64_t half_tp = (uint64_t)(T + 1) >> 1;
   for (int kt = 0; kt < nkt; ++kt) {
@@ -510,42 +579,57 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(const bf16_t* __restri
     }
     const char* K_ = ldsK(cur);
     const char* V_ = ldsV(cur);
-    f32x4_t ds[4];
+    f32x4_t ds[NG][4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      f32x4_t sa = f32x4_t{0.f, 0.f, 0.f, 0.f}, pa = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      f32x4_t sa[NG], pa[NG];
+#pragma unroll
+      for (int u = 0; u < NG; ++u) {
+        sa[u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        pa[u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      }
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         const bf16x8_t ka = lds_b128(K_, swz128(16 * s + (lane & 15), ks * 32 + 8 * g));
         const bf16x8_t va = lds_b128(V_, ((16 * s + (lane & 15)) * PADROW + ks * 32 + 8 * g) * 2);
-        sa = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka, qf[ks], sa, 0, 0, 0);
-        pa = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, of[ks], pa, 0, 0, 0);
-      }
-      uint32_t hb[2] = {0u, 0u};
-      if (drop_p > 0.f) {
-        const int64_t key0 = (int64_t)kt * KT + 16 * s + 4 * g;
-        hb[0] = attn_hash(seed, arow, key0, half_tp);
-        hb[1] = attn_hash(seed, arow, key0 + 2, half_tp);
-      }
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int64_t key = (int64_t)kt * KT + 16 * s + 4 * g + i;
-        float sv = sa[i];
-        if (key >= klen) sv += -10000.0f;
-        float p = __expf(sv - my_lse);
-        if (key >= T || qme >= T) p = 0.f;
-        const float z = drop_p > 0.f ? attn_keep(hb[i >> 1], i & 1, thr, inv_keep) : 1.f;
-        ds[s][i] = p * (pa[i] * z - my_D);
+        for (int u = 0; u < NG; ++u) {
+          sa[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka, qf[u][ks], sa[u], 0, 0, 0);
+          pa[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, of[u][ks], pa[u], 0, 0, 0);
+        }
+      }
+      const int kb = kt * KT + 16 * s + 4 * g;
+#pragma unroll
+      for (int u = 0; u < NG; ++u) {
+        uint32_t hb[2] = {0u, 0u};
+        if constexpr (DROP) {
+          const uint64_t pr = hrow[u] + (uint64_t)(kb >> 1);
+          hb[0] = drop_bits2(seed, pr);
+          hb[1] = drop_bits2(seed, pr + 1);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int key = kb + i;
+          float sv = sa[u][i];
+          sv = key >= klen32 ? sv - 10000.0f : sv;
+          float p = __expf(sv - my_lse[u]);
+          p = (key >= T32 || qout[u]) ? 0.f : p;
+          const float z = DROP ? attn_keep(hb[i >> 1], i & 1, thr, inv_keep) : 1.f;
+          ds[u][s][i] = p * (pa[u][i] * z - my_D[u]);
+        }
       }
     }
     // dQ'^T[d][q] += K^T[d][key] dS^T[key][q]
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      const bf16x8_t dsf = pack_frag(ds[2 * kk], ds[2 * kk + 1]);
+      bf16x8_t dsf[NG];
+#pragma unroll
+      for (int u = 0; u < NG; ++u) dsf[u] = pack_frag(ds[u][2 * kk], ds[u][2 * kk + 1]);
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
         const bf16x8_t kt_f = tr_frag(K_, 32 * kk + 4 * g, 32 * kk + 16 + 4 * g, 16 * d, lane);
-        dq[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kt_f, dsf, dq[d], 0, 0, 0);
+#pragma unroll
+        for (int u = 0; u < NG; ++u) dq[u][d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kt_f, dsf[u], dq[u][d], 0, 0, 0);
       }
     }
     if (more) {
@@ -554,13 +638,15 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(const bf16_t* __restri
     }
     __syncthreads();
   }
-  if (qme < T) {
-    bf16_t* rowp = dqkv + (b * T + qme) * RS + h * HD;
+#pragma unroll
+  for (int u = 0; u < NG; ++u) {
+    if (qme[u] >= T) continue;
+    bf16_t* rowp = dqkv + (b * T + qme[u]) * RS + h * HD;
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
       const int col = 16 * d + 4 * g;
-      *reinterpret_cast<uint2*>(rowp + col) = make_uint2(pack2bf(dq[d][0] * scale, dq[d][1] * scale),
-                                                         pack2bf(dq[d][2] * scale, dq[d][3] * scale));
+      *reinterpret_cast<uint2*>(rowp + col) = make_uint2(pack2bf(dq[u][d][0] * scale, dq[u][d][1] * scale),
+                                                         pack2bf(dq[u][d][2] * scale, dq[u][d][3] * scale));
     }
   }
 }
@@ -575,10 +661,15 @@ extern "C" int dph_attention_fwd(const void* qkv, void* o_unmasked, void* o_mask
                                  float scale, float dropout_p, uint64_t seed, hipStream_t stream) {
   DPH_REQUIRE(qkv && o_unmasked && o_masked && lse && B > 0 && T > 0 && H > 0, "dph_attention_fwd: bad args");
   AttnShape sh{B, T, H, 3 * H * HD};
-  dim3 grid((unsigned)cdiv(T, QT), (unsigned)H, (unsigned)B);
-  hipLaunchKernelGGL(attn_fwd_kernel, grid, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(qkv),
-                     reinterpret_cast<bf16_t*>(o_unmasked), reinterpret_cast<bf16_t*>(o_masked), lse, head_mask,
-                     key_len, sh, scale, dropout_p, seed);
+  dim3 grid((unsigned)cdiv(T, RB), (unsigned)H, (unsigned)B);
+  if (dropout_p > 0.f)
+    hipLaunchKernelGGL(attn_fwd_kernel<true>, grid, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(qkv),
+                       reinterpret_cast<bf16_t*>(o_unmasked), reinterpret_cast<bf16_t*>(o_masked), lse, head_mask,
+                       key_len, sh, scale, dropout_p, seed);
+  else
+    hipLaunchKernelGGL(attn_fwd_kernel<false>, grid, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(qkv),
+                       reinterpret_cast<bf16_t*>(o_unmasked), reinterpret_cast<bf16_t*>(o_masked), lse, head_mask,
+                       key_len, sh, scale, dropout_p, seed);
   return check_launch("dph_attention_fwd");
 }
 
@@ -597,15 +688,25 @@ extern "C" int dph_attention_bwd(const void* qkv, const void* do_masked, const f
                                  int64_t H, float scale, float dropout_p, uint64_t seed, hipStream_t stream) {
   DPH_REQUIRE(qkv && do_masked && lse && Dvec && dqkv && B > 0 && T > 0 && H > 0, "dph_attention_bwd: bad args");
   AttnShape sh{B, T, H, 3 * H * HD};
-  dim3 grid((unsigned)cdiv(T, KT), (unsigned)H, (unsigned)B);
-  hipLaunchKernelGGL(attn_bwd_dkv_kernel, grid, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(qkv),
-                     reinterpret_cast<const bf16_t*>(do_masked), head_mask, lse, Dvec, reinterpret_cast<bf16_t*>(dqkv),
-                     key_len, sh, scale, dropout_p, seed);
+  dim3 grid((unsigned)cdiv(T, RB), (unsigned)H, (unsigned)B);
+  if (dropout_p > 0.f)
+    hipLaunchKernelGGL(attn_bwd_dkv_kernel<true>, grid, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(qkv),
+                       reinterpret_cast<const bf16_t*>(do_masked), head_mask, lse, Dvec, reinterpret_cast<bf16_t*>(dqkv),
+                       key_len, sh, scale, dropout_p, seed);
+  else
+    hipLaunchKernelGGL(attn_bwd_dkv_kernel<false>, grid, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(qkv),
+                       reinterpret_cast<const bf16_t*>(do_masked), head_mask, lse, Dvec, reinterpret_cast<bf16_t*>(dqkv),
+                       key_len, sh, scale, dropout_p, seed);
   int rc = check_launch("dph_attention_bwd dkv");
   if (rc) return rc;
-  dim3 grid2((unsigned)cdiv(T, QT), (unsigned)H, (unsigned)B);
-  hipLaunchKernelGGL(attn_bwd_dq_kernel, grid2, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(qkv),
-                     reinterpret_cast<const bf16_t*>(do_masked), head_mask, lse, Dvec, reinterpret_cast<bf16_t*>(dqkv),
-                     key_len, sh, scale, dropout_p, seed);
+  dim3 grid2((unsigned)cdiv(T, RB), (unsigned)H, (unsigned)B);
+  if (dropout_p > 0.f)
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<true>, grid2, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(qkv),
+                       reinterpret_cast<const bf16_t*>(do_masked), head_mask, lse, Dvec, reinterpret_cast<bf16_t*>(dqkv),
+                       key_len, sh, scale, dropout_p, seed);
+  else
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<false>, grid2, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(qkv),
+                       reinterpret_cast<const bf16_t*>(do_masked), head_mask, lse, Dvec, reinterpret_cast<bf16_t*>(dqkv),
+                       key_len, sh, scale, dropout_p, seed);
   return check_launch("dph_attention_bwd dq");
 }

@@ -91,8 +91,10 @@ def test_graph_replay_matches_eager():
     torch.cuda.synchronize()
     assert gr._graph is not None, "graph capture fell back to eager"
     assert ea.module.global_step == gr.module.global_step
-    for a, b in zip(le, lg):
-        assert abs(a - b) <= 1e-4 * max(1.0, abs(a)), (le, lg)
+    # losses: as close as two eager runs are (fp32 atomic order in weight-gradient reductions,
+    # amplified by Adam over the steps) plus 1e-4
+    for a, b, c in zip(le, lg, lb):
+        assert abs(a - b) <= 1e-4 * max(1.0, abs(a)) + 4 * abs(a - c), (le, lg, lb)
     assert len(set(round(x, 6) for x in lg)) > 1, "replayed steps did not train"
     pa = dict(ea.module.named_parameters())
     pb = dict(eb.module.named_parameters())
