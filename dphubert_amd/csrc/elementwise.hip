@@ -305,6 +305,78 @@ extern "C" int dph_transpose_bf16(const void* src, int64_t R, int64_t C, void* d
   return check_launch("dph_transpose_bf16");
 }
 
+namespace dph {
+namespace {
+// Batched image refresh after the optimizer step (one launch each instead of ~85 casts + ~50
+// transposes of 1-2 M elements, each a few-us launch):
+//   cast:      tab[e] = {src fp32*, dst bf16*, n}; grid (blocks, entries), grid-stride per entry
+//   transpose: tab[e] = {src bf16*, dst bf16*, R, C}; grid (blocks, entries), 64x64 tiles
+__global__ void __launch_bounds__(256) cast_bf16_multi_kernel(const int64_t* __restrict__ tab) {
+  const int64_t* e = tab + 3 * blockIdx.y;
+  const float* src = reinterpret_cast<const float*>(e[0]);
+  bf16_t* dst = reinterpret_cast<bf16_t*>(e[1]);
+  const int64_t n = e[2];
+  for (int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4; i < n; i += (int64_t)gridDim.x * 1024) {
+    if (i + 4 <= n) {
+      const float4 v = *reinterpret_cast<const float4*>(src + i);
+      *reinterpret_cast<uint2*>(dst + i) = make_uint2(pack2bf(v.x, v.y), pack2bf(v.z, v.w));
+    } else {
+      for (int64_t j = i; j < n; ++j) dst[j] = f2bf(src[j]);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) transpose_bf16_multi_kernel(const int64_t* __restrict__ tab) {
+  __shared__ uint16_t t[64][72];
+  const int64_t* e = tab + 4 * blockIdx.y;
+  const bf16_t* src = reinterpret_cast<const bf16_t*>(e[0]);
+  bf16_t* dst = reinterpret_cast<bf16_t*>(e[1]);
+  const int64_t R = e[2], C = e[3];
+  const int64_t ctiles = (C + 63) / 64, ntiles = ((R + 63) / 64) * ctiles;
+  const int tid = threadIdx.x;
+  const int c8 = (tid & 7) * 8;
+  for (int64_t tt = blockIdx.x; tt < ntiles; tt += gridDim.x) {
+    const int64_t r0 = (tt / ctiles) * 64, c0 = (tt % ctiles) * 64;
+    __syncthreads();   // previous tile's reads done
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int r = (tid >> 3) + 32 * h;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (r0 + r < R && c0 + c8 < C) v = *reinterpret_cast<const uint4*>(src + (r0 + r) * C + c0 + c8);
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        t[r][c8 + 2 * q] = (uint16_t)(w[q] & 0xffffu);
+        t[r][c8 + 2 * q + 1] = (uint16_t)(w[q] >> 16);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int c = (tid >> 3) + 32 * h;
+      if (c0 + c >= C || r0 + c8 >= R) continue;
+      uint32_t w[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) w[q] = (uint32_t)t[c8 + 2 * q][c] | ((uint32_t)t[c8 + 2 * q + 1][c] << 16);
+      *reinterpret_cast<uint4*>(dst + (c0 + c) * R + r0 + c8) = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+  }
+}
+}  // namespace
+}  // namespace dph
+
+extern "C" int dph_cast_bf16_multi(const int64_t* table, int64_t n_entries, hipStream_t stream) {
+  DPH_REQUIRE(table && n_entries > 0 && n_entries < 65536, "dph_cast_bf16_multi: bad args");
+  hipLaunchKernelGGL(dph::cast_bf16_multi_kernel, dim3(64, (unsigned)n_entries), dim3(256), 0, stream, table);
+  return check_launch("dph_cast_bf16_multi");
+}
+
+extern "C" int dph_transpose_bf16_multi(const int64_t* table, int64_t n_entries, hipStream_t stream) {
+  DPH_REQUIRE(table && n_entries > 0 && n_entries < 65536, "dph_transpose_bf16_multi: bad args");
+  hipLaunchKernelGGL(dph::transpose_bf16_multi_kernel, dim3(128, (unsigned)n_entries), dim3(256), 0, stream, table);
+  return check_launch("dph_transpose_bf16_multi");
+}
+
 extern "C" int dph_cast_bf16(const float* src, void* dst, int64_t n, hipStream_t stream) {
   DPH_REQUIRE(src && dst && n > 0, "dph_cast_bf16: bad args");
   hipLaunchKernelGGL(cast_bf16_kernel, dim3((unsigned)cdiv(cdiv(n, 4), 256)), dim3(256), 0, stream, src,

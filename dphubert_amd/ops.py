@@ -113,8 +113,58 @@ def bf16_image(*ts: torch.Tensor) -> torch.Tensor:
         n = t.numel()
         call("dph_cast_bf16", ptr(t.detach()), out.data_ptr() + off * 2, n, _s())
         off += n
+    if hit is not None:
+        _REFRESH.pop(id(hit[1]), None)
+        _T_REFRESH.pop(id(hit[1]), None)
     owner._dph_img = (key, out)
+    if all(t.requires_grad for t in ts):
+        _REFRESH[id(out)] = (owner, ts, out)
     return out
+
+
+# Images of trained weights are refreshed IN PLACE right after the optimizer step by two batched
+# launches (refresh_images, called by FusedAdamW.launch): one cast of every registered image and
+# one transpose of every registered W^T image, instead of ~85 + ~50 separate few-us launches spread
+# over the next forward / backward.  The cache keys are moved to the new parameter versions, so the
+# next bf16_image / t_image calls hit.
+_REFRESH = {}       # id(image) -> (owner, sources, image)
+_T_REFRESH = {}     # id(image) -> (image, transposed image)
+_TABLES = {}        # device tables of the batched launches, keyed by their content
+
+
+def _table(rows) -> torch.Tensor:
+    key = tuple(rows)
+    t = _TABLES.get(key)
+    if t is None:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("image refresh table changed during graph capture")
+        # kept for the life of the process: a captured graph reads the table by address
+        t = torch.tensor([v for r in rows for v in r], dtype=torch.int64).to(torch.device("cuda"), non_blocking=False)
+        _TABLES[key] = t
+    return t
+
+
+def refresh_images(updated_ids) -> None:
+    """Recast every registered image whose sources are all in ``updated_ids`` (ids of parameters
+    the optimizer just wrote), re-transpose their W^T images, and re-key both caches."""
+    ents = [e for e in _REFRESH.values() if all(id(t) in updated_ids for t in e[1])]
+    if not ents:
+        return
+    rows = []
+    for _owner, ts, out in ents:
+        off = 0
+        for t in ts:
+            rows.append((t.data_ptr(), out.data_ptr() + off * 2, t.numel()))
+            off += t.numel()
+    tab = _table(rows)
+    call("dph_cast_bf16_multi", ptr(tab), len(rows), _s())
+    for owner, ts, out in ents:
+        owner._dph_img = (("cat",) + _version_key(ts), out)
+    trows = [(img.data_ptr(), tout.data_ptr(), img.shape[0], img.shape[1])
+             for img, tout in (_T_REFRESH.get(id(e[2]), (None, None)) for e in ents) if img is not None]
+    if trows:
+        ttab = _table(trows)
+        call("dph_transpose_bf16_multi", ptr(ttab), len(trows), _s())
 
 
 def f32_cat(*ts: torch.Tensor) -> torch.Tensor:
@@ -183,6 +233,8 @@ def t_image(img: torch.Tensor) -> Optional[torch.Tensor]:
     out = torch.empty(img.shape[1], img.shape[0], dtype=BF16, device=img.device)
     call("dph_transpose_bf16", ptr(img), img.shape[0], img.shape[1], ptr(out), _s())
     img._dph_t = out
+    if id(img) in _REFRESH:
+        _T_REFRESH[id(img)] = (img, out)
     return out
 
 

@@ -141,6 +141,10 @@ class FusedAdamW(torch.optim.Optimizer):
         # the kernel wrote the masters behind autograd's back: bump their version counters so every
         # cached bf16 GEMM image of them (ops.bf16_image & co.) is rebuilt before its next use
         increment_version([p for _, p in plist])
+        # recast (and re-transpose) the bf16 GEMM images of the updated weights in two batched
+        # launches, and move their cache keys to the new versions
+        from . import ops
+        ops.refresh_images({id(p) for _, p in plist})
 
     @torch.no_grad()
     def step(self, closure=None):

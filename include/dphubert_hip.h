@@ -208,6 +208,11 @@ int dph_weight_norm_bwd(const float* dw_img, const float* g, const float* v, con
 int dph_cast_bf16(const float* src, void* dst, int64_t n, hipStream_t stream);
 /* bf16 [R][C] -> [C][R] (R, C multiples of 8): k-contiguous weight image W^T for input-gradient GEMMs */
 int dph_transpose_bf16(const void* src, int64_t R, int64_t C, void* dst, hipStream_t stream);
+/* batched refresh of the bf16 GEMM images after an optimizer step (replaces one dph_cast_bf16 /
+ * dph_transpose_bf16 launch per weight): device tables of {src fp32*, dst bf16*, n} resp.
+ * {src bf16*, dst bf16*, R, C} int64 entries (R, C multiples of 8) */
+int dph_cast_bf16_multi(const int64_t* table, int64_t n_entries, hipStream_t stream);
+int dph_transpose_bf16_multi(const int64_t* table, int64_t n_entries, hipStream_t stream);
 /* conv weight [O][C][k] fp32 -> bf16 [Op][k*Cp] (index j*Cp+c), zero for o >= O or c >= C
  * (channel counts of pruned students padded to multiples of 8) */
 int dph_conv_weight_pack(const float* w, void* dst, int64_t O, int64_t C, int64_t k, int64_t Op, int64_t Cp,
