@@ -1236,7 +1236,8 @@ static int gemm_kind(const DphGemmArgs& a, int64_t kchunk) {
   if (big_ok && a.N <= ring::Tall::BN && a.M > 128) kind = 3;
   // short K (<= 32 slices): the 8-wave 128 x 128 tile (two waves per SIMD per block overlap the
   // fixed per-tile costs; measured +10 % on the K = 768 projections, even at K = 3072)
-  else if (kind == 1 && big_ok && kchunk <= 1024) kind = 5;
+  // (also instead of the 256 x 256 tile: conv dgrad 255984x1536x512 ran 389 TF/s on it)
+  else if ((kind == 1 || kind == 2) && big_ok && kchunk <= 1024) kind = 5;
   const int path = gemm_path_override();
   if (path == 1) kind = 0;
   if (path == 2 && big_ok) kind = 2;

@@ -584,8 +584,12 @@ class FrontendFn(torch.autograd.Function):
             call("dph_conv_weight_unpack_grad", ptr(dwp), ptr(dw), O, Cin, k, Cinp, int(direct), _s())
             # input gradient columns, then col2im fused with the previous layer's GELU/mask backward
             dcols = torch.empty(M, k * Cinp, dtype=BF16, device=dev)
-            K.gemm(K.dense(dz), K.dense(ctx.imgs[i]), K.dense(dcols), M, k * Cinp, Op, a_kcontig=True,
-                   b_kcontig=False)
+            wt = t_image(ctx.imgs[i])     # [k*Cinp][Op]: both operands k-contiguous -> ring kernels
+            if wt is not None:
+                K.gemm(K.dense(dz), K.dense(wt), K.dense(dcols), M, k * Cinp, Op, a_kcontig=True, b_kcontig=True)
+            else:
+                K.gemm(K.dense(dz), K.dense(ctx.imgs[i]), K.dense(dcols), M, k * Cinp, Op, a_kcontig=True,
+                       b_kcontig=False)
             nxt = torch.empty(B * Ls[i - 1], Cinp, dtype=BF16, device=dev)
             if i > 1:
                 dmk = zeros_f32(Cinp, dev) if masks[i - 1] is not None else None
