@@ -1204,7 +1204,7 @@ using namespace dph;
 static int gemm_path_override() {
   const char* e = getenv("DPH_GEMM_PATH");
   if (!e) return 0;
-  return !strcmp(e, "small") ? 1 : !strcmp(e, "big") ? 2 : !strcmp(e, "mid") ? 3 : !strcmp(e, "tall") ? 4 : !strcmp(e, "half") ? 5 : !strcmp(e, "mid8") ? 6 : 0;
+  return !strcmp(e, "small") ? 1 : !strcmp(e, "big") ? 2 : !strcmp(e, "mid") ? 3 : !strcmp(e, "tall") ? 4 : !strcmp(e, "half") ? 5 : !strcmp(e, "mid8") ? 6 : !strcmp(e, "mid8mn") ? 7 : 0;
 }
 
 // an operand the ring kernels can stage: k-contiguous with whole 32-deep k-slices, or mn-contiguous
@@ -1224,7 +1224,7 @@ static int gemm_kind(const DphGemmArgs& a, int64_t kchunk) {
   // fragment and a barrier per 32-k slice), so by default they stay there; DPH_GEMM_PATH=mid/big
   // forces the ring (tests cover both)
   const int path0 = gemm_path_override();
-  const bool layouts = (a.a_kcontig && a.b_kcontig) || (path0 == 3 && !((!a.a_kcontig) && a.b_kcontig));
+  const bool layouts = (a.a_kcontig && a.b_kcontig) || ((path0 == 3 || path0 == 7) && !((!a.a_kcontig) && a.b_kcontig));
   const bool ring_ok = layouts && ring_operand_ok(a.a_kcontig, a.A, a.K) && ring_operand_ok(a.b_kcontig, a.B, a.K) &&
                        (a.splits == 1 || kchunk % ring::KS == 0);
   // the 256x256 tile is k-contiguous only: its 128 accumulators leave no registers for the
@@ -1245,6 +1245,7 @@ static int gemm_kind(const DphGemmArgs& a, int64_t kchunk) {
   if (path == 4 && big_ok) kind = 3;
   if (path == 5 && big_ok) kind = 4;
   if (path == 6 && big_ok) kind = 5;
+  if (path == 7 && ring_ok && !big_ok) kind = 6;     // 8-wave 128x128 tile with mn-contiguous operands
   return kind;
 }
 
@@ -1256,6 +1257,7 @@ extern "C" const char* dph_gemm_variant(const DphGemmArgs* args) {
   if (!args) return "";
   const DphGemmArgs& a = *args;
   const int kind = gemm_kind(a, gemm_kchunk(a));
+  if (kind == 6) return a.a_kcontig ? "ring::Cfg<128, 128, 64, 32>, true, false>" : "ring::Cfg<128, 128, 64, 32>, false, false>";
   if (kind == 5) return "ring::Cfg<128, 128, 64, 32>, true, true>";
   if (kind == 4) return "ring::Cfg<128, 64, 64, 32>, true, true>";
   if (kind == 3) return "ring::Cfg<256, 64, 128, 32>, true, true>";
@@ -1314,7 +1316,10 @@ extern "C" int dph_gemm(const DphGemmArgs* args, hipStream_t stream) {
   // when there are >= ~2 full rounds of tiles over the 256 CUs at one block per CU, else the
   // 128x128 tile (DPH_GEMM_PATH=small|big|mid forces a path, for tests)
   const int kind = gemm_kind(a, kchunk);
-  if (kind == 5) {
+  if (kind == 6) {
+    DPH_REQUIRE(cdiv(a.M, ring::Mid8::BM) < 65536 && a.batch * a.splits < 65536, "dph_gemm: grid too large");
+    launch_ring<ring::Mid8, true>(a, kchunk, stream);
+  } else if (kind == 5) {
     DPH_REQUIRE(cdiv(a.M, ring::Mid8::BM) < 65536 && a.batch * a.splits < 65536, "dph_gemm: grid too large");
     launch_ring<ring::Mid8, false>(a, kchunk, stream);
   } else if (kind == 4) {

@@ -9,7 +9,7 @@ pytestmark = pytest.mark.gpu
 torch.manual_seed(0)
 
 
-@pytest.fixture(autouse=True, params=["small", "mid", "big", "wide", "tall", "half", "mid8"])
+@pytest.fixture(autouse=True, params=["small", "mid", "big", "wide", "tall", "half", "mid8", "mid8mn"])
 def gemm_path(request, monkeypatch):
     """Run every test on each GEMM path: the 128x128 register-staged kernel and the 128x128 /
     256x256 / 256x64 LDS-DMA ring kernels (taken where their constraints hold: both operands

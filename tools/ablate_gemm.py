@@ -34,10 +34,16 @@ else:
     import torch
     from dphubert_amd import kernels as K
     M, N, Kd = (int(x) for x in sys.argv[2:5])
-    A = (torch.rand(M, Kd, device="cuda") * 2 - 1).to(torch.bfloat16)
-    B = (torch.rand(N, Kd, device="cuda") * 2 - 1).to(torch.bfloat16)
-    C = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-    f = lambda: K.gemm(K.dense(A), K.dense(B), K.dense(C), M, N, Kd, a_kcontig=True, b_kcontig=True)  # noqa: E731
+    ak = sys.argv[5] != "0" if len(sys.argv) > 5 else True       # operand layouts: 1 k-contiguous, 0 mn
+    bk = sys.argv[6] != "0" if len(sys.argv) > 6 else True
+    splits = int(sys.argv[7]) if len(sys.argv) > 7 else 1
+    A = (torch.rand(M, Kd, device="cuda") * 2 - 1).to(torch.bfloat16) if ak else \
+        (torch.rand(Kd, M, device="cuda") * 2 - 1).to(torch.bfloat16)
+    B = (torch.rand(N, Kd, device="cuda") * 2 - 1).to(torch.bfloat16) if bk else \
+        (torch.rand(Kd, N, device="cuda") * 2 - 1).to(torch.bfloat16)
+    C = torch.empty(M, N, device="cuda", dtype=torch.float32 if splits > 1 else torch.bfloat16)
+    f = lambda: K.gemm(K.dense(A), K.dense(B), K.dense(C), M, N, Kd, a_kcontig=ak, b_kcontig=bk,  # noqa: E731
+                       c_dtype=K.OUT_F32 if splits > 1 else K.OUT_BF16, splits=splits)
     for _ in range(3):
         f()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
