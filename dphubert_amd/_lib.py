@@ -83,6 +83,7 @@ _SIGS = {
     "dph_cast_bf16": ([vp, vp, i64, S], C.c_int),
     "dph_transpose_bf16": ([vp, i64, i64, vp, S], C.c_int),
     "dph_cast_bf16_multi": ([vp, i64, S], C.c_int),
+    "dph_conv_lengths": ([vp, vp, i64, i64, vp, vp, S], C.c_int),
     "dph_transpose_bf16_multi": ([vp, i64, S], C.c_int),
     "dph_conv_weight_pack": ([vp, vp, i64, i64, i64, i64, i64, S], C.c_int),
     "dph_conv_weight_unpack_grad": ([vp, vp, i64, i64, i64, i64, C.c_int, S], C.c_int),
@@ -105,7 +106,7 @@ _SIGS = {
 }
 
 _lib = None
-ABI_VERSION = 8     # include/dphubert_hip.h layout (3: dph_adamw_step_dev, dph_set_rng_epoch; 4: dph_event_*; 5: LN bwd / colsum workspaces)
+ABI_VERSION = 9     # include/dphubert_hip.h layout (3: dph_adamw_step_dev, dph_set_rng_epoch; 4: dph_event_*; 5: LN bwd / colsum workspaces)
 
 
 class DphError(RuntimeError):

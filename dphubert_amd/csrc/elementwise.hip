@@ -377,6 +377,43 @@ extern "C" int dph_transpose_bf16_multi(const int64_t* table, int64_t n_entries,
   return check_launch("dph_transpose_bf16_multi");
 }
 
+namespace dph {
+namespace {
+struct ConvGeom {
+  int32_t k[16], s[16];
+  int32_t n;
+};
+// frame lengths through the conv stack (components.py:179-181 per layer:
+// L = max(0, floor((L - k) / s) + 1)), all layers in one launch
+__global__ void conv_lengths_kernel(const int64_t* __restrict__ in, int64_t* __restrict__ out, int64_t n, ConvGeom g) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  int64_t L = in[i];
+  for (int l = 0; l < g.n; ++l) {
+    const int64_t d = L - g.k[l];
+    const int64_t q = d >= 0 ? d / g.s[l] : -((-d + g.s[l] - 1) / g.s[l]);   // floor division
+    L = q + 1 > 0 ? q + 1 : 0;
+  }
+  out[i] = L;
+}
+}  // namespace
+}  // namespace dph
+
+extern "C" int dph_conv_lengths(const int64_t* len_in, int64_t* len_out, int64_t n, int64_t n_layers,
+                                const int32_t* kernel_sizes, const int32_t* strides, hipStream_t stream) {
+  DPH_REQUIRE(len_in && len_out && n > 0 && n_layers > 0 && n_layers <= 16 && kernel_sizes && strides,
+              "dph_conv_lengths: bad args");
+  dph::ConvGeom g{};
+  for (int64_t l = 0; l < n_layers; ++l) {
+    DPH_REQUIRE(strides[l] > 0, "dph_conv_lengths: stride must be > 0");
+    g.k[l] = kernel_sizes[l];
+    g.s[l] = strides[l];
+  }
+  g.n = (int32_t)n_layers;
+  hipLaunchKernelGGL(dph::conv_lengths_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, stream, len_in, len_out, n, g);
+  return check_launch("dph_conv_lengths");
+}
+
 extern "C" int dph_cast_bf16(const float* src, void* dst, int64_t n, hipStream_t stream) {
   DPH_REQUIRE(src && dst && n > 0, "dph_cast_bf16: bad args");
   hipLaunchKernelGGL(cast_bf16_kernel, dim3((unsigned)cdiv(cdiv(n, 4), 256)), dim3(256), 0, stream, src,

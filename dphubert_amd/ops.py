@@ -238,6 +238,18 @@ def t_image(img: torch.Tensor) -> Optional[torch.Tensor]:
     return out
 
 
+def conv_frame_lengths(length: torch.Tensor, layers) -> torch.Tensor:
+    """components.py:179-181 over every conv layer (L = max(0, floor((L - k) / s) + 1)) in one launch."""
+    import ctypes
+    n = len(layers)
+    ks = (ctypes.c_int32 * n)(*[int(k) for _, k, _ in layers])
+    ss = (ctypes.c_int32 * n)(*[int(s_) for _, _, s_ in layers])
+    src = length.to(torch.int64).contiguous()
+    out = torch.empty_like(src)
+    call("dph_conv_lengths", ptr(src), ptr(out), src.numel(), n, ctypes.addressof(ks), ctypes.addressof(ss), _s())
+    return out
+
+
 def padded_vec(v: Optional[torch.Tensor], n_p: int) -> Optional[torch.Tensor]:
     """fp32 vector zero-padded to n_p (bias / mask of a pruned width); the same tensor if no padding."""
     if v is None or v.numel() == n_p:

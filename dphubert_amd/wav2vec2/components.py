@@ -176,9 +176,7 @@ class FeatureExtractor(Module):
         else:
             y = y.view(B, T, C)
         if length is not None:
-            for (_, k, s) in layers:
-                length = torch.div(length - k, s, rounding_mode="floor") + 1
-                length = torch.max(torch.zeros_like(length), length)
+            length = ops.conv_frame_lengths(length, layers)
         return y, length
 
     def get_num_params_and_final_out_channels(self):

@@ -212,6 +212,10 @@ int dph_transpose_bf16(const void* src, int64_t R, int64_t C, void* dst, hipStre
  * dph_transpose_bf16 launch per weight): device tables of {src fp32*, dst bf16*, n} resp.
  * {src bf16*, dst bf16*, R, C} int64 entries (R, C multiples of 8) */
 int dph_cast_bf16_multi(const int64_t* table, int64_t n_entries, hipStream_t stream);
+/* frame lengths after the conv stack (components.py:179-181, every layer in one launch);
+ * kernel_sizes / strides are HOST arrays of n_layers (<= 16) entries, read at call time */
+int dph_conv_lengths(const int64_t* len_in, int64_t* len_out, int64_t n, int64_t n_layers,
+                     const int32_t* kernel_sizes, const int32_t* strides, hipStream_t stream);
 int dph_transpose_bf16_multi(const int64_t* table, int64_t n_entries, hipStream_t stream);
 /* conv weight [O][C][k] fp32 -> bf16 [Op][k*Cp] (index j*Cp+c), zero for o >= O or c >= C
  * (channel counts of pruned students padded to multiples of 8) */

@@ -373,3 +373,18 @@ def test_conv0_gn_bwd_fp32_reference(B, S, C):
     for name, got in (("w", dw), ("gamma", dg), ("beta", db), ("mask", dm)):
         e = rel_l2(got.cpu().double(), pr[name].grad)
         assert e < 2e-3, (name, e)
+
+
+def test_conv_frame_lengths():
+    """One-launch frame lengths == the reference's per-layer floor division + clamp
+    (components.py:179-181), including lengths shorter than the receptive field."""
+    from dphubert_amd import ops
+    layers = [(512, 10, 5)] + [(512, 3, 2)] * 4 + [(512, 2, 2)] * 2
+    L = torch.tensor([0, 1, 9, 10, 399, 400, 401, 12000, 160000, 159999], dtype=torch.int64)
+    ref = L.clone()
+    for (_, k, s) in layers:
+        ref = torch.div(ref - k, s, rounding_mode="floor") + 1
+        ref = torch.max(torch.zeros_like(ref), ref)
+    got = ops.conv_frame_lengths(L.to(DEV), layers)
+    torch.cuda.synchronize()
+    assert torch.equal(got.cpu(), ref)
