@@ -84,6 +84,10 @@ _SIGS = {
     "dph_transpose_bf16": ([vp, i64, i64, vp, S], C.c_int),
     "dph_cast_bf16_multi": ([vp, i64, S], C.c_int),
     "dph_conv_lengths": ([vp, vp, i64, i64, vp, vp, S], C.c_int),
+    "dph_conv0_bwd": ([vp, i64, i64, i64, i64, i64, vp, vp, vp, S], C.c_int),
+    "dph_gelu_mask_fwd": ([vp, vp, vp, i64, i64, S], C.c_int),
+    "dph_layernorm_gelu_fwd": ([vp, C.c_int, vp, vp, vp, vp, vp, vp, vp, i64, i64, f32, S], C.c_int),
+    "dph_layernorm_bwd_x32": ([vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, vp, i64, S], C.c_int),
     "dph_transpose_bf16_multi": ([vp, i64, S], C.c_int),
     "dph_conv_weight_pack": ([vp, vp, i64, i64, i64, i64, i64, S], C.c_int),
     "dph_conv_weight_unpack_grad": ([vp, vp, i64, i64, i64, i64, C.c_int, S], C.c_int),
@@ -106,7 +110,7 @@ _SIGS = {
 }
 
 _lib = None
-ABI_VERSION = 9     # include/dphubert_hip.h layout (3: dph_adamw_step_dev, dph_set_rng_epoch; 4: dph_event_*; 5: LN bwd / colsum workspaces)
+ABI_VERSION = 10     # include/dphubert_hip.h layout (3: dph_adamw_step_dev, dph_set_rng_epoch; 4: dph_event_*; 5: LN bwd / colsum workspaces)
 
 
 class DphError(RuntimeError):

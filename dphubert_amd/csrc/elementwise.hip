@@ -414,6 +414,38 @@ extern "C" int dph_conv_lengths(const int64_t* len_in, int64_t* len_out, int64_t
   return check_launch("dph_conv_lengths");
 }
 
+namespace dph {
+namespace {
+// y = GELU(h) * mask[c] over a dense [rows][C] bf16 tensor (layer_norm-mode conv layers,
+// components.py:110-114 after the LayerNorm); 8 columns per thread
+__global__ void __launch_bounds__(256) gelu_mask_fwd_kernel(const bf16_t* __restrict__ h, const float* __restrict__ mask,
+                                                            bf16_t* __restrict__ y, int64_t rows, int64_t C) {
+  const int64_t c8n = C / 8;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows * c8n) return;
+  const int64_t c0 = (i % c8n) * 8;
+  const uint4 v = *reinterpret_cast<const uint4*>(h + i * 8);
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  uint32_t o[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float a = gelu_f(__uint_as_float(w[q] << 16)) * (mask ? mask[c0 + 2 * q] : 1.f);
+    const float b = gelu_f(__uint_as_float(w[q] & 0xffff0000u)) * (mask ? mask[c0 + 2 * q + 1] : 1.f);
+    o[q] = pack2bf(a, b);
+  }
+  *reinterpret_cast<uint4*>(y + i * 8) = make_uint4(o[0], o[1], o[2], o[3]);
+}
+}  // namespace
+}  // namespace dph
+
+extern "C" int dph_gelu_mask_fwd(const void* h, const float* mask, void* y, int64_t rows, int64_t C,
+                                 hipStream_t stream) {
+  DPH_REQUIRE(h && y && rows > 0 && C > 0 && C % 8 == 0, "dph_gelu_mask_fwd: bad args (C %% 8 == 0 required)");
+  hipLaunchKernelGGL(dph::gelu_mask_fwd_kernel, dim3((unsigned)cdiv(rows * (C / 8), 256)), dim3(256), 0, stream,
+                     reinterpret_cast<const bf16_t*>(h), mask, reinterpret_cast<bf16_t*>(y), rows, C);
+  return check_launch("dph_gelu_mask_fwd");
+}
+
 extern "C" int dph_cast_bf16(const float* src, void* dst, int64_t n, hipStream_t stream) {
   DPH_REQUIRE(src && dst && n > 0, "dph_cast_bf16: bad args");
   hipLaunchKernelGGL(cast_bf16_kernel, dim3((unsigned)cdiv(cdiv(n, 4), 256)), dim3(256), 0, stream, src,

@@ -388,6 +388,70 @@ __global__ void __launch_bounds__(256) conv0_gn_bwd_kernel(const float* __restri
   }
 }
 
+// Backward of the plain conv0 (layer_norm-mode extractors, components.py:107 conv with optional
+// bias, its LayerNorm / GELU / mask backward already applied to dz): dw[c][j] += sum_{b,t} dz*x_j,
+// dbias[c] += sum_{b,t} dz.  Same thread layout as the GN backward; one atomic per (c, tap) per block.
+template <int CPT>
+__global__ void __launch_bounds__(256) conv0_plain_bwd_kernel(const float* __restrict__ wave, Conv0 p,
+                                                              const bf16_t* __restrict__ dz, float* __restrict__ dw,
+                                                              float* __restrict__ dbias) {
+  constexpr int NA = K0 + 1;
+  __shared__ float xs[BWD_ROWS * S0 + K0];
+  __shared__ float red[256 * CPT];
+  const int64_t b = blockIdx.y;
+  const int64_t t0 = (int64_t)blockIdx.x * BWD_ROWS;
+  const int nt = (int)min<int64_t>(BWD_ROWS, p.L0 - t0);
+  stage_wave(xs, wave, p, b, t0, nt);
+  RowLayout<CPT> L(p.C);
+  const int tid = threadIdx.x;
+  const bool active = tid < L.tpr * L.rpp;
+  const int64_t c0 = active ? (int64_t)(tid % L.tpr) * CPT : 0;
+  const int r0 = active ? tid / L.tpr : 0;
+  float acc[CPT][NA];
+#pragma unroll
+  for (int i = 0; i < CPT; ++i)
+#pragma unroll
+    for (int q = 0; q < NA; ++q) acc[i][q] = 0.f;
+  const int nper = (nt + L.rpp - 1) / L.rpp;
+  const int ta = r0 * nper;
+  const int tb = min(nt, ta + nper);
+  if (active && ta < tb) {
+    const bf16_t* dzrow = dz + ((b * p.L0) + t0) * p.C + c0;
+    float x[K0];
+    win_load(x, xs, ta);
+    for (int t = ta; t < tb; ++t) {
+      float d[CPT];
+      load_dyc<CPT>(dzrow + (int64_t)t * p.C, c0, p.C, d);
+#pragma unroll
+      for (int i = 0; i < CPT; ++i) {
+#pragma unroll
+        for (int j = 0; j < K0; ++j) acc[i][j] = fmaf(d[i], x[j], acc[i][j]);
+        acc[i][K0] += d[i];
+      }
+      if (t + 1 < tb) win_advance(x, xs, t);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < NA; ++q) {
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) red[tid * CPT + i] = acc[i][q];
+    __syncthreads();
+    if (active && r0 == 0) {
+#pragma unroll
+      for (int i = 0; i < CPT; ++i) {
+        float sm = 0.f;
+        for (int r = 0; r < L.rpp; ++r) sm += red[(r * L.tpr + (tid % L.tpr)) * CPT + i];
+        const int64_t c = c0 + i;
+        if (c < p.C) {
+          if (q < K0) atomicAdd(dw + c * K0 + q, sm);
+          else if (dbias) atomicAdd(dbias + c, sm);
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // per utterance: S[j] = sum_t x_j[t], G[k][j] = sum_t x_k[t] x_j[t] (x_j[t] = wave[s0*t + j], t < L0),
 // fp64, packed: gram[b][0..9] = S, gram[b][10 + j*(j+1)/2 + k] = G[k][j] (k <= j).  Grid (chunks of
 // GRAM_ROWS time steps, B); blocks add their partial sums with fp64 atomics (gram zeroed first).
@@ -592,6 +656,21 @@ extern "C" int dph_conv0_fwd(const float* wave, int64_t B, int64_t S, const floa
                      stream, wave, w, bias, p, (const float*)nullptr, (const float*)nullptr, (const float*)nullptr,
                      (const float*)nullptr, (const float*)nullptr, reinterpret_cast<bf16_t*>(y));
   return check_launch("dph_conv0_fwd");
+}
+
+extern "C" int dph_conv0_bwd(const float* wave, int64_t B, int64_t S, int64_t C, int64_t k0, int64_t s0,
+                             const void* dz, float* dw, float* dbias, hipStream_t stream) {
+  DPH_REQUIRE(wave && dz && dw, "dph_conv0_bwd: null pointer");
+  if (k0 != K0 || s0 != S0) {
+    set_error("dph_conv0_bwd: conv0 kernel/stride (%lld,%lld) unsupported (only (10,5))", (long long)k0,
+              (long long)s0);
+    return DPH_EUNSUPPORTED;
+  }
+  DPH_REQUIRE(S >= K0 && C <= 1024, "dph_conv0_bwd: unsupported (C > 1024)");
+  Conv0 p = make_conv0(B, S, C);
+  hipLaunchKernelGGL(conv0_plain_bwd_kernel<4>, dim3((unsigned)cdiv(p.L0, BWD_ROWS), (unsigned)B), dim3(256), 0,
+                     stream, wave, p, reinterpret_cast<const bf16_t*>(dz), dw, dbias);
+  return check_launch("dph_conv0_bwd");
 }
 
 extern "C" int64_t dph_conv0_gn_bwd_workspace(int64_t B, int64_t C) {

@@ -22,6 +22,18 @@ __device__ __forceinline__ void unpack4(uint2 r, float (&o)[4]) {
   o[3] = __uint_as_float(r.y & 0xffff0000u);
 }
 
+// LayerNorm inputs are bf16, or fp32 for the layer_norm-mode conv layers (pre-LN conv outputs kept
+// in fp32: 7 stacked bf16 roundings of the pre-LN values measured 1.02e-2 hidden rel-L2 vs the fp32
+// reference, over the 1e-2 bar)
+template <typename XT> struct XRaw;
+template <> struct XRaw<bf16_t> { using T = uint2; };
+template <> struct XRaw<float> { using T = float4; };
+__device__ __forceinline__ uint2 ldx4(const bf16_t* p) { return *reinterpret_cast<const uint2*>(p); }
+__device__ __forceinline__ float4 ldx4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ void unpack4(float4 r, float (&o)[4]) {
+  o[0] = r.x; o[1] = r.y; o[2] = r.z; o[3] = r.w;
+}
+
 // per-column vector (gamma / beta / scale) for the NV 4-column chunks a lane owns; 0 past D
 template <int NV>
 __device__ __forceinline__ void load_cols(const float* __restrict__ v, int D, int lane, float fill, float (&o)[NV][4]) {
@@ -41,24 +53,27 @@ __device__ __forceinline__ void load_cols(const float* __restrict__ v, int D, in
 // Forward: one wave owns LN_FWD_RPW rows; gamma/beta live in registers, all row loads are issued
 // first (latency of the HBM reads overlaps across rows), fp32 two-pass statistics in registers.
 // Rows have stride ld >= D (ld % 4 == 0); columns [D, ld) are row padding: read as 0, written as 0.
-template <int NV>
-__global__ void __launch_bounds__(256) ln_fwd_kernel(const bf16_t* __restrict__ x, const float* __restrict__ xscale,
+// GM: also y2 = GELU(LN(x)) * gm_mask[c] from the fp32 normalised value (layer_norm-mode conv
+// layers, components.py:54-61 + :110-114); y (the bf16 LN output, kept for the GELU backward) may be NULL.
+template <int NV, bool GM = false, typename XT = bf16_t>
+__global__ void __launch_bounds__(256) ln_fwd_kernel(const XT* __restrict__ x, const float* __restrict__ xscale,
                                                      const float* __restrict__ gamma, const float* __restrict__ beta,
                                                      bf16_t* __restrict__ y, float* __restrict__ mean_out,
                                                      float* __restrict__ rstd_out, int64_t rows, int D, int ld,
-                                                     float eps, float drop_p, uint64_t seed) {
+                                                     float eps, float drop_p, uint64_t seed,
+                                                     const float* __restrict__ gm_mask = nullptr,
+                                                     bf16_t* __restrict__ y2 = nullptr) {
   seed = epoch_seed(seed);   // per-step RNG epoch (graph replays)
   const int lane = threadIdx.x & 63;
   const int64_t r0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * LN_FWD_RPW;
   if (r0 >= rows) return;
-  uint2 raw[LN_FWD_RPW][NV];
+  typename XRaw<XT>::T raw[LN_FWD_RPW][NV];
 #pragma unroll
   for (int r = 0; r < LN_FWD_RPW; ++r)
 #pragma unroll
     for (int c = 0; c < NV; ++c) {
       const int col = (c * 64 + lane) * 4;
-      raw[r][c] = (r0 + r < rows && col < D) ? *reinterpret_cast<const uint2*>(x + (r0 + r) * ld + col)
-                                              : make_uint2(0, 0);
+      raw[r][c] = (r0 + r < rows && col < D) ? ldx4(x + (r0 + r) * ld + col) : typename XRaw<XT>::T{};
     }
   float ga[NV][4], be[NV][4], xs[NV][4];
   load_cols<NV>(gamma, D, lane, 1.f, ga);
@@ -103,7 +118,13 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const bf16_t* __restrict__ 
         float o[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) o[i] = (col + i < D) ? ((v[c][i] - mean) * rstd * ga[c][i] + be[c][i]) * z[i] : 0.f;
-        *reinterpret_cast<uint2*>(y + row * ld + col) = make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
+        if (!GM || y) *reinterpret_cast<uint2*>(y + row * ld + col) = make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
+        if constexpr (GM) {
+          float g[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) g[i] = (col + i < D) ? gelu_f(o[i]) * (gm_mask ? gm_mask[col + i] : 1.f) : 0.f;
+          *reinterpret_cast<uint2*>(y2 + row * ld + col) = make_uint2(pack2bf(g[0], g[1]), pack2bf(g[2], g[3]));
+        }
       }
     }
     if (lane == 0) {
@@ -118,9 +139,9 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const bf16_t* __restrict__ 
 // across the block's waves with LDS atomics, and written as one slab row per block; slab_reduce
 // adds the columns into the outputs.  (One global atomic per column per block -- ~500 blocks onto
 // the same 2304 addresses -- measured 0.09 TB/s: same-address atomics serialise at the memory side.)
-template <int NV>
+template <int NV, typename XT = bf16_t>
 __global__ void __launch_bounds__(64 * LN_BWD_WAVES) ln_bwd_kernel(
-    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const float* __restrict__ xscale,
+    const bf16_t* __restrict__ dy, const XT* __restrict__ x, const float* __restrict__ xscale,
     const float* __restrict__ gamma, const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
     bf16_t* __restrict__ dx, float* __restrict__ dgamma, float* __restrict__ dbeta, int64_t rows, int D, int ld,
     float drop_p, uint64_t seed, bf16_t* __restrict__ branch, float branch_p, uint64_t branch_seed,
@@ -131,14 +152,15 @@ __global__ void __launch_bounds__(64 * LN_BWD_WAVES) ln_bwd_kernel(
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int64_t r0 = ((int64_t)blockIdx.x * LN_BWD_WAVES + wave) * LN_BWD_RPW;
-  uint2 rx[LN_BWD_RPW][NV], rd[LN_BWD_RPW][NV];
+  typename XRaw<XT>::T rx[LN_BWD_RPW][NV];
+  uint2 rd[LN_BWD_RPW][NV];
 #pragma unroll
   for (int r = 0; r < LN_BWD_RPW; ++r)
 #pragma unroll
     for (int c = 0; c < NV; ++c) {
       const int col = (c * 64 + lane) * 4;
       const bool ok = r0 + r < rows && col < D;
-      rx[r][c] = ok ? *reinterpret_cast<const uint2*>(x + (r0 + r) * ld + col) : make_uint2(0, 0);
+      rx[r][c] = ok ? ldx4(x + (r0 + r) * ld + col) : typename XRaw<XT>::T{};
       rd[r][c] = ok ? *reinterpret_cast<const uint2*>(dy + (r0 + r) * ld + col) : make_uint2(0, 0);
     }
   float ga[NV][4], xs[NV][4];
@@ -390,6 +412,33 @@ extern "C" int dph_layernorm_fwd_ld(const void* x, const float* xscale, const fl
   return check_launch("dph_layernorm_fwd");
 }
 
+extern "C" int dph_layernorm_gelu_fwd(const void* x, int x_f32, const float* gamma, const float* beta, void* h,
+                                      const float* mask, void* y, float* mean, float* rstd, int64_t rows, int64_t D,
+                                      float eps, hipStream_t stream) {
+  DPH_REQUIRE(x && gamma && beta && y && mean && rstd, "dph_layernorm_gelu_fwd: null pointer");
+  DPH_REQUIRE(D >= 1 && D % 4 == 0 && D <= LN_MAXV * 256 && rows > 0, "dph_layernorm_gelu_fwd: unsupported D=%lld",
+              (long long)D);
+  const dim3 grid((unsigned)cdiv(rows, 4 * LN_FWD_RPW));
+#define LNG_LAUNCH(NV)                                                                                           \
+  if (x_f32)                                                                                                     \
+    hipLaunchKernelGGL((ln_fwd_kernel<NV, true, float>), grid, dim3(256), 0, stream,                              \
+                       reinterpret_cast<const float*>(x), (const float*)nullptr, gamma, beta,                      \
+                       reinterpret_cast<bf16_t*>(h), mean, rstd, rows, (int)D, (int)D, eps, 0.f, (uint64_t)0, mask, \
+                       reinterpret_cast<bf16_t*>(y));                                                             \
+  else                                                                                                           \
+    hipLaunchKernelGGL((ln_fwd_kernel<NV, true>), grid, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(x), \
+                       (const float*)nullptr, gamma, beta, reinterpret_cast<bf16_t*>(h), mean, rstd, rows, (int)D, \
+                       (int)D, eps, 0.f, (uint64_t)0, mask, reinterpret_cast<bf16_t*>(y))
+  switch (cdiv(D, 256)) {
+    case 1: LNG_LAUNCH(1); break;
+    case 2: LNG_LAUNCH(2); break;
+    case 3: LNG_LAUNCH(3); break;
+    default: LNG_LAUNCH(4); break;
+  }
+#undef LNG_LAUNCH
+  return check_launch("dph_layernorm_gelu_fwd");
+}
+
 extern "C" int dph_layernorm_fwd(const void* x, const float* xscale, const float* gamma, const float* beta, void* y,
                                  float* mean, float* rstd, int64_t rows, int64_t D, float eps, float dropout_p,
                                  uint64_t seed, hipStream_t stream) {
@@ -437,6 +486,38 @@ extern "C" int dph_layernorm_bwd_ld(const void* dy, const void* x, const float* 
                        0, stream, ws, nblk, 3 * D, D, dgamma, dbeta, branch_colsum);
   }
   return check_launch("dph_layernorm_bwd");
+}
+
+extern "C" int dph_layernorm_bwd_x32(const void* dy, const float* x, const float* gamma, const float* mean,
+                                     const float* rstd, void* dx, float* dgamma, float* dbeta, int64_t rows, int64_t D,
+                                     float* ws, int64_t ws_bytes, hipStream_t stream) {
+  DPH_REQUIRE(dy && x && gamma && mean && rstd && dx, "dph_layernorm_bwd_x32: null pointer");
+  DPH_REQUIRE(D >= 1 && D % 4 == 0 && D <= LN_MAXV * 256 && rows > 0, "dph_layernorm_bwd_x32: unsupported D=%lld",
+              (long long)D);
+  const bool sums = dgamma || dbeta;
+  DPH_REQUIRE(!sums || (ws && ws_bytes >= dph_layernorm_bwd_workspace(rows, D)),
+              "dph_layernorm_bwd_x32: workspace too small (%lld < %lld bytes)", (long long)ws_bytes,
+              (long long)dph_layernorm_bwd_workspace(rows, D));
+  const dim3 grid((unsigned)cdiv(rows, LN_BWD_WAVES * LN_BWD_RPW));
+#define LN_BWD32_LAUNCH(NV)                                                                                      \
+  hipLaunchKernelGGL((ln_bwd_kernel<NV, float>), grid, dim3(64 * LN_BWD_WAVES), 0, stream,                       \
+                     reinterpret_cast<const bf16_t*>(dy), x, (const float*)nullptr, gamma, mean, rstd,           \
+                     reinterpret_cast<bf16_t*>(dx), dgamma, dbeta, rows, (int)D, (int)D, 0.f, (uint64_t)0,        \
+                     (bf16_t*)nullptr, 0.f, (uint64_t)0, (const float*)nullptr, (float*)nullptr,                  \
+                     (const bf16_t*)nullptr, (float*)nullptr, (const bf16_t*)nullptr, ws)
+  switch (cdiv(D, 256)) {
+    case 1: LN_BWD32_LAUNCH(1); break;
+    case 2: LN_BWD32_LAUNCH(2); break;
+    case 3: LN_BWD32_LAUNCH(3); break;
+    default: LN_BWD32_LAUNCH(4); break;
+  }
+#undef LN_BWD32_LAUNCH
+  if (sums) {
+    const int64_t nblk = grid.x;
+    hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)cdiv(3 * D, 64), (unsigned)slab_groups(nblk)), dim3(256),
+                       0, stream, ws, nblk, 3 * D, D, dgamma, dbeta, (float*)nullptr);
+  }
+  return check_launch("dph_layernorm_bwd_x32");
 }
 
 extern "C" int dph_wave_layernorm(const float* x, const int64_t* lengths, int64_t B, int64_t S, float eps, float* y,

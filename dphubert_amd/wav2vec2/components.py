@@ -135,10 +135,16 @@ class FeatureExtractor(Module):
         self.dummy_weight = nn.Parameter(torch.ones(conv_layers[-1].conv.out_channels, dtype=torch.float32),
                                          requires_grad=False)
 
+    def _ln_mode(self) -> bool:
+        """layer_norm-mode extractor (every conv layer carries a LayerNorm over channels)."""
+        return all(isinstance(l.layer_norm, LayerNorm) for l in self.conv_layers)
+
     def _check_supported(self):
+        if self._ln_mode():
+            return
         l0 = self.conv_layers[0]
         if not isinstance(l0.layer_norm, nn.GroupNorm):
-            raise NotImplementedError("layer_norm-mode extractor (Large) is not on the HIP path yet")
+            raise NotImplementedError("mixed extractor normalisation is not on the HIP path")
         for layer in self.conv_layers:
             if layer.conv.bias is not None:
                 raise NotImplementedError("conv bias (Large extractor) is not on the HIP path yet")
@@ -160,10 +166,15 @@ class FeatureExtractor(Module):
         need = torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
         cfg = ops.FrontendCfg(layers, B, S, need)
         flat = []
-        for l, m in zip(self.conv_layers, masks):
-            flat += [l.conv.weight, m]
-        y = ops.FrontendFn.apply(cfg, x.contiguous().float(), self.dummy_weight, l0.layer_norm.weight,
-                                 l0.layer_norm.bias, *flat)
+        if self._ln_mode():
+            for l, m in zip(self.conv_layers, masks):
+                flat += [l.conv.weight, l.conv.bias, l.layer_norm.weight, l.layer_norm.bias, m]
+            y = ops.FrontendLNFn.apply(cfg, x.contiguous().float(), self.dummy_weight, *flat)
+        else:
+            for l, m in zip(self.conv_layers, masks):
+                flat += [l.conv.weight, m]
+            y = ops.FrontendFn.apply(cfg, x.contiguous().float(), self.dummy_weight, l0.layer_norm.weight,
+                                     l0.layer_norm.bias, *flat)
         T = ops.conv_lengths(S, layers)[-1]
         C = layers[-1][0]
         Cp = ops.pad8(C)

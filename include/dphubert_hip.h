@@ -105,6 +105,16 @@ const char* dph_gemm_variant(const DphGemmArgs* args);
 int dph_layernorm_fwd(const void* x, const float* xscale, const float* gamma, const float* beta, void* y,
                       float* mean, float* rstd, int64_t rows, int64_t D, float eps, float dropout_p,
                       uint64_t seed, hipStream_t stream);
+/* fused LayerNorm + exact GELU + channel mask (layer_norm-mode conv layers, components.py:54-61,
+ * :110-114): y = GELU(LN(x)) * mask[c] computed from the fp32 LN value; h (may be NULL) receives
+ * the bf16 LN output for the GELU backward; x is bf16, or fp32 when x_f32.  D % 4 == 0. */
+int dph_layernorm_gelu_fwd(const void* x, int x_f32, const float* gamma, const float* beta, void* h, const float* mask,
+                           void* y, float* mean, float* rstd, int64_t rows, int64_t D, float eps, hipStream_t stream);
+/* LN backward with an fp32 input x (the fp32 pre-LN conv outputs of layer_norm-mode extractors);
+ * dy / dx bf16, dgamma / dbeta accumulate */
+int dph_layernorm_bwd_x32(const void* dy, const float* x, const float* gamma, const float* mean, const float* rstd,
+                          void* dx, float* dgamma, float* dbeta, int64_t rows, int64_t D, float* ws, int64_t ws_bytes,
+                          hipStream_t stream);
 /* dx = LN backward; dgamma/dbeta accumulate (atomics).  Optional branch output
  * (residual sub-branch gradient): branch = dx * drop(branch_p, branch_seed) * (*branch_smask),
  * branch_colsum += column sums of branch, branch_sdot += sum(dx*drop*branch_pre).
@@ -177,6 +187,14 @@ int dph_conv0_gn_bwd(const float* wave, int64_t B, int64_t S, const float* w, in
 /* plain conv0 (no norm, used by layer_norm-mode extractors): y[b][t][c] = sum_j w[c][j]*x[b][s0*t+j] (+bias) */
 int dph_conv0_fwd(const float* wave, int64_t B, int64_t S, const float* w, const float* bias, int64_t C,
                   int64_t k0, int64_t s0, void* y, hipStream_t stream);
+
+/* its backward (dz = gradient of the conv0 output, LN/GELU/mask backward already applied):
+ * dw[c][j] += sum dz[b][t][c] * x[b][s0*t+j], dbias[c] += sum dz (dbias may be NULL); accumulates */
+int dph_conv0_bwd(const float* wave, int64_t B, int64_t S, int64_t C, int64_t k0, int64_t s0, const void* dz,
+                  float* dw, float* dbias, hipStream_t stream);
+/* y = GELU(h) * mask[c] on a dense bf16 [rows][C] tensor (C % 8 == 0; mask may be NULL):
+ * layer_norm-mode conv layers after their LayerNorm (components.py:110-114) */
+int dph_gelu_mask_fwd(const void* h, const float* mask, void* y, int64_t rows, int64_t C, hipStream_t stream);
 
 /* Fused col2im + GELU/mask backward for a strided conv layer (k, s):
  * dy_in[b][t'][c] = sum_{t,j: s*t+j==t'} dcols[b][t][j*C+c]; then, if z_pre != NULL,

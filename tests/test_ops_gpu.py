@@ -153,6 +153,36 @@ def test_frontend_vs_oracle():
         assert e < 6e-2, (key, e)
 
 
+@pytest.mark.parametrize("conv_bias", [True, False])
+def test_frontend_layer_norm_mode_vs_oracle(conv_bias):
+    """layer_norm-mode extractor (HuBERT-Large: no conv bias; wav2vec2-Large-LV60: conv bias):
+    conv (+bias) -> LayerNorm over channels -> GELU -> mask on every layer, fwd + bwd vs the oracle."""
+    cfg = _cfg(1, extractor_mode="layer_norm", extractor_conv_bias=conv_bias, extractor_prune_conv_channels=True)
+    m, sd = _model(cfg, seed=2)
+    fe = m.feature_extractor.train()
+    g = torch.Generator().manual_seed(9)
+    wave = 0.1 * torch.randn(2, 8000, generator=g)
+    us = {f"feature_extractor.conv_layers.{i}.hard_concrete": torch.rand(512, generator=g) * 0.98 + 0.01
+          for i in range(7)}
+    for i, l in enumerate(fe.conv_layers):
+        l.hard_concrete.set_noise(us[f"feature_extractor.conv_layers.{i}.hard_concrete"])
+    y, _ = fe(wave.to(DEV), None)
+    gy = torch.randn(y.shape, generator=g).to(torch.bfloat16)
+    y.backward(gy.to(DEV))
+    psd = {k: v.clone().requires_grad_(True) for k, v in sd.items() if k.startswith("feature_extractor")}
+    psd["feature_extractor.dummy_weight"] = sd["feature_extractor.dummy_weight"]
+    masks = {n: ref.hc_sample(psd[n + ".log_alpha"], u) for n, u in us.items()}
+    yr, _ = ref.feature_extractor(psd, cfg, wave, None, masks)
+    yr.backward(gy.float())
+    assert rel_l2(y.float().cpu(), yr.detach()) < 2e-2
+    for n, p in fe.named_parameters():
+        if not p.requires_grad:
+            continue
+        key = "feature_extractor." + n
+        e = rel_l2(p.grad.cpu(), psd[key].grad)
+        assert e < 6e-2, (key, e)
+
+
 def test_encoder_layer_vs_oracle():
     cfg = _cfg(1, encoder_prune_attention_heads=True, encoder_prune_attention_layer=True,
                encoder_prune_feed_forward_intermediate=True, encoder_prune_feed_forward_layer=True)

@@ -152,3 +152,13 @@ def test_prenorm_normalize_waveform_g6():
     _check_step(fx, out)
     for h, g in zip(out["student_hiddens"], fx["student_hiddens"]):
         assert rel_l2(h, g) < 1e-5
+
+
+def test_layer_norm_extractor_g7():
+    """layer_norm-mode extractor with conv bias (LayerNorm over channels after every conv) + pre-norm
+    layers: the oracle restatement against the reference's own step on the same inputs."""
+    fx = load_golden("g7_lnext.pt")
+    out = _run_fixture(fx)
+    _check_step(fx, out)
+    for h, g in zip(out["student_hiddens"], fx["student_hiddens"]):
+        assert rel_l2(h, g) < 1e-5

@@ -333,9 +333,21 @@ def gen_prenorm():
                     lambdas=(0.2, 0.1), global_step=2500, lengths=[24000, 18000], full=True)
 
 
+def gen_lnext():
+    """G7: layer_norm-mode extractor with conv bias (wav2vec2-Large-LV60 / HuBERT-Large family:
+    LayerNorm over channels after every conv) + pre-norm layers, 2-layer shape, padded batch."""
+    cfg = small_cfg(2, extractor_mode="layer_norm", extractor_conv_bias=True, encoder_layer_norm_first=True)
+    return run_step(cfg, cfg, "0.1,2", B=2, S=24000, units="conv,head,interm", lambdas=(0.2, 0.1),
+                    global_step=2500, lengths=[24000, 19000], full=True)
+
+
 def main():
     OUT.mkdir(parents=True, exist_ok=True)
     torch.set_num_threads(8)
+    if "--only-lnext" in sys.argv:
+        torch.save(gen_lnext(), OUT / "g7_lnext.pt")
+        print("g7 done")
+        return
     if "--only-data" in sys.argv:
         torch.save(gen_data(), OUT / "g5_data.pt")
         print("g5 done")
