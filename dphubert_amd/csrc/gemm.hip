@@ -62,11 +62,12 @@ __device__ __forceinline__ int64_t z_addr(const DphMat& d, int64_t z) {
 __device__ __forceinline__ int swz(int k) { return (k & 3) | (((k >> 3) & 1) << 2); }
 
 // ---- staging: global -> registers ----------------------------------------
-template <bool KC>
+template <bool KC, int NT = NTHREADS>
 struct Stager {
+  static constexpr int CH = (128 * BK / 8) / NT;   // 16-B chunks per thread per operand tile
   const bf16_t* base;   // operand base incl. batch offset
-  int64_t roff[CHUNKS];  // k-contig: per-chunk row offsets (fixed per block)
-  bool rvalid[CHUNKS];
+  int64_t roff[CH];  // k-contig: per-chunk row offsets (fixed per block)
+  bool rvalid[CH];
   int64_t r0;           // first row/col of the tile (M or N index)
   int64_t R;            // rows (M or N)
   DphMat d;
@@ -78,8 +79,8 @@ struct Stager {
     R = Rn;
     if constexpr (KC) {
 #pragma unroll
-      for (int i = 0; i < CHUNKS; ++i) {
-        int c = tid + NTHREADS * i;
+      for (int i = 0; i < CH; ++i) {
+        int c = tid + NT * i;
         int64_t r = tile0 + (c >> 3);
         rvalid[i] = r < Rn;
         roff[i] = row_addr(dm, rvalid[i] ? r : Rn - 1);
@@ -89,10 +90,10 @@ struct Stager {
 
   // Loads are unconditional (addresses clamped into the operand) so hipcc can keep several
   // tiles in flight with counted vmcnt; out-of-range chunks are zeroed at store time.
-  __device__ __forceinline__ void load(uint4 (&reg)[CHUNKS], int64_t k0, int64_t kend, int tid) const {
+  __device__ __forceinline__ void load(uint4 (&reg)[CH], int64_t k0, int64_t kend, int tid) const {
 #pragma unroll
-    for (int i = 0; i < CHUNKS; ++i) {
-      int c = tid + NTHREADS * i;
+    for (int i = 0; i < CH; ++i) {
+      int c = tid + NT * i;
       if constexpr (KC) {
         int64_t k = min(k0 + (c & 7) * 8, kend - 8);
         reg[i] = *reinterpret_cast<const uint4*>(base + roff[i] + k);
@@ -104,10 +105,10 @@ struct Stager {
     }
   }
 
-  __device__ __forceinline__ void store(char* lds, const uint4 (&reg)[CHUNKS], int64_t k0, int64_t kend, int tid) const {
+  __device__ __forceinline__ void store(char* lds, const uint4 (&reg)[CH], int64_t k0, int64_t kend, int tid) const {
 #pragma unroll
-    for (int i = 0; i < CHUNKS; ++i) {
-      int c = tid + NTHREADS * i;
+    for (int i = 0; i < CH; ++i) {
+      int c = tid + NT * i;
       int byte;
       bool ok;
       if constexpr (KC) {
@@ -443,8 +444,8 @@ __device__ __forceinline__ void tile_epi(const DphGemmArgs& a, int64_t z, int64_
 constexpr int CROW = BN + 4;                       // padded fp32 row
 constexpr int LDS_C = BM * CROW * 4;               // 67,584 B
 
-template <bool AK, bool BKc>
-__global__ void __launch_bounds__(NTHREADS, 2) gemm_kernel(const DphGemmArgs a, int64_t kchunk) {
+template <bool AK, bool BKc, int NT = NTHREADS>
+__global__ void __launch_bounds__(NT, 2) gemm_kernel(const DphGemmArgs a, int64_t kchunk) {
   constexpr int PIPE = 2 * (TileBytes<AK>::v + TileBytes<BKc>::v);
   __shared__ __attribute__((aligned(16))) char smem[PIPE > LDS_C ? PIPE : LDS_C];
   char* const ldsA0 = smem;
@@ -455,8 +456,13 @@ __global__ void __launch_bounds__(NTHREADS, 2) gemm_kernel(const DphGemmArgs a, 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const int wm = wave >> 1;   // 0..1 -> rows wm*64 .. +64
-  const int wn = wave & 1;    // 0..1 -> cols wn*64 .. +64
+  // NT = 256: 4 waves 2 (M) x 2 (N) of 64x64; NT = 512: 8 waves 2 x 4 of 64x32 (two waves per SIMD
+  // per block: one wave's fragment reads / barrier wait overlap the other's MFMAs)
+  constexpr int NWN = NT / 128;            // waves along N
+  constexpr int KWTN = BN / NWN;           // wave tile width
+  constexpr int KNJ = KWTN / 16;
+  const int wm = wave / NWN;
+  const int wn = wave % NWN;
 
   const int64_t zz = blockIdx.z;
   const int64_t split = zz % a.splits;
@@ -487,22 +493,22 @@ __global__ void __launch_bounds__(NTHREADS, 2) gemm_kernel(const DphGemmArgs a, 
   const int64_t kbeg = split * kchunk;
   const int64_t kend = min(a.K, kbeg + kchunk);
 
-  Stager<AK> sa;
-  Stager<BKc> sb;
+  Stager<AK, NT> sa;
+  Stager<BKc, NT> sb;
   sa.init(a.A, reinterpret_cast<const bf16_t*>(a.A.ptr) + z_addr(a.A, z), m0, a.M, tid);
   sb.init(a.B, reinterpret_cast<const bf16_t*>(a.B.ptr) + z_addr(a.B, z), n0, a.N, tid);
 
-  f32x4_t acc[4][NJ];
+  f32x4_t acc[4][KNJ];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < KNJ; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   // Pipeline: LDS double buffer + one register stage.  Tile t+1 is issued into registers at the
   // top of step t (unconditional loads: counted vmcnt), tile t is computed from LDS, then tile
   // t+1 is written to the other LDS buffer behind one barrier.  Two co-resident blocks per CU
   // (73 KB LDS, <=256 VGPR) overlap each other's load latency.
-  uint4 ra[CHUNKS], rb[CHUNKS];
+  uint4 ra[Stager<AK, NT>::CH], rb[Stager<BKc, NT>::CH];
   const int nk = (int)cdiv(max<int64_t>(kend - kbeg, 0), BK);
   auto kof = [&](int t) { return kbeg + (int64_t)t * BK; };
   if (nk > 0) {
@@ -523,15 +529,15 @@ __global__ void __launch_bounds__(NTHREADS, 2) gemm_kernel(const DphGemmArgs a, 
     const char* LB = LDSB(cur);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      bf16x8_t af[4], bfr[NJ];
+      bf16x8_t af[4], bfr[KNJ];
 #pragma unroll
       for (int i = 0; i < 4; ++i) af[i] = frag<AK>(LA, wm * 64 + 16 * i, ks, lane);
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) bfr[j] = frag<BKc>(LB, wn * WTN + 16 * j, ks, lane);
+      for (int j = 0; j < KNJ; ++j) bfr[j] = frag<BKc>(LB, wn * KWTN + 16 * j, ks, lane);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < NJ; ++j)
+        for (int j = 0; j < KNJ; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
     }
     if (more) {
@@ -549,8 +555,8 @@ __global__ void __launch_bounds__(NTHREADS, 2) gemm_kernel(const DphGemmArgs a, 
   for (int i = 0; i < 4; ++i) {
     const int r = wm * 64 + 16 * i + (lane & 15);
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int c = wn * WTN + 16 * j + 4 * (lane >> 4);
+    for (int j = 0; j < KNJ; ++j) {
+      const int c = wn * KWTN + 16 * j + 4 * (lane >> 4);
       *reinterpret_cast<float4*>(ct + r * CROW + c) = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2],
                                                                    acc[i][j][3]);
     }
@@ -562,8 +568,8 @@ __global__ void __launch_bounds__(NTHREADS, 2) gemm_kernel(const DphGemmArgs a, 
   if (a.splits > 1) {
     float* ws = reinterpret_cast<float*>(a.workspace) + (zz * a.M) * a.N;
 #pragma unroll 2
-    for (int p = 0; p < BM * BN / 8 / NTHREADS; ++p) {
-      const int r = r0 + (NTHREADS / 16) * p;
+    for (int p = 0; p < BM * BN / 8 / NT; ++p) {
+      const int r = r0 + (NT / 16) * p;
       const int64_t m = m0 + r;
       const int64_t n = n0 + c8;
       if (m >= a.M || n >= a.N) continue;
@@ -585,11 +591,11 @@ __global__ void __launch_bounds__(NTHREADS, 2) gemm_kernel(const DphGemmArgs a, 
     csa[q] = 0.f;
   }
   if (tile_epi_ok(a, n0 + c8)) {
-    tile_epi<BM * BN / 8 / NTHREADS, NTHREADS / 16>(a, z, m0 + r0, n0 + c8, ct + r0 * CROW + c8, CROW, cso, csa);
+    tile_epi<BM * BN / 8 / NT, NT / 16>(a, z, m0 + r0, n0 + c8, ct + r0 * CROW + c8, CROW, cso, csa);
   } else {
 #pragma unroll 1
-  for (int p = 0; p < BM * BN / 8 / NTHREADS; ++p) {
-    const int r = r0 + (NTHREADS / 16) * p;
+  for (int p = 0; p < BM * BN / 8 / NT; ++p) {
+    const int r = r0 + (NT / 16) * p;
     const float* src = ct + r * CROW + c8;
     float v[8];
     const float4 x0 = *reinterpret_cast<const float4*>(src);
@@ -616,7 +622,7 @@ __global__ void __launch_bounds__(NTHREADS, 2) gemm_kernel(const DphGemmArgs a, 
     }
     __syncthreads();
     float* red = reinterpret_cast<float*>(smem);   // [waves][2][128]
-    if (lane < 16) {
+    if (lane < 16) {   // (NT / 16 rows per pass: lanes l, l^16, ... share columns)
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         red[(wave * 2 + 0) * 128 + c8 + q] = cso[q];
@@ -631,7 +637,7 @@ __global__ void __launch_bounds__(NTHREADS, 2) gemm_kernel(const DphGemmArgs a, 
         const int64_t csn = a.colsum_n > 0 ? a.colsum_n : a.N;
         float so = 0.f, sx = 0.f;
 #pragma unroll
-        for (int w = 0; w < NTHREADS / 64; ++w) {
+        for (int w = 0; w < NT / 64; ++w) {
           so += red[(w * 2 + 0) * 128 + tid];
           sx += red[(w * 2 + 1) * 128 + tid];
         }
@@ -1199,6 +1205,19 @@ __global__ void splitk_reduce_kernel(const DphGemmArgs a) {
 
 using namespace dph;
 
+// register-staged kernel width: 512 threads (8 waves of 64x32) for K chunks <= 8192, where the
+// second wave per SIMD hides the per-k-step fragment reads and barrier (wgrad shapes +1-3 %, a
+// (k, mn) 7984x3072x768 +14 %); 256 (4 waves of 64x64) for the long-K conv weight gradients (-3 %
+// with 8 waves).  DPH_GEMM_SMALL_NT=256|512 forces one.
+static int small_nt(int64_t kchunk) {
+  static const int v = [] {
+    const char* e = getenv("DPH_GEMM_SMALL_NT");
+    return e ? atoi(e) : 0;
+  }();
+  if (v == 256 || v == 512) return v;
+  return kchunk <= 8192 ? 512 : 256;
+}
+
 // DPH_GEMM_PATH: unset/auto = size-based choice, "small" = 128x128 kernel only, "big" = large-tile
 // kernel wherever its layout constraints allow (tests exercise both paths in one process)
 static int gemm_path_override() {
@@ -1267,10 +1286,11 @@ extern "C" const char* dph_gemm_variant(const DphGemmArgs* args) {
     if (a.a_kcontig) return "ring::Cfg<128, 128, 64, 64>, true, false>";
     return "ring::Cfg<128, 128, 64, 64>, false, false>";
   }
-  if (a.a_kcontig && a.b_kcontig) return "gemm_kernel<true, true>";
-  if (a.a_kcontig) return "gemm_kernel<true, false>";
-  if (a.b_kcontig) return "gemm_kernel<false, true>";
-  return "gemm_kernel<false, false>";
+  const bool w8 = small_nt(gemm_kchunk(a)) == 512;
+  if (a.a_kcontig && a.b_kcontig) return w8 ? "gemm_kernel<true, true, 512>" : "gemm_kernel<true, true>";
+  if (a.a_kcontig) return w8 ? "gemm_kernel<true, false, 512>" : "gemm_kernel<true, false>";
+  if (a.b_kcontig) return w8 ? "gemm_kernel<false, true, 512>" : "gemm_kernel<false, true>";
+  return w8 ? "gemm_kernel<false, false, 512>" : "gemm_kernel<false, false>";
 }
 
 template <class Cf, bool MN>
@@ -1338,6 +1358,16 @@ extern "C" int dph_gemm(const DphGemmArgs* args, hipStream_t stream) {
   } else {
   dim3 grid((unsigned)cdiv(a.N, BN), (unsigned)cdiv(a.M, BM), (unsigned)(a.batch * a.splits));
   DPH_REQUIRE(grid.y < 65536 && grid.z < 65536, "dph_gemm: grid too large");
+  if (small_nt(kchunk) == 512) {
+    if (a.a_kcontig && a.b_kcontig)
+      hipLaunchKernelGGL((gemm_kernel<true, true, 512>), grid, dim3(512), 0, stream, a, kchunk);
+    else if (a.a_kcontig && !a.b_kcontig)
+      hipLaunchKernelGGL((gemm_kernel<true, false, 512>), grid, dim3(512), 0, stream, a, kchunk);
+    else if (!a.a_kcontig && a.b_kcontig)
+      hipLaunchKernelGGL((gemm_kernel<false, true, 512>), grid, dim3(512), 0, stream, a, kchunk);
+    else
+      hipLaunchKernelGGL((gemm_kernel<false, false, 512>), grid, dim3(512), 0, stream, a, kchunk);
+  } else {
   if (a.a_kcontig && a.b_kcontig)
     hipLaunchKernelGGL((gemm_kernel<true, true>), grid, dim3(NTHREADS), 0, stream, a, kchunk);
   else if (a.a_kcontig && !a.b_kcontig)
@@ -1346,6 +1376,7 @@ extern "C" int dph_gemm(const DphGemmArgs* args, hipStream_t stream) {
     hipLaunchKernelGGL((gemm_kernel<false, true>), grid, dim3(NTHREADS), 0, stream, a, kchunk);
   else
     hipLaunchKernelGGL((gemm_kernel<false, false>), grid, dim3(NTHREADS), 0, stream, a, kchunk);
+  }
   }
   int rc = check_launch("dph_gemm");
   if (rc) return rc;
