@@ -219,6 +219,9 @@ def padded_image(w: torch.Tensor, rows_p: int, cols_p: int) -> torch.Tensor:
 # input-gradient GEMMs take the transposed weight image (k-contiguous B: ring kernels); DPH_DGRAD_T=0
 # keeps the mn-contiguous B operand (register-staged kernel) for A/B timing
 _DGRAD_T = os.environ.get("DPH_DGRAD_T", "1") != "0"
+# strided-conv input gradients by output phase (no column gradient / col2im); DPH_PHASE_DGRAD=0 keeps
+# the column path (A/B timing, tests of both)
+_PHASE_DGRAD = os.environ.get("DPH_PHASE_DGRAD", "1") != "0"
 
 
 def t_image(img: torch.Tensor) -> Optional[torch.Tensor]:
@@ -486,6 +489,53 @@ def conv_lengths(S: int, layers) -> List[int]:
     return out
 
 
+def conv_dgrad_phases(dz: torch.Tensor, wt: torch.Tensor, B: int, Lout: int, Lin: int, O: int, Cin: int, k: int,
+                      s: int, z_pre: Optional[torch.Tensor] = None, cm: Optional[torch.Tensor] = None,
+                      dmask: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+    """Input gradient of a strided conv layer WITHOUT the [B*Lout][k*Cin] column gradient and its
+    col2im pass: d_in[b][t'] = sum_{s*t + j = t'} dz[b][t] @ W_j, split by output phase (t' even /
+    odd) into GEMMs that write d_in rows in place (components.py:107 conv backward).  With z_pre
+    the previous layer's GELU'/mask backward runs in the GEMM epilogue (out = d*mask*GELU'(z_pre),
+    dmask += d*GELU(z_pre)).  s = 2 and k in (2, 3) (every wav2vec2 / HuBERT conv1-6); returns None
+    for other geometries (caller keeps the column path).  wt: transposed conv image [k*Cin][O]."""
+    if s != 2 or k not in (2, 3) or Lout < 1 or Lin < 2 * Lout + k - 2:
+        return None
+    dev = dz.device
+    d = torch.empty(B * Lin, Cin, dtype=BF16, device=dev)
+    zflat = z_pre.view(-1) if z_pre is not None else None
+
+    def gemm(A, Bm, coff, c_rpb, M, N, Kd, colmask=None, caux=None):
+        kw = {}
+        if z_pre is not None:
+            kw = dict(act=K.ACT_GELU_BWD, aux_in=zflat[coff:], colmask=colmask, colsum_aux=caux)
+        K.gemm(A, Bm, K.mat(d, 2 * Cin if c_rpb > 1 else Cin, rows_per_batch=c_rpb, batch_stride=Lin * Cin,
+                            offset=coff), M, N, Kd, a_kcontig=True, b_kcontig=True, **kw)
+
+    if k == 2:
+        # t' = 2t + j: one GEMM over both taps, N = 2*Cin (the [W_0^T; W_1^T] rows of wt)
+        cm2 = torch.cat([cm, cm]) if (z_pre is not None and cm is not None) else None
+        dm2 = zeros_f32(2 * Cin, dev) if (z_pre is not None and dmask is not None) else None
+        gemm(K.mat(dz, O), K.dense(wt), 0, Lout, B * Lout, 2 * Cin, O, cm2, dm2)
+        if dm2 is not None:
+            dmask += dm2[:Cin] + dm2[Cin:]
+        if Lin > 2 * Lout:
+            d.view(B, Lin, Cin)[:, 2 * Lout:].zero_()
+        return d
+    # k == 3: odd rows 2m+1 <- dz[m] W_1; interior even rows 2m (1 <= m < Lout) <- [dz[m-1], dz[m]] @
+    # [W_2; W_0] (K = 2*O over two consecutive dz rows); edge rows 0 <- dz[0] W_0, 2*Lout <- dz[Lout-1] W_2
+    gemm(K.mat(dz, O), K.mat(wt, O, offset=Cin * O), Cin, Lout, B * Lout, Cin, O, cm, dmask)
+    if Lout > 1:
+        weven = torch.cat([wt[2 * Cin:3 * Cin], wt[:Cin]], dim=1)
+        gemm(K.mat(dz, O, rows_per_batch=Lout - 1, batch_stride=Lout * O), K.dense(weven), 2 * Cin, Lout - 1,
+             B * (Lout - 1), Cin, 2 * O, cm, dmask)
+    gemm(K.mat(dz, O, rows_per_batch=1, batch_stride=Lout * O), K.mat(wt, O), 0, 1, B, Cin, O, cm, dmask)
+    gemm(K.mat(dz, O, rows_per_batch=1, batch_stride=Lout * O, offset=(Lout - 1) * O), K.mat(wt, O, offset=2 * Cin * O),
+         2 * Lout * Cin, 1, B, Cin, O, cm, dmask)
+    if Lin > 2 * Lout + 1:
+        d.view(B, Lin, Cin)[:, 2 * Lout + 1:].zero_()
+    return d
+
+
 class FrontendFn(torch.autograd.Function):
     """wave (B,S) fp32 -> channels-last features (B*T, C) bf16 (x dummy_weight).
 
@@ -594,24 +644,31 @@ class FrontendFn(torch.autograd.Function):
                                c_dtype=K.OUT_F32, splits=splits, device=dev))
             dw, direct = go.buf(pws[i], zero=False)
             call("dph_conv_weight_unpack_grad", ptr(dwp), ptr(dw), O, Cin, k, Cinp, int(direct), _s())
-            # input gradient columns, then col2im fused with the previous layer's GELU/mask backward
-            dcols = torch.empty(M, k * Cinp, dtype=BF16, device=dev)
+            # input gradient, fused with the previous layer's GELU/mask backward (i > 1): phase GEMMs
+            # writing d_in in place, or the column gradient + col2im for other conv geometries
             wt = t_image(ctx.imgs[i])     # [k*Cinp][Op]: both operands k-contiguous -> ring kernels
-            if wt is not None:
-                K.gemm(K.dense(dz), K.dense(wt), K.dense(dcols), M, k * Cinp, Op, a_kcontig=True, b_kcontig=True)
-            else:
-                K.gemm(K.dense(dz), K.dense(ctx.imgs[i]), K.dense(dcols), M, k * Cinp, Op, a_kcontig=True,
-                       b_kcontig=False)
-            nxt = torch.empty(B * Ls[i - 1], Cinp, dtype=BF16, device=dev)
-            if i > 1:
-                dmk = zeros_f32(Cinp, dev) if masks[i - 1] is not None else None
-                call("dph_col2im_gelu_bwd", ptr(dcols), B, Ls[i], Ls[i - 1], Cinp, k, s, ptr(ctx.zs[i - 1]),
-                     ptr(ctx.cms[i - 1]), ptr(nxt), ptr(dmk) if dmk is not None else
-                     ptr(zeros_f32(Cinp, dev)), _s())
-                g_m[i - 1] = dmk[:Cin] if dmk is not None else None
-            else:
-                call("dph_col2im_gelu_bwd", ptr(dcols), B, Ls[i], Ls[i - 1], Cinp, k, s, None, None, ptr(nxt), None,
-                     _s())
+            dmk = (zeros_f32(Cinp, dev) if masks[i - 1] is not None else zeros_f32(Cinp, dev)) if i > 1 else None
+            nxt = None
+            if wt is not None and _PHASE_DGRAD:
+                nxt = conv_dgrad_phases(dz, wt, B, Ls[i], Ls[i - 1], Op, Cinp, k, s,
+                                        z_pre=ctx.zs[i - 1] if i > 1 else None,
+                                        cm=ctx.cms[i - 1] if i > 1 else None, dmask=dmk)
+            if nxt is None:
+                dcols = torch.empty(M, k * Cinp, dtype=BF16, device=dev)
+                if wt is not None:
+                    K.gemm(K.dense(dz), K.dense(wt), K.dense(dcols), M, k * Cinp, Op, a_kcontig=True, b_kcontig=True)
+                else:
+                    K.gemm(K.dense(dz), K.dense(ctx.imgs[i]), K.dense(dcols), M, k * Cinp, Op, a_kcontig=True,
+                           b_kcontig=False)
+                nxt = torch.empty(B * Ls[i - 1], Cinp, dtype=BF16, device=dev)
+                if i > 1:
+                    call("dph_col2im_gelu_bwd", ptr(dcols), B, Ls[i], Ls[i - 1], Cinp, k, s, ptr(ctx.zs[i - 1]),
+                         ptr(ctx.cms[i - 1]), ptr(nxt), ptr(dmk), _s())
+                else:
+                    call("dph_col2im_gelu_bwd", ptr(dcols), B, Ls[i], Ls[i - 1], Cinp, k, s, None, None, ptr(nxt),
+                         None, _s())
+            if i > 1 and masks[i - 1] is not None:
+                g_m[i - 1] = dmk[:Cin]
             dz = nxt
         # layer 0: conv0 + GroupNorm + GELU + mask, recomputed from the waveform
         C0, k0, s0 = layers[0]
@@ -761,17 +818,22 @@ class FrontendLNFn(torch.autograd.Function):
                                c_dtype=K.OUT_F32, splits=splits, device=dev))
             dw, direct = go.buf(w, zero=False)
             call("dph_conv_weight_unpack_grad", ptr(dwp), ptr(dw), C, Cin, k, Cin, int(direct), _s())
-            dcols = torch.empty(rows, k * Cin, dtype=BF16, device=dev)
             wt = t_image(ctx.imgs[i])
-            if wt is not None:
-                K.gemm(K.dense(dz), K.dense(wt), K.dense(dcols), rows, k * Cin, C, a_kcontig=True, b_kcontig=True)
-            else:
-                K.gemm(K.dense(dz), K.dense(ctx.imgs[i]), K.dense(dcols), rows, k * Cin, C, a_kcontig=True,
-                       b_kcontig=False)
-            dh = torch.empty(B * Ls[i - 1], Cin, dtype=BF16, device=dev)
             dmk = zeros_f32(Cin, dev)
-            call("dph_col2im_gelu_bwd", ptr(dcols), B, Ls[i], Ls[i - 1], Cin, k, s, ptr(ctx.hs[i - 1]),
-                 ptr(ctx.cms[i - 1]), ptr(dh), ptr(dmk), _s())
+            dh = None
+            if wt is not None and _PHASE_DGRAD:
+                dh = conv_dgrad_phases(dz, wt, B, Ls[i], Ls[i - 1], C, Cin, k, s, z_pre=ctx.hs[i - 1],
+                                       cm=ctx.cms[i - 1], dmask=dmk)
+            if dh is None:
+                dcols = torch.empty(rows, k * Cin, dtype=BF16, device=dev)
+                if wt is not None:
+                    K.gemm(K.dense(dz), K.dense(wt), K.dense(dcols), rows, k * Cin, C, a_kcontig=True, b_kcontig=True)
+                else:
+                    K.gemm(K.dense(dz), K.dense(ctx.imgs[i]), K.dense(dcols), rows, k * Cin, C, a_kcontig=True,
+                           b_kcontig=False)
+                dh = torch.empty(B * Ls[i - 1], Cin, dtype=BF16, device=dev)
+                call("dph_col2im_gelu_bwd", ptr(dcols), B, Ls[i], Ls[i - 1], Cin, k, s, ptr(ctx.hs[i - 1]),
+                     ptr(ctx.cms[i - 1]), ptr(dh), ptr(dmk), _s())
             if ctx.has_mask[i - 1]:
                 g_m[i - 1] = dmk
         # the conv0 weight gradient went through dph_conv0_bwd, which accumulates (needs a zeroed

@@ -418,3 +418,27 @@ def test_conv_frame_lengths():
     got = ops.conv_frame_lengths(L.to(DEV), layers)
     torch.cuda.synchronize()
     assert torch.equal(got.cpu(), ref)
+
+
+def test_conv_dgrad_phases_match_column_path(monkeypatch):
+    """Strided-conv input gradients by output phase (GEMMs writing d_in in place, GELU'/mask in the
+    epilogue) == the column-gradient + col2im path on the same inputs (fp32 accumulation both ways;
+    the bf16 output rounding of the two orders differs, hence 1e-2)."""
+    from dphubert_amd import ops
+    cfg = _cfg(1, extractor_prune_conv_channels=True)
+    grads = []
+    for phase in (True, False):
+        monkeypatch.setattr(ops, "_PHASE_DGRAD", phase)
+        m, sd = _model(cfg, seed=7)
+        fe = m.feature_extractor.train()
+        g = torch.Generator().manual_seed(3)
+        wave = 0.1 * torch.randn(3, 12345, generator=g)     # odd lengths at several layers
+        for i, l in enumerate(fe.conv_layers):
+            l.hard_concrete.set_noise(torch.rand(512, generator=g) * 0.98 + 0.01)
+        y, _ = fe(wave.to(DEV), None)
+        gy = torch.randn(y.shape, generator=g).to(torch.bfloat16)
+        y.backward(gy.to(DEV))
+        torch.cuda.synchronize()
+        grads.append({n: p.grad.detach().float().cpu().clone() for n, p in fe.named_parameters() if p.grad is not None})
+    for n in grads[0]:
+        assert rel_l2(grads[0][n], grads[1][n]) < 1e-2, n
