@@ -489,20 +489,31 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkv_kernel(const bf16_t* __re
     if (more) store_tiles(cur ^ 1, qt + 1);
     __syncthreads();
   }
-  // lane holds dK[key = k0 + 16u + 4g + i][d = 16dd + (lane&15)]
+  // lane holds dK[key = k0 + 16u + 4g + i][d = 16dd + (lane&15)]: stage the wave's [32 keys][64] bf16
+  // tile in LDS and store whole 128-B key rows with 16-B stores (4 per lane per tensor instead of 32
+  // scattered 2-byte stores)
+  __syncthreads();   // every wave is done with the Q / dO tiles
+  uint16_t* st = reinterpret_cast<uint16_t*>(smem) + wave * (16 * NG * HD);
 #pragma unroll
-  for (int u = 0; u < NG; ++u)
+  for (int tsel = 0; tsel < 2; ++tsel) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int64_t key = k0 + 16 * u + 4 * g + i;
-      if (key >= T) continue;
-      bf16_t* rowp = dqkv + (b * T + key) * RS;
+    for (int u = 0; u < NG; ++u)
 #pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        rowp[(H + h) * HD + 16 * d + (lane & 15)] = f2bf(dk[u][d][i]);
-        rowp[(2 * H + h) * HD + 16 * d + (lane & 15)] = f2bf(dv[u][d][i]);
-      }
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int d = 0; d < 4; ++d)
+          st[(16 * u + 4 * g + i) * HD + 16 * d + (lane & 15)] = f2bf(tsel == 0 ? dk[u][d][i] : dv[u][d][i]);
+    __syncthreads();
+#pragma unroll
+    for (int ps = 0; ps < 16 * NG / 8; ++ps) {
+      const int r = (lane >> 3) + 8 * ps;
+      const int64_t key = k0 + r;
+      const uint4 v = *reinterpret_cast<const uint4*>(st + r * HD + (lane & 7) * 8);
+      if (key < T)
+        *reinterpret_cast<uint4*>(dqkv + (b * T + key) * RS + ((tsel + 1) * H + h) * HD + (lane & 7) * 8) = v;
     }
+    __syncthreads();
+  }
 }
 
 // ---------------------------------------------------------------------------
