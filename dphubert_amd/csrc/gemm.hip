@@ -445,7 +445,8 @@ constexpr int CROW = BN + 4;                       // padded fp32 row
 constexpr int LDS_C = BM * CROW * 4;               // 67,584 B
 
 template <bool AK, bool BKc, int NT = NTHREADS>
-__global__ void __launch_bounds__(NT, 2) gemm_kernel(const DphGemmArgs a, int64_t kchunk) {
+__global__ void __launch_bounds__(NT, 2) gemm_kernel(const DphGemmArgs a, int64_t kchunk,
+                                                     unsigned* __restrict__ tile_cnt = nullptr) {
   constexpr int PIPE = 2 * (TileBytes<AK>::v + TileBytes<BKc>::v);
   __shared__ __attribute__((aligned(16))) char smem[PIPE > LDS_C ? PIPE : LDS_C];
   char* const ldsA0 = smem;
@@ -581,6 +582,48 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(const DphGemmArgs a, int64_
       } else {
         for (int q = 0; q < 8 && n + q < a.N; ++q) dst[q] = src[q];
       }
+    }
+    if (tile_cnt == nullptr) return;   // a separate splitk_reduce_kernel combines the slices
+    // In-launch split-K combine (guide: "Projection GEMM at M = 256", item 2): publish this slice
+    // (stores drained, agent-scope release, then the ticket), and the block that draws the last
+    // ticket of the tile acquires, sums every slice's slab and runs the epilogue.  No block waits on
+    // another, so any placement of a tile's slices over XCDs / CUs is correct.
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    unsigned* flag = reinterpret_cast<unsigned*>(smem);
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int64_t tile = z * ((int64_t)gridDim.x * gridDim.y) + tm * gridDim.x + tn;
+      const unsigned old = __hip_atomic_fetch_add(tile_cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const bool last = old == (unsigned)(a.splits - 1);
+      if (last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        tile_cnt[tile] = 0u;   // ready for the next launch on the same counters
+      }
+      flag[0] = last ? 1u : 0u;
+    }
+    __syncthreads();
+    if (flag[0] == 0u) return;
+    const float* ws0 = reinterpret_cast<const float*>(a.workspace) + ((z * a.splits) * a.M) * a.N;
+    const int64_t sstride = a.M * a.N;
+#pragma unroll 1
+    for (int p = 0; p < BM * BN / 8 / NT; ++p) {
+      const int r = r0 + (NT / 16) * p;
+      const int64_t m = m0 + r;
+      const int64_t n = n0 + c8;
+      if (m >= a.M || n >= a.N) continue;
+      float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      const bool vec = n + 8 <= a.N && (a.N & 3) == 0;
+      for (int sp = 0; sp < a.splits; ++sp) {
+        float t[8];
+        load8_f32(ws0 + sp * sstride + m * a.N + n, vec, (int)min<int64_t>(8, a.N - n), t);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] += t[q];
+      }
+      Cs8 cs;
+      epilogue8(a, z, m, n, v, cs);
     }
     return;
   }
@@ -1358,25 +1401,38 @@ extern "C" int dph_gemm(const DphGemmArgs* args, hipStream_t stream) {
   } else {
   dim3 grid((unsigned)cdiv(a.N, BN), (unsigned)cdiv(a.M, BM), (unsigned)(a.batch * a.splits));
   DPH_REQUIRE(grid.y < 65536 && grid.z < 65536, "dph_gemm: grid too large");
+  // split-K on the register-staged kernel: slices are combined inside the launch by the last-arriving
+  // block of each tile when the workspace carries the per-tile tickets (zeroed here, reset by the
+  // combining block)
+  unsigned* cnt = nullptr;
+  if (a.splits > 1) {
+    const int64_t slab = (int64_t)a.batch * a.splits * a.M * a.N * 4;
+    const int64_t tiles = (int64_t)grid.x * grid.y * a.batch;
+    if (a.workspace_bytes >= slab + tiles * 4) {
+      cnt = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(a.workspace) + slab);
+      hipMemsetAsync(cnt, 0, tiles * 4, stream);
+    }
+  }
   if (small_nt(kchunk) == 512) {
     if (a.a_kcontig && a.b_kcontig)
-      hipLaunchKernelGGL((gemm_kernel<true, true, 512>), grid, dim3(512), 0, stream, a, kchunk);
+      hipLaunchKernelGGL((gemm_kernel<true, true, 512>), grid, dim3(512), 0, stream, a, kchunk, cnt);
     else if (a.a_kcontig && !a.b_kcontig)
-      hipLaunchKernelGGL((gemm_kernel<true, false, 512>), grid, dim3(512), 0, stream, a, kchunk);
+      hipLaunchKernelGGL((gemm_kernel<true, false, 512>), grid, dim3(512), 0, stream, a, kchunk, cnt);
     else if (!a.a_kcontig && a.b_kcontig)
-      hipLaunchKernelGGL((gemm_kernel<false, true, 512>), grid, dim3(512), 0, stream, a, kchunk);
+      hipLaunchKernelGGL((gemm_kernel<false, true, 512>), grid, dim3(512), 0, stream, a, kchunk, cnt);
     else
-      hipLaunchKernelGGL((gemm_kernel<false, false, 512>), grid, dim3(512), 0, stream, a, kchunk);
+      hipLaunchKernelGGL((gemm_kernel<false, false, 512>), grid, dim3(512), 0, stream, a, kchunk, cnt);
   } else {
   if (a.a_kcontig && a.b_kcontig)
-    hipLaunchKernelGGL((gemm_kernel<true, true>), grid, dim3(NTHREADS), 0, stream, a, kchunk);
+    hipLaunchKernelGGL((gemm_kernel<true, true>), grid, dim3(NTHREADS), 0, stream, a, kchunk, cnt);
   else if (a.a_kcontig && !a.b_kcontig)
-    hipLaunchKernelGGL((gemm_kernel<true, false>), grid, dim3(NTHREADS), 0, stream, a, kchunk);
+    hipLaunchKernelGGL((gemm_kernel<true, false>), grid, dim3(NTHREADS), 0, stream, a, kchunk, cnt);
   else if (!a.a_kcontig && a.b_kcontig)
-    hipLaunchKernelGGL((gemm_kernel<false, true>), grid, dim3(NTHREADS), 0, stream, a, kchunk);
+    hipLaunchKernelGGL((gemm_kernel<false, true>), grid, dim3(NTHREADS), 0, stream, a, kchunk, cnt);
   else
-    hipLaunchKernelGGL((gemm_kernel<false, false>), grid, dim3(NTHREADS), 0, stream, a, kchunk);
+    hipLaunchKernelGGL((gemm_kernel<false, false>), grid, dim3(NTHREADS), 0, stream, a, kchunk, cnt);
   }
+  if (cnt != nullptr) return check_launch("dph_gemm");
   }
   int rc = check_launch("dph_gemm");
   if (rc) return rc;
