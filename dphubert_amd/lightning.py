@@ -122,6 +122,8 @@ class DistillModule(nn.Module):
         self.num_workers = num_workers
         self.global_step = 0
         self.target_sparsity_dev = None    # 0-d device view set by trainer.Trainer (stepstate block)
+        self.teacher_stream = None         # side HIP stream for the teacher forward (trainer.Trainer)
+        self._teacher_arena = ops.new_zero_arena()
         self.logged = {}
         # distinct projection modules (shared per group, distill.py:94-99) and the per-layer index into them
         uniq, index = [], []
@@ -171,10 +173,25 @@ class DistillModule(nn.Module):
     def _step(self, batch, batch_idx, mode):
         waveforms, lengths = batch
         self.teacher_model.eval()
-        with torch.no_grad():
-            teacher_hiddens, teacher_lengths = self.teacher_model.extract_features(waveforms, lengths)
-            t_layers = [teacher_hiddens[idx] for idx in self.distill_layers]
+        side = self.teacher_stream if waveforms.is_cuda else None
+        if side is not None:
+            # the frozen teacher runs on its own HIP stream, concurrently with the student forward: its
+            # kernels fill the CUs the student's GEMM tile rounds and latency-bound launches leave idle
+            # (forked / joined with stream waits, so a HIP-graph capture records both branches)
+            main = torch.cuda.current_stream()
+            side.wait_stream(main)
+            with torch.cuda.stream(side), torch.no_grad(), ops.private_zero_arena(self._teacher_arena):
+                teacher_hiddens, teacher_lengths = self.teacher_model.extract_features(waveforms, lengths)
+                t_layers = [teacher_hiddens[idx] for idx in self.distill_layers]
+        else:
+            with torch.no_grad():
+                teacher_hiddens, teacher_lengths = self.teacher_model.extract_features(waveforms, lengths)
+                t_layers = [teacher_hiddens[idx] for idx in self.distill_layers]
         student_hiddens, student_lengths = self.student_model.extract_features(waveforms, lengths)
+        if side is not None:
+            main.wait_stream(side)
+            for t in t_layers:
+                t.record_stream(main)
         if self.distill_mode == "layer2layer":
             s_layers = [student_hiddens[idx] for idx in self.distill_layers]
         elif self.distill_mode == "predlayer":

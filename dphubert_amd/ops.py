@@ -288,11 +288,38 @@ class _ZeroArena:
 _ZEROS = _ZeroArena()
 
 
+_ARENAS = []
+
+
+def new_zero_arena() -> _ZeroArena:
+    a = _ZeroArena()
+    _ARENAS.append(a)
+    return a
+
+
+class private_zero_arena:
+    """Route zeros_f32 to ``arena`` inside the block (work on a side stream must not share arena
+    chunks whose zero fill sits on another stream)."""
+
+    def __init__(self, arena: _ZeroArena):
+        self.arena = arena
+
+    def __enter__(self):
+        global _ZEROS
+        self.prev, _ZEROS = _ZEROS, self.arena
+        return self.arena
+
+    def __exit__(self, *exc):
+        global _ZEROS
+        _ZEROS = self.prev
+
+
 def reset_zero_arena():
     """Start a fresh arena chunk on the next request (around a HIP-graph capture: slices handed out
     inside the capture must come from a chunk whose zero fill is itself part of the graph)."""
-    _ZEROS.buf = None
-    _ZEROS.off = 0
+    for a in [_ZEROS] + _ARENAS:
+        a.buf = None
+        a.off = 0
 
 
 def zeros_f32(shape, dev) -> torch.Tensor:

@@ -17,6 +17,7 @@ reference schedule exactly while the host does ~50 us of work per step instead o
 """
 
 import copy
+import os
 import warnings
 from typing import List, Optional
 
@@ -147,6 +148,10 @@ class Trainer:
         self._static_loss = None
         self._prof_loss = None
         self.scalars = None
+        # teacher forward on a side stream (DPH_TEACHER_STREAM=0 keeps one stream)
+        if os.environ.get("DPH_TEACHER_STREAM", "1") != "0" and torch.cuda.is_available() and \
+                next(module.parameters()).is_cuda:
+            module.teacher_stream = torch.cuda.Stream()
 
     # ---- per-step device scalars -------------------------------------------------------------
     def _bind_scalars(self, device):
