@@ -109,6 +109,9 @@ def seeded_tensor(name: str, shape: Tuple[int, ...], seed: int = 0) -> torch.Ten
         for s in shape[1:]:
             fan_in *= s
         return torch.randn(shape, generator=g) / math.sqrt(max(fan_in, 1))
+    if leaf == "gru_rel_pos_const":
+        # WavLM gate constant: reference init is ones (components.py:541); perturbed so its grad is non-trivial
+        return 1.0 + 0.1 * torch.randn(shape, generator=g)
     if leaf in ("lambda1", "lambda2"):
         return torch.zeros(shape)
     return 0.02 * torch.randn(shape, generator=g)

@@ -162,3 +162,23 @@ def test_layer_norm_extractor_g7():
     _check_step(fx, out)
     for h, g in zip(out["student_hiddens"], fx["student_hiddens"]):
         assert rel_l2(h, g) < 1e-5
+
+
+def test_wavlm_g8():
+    """WavLM layers (bucketed relative-position bias shared from layer 0, per-layer gate, a layer with 9 of 12
+    heads remaining): the oracle restatement against the reference's own step on the same inputs."""
+    fx = load_golden("g8_wavlm.pt")
+    assert [(k, tuple(s)) for k, s in ref.state_dict_shapes(fx["scfg"])] == [(k, tuple(s)) for k, s in
+                                                                              fx["sd_schema"]]
+    out = _run_fixture(fx)
+    _check_step(fx, out)
+    for h, g in zip(out["student_hiddens"], fx["student_hiddens"]):
+        assert rel_l2(h, g) < 1e-5
+
+
+def test_wavlm_relative_position_bucket():
+    """Bucket index tables (integer, bit-exact) for WavLM Base (320 buckets / 800) and a small config."""
+    fx = load_golden("g8_wavlm.pt")
+    for key, (nb, md, T) in (("bucket_320_800_T1000", (320, 800, 1000)), ("bucket_32_40_T200", (32, 40, 200))):
+        rel = torch.arange(T)[None, :] - torch.arange(T)[:, None]
+        assert torch.equal(ref.relative_position_bucket(rel, nb, md)[0], fx[key])

@@ -341,9 +341,47 @@ def gen_lnext():
                     global_step=2500, lengths=[24000, 19000], full=True)
 
 
+def wavlm_cfg(n_layers, remaining_heads=None, **kw):
+    """WavLM config (model.py:736 wavlm_model keys): no encoder_num_heads / encoder_head_dim, total + remaining
+    heads per layer, relative-position buckets."""
+    c = small_cfg(n_layers)
+    del c["encoder_num_heads"], c["encoder_head_dim"]
+    c.update(encoder_total_num_heads=[12] * n_layers,
+             encoder_remaining_heads=remaining_heads or [list(range(12))] * n_layers,
+             encoder_num_buckets=32, encoder_max_distance=40)
+    c.update(kw)
+    return c
+
+
+def gen_wavlm():
+    """G8: WavLM layers (WavLMSelfAttention, components.py:486-659: bucketed relative-position bias from layer
+    0's embedding shared by every layer, GRU-style gate per layer) on the 2-layer shape, padded batch, layer 1
+    with 9 of 12 heads remaining, regulariser active.  num_buckets 32 / max_distance 40 so T = 74 frames reach
+    both the log-spaced buckets and the num_buckets-1 cap."""
+    cfg = wavlm_cfg(2, remaining_heads=[list(range(12)), [0, 1, 3, 4, 6, 7, 8, 10, 11]])
+    fx = run_step(cfg, cfg, "0.1,2", B=2, S=24000, units="conv,head,interm", lambdas=(0.2, 0.1),
+                  global_step=2500, lengths=[24000, 19000], full=True)
+    m, _ = seeded_model(dict(cfg, **units_flags("conv,head,interm")), 0)
+    fx["sd_schema"] = [(k, tuple(v.shape)) for k, v in m.state_dict().items()]
+    fx["num_params_init"] = float(m.get_num_params())
+    # the bucket table of the reference for T = 74 and a long T (integer index data)
+    from wav2vec2.components import WavLMSelfAttention
+    att = WavLMSelfAttention(64, 1, has_relative_attention_bias=True, num_buckets=320, max_distance=800)
+    fx["bucket_320_800_T1000"] = att._relative_positions_bucket(
+        torch.arange(1000)[None, :] - torch.arange(1000)[:, None], bidirectional=True)[0].clone()
+    att = WavLMSelfAttention(64, 1, has_relative_attention_bias=True, num_buckets=32, max_distance=40)
+    fx["bucket_32_40_T200"] = att._relative_positions_bucket(
+        torch.arange(200)[None, :] - torch.arange(200)[:, None], bidirectional=True)[0].clone()
+    return fx
+
+
 def main():
     OUT.mkdir(parents=True, exist_ok=True)
     torch.set_num_threads(8)
+    if "--only-wavlm" in sys.argv:
+        torch.save(gen_wavlm(), OUT / "g8_wavlm.pt")
+        print("g8 done")
+        return
     if "--only-lnext" in sys.argv:
         torch.save(gen_lnext(), OUT / "g7_lnext.pt")
         print("g7 done")
