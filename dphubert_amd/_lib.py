@@ -70,6 +70,13 @@ _SIGS = {
     "dph_attention_fwd": ([vp, vp, vp, vp, vp, vp, i64, i64, i64, f32, f32, u64, S], C.c_int),
     "dph_attention_bwd_prep": ([vp, vp, vp, vp, vp, i64, i64, i64, S], C.c_int),
     "dph_attention_bwd": ([vp, vp, vp, vp, vp, vp, vp, i64, i64, i64, f32, f32, u64, S], C.c_int),
+    "dph_attention_fwd_relpos": ([vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, i64, f32, f32, u64, S], C.c_int),
+    "dph_attention_bwd_relpos": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, i64, f32, f32, u64, S],
+                                 C.c_int),
+    "dph_relpos_table": ([vp, vp, vp, vp, i64, i64, i64, i64, i64, S], C.c_int),
+    "dph_relpos_table_bwd": ([vp, vp, vp, i64, i64, i64, i64, i64, S], C.c_int),
+    "dph_wavlm_gate_fwd": ([vp, i64, vp, vp, vp, vp, vp, i64, i64, i64, i64, S], C.c_int),
+    "dph_wavlm_gate_bwd": ([vp, i64, vp, vp, vp, vp, vp, vp, i64, vp, vp, vp, vp, i64, i64, i64, i64, S], C.c_int),
     "dph_conv0_gn_fwd": ([vp, i64, i64, vp, i64, i64, i64, vp, vp, vp, vp, vp, vp, vp, i64, S], C.c_int),
     "dph_conv0_gn_bwd_workspace": ([i64, i64], i64),
     "dph_conv0_gn_bwd": ([vp, i64, i64, vp, i64, i64, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, S],
@@ -110,7 +117,7 @@ _SIGS = {
 }
 
 _lib = None
-ABI_VERSION = 10     # include/dphubert_hip.h layout (3: dph_adamw_step_dev, dph_set_rng_epoch; 4: dph_event_*; 5: LN bwd / colsum workspaces)
+ABI_VERSION = 11     # include/dphubert_hip.h layout (3: dph_adamw_step_dev, dph_set_rng_epoch; 4: dph_event_*; 5: LN bwd / colsum workspaces)
 
 
 class DphError(RuntimeError):

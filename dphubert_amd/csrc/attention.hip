@@ -72,6 +72,22 @@ struct AttnShape {
   int64_t B, T, H, RS;  // RS = row stride of qkv (3*H*64)
 };
 
+// WavLM gated relative-position bias (components.py:629-651): score[b,h,q,k] += gate[b,h,q] * tab[h][k-q+T-1].
+// tab holds the bucketed embedding already gathered per remaining head (dph_relpos_table), gate the per-query
+// GRU gate (dph_wavlm_gate_fwd).  Backward: dgate[b,h,q] = sum_k dS*tab (row sums, written), dtab[h][r] +=
+// sum over the diagonal r of dS*gate (LDS histogram per block, then global atomics).
+struct RelBias {
+  const float* tab;    // [H][2T-1]
+  const float* gate;   // [B][H][T]
+  float* dgate;        // [B][H][T]
+  float* dtab;         // [H][2T-1], accumulated
+};
+
+// clamped diagonal index: rows / keys past T (masked to 0 probability) read a valid entry
+__device__ __forceinline__ int rel_idx(int key, int q, int T32) {
+  return min(key, T32 - 1) - min(q, T32 - 1) + T32 - 1;
+}
+
 // Dropout of the attention probabilities: element (row = (b*H+h)*T + q, key) draws 16 bits from ONE
 // 32-bit hash per (row, key pair) -- rows padded to an even key count, so the 4 consecutive keys a
 // lane holds in the forward / dQ kernels cost 2 hashes, and in the dK/dV kernel (4 queries of one
@@ -128,12 +144,12 @@ constexpr int RB = 4 * 16 * NG;   // rows per block: 128
 // one basic block (runtime `if`s split it and kept hipcc from overlapping one query group's
 // softmax with the other group's MFMAs).
 // ---------------------------------------------------------------------------
-template <bool DROP>
+template <bool DROP, bool BIAS>
 __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ o_u,
                                                           bf16_t* __restrict__ o_m, float* __restrict__ lse,
                                                           const float* __restrict__ head_mask,
                                                           const int64_t* __restrict__ key_len, AttnShape sh,
-                                                          float scale, float drop_p, uint64_t seed) {
+                                                          float scale, float drop_p, uint64_t seed, RelBias rb) {
   seed = epoch_seed(seed);   // per-step RNG epoch (graph replays)
   __shared__ __attribute__((aligned(16))) char smem[2 * (KTILE_PAD_BYTES + TILE_SWZ_BYTES)];
   const int tid = threadIdx.x;
@@ -155,6 +171,10 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(const bf16_t* __restri
     qme[u] = q0 + 16 * u + (lane & 15);
     hrow[u] = ((uint64_t)(b * H + h) * T + (uint64_t)qme[u]) * half_tp;
   }
+  const float* tb = BIAS ? rb.tab + h * (2 * T - 1) : nullptr;
+  float gq[NG];
+#pragma unroll
+  for (int u = 0; u < NG; ++u) gq[u] = (BIAS && qme[u] < T) ? rb.gate[(b * H + h) * T + qme[u]] : 0.f;
 
   // Q' = scale*q fragments (B operand of S^T = K Q'^T): Q'[q = lane&15][hd = 32ks + 8g + j]
   bf16x8_t qf[NG][2];
@@ -221,6 +241,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(const bf16_t* __restri
         for (int i = 0; i < 4; ++i) {
           const int key = kb + 16 * s + i;
           float v = sacc[u][s][i];
+          if constexpr (BIAS) v += gq[u] * tb[rel_idx(key, (int)qme[u], T32)];
           v = key >= klen ? v - 10000.0f : v;
           v = key >= T32 ? -INFINITY : v;
           sacc[u][s][i] = v;
@@ -331,17 +352,17 @@ __global__ void __launch_bounds__(256) attn_bwd_prep_kernel(const bf16_t* __rest
 // backward dK, dV: block = (128 keys, h, b), wave w owns keys k0 = 128*bx + 32w + 16u + (0..15),
 // u < NG.  Loops over query steps of 32 rows; Q' and dO' (= hm*dO_m) tiles staged in LDS.
 // ---------------------------------------------------------------------------
-template <bool DROP>
+template <bool DROP, bool BIAS>
 __global__ void __launch_bounds__(256, 2) attn_bwd_dkv_kernel(const bf16_t* __restrict__ qkv,
                                                            const bf16_t* __restrict__ dom,
                                                            const float* __restrict__ head_mask,
                                                            const float* __restrict__ lse,
                                                            const float* __restrict__ Dv, bf16_t* __restrict__ dqkv,
                                                            const int64_t* __restrict__ key_len, AttnShape sh,
-                                                           float scale, float drop_p, uint64_t seed) {
+                                                           float scale, float drop_p, uint64_t seed, RelBias rb) {
   seed = epoch_seed(seed);   // per-step RNG epoch (graph replays)
   constexpr int TB = QT_BWD * 128;   // 4096 B per tile
-  __shared__ __attribute__((aligned(16))) char smem[2 * (2 * TB) + 2 * 2 * QT_BWD * 4];
+  __shared__ __attribute__((aligned(16))) char smem[2 * (2 * TB) + 3 * 2 * QT_BWD * 4];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
@@ -394,6 +415,8 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkv_kernel(const bf16_t* __re
   auto ldsO = [&](int buf) { return smem + buf * 2 * TB + TB; };
   float* lse_s = reinterpret_cast<float*>(smem + 4 * TB);        // [2][32]
   float* dv_s = reinterpret_cast<float*>(smem + 4 * TB + 2 * QT_BWD * 4);
+  float* g_s = reinterpret_cast<float*>(smem + 4 * TB + 4 * QT_BWD * 4);   // [2][32] gates (BIAS)
+  const float* tb = BIAS ? rb.tab + h * (2 * T - 1) : nullptr;
 
   const int nqt = (int)cdiv(T, QT_BWD);
   uint4 rq[1], ro[1];
@@ -408,6 +431,7 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkv_kernel(const bf16_t* __re
       const int64_t q = (int64_t)qt * QT_BWD + tid;
       lse_s[buf * QT_BWD + tid] = q < T ? lse[(b * H + h) * T + q] : 0.f;
       dv_s[buf * QT_BWD + tid] = q < T ? Dv[(b * H + h) * T + q] : 0.f;
+      if constexpr (BIAS) g_s[buf * QT_BWD + tid] = q < T ? rb.gate[(b * H + h) * T + q] : 0.f;
     }
   };
   load_tiles(0);
@@ -464,6 +488,7 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkv_kernel(const bf16_t* __re
           const int ql = 16 * w + 4 * g + i;
           const int q = qt * QT_BWD + ql;
           float sv = sacc[u][w][i];
+          if constexpr (BIAS) sv += g_s[cur * QT_BWD + ql] * tb[rel_idx((int)kme[u], q, T32)];
           sv = kpad[u] ? sv - 10000.0f : sv;
           float p = __expf(sv - lse_s[cur * QT_BWD + ql]);
           p = (q >= T32 || kout[u]) ? 0.f : p;
@@ -519,14 +544,15 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkv_kernel(const bf16_t* __re
 // ---------------------------------------------------------------------------
 // backward dQ: block = (128 query rows, h, b), 4 waves x 2 x 16 rows; loops over key tiles.
 // ---------------------------------------------------------------------------
-template <bool DROP>
+template <bool DROP, bool BIAS>
 __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(const bf16_t* __restrict__ qkv,
                                                           const bf16_t* __restrict__ dom,
                                                           const float* __restrict__ head_mask,
                                                           const float* __restrict__ lse,
                                                           const float* __restrict__ Dv, bf16_t* __restrict__ dqkv,
                                                           const int64_t* __restrict__ key_len, AttnShape sh,
-                                                          float scale, float drop_p, uint64_t seed) {
+                                                          float scale, float drop_p, uint64_t seed, RelBias rb) {
+  extern __shared__ float hist[];   // BIAS: [T + RB - 1] diagonal sums of dS * gate for this block's rows
   seed = epoch_seed(seed);   // per-step RNG epoch (graph replays)
   __shared__ __attribute__((aligned(16))) char smem[2 * (TILE_SWZ_BYTES + KTILE_PAD_BYTES)];
   const int tid = threadIdx.x;
@@ -569,6 +595,16 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(const bf16_t* __res
 #pragma unroll
     for (int d = 0; d < 4; ++d) dq[u][d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   }
+  const float* tb = BIAS ? rb.tab + h * (2 * T - 1) : nullptr;
+  float gq[NG], dg[NG];
+  const int qb0 = (int)blockIdx.x * RB;
+#pragma unroll
+  for (int u = 0; u < NG; ++u) {
+    gq[u] = (BIAS && qme[u] < T) ? rb.gate[(b * H + h) * T + qme[u]] : 0.f;
+    dg[u] = 0.f;
+  }
+  if constexpr (BIAS)
+    for (int i = tid; i < T32 + RB - 1; i += 256) hist[i] = 0.f;   // ordered before use by the first barrier
 
   auto ldsK = [&](int buf) { return smem + buf * (TILE_SWZ_BYTES + KTILE_PAD_BYTES); };
   auto ldsV = [&](int buf) { return smem + buf * (TILE_SWZ_BYTES + KTILE_PAD_BYTES) + TILE_SWZ_BYTES; };
@@ -622,11 +658,21 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(const bf16_t* __res
         for (int i = 0; i < 4; ++i) {
           const int key = kb + i;
           float sv = sa[u][i];
+          float tv = 0.f;
+          if constexpr (BIAS) {
+            tv = tb[rel_idx(key, (int)qme[u], T32)];
+            sv += gq[u] * tv;
+          }
           sv = key >= klen32 ? sv - 10000.0f : sv;
           float p = __expf(sv - my_lse[u]);
           p = (key >= T32 || qout[u]) ? 0.f : p;
           const float z = DROP ? attn_keep(hb[i >> 1], i & 1, thr, inv_keep) : 1.f;
-          ds[u][s][i] = p * (pa[u][i] * z - my_D[u]);
+          const float dsv = p * (pa[u][i] * z - my_D[u]);
+          ds[u][s][i] = dsv;
+          if constexpr (BIAS) {
+            dg[u] += dsv * tv;
+            if (key < T32 && !qout[u]) atomicAdd(&hist[key - (int)qme[u] + qb0 + RB - 1], dsv * gq[u]);
+          }
         }
       }
     }
@@ -649,6 +695,23 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(const bf16_t* __res
     }
     __syncthreads();
   }
+  if constexpr (BIAS) {
+#pragma unroll
+    for (int u = 0; u < NG; ++u) {
+      float v = dg[u];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      if (g == 0 && qme[u] < T) rb.dgate[(b * H + h) * T + qme[u]] = v;
+    }
+    __syncthreads();   // all histogram adds of the block are done
+    float* dt = rb.dtab + h * (2 * T - 1);
+    const int off = T32 - 1 - (qb0 + RB - 1);   // global diagonal index of hist[0]
+    for (int i = tid; i < T32 + RB - 1; i += 256) {
+      const int gi = i + off;
+      const float v = hist[i];
+      if (gi >= 0 && gi < 2 * T32 - 1 && v != 0.f) atomicAdd(dt + gi, v);
+    }
+  }
 #pragma unroll
   for (int u = 0; u < NG; ++u) {
     if (qme[u] >= T) continue;
@@ -667,21 +730,79 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(const bf16_t* __res
 
 using namespace dph;
 
+namespace {
+
+template <bool DROP, bool BIAS>
+void launch_fwd(dim3 grid, hipStream_t stream, const void* qkv, void* o_u, void* o_m, float* lse, const float* hm,
+                const int64_t* key_len, AttnShape sh, float scale, float p, uint64_t seed, RelBias rb) {
+  hipLaunchKernelGGL((attn_fwd_kernel<DROP, BIAS>), grid, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(qkv),
+                     reinterpret_cast<bf16_t*>(o_u), reinterpret_cast<bf16_t*>(o_m), lse, hm, key_len, sh, scale, p,
+                     seed, rb);
+}
+
+template <bool DROP, bool BIAS>
+void launch_bwd(dim3 grid, hipStream_t stream, const void* qkv, const void* dom, const float* hm, const float* lse,
+                const float* Dvec, void* dqkv, const int64_t* key_len, AttnShape sh, float scale, float p,
+                uint64_t seed, RelBias rb) {
+  hipLaunchKernelGGL((attn_bwd_dkv_kernel<DROP, BIAS>), grid, dim3(256), 0, stream,
+                     reinterpret_cast<const bf16_t*>(qkv), reinterpret_cast<const bf16_t*>(dom), hm, lse, Dvec,
+                     reinterpret_cast<bf16_t*>(dqkv), key_len, sh, scale, p, seed, rb);
+  const size_t hist_bytes = BIAS ? (size_t)(sh.T + RB - 1) * sizeof(float) : 0;
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<DROP, BIAS>), grid, dim3(256), hist_bytes, stream,
+                     reinterpret_cast<const bf16_t*>(qkv), reinterpret_cast<const bf16_t*>(dom), hm, lse, Dvec,
+                     reinterpret_cast<bf16_t*>(dqkv), key_len, sh, scale, p, seed, rb);
+}
+
+}  // namespace
+
+static int attention_fwd(const void* qkv, void* o_unmasked, void* o_masked, float* lse, const float* head_mask,
+                         const int64_t* key_len, int64_t B, int64_t T, int64_t H, float scale, float dropout_p,
+                         uint64_t seed, RelBias rb, hipStream_t stream) {
+  AttnShape sh{B, T, H, 3 * H * HD};
+  dim3 grid((unsigned)cdiv(T, RB), (unsigned)H, (unsigned)B);
+  const bool bias = rb.tab != nullptr;
+  if (dropout_p > 0.f) {
+    if (bias) launch_fwd<true, true>(grid, stream, qkv, o_unmasked, o_masked, lse, head_mask, key_len, sh, scale, dropout_p, seed, rb);
+    else launch_fwd<true, false>(grid, stream, qkv, o_unmasked, o_masked, lse, head_mask, key_len, sh, scale, dropout_p, seed, rb);
+  } else {
+    if (bias) launch_fwd<false, true>(grid, stream, qkv, o_unmasked, o_masked, lse, head_mask, key_len, sh, scale, dropout_p, seed, rb);
+    else launch_fwd<false, false>(grid, stream, qkv, o_unmasked, o_masked, lse, head_mask, key_len, sh, scale, dropout_p, seed, rb);
+  }
+  return check_launch("dph_attention_fwd");
+}
+
+static int attention_bwd(const void* qkv, const void* do_masked, const float* head_mask, const float* lse,
+                         const float* Dvec, void* dqkv, const int64_t* key_len, int64_t B, int64_t T, int64_t H,
+                         float scale, float dropout_p, uint64_t seed, RelBias rb, hipStream_t stream) {
+  AttnShape sh{B, T, H, 3 * H * HD};
+  dim3 grid((unsigned)cdiv(T, RB), (unsigned)H, (unsigned)B);
+  const bool bias = rb.tab != nullptr;
+  if (dropout_p > 0.f) {
+    if (bias) launch_bwd<true, true>(grid, stream, qkv, do_masked, head_mask, lse, Dvec, dqkv, key_len, sh, scale, dropout_p, seed, rb);
+    else launch_bwd<true, false>(grid, stream, qkv, do_masked, head_mask, lse, Dvec, dqkv, key_len, sh, scale, dropout_p, seed, rb);
+  } else {
+    if (bias) launch_bwd<false, true>(grid, stream, qkv, do_masked, head_mask, lse, Dvec, dqkv, key_len, sh, scale, dropout_p, seed, rb);
+    else launch_bwd<false, false>(grid, stream, qkv, do_masked, head_mask, lse, Dvec, dqkv, key_len, sh, scale, dropout_p, seed, rb);
+  }
+  return check_launch("dph_attention_bwd");
+}
+
 extern "C" int dph_attention_fwd(const void* qkv, void* o_unmasked, void* o_masked, float* lse,
                                  const float* head_mask, const int64_t* key_len, int64_t B, int64_t T, int64_t H,
                                  float scale, float dropout_p, uint64_t seed, hipStream_t stream) {
   DPH_REQUIRE(qkv && o_unmasked && o_masked && lse && B > 0 && T > 0 && H > 0, "dph_attention_fwd: bad args");
-  AttnShape sh{B, T, H, 3 * H * HD};
-  dim3 grid((unsigned)cdiv(T, RB), (unsigned)H, (unsigned)B);
-  if (dropout_p > 0.f)
-    hipLaunchKernelGGL(attn_fwd_kernel<true>, grid, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(qkv),
-                       reinterpret_cast<bf16_t*>(o_unmasked), reinterpret_cast<bf16_t*>(o_masked), lse, head_mask,
-                       key_len, sh, scale, dropout_p, seed);
-  else
-    hipLaunchKernelGGL(attn_fwd_kernel<false>, grid, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(qkv),
-                       reinterpret_cast<bf16_t*>(o_unmasked), reinterpret_cast<bf16_t*>(o_masked), lse, head_mask,
-                       key_len, sh, scale, dropout_p, seed);
-  return check_launch("dph_attention_fwd");
+  return attention_fwd(qkv, o_unmasked, o_masked, lse, head_mask, key_len, B, T, H, scale, dropout_p, seed,
+                       RelBias{nullptr, nullptr, nullptr, nullptr}, stream);
+}
+
+extern "C" int dph_attention_fwd_relpos(const void* qkv, void* o_unmasked, void* o_masked, float* lse,
+                                        const float* head_mask, const int64_t* key_len, const float* rel_tab,
+                                        const float* gate, int64_t B, int64_t T, int64_t H, float scale,
+                                        float dropout_p, uint64_t seed, hipStream_t stream) {
+  DPH_REQUIRE(qkv && o_unmasked && o_masked && lse && rel_tab && gate && B > 0 && T > 0 && T <= 4096 && H > 0,
+              "dph_attention_fwd_relpos: bad args (T <= 4096)");
+  return attention_fwd(qkv, o_unmasked, o_masked, lse, head_mask, key_len, B, T, H, scale, dropout_p, seed,
+                       RelBias{rel_tab, gate, nullptr, nullptr}, stream);
 }
 
 extern "C" int dph_attention_bwd_prep(const void* do_masked, const void* o_unmasked, const float* head_mask,
@@ -698,26 +819,18 @@ extern "C" int dph_attention_bwd(const void* qkv, const void* do_masked, const f
                                  const float* Dvec, void* dqkv, const int64_t* key_len, int64_t B, int64_t T,
                                  int64_t H, float scale, float dropout_p, uint64_t seed, hipStream_t stream) {
   DPH_REQUIRE(qkv && do_masked && lse && Dvec && dqkv && B > 0 && T > 0 && H > 0, "dph_attention_bwd: bad args");
-  AttnShape sh{B, T, H, 3 * H * HD};
-  dim3 grid((unsigned)cdiv(T, RB), (unsigned)H, (unsigned)B);
-  if (dropout_p > 0.f)
-    hipLaunchKernelGGL(attn_bwd_dkv_kernel<true>, grid, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(qkv),
-                       reinterpret_cast<const bf16_t*>(do_masked), head_mask, lse, Dvec, reinterpret_cast<bf16_t*>(dqkv),
-                       key_len, sh, scale, dropout_p, seed);
-  else
-    hipLaunchKernelGGL(attn_bwd_dkv_kernel<false>, grid, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(qkv),
-                       reinterpret_cast<const bf16_t*>(do_masked), head_mask, lse, Dvec, reinterpret_cast<bf16_t*>(dqkv),
-                       key_len, sh, scale, dropout_p, seed);
-  int rc = check_launch("dph_attention_bwd dkv");
-  if (rc) return rc;
-  dim3 grid2((unsigned)cdiv(T, RB), (unsigned)H, (unsigned)B);
-  if (dropout_p > 0.f)
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<true>, grid2, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(qkv),
-                       reinterpret_cast<const bf16_t*>(do_masked), head_mask, lse, Dvec, reinterpret_cast<bf16_t*>(dqkv),
-                       key_len, sh, scale, dropout_p, seed);
-  else
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<false>, grid2, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(qkv),
-                       reinterpret_cast<const bf16_t*>(do_masked), head_mask, lse, Dvec, reinterpret_cast<bf16_t*>(dqkv),
-                       key_len, sh, scale, dropout_p, seed);
-  return check_launch("dph_attention_bwd dq");
+  return attention_bwd(qkv, do_masked, head_mask, lse, Dvec, dqkv, key_len, B, T, H, scale, dropout_p, seed,
+                       RelBias{nullptr, nullptr, nullptr, nullptr}, stream);
+}
+
+extern "C" int dph_attention_bwd_relpos(const void* qkv, const void* do_masked, const float* head_mask,
+                                        const float* lse, const float* Dvec, void* dqkv, const int64_t* key_len,
+                                        const float* rel_tab, const float* gate, float* dgate, float* drel_tab,
+                                        int64_t B, int64_t T, int64_t H, float scale, float dropout_p, uint64_t seed,
+                                        hipStream_t stream) {
+  DPH_REQUIRE(qkv && do_masked && lse && Dvec && dqkv && rel_tab && gate && dgate && drel_tab && B > 0 && T > 0 &&
+                  T <= 4096 && H > 0,
+              "dph_attention_bwd_relpos: bad args (T <= 4096)");
+  return attention_bwd(qkv, do_masked, head_mask, lse, Dvec, dqkv, key_len, B, T, H, scale, dropout_p, seed,
+                       RelBias{rel_tab, gate, dgate, drel_tab}, stream);
 }

@@ -1,0 +1,280 @@
+// WavLM relative-position bias and its GRU-style gate (WavLMSelfAttention, components.py:486-659).
+//
+// The reference materialises position_bias (B*H, T, T) fp32 from an Embedding lookup of bucketed offsets and
+// multiplies it by a per-(b, h, q) gate before adding it to the scores.  Here nothing of size T x T exists:
+//   * dph_relpos_table  -> tab[h][r] = embed[bucket(r - (T-1))][head[h]], r in [0, 2T-1) (one diagonal per r);
+//     the attention kernels add gate[b,h,q] * tab[h][k - q + T - 1] to each score in registers.
+//   * dph_wavlm_gate_fwd -> gate[b][h][t] from the attention input x (Linear(head_dim, 8), 2 groups of 4 summed,
+//     sigmoid, gate = ga * (gb * c[h] - 1) + 2), components.py:637-643.
+//   * backward: the attention dQ kernel emits dgate (row sums of dS * tab) and dtab (diagonal sums of dS * gate);
+//     dph_relpos_table_bwd folds dtab into the embedding gradient, dph_wavlm_gate_bwd turns dgate into
+//     d(gate weights, bias, const) and adds the input gradient into dx.
+#include <cmath>
+
+#include "common.h"
+
+namespace dph {
+namespace {
+
+// components.py:563-600, bidirectional: evaluated in fp32 exactly as the reference (log of the fp32 ratio,
+// divided by log(max_distance / max_exact) rounded to fp32, times (num_buckets - max_exact), truncated).
+__device__ __forceinline__ int relpos_bucket(int rel, int num_buckets, int max_distance, float log_ratio) {
+  const int nb = num_buckets / 2;
+  int out = rel > 0 ? nb : 0;
+  const int r = rel < 0 ? -rel : rel;
+  const int max_exact = nb / 2;
+  if (r < max_exact) return out + r;
+  const float lr = logf((float)r / (float)max_exact);
+  int large = max_exact + (int)((lr / log_ratio) * (float)(nb - max_exact));
+  large = min(large, nb - 1);
+  return out + large;
+}
+
+__global__ void relpos_table_kernel(const float* __restrict__ embed, const int64_t* __restrict__ heads,
+                                    float* __restrict__ tab, int64_t* __restrict__ buckets, int T, int H, int Htot,
+                                    int num_buckets, int max_distance, float log_ratio) {
+  const int R = 2 * T - 1;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= R * H) return;
+  const int h = i / R, r = i % R;
+  const int bk = relpos_bucket(r - (T - 1), num_buckets, max_distance, log_ratio);
+  const int hh = heads ? (int)heads[h] : h;
+  if (tab) tab[i] = embed[(int64_t)bk * Htot + hh];
+  if (buckets && h == 0) buckets[r] = bk;
+}
+
+__global__ void relpos_table_bwd_kernel(const float* __restrict__ dtab, const int64_t* __restrict__ heads,
+                                        float* __restrict__ dembed, int T, int H, int Htot, int num_buckets,
+                                        int max_distance, float log_ratio) {
+  const int R = 2 * T - 1;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= R * H) return;
+  const int h = i / R, r = i % R;
+  const float v = dtab[i];
+  if (v == 0.f) return;
+  const int bk = relpos_bucket(r - (T - 1), num_buckets, max_distance, log_ratio);
+  const int hh = heads ? (int)heads[h] : h;
+  atomicAdd(dembed + (int64_t)bk * Htot + hh, v);
+}
+
+constexpr int HDG = 64;   // gate head dim
+
+struct GateArgs {
+  const bf16_t* x;         // [B*T][ldx], head hh occupies columns hh*64 .. +63
+  int64_t ldx;
+  const float* w;          // [8][64]
+  const float* bias;       // [8]
+  const float* gconst;     // [Htot]
+  const int64_t* heads;    // [H] total-head index of each remaining head (null = identity)
+  int64_t B, T, H;
+};
+
+// logits z[8] of (b, t, head hh) and the two sigmoids
+__device__ __forceinline__ void gate_logits(const GateArgs& a, const float* w_s, int64_t bt, int hh, float (&xv)[HDG],
+                                            float& ga, float& gb) {
+  const bf16_t* xp = a.x + bt * a.ldx + (int64_t)hh * HDG;
+#pragma unroll
+  for (int k = 0; k < HDG; k += 8) {
+    const uint4 v = *reinterpret_cast<const uint4*>(xp + k);
+    const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      xv[k + 2 * q] = __uint_as_float(wv[q] << 16);
+      xv[k + 2 * q + 1] = __uint_as_float(wv[q] & 0xffff0000u);
+    }
+  }
+  float za = 0.f, zb = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float z = a.bias[j];
+#pragma unroll 16
+    for (int d = 0; d < HDG; ++d) z += w_s[j * HDG + d] * xv[d];
+    if (j < 4) za += z; else zb += z;
+  }
+  ga = 1.f / (1.f + __expf(-za));
+  gb = 1.f / (1.f + __expf(-zb));
+}
+
+// one thread per (b, t, h); threads of a block share (b, t) rows of consecutive heads
+__global__ void __launch_bounds__(256) wavlm_gate_fwd_kernel(GateArgs a, float* __restrict__ gate) {
+  __shared__ float w_s[8 * HDG];
+  for (int i = threadIdx.x; i < 8 * HDG; i += 256) w_s[i] = a.w[i];
+  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.B * a.T * a.H) return;
+  const int h = (int)(i % a.H);
+  const int64_t bt = i / a.H;
+  const int hh = a.heads ? (int)a.heads[h] : h;
+  float xv[HDG], ga, gb;
+  gate_logits(a, w_s, bt, hh, xv, ga, gb);
+  const int64_t b = bt / a.T, t = bt % a.T;
+  gate[(b * a.H + h) * a.T + t] = ga * (gb * a.gconst[hh] - 1.f) + 2.f;
+}
+
+// backward, pass 1: per (b, t, h): dz (both groups of 4 share one gradient), dx += dz W, db, dconst; dz -> scratch
+__global__ void __launch_bounds__(256) wavlm_gate_bwd_kernel(GateArgs a, const float* __restrict__ dgate,
+                                                             bf16_t* __restrict__ dx, int64_t lddx,
+                                                             float* __restrict__ dz_out, float* __restrict__ db,
+                                                             float* __restrict__ dconst) {
+  __shared__ float w_s[8 * HDG];
+  for (int i = threadIdx.x; i < 8 * HDG; i += 256) w_s[i] = a.w[i];
+  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const bool live = i < a.B * a.T * a.H;
+  float dza = 0.f, dzb = 0.f, dc = 0.f;
+  int hh = 0;
+  if (live) {
+    const int h = (int)(i % a.H);
+    const int64_t bt = i / a.H;
+    hh = a.heads ? (int)a.heads[h] : h;
+    float xv[HDG], ga, gb;
+    gate_logits(a, w_s, bt, hh, xv, ga, gb);
+    const int64_t b = bt / a.T, t = bt % a.T;
+    const float dg = dgate[(b * a.H + h) * a.T + t];
+    const float c = a.gconst[hh];
+    const float dga = dg * (gb * c - 1.f);
+    const float dgb = dg * ga * c;
+    dc = dg * ga * gb;
+    dza = dga * ga * (1.f - ga);
+    dzb = dgb * gb * (1.f - gb);
+    dz_out[i * 2] = dza;
+    dz_out[i * 2 + 1] = dzb;
+    // dx[d] += sum_j dz_j W[j][d]  (read-modify-write of this head's 64 bf16; heads of a row are disjoint)
+    bf16_t* xp = dx + bt * lddx + (int64_t)hh * HDG;
+#pragma unroll
+    for (int k = 0; k < HDG; k += 8) {
+      uint4 v = *reinterpret_cast<const uint4*>(xp + k);
+      uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float acc[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int d = k + 2 * q + e;
+          float sa = 0.f, sb = 0.f;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            sa += w_s[j * HDG + d];
+            sb += w_s[(j + 4) * HDG + d];
+          }
+          acc[e] = dza * sa + dzb * sb;
+        }
+        wv[q] = pack2bf(__uint_as_float(wv[q] << 16) + acc[0], __uint_as_float(wv[q] & 0xffff0000u) + acc[1]);
+      }
+      *reinterpret_cast<uint4*>(xp + k) = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+    }
+  }
+  // db[j] = sum dz_j (j < 4: dza, else dzb); dconst[hh] += dc
+  const float sa = wave_sum(dza), sb = wave_sum(dzb);
+  if ((threadIdx.x & 63) == 0) {
+    atomicAdd(db + 0, sa);
+    atomicAdd(db + 4, sb);
+  }
+  if (live) atomicAdd(dconst + hh, dc);
+}
+
+// backward, pass 2: dW[j][d] = sum_n dz[n][j/4] x[n][d]; block = 256 rows n, thread (jg = t>>6 in {0..3}, d = t&63)
+// sums a quarter of the rows for both groups, LDS-combined, then atomics (db rows 1-3, 5-7 copied at the end).
+__global__ void __launch_bounds__(256) wavlm_gate_wgrad_kernel(GateArgs a, const float* __restrict__ dz,
+                                                               float* __restrict__ dw) {
+  __shared__ float red[4][2][HDG];
+  const int d = threadIdx.x & 63;
+  const int part = threadIdx.x >> 6;
+  const int64_t N = a.B * a.T * a.H;
+  const int64_t n0 = (int64_t)blockIdx.x * 256;
+  float acc_a = 0.f, acc_b = 0.f;
+  for (int r = part; r < 256; r += 4) {
+    const int64_t n = n0 + r;
+    if (n >= N) break;
+    const int h = (int)(n % a.H);
+    const int64_t bt = n / a.H;
+    const int hh = a.heads ? (int)a.heads[h] : h;
+    const float xv = bf2f(a.x[bt * a.ldx + (int64_t)hh * HDG + d]);
+    acc_a += dz[n * 2] * xv;
+    acc_b += dz[n * 2 + 1] * xv;
+  }
+  red[part][0][d] = acc_a;
+  red[part][1][d] = acc_b;
+  __syncthreads();
+  if (part < 2) {
+    const float v = red[0][part][d] + red[1][part][d] + red[2][part][d] + red[3][part][d];
+    // the 4 logits of a group share the same gradient: one atomic per group row, replicated by dph_wavlm_gate_bwd
+    atomicAdd(dw + (part * 4) * HDG + d, v);
+  }
+}
+
+// dW / db rows of one group are identical (each logit of a group gets the group's gradient): replicate row 0 / 4
+__global__ void wavlm_gate_replicate_kernel(float* __restrict__ dw, float* __restrict__ db, const float* __restrict__ dw0,
+                                            const float* __restrict__ db0) {
+  const int t = threadIdx.x;   // 512 threads: (j, d)
+  const int j = t >> 6, d = t & 63;
+  dw[j * HDG + d] += dw0[(j < 4 ? 0 : 4) * HDG + d];
+  if (d == 0) db[j] += db0[j < 4 ? 0 : 4];
+}
+
+}  // namespace
+}  // namespace dph
+
+using namespace dph;
+
+static float relpos_log_ratio(int64_t num_buckets, int64_t max_distance) {
+  const int64_t max_exact = (num_buckets / 2) / 2;
+  // python float math.log(max_distance / max_exact), rounded to fp32 when it meets the fp32 tensor
+  return (float)std::log((double)max_distance / (double)max_exact);
+}
+
+extern "C" int dph_relpos_table(const float* embed, const int64_t* heads, float* tab, int64_t* buckets, int64_t T,
+                                int64_t H, int64_t Htot, int64_t num_buckets, int64_t max_distance,
+                                hipStream_t stream) {
+  DPH_REQUIRE((tab ? embed != nullptr : true) && (tab || buckets) && T > 0 && T <= 4096 && H > 0 && Htot >= H &&
+                  num_buckets >= 4 && max_distance > num_buckets / 4,
+              "dph_relpos_table: bad args");
+  const int n = (int)((2 * T - 1) * H);
+  hipLaunchKernelGGL(relpos_table_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, stream, embed, heads, tab,
+                     buckets, (int)T, (int)H, (int)Htot, (int)num_buckets, (int)max_distance,
+                     relpos_log_ratio(num_buckets, max_distance));
+  return check_launch("dph_relpos_table");
+}
+
+extern "C" int dph_relpos_table_bwd(const float* dtab, const int64_t* heads, float* dembed, int64_t T, int64_t H,
+                                    int64_t Htot, int64_t num_buckets, int64_t max_distance, hipStream_t stream) {
+  DPH_REQUIRE(dtab && dembed && T > 0 && T <= 4096 && H > 0 && Htot >= H && num_buckets >= 4 &&
+                  max_distance > num_buckets / 4,
+              "dph_relpos_table_bwd: bad args");
+  const int n = (int)((2 * T - 1) * H);
+  hipLaunchKernelGGL(relpos_table_bwd_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, stream, dtab, heads, dembed,
+                     (int)T, (int)H, (int)Htot, (int)num_buckets, (int)max_distance,
+                     relpos_log_ratio(num_buckets, max_distance));
+  return check_launch("dph_relpos_table_bwd");
+}
+
+extern "C" int dph_wavlm_gate_fwd(const void* x, int64_t ldx, const float* w, const float* bias, const float* gconst,
+                                  const int64_t* heads, float* gate, int64_t B, int64_t T, int64_t H, int64_t head_dim,
+                                  hipStream_t stream) {
+  DPH_REQUIRE(x && w && bias && gconst && gate && B > 0 && T > 0 && H > 0 && head_dim == HDG && ldx % 8 == 0,
+              "dph_wavlm_gate_fwd: bad args (head_dim 64, ldx % 8 == 0)");
+  GateArgs a{reinterpret_cast<const bf16_t*>(x), ldx, w, bias, gconst, heads, B, T, H};
+  hipLaunchKernelGGL(wavlm_gate_fwd_kernel, dim3((unsigned)cdiv(B * T * H, 256)), dim3(256), 0, stream, a, gate);
+  return check_launch("dph_wavlm_gate_fwd");
+}
+
+// dx (bf16, ld lddx) is ADDED to; dw [8][64], db [8], dconst [Htot] accumulate; ws = 2*B*T*H + 520 floats
+extern "C" int dph_wavlm_gate_bwd(const void* x, int64_t ldx, const float* w, const float* bias, const float* gconst,
+                                  const int64_t* heads, const float* dgate, void* dx, int64_t lddx, float* dw,
+                                  float* db, float* dconst, float* ws, int64_t B, int64_t T, int64_t H,
+                                  int64_t head_dim, hipStream_t stream) {
+  DPH_REQUIRE(x && w && bias && gconst && dgate && dx && dw && db && dconst && ws && B > 0 && T > 0 && H > 0 &&
+                  head_dim == HDG && ldx % 8 == 0 && lddx % 8 == 0,
+              "dph_wavlm_gate_bwd: bad args");
+  GateArgs a{reinterpret_cast<const bf16_t*>(x), ldx, w, bias, gconst, heads, B, T, H};
+  const int64_t N = B * T * H;
+  float* dz = ws;
+  float* dw0 = ws + 2 * N;          // [8][64] (rows 0 and 4 used)
+  float* db0 = dw0 + 8 * HDG;       // [8]
+  if (hipMemsetAsync(dw0, 0, (8 * HDG + 8) * sizeof(float), stream) != hipSuccess) return check_launch("dph_wavlm_gate_bwd memset");
+  hipLaunchKernelGGL(wavlm_gate_bwd_kernel, dim3((unsigned)cdiv(N, 256)), dim3(256), 0, stream, a, dgate,
+                     reinterpret_cast<bf16_t*>(dx), lddx, dz, db0, dconst);
+  hipLaunchKernelGGL(wavlm_gate_wgrad_kernel, dim3((unsigned)cdiv(N, 256)), dim3(256), 0, stream, a, dz, dw0);
+  hipLaunchKernelGGL(wavlm_gate_replicate_kernel, dim3(1), dim3(512), 0, stream, dw, db, dw0, db0);
+  return check_launch("dph_wavlm_gate_bwd");
+}

@@ -1057,6 +1057,33 @@ class PosConvFn(torch.autograd.Function):
 # ---------------------------------------------------------------------------
 # Encoder layer (post-norm; HuBERT/wav2vec2 Base)
 # ---------------------------------------------------------------------------
+class RelPosTableFn(torch.autograd.Function):
+    """WavLM position bias (compute_bias, components.py:546-561) as one value per diagonal:
+    embed [num_buckets][H] fp32 -> rel_tab [H][2T-1] fp32, rel_tab[h][r] = embed[bucket(r-(T-1))][h].
+    Backward scatters the diagonal gradients back into the embedding rows (Embedding backward)."""
+
+    @staticmethod
+    def forward(ctx, embed, T, num_buckets, max_distance):
+        if not embed.is_cuda:
+            raise ValueError("RelPosTableFn: the HIP path needs device tensors")
+        Htot = embed.shape[1]
+        e = embed.detach().contiguous()
+        tab = torch.empty(Htot, 2 * T - 1, dtype=F32, device=embed.device)
+        call("dph_relpos_table", ptr(e), None, ptr(tab), None, T, Htot, Htot, num_buckets, max_distance, _s())
+        ctx.meta = (embed, T, num_buckets, max_distance)
+        return tab
+
+    @staticmethod
+    def backward(ctx, dtab):
+        embed, T, nb, md = ctx.meta
+        go = GradOut(embed.device)
+        de, _ = go.buf(embed)
+        call("dph_relpos_table_bwd", ptr(dtab.contiguous()), None, ptr(de), T, embed.shape[1], embed.shape[1], nb, md,
+             _s())
+        go.done()
+        return go.ret(embed), None, None, None
+
+
 class EncoderLayerFn(torch.autograd.Function):
     """h (B*T, D) bf16 -> layer output (B*T, D) bf16.
 
@@ -1067,7 +1094,8 @@ class EncoderLayerFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, cfg, h, wq, wk, wv, bq, bk, bv, wo, bo, ln1_w, ln1_b, w1, b1, w2, b2, ln2_w, ln2_b, hm, lma,
-                im, lmf):
+                im, lmf, rel_tab=None, gw=None, gb=None, gc=None, heads=None):
+        ctx.wl = dict(rel_tab=rel_tab, gw=gw, gb=gb, gc=gc, heads=heads) if rel_tab is not None else None
         if cfg.get("pre_norm"):
             return EncoderLayerFn._forward_pre(ctx, cfg, h, wq, wk, wv, bq, bk, bv, wo, bo, ln1_w, ln1_b, w1, b1, w2,
                                                b2, ln2_w, ln2_b, hm, lma, im, lmf)
@@ -1089,8 +1117,7 @@ class EncoderLayerFn(torch.autograd.Function):
             o_m = torch.empty(M, Dh, dtype=BF16, device=dev)
             lse = torch.empty(B * H * T, dtype=F32, device=dev)
             seed_a = SEEDS.next() if cfg["p_attn"] > 0 else 0
-            call("dph_attention_fwd", ptr(qkv), ptr(o_u), ptr(o_m), ptr(lse), ptr(hm), ptr(cfg["lengths"]), B, T, H,
-                 cfg["head_dim"] ** -0.5, cfg["p_attn"], seed_a, _s())
+            sv["gate"] = EncoderLayerFn._attention_fwd(ctx, cfg, h, qkv, o_u, o_m, lse, hm, seed_a)
             Wo = bf16_image(wo)
             seed_d = SEEDS.next() if cfg["p_drop"] > 0 else 0
             a_pre = torch.empty(M, D, dtype=BF16, device=dev) if (need and lma is not None) else None
@@ -1164,8 +1191,7 @@ class EncoderLayerFn(torch.autograd.Function):
             o_m = torch.empty(M, Dh, dtype=BF16, device=dev)
             lse = torch.empty(B * H * T, dtype=F32, device=dev)
             seed_a = SEEDS.next() if cfg["p_attn"] > 0 else 0
-            call("dph_attention_fwd", ptr(qkv), ptr(o_u), ptr(o_m), ptr(lse), ptr(hm), ptr(cfg["lengths"]), B, T, H,
-                 cfg["head_dim"] ** -0.5, cfg["p_attn"], seed_a, _s())
+            sv["gate"] = EncoderLayerFn._attention_fwd(ctx, cfg, xn1, qkv, o_u, o_m, lse, hm, seed_a)
             Wo = bf16_image(wo)
             seed_d = SEEDS.next() if cfg["p_drop"] > 0 else 0
             a_pre = torch.empty(M, D, dtype=BF16, device=dev) if (need and lma is not None) else None
@@ -1261,13 +1287,13 @@ class EncoderLayerFn(torch.autograd.Function):
             g["hm"] = z(H) if has_hm else None
             call("dph_attention_bwd_prep", ptr(do_m), ptr(sv["o_u"]), ptr(hm), ptr(Dvec), ptr(g["hm"]), B, T, H, _s())
             dqkv = torch.empty_like(sv["qkv"])
-            call("dph_attention_bwd", ptr(sv["qkv"]), ptr(do_m), ptr(hm), ptr(sv["lse"]), ptr(Dvec), ptr(dqkv),
-                 ptr(cfg["lengths"]), B, T, H, cfg["head_dim"] ** -0.5, cfg["p_attn"], sv["seed_a"], _s())
+            wl_g = EncoderLayerFn._attention_bwd(ctx, cfg, sv, do_m, hm, Dvec, dqkv)
             dbqkv, _ = go.buf(pr["bq"], pr["bk"], pr["bv"])
             call("dph_colsum", ptr(dqkv), ptr(dbqkv), M, dqkv.shape[1], *colsum_ws(M, dqkv.shape[1], dev), _s())
             dwqkv, direct = go.buf(pr["wq"], pr["wk"], pr["wv"], zero=False)
             k4 = K.linear_wgrad(dqkv, xn1, dwqkv, accumulate=direct)
             dxn1 = K.linear_dgrad(dqkv, sv["Wqkv"], w_t=t_image(sv["Wqkv"]))
+            EncoderLayerFn._gate_bwd(ctx, cfg, xn1, dxn1, wl_g, go)
             dh = torch.empty_like(dout)
             dln1w, _ = go.buf(pr["ln1_w"])
             dln1b, _ = go.buf(pr["ln1_b"])
@@ -1281,7 +1307,68 @@ class EncoderLayerFn(torch.autograd.Function):
         order = ["wq", "wk", "wv", "bq", "bk", "bv", "wo", "bo", "ln1_w", "ln1_b", "w1", "b1", "w2", "b2", "ln2_w",
                  "ln2_b"]
         return (None, dh) + tuple(go.ret(pr[k]) for k in order) + (g.get("hm"), g.get("lma"), g.get("im"),
-                                                                    g.get("lmf"))
+                                                                    g.get("lmf")) + EncoderLayerFn._wl_ret(ctx, go)
+
+    # ---------------- WavLM gated relative-position bias (components.py:629-651) ----------------
+    @staticmethod
+    def _attention_fwd(ctx, cfg, x_att, qkv, o_u, o_m, lse, hm, seed_a):
+        """Attention forward; with a WavLM bias the per-query gate is computed from the attention input first
+        (dph_wavlm_gate_fwd) and the kernels add gate * rel_tab[k-q] to the scores.  Returns the gate."""
+        B, T, H = cfg["B"], cfg["T"], cfg["H"]
+        wl = ctx.wl
+        if wl is None:
+            call("dph_attention_fwd", ptr(qkv), ptr(o_u), ptr(o_m), ptr(lse), ptr(hm), ptr(cfg["lengths"]), B, T, H,
+                 cfg["head_dim"] ** -0.5, cfg["p_attn"], seed_a, _s())
+            return None
+        if cfg["head_dim"] != 64:
+            raise NotImplementedError("WavLM gate: head_dim 64 only")
+        gate = torch.empty(B * H * T, dtype=F32, device=qkv.device)
+        call("dph_wavlm_gate_fwd", ptr(x_att), x_att.shape[1], ptr(wl["gw"]), ptr(wl["gb"]), ptr(wl["gc"]),
+             ptr(wl["heads"]), ptr(gate), B, T, H, 64, _s())
+        wl["rel_tab"] = wl["rel_tab"].contiguous()
+        call("dph_attention_fwd_relpos", ptr(qkv), ptr(o_u), ptr(o_m), ptr(lse), ptr(hm), ptr(cfg["lengths"]),
+             ptr(wl["rel_tab"]), ptr(gate), B, T, H, cfg["head_dim"] ** -0.5, cfg["p_attn"], seed_a, _s())
+        return gate
+
+    @staticmethod
+    def _attention_bwd(ctx, cfg, sv, do_m, hm, Dvec, dqkv):
+        B, T, H = cfg["B"], cfg["T"], cfg["H"]
+        wl = ctx.wl
+        if wl is None:
+            call("dph_attention_bwd", ptr(sv["qkv"]), ptr(do_m), ptr(hm), ptr(sv["lse"]), ptr(Dvec), ptr(dqkv),
+                 ptr(cfg["lengths"]), B, T, H, cfg["head_dim"] ** -0.5, cfg["p_attn"], sv["seed_a"], _s())
+            return None
+        dev = dqkv.device
+        dgate = torch.empty(B * H * T, dtype=F32, device=dev)
+        dtab = torch.zeros(wl["rel_tab"].shape, dtype=F32, device=dev)
+        call("dph_attention_bwd_relpos", ptr(sv["qkv"]), ptr(do_m), ptr(hm), ptr(sv["lse"]), ptr(Dvec), ptr(dqkv),
+             ptr(cfg["lengths"]), ptr(wl["rel_tab"]), ptr(sv["gate"]), ptr(dgate), ptr(dtab), B, T, H,
+             cfg["head_dim"] ** -0.5, cfg["p_attn"], sv["seed_a"], _s())
+        return dgate, dtab
+
+    @staticmethod
+    def _gate_bwd(ctx, cfg, x_att, dx_att, wl_g, go):
+        """The gate's backward: its input gradient is added into dx_att (the attention input's gradient)."""
+        wl = ctx.wl
+        if wl is None:
+            return
+        B, T, H = cfg["B"], cfg["T"], cfg["H"]
+        dgate, dtab = wl_g
+        dgw, _ = go.buf(wl["gw"])
+        dgb, _ = go.buf(wl["gb"])
+        dgc, _ = go.buf(wl["gc"])
+        ws = torch.empty(2 * B * T * H + 520, dtype=F32, device=dx_att.device)
+        call("dph_wavlm_gate_bwd", ptr(x_att), x_att.shape[1], ptr(wl["gw"]), ptr(wl["gb"]), ptr(wl["gc"]),
+             ptr(wl["heads"]), ptr(dgate), ptr(dx_att), dx_att.shape[1], ptr(dgw), ptr(dgb), ptr(dgc), ptr(ws),
+             B, T, H, 64, _s())
+        wl["dtab"] = dtab
+
+    @staticmethod
+    def _wl_ret(ctx, go):
+        wl = ctx.wl
+        if wl is None:
+            return (None,) * 5
+        return (wl.get("dtab"), go.ret(wl["gw"]), go.ret(wl["gb"]), go.ret(wl["gc"]), None)
 
     @staticmethod
     def backward(ctx, dout):
@@ -1345,13 +1432,13 @@ class EncoderLayerFn(torch.autograd.Function):
             g["hm"] = z(H) if has_hm else None
             call("dph_attention_bwd_prep", ptr(do_m), ptr(sv["o_u"]), ptr(hm), ptr(Dvec), ptr(g["hm"]), B, T, H, _s())
             dqkv = torch.empty_like(sv["qkv"])
-            call("dph_attention_bwd", ptr(sv["qkv"]), ptr(do_m), ptr(hm), ptr(sv["lse"]), ptr(Dvec), ptr(dqkv),
-                 ptr(cfg["lengths"]), B, T, H, cfg["head_dim"] ** -0.5, cfg["p_attn"], sv["seed_a"], _s())
+            wl_g = EncoderLayerFn._attention_bwd(ctx, cfg, sv, do_m, hm, Dvec, dqkv)
             dbqkv, _ = go.buf(pr["bq"], pr["bk"], pr["bv"])
             call("dph_colsum", ptr(dqkv), ptr(dbqkv), M, dqkv.shape[1], *colsum_ws(M, dqkv.shape[1], dev), _s())
             dwqkv, direct = go.buf(pr["wq"], pr["wk"], pr["wv"], zero=False)
             k4 = K.linear_wgrad(dqkv, h, dwqkv, accumulate=direct)
             dh = K.linear_dgrad(dqkv, sv["Wqkv"], w_t=t_image(sv["Wqkv"]), residual=ds1)
+            EncoderLayerFn._gate_bwd(ctx, cfg, h, dh, wl_g, go)
             del k3, k4
         else:
             call("dph_layernorm_bwd", ptr(dh1), ptr(s1), None, ptr(ln1_w), ptr(mu1), ptr(rs1), ptr(ds1),
@@ -1362,7 +1449,7 @@ class EncoderLayerFn(torch.autograd.Function):
         order = ["wq", "wk", "wv", "bq", "bk", "bv", "wo", "bo", "ln1_w", "ln1_b", "w1", "b1", "w2", "b2", "ln2_w",
                  "ln2_b"]
         return (None, dh) + tuple(go.ret(pr[k]) for k in order) + (g.get("hm"), g.get("lma"), g.get("im"),
-                                                                    g.get("lmf"))
+                                                                    g.get("lmf")) + EncoderLayerFn._wl_ret(ctx, go)
 
 
 # ---------------------------------------------------------------------------

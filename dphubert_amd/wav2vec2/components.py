@@ -345,6 +345,72 @@ class SelfAttention(Module):
         return new_config
 
 
+class WavLMSelfAttention(SelfAttention):
+    """WavLM attention (components.py:486-693): SelfAttention over ``remaining_heads`` of ``total_num_heads`` plus
+    the gated relative-position bias.  Layer 0 owns ``rel_attn_embed`` (num_buckets x total heads); its bucketed
+    table (``ops.RelPosTableFn``, one value per diagonal) is the ``position_bias`` handed to every later layer,
+    and each layer gates it per query (``gru_rel_pos_linear`` / ``gru_rel_pos_const``) inside the attention
+    kernels -- no (B*H, T, T) tensor is built.  Parameter names and registration order follow the reference."""
+
+    def __init__(self, embed_dim: int, total_num_heads: int, remaining_heads: Optional[List[int]] = None,
+                 dropout: float = 0.0, bias: bool = True, has_relative_attention_bias: bool = False,
+                 num_buckets: int = 32, max_distance: int = 128, gru_rel_pos: bool = True,
+                 prune_heads: bool = False, prune_layer: bool = False):
+        self.total_num_heads = total_num_heads
+        self.remaining_heads = list(range(total_num_heads)) if remaining_heads is None else list(remaining_heads)
+        head_dim = embed_dim // total_num_heads
+        super().__init__(embed_dim, len(self.remaining_heads), head_dim, dropout, prune_heads, prune_layer)
+        if not bias:
+            raise NotImplementedError("WavLMSelfAttention(bias=False): the reference builder always uses bias")
+        if not gru_rel_pos:
+            raise NotImplementedError("WavLMSelfAttention(gru_rel_pos=False): the reference builder always gates")
+        self.has_relative_attention_bias = has_relative_attention_bias
+        self.num_buckets = num_buckets
+        self.max_distance = max_distance
+        self.rel_attn_embed = nn.Embedding(num_buckets, total_num_heads) if has_relative_attention_bias else None
+        self.gru_rel_pos = gru_rel_pos
+        self.gru_rel_pos_linear = nn.Linear(head_dim, 8)
+        self.gru_rel_pos_const = nn.Parameter(torch.ones(1, total_num_heads, 1, 1))
+        self.has_position_bias = True
+        self._heads_dev = None
+
+    def heads_tensor(self, dev) -> Optional[Tensor]:
+        """int64 device tensor of the remaining heads' indices (None when every head remains)."""
+        if self.remaining_heads == list(range(self.total_num_heads)):
+            return None
+        if self._heads_dev is None or self._heads_dev.device != dev:
+            self._heads_dev = torch.tensor(self.remaining_heads, dtype=torch.int64, device=dev)
+        return self._heads_dev
+
+    def prune(self):
+        """components.py:661-693 (``remaining_heads`` = nonzero head-mask indices, as the reference)."""
+        new_config = {"use_attention": True, "remaining_heads": self.remaining_heads}
+        if self.hard_concrete_for_layer is not None:
+            assert not self.hard_concrete_for_layer.training
+            layer_mask = self.hard_concrete_for_layer()
+            self.out_proj.weight.data *= layer_mask
+            self.out_proj.bias.data *= layer_mask
+            if layer_mask == 0:
+                new_config["use_attention"] = False
+            self.hard_concrete_for_layer = None
+        if self.hard_concrete_for_heads is not None:
+            assert not self.hard_concrete_for_heads.training
+            head_mask = self.hard_concrete_for_heads()
+            new_config["remaining_heads"] = head_mask.nonzero().squeeze(-1).tolist()
+            if len(new_config["remaining_heads"]) == 0:
+                new_config["use_attention"] = False
+            else:
+                full_mask = head_mask.repeat_interleave(self.head_dim)
+                full_index = full_mask.nonzero().squeeze(-1)
+                prune_linear_layer(self.k_proj, full_index, "output")
+                prune_linear_layer(self.v_proj, full_index, "output")
+                prune_linear_layer(self.q_proj, full_index, "output")
+                self.out_proj.weight.data *= full_mask
+                prune_linear_layer(self.out_proj, full_index, "input")
+            self.hard_concrete_for_heads = None
+        return new_config
+
+
 class FeedForward(Module):
     """Linear -> GELU -> dropout -> x interm mask -> Linear -> dropout -> x layer mask (components.py:696-791)."""
 
@@ -441,6 +507,18 @@ class EncoderLayer(Module):
         }
         if ff is not None and tr and ff.output_dropout.p != self.dropout.p:
             raise NotImplementedError("FFN output dropout != layer dropout")
+        rel_tab = gw = gb = gc = heads = None
+        if isinstance(att, WavLMSelfAttention):
+            # components.py:629-631: only the layer owning the embedding builds the bias, and only when none was
+            # handed in (a dropped layer 0 leaves every later layer without one, as in the reference)
+            if att.rel_attn_embed is not None and position_bias is None:
+                position_bias = ops.RelPosTableFn.apply(att.rel_attn_embed.weight, T, att.num_buckets,
+                                                        att.max_distance)
+            if position_bias is not None:
+                heads = att.heads_tensor(x.device)
+                rel_tab = position_bias if heads is None else position_bias.index_select(0, heads)
+                gw, gb, gc = att.gru_rel_pos_linear.weight, att.gru_rel_pos_linear.bias, att.gru_rel_pos_const
+                cfg["wavlm"] = True
         a = att
         out = ops.EncoderLayerFn.apply(
             cfg, x.reshape(B * T, D),
@@ -450,7 +528,7 @@ class EncoderLayer(Module):
             self.layer_norm.weight, self.layer_norm.bias,
             ff.intermediate_dense.weight if ff else None, ff.intermediate_dense.bias if ff else None,
             ff.output_dense.weight if ff else None, ff.output_dense.bias if ff else None,
-            self.final_layer_norm.weight, self.final_layer_norm.bias, hm, lma, im, lmf)
+            self.final_layer_norm.weight, self.final_layer_norm.bias, hm, lma, im, lmf, rel_tab, gw, gb, gc, heads)
         return out.view(B, T, D), position_bias
 
     def get_num_params(self):
@@ -605,6 +683,36 @@ def _get_feature_extractor(norm_mode: str, shapes: List[Tuple[int, int, int]], b
                                      prune_conv_channels=prune_conv_channels))
         in_channels = out_channels
     return FeatureExtractor(nn.ModuleList(blocks))
+
+
+def _get_wavlm_encoder(in_features: int, embed_dim: int, dropout_input: float, pos_conv_kernel: int,
+                       pos_conv_groups: int, num_layers: int, use_attention: List[bool], use_feed_forward: List[bool],
+                       total_num_heads: List[int], remaining_heads: List[List[int]], num_buckets: int,
+                       max_distance: int, attention_dropout: float, ff_interm_features: List[int],
+                       ff_interm_dropout: float, dropout: float, layer_norm_first: bool, layer_drop: float,
+                       prune_attention_heads: bool = False, prune_attention_layer: bool = False,
+                       prune_feed_forward_intermediate: bool = False,
+                       prune_feed_forward_layer: bool = False) -> Encoder:
+    """components.py:1289-1386: the wav2vec2 encoder with WavLMSelfAttention (relative-position embedding in
+    layer 0 only)."""
+    feature_projection = FeatureProjection(in_features, embed_dim, dropout_input)
+    pos_conv = ConvolutionalPositionalEmbedding(embed_dim, pos_conv_kernel, pos_conv_groups)
+    encoder_layers = nn.ModuleList()
+    for i in range(num_layers):
+        attention = WavLMSelfAttention(embed_dim=embed_dim, total_num_heads=total_num_heads[i],
+                                       remaining_heads=remaining_heads[i], dropout=attention_dropout,
+                                       has_relative_attention_bias=(i == 0), num_buckets=num_buckets,
+                                       max_distance=max_distance, prune_heads=prune_attention_heads,
+                                       prune_layer=prune_attention_layer) if use_attention[i] else None
+        feed_forward = FeedForward(io_features=embed_dim, intermediate_features=ff_interm_features[i],
+                                   intermediate_dropout=ff_interm_dropout, output_dropout=dropout,
+                                   prune_intermediate=prune_feed_forward_intermediate,
+                                   prune_layer=prune_feed_forward_layer) if use_feed_forward[i] else None
+        encoder_layers.append(EncoderLayer(attention=attention, dropout=dropout, layer_norm_first=layer_norm_first,
+                                           feed_forward=feed_forward, embed_dim=embed_dim))
+    transformer = Transformer(pos_conv_embed=pos_conv, dropout=dropout, layers=encoder_layers,
+                              layer_norm_first=not layer_norm_first, layer_drop=layer_drop)
+    return Encoder(feature_projection, transformer)
 
 
 def _get_encoder(in_features: int, embed_dim: int, dropout_input: float, pos_conv_kernel: int,

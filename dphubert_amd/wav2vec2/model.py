@@ -105,8 +105,63 @@ class Wav2Vec2Model(Module):
 def wav2vec2_model(**configs) -> Wav2Vec2Model:
     """Wraps the original wav2vec2_model (model.py:172-178)."""
     if "encoder_remaining_heads" in configs:
-        raise NotImplementedError("WavLM models (encoder_remaining_heads) are outside the HIP hot path (SURVEY 8f)")
+        return wavlm_model(**configs)
     return wav2vec2_model_original(**configs)
+
+
+def wavlm_model(
+    extractor_mode: str,
+    extractor_conv_layer_config: Optional[List[Tuple[int, int, int]]],
+    extractor_conv_bias: bool,
+    encoder_embed_dim: int,
+    encoder_projection_dropout: float,
+    encoder_pos_conv_kernel: int,
+    encoder_pos_conv_groups: int,
+    encoder_num_layers: int,
+    encoder_use_attention: List[bool],
+    encoder_use_feed_forward: List[bool],
+    encoder_total_num_heads: List[int],
+    encoder_remaining_heads: List[List[int]],
+    encoder_num_buckets: int,
+    encoder_max_distance: int,
+    encoder_attention_dropout: float,
+    encoder_ff_interm_features: List[int],
+    encoder_ff_interm_dropout: float,
+    encoder_dropout: float,
+    encoder_layer_norm_first: bool,
+    encoder_layer_drop: float,
+    aux_num_out: Optional[int],
+    normalize_waveform: bool,
+    extractor_prune_conv_channels: bool = False,
+    encoder_prune_attention_heads: bool = False,
+    encoder_prune_attention_layer: bool = False,
+    encoder_prune_feed_forward_intermediate: bool = False,
+    encoder_prune_feed_forward_layer: bool = False,
+) -> Wav2Vec2Model:
+    """model.py:736-862 (same arguments, same defaults): WavLM = wav2vec2 frontend + encoder with
+    WavLMSelfAttention."""
+    if extractor_conv_layer_config is None:
+        extractor_conv_layer_config = [(512, 10, 5)] + [(512, 3, 2)] * 4 + [(512, 2, 2)] * 2
+    extractor_conv_layer_config = [tuple(c) for c in extractor_conv_layer_config]
+    feature_extractor = components._get_feature_extractor(
+        extractor_mode, extractor_conv_layer_config, extractor_conv_bias,
+        prune_conv_channels=extractor_prune_conv_channels)
+    encoder = components._get_wavlm_encoder(
+        in_features=extractor_conv_layer_config[-1][0], embed_dim=encoder_embed_dim,
+        dropout_input=encoder_projection_dropout, pos_conv_kernel=encoder_pos_conv_kernel,
+        pos_conv_groups=encoder_pos_conv_groups, num_layers=encoder_num_layers, use_attention=encoder_use_attention,
+        use_feed_forward=encoder_use_feed_forward, total_num_heads=encoder_total_num_heads,
+        remaining_heads=encoder_remaining_heads, num_buckets=encoder_num_buckets, max_distance=encoder_max_distance,
+        attention_dropout=encoder_attention_dropout, ff_interm_features=encoder_ff_interm_features,
+        ff_interm_dropout=encoder_ff_interm_dropout, dropout=encoder_dropout,
+        layer_norm_first=encoder_layer_norm_first, layer_drop=encoder_layer_drop,
+        prune_attention_heads=encoder_prune_attention_heads, prune_attention_layer=encoder_prune_attention_layer,
+        prune_feed_forward_intermediate=encoder_prune_feed_forward_intermediate,
+        prune_feed_forward_layer=encoder_prune_feed_forward_layer)
+    aux = None
+    if aux_num_out is not None:
+        aux = torch.nn.Linear(in_features=encoder_embed_dim, out_features=aux_num_out)
+    return Wav2Vec2Model(normalize_waveform, feature_extractor, encoder, aux)
 
 
 def wav2vec2_model_original(

@@ -171,6 +171,44 @@ int dph_attention_bwd(const void* qkv, const void* do_masked, const float* head_
                       float scale, float dropout_p, uint64_t seed, hipStream_t stream);
 
 /* ------------------------------------------------------------------------ *
+ * WavLM gated relative-position bias (WavLMSelfAttention, components.py:486-659).
+ * The reference builds position_bias (B*H,T,T) = Embedding(bucket(k-q)) in
+ * layer 0 (compute_bias :546-561, _relative_positions_bucket :563-600), passes
+ * it to every layer, multiplies it per layer by the gate of :637-644 and adds
+ * it to the scores (:649-651 -> SelfAttention :413).  Here no T x T tensor
+ * exists: rel_tab [H][2T-1] fp32 is one value per diagonal r = k-q+T-1 for each
+ * remaining head, gate [B][H][T] fp32 one value per query row.
+ * ------------------------------------------------------------------------ */
+/* attention forward with score += gate[b,h,q] * rel_tab[h][k-q+T-1] (T <= 4096) */
+int dph_attention_fwd_relpos(const void* qkv, void* o_unmasked, void* o_masked, float* lse, const float* head_mask,
+                             const int64_t* key_len, const float* rel_tab, const float* gate, int64_t B, int64_t T,
+                             int64_t H, float scale, float dropout_p, uint64_t seed, hipStream_t stream);
+/* its backward: dqkv as dph_attention_bwd, plus dgate [B][H][T] (written) = sum_k dS*rel_tab and
+ * drel_tab [H][2T-1] (ACCUMULATED, zero it first) = diagonal sums of dS*gate */
+int dph_attention_bwd_relpos(const void* qkv, const void* do_masked, const float* head_mask, const float* lse,
+                             const float* Dvec, void* dqkv, const int64_t* key_len, const float* rel_tab,
+                             const float* gate, float* dgate, float* drel_tab, int64_t B, int64_t T, int64_t H,
+                             float scale, float dropout_p, uint64_t seed, hipStream_t stream);
+/* rel_tab[h][r] = embed[bucket(r-(T-1))][heads[h]] (embed [num_buckets][Htot] fp32; heads [H] int64 or NULL =
+ * identity); buckets [2T-1] int64 (optional) receives the bucket index table; either output may be NULL */
+int dph_relpos_table(const float* embed, const int64_t* heads, float* rel_tab, int64_t* buckets, int64_t T,
+                     int64_t H, int64_t Htot, int64_t num_buckets, int64_t max_distance, hipStream_t stream);
+/* dembed[bucket][heads[h]] += drel_tab[h][r] (the Embedding backward) */
+int dph_relpos_table_bwd(const float* drel_tab, const int64_t* heads, float* dembed, int64_t T, int64_t H,
+                         int64_t Htot, int64_t num_buckets, int64_t max_distance, hipStream_t stream);
+/* gate[b][h][t] = ga*(gb*gconst[hh]-1)+2, (ga, gb) = sigmoid of the 2 group sums of Linear(64, 8)(x[b,t,hh*64:+64])
+ * (components.py:637-643; x bf16 [B*T][ldx], hh = heads[h]) */
+int dph_wavlm_gate_fwd(const void* x, int64_t ldx, const float* w, const float* bias, const float* gconst,
+                       const int64_t* heads, float* gate, int64_t B, int64_t T, int64_t H, int64_t head_dim,
+                       hipStream_t stream);
+/* its backward: dx (bf16, ld lddx) += the gate's input gradient; dw [8][64], db [8], dconst [Htot] ACCUMULATE;
+ * ws: (2*B*T*H + 520) floats */
+int dph_wavlm_gate_bwd(const void* x, int64_t ldx, const float* w, const float* bias, const float* gconst,
+                       const int64_t* heads, const float* dgate, void* dx, int64_t lddx, float* dw, float* db,
+                       float* dconst, float* ws, int64_t B, int64_t T, int64_t H, int64_t head_dim,
+                       hipStream_t stream);
+
+/* ------------------------------------------------------------------------ *
  * Conv frontend (FeatureExtractor, components.py:94-120, 158-185,
  * 1071-1076): conv0 (1 -> C, kernel k0, stride s0, no bias) + GroupNorm(C,C)
  * + GELU + HardConcrete channel mask, output channels-last bf16 [B][L][C].
