@@ -116,6 +116,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=16, help="utterances per GPU (run.sh: 160 s per GPU)")
     ap.add_argument("--seconds", type=float, default=10.0)
+    ap.add_argument("--model", choices=["hubert-base", "wavlm-base"], default="hubert-base",
+                    help="teacher/student family (the headline metric is quoted on hubert-base)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--traffic", choices=["auto", "off"], default="auto",
@@ -144,11 +146,12 @@ def main():
 
     from dphubert_amd import ops
     from dphubert_amd.kernels import LaunchProfiler
-    from dphubert_amd.synthetic import HUBERT_BASE_CONFIG, synthetic_batch
+    from dphubert_amd.synthetic import HUBERT_BASE_CONFIG, WAVLM_BASE_CONFIG, synthetic_batch
     from dphubert_amd.trainer import Trainer, build_distill_module
 
     ops.manual_seed(2022 + rank)
-    module = build_distill_module(HUBERT_BASE_CONFIG, pruning_units="conv,head,interm", distill_layers="0.4,8,12",
+    model_cfg = WAVLM_BASE_CONFIG if args.model == "wavlm-base" else HUBERT_BASE_CONFIG
+    module = build_distill_module(model_cfg, pruning_units="conv,head,interm", distill_layers="0.4,8,12",
                                   use_reg=True)
     module.global_step = 5000            # target sparsity reached (0.75)
     module = module.to(dev)
@@ -204,8 +207,9 @@ def main():
     log(f"loss {loss.item():.5f}  step {ms:.2f} ms  {value:.1f} audio-s/s  "
         f"({FLOP_PER_UTT_BASE * args.batch * args.seconds / 10 / (ms / 1e3) / 1e12:.0f} TFLOP/s algorithmic/GPU)")
 
+    fam = "WavLM-Base" if args.model == "wavlm-base" else "HuBERT-Base"
     out = {
-        "metric": "audio-seconds/sec/node (HuBERT-Base distill step, 10s utts)",
+        "metric": f"audio-seconds/sec/node ({fam} distill step, 10s utts)",
         "value": round(value, 2),
         "unit": "audio-seconds/sec",
         "n_gpus": world,
@@ -216,8 +220,8 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "bf16",
-        "data": "synthetic (0.1*randn 16 kHz waveforms, seeded random-init HuBERT-Base weights)",
-        "config": {"workload": "distill.py step: HuBERT-Base teacher (eval) + student (train, HardConcrete "
+        "data": f"synthetic (0.1*randn 16 kHz waveforms, seeded random-init {fam} weights)",
+        "config": {"workload": f"distill.py step: {fam} teacher (eval) + student (train, HardConcrete "
                                "conv,head,interm, dropout) + L1/cos distill loss + sparsity Lagrangian + AdamW",
                    "utterances_per_gpu": args.batch, "seconds_per_utt": args.seconds,
                    "global_batch_audio_s": world * args.batch * args.seconds, "distill_layers": "0.4,8,12",

@@ -56,6 +56,12 @@ HUBERT_BASE_CONFIG = dict(
     encoder_prune_feed_forward_layer=False,
 )
 
+# WavLM Base (model.py:865-914 wavlm_base; convert_wavlm_from_hf.py config layout: total + remaining heads per layer,
+# 320 relative-position buckets up to 800 frames)
+WAVLM_BASE_CONFIG = {k: v for k, v in HUBERT_BASE_CONFIG.items() if k not in ("encoder_num_heads", "encoder_head_dim")}
+WAVLM_BASE_CONFIG.update(encoder_total_num_heads=[12] * 12, encoder_remaining_heads=[list(range(12))] * 12,
+                         encoder_num_buckets=320, encoder_max_distance=800)
+
 # wav2vec2-large teacher of run_large.sh (convert_wav2vec2_large_from_fairseq.py:19-40)
 HUBERT_LARGE_CONFIG = dict(
     HUBERT_BASE_CONFIG,

@@ -69,3 +69,29 @@ def test_prune_checkpoint_round_trip(tmp_path):
     pm2 = load_pruned_model(tmp_path / "final" / "pruned_hubert_base.pth")
     for (a, x), (b, y) in zip(pm.state_dict().items(), pm2.state_dict().items()):
         assert a == b and torch.equal(x, y)
+
+
+def test_wavlm_prune_matches_reference():
+    """WavLM prune (components.py:661-693: remaining_heads lists) vs the reference's prune() (fixture g9), and
+    the oracle's forward of the pruned architecture vs the reference's pruned model on a padded batch."""
+    from oracle import hubert_ref as ref
+    fx = load_golden("g9_wavlm_prune.pt")
+    m = _model(fx)
+    pcfg = prune_config(m, fx["cfg"])
+    assert pcfg["encoder_remaining_heads"] == fx["remaining_heads"]
+    assert "encoder_num_heads" not in pcfg
+    assert [list(x) for x in pcfg["extractor_conv_layer_config"]] == fx["conv_config"]
+    assert pcfg["encoder_use_attention"] == fx["use_attention"]
+    assert pcfg["encoder_ff_interm_features"] == fx["ff_interm_features"]
+    sd = m.state_dict()
+    assert set(sd) == set(fx["state_dict_ck"])
+    for k, ck in fx["state_dict_ck"].items():
+        e_sample, e_sq = ck_close(sd[k], ck)
+        assert e_sample < 1e-6 and e_sq < 1e-6, k
+    pm = wav2vec2_model(**copy.deepcopy(pcfg))
+    pm.load_state_dict(sd, strict=True)
+    psd = {k: v.detach() for k, v in sd.items()}
+    with torch.no_grad():
+        hs, _ = ref.extract_features(psd, pcfg, fx["wave"], fx["lengths"])
+    for h, g in zip(hs, fx["pruned_hiddens"]):
+        assert ((h - g).norm() / g.norm()).item() < 1e-5

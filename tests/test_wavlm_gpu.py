@@ -110,3 +110,25 @@ def test_wavlm_layer_fwd_bwd_vs_oracle(pre_norm, remaining):
     for n, e in errs.items():
         assert e < 3e-2, (n, e)
     assert db_err < 2e-3 * _dz_abs_sum(cfg, sd, wave, ln, R)
+
+
+def test_pruned_wavlm_forward_vs_reference():
+    """The reference's pruned WavLM (ragged remaining heads per layer, ragged FFN widths; fixture g9) forward
+    on the HIP path, padded batch: hidden rel-L2 < 1e-2."""
+    from dphubert_amd.cli import prune_config
+    from dphubert_amd.wav2vec2.model import wav2vec2_model
+    fx = load_golden("g9_wavlm_prune.pt")
+    m = wav2vec2_model(**copy.deepcopy(fx["cfg"]))
+    sd = seeded_sd(fx["cfg"], fx["seed"])
+    sd.update(fx["log_alpha"])
+    m.load_state_dict(sd)
+    pcfg = prune_config(m, fx["cfg"])
+    pm = wav2vec2_model(**copy.deepcopy(pcfg))
+    pm.load_state_dict(m.state_dict(), strict=True)
+    pm = pm.to(DEV).eval()
+    with torch.no_grad():
+        hs, _ = pm.extract_features(fx["wave"].to(DEV), fx["lengths"].to(DEV))
+    torch.cuda.synchronize()
+    for h, g in zip(hs, fx["pruned_hiddens"]):
+        e = rel_l2(h.float().cpu(), g)
+        assert e < 1e-2, e

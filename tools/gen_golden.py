@@ -375,9 +375,47 @@ def gen_wavlm():
     return fx
 
 
+def gen_wavlm_prune():
+    """G9: eval-mode prune() of a WavLM model (WavLMSelfAttention.prune, components.py:661-693: remaining_heads
+    instead of num_heads) with all five units, rebuilt from the pruned config (prune.py:25-39), plus the pruned
+    model's hidden states on a padded batch."""
+    cfg = wavlm_cfg(2, **units_flags("conv,head,interm,attlayer,ffnlayer"))
+    m, sd = seeded_model(cfg, 5)
+    g = torch.Generator()
+    g.manual_seed(12)
+    la = {}
+    with torch.no_grad():
+        for n, p in m.named_parameters():
+            if n.endswith("log_alpha"):
+                v = torch.randn(p.shape, generator=g) * 3.0 + (1.0 if p.numel() > 1 else 3.0)
+                p.copy_(v)
+                la[n] = v.clone()
+    wave, ln = wave_batch(2, 24000, seed=9, lengths=[24000, 20000])
+    conv_config, use_attention, use_feed_forward, num_heads, remaining_heads, ff_interm = m.prune()
+    pcfg = dict(cfg, extractor_conv_layer_config=conv_config, encoder_use_attention=use_attention,
+                encoder_use_feed_forward=use_feed_forward, encoder_remaining_heads=remaining_heads,
+                encoder_ff_interm_features=ff_interm, extractor_prune_conv_channels=False,
+                encoder_prune_attention_heads=False, encoder_prune_attention_layer=False,
+                encoder_prune_feed_forward_intermediate=False, encoder_prune_feed_forward_layer=False)
+    pm = wav2vec2_model(**copy.deepcopy(pcfg))
+    pm.load_state_dict(m.state_dict(), strict=True)
+    pm.eval()
+    with torch.no_grad():
+        h, _ = pm.extract_features(wave, ln)
+    return {"cfg": cfg, "seed": 5, "log_alpha": la, "conv_config": [list(x) for x in conv_config],
+            "use_attention": use_attention, "use_feed_forward": use_feed_forward, "remaining_heads": remaining_heads,
+            "num_heads": num_heads, "ff_interm_features": ff_interm, "pruned_cfg": pcfg,
+            "state_dict_ck": {k: checksum(v) for k, v in m.state_dict().items()},
+            "wave": wave, "lengths": ln, "pruned_hiddens": [x.clone() for x in h]}
+
+
 def main():
     OUT.mkdir(parents=True, exist_ok=True)
     torch.set_num_threads(8)
+    if "--only-wavlm-prune" in sys.argv:
+        torch.save(gen_wavlm_prune(), OUT / "g9_wavlm_prune.pt")
+        print("g9 done")
+        return
     if "--only-wavlm" in sys.argv:
         torch.save(gen_wavlm(), OUT / "g8_wavlm.pt")
         print("g8 done")
