@@ -669,12 +669,28 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(const bf16_t* __res
           const float z = DROP ? attn_keep(hb[i >> 1], i & 1, thr, inv_keep) : 1.f;
           const float dsv = p * (pa[u][i] * z - my_D[u]);
           ds[u][s][i] = dsv;
-          if constexpr (BIAS) {
-            dg[u] += dsv * tv;
-            if (key < T32 && !qout[u]) atomicAdd(&hist[key - (int)qme[u] + qb0 + RB - 1], dsv * gq[u]);
-          }
+          if constexpr (BIAS) dg[u] += dsv * tv;
         }
       }
+    }
+    if constexpr (BIAS) {
+      // diagonal sums of dS * gate: element (u, s, i) sits on diagonal kt*64 + 16(s-u) + 4g + i - (q - qb0 - ...)
+      // of this block's histogram, so the query groups u meeting on the same s-u are added first (NG + 3
+      // diagonals x 4 instead of NG x 4 x 4 LDS atomics); masked elements are exactly 0 and skipped
+      const int base = kt * KT + 4 * g - wave * 16 * NG - (lane & 15) + RB - 1;
+#pragma unroll
+      for (int dd = -(NG - 1); dd < 4; ++dd)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float v = 0.f;
+#pragma unroll
+          for (int u = 0; u < NG; ++u) {
+            const int s = dd + u;
+            if (s >= 0 && s < 4) v += ds[u][s][i] * gq[u];
+          }
+          const int idx = base + 16 * dd + i;
+          if (v != 0.f && idx >= 0 && idx < T32 + RB - 1) atomicAdd(&hist[idx], v);
+        }
     }
     // dQ'^T[d][q] += K^T[d][key] dS^T[key][q]
 #pragma unroll

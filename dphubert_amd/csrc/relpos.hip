@@ -69,27 +69,42 @@ struct GateArgs {
   int64_t B, T, H;
 };
 
-// logits z[8] of (b, t, head hh) and the two sigmoids
-__device__ __forceinline__ void gate_logits(const GateArgs& a, const float* w_s, int64_t bt, int hh, float (&xv)[HDG],
-                                            float& ga, float& gb) {
+// The 4 logits of a group are only ever summed (components.py:639 .view(..., 2, 4).sum(-1)), so each group is
+// ONE dot product with the group's summed weight row: w_s = [wa[64] | wb[64] | ba | bb] built per block.
+__device__ __forceinline__ void load_group_weights(const GateArgs& a, float* w_s) {
+  const int t = threadIdx.x;
+  if (t < 2 * HDG) {
+    const int grp = t / HDG, d = t % HDG;
+    float v = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v += a.w[(4 * grp + j) * HDG + d];
+    w_s[t] = v;
+  } else if (t < 2 * HDG + 2) {
+    const int grp = t - 2 * HDG;
+    w_s[t] = a.bias[4 * grp] + a.bias[4 * grp + 1] + a.bias[4 * grp + 2] + a.bias[4 * grp + 3];
+  }
+}
+
+// group sums (za, zb) of (b, t, head hh) and their sigmoids
+__device__ __forceinline__ void gate_logits(const GateArgs& a, const float* w_s, int64_t bt, int hh, float& ga,
+                                            float& gb) {
   const bf16_t* xp = a.x + bt * a.ldx + (int64_t)hh * HDG;
+  float za = w_s[2 * HDG], zb = w_s[2 * HDG + 1];
 #pragma unroll
   for (int k = 0; k < HDG; k += 8) {
     const uint4 v = *reinterpret_cast<const uint4*>(xp + k);
     const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+    const float4 a0 = *reinterpret_cast<const float4*>(w_s + k), a1 = *reinterpret_cast<const float4*>(w_s + k + 4);
+    const float4 b0 = *reinterpret_cast<const float4*>(w_s + HDG + k);
+    const float4 b1 = *reinterpret_cast<const float4*>(w_s + HDG + k + 4);
+    const float wa[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+    const float wb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      xv[k + 2 * q] = __uint_as_float(wv[q] << 16);
-      xv[k + 2 * q + 1] = __uint_as_float(wv[q] & 0xffff0000u);
+      const float x0 = __uint_as_float(wv[q] << 16), x1 = __uint_as_float(wv[q] & 0xffff0000u);
+      za += wa[2 * q] * x0 + wa[2 * q + 1] * x1;
+      zb += wb[2 * q] * x0 + wb[2 * q + 1] * x1;
     }
-  }
-  float za = 0.f, zb = 0.f;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    float z = a.bias[j];
-#pragma unroll 16
-    for (int d = 0; d < HDG; ++d) z += w_s[j * HDG + d] * xv[d];
-    if (j < 4) za += z; else zb += z;
   }
   ga = 1.f / (1.f + __expf(-za));
   gb = 1.f / (1.f + __expf(-zb));
@@ -97,27 +112,30 @@ __device__ __forceinline__ void gate_logits(const GateArgs& a, const float* w_s,
 
 // one thread per (b, t, h); threads of a block share (b, t) rows of consecutive heads
 __global__ void __launch_bounds__(256) wavlm_gate_fwd_kernel(GateArgs a, float* __restrict__ gate) {
-  __shared__ float w_s[8 * HDG];
-  for (int i = threadIdx.x; i < 8 * HDG; i += 256) w_s[i] = a.w[i];
+  __shared__ __attribute__((aligned(16))) float w_s[2 * HDG + 4];
+  load_group_weights(a, w_s);
   __syncthreads();
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= a.B * a.T * a.H) return;
   const int h = (int)(i % a.H);
   const int64_t bt = i / a.H;
   const int hh = a.heads ? (int)a.heads[h] : h;
-  float xv[HDG], ga, gb;
-  gate_logits(a, w_s, bt, hh, xv, ga, gb);
+  float ga, gb;
+  gate_logits(a, w_s, bt, hh, ga, gb);
   const int64_t b = bt / a.T, t = bt % a.T;
   gate[(b * a.H + h) * a.T + t] = ga * (gb * a.gconst[hh] - 1.f) + 2.f;
 }
 
-// backward, pass 1: per (b, t, h): dz (both groups of 4 share one gradient), dx += dz W, db, dconst; dz -> scratch
+// backward, pass 1: per (b, t, h): group gradients dza, dzb (each of a group's 4 logits gets it), dx += dza wa +
+// dzb wb, db, dconst; (dza, dzb) -> scratch for the weight gradient
 __global__ void __launch_bounds__(256) wavlm_gate_bwd_kernel(GateArgs a, const float* __restrict__ dgate,
                                                              bf16_t* __restrict__ dx, int64_t lddx,
                                                              float* __restrict__ dz_out, float* __restrict__ db,
                                                              float* __restrict__ dconst) {
-  __shared__ float w_s[8 * HDG];
-  for (int i = threadIdx.x; i < 8 * HDG; i += 256) w_s[i] = a.w[i];
+  __shared__ __attribute__((aligned(16))) float w_s[2 * HDG + 4];
+  __shared__ float dc_s[64];   // per-block dconst partials (total heads <= 64)
+  load_group_weights(a, w_s);
+  if (threadIdx.x < 64) dc_s[threadIdx.x] = 0.f;
   __syncthreads();
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const bool live = i < a.B * a.T * a.H;
@@ -127,8 +145,8 @@ __global__ void __launch_bounds__(256) wavlm_gate_bwd_kernel(GateArgs a, const f
     const int h = (int)(i % a.H);
     const int64_t bt = i / a.H;
     hh = a.heads ? (int)a.heads[h] : h;
-    float xv[HDG], ga, gb;
-    gate_logits(a, w_s, bt, hh, xv, ga, gb);
+    float ga, gb;
+    gate_logits(a, w_s, bt, hh, ga, gb);
     const int64_t b = bt / a.T, t = bt % a.T;
     const float dg = dgate[(b * a.H + h) * a.T + t];
     const float c = a.gconst[hh];
@@ -139,7 +157,7 @@ __global__ void __launch_bounds__(256) wavlm_gate_bwd_kernel(GateArgs a, const f
     dzb = dgb * gb * (1.f - gb);
     dz_out[i * 2] = dza;
     dz_out[i * 2 + 1] = dzb;
-    // dx[d] += sum_j dz_j W[j][d]  (read-modify-write of this head's 64 bf16; heads of a row are disjoint)
+    // dx[d] += dza wa[d] + dzb wb[d]  (read-modify-write of this head's 64 bf16; heads of a row are disjoint)
     bf16_t* xp = dx + bt * lddx + (int64_t)hh * HDG;
 #pragma unroll
     for (int k = 0; k < HDG; k += 8) {
@@ -147,19 +165,10 @@ __global__ void __launch_bounds__(256) wavlm_gate_bwd_kernel(GateArgs a, const f
       uint32_t wv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        float acc[2];
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          const int d = k + 2 * q + e;
-          float sa = 0.f, sb = 0.f;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            sa += w_s[j * HDG + d];
-            sb += w_s[(j + 4) * HDG + d];
-          }
-          acc[e] = dza * sa + dzb * sb;
-        }
-        wv[q] = pack2bf(__uint_as_float(wv[q] << 16) + acc[0], __uint_as_float(wv[q] & 0xffff0000u) + acc[1]);
+        const int d = k + 2 * q;
+        const float a0 = dza * w_s[d] + dzb * w_s[HDG + d];
+        const float a1 = dza * w_s[d + 1] + dzb * w_s[HDG + d + 1];
+        wv[q] = pack2bf(__uint_as_float(wv[q] << 16) + a0, __uint_as_float(wv[q] & 0xffff0000u) + a1);
       }
       *reinterpret_cast<uint4*>(xp + k) = make_uint4(wv[0], wv[1], wv[2], wv[3]);
     }
@@ -170,7 +179,9 @@ __global__ void __launch_bounds__(256) wavlm_gate_bwd_kernel(GateArgs a, const f
     atomicAdd(db + 0, sa);
     atomicAdd(db + 4, sb);
   }
-  if (live) atomicAdd(dconst + hh, dc);
+  if (live) atomicAdd(&dc_s[hh], dc);
+  __syncthreads();
+  if (threadIdx.x < 64 && dc_s[threadIdx.x] != 0.f) atomicAdd(dconst + threadIdx.x, dc_s[threadIdx.x]);
 }
 
 // backward, pass 2: dW[j][d] = sum_n dz[n][j/4] x[n][d]; block = 256 rows n, thread (jg = t>>6 in {0..3}, d = t&63)
@@ -264,8 +275,8 @@ extern "C" int dph_wavlm_gate_bwd(const void* x, int64_t ldx, const float* w, co
                                   float* db, float* dconst, float* ws, int64_t B, int64_t T, int64_t H,
                                   int64_t head_dim, hipStream_t stream) {
   DPH_REQUIRE(x && w && bias && gconst && dgate && dx && dw && db && dconst && ws && B > 0 && T > 0 && H > 0 &&
-                  head_dim == HDG && ldx % 8 == 0 && lddx % 8 == 0,
-              "dph_wavlm_gate_bwd: bad args");
+                  head_dim == HDG && ldx % 8 == 0 && lddx % 8 == 0 && ldx / HDG <= 64,
+              "dph_wavlm_gate_bwd: bad args (head_dim 64, <= 64 heads)");
   GateArgs a{reinterpret_cast<const bf16_t*>(x), ldx, w, bias, gconst, heads, B, T, H};
   const int64_t N = B * T * H;
   float* dz = ws;

@@ -2,7 +2,7 @@
 # WavLM: GPU tests, WavLM-Base bench (graph replay), kernel-trace profile of the same bench.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-O=$R/gpurun_out/wl2
+O=$R/gpurun_out/${TAG:-wl2}
 mkdir -p "$O"
 cd "$R" || exit 1
 timeout -k 10 300 python -u -m pytest tests/test_wavlm_gpu.py -x -v -s --timeout 120 --timeout-method thread > "$O/wavlm.log" 2>&1 || { tail -40 "$O/wavlm.log"; exit 1; }
