@@ -688,8 +688,14 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(const bf16_t* __res
             const int s = dd + u;
             if (s >= 0 && s < 4) v += ds[u][s][i] * gq[u];
           }
+          // lanes (g, l), (g+1, l+4), (g+2, l+8), (g+3, l+12) sit on the same diagonal: fold the chain with two
+          // shuffles so only its first lane (g == 0 or l < 4) issues the atomic (no same-address collisions)
+          const float v1 = __shfl(v, (lane + 20) & 63, 64);
+          v += (g <= 2 && (lane & 15) <= 11) ? v1 : 0.f;
+          const float v2 = __shfl(v, (lane + 40) & 63, 64);
+          v += (g <= 1 && (lane & 15) <= 7) ? v2 : 0.f;
           const int idx = base + 16 * dd + i;
-          if (v != 0.f && idx >= 0 && idx < T32 + RB - 1) atomicAdd(&hist[idx], v);
+          if ((g == 0 || (lane & 15) < 4) && v != 0.f && idx >= 0 && idx < T32 + RB - 1) atomicAdd(&hist[idx], v);
         }
     }
     // dQ'^T[d][q] += K^T[d][key] dS^T[key][q]
