@@ -88,6 +88,16 @@ __device__ __forceinline__ int rel_idx(int key, int q, int T32) {
   return min(key, T32 - 1) - min(q, T32 - 1) + T32 - 1;
 }
 
+// A block of RB query rows (or RB keys) over all T keys (queries) touches T + RB - 1 consecutive diagonals,
+// starting at `off`: stage that window of the head's table in LDS (dynamic shared memory) once per block.
+constexpr int RBW = 128;   // == RB (defined below), rows / keys per block
+__device__ __forceinline__ void stage_tab_window(float* tw, const float* tab_h, int off, int T32) {
+  for (int j = threadIdx.x; j < T32 + RBW - 1; j += 256) {
+    const int gi = j + off;
+    tw[j] = (gi >= 0 && gi < 2 * T32 - 1) ? tab_h[gi] : 0.f;
+  }
+}
+
 // Dropout of the attention probabilities: element (row = (b*H+h)*T + q, key) draws 16 bits from ONE
 // 32-bit hash per (row, key pair) -- rows padded to an even key count, so the 4 consecutive keys a
 // lane holds in the forward / dQ kernels cost 2 hashes, and in the dK/dV kernel (4 queries of one
@@ -137,6 +147,7 @@ constexpr int TILE_SWZ_BYTES = KT * 128;           // 8192
 // fragment reads alone filled the CU's LDS bandwidth (~1 KB per 16-cycle MFMA per wave).
 constexpr int NG = 2;
 constexpr int RB = 4 * 16 * NG;   // rows per block: 128
+static_assert(RB == RBW, "table window width");
 
 // ---------------------------------------------------------------------------
 // forward: block = (128 query rows, head h, utterance b), 4 waves x 2 x 16 rows.
@@ -171,7 +182,9 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(const bf16_t* __restri
     qme[u] = q0 + 16 * u + (lane & 15);
     hrow[u] = ((uint64_t)(b * H + h) * T + (uint64_t)qme[u]) * half_tp;
   }
-  const float* tb = BIAS ? rb.tab + h * (2 * T - 1) : nullptr;
+  extern __shared__ float tw[];   // BIAS: [T + RB - 1] table window of this block's diagonals
+  const int toff = T32 - 1 - ((int)blockIdx.x * RB + RB - 1);
+  if constexpr (BIAS) stage_tab_window(tw, rb.tab + h * (2 * T - 1), toff, T32);   // ordered by the first barrier
   float gq[NG];
 #pragma unroll
   for (int u = 0; u < NG; ++u) gq[u] = (BIAS && qme[u] < T) ? rb.gate[(b * H + h) * T + qme[u]] : 0.f;
@@ -241,7 +254,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(const bf16_t* __restri
         for (int i = 0; i < 4; ++i) {
           const int key = kb + 16 * s + i;
           float v = sacc[u][s][i];
-          if constexpr (BIAS) v += gq[u] * tb[rel_idx(key, (int)qme[u], T32)];
+          if constexpr (BIAS) v += gq[u] * tw[rel_idx(key, (int)qme[u], T32) - toff];
           v = key >= klen ? v - 10000.0f : v;
           v = key >= T32 ? -INFINITY : v;
           sacc[u][s][i] = v;
@@ -416,7 +429,9 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkv_kernel(const bf16_t* __re
   float* lse_s = reinterpret_cast<float*>(smem + 4 * TB);        // [2][32]
   float* dv_s = reinterpret_cast<float*>(smem + 4 * TB + 2 * QT_BWD * 4);
   float* g_s = reinterpret_cast<float*>(smem + 4 * TB + 4 * QT_BWD * 4);   // [2][32] gates (BIAS)
-  const float* tb = BIAS ? rb.tab + h * (2 * T - 1) : nullptr;
+  extern __shared__ float tw[];   // BIAS: [T + RB - 1] table window (diagonals of this block's keys)
+  const int toff = (int)blockIdx.x * RB;
+  if constexpr (BIAS) stage_tab_window(tw, rb.tab + h * (2 * T - 1), toff, (int)T);   // ordered by the first barrier
 
   const int nqt = (int)cdiv(T, QT_BWD);
   uint4 rq[1], ro[1];
@@ -488,7 +503,7 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkv_kernel(const bf16_t* __re
           const int ql = 16 * w + 4 * g + i;
           const int q = qt * QT_BWD + ql;
           float sv = sacc[u][w][i];
-          if constexpr (BIAS) sv += g_s[cur * QT_BWD + ql] * tb[rel_idx((int)kme[u], q, T32)];
+          if constexpr (BIAS) sv += g_s[cur * QT_BWD + ql] * tw[rel_idx((int)kme[u], q, T32) - toff];
           sv = kpad[u] ? sv - 10000.0f : sv;
           float p = __expf(sv - lse_s[cur * QT_BWD + ql]);
           p = (q >= T32 || kout[u]) ? 0.f : p;
@@ -552,7 +567,7 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(const bf16_t* __res
                                                           const float* __restrict__ Dv, bf16_t* __restrict__ dqkv,
                                                           const int64_t* __restrict__ key_len, AttnShape sh,
                                                           float scale, float drop_p, uint64_t seed, RelBias rb) {
-  extern __shared__ float hist[];   // BIAS: [T + RB - 1] diagonal sums of dS * gate for this block's rows
+  extern __shared__ float dyn[];   // BIAS: hist [T + RB - 1] (diagonal sums of dS * gate) | table window [T + RB - 1]
   seed = epoch_seed(seed);   // per-step RNG epoch (graph replays)
   __shared__ __attribute__((aligned(16))) char smem[2 * (TILE_SWZ_BYTES + KTILE_PAD_BYTES)];
   const int tid = threadIdx.x;
@@ -595,16 +610,20 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(const bf16_t* __res
 #pragma unroll
     for (int d = 0; d < 4; ++d) dq[u][d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   }
-  const float* tb = BIAS ? rb.tab + h * (2 * T - 1) : nullptr;
-  float gq[NG], dg[NG];
+  float* hist = dyn;
+  float* tw = dyn + (T32 + RB - 1);
   const int qb0 = (int)blockIdx.x * RB;
+  const int toff = T32 - 1 - (qb0 + RB - 1);
+  float gq[NG], dg[NG];
 #pragma unroll
   for (int u = 0; u < NG; ++u) {
     gq[u] = (BIAS && qme[u] < T) ? rb.gate[(b * H + h) * T + qme[u]] : 0.f;
     dg[u] = 0.f;
   }
-  if constexpr (BIAS)
+  if constexpr (BIAS) {
     for (int i = tid; i < T32 + RB - 1; i += 256) hist[i] = 0.f;   // ordered before use by the first barrier
+    stage_tab_window(tw, rb.tab + h * (2 * T - 1), toff, T32);
+  }
 
   auto ldsK = [&](int buf) { return smem + buf * (TILE_SWZ_BYTES + KTILE_PAD_BYTES); };
   auto ldsV = [&](int buf) { return smem + buf * (TILE_SWZ_BYTES + KTILE_PAD_BYTES) + TILE_SWZ_BYTES; };
@@ -660,7 +679,7 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(const bf16_t* __res
           float sv = sa[u][i];
           float tv = 0.f;
           if constexpr (BIAS) {
-            tv = tb[rel_idx(key, (int)qme[u], T32)];
+            tv = tw[rel_idx(key, (int)qme[u], T32) - toff];
             sv += gq[u] * tv;
           }
           sv = key >= klen32 ? sv - 10000.0f : sv;
@@ -757,7 +776,8 @@ namespace {
 template <bool DROP, bool BIAS>
 void launch_fwd(dim3 grid, hipStream_t stream, const void* qkv, void* o_u, void* o_m, float* lse, const float* hm,
                 const int64_t* key_len, AttnShape sh, float scale, float p, uint64_t seed, RelBias rb) {
-  hipLaunchKernelGGL((attn_fwd_kernel<DROP, BIAS>), grid, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(qkv),
+  const size_t tw_bytes = BIAS ? (size_t)(sh.T + RB - 1) * sizeof(float) : 0;
+  hipLaunchKernelGGL((attn_fwd_kernel<DROP, BIAS>), grid, dim3(256), tw_bytes, stream, reinterpret_cast<const bf16_t*>(qkv),
                      reinterpret_cast<bf16_t*>(o_u), reinterpret_cast<bf16_t*>(o_m), lse, hm, key_len, sh, scale, p,
                      seed, rb);
 }
@@ -766,11 +786,11 @@ template <bool DROP, bool BIAS>
 void launch_bwd(dim3 grid, hipStream_t stream, const void* qkv, const void* dom, const float* hm, const float* lse,
                 const float* Dvec, void* dqkv, const int64_t* key_len, AttnShape sh, float scale, float p,
                 uint64_t seed, RelBias rb) {
-  hipLaunchKernelGGL((attn_bwd_dkv_kernel<DROP, BIAS>), grid, dim3(256), 0, stream,
+  const size_t tw_bytes = BIAS ? (size_t)(sh.T + RB - 1) * sizeof(float) : 0;
+  hipLaunchKernelGGL((attn_bwd_dkv_kernel<DROP, BIAS>), grid, dim3(256), tw_bytes, stream,
                      reinterpret_cast<const bf16_t*>(qkv), reinterpret_cast<const bf16_t*>(dom), hm, lse, Dvec,
                      reinterpret_cast<bf16_t*>(dqkv), key_len, sh, scale, p, seed, rb);
-  const size_t hist_bytes = BIAS ? (size_t)(sh.T + RB - 1) * sizeof(float) : 0;
-  hipLaunchKernelGGL((attn_bwd_dq_kernel<DROP, BIAS>), grid, dim3(256), hist_bytes, stream,
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<DROP, BIAS>), grid, dim3(256), 2 * tw_bytes, stream,
                      reinterpret_cast<const bf16_t*>(qkv), reinterpret_cast<const bf16_t*>(dom), hm, lse, Dvec,
                      reinterpret_cast<bf16_t*>(dqkv), key_len, sh, scale, p, seed, rb);
 }
@@ -821,8 +841,8 @@ extern "C" int dph_attention_fwd_relpos(const void* qkv, void* o_unmasked, void*
                                         const float* head_mask, const int64_t* key_len, const float* rel_tab,
                                         const float* gate, int64_t B, int64_t T, int64_t H, float scale,
                                         float dropout_p, uint64_t seed, hipStream_t stream) {
-  DPH_REQUIRE(qkv && o_unmasked && o_masked && lse && rel_tab && gate && B > 0 && T > 0 && T <= 4096 && H > 0,
-              "dph_attention_fwd_relpos: bad args (T <= 4096)");
+  DPH_REQUIRE(qkv && o_unmasked && o_masked && lse && rel_tab && gate && B > 0 && T > 0 && T <= 3584 && H > 0,
+              "dph_attention_fwd_relpos: bad args (T <= 3584)");
   return attention_fwd(qkv, o_unmasked, o_masked, lse, head_mask, key_len, B, T, H, scale, dropout_p, seed,
                        RelBias{rel_tab, gate, nullptr, nullptr}, stream);
 }
@@ -851,8 +871,8 @@ extern "C" int dph_attention_bwd_relpos(const void* qkv, const void* do_masked, 
                                         int64_t B, int64_t T, int64_t H, float scale, float dropout_p, uint64_t seed,
                                         hipStream_t stream) {
   DPH_REQUIRE(qkv && do_masked && lse && Dvec && dqkv && rel_tab && gate && dgate && drel_tab && B > 0 && T > 0 &&
-                  T <= 4096 && H > 0,
-              "dph_attention_bwd_relpos: bad args (T <= 4096)");
+                  T <= 3584 && H > 0,
+              "dph_attention_bwd_relpos: bad args (T <= 3584: two [T+127] fp32 LDS windows + 34 KB of tiles)");
   return attention_bwd(qkv, do_masked, head_mask, lse, Dvec, dqkv, key_len, B, T, H, scale, dropout_p, seed,
                        RelBias{rel_tab, gate, dgate, drel_tab}, stream);
 }

@@ -179,7 +179,7 @@ int dph_attention_bwd(const void* qkv, const void* do_masked, const float* head_
  * exists: rel_tab [H][2T-1] fp32 is one value per diagonal r = k-q+T-1 for each
  * remaining head, gate [B][H][T] fp32 one value per query row.
  * ------------------------------------------------------------------------ */
-/* attention forward with score += gate[b,h,q] * rel_tab[h][k-q+T-1] (T <= 4096) */
+/* attention forward with score += gate[b,h,q] * rel_tab[h][k-q+T-1] (T <= 3584) */
 int dph_attention_fwd_relpos(const void* qkv, void* o_unmasked, void* o_masked, float* lse, const float* head_mask,
                              const int64_t* key_len, const float* rel_tab, const float* gate, int64_t B, int64_t T,
                              int64_t H, float scale, float dropout_p, uint64_t seed, hipStream_t stream);
