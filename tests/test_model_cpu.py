@@ -8,7 +8,7 @@ import math
 import pytest
 import torch
 
-from dphubert_amd.synthetic import HUBERT_BASE_CONFIG, HUBERT_LARGE_CONFIG
+from dphubert_amd.synthetic import HUBERT_BASE_CONFIG, HUBERT_LARGE_CONFIG, WAVLM_BASE_CONFIG
 from dphubert_amd.wav2vec2.model import wav2vec2_model
 from dphubert_amd.wav2vec2.components import _PolyCtx
 from helpers import load_golden, seeded_sd
@@ -19,7 +19,8 @@ ALL_UNITS = dict(extractor_prune_conv_channels=True, encoder_prune_attention_hea
                  encoder_prune_feed_forward_layer=True)
 
 
-@pytest.mark.parametrize("cfg", [HUBERT_BASE_CONFIG, HUBERT_LARGE_CONFIG, dict(HUBERT_BASE_CONFIG, **ALL_UNITS)])
+@pytest.mark.parametrize("cfg", [HUBERT_BASE_CONFIG, HUBERT_LARGE_CONFIG, dict(HUBERT_BASE_CONFIG, **ALL_UNITS),
+                                 WAVLM_BASE_CONFIG, dict(WAVLM_BASE_CONFIG, **ALL_UNITS)])
 def test_state_dict_schema_matches_reference(cfg):
     m = wav2vec2_model(**copy.deepcopy(cfg))
     ours = [(k, tuple(v.shape)) for k, v in m.state_dict().items()]
@@ -57,6 +58,18 @@ def test_expected_params_polynomial(units):
     want = float(ref.get_num_params(sd, cfg))
     got = _eval_poly(m, sd)
     assert abs(got - want) <= 1e-6 * want
+
+
+def test_wavlm_expected_params_and_schema_vs_reference():
+    """WavLM: the state_dict schema and the initial expected #params of the reference's own model (fixture g8:
+    the relative-position embedding and gate are not counted, as WavLMSelfAttention inherits get_num_params)."""
+    fx = load_golden("g8_wavlm.pt")
+    cfg = dict(fx["scfg"])
+    m = wav2vec2_model(**copy.deepcopy(cfg))
+    assert [(k, tuple(v.shape)) for k, v in m.state_dict().items()] == [(k, tuple(s)) for k, s in fx["sd_schema"]]
+    sd = seeded_sd(cfg, 0)
+    m.load_state_dict(sd)
+    assert abs(_eval_poly(m, sd) - fx["num_params_init"]) <= 1e-6 * fx["num_params_init"]
 
 
 def test_expected_params_matches_golden():
