@@ -696,26 +696,47 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(const bf16_t* __res
       // diagonal sums of dS * gate: element (u, s, i) sits on diagonal kt*64 + 16(s-u) + 4g + i - (q - qb0 - ...)
       // of this block's histogram, so the query groups u meeting on the same s-u are added first (NG + 3
       // diagonals x 4 instead of NG x 4 x 4 LDS atomics); masked elements are exactly 0 and skipped
-      const int base = kt * KT + 4 * g - wave * 16 * NG - (lane & 15) + RB - 1;
+      const int l = lane & 15;
+      const int base = kt * KT + 4 * g - wave * 16 * NG - l + RB - 1;
 #pragma unroll
-      for (int dd = -(NG - 1); dd < 4; ++dd)
+      for (int dd = -(NG - 1); dd < 4; ++dd) {
+        float v[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          float v = 0.f;
+          v[i] = 0.f;
 #pragma unroll
           for (int u = 0; u < NG; ++u) {
             const int s = dd + u;
-            if (s >= 0 && s < 4) v += ds[u][s][i] * gq[u];
+            if (s >= 0 && s < 4) v[i] += ds[u][s][i] * gq[u];
           }
-          // lanes (g, l), (g+1, l+4), (g+2, l+8), (g+3, l+12) sit on the same diagonal: fold the chain with two
-          // shuffles so only its first lane (g == 0 or l < 4) issues the atomic (no same-address collisions)
-          const float v1 = __shfl(v, (lane + 20) & 63, 64);
-          v += (g <= 2 && (lane & 15) <= 11) ? v1 : 0.f;
-          const float v2 = __shfl(v, (lane + 40) & 63, 64);
-          v += (g <= 1 && (lane & 15) <= 7) ? v2 : 0.f;
-          const int idx = base + 16 * dd + i;
-          if ((g == 0 || (lane & 15) < 4) && v != 0.f && idx >= 0 && idx < T32 + RB - 1) atomicAdd(&hist[idx], v);
         }
+        // element (l, i) and (l + 1, i + 1) share a diagonal: fold each chain (l, 0), (l+1, 1), (l+2, 2),
+        // (l+3, 3) into its first cell -- heads are then (l, 0) for every lane plus (0, i > 0)
+        const float a1 = __shfl_down(v[1], 1, 64), a2 = __shfl_down(v[2], 1, 64), a3 = __shfl_down(v[3], 1, 64);
+        if (l <= 14) {
+          v[0] += a1;
+          v[1] += a2;
+          v[2] += a3;
+        }
+        const float b2 = __shfl_down(v[2], 2, 64), b3 = __shfl_down(v[3], 2, 64);
+        if (l <= 13) {
+          v[0] += b2;
+          v[1] += b3;
+        }
+        // the (l = 0, i > 0) heads ride on lanes l = 1..3 of the same g in a second atomic
+        const float e1 = __shfl(v[1], lane & 48, 64), e2 = __shfl(v[2], lane & 48, 64), e3 = __shfl(v[3], lane & 48, 64);
+        const float ex = l == 1 ? e1 : (l == 2 ? e2 : e3);
+        // lanes (g, l), (g+1, l+4), (g+2, l+8), (g+3, l+12) share the i = 0 diagonal: fold along g as well
+        float w = v[0];
+        const float w1 = __shfl(w, (lane + 20) & 63, 64);
+        w += (g <= 2 && l <= 11) ? w1 : 0.f;
+        const float w2 = __shfl(w, (lane + 40) & 63, 64);
+        w += (g <= 1 && l <= 7) ? w2 : 0.f;
+        const int idx = base + 16 * dd;
+        if ((g == 0 || l < 4) && w != 0.f && idx >= 0 && idx < T32 + RB - 1) atomicAdd(&hist[idx], w);
+        const int idx2 = base + 2 * l + 16 * dd;   // diagonal of head (g, 0, i = l)
+        if (l >= 1 && l <= 3 && ex != 0.f && idx2 >= 0 && idx2 < T32 + RB - 1) atomicAdd(&hist[idx2], ex);
+      }
     }
     // dQ'^T[d][q] += K^T[d][key] dS^T[key][q]
 #pragma unroll
