@@ -173,15 +173,20 @@ __global__ void __launch_bounds__(256) wavlm_gate_bwd_kernel(GateArgs a, const f
       *reinterpret_cast<uint4*>(xp + k) = make_uint4(wv[0], wv[1], wv[2], wv[3]);
     }
   }
-  // db[j] = sum dz_j (j < 4: dza, else dzb); dconst[hh] += dc
+  // db[j] = sum dz_j (j < 4: dza, else dzb): wave sums -> one atomic pair per block; dconst[hh] += dc
+  __shared__ float red[2][4];
   const float sa = wave_sum(dza), sb = wave_sum(dzb);
   if ((threadIdx.x & 63) == 0) {
-    atomicAdd(db + 0, sa);
-    atomicAdd(db + 4, sb);
+    red[0][threadIdx.x >> 6] = sa;
+    red[1][threadIdx.x >> 6] = sb;
   }
   if (live) atomicAdd(&dc_s[hh], dc);
   __syncthreads();
   if (threadIdx.x < 64 && dc_s[threadIdx.x] != 0.f) atomicAdd(dconst + threadIdx.x, dc_s[threadIdx.x]);
+  if (threadIdx.x == 0) {
+    atomicAdd(db + 0, red[0][0] + red[0][1] + red[0][2] + red[0][3]);
+    atomicAdd(db + 4, red[1][0] + red[1][1] + red[1][2] + red[1][3]);
+  }
 }
 
 // backward, pass 2: dW[j][d] = sum_n dz[n][j/4] x[n][d]; block = 256 rows n, thread (jg = t>>6 in {0..3}, d = t&63)
@@ -208,19 +213,28 @@ __global__ void __launch_bounds__(256) wavlm_gate_wgrad_kernel(GateArgs a, const
   red[part][1][d] = acc_b;
   __syncthreads();
   if (part < 2) {
-    const float v = red[0][part][d] + red[1][part][d] + red[2][part][d] + red[3][part][d];
-    // the 4 logits of a group share the same gradient: one atomic per group row, replicated by dph_wavlm_gate_bwd
-    atomicAdd(dw + (part * 4) * HDG + d, v);
+    // the 4 logits of a group share the same gradient: one partial row per group and block (no atomics: ~1500
+    // blocks' atomics on 128 addresses serialised), summed over blocks by wavlm_gate_finish_kernel
+    dw[((int64_t)blockIdx.x * 2 + part) * HDG + d] = red[0][part][d] + red[1][part][d] + red[2][part][d] + red[3][part][d];
   }
 }
 
-// dW / db rows of one group are identical (each logit of a group gets the group's gradient): replicate row 0 / 4
-__global__ void wavlm_gate_replicate_kernel(float* __restrict__ dw, float* __restrict__ db, const float* __restrict__ dw0,
-                                            const float* __restrict__ db0) {
-  const int t = threadIdx.x;   // 512 threads: (j, d)
-  const int j = t >> 6, d = t & 63;
-  dw[j * HDG + d] += dw0[(j < 4 ? 0 : 4) * HDG + d];
-  if (d == 0) db[j] += db0[j < 4 ? 0 : 4];
+// dW / db rows of one group are identical (each logit of a group gets the group's gradient): sum the per-block
+// partial rows, 32 blocks' partials per finishing block, and add them to all 4 rows of the group
+constexpr int FIN_CHUNK = 32;
+__global__ void __launch_bounds__(128) wavlm_gate_finish_kernel(float* __restrict__ dw, float* __restrict__ db,
+                                                                const float* __restrict__ part, int nblk,
+                                                                const float* __restrict__ db0) {
+  const int t = threadIdx.x;   // 128 threads: (group, d)
+  const int grp = t >> 6, d = t & 63;
+  const int k0 = blockIdx.x * FIN_CHUNK;
+  const int k1 = min(k0 + FIN_CHUNK, nblk);
+  float acc = 0.f;
+  for (int k = k0; k < k1; ++k) acc += part[((int64_t)k * 2 + grp) * HDG + d];
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj) atomicAdd(dw + (grp * 4 + jj) * HDG + d, acc);
+  if (blockIdx.x == 0 && d == 0)
+    for (int jj = 0; jj < 4; ++jj) db[grp * 4 + jj] += db0[grp * 4];
 }
 
 }  // namespace
@@ -269,7 +283,8 @@ extern "C" int dph_wavlm_gate_fwd(const void* x, int64_t ldx, const float* w, co
   return check_launch("dph_wavlm_gate_fwd");
 }
 
-// dx (bf16, ld lddx) is ADDED to; dw [8][64], db [8], dconst [Htot] accumulate; ws = 2*B*T*H + 520 floats
+// dx (bf16, ld lddx) is ADDED to; dw [8][64], db [8], dconst [Htot] accumulate;
+// ws = 2*N + 8 + 128*ceil(N/256) floats, N = B*T*H
 extern "C" int dph_wavlm_gate_bwd(const void* x, int64_t ldx, const float* w, const float* bias, const float* gconst,
                                   const int64_t* heads, const float* dgate, void* dx, int64_t lddx, float* dw,
                                   float* db, float* dconst, float* ws, int64_t B, int64_t T, int64_t H,
@@ -279,13 +294,15 @@ extern "C" int dph_wavlm_gate_bwd(const void* x, int64_t ldx, const float* w, co
               "dph_wavlm_gate_bwd: bad args (head_dim 64, <= 64 heads)");
   GateArgs a{reinterpret_cast<const bf16_t*>(x), ldx, w, bias, gconst, heads, B, T, H};
   const int64_t N = B * T * H;
+  const int nblk = (int)cdiv(N, 256);
   float* dz = ws;
-  float* dw0 = ws + 2 * N;          // [8][64] (rows 0 and 4 used)
-  float* db0 = dw0 + 8 * HDG;       // [8]
-  if (hipMemsetAsync(dw0, 0, (8 * HDG + 8) * sizeof(float), stream) != hipSuccess) return check_launch("dph_wavlm_gate_bwd memset");
+  float* db0 = ws + 2 * N;          // [8] (entries 0 and 4 used)
+  float* part = db0 + 8;            // [nblk][2][64] per-block group rows of dW
+  if (hipMemsetAsync(db0, 0, 8 * sizeof(float), stream) != hipSuccess) return check_launch("dph_wavlm_gate_bwd memset");
   hipLaunchKernelGGL(wavlm_gate_bwd_kernel, dim3((unsigned)cdiv(N, 256)), dim3(256), 0, stream, a, dgate,
                      reinterpret_cast<bf16_t*>(dx), lddx, dz, db0, dconst);
-  hipLaunchKernelGGL(wavlm_gate_wgrad_kernel, dim3((unsigned)cdiv(N, 256)), dim3(256), 0, stream, a, dz, dw0);
-  hipLaunchKernelGGL(wavlm_gate_replicate_kernel, dim3(1), dim3(512), 0, stream, dw, db, dw0, db0);
+  hipLaunchKernelGGL(wavlm_gate_wgrad_kernel, dim3((unsigned)nblk), dim3(256), 0, stream, a, dz, part);
+  hipLaunchKernelGGL(wavlm_gate_finish_kernel, dim3((unsigned)cdiv(nblk, FIN_CHUNK)), dim3(128), 0, stream, dw, db,
+                     part, nblk, db0);
   return check_launch("dph_wavlm_gate_bwd");
 }

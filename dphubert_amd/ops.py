@@ -1357,7 +1357,8 @@ class EncoderLayerFn(torch.autograd.Function):
         dgw, _ = go.buf(wl["gw"])
         dgb, _ = go.buf(wl["gb"])
         dgc, _ = go.buf(wl["gc"])
-        ws = torch.empty(2 * B * T * H + 520, dtype=F32, device=dx_att.device)
+        N = B * T * H
+        ws = torch.empty(2 * N + 8 + 128 * ((N + 255) // 256), dtype=F32, device=dx_att.device)
         call("dph_wavlm_gate_bwd", ptr(x_att), x_att.shape[1], ptr(wl["gw"]), ptr(wl["gb"]), ptr(wl["gc"]),
              ptr(wl["heads"]), ptr(dgate), ptr(dx_att), dx_att.shape[1], ptr(dgw), ptr(dgb), ptr(dgc), ptr(ws),
              B, T, H, 64, _s())

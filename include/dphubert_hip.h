@@ -202,7 +202,7 @@ int dph_wavlm_gate_fwd(const void* x, int64_t ldx, const float* w, const float* 
                        const int64_t* heads, float* gate, int64_t B, int64_t T, int64_t H, int64_t head_dim,
                        hipStream_t stream);
 /* its backward: dx (bf16, ld lddx) += the gate's input gradient; dw [8][64], db [8], dconst [Htot] ACCUMULATE;
- * ws: (2*B*T*H + 520) floats */
+ * ws: 2*N + 8 + 128*ceil(N/256) floats, N = B*T*H */
 int dph_wavlm_gate_bwd(const void* x, int64_t ldx, const float* w, const float* bias, const float* gconst,
                        const int64_t* heads, const float* dgate, void* dx, int64_t lddx, float* dw, float* db,
                        float* dconst, float* ws, int64_t B, int64_t T, int64_t H, int64_t head_dim,
