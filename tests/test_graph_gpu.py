@@ -18,19 +18,25 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-def _cfg():
-    from dphubert_amd.synthetic import HUBERT_BASE_CONFIG
-    cfg = copy.deepcopy(HUBERT_BASE_CONFIG)
+def _cfg(family="hubert"):
+    from dphubert_amd.synthetic import HUBERT_BASE_CONFIG, WAVLM_BASE_CONFIG
+    if family == "wavlm":
+        # WavLM: the relative-position table, gate and their gradients run inside the captured graph too
+        cfg = copy.deepcopy(WAVLM_BASE_CONFIG)
+        cfg.update(encoder_total_num_heads=[12] * 2, encoder_remaining_heads=[list(range(12))] * 2)
+    else:
+        cfg = copy.deepcopy(HUBERT_BASE_CONFIG)
+        cfg.update(encoder_num_heads=[12] * 2)
     cfg.update(encoder_num_layers=2, encoder_use_attention=[True] * 2, encoder_use_feed_forward=[True] * 2,
-               encoder_num_heads=[12] * 2, encoder_ff_interm_features=[3072] * 2, encoder_projection_dropout=0.0,
+               encoder_ff_interm_features=[3072] * 2, encoder_projection_dropout=0.0,
                encoder_attention_dropout=0.0, encoder_ff_interm_dropout=0.0, encoder_dropout=0.0,
                encoder_layer_drop=0.0)
     return cfg
 
 
-def _module(seed=3):
+def _module(seed=3, family="hubert"):
     from dphubert_amd.trainer import build_distill_module
-    dm = build_distill_module(_cfg(), pruning_units="conv,head,interm", distill_layers="0.1,2", seed=seed,
+    dm = build_distill_module(_cfg(family), pruning_units="conv,head,interm", distill_layers="0.1,2", seed=seed,
                               learning_rate=2e-3, warmup_updates=2, max_updates=10, sparsity_warmup_updates=4)
     with torch.no_grad():
         dm.lambda1.fill_(0.3)
@@ -74,15 +80,16 @@ def test_optimizer_updates_reach_gemm_images():
         assert torch.equal(a, b)
 
 
-def test_graph_replay_matches_eager():
+@pytest.mark.parametrize("family", ["hubert", "wavlm"])
+def test_graph_replay_matches_eager(family):
     """Replayed steps track eager steps as closely as two eager runs track each other (the only
     run-to-run difference is the fp32 atomic order of gradient reductions, which AdamW's
     normalisation amplifies on tiny gradients)."""
     from dphubert_amd.trainer import Trainer
     batch = _batch()
-    ea = Trainer(_module(), clip_norm=10.0)
-    eb = Trainer(_module(), clip_norm=10.0)
-    gr = Trainer(_module(), clip_norm=10.0, graphs=True, graph_warmup=1)
+    ea = Trainer(_module(family=family), clip_norm=10.0)
+    eb = Trainer(_module(family=family), clip_norm=10.0)
+    gr = Trainer(_module(family=family), clip_norm=10.0, graphs=True, graph_warmup=1)
     le, lb, lg = [], [], []
     for _ in range(5):
         le.append(ea.step(batch).item())
