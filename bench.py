@@ -35,11 +35,34 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(batch: int = 1, steps: int = 2, seconds: float = 10.0):
-    """Time the fp32 CPU oracle (oracle/hubert_ref.py) on a bounded sample of the same step."""
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def host_cores() -> int:
+    """Host cores this process may use: its CPU affinity set, bounded by the job's thread budget
+    (OMP_NUM_THREADS, which the GPU box sets to this job's CPU share; os.cpu_count() there reports the
+    whole machine, whose other cores belong to other jobs)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
+def cpu_baseline(batch: int = 2, warmup: int = 3, steps: int = 5, seconds: float = 10.0):
+    """Time the fp32 CPU oracle (oracle/hubert_ref.py) on a bounded sample of the same step
+    (B=2, 3 warm-up + 5 timed steps, all host cores of this job, CPU model stated)."""
     from dphubert_amd.synthetic import HUBERT_BASE_CONFIG, seeded_state_dict, synthetic_batch
     from oracle import hubert_ref as ref
-    threads = min(os.cpu_count() or 1, 16)
+    threads = host_cores()
     torch.set_num_threads(threads)
     cfg = copy.deepcopy(HUBERT_BASE_CONFIG)
     scfg = dict(cfg, extractor_prune_conv_channels=True, encoder_prune_attention_heads=True,
@@ -55,16 +78,19 @@ def cpu_baseline(batch: int = 1, steps: int = 2, seconds: float = 10.0):
     kw = dict(teacher_sd=tsd, teacher_cfg=cfg, student_sd=ssd, student_cfg=scfg, proj_sd=psd,
               distill_layers=[0, 4, 8, 12], proj_index=[0, 1, 1, 1], wave=wave, lengths=lengths, u=u,
               lambdas=(0.0, 0.0), global_step=5000, original_num_params=94371456)
-    ref.distill_step(**kw)                      # warm-up
-    t0 = time.perf_counter()
-    for _ in range(steps):
+    for _ in range(warmup):
         ref.distill_step(**kw)
-    dt = time.perf_counter() - t0
-    return {"value": round(batch * seconds * steps / dt, 3), "unit": "audio-seconds/sec", "cores": threads,
-            "kind": "port",
+    times = []
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        ref.distill_step(**kw)
+        times.append(time.perf_counter() - t0)
+    dt = sorted(times)[len(times) // 2]          # median step
+    return {"value": round(batch * seconds / dt, 3), "unit": "audio-seconds/sec", "cores": threads,
+            "kind": "port", "cpu_model": _cpu_model(), "median_step_s": round(dt, 3),
             "sample": f"oracle/hubert_ref.py distill_step (teacher fwd + student fwd/bwd + loss + reg, fp32, no "
-                      f"optimizer), HuBERT-Base 12 layers, B={batch} x {seconds:.0f} s, {steps} timed steps after 1 "
-                      f"warm-up, torch CPU {threads} threads"}
+                      f"optimizer), HuBERT-Base 12 layers, B={batch} x {seconds:.0f} s, median of {steps} timed steps "
+                      f"after {warmup} warm-up, torch CPU {threads} threads on {_cpu_model()}"}
 
 
 def pmc_traffic(args):
@@ -122,6 +148,9 @@ def main():
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--traffic", choices=["auto", "off"], default="auto",
                     help="auto: measure per-launch HBM bytes of the GEMMs with rocprofv3 PMC passes (rank 0, N=1)")
+    ap.add_argument("--grad-comm", choices=["fp32", "bf16"], default="fp32",
+                    help="payload of the gradient all-reduce at N > 1 (bf16: half the xGMI bytes)")
+    ap.add_argument("--accum", type=int, default=1, help="micro-batches per optimizer step (a step = one micro-batch)")
     ap.add_argument("--graphs", choices=["on", "off"], default="on",
                     help="on: replay the whole step as one captured HIP graph after the eager warm-up steps")
     args = ap.parse_args()
@@ -156,13 +185,18 @@ def main():
     module.global_step = 5000            # target sparsity reached (0.75)
     module = module.to(dev)
     graphs = args.graphs == "on"
-    trainer = Trainer(module, clip_norm=10.0, graphs=graphs, graph_warmup=2)
+    trainer = Trainer(module, clip_norm=10.0, graphs=graphs, graph_warmup=2, accum_grad=args.accum,
+                      grad_dtype=torch.bfloat16 if args.grad_comm == "bf16" else torch.float32)
     samples = int(args.seconds * 16000)
     wave, lengths = synthetic_batch(args.batch, samples, seed=2022 + rank)
     batch = (wave.to(dev), lengths.to(dev))
 
     # warm-up: 2 eager steps, then (graphs) the capture + first replay
-    for i in range(max(args.warmup, 3 if graphs else 1)):
+    if args.accum < 1 or args.steps < args.accum:
+        raise SystemExit("--accum must be >= 1 and <= --steps")
+    # warm-up in whole optimizer steps (the trainer captures its graphs after 2 eager optimizer steps)
+    n_warm = max(args.warmup, 3 if graphs else 1) * args.accum
+    for i in range(n_warm):
         loss = trainer.step(batch)
     torch.cuda.synchronize()
     graphed = trainer._graph is not None
@@ -185,8 +219,9 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     in_loop = prof is not None and prof_mode != "eager step right after the timed region (same kernels)"
+    last_final = (args.steps // args.accum) * args.accum - 1    # the last micro-step that ends an optimizer step
     for i in range(args.steps):
-        last = in_loop and i == args.steps - 1
+        last = in_loop and i == last_final
         if last and not graphed:
             prof.__enter__()
         loss = trainer.step(batch, profiled=last)
@@ -225,18 +260,18 @@ def main():
                                "conv,head,interm, dropout) + L1/cos distill loss + sparsity Lagrangian + AdamW",
                    "utterances_per_gpu": args.batch, "seconds_per_utt": args.seconds,
                    "global_batch_audio_s": world * args.batch * args.seconds, "distill_layers": "0.4,8,12",
-                   "parallelism": f"dp{world}"},
+                   "parallelism": f"dp{world}", "accum_grad": args.accum, "grad_comm": args.grad_comm},
         "peak_hbm_gib": round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 2),
         "step_mode": "hip_graph" if graphed else "eager",
     }
     if prof is not None and not in_loop:
         torch.cuda.synchronize()
-        trainer._graph, saved = None, trainer._graph      # one eager step with the profiler on
+        saved, trainer._graphs = trainer._graphs, {}      # one eager step with the profiler on
         g_on = trainer.graphs
         trainer.graphs = False
         with prof:
             trainer.step(batch)
-        trainer.graphs, trainer._graph = g_on, saved
+        trainer.graphs, trainer._graphs = g_on, saved
     if prof is not None:
         prof.__exit__(None, None, None)
         summ = prof.summary()

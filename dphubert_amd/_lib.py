@@ -51,6 +51,10 @@ class DphAdamDyn(C.Structure):
     _fields_ = [("g", DphAdamGroup * 4), ("step", f32), ("pad_", f32 * 3)]
 
 
+class DphHcEntry(C.Structure):
+    _fields_ = [("log_alpha", vp), ("u_in", vp), ("dmask", vp), ("dlog_alpha", vp), ("n", i64), ("offset", i64)]
+
+
 S = vp  # hipStream_t
 
 _SIGS = {
@@ -104,6 +108,8 @@ _SIGS = {
     "dph_distill_loss_bwd": ([vp, vp, vp, vp, i64, i64, i64, i64, f32, f32, f32, C.c_int, vp, S], C.c_int),
     "dph_hc_sample_fwd": ([vp, vp, vp, vp, i64, u64, f32, f32, f32, f32, S], C.c_int),
     "dph_hc_sample_bwd": ([vp, vp, vp, vp, i64, f32, f32, f32, S], C.c_int),
+    "dph_hc_bank_fwd": ([vp, i64, vp, vp, u64, f32, f32, f32, f32, S], C.c_int),
+    "dph_hc_bank_bwd": ([vp, i64, vp, f32, f32, f32, S], C.c_int),
     "dph_expected_params_fwd": ([vp, vp, i64, vp, vp, i64, C.c_double, f32, vp, vp, S], C.c_int),
     "dph_expected_params_bwd": ([vp, vp, vp, vp, i64, vp, vp, i64, vp, vp, f32, S], C.c_int),
     "dph_grad_sumsq": ([vp, i64, vp, vp, i64, vp, S], C.c_int),
@@ -117,7 +123,9 @@ _SIGS = {
 }
 
 _lib = None
-ABI_VERSION = 11     # include/dphubert_hip.h layout (3: dph_adamw_step_dev, dph_set_rng_epoch; 4: dph_event_*; 5: LN bwd / colsum workspaces)
+# include/dphubert_hip.h layout (3: dph_adamw_step_dev, dph_set_rng_epoch; 4: dph_event_*; 5: LN bwd / colsum
+# workspaces; 12: dph_hc_bank_fwd / dph_hc_bank_bwd)
+ABI_VERSION = 12
 
 
 class DphError(RuntimeError):

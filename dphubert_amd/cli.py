@@ -63,6 +63,14 @@ def _common_args(p: argparse.ArgumentParser, lr: float, warmup: int, max_updates
                    help="train on this many seeded synthetic utterances per GPU per step instead of --tsv_dir")
     p.add_argument("--synthetic_seconds", default=10.0, type=float)
     p.add_argument("--save_interval", default=0, type=int, help="also checkpoint every N updates (0: at the end)")
+    p.add_argument("--graphs", default="auto", choices=["auto", "on", "off"],
+                   help="replay each optimizer step as one captured HIP graph; auto: on for fixed-shape "
+                        "(--synthetic_utterances) batches, off for bucketed corpus batches (their length varies)")
+    p.add_argument("--grad_comm_dtype", default="fp32", choices=["fp32", "bf16"],
+                   help="payload of the data-parallel gradient all-reduce (bf16 halves the xGMI bytes)")
+    p.add_argument("--reshuffle_each_epoch", action="store_true",
+                   help="new batch order every epoch (the reference's DistributedBatchSampler permutes once, so by "
+                        "default every epoch repeats epoch 0's order, as the reference does)")
 
 
 def distill_parser():
@@ -84,9 +92,42 @@ def final_distill_parser():
 # ---------------------------------------------------------------------------------------------
 # launch helpers
 # ---------------------------------------------------------------------------------------------
+def _slurm_first_host(nodelist: str) -> str:
+    """First host of a SLURM nodelist ("n1,n2", "gpu[03-06,09]", "a[1-2],b7")."""
+    head = nodelist.split(",")[0] if "[" not in nodelist.split(",")[0] else nodelist[:nodelist.index("]") + 1]
+    if "[" not in head:
+        return head
+    prefix, rng = head.split("[", 1)
+    first = rng.rstrip("]").split(",")[0].split("-")[0]
+    return prefix + first
+
+
+def _slurm_env(env=None):
+    """run.sh:4,48 starts one task per GPU with srun: SLURM sets SLURM_NTASKS / SLURM_PROCID / SLURM_LOCALID, not
+    torch.distributed's WORLD_SIZE / RANK / LOCAL_RANK.  Returns those three (+ MASTER_ADDR / MASTER_PORT) when this
+    process is one task of a multi-task srun step, else None."""
+    env = os.environ if env is None else env
+    if "WORLD_SIZE" in env or int(env.get("SLURM_NTASKS", "1")) <= 1 or "SLURM_PROCID" not in env:
+        return None
+    out = {"WORLD_SIZE": env["SLURM_NTASKS"], "RANK": env["SLURM_PROCID"],
+           "LOCAL_RANK": env.get("SLURM_LOCALID", "0")}
+    if "MASTER_ADDR" not in env:
+        nodes = env.get("SLURM_STEP_NODELIST") or env.get("SLURM_JOB_NODELIST") or ""
+        one_node = int(env.get("SLURM_NNODES", env.get("SLURM_JOB_NUM_NODES", "1"))) <= 1
+        out["MASTER_ADDR"] = "127.0.0.1" if one_node or not nodes else _slurm_first_host(nodes)
+    if "MASTER_PORT" not in env:
+        # one port per job, shared by every task of it
+        out["MASTER_PORT"] = str(20000 + int(env.get("SLURM_JOB_ID", "9531")) % 20000)
+    return out
+
+
 def _maybe_relaunch(args, argv):
-    """Single node, --gpus N > 1, not yet under torch.distributed.run: start it as a child process
-    (never exec: nothing has touched the GPU yet, and the parent only waits)."""
+    """Single node, --gpus N > 1, not yet under torch.distributed.run or a multi-task srun step: start it as a
+    child process (never exec: nothing has touched the GPU yet, and the parent only waits)."""
+    slurm = _slurm_env()
+    if slurm is not None:
+        os.environ.update(slurm)    # this task is one rank already (srun --ntasks-per-node, run.sh:4)
+        return
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         if args.num_nodes != 1:
             raise SystemExit("multi-node: launch with torch.distributed.run on every node")
@@ -98,6 +139,9 @@ def _maybe_relaunch(args, argv):
 
 
 def _init_dist():
+    slurm = _slurm_env()
+    if slurm is not None:
+        os.environ.update(slurm)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -119,8 +163,15 @@ def _split_groups(distill_layers: str):
     return groups, [l for g in groups for l in g]
 
 
-def _projections(groups, d_s, d_t, identity: bool):
+def _projections(groups, d_s, d_t, identity: bool, mode: str = "layer2layer"):
     projs = nn.ModuleList()
+    if mode == "predlayer":      # distill.py:100-107: independent Linear + GELU per distilled layer, default init
+        for g in groups:
+            for _ in g:
+                projs.append(nn.Sequential(nn.Linear(d_s, d_t), nn.GELU()))
+        return projs
+    if mode != "layer2layer":
+        raise ValueError(f"Invalid distill mode: {mode}")
     for g in groups:
         lin = nn.Linear(d_s, d_t)
         if identity:     # distill.py:24-26
@@ -147,10 +198,35 @@ def _batches(args, rank, world, dev):
     from .data import train_loader
     epoch = 0
     while True:
+        # the reference's DistributedBatchSampler permutes its batch list once (seed 0) and set_epoch does not
+        # re-permute it, so every epoch repeats one order; --reshuffle_each_epoch opts into a new order per epoch
         for w, ln in train_loader(args.tsv_dir, args.train_subset, args.seconds_per_batch, args.num_workers,
-                                  seed=epoch, rank=rank, world=world):
+                                  seed=epoch if args.reshuffle_each_epoch else 0, rank=rank, world=world):
             yield w.to(dev, non_blocking=True), ln.to(dev, non_blocking=True)
         epoch += 1
+        yield None                       # epoch boundary: validation (lightning.py:302-304, 326-342)
+
+
+def _validate(args, module, rank, world, dev):
+    """Lightning's validation loop over the ``valid`` subset (lightning.py:302-304, 326-342): eval mode, no grad,
+    the same _step; returns the mean of each logged valid_* value over this rank's share of the batches."""
+    from .data import val_loader
+    path = pathlib.Path(args.tsv_dir) / "valid.tsv"
+    if not path.exists():
+        return None
+    module.eval()
+    sums, n = {}, 0
+    with torch.no_grad():
+        for i, (w, ln) in enumerate(val_loader(args.tsv_dir, args.seconds_per_batch, args.num_workers)):
+            if i % world != rank:
+                continue
+            module._step((w.to(dev, non_blocking=True), ln.to(dev, non_blocking=True)), i, "valid")
+            for k, v in module.logged.items():
+                if k.startswith("valid_"):
+                    sums[k] = sums.get(k, 0.0) + float(v)
+            n += 1
+    module.train()
+    return {k: v / max(n, 1) for k, v in sums.items()}
 
 
 def _train(args, module, world, rank, dev):
@@ -159,7 +235,9 @@ def _train(args, module, world, rank, dev):
     from . import ops
     ops.manual_seed(2022 + rank)
     module = module.to(dev)
-    trainer = Trainer(module, clip_norm=args.clip_norm, accum_grad=args.accum_grad)
+    graphs = args.graphs == "on" or (args.graphs == "auto" and args.synthetic_utterances > 0)
+    trainer = Trainer(module, clip_norm=args.clip_norm, accum_grad=args.accum_grad, graphs=graphs,
+                      grad_dtype=torch.bfloat16 if args.grad_comm_dtype == "bf16" else torch.float32)
     ckpt_dir = args.exp_dir / "ckpts"
     if args.resume_checkpoint is not None:
         ck = _load(args.resume_checkpoint)
@@ -178,6 +256,14 @@ def _train(args, module, world, rank, dev):
     while module.global_step < args.max_updates:
         for _ in range(args.accum_grad):
             batch = next(feed)
+            while batch is None:         # end of an epoch of the corpus
+                val = _validate(args, module, rank, world, dev)
+                if rank == 0 and val:
+                    line = json.dumps(dict({"step": module.global_step}, **{k: round(v, 6) for k, v in val.items()}))
+                    print(line, flush=True)
+                    log_f.write(line + "\n")
+                    log_f.flush()
+                batch = next(feed)
             audio += batch[0].shape[0] * batch[0].shape[1] / 16000.0
             loss = trainer.step(batch)
         gs = module.global_step
@@ -235,10 +321,9 @@ def distill_main(argv=None):
     res = student.load_state_dict(sck["state_dict"], strict=False)
     _LG.info("student: missing %s, unexpected %s", res.missing_keys, res.unexpected_keys)
     groups, layers = _split_groups(args.distill_layers)
-    if args.distill_mode != "layer2layer":
-        raise NotImplementedError("predlayer distill mode is not on the HIP path")
     projs = _projections(groups, student.encoder.feature_projection.projection.out_features,
-                         teacher.encoder.feature_projection.projection.out_features, identity=True)
+                         teacher.encoder.feature_projection.projection.out_features, identity=True,
+                         mode=args.distill_mode)
     module = DistillModule(teacher_model=teacher, student_model=student, distill_mode=args.distill_mode,
                            distill_layers=layers, distill_linear_projs=projs,
                            distill_loss=DistillLoss(args.l2_weight, args.l1_weight, args.cos_weight, args.cos_type),
@@ -272,10 +357,9 @@ def final_distill_main(argv=None):
     student = wav2vec2_model(**sck["config"])
     student.load_state_dict(sck["state_dict"], strict=False)
     groups, layers = _split_groups(args.distill_layers)
-    if args.distill_mode != "layer2layer":
-        raise NotImplementedError("predlayer distill mode is not on the HIP path")
     projs = _projections(groups, student.encoder.feature_projection.projection.out_features,
-                         teacher.encoder.feature_projection.projection.out_features, identity=False)
+                         teacher.encoder.feature_projection.projection.out_features, identity=False,
+                         mode=args.distill_mode)
     projs.load_state_dict(sck["distill_linear_projs"])
     module = DistillModule(teacher_model=teacher, student_model=student, distill_mode=args.distill_mode,
                            distill_layers=layers, distill_linear_projs=projs,

@@ -37,6 +37,51 @@ __global__ void hc_bwd_kernel(const float* __restrict__ la, const float* __restr
   dla[i] += dm[i] * pass * (hi - lo) * s * (1.0f - s) / beta;
 }
 
+// ---- batched gates: every HardConcrete module of a model in one launch (forward) / one launch
+// (backward), instead of one pair of launches per module (31 per step for HuBERT-Base conv,head,interm).
+// The entry table travels BY VALUE in the kernel arguments, so a captured HIP graph replays it with
+// no device-side table; DPH_HC_BANK_CHUNK entries per launch.
+constexpr int kBankChunk = DPH_HC_BANK_CHUNK;
+struct BankArgs {
+  const float* la[kBankChunk];
+  const float* uin[kBankChunk];   // fwd: injected u (NULL: draw); bwd: unused
+  float* dst[kBankChunk];          // fwd: unused (mask at mask_flat + off); bwd: dlog_alpha (+=)
+  const float* dm[kBankChunk];     // bwd: dmask (NULL: no gradient reached this gate)
+  int64_t off[kBankChunk];         // offset of the entry in the flat u / mask buffers
+  int32_t n[kBankChunk];
+};
+
+__device__ __forceinline__ float hc_s(float u, float la, float beta) {
+  return 1.0f / (1.0f + __expf(-((__logf(u / (1.0f - u)) + la) / beta)));
+}
+
+// grid (ceil(max n / 256), entries)
+__global__ void __launch_bounds__(256) hc_bank_fwd_kernel(BankArgs a, float* __restrict__ u_flat,
+                                                          float* __restrict__ mask_flat, uint64_t seed, float beta,
+                                                          float lo, float hi, float eps) {
+  seed = epoch_seed(seed);
+  const int e = blockIdx.y;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.n[e]) return;
+  const int64_t f = a.off[e] + i;
+  // u ~ U(eps, 1-eps) (hardconcrete.py:96), counter = flat index over the whole bank
+  const float u = a.uin[e] ? a.uin[e][i] : eps + (1.0f - 2.0f * eps) * rand_uniform(seed, (uint64_t)f);
+  u_flat[f] = u;
+  const float v = hc_s(u, a.la[e][i], beta) * (hi - lo) + lo;
+  mask_flat[f] = fminf(fmaxf(v, 0.0f), 1.0f);
+}
+
+__global__ void __launch_bounds__(256) hc_bank_bwd_kernel(BankArgs a, const float* __restrict__ u_flat, float beta,
+                                                          float lo, float hi) {
+  const int e = blockIdx.y;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.n[e] || a.dm[e] == nullptr) return;
+  const float s = hc_s(u_flat[a.off[e] + i], a.la[e][i], beta);
+  const float v = s * (hi - lo) + lo;
+  const float pass = (v >= 0.0f && v <= 1.0f) ? 1.0f : 0.0f;   // clamp backward on the closed interval
+  a.dst[e][i] += a.dm[e][i] * pass * (hi - lo) * s * (1.0f - s) / beta;
+}
+
 // l0[g] = sum_i sigmoid(la_g[i] + bias), one block per group
 __global__ void __launch_bounds__(256) l0_kernel(const float* const* __restrict__ ptrs,
                                                  const int64_t* __restrict__ sizes, float bias,
@@ -128,6 +173,48 @@ extern "C" int dph_hc_sample_bwd(const float* log_alpha, const float* u, const f
   hipLaunchKernelGGL(hc_bwd_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, stream, log_alpha, u, dmask,
                      dlog_alpha, n, beta, limit_l, limit_r);
   return check_launch("dph_hc_sample_bwd");
+}
+
+static int bank_launch(bool fwd, const DphHcEntry* entries, int64_t n_entries, float* u_flat, float* mask_flat,
+                       uint64_t seed, float beta, float lo, float hi, float eps, hipStream_t stream) {
+  for (int64_t c0 = 0; c0 < n_entries; c0 += kBankChunk) {
+    const int ne = (int)std::min<int64_t>(kBankChunk, n_entries - c0);
+    BankArgs a = {};
+    int64_t nmax = 0;
+    for (int e = 0; e < ne; ++e) {
+      const DphHcEntry& x = entries[c0 + e];
+      DPH_REQUIRE(x.log_alpha && x.n > 0 && x.n < (1ll << 31) && x.offset >= 0, "dph_hc_bank: bad entry %lld",
+                  (long long)(c0 + e));
+      DPH_REQUIRE(fwd || x.dmask == nullptr || x.dlog_alpha, "dph_hc_bank_bwd: entry %lld has a dmask but no "
+                  "dlog_alpha", (long long)(c0 + e));
+      a.la[e] = x.log_alpha;
+      a.uin[e] = x.u_in;
+      a.dst[e] = x.dlog_alpha;
+      a.dm[e] = x.dmask;
+      a.off[e] = x.offset;
+      a.n[e] = (int32_t)x.n;
+      nmax = std::max<int64_t>(nmax, x.n);
+    }
+    const dim3 grid((unsigned)cdiv(nmax, 256), (unsigned)ne);
+    if (fwd)
+      hipLaunchKernelGGL(hc_bank_fwd_kernel, grid, dim3(256), 0, stream, a, u_flat, mask_flat, seed, beta, lo, hi, eps);
+    else
+      hipLaunchKernelGGL(hc_bank_bwd_kernel, grid, dim3(256), 0, stream, a, (const float*)u_flat, beta, lo, hi);
+  }
+  return check_launch(fwd ? "dph_hc_bank_fwd" : "dph_hc_bank_bwd");
+}
+
+extern "C" int dph_hc_bank_fwd(const DphHcEntry* entries, int64_t n_entries, float* u_flat, float* mask_flat,
+                               uint64_t seed, float beta, float limit_l, float limit_r, float eps, hipStream_t stream) {
+  DPH_REQUIRE(entries && n_entries > 0 && u_flat && mask_flat, "dph_hc_bank_fwd: bad args");
+  return bank_launch(true, entries, n_entries, u_flat, mask_flat, seed, beta, limit_l, limit_r, eps, stream);
+}
+
+extern "C" int dph_hc_bank_bwd(const DphHcEntry* entries, int64_t n_entries, const float* u_flat, float beta,
+                               float limit_l, float limit_r, hipStream_t stream) {
+  DPH_REQUIRE(entries && n_entries > 0 && u_flat, "dph_hc_bank_bwd: bad args");
+  return bank_launch(false, entries, n_entries, const_cast<float*>(u_flat), nullptr, 0, beta, limit_l, limit_r, 0.f,
+                     stream);
 }
 
 extern "C" int dph_expected_params_fwd(const float* const* la_ptrs, const int64_t* la_sizes, int64_t n_groups,

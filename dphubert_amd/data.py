@@ -212,3 +212,13 @@ def train_loader(tsv_dir, subset: str, seconds_per_batch: float, num_workers: in
     ds_sampler = DistributedBatchSampler(bs, num_replicas=world, rank=rank, shuffle=True, seed=seed)
     return torch.utils.data.DataLoader(ds, batch_sampler=ds_sampler, collate_fn=CollateFnAudio(pad=False),
                                        num_workers=num_workers, pin_memory=torch.cuda.is_available())
+
+
+def val_loader(tsv_dir, seconds_per_batch: float, num_workers: int = 1):
+    """distill.py's validation dataloader (lightning.py:326-342): the ``valid`` subset, same bucketing, no rank
+    split or shuffle (callers take every world-th batch)."""
+    ds = AudioDataset(tsv_dir, "valid")
+    bs = BucketizeBatchSampler(ds.len_list, num_buckets=1000, max_token_count=int(seconds_per_batch * 16000),
+                               min_len=32000, max_len=250000, shuffle=False)
+    return torch.utils.data.DataLoader(ds, batch_sampler=bs, collate_fn=CollateFnAudio(pad=False),
+                                       num_workers=num_workers, pin_memory=torch.cuda.is_available())

@@ -14,7 +14,11 @@ NCCL).  Design for one 8x MI355X node:
 * bucket size defaults to 64 MB: the ring all-reduce on xGMI is per-link
   bound, so few large collectives beat DDP's 25 MB default;
 * the average is applied in the collective (``ReduceOp.AVG``) on RCCL, or by
-  a scale after SUM on gloo (CPU tests).
+  a scale after SUM on gloo (CPU tests);
+* ``comm_dtype=torch.bfloat16`` halves the payload on the links (191 MB
+  instead of 382 MB per step): each bucket is cast to a persistent bf16 buffer right
+  before its collective and cast back into the fp32 bucket after it; the optimizer
+  still reads fp32 gradients (masters and moments stay fp32).
 """
 
 from typing import Iterable, List, Optional, Sequence
@@ -34,7 +38,11 @@ class GradReducer:
     """
 
     def __init__(self, params: Iterable[torch.nn.Parameter], bucket_mb: float = 64.0, process_group=None,
-                 groups: Optional[Sequence[Sequence[torch.nn.Parameter]]] = None, direct: bool = True):
+                 groups: Optional[Sequence[Sequence[torch.nn.Parameter]]] = None, direct: bool = True,
+                 comm_dtype: torch.dtype = torch.float32):
+        if comm_dtype not in (torch.float32, torch.bfloat16):
+            raise ValueError(f"comm_dtype must be float32 or bfloat16, got {comm_dtype}")
+        self.comm_dtype = comm_dtype
         self.group = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
         ps: List[torch.nn.Parameter] = []
@@ -92,6 +100,9 @@ class GradReducer:
         self._hooks = [p.register_post_accumulate_grad_hook(self._hook) for p in self.params]
         self.backend = dist.get_backend(process_group) if dist.is_initialized() else None
         self.enabled = self.world > 1
+        # persistent bf16 payload buffers (allocated once: a captured HIP graph replays them by address)
+        self.payload = [torch.empty(f.numel(), dtype=torch.bfloat16, device=f.device) if
+                        (self.enabled and comm_dtype == torch.bfloat16) else None for f in self.flat]
         self.sync = True
         self._seen = set()
 
@@ -134,6 +145,9 @@ class GradReducer:
 
     def _launch(self, bi):
         f = self.flat[bi]
+        if self.payload[bi] is not None:
+            f = self.payload[bi]
+            f.copy_(self.flat[bi])                 # stream-ordered after the bucket's last gradient kernel
         if self.backend == "nccl":
             self._handles[bi] = dist.all_reduce(f, op=dist.ReduceOp.AVG, group=self.group, async_op=True)
         else:
@@ -148,6 +162,8 @@ class GradReducer:
                 self._launch(bi)
         for bi, h in enumerate(self._handles):
             h.wait()
+            if self.payload[bi] is not None:
+                self.flat[bi].copy_(self.payload[bi])
             if self.backend != "nccl":
                 self.flat[bi].div_(self.world)
         for p in self.params:

@@ -128,6 +128,12 @@ class DistillModule(nn.Module):
         # distinct projection modules (shared per group, distill.py:94-99) and the per-layer index into them
         uniq, index = [], []
         for m in distill_linear_projs:
+            if distill_mode == "predlayer":
+                # nn.Sequential(nn.Linear, nn.GELU) per distilled layer (distill.py:100-107), never shared
+                if not (isinstance(m, nn.Sequential) and isinstance(m[0], nn.Linear) and isinstance(m[1], nn.GELU)
+                        and m[1].approximate == "none"):
+                    raise ValueError("predlayer distill heads must be nn.Sequential(nn.Linear, nn.GELU())")
+                m = m[0]
             for j, u in enumerate(uniq):
                 if u is m:
                     index.append(j)
@@ -195,12 +201,15 @@ class DistillModule(nn.Module):
         if self.distill_mode == "layer2layer":
             s_layers = [student_hiddens[idx] for idx in self.distill_layers]
         elif self.distill_mode == "predlayer":
-            raise NotImplementedError("predlayer distill mode (Linear+GELU heads) is not on the HIP path yet")
+            # lightning.py:259-260: every head projects the LAST student hidden state
+            s_layers = [student_hiddens[-1]] * len(self.distill_layers)
         else:
             raise ValueError(f"Invalid distill mode: {self.distill_mode}")
         B, T, Ds = s_layers[0].shape
         cfg = dict(self.distill_loss.cfg(), L=len(s_layers), P=len(self._proj_uniq), B=B, T=T,
                    proj_index=self._proj_index)
+        if self.distill_mode == "predlayer":
+            cfg.update(head_act="gelu", shared_input=True)
         pw = []
         for m in self._proj_uniq:
             pw += [m.weight, m.bias]

@@ -424,6 +424,94 @@ class HardConcreteFn(torch.autograd.Function):
         return dla, None
 
 
+class HardConcreteBank:
+    """Every HardConcrete gate of one model (in the order of its expected-size polynomial table), sampled by
+    ONE launch per step and differentiated by ONE launch, together with the expected #params (model.py:109-113)
+    so that both gradients of a log_alpha land in one backward node (no AccumulateGrad adds)."""
+
+    def __init__(self, mods, table: "ExpectedParamsTable"):
+        self.mods = list(mods)
+        self.table = table
+        self.sizes = [m.log_alpha.numel() for m in self.mods]
+        self.offsets = _offs(table) if table is not None else []
+        self.total = sum(self.sizes)
+
+    def noise(self, m):
+        """Injected u of a gate (HardConcrete.set_noise) as a device fp32 tensor (converted once), or None."""
+        u = m._noise
+        if u is None:
+            return None
+        hit = getattr(m, "_noise_dev", None)
+        if hit is not None and hit[0] is u:
+            return hit[1]
+        d = u.to(m.log_alpha.device, torch.float32).contiguous()
+        m._noise_dev = (u, d)
+        return d
+
+
+def _hc_entries(rows):
+    arr = (_lib.DphHcEntry * len(rows))()
+    for e, (la, uin, dm, dla, n, off) in zip(arr, rows):
+        e.log_alpha, e.u_in, e.dmask, e.dlog_alpha, e.n, e.offset = la, uin, dm, dla, n, off
+    return arr
+
+
+class HardConcreteBankFn(torch.autograd.Function):
+    """forward(bank, *log_alphas) -> (*masks, expected #params); backward: one poly-gradient launch + one gate
+    launch, accumulating straight into the data-parallel buckets when their sinks are armed."""
+
+    @staticmethod
+    def forward(ctx, bank: HardConcreteBank, *las):
+        dev = las[0].device
+        u = torch.empty(bank.total, dtype=F32, device=dev)
+        masks = torch.empty(bank.total, dtype=F32, device=dev)
+        noise = [bank.noise(m) for m in bank.mods]
+        rows = [(la.data_ptr(), ptr(nz), None, None, n, off) for la, nz, n, off in
+                zip(las, noise, bank.sizes, bank.offsets)]
+        call("dph_hc_bank_fwd", _hc_entries(rows), len(rows), ptr(u), ptr(masks), SEEDS.next(), HC_BETA, HC_LIMIT_L,
+             HC_LIMIT_R, HC_EPS, _s())
+        table = bank.table
+        l0 = torch.empty(len(las), dtype=F32, device=dev)
+        num = torch.empty((), dtype=F32, device=dev)
+        call("dph_expected_params_fwd", ptr(table.ptr_table(las)), ptr(table.sizes), len(las), ptr(table.coef),
+             ptr(table.idx), table.n_terms, table.constant, HC_BIAS, ptr(l0), ptr(num), _s())
+        ctx.bank = bank
+        ctx.save_for_backward(u, l0, *las)
+        return tuple(masks[o:o + n].view_as(la) for la, n, o in zip(las, bank.sizes, bank.offsets)) + (num,)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        bank = ctx.bank
+        u, l0, *las = ctx.saved_tensors
+        dmasks, dnum = grads[:-1], grads[-1]
+        dev = u.device
+        table = bank.table
+        sinks = [getattr(la, "_dph_sink", None) for la in las]
+        direct = all(sk is not None for sk in sinks) and all(sk[0] is sinks[0][0] for sk in sinks)
+        if direct:
+            gflat = sinks[0][0]
+            goff = _table([(sk[1],) for sk in sinks])
+            dst = [gflat.data_ptr() + 4 * sk[1] for sk in sinks]
+        else:
+            gflat = zeros_f32(bank.total, dev)
+            goff = table.offsets
+            dst = [gflat.data_ptr() + 4 * o for o in bank.offsets]
+        if dnum is not None:
+            call("dph_expected_params_bwd", ptr(table.ptr_table(las)), ptr(gflat), ptr(goff), ptr(table.sizes),
+                 len(las), ptr(table.coef), ptr(table.idx), table.n_terms, ptr(l0), ptr(dnum.contiguous()), HC_BIAS,
+                 _s())
+        keep = [dm.contiguous() if dm is not None else None for dm in dmasks]
+        rows = [(la.data_ptr(), None, ptr(dm), d, n, off) for la, dm, d, n, off in
+                zip(las, keep, dst, bank.sizes, bank.offsets)]
+        if any(dm is not None for dm in keep):
+            call("dph_hc_bank_bwd", _hc_entries(rows), len(rows), ptr(u), HC_BETA, HC_LIMIT_L, HC_LIMIT_R, _s())
+        if direct:
+            for la in las:
+                la._dph_sink_ready(la)
+            return (None,) * (1 + len(las))
+        return (None,) + tuple(gflat[o:o + n].view_as(la) for la, n, o in zip(las, bank.sizes, bank.offsets))
+
+
 # ---------------------------------------------------------------------------
 # Expected number of parameters (differentiable, from l0 norms)
 # ---------------------------------------------------------------------------
@@ -1475,9 +1563,16 @@ class DistillProjLossFn(torch.autograd.Function):
         dev = sh[0].device
         s = torch.empty(L, M, Dt, dtype=F32, device=dev)
         imgs = [bf16_image(pw[2 * p]) for p in range(P)]
+        # predlayer heads (distill.py:100-107): Linear + exact-erf GELU in the GEMM epilogue, the pre-activation
+        # kept in bf16 for the backward
+        gelu = cfg.get("head_act") == "gelu"
+        pre = torch.empty(L, M, Dt, dtype=BF16, device=dev) if gelu else None
         for l in range(L):
             p = cfg["proj_index"][l]
-            K.linear_fwd(sh[l], imgs[p], pw[2 * p + 1], out=s[l])
+            if gelu:
+                K.linear_fwd(sh[l], imgs[p], pw[2 * p + 1], out=s[l], act=K.ACT_GELU, pre_out=pre[l])
+            else:
+                K.linear_fwd(sh[l], imgs[p], pw[2 * p + 1], out=s[l])
         rowstats = torch.empty(L * M * 3, dtype=F32, device=dev)
         partial = torch.empty(3, dtype=F32, device=dev)
         out = torch.empty(4, dtype=F32, device=dev)
@@ -1486,6 +1581,7 @@ class DistillProjLossFn(torch.autograd.Function):
              int(cfg["cos_type"] == "log_sig"), ptr(rowstats), ptr(partial), ptr(out), _s())
         ctx.cfg = cfg
         ctx.params = pw
+        ctx.pre = pre
         ctx.save_for_backward(s, rowstats, *sh, *imgs, *th)
         return out[0], out[1], out[2], out[3]
 
@@ -1510,13 +1606,25 @@ class DistillProjLossFn(torch.autograd.Function):
         pw = ctx.params
         dW = [go.buf(pw[2 * p])[0] for p in range(P)]
         db = [go.buf(pw[2 * p + 1])[0] for p in range(P)]
+        if ctx.pre is not None:
+            # through the heads' GELU: dz = ds * gelu'(pre), in place
+            call("dph_gelu_mask_bwd", ptr(ds), ptr(ctx.pre), None, ptr(ds), None, L * M, Dt, _s())
+            ctx.pre = None
+        # predlayer: every head reads the same (last) hidden state -> one chained input gradient
+        shared = cfg.get("shared_input", False)
         dh = []
         keep = []
+        acc = None
         for l in range(L):
             p = cfg["proj_index"][l]
             keep.append(K.linear_wgrad(ds[l], sh[l], dW[p], accumulate=True))
             call("dph_colsum", ptr(ds[l]), ptr(db[p]), M, Dt, *colsum_ws(M, Dt, dev), _s())
-            dh.append(K.linear_dgrad(ds[l], imgs[p], w_t=t_image(imgs[p])))
+            if shared:
+                acc = K.linear_dgrad(ds[l], imgs[p], w_t=t_image(imgs[p]), residual=acc)
+            else:
+                dh.append(K.linear_dgrad(ds[l], imgs[p], w_t=t_image(imgs[p])))
+        if shared:
+            dh = [acc] + [None] * (L - 1)
         go.done()
         grads = [None] + dh
         for p in range(P):

@@ -120,38 +120,54 @@ class Trainer:
     """One process per GPU; call ``step(batch)`` per micro-batch (optimizer update every
     ``accum_grad`` calls).
 
-    ``graphs=True``: the first ``graph_warmup`` steps run eagerly (they build the optimizer state,
-    the gradient buckets and every cached GEMM image), the next one captures the whole step into a
-    HIP graph, and every later step copies its batch into the graph's static input buffers and
-    replays it.  Batches must keep one shape; ``accum_grad`` must be 1.  If the capture fails (an
-    op on the path that cannot be captured) the trainer warns and stays eager.
+    ``graphs=True``: the first ``graph_warmup`` optimizer steps run eagerly (they build the optimizer state,
+    the gradient buckets and every cached GEMM image); after that every micro-step replays a captured HIP
+    graph of its kind -- (first micro-step: zero the buckets) x (final micro-step: all-reduce, clip, AdamW);
+    one graph when ``accum_grad`` is 1, three when it is > 2 (run_large.sh:54's ``--accum_grad 3``) -- each
+    captured the first time it is needed, all sharing one memory pool.  Every micro-step copies its batch into
+    the graphs' static input buffers, so batches must keep one shape.  If a capture fails (an op on the path
+    that cannot be captured) the trainer warns and stays eager.
     """
 
     def __init__(self, module: DistillModule, clip_norm: float = 10.0, bucket_mb: float = 64.0,
-                 accum_grad: int = 1, graphs: bool = False, graph_warmup: int = 2):
+                 accum_grad: int = 1, graphs: bool = False, graph_warmup: int = 2, grad_dtype=torch.float32):
         self.module = module
         opt = module.configure_optimizers(clip_norm=clip_norm)
         self.optimizer = opt["optimizer"]
         self.scheduler = opt["lr_scheduler"]["scheduler"]
         params = [p for g in self.optimizer.param_groups for p in g["params"]]
-        self.reducer = GradReducer(params, bucket_mb=bucket_mb, groups=fused_grad_groups(module.student_model))
-        self.accum_grad = accum_grad
+        self.reducer = GradReducer(params, bucket_mb=bucket_mb, groups=fused_grad_groups(module.student_model),
+                                   comm_dtype=grad_dtype)
+        if accum_grad < 1:
+            raise ValueError("accum_grad must be >= 1")
+        self.accum_grad = int(accum_grad)
         self._micro = 0
-        if graphs and accum_grad != 1:
-            raise ValueError("Trainer(graphs=True) replays whole optimizer steps: accum_grad must be 1")
         self.graphs = bool(graphs)
         self.graph_warmup = max(1, int(graph_warmup))
-        self._n_eager = 0
-        self._graph = None
+        self._n_eager = 0                # eager OPTIMIZER steps so far
+        self._graphs = {}                # (zero, final) -> (graph, static loss)
+        self._pool = None
         self._prof_graph = None
         self._static = None
-        self._static_loss = None
         self._prof_loss = None
         self.scalars = None
         # teacher forward on a side stream (DPH_TEACHER_STREAM=0 keeps one stream)
         if os.environ.get("DPH_TEACHER_STREAM", "1") != "0" and torch.cuda.is_available() and \
                 next(module.parameters()).is_cuda:
             module.teacher_stream = torch.cuda.Stream()
+
+    @property
+    def _graph(self):
+        """The graph of the final micro-step (the whole optimizer step when accum_grad is 1), or None."""
+        g = self._graphs.get((self.accum_grad == 1, True))
+        return g[0] if g is not None else None
+
+    @_graph.setter
+    def _graph(self, value):
+        if value is None:
+            self._graphs = {}
+        else:
+            raise AttributeError("graphs are captured by Trainer.step")
 
     # ---- per-step device scalars -------------------------------------------------------------
     def _bind_scalars(self, device):
@@ -168,9 +184,9 @@ class Trainer:
                                           adam_step=adam_step)
 
     # ---- the GPU half of one (micro-)step: no host sync, capturable ---------------------------
-    def _gpu_step(self, batch, final: bool):
+    def _gpu_step(self, batch, zero: bool, final: bool):
         m = self.module
-        self.reducer.prepare(zero=self._micro == 0, sync=final)
+        self.reducer.prepare(zero=zero, sync=final)
         loss = m.training_step(batch, 0)
         (loss / self.accum_grad if self.accum_grad > 1 else loss).backward()
         if final:
@@ -178,19 +194,21 @@ class Trainer:
             self.optimizer.launch()
         return loss
 
-    def _capture(self, prof=None):
-        """Record one whole step into a HIP graph (nothing executes during capture)."""
+    def _capture(self, zero: bool, final: bool, prof=None):
+        """Record one (micro-)step into a HIP graph (nothing executes during capture)."""
         from .kernels import LaunchProfiler
         ops.reset_zero_arena()           # zero-filled scratch must be allocated (and filled) inside the graph
         g = torch.cuda.CUDAGraph()
         try:
             if prof is not None:
                 LaunchProfiler.active = prof
-            with torch.cuda.graph(g):
-                loss = self._gpu_step(self._static, True)
+            with torch.cuda.graph(g, pool=self._pool):
+                loss = self._gpu_step(self._static, zero, final)
         finally:
             LaunchProfiler.active = None
             ops.reset_zero_arena()
+        if self._pool is None:
+            self._pool = g.pool()
         return g, loss
 
     def _set_static(self, batch):
@@ -207,7 +225,7 @@ class Trainer:
             sl.copy_(lengths)
 
     def prepare_profiled_step(self, prof):
-        """Capture a second graph of the step whose GEMM launches are bracketed by timing events
+        """Capture a second graph of the final micro-step whose GEMM launches are bracketed by timing events
         (bench.py's live roofline); ``step(batch, profiled=True)`` replays it."""
         if self._graph is None:
             raise RuntimeError("prepare_profiled_step needs the main graph (run the warm-up steps first)")
@@ -216,7 +234,7 @@ class Trainer:
         # the rocprof trace for the same launches)
         side, self.module.teacher_stream = self.module.teacher_stream, None
         try:
-            self._prof_graph, self._prof_loss = self._capture(prof)
+            self._prof_graph, self._prof_loss = self._capture(self.accum_grad == 1, True, prof)
         finally:
             self.module.teacher_stream = side
 
@@ -225,37 +243,39 @@ class Trainer:
         m = self.module
         m.train()
         dev = batch[0].device
+        zero = self._micro == 0
         final = self._micro + 1 == self.accum_grad
         adam_step = self.optimizer.begin_step() if final else self.optimizer._step + 1
         self._upload(dev, adam_step)
+        loss = None
         if self.graphs and self._n_eager >= self.graph_warmup:
             self._set_static(batch)
-            if self._graph is None:
+            key = (zero, final)
+            if key not in self._graphs:
                 try:
-                    self._graph, self._static_loss = self._capture()
+                    self._graphs[key] = self._capture(zero, final)
                 except Exception as e:  # noqa: BLE001 -- uncapturable op: stay eager
                     warnings.warn(f"HIP graph capture failed, running eagerly: {e!r}")
                     self.graphs = False
-                    self._graph = None
-            if self._graph is not None:
-                if profiled and self._prof_graph is not None:
+                    self._graphs = {}
+            if key in self._graphs:
+                if profiled and final and self._prof_graph is not None:
                     self._prof_graph.replay()
                     loss = self._prof_loss
                 else:
-                    self._graph.replay()
-                    loss = self._static_loss
-            else:
-                loss = self._gpu_step(batch, final)
-        else:
-            loss = self._gpu_step(batch, final)
-            self._n_eager += 1
+                    g, loss = self._graphs[key]
+                    g.replay()
+        if loss is None:
+            loss = self._gpu_step(batch, zero, final)
+            if final:
+                self._n_eager += 1
         if not final:
             self._micro += 1
             return loss.detach()
         self._micro = 0
         loss = loss.detach()
         self.scheduler.step()
-        if self._graph is None:
+        if not self._graphs:
             for g in self.optimizer.param_groups:
                 for p in g["params"]:
                     p.grad = None

@@ -32,6 +32,7 @@ class HardConcrete(nn.Module):
         self.eps = eps
         self.compiled_mask = None
         self._noise: Optional[torch.Tensor] = None
+        self._bank_mask: Optional[torch.Tensor] = None   # this step's mask from the model's batched launch
         self.reset_parameters()
 
     def reset_parameters(self):
@@ -49,6 +50,9 @@ class HardConcrete(nn.Module):
     def forward(self) -> torch.Tensor:
         if self.training:
             self.compiled_mask = None
+            if self._bank_mask is not None:      # sampled with every other gate of the model in one launch
+                m, self._bank_mask = self._bank_mask, None
+                return m
             if not self.log_alpha.is_cuda:
                 raise RuntimeError("HardConcrete training-mode sampling runs on the GPU only (no CPU path)")
             u = self._noise

@@ -29,6 +29,10 @@ class Wav2Vec2Model(Module):
         self.aux = aux
         self._np_table = None
         self._np_key = None
+        self._np_mods = None
+        self._bank = None
+        self._bank_num = None      # (expected #params of the last batched gate launch, log_alpha versions)
+        self._lmax_hint = None     # crop length of the last eager _normalize (used while a HIP graph is captured)
 
     def _normalize(self, waveforms, lengths):
         """model.py:96-103: per-utterance LayerNorm over each waveform's valid samples (HIP kernel),
@@ -41,18 +45,54 @@ class Wav2Vec2Model(Module):
         y = torch.empty_like(x)
         ops.call("dph_wave_layernorm", ops.ptr(x), ops.ptr(ln), B, S, 1e-5, ops.ptr(y), ops._s())
         if ln is not None:
-            lmax = int(ln.max())
+            # pad_sequence cuts the batch to max(lengths); that needs the value on the host.  While a HIP graph
+            # is being captured no device->host read is allowed: the crop of the preceding eager step (same
+            # batch shape) is reused -- crop-to-min collation gives lmax == S anyway
+            if torch.cuda.is_current_stream_capturing():
+                if self._lmax_hint is None or self._lmax_hint[0] != S:
+                    raise RuntimeError("normalize_waveform under HIP-graph capture needs an eager step of the same "
+                                       "batch shape first (its crop length is reused)")
+                lmax = self._lmax_hint[1]
+            else:
+                lmax = int(ln.max())
+                self._lmax_hint = (S, lmax)
             if lmax < S:
                 y = y[:, :lmax].contiguous()
         return y
+
+    def _sample_gates(self):
+        """Training mode: sample every HardConcrete gate of the model in ONE launch (and its expected #params)
+        before the forward; each gate's forward() then hands out its slice."""
+        self._bank_num = None
+        if not self.training or not next(self.parameters()).is_cuda:
+            return
+        self._ensure_table()
+        mods = self._np_mods
+        if not mods:
+            return
+        if self._bank is None or self._bank.mods != mods:
+            self._bank = ops.HardConcreteBank(mods, self._np_table)
+        las = [m.log_alpha for m in mods]
+        outs = ops.HardConcreteBankFn.apply(self._bank, *las)
+        for m, mask in zip(mods, outs[:-1]):
+            m._bank_mask = mask
+        self._bank_num = (outs[-1], tuple((id(la), la._version) for la in las))
+
+    def _drop_gates(self):
+        for m in (self._np_mods or []) if self._bank is not None else []:
+            m._bank_mask = None
 
     def extract_features(self, waveforms: Tensor, lengths: Optional[Tensor] = None,
                          num_layers: Optional[int] = None) -> Tuple[List[Tensor], Optional[Tensor]]:
         """model.py:57-107.  Returns the N+1 hidden states (B, T, D) (bf16) and the frame lengths."""
         if self.normalize_waveform:
             waveforms = self._normalize(waveforms, lengths)
-        x, lengths = self.feature_extractor(waveforms, lengths)
-        x = self.encoder.extract_features(x, lengths, num_layers)
+        self._sample_gates()
+        try:
+            x, lengths = self.feature_extractor(waveforms, lengths)
+            x = self.encoder.extract_features(x, lengths, num_layers)
+        finally:
+            self._drop_gates()
         return x, lengths
 
     # ---- expected size ----------------------------------------------------
@@ -62,9 +102,8 @@ class Wav2Vec2Model(Module):
         total = fe_poly + self.encoder.poly(ctx, in_feat)
         return total, ctx.mods
 
-    def get_num_params(self):
-        """Differentiable expected parameter count (model.py:109-113) as a 0-d device tensor."""
-        key = tuple(id(m) for m in self.modules())
+    def _ensure_table(self):
+        key = tuple(id(m) for m in self.modules()) + (next(self.parameters()).device,)
         if self._np_key != key:
             poly, mods = self._num_params_poly()
             terms = [(c, k) for k, c in poly.t.items() if k and c != 0.0]
@@ -73,7 +112,19 @@ class Wav2Vec2Model(Module):
             self._np_table = ops.ExpectedParamsTable(terms, constant, [m.n_in for m in mods], dev)
             self._np_mods = mods
             self._np_key = key
+            self._bank = None
+
+    def get_num_params(self):
+        """Differentiable expected parameter count (model.py:109-113) as a 0-d device tensor.  In training mode
+        it is the value computed with this step's batched gate launch (one backward node for both gradients of
+        every log_alpha), while the log_alphas are unchanged since."""
+        self._ensure_table()
         las = [m.log_alpha for m in self._np_mods]
+        if self._bank_num is not None:
+            num, key = self._bank_num
+            self._bank_num = None
+            if key == tuple((id(la), la._version) for la in las):
+                return num
         if not las:
             return torch.tensor(float(self._np_table.constant), device=next(self.parameters()).device)
         return ops.ExpectedParamsFn.apply(self._np_table, *las)
@@ -89,14 +140,20 @@ class Wav2Vec2Model(Module):
         remaining_heads = transformer_config["remaining_heads"]
         ff_interm_features = transformer_config["ff_interm_features"]
         self._np_key = None
+        self._bank = None
+        self._bank_num = None
         return conv_config, use_attention, use_feed_forward, num_heads, remaining_heads, ff_interm_features
 
     def forward(self, waveforms: Tensor, lengths: Optional[Tensor] = None) -> Tuple[Tensor, Optional[Tensor]]:
         """model.py:127-169."""
         if self.normalize_waveform:
             waveforms = self._normalize(waveforms, lengths)
-        x, lengths = self.feature_extractor(waveforms, lengths)
-        x = self.encoder(x, lengths)
+        self._sample_gates()
+        try:
+            x, lengths = self.feature_extractor(waveforms, lengths)
+            x = self.encoder(x, lengths)
+        finally:
+            self._drop_gates()
         if self.aux is not None:
             x = self.aux(x.float())
         return x, lengths

@@ -318,6 +318,26 @@ int dph_hc_sample_fwd(const float* log_alpha, const float* u_in, float* u_out, f
 int dph_hc_sample_bwd(const float* log_alpha, const float* u, const float* dmask, float* dlog_alpha, int64_t n,
                       float beta, float limit_l, float limit_r, hipStream_t stream);
 
+/* Batched gates: every HardConcrete module of a model in ONE forward launch and ONE backward launch
+ * (per DPH_HC_BANK_CHUNK entries) instead of a pair per module (hardconcrete.py:85-99 called by
+ * components.py:112-114, :424-434, :735-746 once per module and step).  The host array `entries` is
+ * read at call time and travels by value in the kernel arguments (capturable in a HIP graph).
+ * fwd: u_flat[off+i] = u_in ? u_in[i] : U(eps, 1-eps) from (seed, off+i); mask_flat[off+i] = gate.
+ * bwd: for entries with dmask != NULL: dlog_alpha[i] += dmask[i] * dgate/dlog_alpha (u from u_flat). */
+#define DPH_HC_BANK_CHUNK 32
+typedef struct DphHcEntry {
+  const float* log_alpha;  /* [n] */
+  const float* u_in;       /* fwd: injected noise [n] or NULL */
+  const float* dmask;      /* bwd: [n] or NULL */
+  float* dlog_alpha;       /* bwd: [n], accumulated */
+  int64_t n;
+  int64_t offset;          /* into u_flat / mask_flat */
+} DphHcEntry;
+int dph_hc_bank_fwd(const DphHcEntry* entries, int64_t n_entries, float* u_flat, float* mask_flat, uint64_t seed,
+                    float beta, float limit_l, float limit_r, float eps, hipStream_t stream);
+int dph_hc_bank_bwd(const DphHcEntry* entries, int64_t n_entries, const float* u_flat, float beta, float limit_l,
+                    float limit_r, hipStream_t stream);
+
 /* Expected #params as a polynomial in the l0 norms of n_groups HardConcrete
  * modules: value = const + sum_t coef[t] * prod_{i<3, idx[t][i]>=0} l0[idx[t][i]],
  * l0[g] = sum sigmoid(la_g + bias).  la_ptrs/la_sizes: device arrays of

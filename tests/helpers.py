@@ -46,11 +46,20 @@ def rel_l2(a, b):
 
 
 def ck_close(t, ck, rtol=1e-5, atol=1e-6):
-    """Compare a tensor with a golden checksum dict."""
+    """Compare a tensor with a golden checksum dict: (max |sample err| / max |sample|, relative sum-of-squares
+    error)."""
+    e_max, _, e_sq = ck_errors(t, ck, atol)
+    return e_max, e_sq
+
+
+def ck_errors(t, ck, atol=1e-6):
+    """(max |sample err| / max |sample|, rel-L2 of the sampled entries, relative sum-of-squares error)."""
     t = t.detach().double().flatten()
     assert t.numel() == ck["n"], (t.numel(), ck["n"])
-    s = t[ck["sample_idx"]].float()
-    err = (s - ck["sample"]).abs().max().item()
-    scale = ck["sample"].abs().max().item() + atol
+    s = t[ck["sample_idx"]]
+    want = ck["sample"].double()
+    err = (s - want).abs().max().item()
+    scale = want.abs().max().item() + atol
+    rl2 = ((s - want).norm() / want.norm().clamp_min(1e-30)).item()
     sq = (t * t).sum().item()
-    return err / scale, abs(sq - ck["sq"]) / max(ck["sq"], 1e-30)
+    return err / scale, rl2, abs(sq - ck["sq"]) / max(ck["sq"], 1e-30)

@@ -79,13 +79,26 @@ def _reference_grads(world, accum):
     return {n: p.grad / world for n, p in net.named_parameters()}
 
 
-def _worker(rank, world, port, sink, accum, bucket_mb, q):
+def _reference_abs_mean(world, accum):
+    """mean over ranks of |rank's accumulated gradient| (the scale the bf16 rounding error is relative to)."""
+    out = {}
+    for r in range(world):
+        net = Net(sink=False)
+        for m in range(accum):
+            (net(_inputs(r, m)) / accum).backward()
+        for n, p in net.named_parameters():
+            out[n] = out.get(n, 0) + p.grad.abs() / world
+    return out
+
+
+def _worker(rank, world, port, sink, accum, bucket_mb, q, comm="fp32"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         net = Net(sink=sink)
-        red = GradReducer(list(net.parameters()), bucket_mb=bucket_mb, groups=net.groups())
+        red = GradReducer(list(net.parameters()), bucket_mb=bucket_mb, groups=net.groups(),
+                          comm_dtype=torch.bfloat16 if comm == "bf16" else torch.float32)
         for m in range(accum):
             red.prepare(zero=m == 0, sync=m + 1 == accum)
             (net(_inputs(rank, m)) / accum).backward()
@@ -106,14 +119,20 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("sink,accum,bucket_mb", [(False, 1, 64.0), (True, 1, 64.0), (True, 2, 1e-4),
-                                                  (False, 3, 1e-4)])
-def test_grad_reducer_gloo_ws2(sink, accum, bucket_mb):
+@pytest.mark.parametrize("sink,accum,bucket_mb,comm", [(False, 1, 64.0, "fp32"), (True, 1, 64.0, "fp32"),
+                                                       (True, 2, 1e-4, "fp32"), (False, 3, 1e-4, "fp32"),
+                                                       (True, 1, 64.0, "bf16"), (True, 3, 1e-4, "bf16"),
+                                                       (False, 2, 64.0, "bf16")])
+def test_grad_reducer_gloo_ws2(sink, accum, bucket_mb, comm):
+    """fp32 payload: exact mean of the ranks' accumulated gradients.  bf16 payload (half the link
+    bytes): each rank's accumulated gradient is rounded to bf16 (8 mantissa bits) before the sum, so the mean
+    is within 2 bf16 ulps (2 * 2^-8 relative) of the exact one, elementwise."""
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, sink, accum, bucket_mb, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, sink, accum, bucket_mb, q, comm))
+             for r in range(world)]
     for p in procs:
         p.start()
     got = dict(q.get(timeout=120) for _ in range(world))
@@ -123,7 +142,13 @@ def test_grad_reducer_gloo_ws2(sink, accum, bucket_mb):
     want = _reference_grads(world, accum)
     for r in range(world):
         for n, g in want.items():
-            assert torch.allclose(torch.from_numpy(got[r][n]), g, rtol=1e-5, atol=1e-6), (r, n)
+            x = torch.from_numpy(got[r][n])
+            if comm == "bf16":
+                bound = 2 * 2.0 ** -8 * _reference_abs_mean(world, accum)[n] + 1e-6
+                assert ((x - g).abs() <= bound).all(), (r, n, (x - g).abs().max())
+                assert torch.equal(torch.from_numpy(got[0][n]), x)   # every rank holds the same reduced values
+            else:
+                assert torch.allclose(x, g, rtol=1e-5, atol=1e-6), (r, n)
 
 
 def test_grad_out_fallback_without_reducer():

@@ -20,6 +20,17 @@ DEV = "cuda"
 
 def _cfg(family="hubert"):
     from dphubert_amd.synthetic import HUBERT_BASE_CONFIG, WAVLM_BASE_CONFIG
+    if family == "large":
+        # HuBERT-Large family at Large width (convert_hubert_large_from_fairseq.py:19-40): layer_norm extractor,
+        # pre-norm layers, normalize_waveform (its crop length is replayed from the eager step)
+        cfg = copy.deepcopy(HUBERT_BASE_CONFIG)
+        cfg.update(extractor_mode="layer_norm", encoder_embed_dim=1024, encoder_num_heads=[16] * 2,
+                   encoder_layer_norm_first=True, normalize_waveform=True)
+        cfg.update(encoder_num_layers=2, encoder_use_attention=[True] * 2, encoder_use_feed_forward=[True] * 2,
+                   encoder_ff_interm_features=[4096] * 2, encoder_projection_dropout=0.0,
+                   encoder_attention_dropout=0.0, encoder_ff_interm_dropout=0.0, encoder_dropout=0.0,
+                   encoder_layer_drop=0.0)
+        return cfg
     if family == "wavlm":
         # WavLM: the relative-position table, gate and their gradients run inside the captured graph too
         cfg = copy.deepcopy(WAVLM_BASE_CONFIG)
@@ -80,24 +91,26 @@ def test_optimizer_updates_reach_gemm_images():
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("family", ["hubert", "wavlm"])
-def test_graph_replay_matches_eager(family):
+@pytest.mark.parametrize("family,accum", [("hubert", 1), ("wavlm", 1), ("large", 1), ("hubert", 3), ("large", 2)])
+def test_graph_replay_matches_eager(family, accum):
     """Replayed steps track eager steps as closely as two eager runs track each other (the only
     run-to-run difference is the fp32 atomic order of gradient reductions, which AdamW's
-    normalisation amplifies on tiny gradients)."""
+    normalisation amplifies on tiny gradients).  accum > 1: first / middle / final micro-step graphs
+    (run_large.sh:54 --accum_grad 3)."""
     from dphubert_amd.trainer import Trainer
     batch = _batch()
-    ea = Trainer(_module(family=family), clip_norm=10.0)
-    eb = Trainer(_module(family=family), clip_norm=10.0)
-    gr = Trainer(_module(family=family), clip_norm=10.0, graphs=True, graph_warmup=1)
+    ea = Trainer(_module(family=family), clip_norm=10.0, accum_grad=accum)
+    eb = Trainer(_module(family=family), clip_norm=10.0, accum_grad=accum)
+    gr = Trainer(_module(family=family), clip_norm=10.0, graphs=True, graph_warmup=1, accum_grad=accum)
     le, lb, lg = [], [], []
-    for _ in range(5):
+    for _ in range(5 * accum):
         le.append(ea.step(batch).item())
         lb.append(eb.step(batch).item())
         lg.append(gr.step(batch).item())
     torch.cuda.synchronize()
     assert gr._graph is not None, "graph capture fell back to eager"
-    assert ea.module.global_step == gr.module.global_step
+    assert len(gr._graphs) == min(accum, 3), sorted(gr._graphs)
+    assert ea.module.global_step == gr.module.global_step == 5
     # losses: as close as two eager runs are (fp32 atomic order in weight-gradient reductions,
     # amplified by Adam over the steps) plus 1e-4
     for a, b, c in zip(le, lg, lb):

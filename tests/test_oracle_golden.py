@@ -71,7 +71,8 @@ def _run_fixture(fx):
     out = ref.distill_step(tsd, tcfg, ssd, scfg, psd, fx["distill_layers"], fx["proj_index"], wave,
                            ln if lengths is not None else None, fx["u"], fx["lambdas"], fx["global_step"],
                            l2_weight=fx["l2"], cos_type=fx["cos_type"],
-                           original_num_params=fx["original_num_params"])
+                           original_num_params=fx["original_num_params"],
+                           distill_mode=fx.get("distill_mode", "layer2layer"))
     return out
 
 
@@ -182,3 +183,32 @@ def test_wavlm_relative_position_bucket():
     for key, (nb, md, T) in (("bucket_320_800_T1000", (320, 800, 1000)), ("bucket_32_40_T200", (32, 40, 200))):
         rel = torch.arange(T)[None, :] - torch.arange(T)[:, None]
         assert torch.equal(ref.relative_position_bucket(rel, nb, md)[0], fx[key])
+
+
+@pytest.mark.slow
+def test_large_dims_max_len_g10():
+    """wav2vec2-Large dimensions (D 1024, 16 heads, FFN 4096, pre-norm, normalize_waveform), one utterance at
+    lightning.py:313's max_len (250000 samples, T = 781 frames) plus a padded one."""
+    fx = load_golden("g10_large.pt")
+    out = _run_fixture(fx)
+    assert out["student_hiddens"][0].shape == (2, 781, 1024)
+    _check_step(fx, out, tol_loss=2e-5, tol_ck=5e-4)
+
+
+def test_hubert_large_layer_norm_extractor_g11():
+    """HuBERT-Large family (layer_norm extractor) at Large dimensions, all five pruning units."""
+    fx = load_golden("g11_large_lnext.pt")
+    out = _run_fixture(fx)
+    _check_step(fx, out, tol_ck=2e-4)
+
+
+def test_predlayer_mode_g12():
+    """predlayer distill mode: independent Linear + GELU heads on the last student hidden state."""
+    fx = load_golden("g12_predlayer.pt")
+    assert fx["distill_mode"] == "predlayer"
+    out = _run_fixture(fx)
+    _check_step(fx, out)
+    for n, ck in fx["proj_grad_ck"].items():
+        # reference heads are nn.Sequential(Linear, GELU): "{i}.0.weight" is the oracle's "{i}.weight"
+        e_sample, e_sq = ck_close(out["proj_grads"][n.replace(".0.", ".", 1)], ck)
+        assert e_sample < 1e-4 and e_sq < 1e-4, (n, e_sample, e_sq)

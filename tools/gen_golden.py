@@ -148,7 +148,7 @@ def wave_batch(B, S, seed=2022, lengths=None):
 
 
 def run_step(tcfg, scfg, distill_layers_str, B, S, units, lambdas, global_step, seed=0, lengths=None,
-             full=False, cos_type="raw", l2=0.0):
+             full=False, cos_type="raw", l2=0.0, distill_mode="layer2layer"):
     """Run the reference DistillModule._step + backward; return a fixture dict."""
     scfg = dict(scfg, **units_flags(units))
     teacher, tsd = seeded_model(tcfg, seed)
@@ -159,22 +159,37 @@ def run_step(tcfg, scfg, distill_layers_str, B, S, units, lambdas, global_step, 
     layers, projs, proj_index = [], torch.nn.ModuleList(), []
     D = scfg["encoder_embed_dim"]
     proj_sd = {}
-    for gi, g in enumerate(groups):
-        lin = torch.nn.Linear(D, tcfg["encoder_embed_dim"])
-        # identity init (distill.py:24-26) perturbed by a seeded delta so grads are non-trivial
-        with torch.no_grad():
-            lin.weight.copy_(torch.eye(D) + seeded_tensor(f"proj{gi}.weight", (D, D), seed) * 0.05)
-            lin.bias.copy_(seeded_tensor(f"proj{gi}.bias", (D,), seed))
-        proj_sd[f"{gi}.weight"] = lin.weight.detach().clone()
-        proj_sd[f"{gi}.bias"] = lin.bias.detach().clone()
-        for l in g:
-            layers.append(l)
-            projs.append(lin)
+    if distill_mode == "layer2layer":
+        for gi, g in enumerate(groups):
+            lin = torch.nn.Linear(D, tcfg["encoder_embed_dim"])
+            # identity init (distill.py:24-26) perturbed by a seeded delta so grads are non-trivial
+            with torch.no_grad():
+                lin.weight.copy_(torch.eye(D) + seeded_tensor(f"proj{gi}.weight", (D, D), seed) * 0.05)
+                lin.bias.copy_(seeded_tensor(f"proj{gi}.bias", (D,), seed))
+            proj_sd[f"{gi}.weight"] = lin.weight.detach().clone()
+            proj_sd[f"{gi}.bias"] = lin.bias.detach().clone()
+            for l in g:
+                layers.append(l)
+                projs.append(lin)
+                proj_index.append(gi)
+    else:
+        # predlayer (distill.py:100-107): one independent Linear + GELU head per distilled layer, all applied to
+        # the last student hidden state (lightning.py:259-260); same seeded weight recipe per head
+        for g in groups:
+            layers.extend(g)
+        for gi in range(len(layers)):
+            lin = torch.nn.Linear(D, tcfg["encoder_embed_dim"])
+            with torch.no_grad():
+                lin.weight.copy_(torch.eye(D) + seeded_tensor(f"proj{gi}.weight", (D, D), seed) * 0.05)
+                lin.bias.copy_(seeded_tensor(f"proj{gi}.bias", (D,), seed))
+            proj_sd[f"{gi}.weight"] = lin.weight.detach().clone()
+            proj_sd[f"{gi}.bias"] = lin.bias.detach().clone()
+            projs.append(torch.nn.Sequential(lin, torch.nn.GELU()))
             proj_index.append(gi)
     loss_mod = ref_lightning.DistillLoss(l2_weight=l2, l1_weight=1.0, cos_weight=1.0, cos_type=cos_type)
     use_reg = lambdas is not None
     dm = ref_lightning.DistillModule(
-        teacher_model=teacher, student_model=student, distill_mode="layer2layer", distill_layers=layers,
+        teacher_model=teacher, student_model=student, distill_mode=distill_mode, distill_layers=layers,
         distill_linear_projs=projs, distill_loss=loss_mod, learning_rate=2e-4, weight_decay=0.0,
         warmup_updates=15000, max_updates=50000, use_reg=use_reg, reg_learning_rate=0.02 if use_reg else None,
         target_sparsity=0.75 if use_reg else None, sparsity_warmup_updates=5000 if use_reg else None,
@@ -207,6 +222,7 @@ def run_step(tcfg, scfg, distill_layers_str, B, S, units, lambdas, global_step, 
         "distill_layers": layers, "proj_index": proj_index,
         "proj_recipe": "eye(D) + 0.05*seeded_tensor('proj{g}.weight'); bias seeded_tensor('proj{g}.bias')",
         "lambdas": list(lambdas) if use_reg else None, "global_step": global_step, "cos_type": cos_type, "l2": l2,
+        "distill_mode": distill_mode,
         "u": rec.u, "loss": loss.detach(),
         "logged": {k: (v if torch.is_tensor(v) else torch.tensor(float(v))) for k, v in dm.logged.items()},
         "original_num_params": dm.original_num_params,
@@ -409,7 +425,50 @@ def gen_wavlm_prune():
             "wave": wave, "lengths": ln, "pruned_hiddens": [x.clone() for x in h]}
 
 
+def large_cfg(n_layers, **kw):
+    """wav2vec2-Large dimensions (convert_wav2vec2_large_from_fairseq.py:19-40; run_large.sh:11 teacher): D 1024,
+    16 heads, FFN 4096, pre-norm, normalize_waveform, group_norm extractor; n_layers of the 24, dropout 0."""
+    c = small_cfg(n_layers, encoder_embed_dim=1024, encoder_num_heads=[16] * n_layers,
+                  encoder_ff_interm_features=[4096] * n_layers, encoder_layer_norm_first=True, normalize_waveform=True)
+    c.update(kw)
+    return c
+
+
+def gen_large():
+    """G10: Large dimensions, 2 layers, one utterance at lightning.py:313's max_len 250000 samples (T = 781) and a
+    shorter padded one, all of conv,head,interm, regulariser active (checksums only: full hiddens are 6 MB each)."""
+    cfg = large_cfg(2)
+    return run_step(cfg, cfg, "0.1,2", B=2, S=250000, units="conv,head,interm", lambdas=(0.2, 0.1),
+                    global_step=2500, lengths=[250000, 201234])
+
+
+def gen_large_ln():
+    """G11: HuBERT-Large family (convert_hubert_large_from_fairseq.py:19-40: layer_norm extractor) at Large
+    dimensions, 2 layers, 1 x 4 s, all five units."""
+    cfg = large_cfg(2, extractor_mode="layer_norm")
+    return run_step(cfg, cfg, "0.1,2", B=1, S=64000, units="conv,head,interm,attlayer,ffnlayer",
+                    lambdas=(0.3, -0.1), global_step=6000)
+
+
+def gen_predlayer():
+    """G12: predlayer distill mode (distill.py:100-107, lightning.py:259-260) on the 2-layer Base shape, three
+    heads (distill layers 0,1,2) on the last hidden state, padded batch, regulariser active."""
+    c = small_cfg(2)
+    return run_step(c, c, "0,1,2", B=2, S=24000, units="conv,head,interm", lambdas=(0.2, 0.1), global_step=2500,
+                    lengths=[24000, 21000], full=True, distill_mode="predlayer")
+
+
 def main():
+    only = [a[len("--only="):] for a in sys.argv[1:] if a.startswith("--only=")]
+    extra = {"g10_large.pt": gen_large, "g11_large_lnext.pt": gen_large_ln, "g12_predlayer.pt": gen_predlayer}
+    if only:
+        OUT.mkdir(parents=True, exist_ok=True)
+        torch.set_num_threads(8)
+        for name in only:
+            fx = extra[name]()
+            torch.save(fx, OUT / name)
+            print(name, "done", fx["loss"].item() if "loss" in fx else "")
+        return
     OUT.mkdir(parents=True, exist_ok=True)
     torch.set_num_threads(8)
     if "--only-wavlm-prune" in sys.argv:

@@ -1,23 +1,56 @@
 #!/bin/bash
-# One GPU-box pass: parity tests, smoke, bench (with PMC traffic + CPU baseline), kernel-trace profile.
-# Usage (from the repo root on the GPU box): bash tools/gpu_round.sh [tag]
+# One GPU-box pass (run from the repo root on the box via gpurun):
+#   bash tools/gpu_round.sh TAG [phase ...]
+# phases (default: parity tests smoke bench prof):
+#   parity  -- tests/test_parity_gpu.py with -s (per-fixture error tables), all cases run; a failure ends the script
+#   tests   -- the whole -m gpu suite, -x
+#   smoke   -- __graft_entry__.smoke()
+#   bench   -- bench.py default line (PMC traffic passes + CPU baseline)
+#   prof    -- rocprofv3 --kernel-trace --stats of a short bench run -> kernel_stats.csv
+#   pmcattn -- rocprofv3 --pmc passes over the attention kernels (tools/attn_bench.py)
+# Every GPU step runs under its own timeout; the first failing step ends the script.
 set -o pipefail
-TAG=${1:-run}
+TAG=${1:-run}; shift
+PHASES=${*:-parity tests smoke bench prof}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/$TAG
 mkdir -p "$O"
 cd "$R" || exit 1
-echo "[gpu_round] pytest -m gpu"
-timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > "$O/pytest_gpu.log" 2>&1 || { tail -30 "$O/pytest_gpu.log"; exit 1; }
-tail -3 "$O/pytest_gpu.log"
-echo "[gpu_round] smoke"
-timeout -k 10 120 python -u __graft_entry__.py smoke > "$O/smoke.log" 2>&1 || { tail -30 "$O/smoke.log"; exit 1; }
-tail -1 "$O/smoke.log"
-echo "[gpu_round] bench"
-timeout -k 10 600 python -u bench.py > "$O/bench.json" 2> "$O/bench.err" || { tail -30 "$O/bench.err"; exit 1; }
-cat "$O/bench.json"
-echo "[gpu_round] rocprofv3 kernel trace"
-cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$O/prof" -o run -- python3 "$R/bench.py" --steps 5 --warmup 3 --no-cpu-baseline --traffic off > "$O/prof_bench.json" 2> "$O/prof_bench.err" || { tail -30 "$O/prof_bench.err"; exit 1; }
-cat "$O/prof_bench.json"
-echo "[gpu_round] done"
+PYT="python -u -m pytest --timeout 120 --timeout-method thread"
+for P in $PHASES; do
+  echo "[gpu_round] $P $(date +%T)"
+  case $P in
+    parity)
+      timeout -k 10 300 $PYT tests/test_parity_gpu.py -m gpu -v -s > "$O/parity.log" 2>&1
+      rc=$?; grep -E "passed|failed|Error" "$O/parity.log" | tail -5
+      [ $rc -eq 0 ] || exit $rc ;;
+    tests)
+      timeout -k 10 900 $PYT tests -m gpu -x -q > "$O/pytest_gpu.log" 2>&1 || { tail -40 "$O/pytest_gpu.log"; exit 1; }
+      tail -3 "$O/pytest_gpu.log" ;;
+    smoke)
+      timeout -k 10 180 python -u __graft_entry__.py smoke > "$O/smoke.log" 2>&1 || { tail -30 "$O/smoke.log"; exit 1; }
+      tail -1 "$O/smoke.log" ;;
+    bench)
+      timeout -k 10 700 python -u bench.py > "$O/bench.json" 2> "$O/bench.err" || { tail -30 "$O/bench.err"; exit 1; }
+      cat "$O/bench.json" ;;
+    prof)
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$O/prof" -o run \
+        -- python3 "$R/bench.py" --steps 5 --warmup 3 --no-cpu-baseline --traffic off \
+        > "$O/prof_bench.json" 2> "$O/prof_bench.err") || { tail -30 "$O/prof_bench.err"; exit 1; }
+      cat "$O/prof_bench.json"
+      f=$(find "$O/prof" -name "*kernel_stats.csv" | head -1)
+      cp "$f" "$O/kernel_stats.csv" && python3 tools/stats_csv.py "$O/kernel_stats.csv" 8 40 ;;
+    pmcattn)
+      i=0
+      for C in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU" \
+               "SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC GRBM_GUI_ACTIVE GRBM_COUNT"; do
+        i=$((i+1))
+        (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc $C --kernel-include-regex attn -f csv \
+          -d "$O/pmcattn/$i" -o run -- python3 "$R/tools/attn_bench.py" > "$O/pmcattn_$i.log" 2>&1) \
+          || { echo "rocprofv3 pass $i failed"; tail -5 "$O/pmcattn_$i.log"; exit 1; }
+      done
+      python3 tools/pmc_summary.py "$O/pmcattn" attn > "$O/pmcattn_summary.txt" && cat "$O/pmcattn_summary.txt" ;;
+    *) echo "unknown phase $P"; exit 2 ;;
+  esac
+done
+echo "[gpu_round] done $(date +%T)"
