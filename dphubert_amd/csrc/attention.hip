@@ -156,7 +156,7 @@ static_assert(RB == RBW, "table window width");
 // softmax with the other group's MFMAs).
 // ---------------------------------------------------------------------------
 template <bool DROP, bool BIAS>
-__global__ void __launch_bounds__(256, 2) attn_fwd_kernel(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ o_u,
+__global__ void __launch_bounds__(256, 2) attn_fwd_kernel(const bf16_t* __restrict__ qkv, float* __restrict__ o_u,
                                                           bf16_t* __restrict__ o_m, float* __restrict__ lse,
                                                           const float* __restrict__ head_mask,
                                                           const int64_t* __restrict__ key_len, AttnShape sh,
@@ -316,7 +316,9 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(const bf16_t* __restri
     for (int d = 0; d < 4; ++d) {
       const int col = 16 * d + 4 * g;
       float v[4] = {oacc[u][d][0] * inv_l, oacc[u][d][1] * inv_l, oacc[u][d][2] * inv_l, oacc[u][d][3] * inv_l};
-      *reinterpret_cast<uint2*>(o_u + obase + col) = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
+      // fp32: the backward's D = rowsum(dO * O) must cancel against sum_j P_j dP_j to fp32 accuracy (a bf16 O
+      // leaves 2^-9 |dO||v| of noise in every dS, which dominates dQ / dK where the softmax saturates)
+      *reinterpret_cast<float4*>(o_u + obase + col) = make_float4(v[0], v[1], v[2], v[3]);
       *reinterpret_cast<uint2*>(o_m + obase + col) =
           make_uint2(pack2bf(v[0] * hm, v[1] * hm), pack2bf(v[2] * hm, v[3] * hm));
     }
@@ -328,7 +330,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(const bf16_t* __restri
 // backward prep: rowdot[b][h][t] = sum_d dO_m * O_u ; D = hm * rowdot ; dhm[h] += sum rowdot
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) attn_bwd_prep_kernel(const bf16_t* __restrict__ dom,
-                                                            const bf16_t* __restrict__ ou,
+                                                            const float* __restrict__ ou,
                                                             const float* __restrict__ head_mask,
                                                             float* __restrict__ Dv, float* __restrict__ dhm,
                                                             int64_t B, int64_t T, int64_t H) {
@@ -338,16 +340,18 @@ __global__ void __launch_bounds__(256) attn_bwd_prep_kernel(const bf16_t* __rest
   float rd = 0.f;
   if (bt < B * T) {
     const bf16_t* a = dom + bt * H * HD + h * HD;
-    const bf16_t* c = ou + bt * H * HD + h * HD;
+    const float* c = ou + bt * H * HD + h * HD;
 #pragma unroll
     for (int k = 0; k < HD; k += 8) {
       uint4 va = *reinterpret_cast<const uint4*>(a + k);
-      uint4 vc = *reinterpret_cast<const uint4*>(c + k);
-      uint32_t wa[4] = {va.x, va.y, va.z, va.w}, wc[4] = {vc.x, vc.y, vc.z, vc.w};
+      const float4 c0 = *reinterpret_cast<const float4*>(c + k);
+      const float4 c1 = *reinterpret_cast<const float4*>(c + k + 4);
+      const float wc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+      uint32_t wa[4] = {va.x, va.y, va.z, va.w};
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        rd += __uint_as_float(wa[q] << 16) * __uint_as_float(wc[q] << 16);
-        rd += __uint_as_float(wa[q] & 0xffff0000u) * __uint_as_float(wc[q] & 0xffff0000u);
+        rd += __uint_as_float(wa[q] << 16) * wc[2 * q];
+        rd += __uint_as_float(wa[q] & 0xffff0000u) * wc[2 * q + 1];
       }
     }
     const int64_t bb = bt / T, t = bt % T;
@@ -799,7 +803,7 @@ void launch_fwd(dim3 grid, hipStream_t stream, const void* qkv, void* o_u, void*
                 const int64_t* key_len, AttnShape sh, float scale, float p, uint64_t seed, RelBias rb) {
   const size_t tw_bytes = BIAS ? (size_t)(sh.T + RB - 1) * sizeof(float) : 0;
   hipLaunchKernelGGL((attn_fwd_kernel<DROP, BIAS>), grid, dim3(256), tw_bytes, stream, reinterpret_cast<const bf16_t*>(qkv),
-                     reinterpret_cast<bf16_t*>(o_u), reinterpret_cast<bf16_t*>(o_m), lse, hm, key_len, sh, scale, p,
+                     reinterpret_cast<float*>(o_u), reinterpret_cast<bf16_t*>(o_m), lse, hm, key_len, sh, scale, p,
                      seed, rb);
 }
 
@@ -874,7 +878,7 @@ extern "C" int dph_attention_bwd_prep(const void* do_masked, const void* o_unmas
   DPH_REQUIRE(do_masked && o_unmasked && Dvec && B > 0 && T > 0 && H > 0, "dph_attention_bwd_prep: bad args");
   dim3 grid((unsigned)cdiv(B * T, 256), (unsigned)H);
   hipLaunchKernelGGL(attn_bwd_prep_kernel, grid, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(do_masked),
-                     reinterpret_cast<const bf16_t*>(o_unmasked), head_mask, Dvec, dhead_mask, B, T, H);
+                     reinterpret_cast<const float*>(o_unmasked), head_mask, Dvec, dhead_mask, B, T, H);
   return check_launch("dph_attention_bwd_prep");
 }
 

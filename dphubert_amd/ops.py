@@ -1201,7 +1201,7 @@ class EncoderLayerFn(torch.autograd.Function):
             Wqkv = bf16_image(wq, wk, wv)
             bqkv = f32_cat(bq, bk, bv)
             qkv = K.linear_fwd(h, Wqkv, bqkv)
-            o_u = torch.empty(M, Dh, dtype=BF16, device=dev)
+            o_u = torch.empty(M, Dh, dtype=F32, device=dev)     # fp32: the backward's D (attention.hip)
             o_m = torch.empty(M, Dh, dtype=BF16, device=dev)
             lse = torch.empty(B * H * T, dtype=F32, device=dev)
             seed_a = SEEDS.next() if cfg["p_attn"] > 0 else 0
@@ -1275,7 +1275,7 @@ class EncoderLayerFn(torch.autograd.Function):
             Dh = wq.shape[0]
             Wqkv = bf16_image(wq, wk, wv)
             qkv = K.linear_fwd(xn1, Wqkv, f32_cat(bq, bk, bv))
-            o_u = torch.empty(M, Dh, dtype=BF16, device=dev)
+            o_u = torch.empty(M, Dh, dtype=F32, device=dev)     # fp32: the backward's D (attention.hip)
             o_m = torch.empty(M, Dh, dtype=BF16, device=dev)
             lse = torch.empty(B * H * T, dtype=F32, device=dev)
             seed_a = SEEDS.next() if cfg["p_attn"] > 0 else 0

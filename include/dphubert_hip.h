@@ -155,13 +155,14 @@ int64_t dph_colsum_workspace(int64_t rows, int64_t cols);
  * Fused multi-head self-attention (flash style), head dim 64.
  * components.py:405-426: q,k,v read from the fused QKV buffer
  * [B*T][3*H*64] (q | k | v), scores (scale*q)k^T + (-1e4 key padding),
- * softmax, dropout(p), @v, x head_mask.  Writes o_unmasked and o_masked
- * ([B*T][H*64] bf16) and the per-row log-sum-exp [B][H][T].
+ * softmax, dropout(p), @v, x head_mask.  Writes o_unmasked ([B*T][H*64] fp32:
+ * the backward's D = rowsum(dO*O) must cancel sum_j P_j dP_j to fp32 accuracy), o_masked
+ * ([B*T][H*64] bf16, the out_proj input) and the per-row log-sum-exp [B][H][T].
  * ------------------------------------------------------------------------ */
 int dph_attention_fwd(const void* qkv, void* o_unmasked, void* o_masked, float* lse, const float* head_mask,
                       const int64_t* key_len, int64_t B, int64_t T, int64_t H, float scale, float dropout_p,
                       uint64_t seed, hipStream_t stream);
-/* backward prep: rowdot[b][h][t] = sum_d do_m*o_u ; D = head_mask*rowdot ;
+/* backward prep: rowdot[b][h][t] = sum_d do_m*o_u (o_u fp32) ; D = head_mask*rowdot ;
  * dhead_mask[h] += sum rowdot */
 int dph_attention_bwd_prep(const void* do_masked, const void* o_unmasked, const float* head_mask, float* Dvec,
                            float* dhead_mask, int64_t B, int64_t T, int64_t H, hipStream_t stream);

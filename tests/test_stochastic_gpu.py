@@ -186,8 +186,8 @@ def test_attention_dropout_keep_rate_and_scale():
     qkv = qkv.reshape(B * T, 3 * D).to(torch.bfloat16).contiguous()
     hm = torch.ones(H, device=DEV)
     lens = torch.full((B,), T, device=DEV, dtype=torch.int64)
-    o_u = torch.empty(B * T, D, device=DEV, dtype=torch.bfloat16)
-    o_m = torch.empty_like(o_u)
+    o_u = torch.empty(B * T, D, device=DEV, dtype=torch.float32)
+    o_m = torch.empty(o_u.shape, device=o_u.device, dtype=torch.bfloat16)
     lse = torch.empty(B * H * T, device=DEV)
     call("dph_attention_fwd", ptr(qkv), ptr(o_u), ptr(o_m), ptr(lse), ptr(hm), ptr(lens), B, T, H, 0.125, p, 99,
          _lib.stream_ptr())

@@ -15,8 +15,8 @@ s = _lib.stream_ptr()
 qkv = (torch.randn(M, 3 * D, device="cuda") * 0.5).to(torch.bfloat16)
 hm = torch.rand(H, device="cuda")
 lens = torch.full((B,), T, device="cuda", dtype=torch.int64)
-o_u = torch.empty(M, D, device="cuda", dtype=torch.bfloat16)
-o_m = torch.empty_like(o_u)
+o_u = torch.empty(M, D, device="cuda", dtype=torch.float32)
+o_m = torch.empty(o_u.shape, device=o_u.device, dtype=torch.bfloat16)
 lse = torch.empty(B * H * T, device="cuda")
 g = torch.randn(M, D, device="cuda").to(torch.bfloat16)
 Dv = torch.empty(B * H * T, device="cuda")

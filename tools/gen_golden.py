@@ -147,9 +147,89 @@ def wave_batch(B, S, seed=2022, lengths=None):
     return w, ln
 
 
+class Bf16Emulation:
+    """Run the reference's nn.Linear / nn.Conv1d layers the way a bf16-operand GEMM path does: input, weight and
+    output rounded to bf16 in the forward (straight-through), the gradients leaving the layer (input gradient) and
+    arriving at it (output gradient) rounded to bf16 in the backward; and the attention probabilities the way a
+    flash kernel with bf16 MFMA operands does: P rounded to bf16 before P @ V, the score gradient dS rounded to bf16
+    before dS @ K / dS^T @ Q.  Used only to MEASURE how sensitive each fixture quantity is to bf16 arithmetic (the
+    fixture's expected values always come from the exact fp32 run)."""
+
+    @staticmethod
+    def _r(t, grad_round=True):
+        tr = t.detach().to(torch.bfloat16).float()
+        out = t + (tr - t.detach())
+        if grad_round and out.requires_grad:
+            out.register_hook(lambda g: g.to(torch.bfloat16).float())
+        return out
+
+    def __enter__(self):
+        self.orig = (torch.nn.Linear.forward, torch.nn.Conv1d.forward, torch.nn.functional.softmax,
+                     torch.nn.functional.layer_norm)
+        r = self._r
+        softmax = self.orig[2]
+        layer_norm = self.orig[3]
+
+        def ln(x, *a, **k):       # bf16 activations in HBM: the LayerNorm reads and writes bf16 rows
+            return r(layer_norm(r(x), *a, **k))
+
+        def sm(x, *a, **k):
+            if x.requires_grad:
+                x.register_hook(lambda g: g.to(torch.bfloat16).float())     # dS
+            return r(softmax(x, *a, **k), False)                                # P (bf16 MFMA operand)
+
+        def lin(mod, x):
+            return r(torch.nn.functional.linear(r(x), r(mod.weight, False), mod.bias))
+
+        def conv(mod, x):
+            return r(mod._conv_forward(r(x), r(mod.weight, False), mod.bias))
+
+        torch.nn.Linear.forward = lin
+        torch.nn.Conv1d.forward = conv
+        torch.nn.functional.softmax = sm
+        torch.nn.functional.layer_norm = ln
+        return self
+
+    def __exit__(self, *exc):
+        (torch.nn.Linear.forward, torch.nn.Conv1d.forward, torch.nn.functional.softmax,
+         torch.nn.functional.layer_norm) = self.orig
+
+
+def _ck_err(a, b):
+    """(rel-L2 of the sampled entries, max sampled error / max sampled magnitude, relative sum of squares) of
+    checksum a against checksum b."""
+    sa, sb = a["sample"].double(), b["sample"].double()
+    rl2 = ((sa - sb).norm() / sb.norm().clamp_min(1e-30)).item()
+    mx = ((sa - sb).abs().max() / (sb.abs().max() + 1e-6)).item()
+    sq = abs(a["sq"] - b["sq"]) / max(b["sq"], 1e-30)
+    return (rl2, mx, sq)
+
+
+def bf16_sensitivity(exact, emulated):
+    """How far each fixture quantity moves when the reference itself runs with bf16-rounded GEMM outputs and
+    activation gradients: the conditioning the GPU parity tolerances are scaled by (tests/test_parity_gpu.py)."""
+    rl2 = lambda a, b: ((a.double() - b.double()).norm() / b.double().norm().clamp_min(1e-30)).item()  # noqa: E731
+    return {
+        "loss": abs(emulated["loss"].item() - exact["loss"].item()),
+        "grad": {n: _ck_err(emulated["grad_ck"][n], ck) for n, ck in exact["grad_ck"].items()},
+        "proj_grad": {n: _ck_err(emulated["proj_grad_ck"][n], ck) for n, ck in exact["proj_grad_ck"].items()},
+        "log_alpha": {n: rl2(emulated["log_alpha_grads"][n], g) for n, g in exact["log_alpha_grads"].items()},
+        "hidden": [_ck_err(a, b) for a, b in zip(emulated["student_hidden_ck"], exact["student_hidden_ck"])],
+    }
+
+
 def run_step(tcfg, scfg, distill_layers_str, B, S, units, lambdas, global_step, seed=0, lengths=None,
-             full=False, cos_type="raw", l2=0.0, distill_mode="layer2layer"):
-    """Run the reference DistillModule._step + backward; return a fixture dict."""
+             full=False, cos_type="raw", l2=0.0, distill_mode="layer2layer", sens=True):
+    """Run the reference DistillModule._step + backward; return a fixture dict (plus, with ``sens``, the bf16
+    sensitivity of every checked quantity from a second run under Bf16Emulation with the same noise)."""
+    if sens:
+        kw = dict(seed=seed, lengths=lengths, full=full, cos_type=cos_type, l2=l2, distill_mode=distill_mode,
+                  sens=False)
+        fx = run_step(tcfg, scfg, distill_layers_str, B, S, units, lambdas, global_step, **kw)
+        with Bf16Emulation():
+            em = run_step(tcfg, scfg, distill_layers_str, B, S, units, lambdas, global_step, **kw)
+        fx["sens"] = bf16_sensitivity(fx, em)
+        return fx
     scfg = dict(scfg, **units_flags(units))
     teacher, tsd = seeded_model(tcfg, seed)
     student, ssd = seeded_model(scfg, seed)   # student init = teacher weights (run.sh:20) + seeded log_alpha
@@ -434,6 +514,12 @@ def large_cfg(n_layers, **kw):
     return c
 
 
+def gen_base12():
+    """G3: full Base 12 layers, 1 x 10 s, distill layers 0.4,8,12 (checksums only)."""
+    return run_step(no_dropout(HUBERT_BASE_CONFIG), no_dropout(HUBERT_BASE_CONFIG), "0.4,8,12", B=1, S=160000,
+                    units="conv,head,interm", lambdas=(0.0, 0.0), global_step=5000)
+
+
 def gen_large():
     """G10: Large dimensions, 2 layers, one utterance at lightning.py:313's max_len 250000 samples (T = 781) and a
     shorter padded one, all of conv,head,interm, regulariser active (checksums only: full hiddens are 6 MB each)."""
@@ -460,7 +546,8 @@ def gen_predlayer():
 
 def main():
     only = [a[len("--only="):] for a in sys.argv[1:] if a.startswith("--only=")]
-    extra = {"g10_large.pt": gen_large, "g11_large_lnext.pt": gen_large_ln, "g12_predlayer.pt": gen_predlayer}
+    extra = {"g10_large.pt": gen_large, "g11_large_lnext.pt": gen_large_ln, "g12_predlayer.pt": gen_predlayer,
+             "g3_base12.pt": gen_base12}
     if only:
         OUT.mkdir(parents=True, exist_ok=True)
         torch.set_num_threads(8)
@@ -508,8 +595,7 @@ def main():
     torch.save(g2b, OUT / "g2b_all_units_padded.pt")
     print("g2b done", g2b["loss"].item())
     # G3: full Base 12 layers, 1 x 10 s, distill layers 0.4,8,12 (checksums only)
-    g3 = run_step(no_dropout(HUBERT_BASE_CONFIG), no_dropout(HUBERT_BASE_CONFIG), "0.4,8,12", B=1, S=160000,
-                  units="conv,head,interm", lambdas=(0.0, 0.0), global_step=5000)
+    g3 = gen_base12()
     torch.save(g3, OUT / "g3_base12.pt")
     print("g3 done", g3["loss"].item())
     torch.save(gen_prune(), OUT / "g4_prune.pt")

@@ -8,6 +8,7 @@
 #   bench   -- bench.py default line (PMC traffic passes + CPU baseline)
 #   prof    -- rocprofv3 --kernel-trace --stats of a short bench run -> kernel_stats.csv
 #   pmcattn -- rocprofv3 --pmc passes over the attention kernels (tools/attn_bench.py)
+#   pmcgemm -- the same over the dominant GEMM shape (7984 x 3072 x 768, tools/gemm_one.py)
 # Every GPU step runs under its own timeout; the first failing step ends the script.
 set -o pipefail
 TAG=${1:-run}; shift
@@ -17,6 +18,23 @@ O=$R/gpurun_out/$TAG
 mkdir -p "$O"
 cd "$R" || exit 1
 PYT="python -u -m pytest --timeout 120 --timeout-method thread"
+# pmc_run TAG KERNEL_REGEX CMD...: two rocprofv3 --pmc passes (8 SQ + 2 GRBM counters each fit one pass) and a
+# kernel-trace pass of the same command, summarised by tools/pmc_summary.py into $O/TAG_summary.txt
+pmc_run() {
+  local tag=$1 rx=$2; shift 2
+  local i=0
+  for C in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU" \
+           "SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_WAIT_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE GRBM_COUNT"; do
+    i=$((i+1))
+    (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc $C --kernel-include-regex "$rx" -f csv \
+      -d "$O/$tag/$i" -o run -- "$@" > "$O/${tag}_$i.log" 2>&1) || { echo "rocprofv3 pass $i failed"; tail -5 "$O/${tag}_$i.log"; return 1; }
+  done
+  (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --kernel-trace --stats --kernel-include-regex "$rx" \
+    -f csv -d "$O/$tag/trace" -o run -- "$@" > "$O/${tag}_trace.log" 2>&1) || { echo "trace pass failed"; return 1; }
+  python3 tools/pmc_summary.py "$O/$tag" > "$O/${tag}_summary.txt" && cat "$O/${tag}_summary.txt"
+  f=$(find "$O/$tag/trace" -name "*kernel_stats.csv" | head -1); [ -n "$f" ] && cp "$f" "$O/${tag}_kernel_stats.csv"
+  return 0
+}
 for P in $PHASES; do
   echo "[gpu_round] $P $(date +%T)"
   case $P in
@@ -41,15 +59,9 @@ for P in $PHASES; do
       f=$(find "$O/prof" -name "*kernel_stats.csv" | head -1)
       cp "$f" "$O/kernel_stats.csv" && python3 tools/stats_csv.py "$O/kernel_stats.csv" 8 40 ;;
     pmcattn)
-      i=0
-      for C in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU" \
-               "SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC GRBM_GUI_ACTIVE GRBM_COUNT"; do
-        i=$((i+1))
-        (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc $C --kernel-include-regex attn -f csv \
-          -d "$O/pmcattn/$i" -o run -- python3 "$R/tools/attn_bench.py" > "$O/pmcattn_$i.log" 2>&1) \
-          || { echo "rocprofv3 pass $i failed"; tail -5 "$O/pmcattn_$i.log"; exit 1; }
-      done
-      python3 tools/pmc_summary.py "$O/pmcattn" attn > "$O/pmcattn_summary.txt" && cat "$O/pmcattn_summary.txt" ;;
+      pmc_run pmcattn attn python3 "$R/tools/attn_bench.py" || exit 1 ;;
+    pmcgemm)
+      pmc_run pmcgemm gemm python3 "$R/tools/gemm_one.py" 7984 3072 768 5 || exit 1 ;;
     *) echo "unknown phase $P"; exit 2 ;;
   esac
 done

@@ -35,8 +35,8 @@ for (B, T, H) in [(2, 99, 12), (4, 499, 12), (2, 1999, 12)]:
     lens = torch.full((B,), T, device=DEV, dtype=torch.int64)
 
     def att():
-        o_u = torch.empty(M, D, device=DEV, dtype=torch.bfloat16)
-        o_m = torch.empty_like(o_u)
+        o_u = torch.empty(M, D, device=DEV, dtype=torch.float32)
+        o_m = torch.empty(o_u.shape, device=o_u.device, dtype=torch.bfloat16)
         lse = torch.empty(B * H * T, device=DEV)
         call("dph_attention_fwd", ptr(qkv), ptr(o_u), ptr(o_m), ptr(lse), ptr(hm), ptr(lens), B, T, H, 0.125, 0.0, 0,
              s)

@@ -20,7 +20,8 @@ for dp, _, fs in os.walk(root):
             k = r["Kernel_Name"]
             if pat and pat not in k:
                 continue
-            short = k.split("(")[0].replace("void ", "")
+            short = k.replace("(anonymous namespace)::", "").replace("void ", "")
+            short = short.split("(")[0]
             acc[short][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k in sorted(acc):
     c = {n: sum(v) / len(v) for n, v in acc[k].items()}
@@ -30,7 +31,8 @@ for k in sorted(acc):
     if "SQ_INSTS_VALU" in c and "SQ_INSTS_MFMA" in c:
         print(f"   VALU/MFMA instructions       {c['SQ_INSTS_VALU'] / max(c['SQ_INSTS_MFMA'], 1):.2f}")
     if "SQ_VALU_MFMA_BUSY_CYCLES" in c and "GRBM_GUI_ACTIVE" in c:
-        # MFMA busy is summed over SIMDs (4 per CU, 256 CUs); GRBM_GUI_ACTIVE is GPU cycles
-        print(f"   MFMA busy / (GPU cycles*1024) {c['SQ_VALU_MFMA_BUSY_CYCLES'] / max(c['GRBM_GUI_ACTIVE'] * 1024, 1):.3f}")
+        # MFMA busy cycles are summed over the 1024 SIMDs; GRBM_GUI_ACTIVE is summed over the 8 XCDs
+        # (MI355X_MICROARCH.md: kernel cycles = GRBM_GUI_ACTIVE / 8)
+        print(f"   MFMA busy fraction           {c['SQ_VALU_MFMA_BUSY_CYCLES'] / max(c['GRBM_GUI_ACTIVE'] / 8 * 1024, 1):.3f}")
     if "SQ_LDS_BANK_CONFLICT" in c and "SQ_ACTIVE_INST_LDS" in c:
         print(f"   LDS conflict / LDS active    {c['SQ_LDS_BANK_CONFLICT'] / max(c['SQ_ACTIVE_INST_LDS'], 1):.3f}")
