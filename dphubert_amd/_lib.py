@@ -71,11 +71,12 @@ _SIGS = {
     "dph_colsum": ([vp, vp, i64, i64, vp, i64, S], C.c_int),
     "dph_colsum_workspace": ([i64, i64], i64),
     "dph_layernorm_bwd_workspace": ([i64, i64], i64),
-    "dph_attention_fwd": ([vp, vp, vp, vp, vp, vp, i64, i64, i64, f32, f32, u64, S], C.c_int),
+    "dph_attention_fwd": ([vp, vp, vp, vp, vp, vp, i64, i64, i64, f32, f32, u64, vp, S], C.c_int),
+    "dph_attention_keep_bytes": ([i64, i64, i64], i64),
     "dph_attention_bwd_prep": ([vp, vp, vp, vp, vp, i64, i64, i64, S], C.c_int),
-    "dph_attention_bwd": ([vp, vp, vp, vp, vp, vp, vp, i64, i64, i64, f32, f32, u64, S], C.c_int),
-    "dph_attention_fwd_relpos": ([vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, i64, f32, f32, u64, S], C.c_int),
-    "dph_attention_bwd_relpos": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, i64, f32, f32, u64, S],
+    "dph_attention_bwd": ([vp, vp, vp, vp, vp, vp, vp, i64, i64, i64, f32, f32, u64, vp, S], C.c_int),
+    "dph_attention_fwd_relpos": ([vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, i64, f32, f32, u64, vp, S], C.c_int),
+    "dph_attention_bwd_relpos": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, i64, f32, f32, u64, vp, S],
                                  C.c_int),
     "dph_relpos_table": ([vp, vp, vp, vp, i64, i64, i64, i64, i64, S], C.c_int),
     "dph_relpos_table_bwd": ([vp, vp, vp, i64, i64, i64, i64, i64, S], C.c_int),

@@ -17,6 +17,8 @@
 // transposed LDS read ds_read_b64_tr_b16 of V / K / dO / Q tiles).
 #include "common.h"
 
+#include <type_traits>
+
 namespace dph {
 namespace {
 
@@ -106,6 +108,19 @@ __device__ __forceinline__ uint32_t attn_hash(uint64_t seed, uint64_t row, int64
   return drop_bits2(seed, row * half_tp + (uint64_t)(key >> 1));
 }
 
+// drop_bits2 for pair indices below 2^32 (every attention shape: B*H*T*ceil(T/2) < 2^32 is checked on the
+// host): the seed's high-word product is a per-launch constant, so a pair costs one xor + hash32
+__device__ __forceinline__ uint32_t seed_mix(uint64_t seed) {
+  return (uint32_t)seed ^ ((uint32_t)(seed >> 32) * 0x85EBCA6Bu);
+}
+__device__ __forceinline__ uint32_t attn_hash32(uint32_t mix, uint32_t pair) { return hash32(pair ^ mix); }
+
+// Stored keep bits (forward -> backward): uint16 word (row, key tile kt, lane group g) holds the keep bit of
+// key kt*64 + 16 s + 4 g + i at bit 4 s + i -- exactly the 16 keys lane group g of a row owns in the forward
+// and dQ MFMA layouts, so those kernels move one aligned uint16 per row and tile, and the dK/dV kernel reads
+// the row's whole 64-bit tile word.
+constexpr float L2E = 1.4426950408889634f;
+
 __device__ __forceinline__ float attn_keep(uint32_t bits, bool odd_key, uint32_t thr, float inv_keep) {
   return ((odd_key ? (bits >> 16) : (bits & 0xffffu)) >= thr) ? inv_keep : 0.f;
 }
@@ -160,8 +175,10 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(const bf16_t* __restri
                                                           bf16_t* __restrict__ o_m, float* __restrict__ lse,
                                                           const float* __restrict__ head_mask,
                                                           const int64_t* __restrict__ key_len, AttnShape sh,
-                                                          float scale, float drop_p, uint64_t seed, RelBias rb) {
+                                                          float scale, float drop_p, uint64_t seed, RelBias rb,
+                                                          uint16_t* __restrict__ keep_out) {
   seed = epoch_seed(seed);   // per-step RNG epoch (graph replays)
+  const uint32_t mix = seed_mix(seed);
   __shared__ __attribute__((aligned(16))) char smem[2 * (KTILE_PAD_BYTES + TILE_SWZ_BYTES)];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -245,60 +262,83 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(const bf16_t* __restri
       }
     }
     const int kb = kt * KT + 4 * g;   // key of (s = 0, i = 0) for this lane
+    // Softmax + dropout + PV of one tile.  MASKED: the tile holds padded (>= klen) or missing (>= T) keys;
+    // every other tile skips the per-element compares (block-uniform choice).  exp via exp2 with log2(e)
+    // folded into one fma per element: p = 2^(s*log2e - m*log2e).
+    auto tile = [&](auto masked_c) {
+      constexpr bool MASKED = decltype(masked_c)::value;
 #pragma unroll
-    for (int u = 0; u < NG; ++u) {
-      float mt = -INFINITY;
+      for (int u = 0; u < NG; ++u) {
+        float mt = -INFINITY;
 #pragma unroll
-      for (int s = 0; s < 4; ++s)
+        for (int s = 0; s < 4; ++s)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int key = kb + 16 * s + i;
-          float v = sacc[u][s][i];
-          if constexpr (BIAS) v += gq[u] * tw[rel_idx(key, (int)qme[u], T32) - toff];
-          v = key >= klen ? v - 10000.0f : v;
-          v = key >= T32 ? -INFINITY : v;
-          sacc[u][s][i] = v;
-          mt = fmaxf(mt, v);
+          for (int i = 0; i < 4; ++i) {
+            const int key = kb + 16 * s + i;
+            float v = sacc[u][s][i];
+            if constexpr (BIAS) v += gq[u] * tw[rel_idx(key, (int)qme[u], T32) - toff];
+            if constexpr (MASKED) {
+              v = key >= klen ? v - 10000.0f : v;
+              v = key >= T32 ? -INFINITY : v;
+            }
+            sacc[u][s][i] = v;
+            mt = fmaxf(mt, v);
+          }
+        mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
+        mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+        const float m_new = fmaxf(m_run[u], mt);
+        const float alpha = __builtin_amdgcn_exp2f((m_run[u] - m_new) * L2E);
+        const float ml = m_new * L2E;
+        float ls = 0.f;
+        uint32_t kbits = 0;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          uint32_t hb[2] = {0u, 0u};
+          if constexpr (DROP) {
+            const uint32_t pr = (uint32_t)(hrow[u] + (uint64_t)((kb + 16 * s) >> 1));
+            hb[0] = attn_hash32(mix, pr);
+            hb[1] = attn_hash32(mix, pr + 1);
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float p = __builtin_amdgcn_exp2f(fmaf(sacc[u][s][i], L2E, -ml));
+            ls += p;
+            if constexpr (DROP) {
+              const bool keep = ((i & 1) ? (hb[i >> 1] >> 16) : (hb[i >> 1] & 0xffffu)) >= thr;
+              kbits |= (keep ? 1u : 0u) << (4 * s + i);
+              sacc[u][s][i] = keep ? p * inv_keep : 0.f;
+            } else {
+              sacc[u][s][i] = p;
+            }
+          }
         }
-      mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
-      mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-      const float m_new = fmaxf(m_run[u], mt);
-      const float alpha = __expf(m_run[u] - m_new);
-      float ls = 0.f;
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        uint32_t hb[2] = {0u, 0u};
         if constexpr (DROP) {
-          const uint64_t pr = hrow[u] + (uint64_t)((kb + 16 * s) >> 1);
-          hb[0] = drop_bits2(seed, pr);
-          hb[1] = drop_bits2(seed, pr + 1);
+          if (keep_out != nullptr && qme[u] < T)
+            keep_out[((b * H + h) * T + qme[u]) * (nkt * 4) + kt * 4 + g] = (uint16_t)kbits;
         }
+        ls += __shfl_xor(ls, 16, 64);
+        ls += __shfl_xor(ls, 32, 64);
+        l_run[u] = l_run[u] * alpha + ls;
+        m_run[u] = m_new;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float p = __expf(sacc[u][s][i] - m_new);
-          ls += p;
-          sacc[u][s][i] = DROP ? p * attn_keep(hb[i >> 1], i & 1, thr, inv_keep) : p;
-        }
-      }
-      ls += __shfl_xor(ls, 16, 64);
-      ls += __shfl_xor(ls, 32, 64);
-      l_run[u] = l_run[u] * alpha + ls;
-      m_run[u] = m_new;
+        for (int d = 0; d < 4; ++d)
 #pragma unroll
-      for (int d = 0; d < 4; ++d)
+          for (int i = 0; i < 4; ++i) oacc[u][d][i] *= alpha;
+        // O^T[d][q] += V^T[d][key] P^T[key][q]; k index of step kk: key(g,j) = 16(2kk + j/4) + 4g + j%4
 #pragma unroll
-        for (int i = 0; i < 4; ++i) oacc[u][d][i] *= alpha;
-      // O^T[d][q] += V^T[d][key] P^T[key][q]; k index of step kk: key(g,j) = 16(2kk + j/4) + 4g + j%4
+        for (int kk = 0; kk < 2; ++kk) {
+          const bf16x8_t pf = pack_frag(sacc[u][2 * kk], sacc[u][2 * kk + 1]);
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const bf16x8_t pf = pack_frag(sacc[u][2 * kk], sacc[u][2 * kk + 1]);
-#pragma unroll
-        for (int d = 0; d < 4; ++d) {
-          const bf16x8_t vf = tr_frag(V_, 32 * kk + 4 * g, 32 * kk + 16 + 4 * g, 16 * d, lane);
-          oacc[u][d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf, oacc[u][d], 0, 0, 0);
+          for (int d = 0; d < 4; ++d) {
+            const bf16x8_t vf = tr_frag(V_, 32 * kk + 4 * g, 32 * kk + 16 + 4 * g, 16 * d, lane);
+            oacc[u][d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf, oacc[u][d], 0, 0, 0);
+          }
         }
       }
-    }
+    };
+    // (the WavLM-bias instantiations keep one masked body: a second copy spills registers there)
+    if (!BIAS && (kt + 1) * KT <= klen && (kt + 1) * KT <= T32) tile(std::integral_constant<bool, BIAS>());
+    else tile(std::integral_constant<bool, true>());
     if (more) {
       stage_store<KT, false>(ldsK(cur ^ 1), rk, tid);
       stage_store<KT, true>(ldsV(cur ^ 1), rv, tid);
@@ -369,17 +409,20 @@ __global__ void __launch_bounds__(256) attn_bwd_prep_kernel(const bf16_t* __rest
 // backward dK, dV: block = (128 keys, h, b), wave w owns keys k0 = 128*bx + 32w + 16u + (0..15),
 // u < NG.  Loops over query steps of 32 rows; Q' and dO' (= hm*dO_m) tiles staged in LDS.
 // ---------------------------------------------------------------------------
-template <bool DROP, bool BIAS>
+template <bool DROP, bool BIAS, bool KEEP>
 __global__ void __launch_bounds__(256, 2) attn_bwd_dkv_kernel(const bf16_t* __restrict__ qkv,
                                                            const bf16_t* __restrict__ dom,
                                                            const float* __restrict__ head_mask,
                                                            const float* __restrict__ lse,
                                                            const float* __restrict__ Dv, bf16_t* __restrict__ dqkv,
                                                            const int64_t* __restrict__ key_len, AttnShape sh,
-                                                           float scale, float drop_p, uint64_t seed, RelBias rb) {
+                                                           float scale, float drop_p, uint64_t seed, RelBias rb,
+                                                           const uint16_t* __restrict__ keep_in) {
   seed = epoch_seed(seed);   // per-step RNG epoch (graph replays)
+  const uint32_t mix = seed_mix(seed);
   constexpr int TB = QT_BWD * 128;   // 4096 B per tile
-  __shared__ __attribute__((aligned(16))) char smem[2 * (2 * TB) + 3 * 2 * QT_BWD * 4];
+  // + stored keep words: [2 bufs][2 key tiles of this block][32 query rows] x 64 bit
+  __shared__ __attribute__((aligned(16))) char smem[2 * (2 * TB) + 3 * 2 * QT_BWD * 4 + 2 * 2 * QT_BWD * 8];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
@@ -399,11 +442,13 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkv_kernel(const bf16_t* __re
   int64_t kme[NG];
   bool kpad[NG], kout[NG];   // key padded (masked -1e4) / past T
   const int T32 = (int)T;
+  float kmask[NG];   // additive key mask in log2 units (-1e4 * log2 e on padded keys)
 #pragma unroll
   for (int u = 0; u < NG; ++u) {
     kme[u] = k0 + 16 * u + (lane & 15);
     kpad[u] = kme[u] >= klen;
     kout[u] = kme[u] >= T;
+    kmask[u] = kpad[u] ? -10000.0f * L2E : 0.f;
   }
 
   // K[key = lane&15][hd 32ks+8g+j], V[...]: B operands of S = Q' K^T and dP = dO V^T
@@ -433,6 +478,19 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkv_kernel(const bf16_t* __re
   float* lse_s = reinterpret_cast<float*>(smem + 4 * TB);        // [2][32]
   float* dv_s = reinterpret_cast<float*>(smem + 4 * TB + 2 * QT_BWD * 4);
   float* g_s = reinterpret_cast<float*>(smem + 4 * TB + 4 * QT_BWD * 4);   // [2][32] gates (BIAS)
+  uint32_t* kw_s = reinterpret_cast<uint32_t*>(smem + 4 * TB + 6 * QT_BWD * 4);   // [2][2][32][2] keep words
+  const int nkt = (int)cdiv(T, KT);
+  constexpr bool use_keep = DROP && KEEP;   // KEEP: read the forward's stored keep bits (else re-hash)
+  // this lane's key inside its 64-key tile: word half and bit of the stored keep word (forward layout)
+  int kt_loc[NG], kbit[NG], khalf[NG];
+#pragma unroll
+  for (int u = 0; u < NG; ++u) {
+    const int key = (int)kme[u];
+    kt_loc[u] = (key >> 6) - 2 * (int)blockIdx.x;
+    const int bit = 16 * ((key >> 2) & 3) + 4 * ((key >> 4) & 3) + (key & 3);
+    khalf[u] = bit >> 5;
+    kbit[u] = bit & 31;
+  }
   extern __shared__ float tw[];   // BIAS: [T + RB - 1] table window (diagonals of this block's keys)
   const int toff = (int)blockIdx.x * RB;
   if constexpr (BIAS) stage_tab_window(tw, rb.tab + h * (2 * T - 1), toff, (int)T);   // ordered by the first barrier
@@ -448,9 +506,18 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkv_kernel(const bf16_t* __re
     stage_store<QT_BWD, true>(ldsO(buf), ro, tid);
     if (tid < QT_BWD) {
       const int64_t q = (int64_t)qt * QT_BWD + tid;
-      lse_s[buf * QT_BWD + tid] = q < T ? lse[(b * H + h) * T + q] : 0.f;
+      lse_s[buf * QT_BWD + tid] = q < T ? lse[(b * H + h) * T + q] * L2E : 0.f;   // log2 units
       dv_s[buf * QT_BWD + tid] = q < T ? Dv[(b * H + h) * T + q] : 0.f;
       if constexpr (BIAS) g_s[buf * QT_BWD + tid] = q < T ? rb.gate[(b * H + h) * T + q] : 0.f;
+    }
+    if (use_keep && tid >= 64 && tid < 128) {   // (constexpr-false unless KEEP)
+      const int r = tid & 31, lt = (tid >> 5) & 1;
+      const int64_t q = (int64_t)qt * QT_BWD + r;
+      const int ktile = 2 * (int)blockIdx.x + lt;
+      uint2 wv = make_uint2(0u, 0u);
+      if (q < T && ktile < nkt)
+        wv = *reinterpret_cast<const uint2*>(keep_in + ((b * H + h) * T + q) * (nkt * 4) + ktile * 4);
+      *reinterpret_cast<uint2*>(kw_s + ((buf * 2 + lt) * QT_BWD + r) * 2) = wv;
     }
   };
   load_tiles(0);
@@ -488,30 +555,41 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkv_kernel(const bf16_t* __re
       f32x4_t pz[2], ds[2];
 #pragma unroll
       for (int w = 0; w < 2; ++w) {
-        // this lane hashes queries ia, ia+1 of its key pair; the neighbour (key ^ 1) the other two
         uint32_t hb[4] = {0u, 0u, 0u, 0u};
         if constexpr (DROP) {
-          const int ia = odd_key ? 2 : 0;
-          const uint64_t qa = (uint64_t)(b * H + h) * T + (uint64_t)(qt * QT_BWD + 16 * w + 4 * g + ia);
-          const uint32_t h0 = attn_hash(seed, qa, kme[u], half_tp);
-          const uint32_t h1 = attn_hash(seed, qa + 1, kme[u], half_tp);
-          const uint32_t o0 = (uint32_t)__shfl_xor((int)h0, 1, 64);
-          const uint32_t o1 = (uint32_t)__shfl_xor((int)h1, 1, 64);
-          hb[0] = odd_key ? o0 : h0;
-          hb[1] = odd_key ? o1 : h1;
-          hb[2] = odd_key ? h0 : o0;
-          hb[3] = odd_key ? h1 : o1;
+          if constexpr (!use_keep) {
+            // this lane hashes queries ia, ia+1 of its key pair; the neighbour (key ^ 1) the other two
+            const int ia = odd_key ? 2 : 0;
+            const uint64_t qa = (uint64_t)(b * H + h) * T + (uint64_t)(qt * QT_BWD + 16 * w + 4 * g + ia);
+            const uint32_t h0 = attn_hash32(mix, (uint32_t)(qa * half_tp + (uint64_t)(kme[u] >> 1)));
+            const uint32_t h1 = attn_hash32(mix, (uint32_t)((qa + 1) * half_tp + (uint64_t)(kme[u] >> 1)));
+            const uint32_t o0 = (uint32_t)__shfl_xor((int)h0, 1, 64);
+            const uint32_t o1 = (uint32_t)__shfl_xor((int)h1, 1, 64);
+            hb[0] = odd_key ? o0 : h0;
+            hb[1] = odd_key ? o1 : h1;
+            hb[2] = odd_key ? h0 : o0;
+            hb[3] = odd_key ? h1 : o1;
+          }
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int ql = 16 * w + 4 * g + i;
-          const int q = qt * QT_BWD + ql;
           float sv = sacc[u][w][i];
-          if constexpr (BIAS) sv += g_s[cur * QT_BWD + ql] * tw[rel_idx((int)kme[u], q, T32) - toff];
-          sv = kpad[u] ? sv - 10000.0f : sv;
-          float p = __expf(sv - lse_s[cur * QT_BWD + ql]);
-          p = (q >= T32 || kout[u]) ? 0.f : p;
-          const float z = DROP ? attn_keep(hb[i], odd_key, thr, inv_keep) : 1.f;
+          if constexpr (BIAS) sv += g_s[cur * QT_BWD + ql] * tw[rel_idx((int)kme[u], qt * QT_BWD + ql, T32) - toff];
+          // padded keys (>= klen) get the -1e4 of the key mask; keys past T and queries past T have zero K / V / Q /
+          // dO / D rows, so their p never reaches a stored dK / dV row or a nonzero product
+          const float p = __builtin_amdgcn_exp2f(fmaf(sv, L2E, kmask[u] - lse_s[cur * QT_BWD + ql]));
+          float z = 1.f;
+          if constexpr (DROP) {
+            bool keep;
+            if constexpr (use_keep) {
+              const uint32_t wd = kw_s[((cur * 2 + kt_loc[u]) * QT_BWD + ql) * 2 + khalf[u]];
+              keep = ((wd >> kbit[u]) & 1u) != 0u;
+            } else {
+              keep = attn_keep(hb[i], odd_key, thr, 1.f) != 0.f;
+            }
+            z = keep ? inv_keep : 0.f;
+          }
           pz[w][i] = p * z;
           ds[w][i] = p * (pacc[u][w][i] * z - dv_s[cur * QT_BWD + ql]);
         }
@@ -563,16 +641,18 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkv_kernel(const bf16_t* __re
 // ---------------------------------------------------------------------------
 // backward dQ: block = (128 query rows, h, b), 4 waves x 2 x 16 rows; loops over key tiles.
 // ---------------------------------------------------------------------------
-template <bool DROP, bool BIAS>
+template <bool DROP, bool BIAS, bool KEEP>
 __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(const bf16_t* __restrict__ qkv,
                                                           const bf16_t* __restrict__ dom,
                                                           const float* __restrict__ head_mask,
                                                           const float* __restrict__ lse,
                                                           const float* __restrict__ Dv, bf16_t* __restrict__ dqkv,
                                                           const int64_t* __restrict__ key_len, AttnShape sh,
-                                                          float scale, float drop_p, uint64_t seed, RelBias rb) {
+                                                          float scale, float drop_p, uint64_t seed, RelBias rb,
+                                                          const uint16_t* __restrict__ keep_in) {
   extern __shared__ float dyn[];   // BIAS: hist [T + RB - 1] (diagonal sums of dS * gate) | table window [T + RB - 1]
   seed = epoch_seed(seed);   // per-step RNG epoch (graph replays)
+  const uint32_t mix = seed_mix(seed);
   __shared__ __attribute__((aligned(16))) char smem[2 * (TILE_SWZ_BYTES + KTILE_PAD_BYTES)];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -609,7 +689,7 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(const bf16_t* __res
       qf[u][ks] = __builtin_bit_cast(bf16x8_t, scale_bf16x8(x, scale));
       of[u][ks] = __builtin_bit_cast(bf16x8_t, scale_bf16x8(c, hm));
     }
-    my_lse[u] = qme[u] < T ? lse[(b * H + h) * T + qme[u]] : 0.f;
+    my_lse[u] = qme[u] < T ? lse[(b * H + h) * T + qme[u]] * L2E : 0.f;   // log2 units: p = 2^(s log2e - lse')
     my_D[u] = qme[u] < T ? Dv[(b * H + h) * T + qme[u]] : 0.f;
 #pragma unroll
     for (int d = 0; d < 4; ++d) dq[u][d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
@@ -650,52 +730,70 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(const bf16_t* __res
     const char* K_ = ldsK(cur);
     const char* V_ = ldsV(cur);
     f32x4_t ds[NG][4];
+    // stored keep bits of this key tile (16 per lane and row), or the in-kernel hash when none were stored
+    uint32_t kw[NG];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      f32x4_t sa[NG], pa[NG];
+    for (int u = 0; u < NG; ++u)
+      kw[u] = (DROP && KEEP && !qout[u]) ? keep_in[((b * H + h) * T + qme[u]) * (nkt * 4) + kt * 4 + g] : 0u;
+    // MASKED: the tile holds padded (>= klen) or missing (>= T) keys.  Elsewhere no per-element compare: rows
+    // past T have zero dO and D, so their dS is exactly 0 whatever p is.
+    auto tile = [&](auto masked_c) {
+      constexpr bool MASKED = decltype(masked_c)::value;
 #pragma unroll
-      for (int u = 0; u < NG; ++u) {
-        sa[u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-        pa[u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-      }
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const bf16x8_t ka = lds_b128(K_, swz128(16 * s + (lane & 15), ks * 32 + 8 * g));
-        const bf16x8_t va = lds_b128(V_, ((16 * s + (lane & 15)) * PADROW + ks * 32 + 8 * g) * 2);
+      for (int s = 0; s < 4; ++s) {
+        f32x4_t sa[NG], pa[NG];
 #pragma unroll
         for (int u = 0; u < NG; ++u) {
-          sa[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka, qf[u][ks], sa[u], 0, 0, 0);
-          pa[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, of[u][ks], pa[u], 0, 0, 0);
-        }
-      }
-      const int kb = kt * KT + 16 * s + 4 * g;
-#pragma unroll
-      for (int u = 0; u < NG; ++u) {
-        uint32_t hb[2] = {0u, 0u};
-        if constexpr (DROP) {
-          const uint64_t pr = hrow[u] + (uint64_t)(kb >> 1);
-          hb[0] = drop_bits2(seed, pr);
-          hb[1] = drop_bits2(seed, pr + 1);
+          sa[u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+          pa[u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
         }
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int key = kb + i;
-          float sv = sa[u][i];
-          float tv = 0.f;
-          if constexpr (BIAS) {
-            tv = tw[rel_idx(key, (int)qme[u], T32) - toff];
-            sv += gq[u] * tv;
+        for (int ks = 0; ks < 2; ++ks) {
+          const bf16x8_t ka = lds_b128(K_, swz128(16 * s + (lane & 15), ks * 32 + 8 * g));
+          const bf16x8_t va = lds_b128(V_, ((16 * s + (lane & 15)) * PADROW + ks * 32 + 8 * g) * 2);
+#pragma unroll
+          for (int u = 0; u < NG; ++u) {
+            sa[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka, qf[u][ks], sa[u], 0, 0, 0);
+            pa[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, of[u][ks], pa[u], 0, 0, 0);
           }
-          sv = key >= klen32 ? sv - 10000.0f : sv;
-          float p = __expf(sv - my_lse[u]);
-          p = (key >= T32 || qout[u]) ? 0.f : p;
-          const float z = DROP ? attn_keep(hb[i >> 1], i & 1, thr, inv_keep) : 1.f;
-          const float dsv = p * (pa[u][i] * z - my_D[u]);
-          ds[u][s][i] = dsv;
-          if constexpr (BIAS) dg[u] += dsv * tv;
+        }
+        const int kb = kt * KT + 16 * s + 4 * g;
+#pragma unroll
+        for (int u = 0; u < NG; ++u) {
+          uint32_t hb[2] = {0u, 0u};
+          if constexpr (DROP && !KEEP) {
+            const uint32_t pr = (uint32_t)(hrow[u] + (uint64_t)(kb >> 1));
+            hb[0] = attn_hash32(mix, pr);
+            hb[1] = attn_hash32(mix, pr + 1);
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int key = kb + i;
+            float sv = sa[u][i];
+            float tv = 0.f;
+            if constexpr (BIAS) {
+              tv = tw[rel_idx(key, (int)qme[u], T32) - toff];
+              sv += gq[u] * tv;
+            }
+            if constexpr (MASKED) sv = key >= klen32 ? sv - 10000.0f : sv;
+            float p = __builtin_amdgcn_exp2f(fmaf(sv, L2E, -my_lse[u]));
+            if constexpr (MASKED) p = (key >= T32 || qout[u]) ? 0.f : p;
+            float z = 1.f;
+            if constexpr (DROP) {
+              bool keep;
+              if constexpr (KEEP) keep = ((kw[u] >> (4 * s + i)) & 1u) != 0u;
+              else keep = attn_keep(hb[i >> 1], i & 1, thr, 1.f) != 0.f;
+              z = keep ? inv_keep : 0.f;
+            }
+            const float dsv = p * (pa[u][i] * z - my_D[u]);
+            ds[u][s][i] = dsv;
+            if constexpr (BIAS) dg[u] += dsv * tv;
+          }
         }
       }
-    }
+    };
+    if (!BIAS && (kt + 1) * KT <= klen32 && (kt + 1) * KT <= T32) tile(std::integral_constant<bool, BIAS>());
+    else tile(std::integral_constant<bool, true>());
     if constexpr (BIAS) {
       // diagonal sums of dS * gate: element (u, s, i) sits on diagonal kt*64 + 16(s-u) + 4g + i - (q - qb0 - ...)
       // of this block's histogram, so the query groups u meeting on the same s-u are added first (NG + 3
@@ -800,76 +898,97 @@ namespace {
 
 template <bool DROP, bool BIAS>
 void launch_fwd(dim3 grid, hipStream_t stream, const void* qkv, void* o_u, void* o_m, float* lse, const float* hm,
-                const int64_t* key_len, AttnShape sh, float scale, float p, uint64_t seed, RelBias rb) {
+                const int64_t* key_len, AttnShape sh, float scale, float p, uint64_t seed, RelBias rb, void* keep) {
   const size_t tw_bytes = BIAS ? (size_t)(sh.T + RB - 1) * sizeof(float) : 0;
   hipLaunchKernelGGL((attn_fwd_kernel<DROP, BIAS>), grid, dim3(256), tw_bytes, stream, reinterpret_cast<const bf16_t*>(qkv),
                      reinterpret_cast<float*>(o_u), reinterpret_cast<bf16_t*>(o_m), lse, hm, key_len, sh, scale, p,
-                     seed, rb);
+                     seed, rb, reinterpret_cast<uint16_t*>(keep));
+}
+
+template <bool DROP, bool BIAS, bool KEEP>
+void launch_bwd_k(dim3 grid, hipStream_t stream, const void* qkv, const void* dom, const float* hm, const float* lse,
+                  const float* Dvec, void* dqkv, const int64_t* key_len, AttnShape sh, float scale, float p,
+                  uint64_t seed, RelBias rb, const void* keep) {
+  const size_t tw_bytes = BIAS ? (size_t)(sh.T + RB - 1) * sizeof(float) : 0;
+  hipLaunchKernelGGL((attn_bwd_dkv_kernel<DROP, BIAS, KEEP>), grid, dim3(256), tw_bytes, stream,
+                     reinterpret_cast<const bf16_t*>(qkv), reinterpret_cast<const bf16_t*>(dom), hm, lse, Dvec,
+                     reinterpret_cast<bf16_t*>(dqkv), key_len, sh, scale, p, seed, rb,
+                     reinterpret_cast<const uint16_t*>(keep));
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<DROP, BIAS, KEEP>), grid, dim3(256), 2 * tw_bytes, stream,
+                     reinterpret_cast<const bf16_t*>(qkv), reinterpret_cast<const bf16_t*>(dom), hm, lse, Dvec,
+                     reinterpret_cast<bf16_t*>(dqkv), key_len, sh, scale, p, seed, rb,
+                     reinterpret_cast<const uint16_t*>(keep));
 }
 
 template <bool DROP, bool BIAS>
 void launch_bwd(dim3 grid, hipStream_t stream, const void* qkv, const void* dom, const float* hm, const float* lse,
                 const float* Dvec, void* dqkv, const int64_t* key_len, AttnShape sh, float scale, float p,
-                uint64_t seed, RelBias rb) {
-  const size_t tw_bytes = BIAS ? (size_t)(sh.T + RB - 1) * sizeof(float) : 0;
-  hipLaunchKernelGGL((attn_bwd_dkv_kernel<DROP, BIAS>), grid, dim3(256), tw_bytes, stream,
-                     reinterpret_cast<const bf16_t*>(qkv), reinterpret_cast<const bf16_t*>(dom), hm, lse, Dvec,
-                     reinterpret_cast<bf16_t*>(dqkv), key_len, sh, scale, p, seed, rb);
-  hipLaunchKernelGGL((attn_bwd_dq_kernel<DROP, BIAS>), grid, dim3(256), 2 * tw_bytes, stream,
-                     reinterpret_cast<const bf16_t*>(qkv), reinterpret_cast<const bf16_t*>(dom), hm, lse, Dvec,
-                     reinterpret_cast<bf16_t*>(dqkv), key_len, sh, scale, p, seed, rb);
+                uint64_t seed, RelBias rb, const void* keep) {
+  if (DROP && keep != nullptr)
+    launch_bwd_k<DROP, BIAS, true>(grid, stream, qkv, dom, hm, lse, Dvec, dqkv, key_len, sh, scale, p, seed, rb, keep);
+  else
+    launch_bwd_k<DROP, BIAS, false>(grid, stream, qkv, dom, hm, lse, Dvec, dqkv, key_len, sh, scale, p, seed, rb, keep);
 }
 
 }  // namespace
 
+// dropout pair indices (row * ceil(T/2) + key/2) must fit 32 bits (the kernels' hoisted seed mix)
+static bool pairs_fit(int64_t B, int64_t T, int64_t H) { return B * H * T * ((T + 1) / 2) < ((int64_t)1 << 32); }
+
+extern "C" int64_t dph_attention_keep_bytes(int64_t B, int64_t T, int64_t H) { return B * H * T * cdiv(T, KT) * 8; }
+
 static int attention_fwd(const void* qkv, void* o_unmasked, void* o_masked, float* lse, const float* head_mask,
                          const int64_t* key_len, int64_t B, int64_t T, int64_t H, float scale, float dropout_p,
-                         uint64_t seed, RelBias rb, hipStream_t stream) {
+                         uint64_t seed, RelBias rb, void* keep, hipStream_t stream) {
   AttnShape sh{B, T, H, 3 * H * HD};
   dim3 grid((unsigned)cdiv(T, RB), (unsigned)H, (unsigned)B);
   const bool bias = rb.tab != nullptr;
+  DPH_REQUIRE(dropout_p <= 0.f || pairs_fit(B, T, H), "dph_attention_fwd: B*H*T*ceil(T/2) >= 2^32 dropout pairs");
+  DPH_REQUIRE(keep == nullptr || (reinterpret_cast<uintptr_t>(keep) & 7) == 0, "dph_attention_fwd: keep bits not 8-B aligned");
   if (dropout_p > 0.f) {
-    if (bias) launch_fwd<true, true>(grid, stream, qkv, o_unmasked, o_masked, lse, head_mask, key_len, sh, scale, dropout_p, seed, rb);
-    else launch_fwd<true, false>(grid, stream, qkv, o_unmasked, o_masked, lse, head_mask, key_len, sh, scale, dropout_p, seed, rb);
+    if (bias) launch_fwd<true, true>(grid, stream, qkv, o_unmasked, o_masked, lse, head_mask, key_len, sh, scale, dropout_p, seed, rb, keep);
+    else launch_fwd<true, false>(grid, stream, qkv, o_unmasked, o_masked, lse, head_mask, key_len, sh, scale, dropout_p, seed, rb, keep);
   } else {
-    if (bias) launch_fwd<false, true>(grid, stream, qkv, o_unmasked, o_masked, lse, head_mask, key_len, sh, scale, dropout_p, seed, rb);
-    else launch_fwd<false, false>(grid, stream, qkv, o_unmasked, o_masked, lse, head_mask, key_len, sh, scale, dropout_p, seed, rb);
+    if (bias) launch_fwd<false, true>(grid, stream, qkv, o_unmasked, o_masked, lse, head_mask, key_len, sh, scale, dropout_p, seed, rb, nullptr);
+    else launch_fwd<false, false>(grid, stream, qkv, o_unmasked, o_masked, lse, head_mask, key_len, sh, scale, dropout_p, seed, rb, nullptr);
   }
   return check_launch("dph_attention_fwd");
 }
 
 static int attention_bwd(const void* qkv, const void* do_masked, const float* head_mask, const float* lse,
                          const float* Dvec, void* dqkv, const int64_t* key_len, int64_t B, int64_t T, int64_t H,
-                         float scale, float dropout_p, uint64_t seed, RelBias rb, hipStream_t stream) {
+                         float scale, float dropout_p, uint64_t seed, RelBias rb, const void* keep, hipStream_t stream) {
   AttnShape sh{B, T, H, 3 * H * HD};
   dim3 grid((unsigned)cdiv(T, RB), (unsigned)H, (unsigned)B);
   const bool bias = rb.tab != nullptr;
+  DPH_REQUIRE(dropout_p <= 0.f || pairs_fit(B, T, H), "dph_attention_bwd: B*H*T*ceil(T/2) >= 2^32 dropout pairs");
+  DPH_REQUIRE(keep == nullptr || (reinterpret_cast<uintptr_t>(keep) & 7) == 0, "dph_attention_bwd: keep bits not 8-B aligned");
   if (dropout_p > 0.f) {
-    if (bias) launch_bwd<true, true>(grid, stream, qkv, do_masked, head_mask, lse, Dvec, dqkv, key_len, sh, scale, dropout_p, seed, rb);
-    else launch_bwd<true, false>(grid, stream, qkv, do_masked, head_mask, lse, Dvec, dqkv, key_len, sh, scale, dropout_p, seed, rb);
+    if (bias) launch_bwd<true, true>(grid, stream, qkv, do_masked, head_mask, lse, Dvec, dqkv, key_len, sh, scale, dropout_p, seed, rb, keep);
+    else launch_bwd<true, false>(grid, stream, qkv, do_masked, head_mask, lse, Dvec, dqkv, key_len, sh, scale, dropout_p, seed, rb, keep);
   } else {
-    if (bias) launch_bwd<false, true>(grid, stream, qkv, do_masked, head_mask, lse, Dvec, dqkv, key_len, sh, scale, dropout_p, seed, rb);
-    else launch_bwd<false, false>(grid, stream, qkv, do_masked, head_mask, lse, Dvec, dqkv, key_len, sh, scale, dropout_p, seed, rb);
+    if (bias) launch_bwd<false, true>(grid, stream, qkv, do_masked, head_mask, lse, Dvec, dqkv, key_len, sh, scale, dropout_p, seed, rb, nullptr);
+    else launch_bwd<false, false>(grid, stream, qkv, do_masked, head_mask, lse, Dvec, dqkv, key_len, sh, scale, dropout_p, seed, rb, nullptr);
   }
   return check_launch("dph_attention_bwd");
 }
 
 extern "C" int dph_attention_fwd(const void* qkv, void* o_unmasked, void* o_masked, float* lse,
                                  const float* head_mask, const int64_t* key_len, int64_t B, int64_t T, int64_t H,
-                                 float scale, float dropout_p, uint64_t seed, hipStream_t stream) {
+                                 float scale, float dropout_p, uint64_t seed, void* keep_bits, hipStream_t stream) {
   DPH_REQUIRE(qkv && o_unmasked && o_masked && lse && B > 0 && T > 0 && H > 0, "dph_attention_fwd: bad args");
   return attention_fwd(qkv, o_unmasked, o_masked, lse, head_mask, key_len, B, T, H, scale, dropout_p, seed,
-                       RelBias{nullptr, nullptr, nullptr, nullptr}, stream);
+                       RelBias{nullptr, nullptr, nullptr, nullptr}, keep_bits, stream);
 }
 
 extern "C" int dph_attention_fwd_relpos(const void* qkv, void* o_unmasked, void* o_masked, float* lse,
                                         const float* head_mask, const int64_t* key_len, const float* rel_tab,
                                         const float* gate, int64_t B, int64_t T, int64_t H, float scale,
-                                        float dropout_p, uint64_t seed, hipStream_t stream) {
+                                        float dropout_p, uint64_t seed, void* keep_bits, hipStream_t stream) {
   DPH_REQUIRE(qkv && o_unmasked && o_masked && lse && rel_tab && gate && B > 0 && T > 0 && T <= 3584 && H > 0,
               "dph_attention_fwd_relpos: bad args (T <= 3584)");
   return attention_fwd(qkv, o_unmasked, o_masked, lse, head_mask, key_len, B, T, H, scale, dropout_p, seed,
-                       RelBias{rel_tab, gate, nullptr, nullptr}, stream);
+                       RelBias{rel_tab, gate, nullptr, nullptr}, keep_bits, stream);
 }
 
 extern "C" int dph_attention_bwd_prep(const void* do_masked, const void* o_unmasked, const float* head_mask,
@@ -884,20 +1003,21 @@ extern "C" int dph_attention_bwd_prep(const void* do_masked, const void* o_unmas
 
 extern "C" int dph_attention_bwd(const void* qkv, const void* do_masked, const float* head_mask, const float* lse,
                                  const float* Dvec, void* dqkv, const int64_t* key_len, int64_t B, int64_t T,
-                                 int64_t H, float scale, float dropout_p, uint64_t seed, hipStream_t stream) {
+                                 int64_t H, float scale, float dropout_p, uint64_t seed, const void* keep_bits,
+                                 hipStream_t stream) {
   DPH_REQUIRE(qkv && do_masked && lse && Dvec && dqkv && B > 0 && T > 0 && H > 0, "dph_attention_bwd: bad args");
   return attention_bwd(qkv, do_masked, head_mask, lse, Dvec, dqkv, key_len, B, T, H, scale, dropout_p, seed,
-                       RelBias{nullptr, nullptr, nullptr, nullptr}, stream);
+                       RelBias{nullptr, nullptr, nullptr, nullptr}, keep_bits, stream);
 }
 
 extern "C" int dph_attention_bwd_relpos(const void* qkv, const void* do_masked, const float* head_mask,
                                         const float* lse, const float* Dvec, void* dqkv, const int64_t* key_len,
                                         const float* rel_tab, const float* gate, float* dgate, float* drel_tab,
                                         int64_t B, int64_t T, int64_t H, float scale, float dropout_p, uint64_t seed,
-                                        hipStream_t stream) {
+                                        const void* keep_bits, hipStream_t stream) {
   DPH_REQUIRE(qkv && do_masked && lse && Dvec && dqkv && rel_tab && gate && dgate && drel_tab && B > 0 && T > 0 &&
                   T <= 3584 && H > 0,
               "dph_attention_bwd_relpos: bad args (T <= 3584: two [T+127] fp32 LDS windows + 34 KB of tiles)");
   return attention_bwd(qkv, do_masked, head_mask, lse, Dvec, dqkv, key_len, B, T, H, scale, dropout_p, seed,
-                       RelBias{rel_tab, gate, dgate, drel_tab}, stream);
+                       RelBias{rel_tab, gate, dgate, drel_tab}, keep_bits, stream);
 }

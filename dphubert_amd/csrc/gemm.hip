@@ -1043,6 +1043,32 @@ __global__ void __launch_bounds__(C::NT, C::MINB) ring_gemm_kernel(const DphGemm
     __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): nxt landed (and slot i+1 reads retired)
     __builtin_amdgcn_sched_barrier(0);
   };
+  // Steady-state step (i + 5 < H): always restages slot i%4 with slice i+4 and reads slice i+1, waits for
+  // at most 2 slices in flight.  No runtime condition is left in the body, so the MFMAs, DMAs and fragment
+  // reads of a slice form one basic block (the generic step's per-chunk `if`s compiled to ~25 scalar
+  // compare / branch instructions per slice that split the MFMAs into blocks of FN).
+  auto step_fast = [&](int i, ring::Frags<C>& cur, ring::Frags<C>& nxt) {
+    ring::wait_slices<C::DMA, 2>();
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    const char* sn = slot(i + 1);
+#pragma unroll
+    for (int q = 0; q < C::FM; ++q) {
+#pragma unroll
+      for (int j = q; j < C::DMA; j += C::FM) issue_one(i + 4, j);
+      if (q < C::FN)
+        nxt.b[q] = BK ? ring::frag(sn + C::HALF_A, wc * C::WTN + 16 * q, lane)
+                      : ring::frag_mn(sn + C::HALF_A, wc * C::WTN + 16 * q, lane, C::BN * 2);
+      nxt.a[q] = AK ? ring::frag(sn, wr * C::WTM + 16 * q, lane) : ring::frag_mn(sn, wr * C::WTM + 16 * q, lane, C::BM * 2);
+#pragma unroll
+      for (int jj = 0; jj < C::FN; ++jj)
+        acc[q][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur.b[jj], cur.a[q], acc[q][jj], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_sched_barrier(0);
+  };
 
   if (H > 0) {
 #pragma unroll
@@ -1068,6 +1094,12 @@ __global__ void __launch_bounds__(C::NT, C::MINB) ring_gemm_kernel(const DphGemm
     __builtin_amdgcn_sched_barrier(0);
     DPH_TSTAMP(st1);
     int i = 0;
+    if (DPH_ABLATE == 0) {
+      for (; i + 6 <= H; i += 2) {       // both steps of the pair have i + 5 < H
+        step_fast(i, f0, f1);
+        step_fast(i + 1, f1, f0);
+      }
+    }
     for (; i + 1 < H; i += 2) {
       step(i, f0, f1);
       step(i + 1, f1, f0);
@@ -1410,7 +1442,7 @@ extern "C" int dph_gemm(const DphGemmArgs* args, hipStream_t stream) {
     const int64_t tiles = (int64_t)grid.x * grid.y * a.batch;
     if (a.workspace_bytes >= slab + tiles * 4) {
       cnt = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(a.workspace) + slab);
-      hipMemsetAsync(cnt, 0, tiles * 4, stream);
+      if (hipMemsetAsync(cnt, 0, tiles * 4, stream) != hipSuccess) return check_launch("dph_gemm split-K ticket memset");
     }
   }
   if (small_nt(kchunk) == 512) {

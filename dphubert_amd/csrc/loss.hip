@@ -147,7 +147,7 @@ extern "C" int dph_distill_loss_fwd(const float* s, const void* const* t_layers,
               "dph_distill_loss_fwd: unsupported L=%lld D=%lld", (long long)L, (long long)D);
   TPtrs tp;
   for (int i = 0; i < DPH_MAX_DISTILL_LAYERS; ++i) tp.p[i] = i < L ? reinterpret_cast<const bf16_t*>(t_layers[i]) : nullptr;
-  hipMemsetAsync(partial, 0, 3 * sizeof(float), stream);
+  if (hipMemsetAsync(partial, 0, 3 * sizeof(float), stream) != hipSuccess) return check_launch("dph_distill_loss_fwd memset");
   const int64_t rows = B * L * T;
   hipLaunchKernelGGL(loss_fwd_kernel, dim3((unsigned)std::min<int64_t>(cdiv(rows, 4), 1024)), dim3(256), 0, stream, s,
                      tp, B, L, T, D,

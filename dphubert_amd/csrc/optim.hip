@@ -81,7 +81,7 @@ using namespace dph;
 extern "C" int dph_grad_sumsq(const DphTensorSlot* slots, int64_t n_slots, const int64_t* chunk_slot,
                               const int64_t* chunk_start, int64_t n_chunks, float* sumsq, hipStream_t stream) {
   DPH_REQUIRE(slots && chunk_slot && chunk_start && sumsq && n_slots > 0 && n_chunks > 0, "dph_grad_sumsq: bad args");
-  hipMemsetAsync(sumsq, 0, sizeof(float), stream);
+  if (hipMemsetAsync(sumsq, 0, sizeof(float), stream) != hipSuccess) return check_launch("dph_grad_sumsq memset");
   hipLaunchKernelGGL(sumsq_kernel, dim3((unsigned)n_chunks), dim3(256), 0, stream, slots, chunk_slot, chunk_start,
                      sumsq);
   return check_launch("dph_grad_sumsq");

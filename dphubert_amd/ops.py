@@ -1404,9 +1404,15 @@ class EncoderLayerFn(torch.autograd.Function):
         (dph_wavlm_gate_fwd) and the kernels add gate * rel_tab[k-q] to the scores.  Returns the gate."""
         B, T, H = cfg["B"], cfg["T"], cfg["H"]
         wl = ctx.wl
+        # attention dropout: the forward stores its keep bits (1 bit per probability, ~6 MB per layer at B=16) and
+        # the backward kernels read them instead of re-hashing every probability twice
+        keep = None
+        if cfg["p_attn"] > 0 and torch.is_grad_enabled():
+            keep = torch.empty(_lib.lib().dph_attention_keep_bytes(B, T, H) // 8, dtype=torch.int64, device=qkv.device)
+        ctx.attn_keep = keep
         if wl is None:
             call("dph_attention_fwd", ptr(qkv), ptr(o_u), ptr(o_m), ptr(lse), ptr(hm), ptr(cfg["lengths"]), B, T, H,
-                 cfg["head_dim"] ** -0.5, cfg["p_attn"], seed_a, _s())
+                 cfg["head_dim"] ** -0.5, cfg["p_attn"], seed_a, ptr(keep), _s())
             return None
         if cfg["head_dim"] != 64:
             raise NotImplementedError("WavLM gate: head_dim 64 only")
@@ -1415,7 +1421,7 @@ class EncoderLayerFn(torch.autograd.Function):
              ptr(wl["heads"]), ptr(gate), B, T, H, 64, _s())
         wl["rel_tab"] = wl["rel_tab"].contiguous()
         call("dph_attention_fwd_relpos", ptr(qkv), ptr(o_u), ptr(o_m), ptr(lse), ptr(hm), ptr(cfg["lengths"]),
-             ptr(wl["rel_tab"]), ptr(gate), B, T, H, cfg["head_dim"] ** -0.5, cfg["p_attn"], seed_a, _s())
+             ptr(wl["rel_tab"]), ptr(gate), B, T, H, cfg["head_dim"] ** -0.5, cfg["p_attn"], seed_a, ptr(keep), _s())
         return gate
 
     @staticmethod
@@ -1424,14 +1430,15 @@ class EncoderLayerFn(torch.autograd.Function):
         wl = ctx.wl
         if wl is None:
             call("dph_attention_bwd", ptr(sv["qkv"]), ptr(do_m), ptr(hm), ptr(sv["lse"]), ptr(Dvec), ptr(dqkv),
-                 ptr(cfg["lengths"]), B, T, H, cfg["head_dim"] ** -0.5, cfg["p_attn"], sv["seed_a"], _s())
+                 ptr(cfg["lengths"]), B, T, H, cfg["head_dim"] ** -0.5, cfg["p_attn"], sv["seed_a"],
+                 ptr(getattr(ctx, "attn_keep", None)), _s())
             return None
         dev = dqkv.device
         dgate = torch.empty(B * H * T, dtype=F32, device=dev)
         dtab = torch.zeros(wl["rel_tab"].shape, dtype=F32, device=dev)
         call("dph_attention_bwd_relpos", ptr(sv["qkv"]), ptr(do_m), ptr(hm), ptr(sv["lse"]), ptr(Dvec), ptr(dqkv),
              ptr(cfg["lengths"]), ptr(wl["rel_tab"]), ptr(sv["gate"]), ptr(dgate), ptr(dtab), B, T, H,
-             cfg["head_dim"] ** -0.5, cfg["p_attn"], sv["seed_a"], _s())
+             cfg["head_dim"] ** -0.5, cfg["p_attn"], sv["seed_a"], ptr(getattr(ctx, "attn_keep", None)), _s())
         return dgate, dtab
 
     @staticmethod

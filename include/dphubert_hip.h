@@ -161,7 +161,11 @@ int64_t dph_colsum_workspace(int64_t rows, int64_t cols);
  * ------------------------------------------------------------------------ */
 int dph_attention_fwd(const void* qkv, void* o_unmasked, void* o_masked, float* lse, const float* head_mask,
                       const int64_t* key_len, int64_t B, int64_t T, int64_t H, float scale, float dropout_p,
-                      uint64_t seed, hipStream_t stream);
+                      uint64_t seed, void* keep_bits, hipStream_t stream);
+/* keep_bits (dropout_p > 0, optional, 8-B aligned, dph_attention_keep_bytes(B, T, H) bytes): the forward
+ * stores its dropout keep decisions (1 bit per probability, uint16 per (row, 64-key tile, lane group)) and
+ * the backward reads them instead of re-hashing (NULL on both sides: regenerated from (seed, element)) */
+int64_t dph_attention_keep_bytes(int64_t B, int64_t T, int64_t H);
 /* backward prep: rowdot[b][h][t] = sum_d do_m*o_u (o_u fp32) ; D = head_mask*rowdot ;
  * dhead_mask[h] += sum rowdot */
 int dph_attention_bwd_prep(const void* do_masked, const void* o_unmasked, const float* head_mask, float* Dvec,
@@ -169,7 +173,7 @@ int dph_attention_bwd_prep(const void* do_masked, const void* o_unmasked, const 
 /* dq|dk|dv into dqkv [B*T][3*H*64] (bf16) */
 int dph_attention_bwd(const void* qkv, const void* do_masked, const float* head_mask, const float* lse,
                       const float* Dvec, void* dqkv, const int64_t* key_len, int64_t B, int64_t T, int64_t H,
-                      float scale, float dropout_p, uint64_t seed, hipStream_t stream);
+                      float scale, float dropout_p, uint64_t seed, const void* keep_bits, hipStream_t stream);
 
 /* ------------------------------------------------------------------------ *
  * WavLM gated relative-position bias (WavLMSelfAttention, components.py:486-659).
@@ -183,13 +187,14 @@ int dph_attention_bwd(const void* qkv, const void* do_masked, const float* head_
 /* attention forward with score += gate[b,h,q] * rel_tab[h][k-q+T-1] (T <= 3584) */
 int dph_attention_fwd_relpos(const void* qkv, void* o_unmasked, void* o_masked, float* lse, const float* head_mask,
                              const int64_t* key_len, const float* rel_tab, const float* gate, int64_t B, int64_t T,
-                             int64_t H, float scale, float dropout_p, uint64_t seed, hipStream_t stream);
+                             int64_t H, float scale, float dropout_p, uint64_t seed, void* keep_bits,
+                             hipStream_t stream);
 /* its backward: dqkv as dph_attention_bwd, plus dgate [B][H][T] (written) = sum_k dS*rel_tab and
  * drel_tab [H][2T-1] (ACCUMULATED, zero it first) = diagonal sums of dS*gate */
 int dph_attention_bwd_relpos(const void* qkv, const void* do_masked, const float* head_mask, const float* lse,
                              const float* Dvec, void* dqkv, const int64_t* key_len, const float* rel_tab,
                              const float* gate, float* dgate, float* drel_tab, int64_t B, int64_t T, int64_t H,
-                             float scale, float dropout_p, uint64_t seed, hipStream_t stream);
+                             float scale, float dropout_p, uint64_t seed, const void* keep_bits, hipStream_t stream);
 /* rel_tab[h][r] = embed[bucket(r-(T-1))][heads[h]] (embed [num_buckets][Htot] fp32; heads [H] int64 or NULL =
  * identity); buckets [2T-1] int64 (optional) receives the bucket index table; either output may be NULL */
 int dph_relpos_table(const float* embed, const int64_t* heads, float* rel_tab, int64_t* buckets, int64_t T,

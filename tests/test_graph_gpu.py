@@ -121,14 +121,17 @@ def test_graph_replay_matches_eager(family, accum):
     names = [n for n, p in gr.module.named_parameters() if p.requires_grad and not n.endswith("k_proj.bias")]
     # k_proj.bias has an exactly-zero gradient (softmax shift invariance): Adam turns the fp32
     # atomic-order noise of that zero into +-lr steps, so it is not comparable run to run.
-    # Per parameter: within 4x the eager-vs-eager drift of the same parameter or 5e-3 (small-gradient
-    # biases drift ~2e-3 between two EAGER runs after 5 Adam steps); all parameters together: within
-    # 4x the eager-vs-eager drift of the whole parameter vector.
+    # Per parameter: within 4x the eager-vs-eager drift of the same parameter or 5e-3; 1-D biases
+    # 1e-2 (their gradients are column sums with heavy cancellation, so Adam's normalised step
+    # turns atomic-order noise into drift of 2e-3..7e-3 between two EAGER runs after 5 steps, and
+    # one eager pair is a noisy estimate of that spread); all parameters together: within 4x the
+    # eager-vs-eager drift of the whole parameter vector.
     pg = dict(gr.module.named_parameters())
     for n in names:
         e = rel_l2(pg[n].detach().cpu(), pa[n].detach().cpu())
         base = rel_l2(pb[n].detach().cpu(), pa[n].detach().cpu())
-        assert e < max(5e-3, 4 * base), (n, e, base)
+        floor = 1e-2 if pg[n].dim() == 1 else 5e-3
+        assert e < max(floor, 4 * base), (n, e, base)
     cat = lambda d: torch.cat([d[n].detach().float().flatten().cpu() for n in names])  # noqa: E731
     e_all, base_all = rel_l2(cat(pg), cat(pa)), rel_l2(cat(pb), cat(pa))
     assert e_all < max(1e-5, 4 * base_all), (e_all, base_all)

@@ -52,7 +52,7 @@ def test_attention_kernel_vs_torch():
     o_m = torch.empty(o_u.shape, device=o_u.device, dtype=torch.bfloat16)
     lse = torch.empty(B * H * T, device=DEV)
     s = _lib.stream_ptr()
-    call("dph_attention_fwd", ptr(qkv), ptr(o_u), ptr(o_m), ptr(lse), ptr(hm), ptr(lens), B, T, H, 0.125, 0.0, 0, s)
+    call("dph_attention_fwd", ptr(qkv), ptr(o_u), ptr(o_m), ptr(lse), ptr(hm), ptr(lens), B, T, H, 0.125, 0.0, 0, None, s)
     # torch fp32 reference of components.py:405-426
     qkv_ref = qkv.float().clone().requires_grad_(True)
     q, k, v = qkv_ref.view(B, T, 3, H, 64).permute(2, 0, 3, 1, 4)
@@ -75,7 +75,7 @@ def test_attention_kernel_vs_torch():
     call("dph_attention_bwd_prep", ptr(g), ptr(o_u), ptr(hm), ptr(Dv), ptr(dhm), B, T, H, s)
     dqkv = torch.empty_like(qkv)
     call("dph_attention_bwd", ptr(qkv), ptr(g), ptr(hm), ptr(lse), ptr(Dv), ptr(dqkv), ptr(lens), B, T, H, 0.125,
-         0.0, 0, s)
+         0.0, 0, None, s)
     torch.cuda.synchronize()
     gq = qkv_ref.grad
     for part in range(3):
@@ -105,11 +105,11 @@ def test_attention_backward_vs_fp64_on_same_inputs(sharp):
     o_u = torch.empty(B * T, D, device=DEV, dtype=torch.float32)
     o_m = torch.empty(B * T, D, device=DEV, dtype=torch.bfloat16)
     lse = torch.empty(B * H * T, device=DEV)
-    call("dph_attention_fwd", ptr(qkv), ptr(o_u), ptr(o_m), ptr(lse), None, None, B, T, H, 0.125, 0.0, 0, s)
+    call("dph_attention_fwd", ptr(qkv), ptr(o_u), ptr(o_m), ptr(lse), None, None, B, T, H, 0.125, 0.0, 0, None, s)
     Dv = torch.empty(B * H * T, device=DEV)
     call("dph_attention_bwd_prep", ptr(g), ptr(o_u), None, ptr(Dv), None, B, T, H, s)
     dqkv = torch.empty_like(qkv)
-    call("dph_attention_bwd", ptr(qkv), ptr(g), None, ptr(lse), ptr(Dv), ptr(dqkv), None, B, T, H, 0.125, 0.0, 0, s)
+    call("dph_attention_bwd", ptr(qkv), ptr(g), None, ptr(lse), ptr(Dv), ptr(dqkv), None, B, T, H, 0.125, 0.0, 0, None, s)
     x = qkv.double().clone().requires_grad_(True)
     q, k, v = x.view(B, T, 3, H, 64).permute(2, 0, 3, 1, 4)
     w = (0.125 * q) @ k.transpose(-1, -2)
@@ -142,7 +142,7 @@ def test_attention_dropout_consistency():
         o_u = torch.empty(B * T, D, device=DEV, dtype=torch.float32)
         o_m = torch.empty(o_u.shape, device=o_u.device, dtype=torch.bfloat16)
         lse = torch.empty(B * H * T, device=DEV)
-        call("dph_attention_fwd", ptr(x), ptr(o_u), ptr(o_m), ptr(lse), None, None, B, T, H, 0.125, 0.3, seed, s)
+        call("dph_attention_fwd", ptr(x), ptr(o_u), ptr(o_m), ptr(lse), None, None, B, T, H, 0.125, 0.3, seed, None, s)
         return o_u, lse
 
     o1, _ = fwd(qkv, 77)
@@ -156,7 +156,7 @@ def test_attention_dropout_consistency():
     Dv = torch.empty(B * H * T, device=DEV)
     call("dph_attention_bwd_prep", ptr(g), ptr(o1), None, ptr(Dv), None, B, T, H, s)
     dqkv = torch.empty_like(qkv)
-    call("dph_attention_bwd", ptr(qkv), ptr(g), None, ptr(lse), ptr(Dv), ptr(dqkv), None, B, T, H, 0.125, 0.3, 77, s)
+    call("dph_attention_bwd", ptr(qkv), ptr(g), None, ptr(lse), ptr(Dv), ptr(dqkv), None, B, T, H, 0.125, 0.3, 77, None, s)
     # o is linear in v: sum(o*g) = sum(v * dv) exactly (up to bf16 rounding)
     lhs = (o1.float() * g.float()).sum()
     dv = dqkv.float().view(B * T, 3, D)[:, 2]
@@ -164,6 +164,46 @@ def test_attention_dropout_consistency():
     rhs = (v * dv).sum()
     torch.cuda.synchronize()
     assert abs(lhs.item() - rhs.item()) <= 2e-2 * abs(lhs.item()) + 1e-2
+
+
+@pytest.mark.parametrize("T,lens", [(499, None), (131, [131, 97])])
+def test_attention_stored_keep_bits_match_rehash(T, lens):
+    """Dropout keep bits stored by the forward and read by dK/dV and dQ give exactly the backward the in-kernel
+    re-hash gives (same seed and RNG epoch); the forward output does not depend on storing them."""
+    from dphubert_amd import _lib
+    from dphubert_amd._lib import call, ptr
+    torch.manual_seed(6)
+    B, H = 2, 3
+    D = H * 64
+    qkv = (torch.randn(B * T, 3 * D, device=DEV) * 0.5).to(torch.bfloat16)
+    g = torch.randn(B * T, D, device=DEV).to(torch.bfloat16)
+    hm = torch.rand(H, device=DEV)
+    ln = torch.tensor(lens, device=DEV, dtype=torch.int64) if lens else None
+    s = _lib.stream_ptr()
+    keep = torch.zeros(_lib.lib().dph_attention_keep_bytes(B, T, H) // 8, dtype=torch.int64, device=DEV)
+
+    def run(kb):
+        o_u = torch.empty(B * T, D, device=DEV, dtype=torch.float32)
+        o_m = torch.empty(B * T, D, device=DEV, dtype=torch.bfloat16)
+        lse = torch.empty(B * H * T, device=DEV)
+        call("dph_attention_fwd", ptr(qkv), ptr(o_u), ptr(o_m), ptr(lse), ptr(hm), ptr(ln), B, T, H, 0.125, 0.1, 99,
+             ptr(kb), s)
+        Dv = torch.empty(B * H * T, device=DEV)
+        call("dph_attention_bwd_prep", ptr(g), ptr(o_u), ptr(hm), ptr(Dv), None, B, T, H, s)
+        dqkv = torch.empty_like(qkv)
+        call("dph_attention_bwd", ptr(qkv), ptr(g), ptr(hm), ptr(lse), ptr(Dv), ptr(dqkv), ptr(ln), B, T, H, 0.125,
+             0.1, 99, ptr(kb), s)
+        torch.cuda.synchronize()
+        return o_u, dqkv
+
+    o1, d1 = run(None)
+    o2, d2 = run(keep)
+    assert torch.equal(o1, o2)
+    assert torch.equal(d1, d2)
+    # the stored bits are the dropout draws (keep rate 1 - p = 0.9; the slots of keys past T are drawn too)
+    import numpy as np
+    frac = np.unpackbits(keep.view(torch.uint8).cpu().numpy()).mean()
+    assert 0.88 < frac < 0.92, frac
 
 
 def test_frontend_vs_oracle():

@@ -93,8 +93,10 @@ def test_hc_device_rng_distribution():
     draws = 3000
     u_all = torch.empty(draws, tot, device=DEV)
     m_all = torch.empty(draws, tot, device=DEV)
+    from dphubert_amd.ops import SeedSource
+    seeds = SeedSource(1000)          # the per-call 64-bit seeds production draws (splitmix64 of a counter)
     for i in range(draws):
-        _bank_call(las, u_all[i], m_all[i], 1000 + i)
+        _bank_call(las, u_all[i], m_all[i], seeds.next())
     u = u_all.double().cpu()
     m = m_all.double().cpu()
     assert u.min().item() >= EPS and u.max().item() <= 1 - EPS
@@ -189,7 +191,7 @@ def test_attention_dropout_keep_rate_and_scale():
     o_u = torch.empty(B * T, D, device=DEV, dtype=torch.float32)
     o_m = torch.empty(o_u.shape, device=o_u.device, dtype=torch.bfloat16)
     lse = torch.empty(B * H * T, device=DEV)
-    call("dph_attention_fwd", ptr(qkv), ptr(o_u), ptr(o_m), ptr(lse), ptr(hm), ptr(lens), B, T, H, 0.125, p, 99,
+    call("dph_attention_fwd", ptr(qkv), ptr(o_u), ptr(o_m), ptr(lse), ptr(hm), ptr(lens), B, T, H, 0.125, p, 99, None,
          _lib.stream_ptr())
     o = o_m.float().cpu()
     kept = o != 0

@@ -37,13 +37,14 @@ def timeit(f, n=20):
     return e0.elapsed_time(e1) / n * 1e3
 
 
-for p in (0.0, 0.1):
+keep = torch.empty(_lib.lib().dph_attention_keep_bytes(B, T, H) // 8, dtype=torch.int64, device="cuda")
+for p, kb in ((0.0, None), (0.1, None), (0.1, keep)):
     fwd = lambda: call("dph_attention_fwd", ptr(qkv), ptr(o_u), ptr(o_m), ptr(lse), ptr(hm), ptr(lens), B, T, H,  # noqa
-                       0.125, p, 7, s)
+                       0.125, p, 7, ptr(kb), s)
     prep = lambda: call("dph_attention_bwd_prep", ptr(g), ptr(o_u), ptr(hm), ptr(Dv), ptr(dhm), B, T, H, s)  # noqa
     bwd = lambda: call("dph_attention_bwd", ptr(qkv), ptr(g), ptr(hm), ptr(lse), ptr(Dv), ptr(dqkv), ptr(lens),  # noqa
-                       B, T, H, 0.125, p, 7, s)
+                       B, T, H, 0.125, p, 7, ptr(kb), s)
     tf, tp, tb = timeit(fwd), timeit(prep), timeit(bwd)
     fl = 4.0 * B * H * T * T * 64
-    print(f"p={p}: fwd {tf:7.1f} us ({fl / tf / 1e6:5.0f} TF/s)  prep {tp:6.1f} us  bwd {tb:7.1f} us "
+    print(f"p={p}{' keep-bits' if kb is not None else ''}: fwd {tf:7.1f} us ({fl / tf / 1e6:5.0f} TF/s)  prep {tp:6.1f} us  bwd {tb:7.1f} us "
           f"({2.5 * fl / tb / 1e6:5.0f} TF/s)", flush=True)

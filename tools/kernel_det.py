@@ -38,7 +38,7 @@ for (B, T, H) in [(2, 99, 12), (4, 499, 12), (2, 1999, 12)]:
         o_u = torch.empty(M, D, device=DEV, dtype=torch.float32)
         o_m = torch.empty(o_u.shape, device=o_u.device, dtype=torch.bfloat16)
         lse = torch.empty(B * H * T, device=DEV)
-        call("dph_attention_fwd", ptr(qkv), ptr(o_u), ptr(o_m), ptr(lse), ptr(hm), ptr(lens), B, T, H, 0.125, 0.0, 0,
+        call("dph_attention_fwd", ptr(qkv), ptr(o_u), ptr(o_m), ptr(lse), ptr(hm), ptr(lens), B, T, H, 0.125, 0.0, 0, None,
              s)
         return o_u, o_m, lse
 
@@ -52,7 +52,7 @@ for (B, T, H) in [(2, 99, 12), (4, 499, 12), (2, 1999, 12)]:
         call("dph_attention_bwd_prep", ptr(g), ptr(o_u), ptr(hm), ptr(Dv), ptr(dhm), B, T, H, s)
         dqkv = torch.empty_like(qkv)
         call("dph_attention_bwd", ptr(qkv), ptr(g), ptr(hm), ptr(lse), ptr(Dv), ptr(dqkv), ptr(lens), B, T, H, 0.125,
-             0.0, 0, s)
+             0.0, 0, None, s)
         return (dqkv,)
 
     check(f"attention_bwd B{B} T{T}", attb)
