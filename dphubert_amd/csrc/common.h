@@ -41,8 +41,13 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
   return __builtin_bit_cast(bf16_t, h);
 }
 
+// two floats -> packed bf16 pair by ONE v_cvt_pk_bf16_f32 (the scalar form compiled to two converts
+// plus a shift / or repack)
+typedef float dph_f32x2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 dph_bf16x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pack2bf(float a, float b) {
-  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+  const dph_bf16x2_t h = __builtin_convertvector((dph_f32x2_t){a, b}, dph_bf16x2_t);
+  return __builtin_bit_cast(uint32_t, h);
 }
 
 // 8 consecutive bf16 -> fp32 (16-B vector load when the row is 8-aligned; masked tail otherwise)

@@ -26,6 +26,8 @@
 // or 16-B (fp32) stores and cheap per-column epilogue vectors.
 #include "common.h"
 
+#include <type_traits>
+
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -407,6 +409,9 @@ __device__ __forceinline__ void tile_epi_rows(const DphGemmArgs& a, int64_t z, i
         if constexpr (ACT == DPH_ACT_GELU_BWD) csa[i] += ax[i];
       }
     }
+#ifdef DPH_EPI_NOSTORE
+    if (v[0] != 1.2345e-30f) continue;   // timing diagnostic: no global stores (results kept live)
+#endif
     if (has_pre)
       *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(a.pre_out) + coff) =
           make_uint4(pack2bf(pre[0], pre[1]), pack2bf(pre[2], pre[3]), pack2bf(pre[4], pre[5]), pack2bf(pre[6], pre[7]));
@@ -722,6 +727,9 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(const DphGemmArgs a, int64_
       __builtin_amdgcn_sched_barrier(0);                                                  \
     }                                                                                     \
   } while (0)
+#ifndef DPH_DIRECT_EPI
+#define DPH_DIRECT_EPI 1    // 0: every ring tile takes the LDS-staged epilogue (A/B builds)
+#endif
 #ifndef DPH_ABLATE
 #define DPH_ABLATE 0        // timing ablations of the ring loop (tools/ablate_gemm.py); 0 = production
 #endif
@@ -787,6 +795,9 @@ struct Cfg {
   static constexpr int EPI = EROWS * CROW * 4;
   static constexpr int LDS = PIPE > EPI ? PIPE : EPI;
   static constexpr int MINB = (NW >= 8 && BM * BN > 128 * 128) ? 1 : (BM * BN <= 128 * 64 ? 3 : 2);   // blocks per CU
+  // HIP's second __launch_bounds__ argument is the minimum number of WAVES PER SIMD (not blocks per CU):
+  // MINB blocks of NW waves over the 4 SIMDs (caps the VGPRs at 512 / WPE)
+  static constexpr int WPE = (MINB * NW + 3) / 4;
 };
 using Big = Cfg<256, 256, 128, 64>;
 using Mid = Cfg<128, 128, 64, 64>;
@@ -797,6 +808,10 @@ using Tall = Cfg<256, 64, 128, 32>;
 using Half = Cfg<128, 64, 64, 32>;
 // 128 x 128 tile with 8 waves of 64 x 32 (two waves per SIMD per block): experiment
 using Mid8 = Cfg<128, 128, 64, 32>;
+// 256 x 128 / 128 x 256 tiles, 8 waves of 64 x 64 (16 MFMAs per wave per slice, 512 B of fragment reads
+// per MFMA; half the L2->LDS bytes per flop of the 128 x 128 tile), one block per CU
+using Wide = Cfg<256, 128, 64, 64>;
+using Flat = Cfg<128, 256, 64, 64>;
 
 // s_waitcnt vmcnt(n * DMA): at most n slices' DMAs still in flight
 template <int DMA, int n>
@@ -882,10 +897,236 @@ __device__ __forceinline__ void mfma_slice(f32x4_t (&acc)[C::FM][C::FN], const F
     for (int j = 0; j < C::FN; ++j)
       acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.b[j], f.a[i], acc[i][j], 0, 0, 0);
 }
+
+// ---- direct (register) epilogue -------------------------------------------------------------
+// The MFMA is issued B-first, so lane l holds, of accumulator fragment (i, j), the 4 consecutive
+// columns n = nw + 16 j + 4 (l >> 4) .. +3 of row m = mw + 16 i + (l & 15).  Each lane finishes and
+// stores those values straight from its registers: no LDS staging, no block barrier.  The code is
+// kept lean because the epilogue is instruction-issue bound: one 64-bit base per lane, fragment
+// offsets i * 16 * row_stride + 16 j (the j part folds into the store's immediate offset), 32-bit
+// row-segment arithmetic, column sums over the 16 rows of a lane group by DPP adds (the first
+// version -- 64-bit row_addr / row-length divisions and ds_bpermute shuffles -- compiled to ~2900
+// instructions per wave and measured 11-13k cycles per 128 x 256 tile, as long as half a K = 768
+// main loop).  Every global input (bias / colmask per column group, aux / residual per element) is
+// issued before the first store, so the wait on them never covers a store (gfx9 counts stores in
+// vmcnt).  Preconditions (direct_epi_ok): N % 4 == 0 (a 4-column group is wholly inside or outside N),
+// C rows addressed as m * row_stride (no rows_per_batch), 4-element aligned strides, 16-B aligned
+// pointers, at most one of aux_in / residual, M * N and the row-length segments within 32 bits.
+__host__ __device__ __forceinline__ bool direct_epi_ok(const DphGemmArgs& a) {
+  const int64_t calign = a.C.row_stride | a.C.batch_stride | a.C.z_outer | a.C.z_inner | a.N | a.vec_z_inner;
+  const uintptr_t palign = reinterpret_cast<uintptr_t>(a.C.ptr) | reinterpret_cast<uintptr_t>(a.pre_out) |
+                           reinterpret_cast<uintptr_t>(a.aux_in) | reinterpret_cast<uintptr_t>(a.residual) |
+                           reinterpret_cast<uintptr_t>(a.bias) | reinterpret_cast<uintptr_t>(a.colmask);
+  return (calign & 3) == 0 && (palign & 15) == 0 && !(a.aux_in && a.residual) && a.C.rows_per_batch == 0 &&
+         a.M < ((int64_t)1 << 31) && (!a.row_len || a.len_rows > 0) &&
+         (a.act == DPH_ACT_GELU_BWD || (!a.colsum_out && !a.colsum_aux));   // column sums: GELU_BWD only
+}
+
+__device__ __forceinline__ void unpack_bf16x4(const uint2 r, float (&o)[4]) {
+  o[0] = __uint_as_float(r.x << 16);
+  o[1] = __uint_as_float(r.x & 0xffff0000u);
+  o[2] = __uint_as_float(r.y << 16);
+  o[3] = __uint_as_float(r.y & 0xffff0000u);
+}
+
+// sum over the 16 lanes of a DPP row (lane bits 0..3); every lane of the row gets the sum
+__device__ __forceinline__ float row16_sum(float v) {
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xb1, 0xf, 0xf, false));    // quad_perm 1,0,3,2
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4e, 0xf, 0xf, false));    // quad_perm 2,3,0,1
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x124, 0xf, 0xf, false));   // row_ror 4
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x128, 0xf, 0xf, false));   // row_ror 8
+  return v;
+}
+
+template <class C, int ACT, bool DROP>
+__device__ __forceinline__ void direct_epi_t(const DphGemmArgs& a, int64_t z, int64_t mw, int64_t nw, int lane,
+                                             const f32x4_t (&acc)[C::FM][C::FN]) {
+  constexpr int FM = C::FM, FN = C::FN;
+  const int64_t N = a.N;
+  const int32_t M = (int32_t)a.M;
+  const int64_t rs = a.C.row_stride;
+  const int32_t ml = (int32_t)mw + (lane & 15);
+  const int64_t nl = nw + 4 * (lane >> 4);
+  const bool nfull = nw + C::WTN <= N;          // wave-uniform: every column group in range
+  const bool mfull = mw + C::WTM <= a.M;
+  const int64_t voff = (a.C.z_div > 0 ? (z % a.C.z_div) : z) * a.vec_z_inner;
+  const int64_t base = z_addr(a.C, z) + (int64_t)ml * rs + nl;      // element offset of fragment (0, 0)
+  const int64_t rstep = 16 * rs;
+  // (arithmetic select of the two pointer VALUES, as in tile_epi_rows)
+  const uintptr_t ax_p = reinterpret_cast<uintptr_t>(a.aux_in), rs_p = reinterpret_cast<uintptr_t>(a.residual);
+  const bf16_t* inp = reinterpret_cast<const bf16_t*>(ax_p | (rs_p & (uintptr_t)(-(intptr_t)(ax_p == 0))));
+  const bool has_in = inp != nullptr, has_res = has_in && ax_p == 0;
+  // (column sums are compiled for the GELU_BWD variants only: the only GEMMs that request them)
+  const bool colsum = ACT == DPH_ACT_GELU_BWD && (a.colsum_out || a.colsum_aux);
+  // per-column factors: bias, csm = colmask * layer mask
+  float bias[FN][4], csm[FN][4];
+  const float sm = a.smask ? *a.smask : 1.0f;
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    float4 b = make_float4(0.f, 0.f, 0.f, 0.f), c = make_float4(1.f, 1.f, 1.f, 1.f);
+    if (nfull || nl + 16 * j < N) {
+      if (a.bias) b = *reinterpret_cast<const float4*>(a.bias + voff + nl + 16 * j);
+      if (a.colmask) c = *reinterpret_cast<const float4*>(a.colmask + voff + nl + 16 * j);
+    }
+    bias[j][0] = b.x; bias[j][1] = b.y; bias[j][2] = b.z; bias[j][3] = b.w;
+    csm[j][0] = c.x * sm; csm[j][1] = c.y * sm; csm[j][2] = c.z * sm; csm[j][3] = c.w * sm;
+  }
+  const float inv_keep = DROP ? 1.0f / (1.0f - a.dropout_p) : 1.0f;
+  const uint32_t thr = DROP ? drop_thr(a.dropout_p) : 0u;
+  const uint64_t seed = DROP ? epoch_seed(a.seed) : 0;
+  // per-element inputs of every fragment, issued together
+  uint2 in[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) in[i][j] = make_uint2(0, 0);
+  if (has_in) {
+    const bf16_t* ib = inp + base;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        if ((mfull || ml + 16 * i < M) && (nfull || nl + 16 * j < N))
+          in[i][j] = *reinterpret_cast<const uint2*>(ib + i * rstep + 16 * j);
+  }
+  // rows past their row_len segment store zeros: 32-bit segment / remainder of the first row, stepped by 16
+  uint32_t zrow = 0;                                   // bit i: row i is a zero row
+  if (a.row_len) {
+    const uint32_t L = (uint32_t)a.len_rows;
+    uint32_t seg = (uint32_t)ml / L, rem = (uint32_t)ml - seg * L;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      if (i) {
+        rem += 16;
+        while (rem >= L) rem -= L, ++seg;
+      }
+      if (ml + 16 * i < M && (int64_t)rem >= a.row_len[seg]) zrow |= 1u << i;
+    }
+  }
+  float cso[FN][4], csa[FN][4];
+#pragma unroll
+  for (int j = 0; j < FN; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) cso[j][r] = csa[j][r] = 0.f;
+  const bool out_bf16 = a.c_dtype == DPH_OUT_BF16, accum = a.c_dtype == DPH_OUT_F32_ACCUM;
+  char* cb = reinterpret_cast<char*>(a.C.ptr) + base * (out_bf16 ? 2 : 4);
+  char* pb = reinterpret_cast<char*>(a.pre_out) + base * 2;
+  const int64_t cstep = rstep * (out_bf16 ? 2 : 4), pstep = rstep * 2;
+  const uint64_t e_base = ((uint64_t)(z * a.M + a.drop_row_offset + ml)) * (uint64_t)N + (uint64_t)nl;
+  // CK: bounds and zero-row checks, any output type (edge tiles, row_len, fp32 outputs); interior tiles
+  // with a bf16 output run the check-free copy
+  auto frags = [&](auto ck) {
+    constexpr bool CK = decltype(ck)::value;
+    const bool obf = !CK || out_bf16;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      if (CK && !mfull && ml + 16 * i >= M) continue;
+      const bool zero_row = CK && ((zrow >> i) & 1u);
+      char* crow = cb + i * cstep;
+      char* prow = pb + i * pstep;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        if (CK && !nfull && nl + 16 * j >= N) continue;
+        float v[4], pre[4], ax[4], xin[4];
+        unpack_bf16x4(in[i][j], xin);
+        uint32_t keep = 0xfu;
+        if constexpr (DROP) {
+          // element e_base + 16 i N + 16 j is even (N % 4 == 0, n % 4 == 0): pairs e/2 and e/2 + 1
+          const uint64_t pr = (e_base + (uint64_t)(16 * i) * (uint64_t)N + 16 * j) >> 1;
+          const uint32_t b0 = drop_bits2(seed, pr), b1 = drop_bits2(seed, pr + 1);
+          keep = ((b0 & 0xffffu) >= thr ? 1u : 0u) | ((b0 >> 16) >= thr ? 2u : 0u) |
+                 ((b1 & 0xffffu) >= thr ? 4u : 0u) | ((b1 >> 16) >= thr ? 8u : 0u);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          pre[r] = fmaf(acc[i][j][r], a.alpha, bias[j][r]);
+          const bool k = (keep >> r) & 1u;
+          ax[r] = 0.f;
+          if constexpr (ACT == DPH_ACT_GELU) {
+            v[r] = k ? gelu_f(pre[r]) * (csm[j][r] * inv_keep) : 0.f;
+          } else if constexpr (ACT == DPH_ACT_GELU_BWD) {
+            const float gz = DROP ? (k ? pre[r] * inv_keep : 0.f) : pre[r];
+            float g, dg;
+            gelu_and_grad(xin[r], g, dg);
+            ax[r] = gz * g;
+            v[r] = gz * dg * csm[j][r];
+          } else {
+            v[r] = DROP ? (k ? pre[r] * (csm[j][r] * inv_keep) : 0.f) : pre[r] * csm[j][r];
+          }
+          // residual: xin is zero without one (GELU_BWD's xin is its aux input, never a residual)
+          if constexpr (ACT != DPH_ACT_GELU_BWD) v[r] += xin[r];
+          if (CK) v[r] = zero_row ? 0.f : v[r];
+        }
+        if (colsum) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            cso[j][r] += v[r];
+            if constexpr (ACT == DPH_ACT_GELU_BWD) csa[j][r] += ax[r];   // (not zeroed on zero rows, as epilogue8)
+          }
+        }
+#ifdef DPH_EPI_NOSTORE
+        asm volatile("" ::"v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(pre[0]));
+        continue;
+#endif
+        if (a.pre_out) *reinterpret_cast<uint2*>(prow + 32 * j) = make_uint2(pack2bf(pre[0], pre[1]), pack2bf(pre[2], pre[3]));
+        if (obf) {
+          *reinterpret_cast<uint2*>(crow + 32 * j) = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
+        } else {
+          float4* q = reinterpret_cast<float4*>(crow + 64 * j);
+          if (accum) {
+            const float4 old = *q;
+            v[0] += old.x; v[1] += old.y; v[2] += old.z; v[3] += old.w;
+          }
+          *q = make_float4(v[0], v[1], v[2], v[3]);
+        }
+      }
+    }
+  };
+  if (mfull && nfull && !a.row_len && out_bf16) frags(std::false_type{});
+  else frags(std::true_type{});
+  if (colsum) {
+    // one atomic per column per wave: lanes 0, 16, 32, 48 hold the sums of their 4-column groups
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        cso[j][r] = row16_sum(cso[j][r]);
+        if constexpr (ACT == DPH_ACT_GELU_BWD) csa[j][r] = row16_sum(csa[j][r]);
+      }
+    if ((lane & 15) == 0) {
+      const int64_t csn = a.colsum_n > 0 ? a.colsum_n : N;
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t n = nl + 16 * j + r;
+          if (n >= csn || n >= N) continue;
+          if (a.colsum_out) atomicAdd(a.colsum_out + voff + n, cso[j][r]);
+          if (ACT == DPH_ACT_GELU_BWD && a.colsum_aux) atomicAdd(a.colsum_aux + voff + n, csa[j][r]);
+        }
+    }
+  }
+}
+
+template <class C>
+__device__ __forceinline__ void direct_epi(const DphGemmArgs& a, int64_t z, int64_t mw, int64_t nw, int lane,
+                                           const f32x4_t (&acc)[C::FM][C::FN]) {
+  const bool drop = a.dropout_p > 0.f;
+  if (a.act == DPH_ACT_GELU) {
+    if (drop) direct_epi_t<C, DPH_ACT_GELU, true>(a, z, mw, nw, lane, acc);
+    else direct_epi_t<C, DPH_ACT_GELU, false>(a, z, mw, nw, lane, acc);
+  } else if (a.act == DPH_ACT_GELU_BWD) {
+    if (drop) direct_epi_t<C, DPH_ACT_GELU_BWD, true>(a, z, mw, nw, lane, acc);
+    else direct_epi_t<C, DPH_ACT_GELU_BWD, false>(a, z, mw, nw, lane, acc);
+  } else {
+    if (drop) direct_epi_t<C, DPH_ACT_NONE, true>(a, z, mw, nw, lane, acc);
+    else direct_epi_t<C, DPH_ACT_NONE, false>(a, z, mw, nw, lane, acc);
+  }
+}
 }  // namespace ring
 
 template <class C, bool AK, bool BK>
-__global__ void __launch_bounds__(C::NT, C::MINB) ring_gemm_kernel(const DphGemmArgs a, int64_t kchunk) {
+__global__ void __launch_bounds__(C::NT, C::WPE) ring_gemm_kernel(const DphGemmArgs a, int64_t kchunk) {
   __shared__ __attribute__((aligned(1024))) char smem[C::LDS];
 #ifdef DPH_STAGGER
   // timing experiment: the second block of each CU in the first dispatch round (linear ids 256..511,
@@ -1115,7 +1356,36 @@ __global__ void __launch_bounds__(C::NT, C::MINB) ring_gemm_kernel(const DphGemm
       for (int j = 0; j < C::FN; ++j) asm volatile("" ::"v"(acc[i][j]));
     return;
   }
-  // ---- epilogue, EROWS rows at a time: accumulators -> LDS fp32 -> row-contiguous ----
+  // ---- epilogue: straight from the accumulators when the layout allows ----
+  auto write_stamps = [&]() {
+    __syncthreads();
+    DPH_TSTAMP(st3);
+    if (tid == 0) {
+      unsigned hw, xcc;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+      unsigned long long* o = reinterpret_cast<unsigned long long*>(a.workspace) +
+                              16 * ((int64_t)blockIdx.y * gridDim.x + blockIdx.x);
+      o[0] = st0; o[1] = st1; o[2] = st2; o[3] = st3; o[4] = hw; o[5] = xcc; o[6] = sA; o[7] = sB; o[8] = sC;
+    }
+  };
+  // (not the 256 x 256 tile: its 128 accumulators leave no room for the epilogue inputs; not the 8-wave
+  // 128 x 128 tile: at 4 waves per SIMD its 128-VGPR budget spilled 50 registers)
+  if constexpr (DPH_DIRECT_EPI && C::FM * C::FN <= 16 && C::WPE <= 3) {
+    if (a.splits == 1 && ring::direct_epi_ok(a)) {
+      DPH_TSTAMP(sA);
+      sB = sA;
+#ifdef DPH_EPI_TWICE
+      ring::direct_epi<C>(a, z, m0 + wr * C::WTM, n0 + wc * C::WTN, lane, acc);   // timing: cold, then warm code
+      DPH_TSTAMP(sB);
+#endif
+      ring::direct_epi<C>(a, z, m0 + wr * C::WTM, n0 + wc * C::WTN, lane, acc);
+      DPH_TSTAMP(sC);
+      if (DPH_STAMP) write_stamps();
+      return;
+    }
+  }
+  // ---- staged epilogue, EROWS rows at a time: accumulators -> LDS fp32 -> row-contiguous ----
   constexpr int TPR = C::BN / 8;              // threads per output row (8 columns each)
   constexpr int RPP = C::NT / TPR;            // rows per pass
   float* ct = reinterpret_cast<float*>(smem);
@@ -1202,16 +1472,7 @@ __global__ void __launch_bounds__(C::NT, C::MINB) ring_gemm_kernel(const DphGemm
     }
   }
   if (DPH_STAMP) {
-    __syncthreads();
-    DPH_TSTAMP(st3);
-    if (tid == 0) {
-      unsigned hw, xcc;
-      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-      unsigned long long* o = reinterpret_cast<unsigned long long*>(a.workspace) +
-                              16 * ((int64_t)blockIdx.y * gridDim.x + blockIdx.x);
-      o[0] = st0; o[1] = st1; o[2] = st2; o[3] = st3; o[4] = hw; o[5] = xcc; o[6] = sA; o[7] = sB; o[8] = sC;
-    }
+    write_stamps();
     return;
   }
   if (a.splits == 1 && ((a.colsum_out != nullptr) || (a.colsum_aux != nullptr))) {
@@ -1249,6 +1510,204 @@ __global__ void __launch_bounds__(C::NT, C::MINB) ring_gemm_kernel(const DphGemm
         if (a.colsum_aux && n < csn) atomicAdd(a.colsum_aux + voff + n, sx);
       }
     }
+  }
+}
+
+// =============================================================================================
+// Persistent ring kernel: gridDim.x blocks (the CU slots) walk the tiles t = blockIdx.x + k*gridDim.x;
+// the k-slices of a block's consecutive tiles form ONE stream through the 4-slot ring, so the first
+// slices of tile k+1 are staged while tile k's last slices are multiplied and while its (direct,
+// register-only) epilogue runs: no per-tile pipeline fill (~4-5k cycles measured per 128 x 256 tile)
+// and no per-tile block launch.  The per-step schedule, counted waits and slot reuse are the ring
+// kernel's; the DMA source pointers switch to the next tile when the issue side crosses into it.
+// Both operands k-contiguous, K % 64 == 0 (an even slice count per tile keeps the two fragment
+// register sets in phase across tiles), splits == 1, direct-epilogue layouts.  Epilogue stores count in
+// vmcnt, which only makes the next steps' counted waits stricter (never looser).
+// =============================================================================================
+template <class C, int ACT, bool DROP>
+__global__ void __launch_bounds__(C::NT, C::WPE) ring_persist_kernel(const DphGemmArgs a, int64_t ntm, int64_t ntn) {
+  __shared__ __attribute__((aligned(1024))) char smem[C::PIPE];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wr = wave / C::WGN;
+  const int wc = wave % C::WGN;
+  const int64_t nt = ntm * ntn;
+  const int64_t G = gridDim.x;
+  const int64_t ntiles = (nt * a.batch - blockIdx.x + G - 1) / G;
+  const int H = (int)(a.K / ring::KS);
+  const int64_t S = ntiles * (int64_t)H;
+  // tile k of this block -> (z, m0, n0): the ring kernel's XCD-grouped, GM-swizzled order over the
+  // virtual block id v (gridDim.x % 8 == 0 or a single round, so v % 8 is this block's XCD)
+  // (32-bit arithmetic: tile counts < 2^31, checked on the host; 64-bit divisions cost ~40 instructions
+  // and their registers each)
+  const uint32_t nt32 = (uint32_t)nt, ntm32 = (uint32_t)ntm, ntn32 = (uint32_t)ntn;
+  auto tile_of = [&](int64_t k, int64_t& z, int64_t& m0, int64_t& n0) {
+    const uint32_t v = (uint32_t)blockIdx.x + (uint32_t)k * (uint32_t)G;
+    const uint32_t zz = v / nt32;
+    const uint32_t bid = v - zz * nt32;
+    const uint32_t q = nt32 >> 3, r = nt32 & 7;
+    const uint32_t xcd = bid & 7, loc = bid >> 3;
+    const uint32_t t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+    constexpr uint32_t GM = C::BM > 128 ? 4 : 8;
+    const uint32_t gsz = GM * ntn32;
+    const uint32_t grp = t / gsz;
+    const uint32_t gm0 = grp * GM;
+    const uint32_t gh = min(GM, ntm32 - gm0);
+    const uint32_t l = t - grp * gsz;
+    const uint32_t lq = l / gh;
+    z = zz;
+    m0 = (int64_t)(gm0 + (l - lq * gh)) * C::BM;
+    n0 = (int64_t)lq * C::BN;
+  };
+  // issue side: DMA sources of the tile being staged (4 slices ahead of the one being multiplied; it
+  // switches to tile k+1 when tile k's slice H-4 is multiplied)
+  const bf16_t* pa[C::DMA_A];
+  const bf16_t* pb[C::DMA_B];
+  auto setup = [&](int64_t k) {
+    int64_t z, m0, n0;
+    tile_of(k, z, m0, n0);
+    const bf16_t* Ab = reinterpret_cast<const bf16_t*>(a.A.ptr) + z_addr(a.A, z);
+    const bf16_t* Bb = reinterpret_cast<const bf16_t*>(a.B.ptr) + z_addr(a.B, z);
+#pragma unroll
+    for (int j = 0; j < C::DMA_A; ++j) {
+      const int c = (j * C::NW + wave) * 64 + lane;
+      const int r = c >> 2;
+      pa[j] = Ab + min(m0 + r, a.M - 1) * a.A.row_stride + ((c & 3) ^ ring::swz_chunk(r)) * 8;
+    }
+#pragma unroll
+    for (int j = 0; j < C::DMA_B; ++j) {
+      const int c = (j * C::NW + wave) * 64 + lane;
+      const int r = c >> 2;
+      pb[j] = Bb + min(n0 + r, a.N - 1) * a.B.row_stride + ((c & 3) ^ ring::swz_chunk(r)) * 8;
+    }
+  };
+  setup(0);
+  // DMA j of stream slice g = slice `is` of the tile being staged
+  auto issue_one = [&](int64_t g, int is, int j) {
+    char* la = smem + (g & (ring::NSLOT - 1)) * C::SLOT;
+    const int64_t ko = (int64_t)is * ring::KS;
+    if (j < C::DMA_A) ring::dma16(pa[j] + ko, la + (j * C::NW + wave) * 1024);
+    else ring::dma16(pb[j - C::DMA_A] + ko, la + C::HALF_A + ((j - C::DMA_A) * C::NW + wave) * 1024);
+  };
+  auto slot = [&](int64_t g) -> const char* { return smem + (g & (ring::NSLOT - 1)) * C::SLOT; };
+
+  f32x4_t acc[C::FM][C::FN];
+#pragma unroll
+  for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+    for (int j = 0; j < C::FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  auto step = [&](int64_t g, int is, ring::Frags<C>& cur, ring::Frags<C>& nxt) {
+    if (g + 3 < S) {
+      ring::wait_slices<C::DMA, 2>();
+    } else if (g + 2 < S) {
+      ring::wait_slices<C::DMA, 1>();
+    } else {
+      ring::wait_slices<C::DMA, 0>();
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    const bool restage = g + 4 < S;
+    const bool rd = g + 1 < S;
+    const char* sn = slot(g + 1);
+#pragma unroll
+    for (int q = 0; q < C::FM; ++q) {
+#pragma unroll
+      for (int j = q; j < C::DMA; j += C::FM)
+        if (restage) issue_one(g + 4, is, j);
+      if (rd) {
+        if (q < C::FN) nxt.b[q] = ring::frag(sn + C::HALF_A, wc * C::WTN + 16 * q, lane);
+        nxt.a[q] = ring::frag(sn, wr * C::WTM + 16 * q, lane);
+      }
+#pragma unroll
+      for (int jj = 0; jj < C::FN; ++jj)
+        acc[q][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur.b[jj], cur.a[q], acc[q][jj], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto step_fast = [&](int64_t g, int is, ring::Frags<C>& cur, ring::Frags<C>& nxt) {
+    ring::wait_slices<C::DMA, 2>();
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    const char* sn = slot(g + 1);
+#pragma unroll
+    for (int q = 0; q < C::FM; ++q) {
+#pragma unroll
+      for (int j = q; j < C::DMA; j += C::FM) issue_one(g + 4, is, j);
+      if (q < C::FN) nxt.b[q] = ring::frag(sn + C::HALF_A, wc * C::WTN + 16 * q, lane);
+      nxt.a[q] = ring::frag(sn, wr * C::WTM + 16 * q, lane);
+#pragma unroll
+      for (int jj = 0; jj < C::FN; ++jj)
+        acc[q][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur.b[jj], cur.a[q], acc[q][jj], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  // prologue: stream slices 0..3, wait for slice 0
+#pragma unroll
+  for (int g = 0; g < ring::NSLOT; ++g)
+    if (g < S) {
+#pragma unroll
+      for (int j = 0; j < C::DMA; ++j) issue_one(g, g, j);
+    }
+  if (S >= 4) {
+    ring::wait_slices<C::DMA, 3>();
+  } else if (S == 3) {
+    ring::wait_slices<C::DMA, 2>();
+  } else if (S == 2) {
+    ring::wait_slices<C::DMA, 1>();
+  } else {
+    ring::wait_slices<C::DMA, 0>();
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  ring::Frags<C> f0, f1;
+  ring::read_frags<C, true, true>(f0, slot(0), wr, wc, lane);
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __builtin_amdgcn_sched_barrier(0);
+  int64_t g = 0;
+#pragma unroll 1
+  for (int64_t k = 0; k < ntiles; ++k) {
+    const bool last = k + 1 == ntiles;
+    // every pair restages two slices except the stream's last two pairs (generic steps: the counted
+    // waits drain and nothing is staged past the end; kept out of the pair loop, whose register
+    // allocation they otherwise spoil: 33 spilled VGPRs with them inside, none without)
+    const int ifast = last ? H - 4 : H;
+#pragma unroll 1
+    for (int i = 0; i < ifast; i += 2, g += 2) {
+      // slices i+4, i+5 of this tile, or (from i = H-4 on) slices i+4-H, i+5-H of the next one
+      int is = i + 4;
+      if (is >= H) {
+        is -= H;
+        if (is == 0) setup(k + 1);
+      }
+      step_fast(g, is, f0, f1);
+      step_fast(g + 1, is + 1, f1, f0);
+    }
+    if (last) {
+      step(g, 0, f0, f1);
+      step(g + 1, 0, f1, f0);
+      step(g + 2, 0, f0, f1);
+      step(g + 3, 0, f1, f0);
+      g += 4;
+    }
+    int64_t z, m0, n0;
+    tile_of(k, z, m0, n0);
+    // (one epilogue variant per kernel: the activation / dropout dispatch happens on the host -- all six
+    // inlined into the tile loop spilled ~1000 VGPRs)
+    ring::direct_epi_t<C, ACT, DROP>(a, z, m0 + wr * C::WTM, n0 + wc * C::WTN, lane, acc);
+#pragma unroll
+    for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+      for (int j = 0; j < C::FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   }
 }
 
@@ -1298,7 +1757,7 @@ static int small_nt(int64_t kchunk) {
 static int gemm_path_override() {
   const char* e = getenv("DPH_GEMM_PATH");
   if (!e) return 0;
-  return !strcmp(e, "small") ? 1 : !strcmp(e, "big") ? 2 : !strcmp(e, "mid") ? 3 : !strcmp(e, "tall") ? 4 : !strcmp(e, "half") ? 5 : !strcmp(e, "mid8") ? 6 : !strcmp(e, "mid8mn") ? 7 : 0;
+  return !strcmp(e, "small") ? 1 : !strcmp(e, "big") ? 2 : !strcmp(e, "mid") ? 3 : !strcmp(e, "tall") ? 4 : !strcmp(e, "half") ? 5 : !strcmp(e, "mid8") ? 6 : !strcmp(e, "mid8mn") ? 7 : !strcmp(e, "wide") ? 8 : !strcmp(e, "flat") ? 9 : 0;
 }
 
 // an operand the ring kernels can stage: k-contiguous with whole 32-deep k-slices, or mn-contiguous
@@ -1332,6 +1791,10 @@ static int gemm_kind(const DphGemmArgs& a, int64_t kchunk) {
   // fixed per-tile costs; measured +10 % on the K = 768 projections, even at K = 3072)
   // (also instead of the 256 x 256 tile: conv dgrad 255984x1536x512 ran 389 TF/s on it)
   else if ((kind == 1 || kind == 2) && big_ok && kchunk <= 1024) kind = 5;
+  // the 128 x 256 tile (8 waves of 64 x 64, persistent grid): long K (the 128 x 128 tiles measured 20 %
+  // slower on 7984 x 768 x 3072 / 2304, the 256 x 256 one 10 % on the 1536-deep conv GEMMs) and N <= 1024
+  // (few 128 x 128 tiles per CU: 7984 x 768 x 768 -11 %)
+  if (big_ok && a.N > ring::Tall::BN && (kchunk >= 1536 || (a.N <= 1024 && kchunk >= 4 * ring::KS))) kind = 8;
   const int path = gemm_path_override();
   if (path == 1) kind = 0;
   if (path == 2 && big_ok) kind = 2;
@@ -1340,6 +1803,8 @@ static int gemm_kind(const DphGemmArgs& a, int64_t kchunk) {
   if (path == 5 && big_ok) kind = 4;
   if (path == 6 && big_ok) kind = 5;
   if (path == 7 && ring_ok && !big_ok) kind = 6;     // 8-wave 128x128 tile with mn-contiguous operands
+  if (path == 8 && big_ok) kind = 7;
+  if (path == 9 && big_ok) kind = 8;
   return kind;
 }
 
@@ -1347,11 +1812,17 @@ static int64_t gemm_kchunk(const DphGemmArgs& a) {
   return a.splits > 1 ? cdiv(cdiv(a.K, a.splits), BK) * BK : a.K;
 }
 
+static bool persist_ok(const DphGemmArgs& a);
+
 extern "C" const char* dph_gemm_variant(const DphGemmArgs* args) {
   if (!args) return "";
   const DphGemmArgs& a = *args;
   const int kind = gemm_kind(a, gemm_kchunk(a));
   if (kind == 6) return a.a_kcontig ? "ring::Cfg<128, 128, 64, 32>, true, false>" : "ring::Cfg<128, 128, 64, 32>, false, false>";
+  if (kind == 8) return persist_ok(a) ? "persist_kernel<dph::(anonymous namespace)::ring::Cfg<128, 256, 64, 64>"
+                                      : "ring::Cfg<128, 256, 64, 64>, true, true>";
+  if (kind == 7) return persist_ok(a) ? "persist_kernel<dph::(anonymous namespace)::ring::Cfg<256, 128, 64, 64>"
+                                      : "ring::Cfg<256, 128, 64, 64>, true, true>";
   if (kind == 5) return "ring::Cfg<128, 128, 64, 32>, true, true>";
   if (kind == 4) return "ring::Cfg<128, 64, 64, 32>, true, true>";
   if (kind == 3) return "ring::Cfg<256, 64, 128, 32>, true, true>";
@@ -1379,6 +1850,50 @@ static void launch_ring(const DphGemmArgs& a, int64_t kchunk, hipStream_t stream
   } else {
     hipLaunchKernelGGL((ring_gemm_kernel<Cf, true, true>), g, dim3(Cf::NT), 0, stream, a, kchunk);
   }
+}
+
+// CU count of the current device (persistent grids)
+static int num_cus() {
+  static int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 256;
+    return v > 0 ? v : 256;
+  }();
+  return n;
+}
+
+// DPH_GEMM_PERSIST=0 keeps the one-tile-per-block ring launch (A/B; read per call like DPH_GEMM_PATH)
+static bool persist_enabled() {
+  const char* e = getenv("DPH_GEMM_PERSIST");
+  return !(e && e[0] == '0');
+}
+
+static bool persist_ok(const DphGemmArgs& a) {
+  // (not GELU_BWD: its epilogue in the tile loop spilled ~100 VGPRs)
+  return persist_enabled() && a.act != DPH_ACT_GELU_BWD && a.splits == 1 && a.a_kcontig && a.b_kcontig &&
+         a.K % (2 * ring::KS) == 0 &&
+         a.K >= 4 * ring::KS && ring::direct_epi_ok(a) && a.A.rows_per_batch == 0 && a.B.rows_per_batch == 0 &&
+         cdiv(a.M, 128) * cdiv(a.N, 128) * a.batch < ((int64_t)1 << 30);
+}
+
+template <class Cf>
+static bool launch_ring_persist(const DphGemmArgs& a, hipStream_t stream) {
+  if (!persist_ok(a)) return false;
+  const int64_t ntm = cdiv(a.M, Cf::BM), ntn = cdiv(a.N, Cf::BN);
+  const int64_t total = ntm * ntn * a.batch;
+  const int64_t slots = (int64_t)num_cus() * Cf::MINB;
+  const int64_t grid = total < slots ? total : slots;
+  const dim3 g((unsigned)grid), b(Cf::NT);
+  const bool drop = a.dropout_p > 0.f;
+  if (a.act == DPH_ACT_GELU) {
+    if (drop) hipLaunchKernelGGL((ring_persist_kernel<Cf, DPH_ACT_GELU, true>), g, b, 0, stream, a, ntm, ntn);
+    else hipLaunchKernelGGL((ring_persist_kernel<Cf, DPH_ACT_GELU, false>), g, b, 0, stream, a, ntm, ntn);
+  } else {
+    if (drop) hipLaunchKernelGGL((ring_persist_kernel<Cf, DPH_ACT_NONE, true>), g, b, 0, stream, a, ntm, ntn);
+    else hipLaunchKernelGGL((ring_persist_kernel<Cf, DPH_ACT_NONE, false>), g, b, 0, stream, a, ntm, ntn);
+  }
+  return true;
 }
 
 extern "C" int dph_gemm(const DphGemmArgs* args, hipStream_t stream) {
@@ -1411,7 +1926,13 @@ extern "C" int dph_gemm(const DphGemmArgs* args, hipStream_t stream) {
   // when there are >= ~2 full rounds of tiles over the 256 CUs at one block per CU, else the
   // 128x128 tile (DPH_GEMM_PATH=small|big|mid forces a path, for tests)
   const int kind = gemm_kind(a, kchunk);
-  if (kind == 6) {
+  if (kind == 8) {
+    DPH_REQUIRE(cdiv(a.M, ring::Flat::BM) < 65536 && a.batch * a.splits < 65536, "dph_gemm: grid too large");
+    if (!launch_ring_persist<ring::Flat>(a, stream)) launch_ring<ring::Flat, false>(a, kchunk, stream);
+  } else if (kind == 7) {
+    DPH_REQUIRE(cdiv(a.M, ring::Wide::BM) < 65536 && a.batch * a.splits < 65536, "dph_gemm: grid too large");
+    if (!launch_ring_persist<ring::Wide>(a, stream)) launch_ring<ring::Wide, false>(a, kchunk, stream);
+  } else if (kind == 6) {
     DPH_REQUIRE(cdiv(a.M, ring::Mid8::BM) < 65536 && a.batch * a.splits < 65536, "dph_gemm: grid too large");
     launch_ring<ring::Mid8, true>(a, kchunk, stream);
   } else if (kind == 5) {

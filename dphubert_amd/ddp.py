@@ -106,6 +106,12 @@ class GradReducer:
         self.sync = True
         self._seen = set()
 
+    def force_enable(self):
+        """Run the collectives even at world size 1 (tests / probes of the RCCL path on one GPU)."""
+        self.enabled = True
+        self.payload = [torch.empty(f.numel(), dtype=torch.bfloat16, device=f.device) if
+                        self.comm_dtype == torch.bfloat16 else None for f in self.flat]
+
     def prepare(self, zero: bool = True, sync: bool = True):
         """Point every .grad at its bucket view (zeroed when ``zero``) before a backward.
 

@@ -1405,9 +1405,10 @@ class EncoderLayerFn(torch.autograd.Function):
         B, T, H = cfg["B"], cfg["T"], cfg["H"]
         wl = ctx.wl
         # attention dropout: the forward stores its keep bits (1 bit per probability, ~6 MB per layer at B=16) and
-        # the backward kernels read them instead of re-hashing every probability twice
+        # the backward kernels read them instead of re-hashing every probability twice (grad mode is off inside an
+        # autograd.Function forward, so the caller's need_grad decides)
         keep = None
-        if cfg["p_attn"] > 0 and torch.is_grad_enabled():
+        if cfg["p_attn"] > 0 and cfg.get("need_grad", True):
             keep = torch.empty(_lib.lib().dph_attention_keep_bytes(B, T, H) // 8, dtype=torch.int64, device=qkv.device)
         ctx.attn_keep = keep
         if wl is None:

@@ -9,12 +9,17 @@ pytestmark = pytest.mark.gpu
 torch.manual_seed(0)
 
 
-@pytest.fixture(autouse=True, params=["small", "mid", "big", "wide", "tall", "half", "mid8", "mid8mn"])
+@pytest.fixture(autouse=True, params=["small", "mid", "big", "wide", "flat", "flat-np", "tall", "half", "mid8",
+                                     "mid8mn"])
 def gemm_path(request, monkeypatch):
     """Run every test on each GEMM path: the 128x128 register-staged kernel and the 128x128 /
-    256x256 / 256x64 LDS-DMA ring kernels (taken where their constraints hold: both operands
+    256x256 / 256x128 / 128x256 / 256x64 LDS-DMA ring kernels (taken where their constraints hold: both operands
     k-contiguous, K % 32 == 0)."""
-    monkeypatch.setenv("DPH_GEMM_PATH", request.param)
+    path = request.param
+    if path.endswith("-np"):            # one tile per block instead of the persistent grid
+        monkeypatch.setenv("DPH_GEMM_PERSIST", "0")
+        path = path[:-3]
+    monkeypatch.setenv("DPH_GEMM_PATH", path)
     return request.param
 
 

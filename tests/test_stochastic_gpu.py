@@ -204,6 +204,37 @@ def test_attention_dropout_keep_rate_and_scale():
     assert torch.equal(o_u.float().cpu() != 0, kept)
 
 
+def test_model_step_passes_stored_keep_bits(monkeypatch):
+    """Training step with attention dropout: the forward stores keep bits and the backward reads them (a non-null
+    keep pointer on both calls); no-grad forwards pass none."""
+    import copy
+    from dphubert_amd import ops
+    from dphubert_amd.synthetic import HUBERT_BASE_CONFIG
+    from dphubert_amd.trainer import seeded_model
+    cfg = copy.deepcopy(HUBERT_BASE_CONFIG)
+    cfg.update(encoder_num_layers=1, encoder_attention_dropout=0.1)
+    m = seeded_model(cfg, 0).to(DEV).train()
+    seen = []
+    real = ops.call
+
+    def spy(name, *args):
+        if name in ("dph_attention_fwd", "dph_attention_bwd"):
+            seen.append((name, args[-2]))
+        return real(name, *args)
+    monkeypatch.setattr(ops, "call", spy)
+    wave = torch.randn(2, 16000, device=DEV) * 0.1
+    x, _ = m(wave)
+    x.float().pow(2).mean().backward()
+    torch.cuda.synchronize()
+    assert [n for n, _ in seen] == ["dph_attention_fwd", "dph_attention_bwd"], seen
+    assert all(k not in (None, 0) for _, k in seen), seen
+    assert seen[0][1] == seen[1][1]
+    seen.clear()
+    with torch.no_grad():
+        m(wave)
+    assert [k for _, k in seen] == [None] or [k for _, k in seen] == [0], seen
+
+
 def test_layernorm_branch_dropout_keep_rate_and_scale():
     from dphubert_amd import _lib
     from dphubert_amd._lib import call, ptr

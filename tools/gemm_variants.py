@@ -12,7 +12,8 @@ from dphubert_amd import kernels as K  # noqa: E402
 M = 16 * 499
 SHAPES = [("qkv fwd", M, 2304, 768), ("ffn1 fwd+gelu", M, 3072, 768), ("ffn2 fwd", M, 768, 3072),
           ("oproj fwd", M, 768, 768), ("ffn2 dgrad(T)", M, 3072, 768), ("ffn1 dgrad(T)", M, 768, 3072),
-          ("qkv dgrad(T)", M, 768, 2304), ("conv2 fwd", 16 * 7999, 512, 1536)]
+          ("qkv dgrad(T)", M, 768, 2304), ("conv2 fwd", 16 * 7999, 512, 1536), ("conv1 fwd", 16 * 15999, 512, 1536),
+          ("conv1 dgrad", 16 * 15999, 1536, 512)]
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 5
 paths = sys.argv[2:] or ["auto", "mid", "mid8"]
 res = {}
@@ -28,6 +29,10 @@ for name, m, n, k in SHAPES:
 
 def run(name, path, iters=20):
     A, B, C, bias, pre, m, n, k = data[name]
+    os.environ.pop("DPH_GEMM_PERSIST", None)
+    if path.endswith("-np"):                 # one tile per block (no persistent grid)
+        os.environ["DPH_GEMM_PERSIST"] = "0"
+        path = path[:-3]
     if path == "auto":
         os.environ.pop("DPH_GEMM_PATH", None)
     else:
@@ -51,6 +56,7 @@ for r in range(rounds):
         for p in paths:
             res.setdefault((name, p), []).append(run(name, p))
 os.environ.pop("DPH_GEMM_PATH", None)
+os.environ.pop("DPH_GEMM_PERSIST", None)
 for name, m, n, k in SHAPES:
     row = []
     for p in paths:

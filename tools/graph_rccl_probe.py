@@ -2,9 +2,11 @@
 
 Single process, world_size 1 over RCCL ("nccl" backend), GradReducer forced on so every bucket
 goes through a real RCCL all-reduce (AVG) launched from the backward hooks during capture.
-Compares 4 replayed steps with 4 eager steps of an identical module.
-Run on the GPU box:  python tools/graph_rccl_probe.py
+Compares 4 replayed optimizer steps with 4 eager steps of an identical module.
+Run on the GPU box:  python tools/graph_rccl_probe.py [--comm fp32|bf16] [--accum N] [--port P]
+(tests/test_graph_gpu.py::test_graph_replay_with_rccl_allreduce runs it as a subprocess)
 """
+import argparse
 import os
 import sys
 
@@ -16,34 +18,60 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 
 
 def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--comm", default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--accum", type=int, default=1)
+    ap.add_argument("--port", default="29533")
+    args = ap.parse_args()
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    os.environ.setdefault("MASTER_PORT", "29533")
+    os.environ["MASTER_PORT"] = args.port
     torch.cuda.set_device(0)
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
     from test_graph_gpu import _batch, _module
     from dphubert_amd.trainer import Trainer
     batch = _batch()
-    ea = Trainer(_module(), clip_norm=10.0)
-    gr = Trainer(_module(), clip_norm=10.0, graphs=True, graph_warmup=1)
-    for t in (ea, gr):
-        t.reducer.enabled = True
-    le, lg = [], []
-    for _ in range(4):
-        le.append(ea.step(batch).item())
+    gd = torch.bfloat16 if args.comm == "bf16" else torch.float32
+    eager = [Trainer(_module(), clip_norm=10.0, accum_grad=args.accum, grad_dtype=gd) for _ in range(3)]
+    gr = Trainer(_module(), clip_norm=10.0, graphs=True, graph_warmup=1, accum_grad=args.accum, grad_dtype=gd)
+    for t in eager + [gr]:
+        t.reducer.force_enable()
+    le = [[] for _ in eager]
+    lg = []
+    for _ in range(4 * args.accum):
+        for t, l in zip(eager, le):
+            l.append(t.step(batch).item())
         lg.append(gr.step(batch).item())
     torch.cuda.synchronize()
-    print("graph captured:", gr._graph is not None)
-    print("eager losses ", le)
-    print("graph losses ", lg)
-    pa = dict(ea.module.named_parameters())
-    worst = 0.0
-    for n, p in gr.module.named_parameters():
-        if p.requires_grad and not n.endswith("k_proj.bias"):   # zero-gradient param (see tests)
-            d = ((p.detach() - pa[n].detach()).norm() / pa[n].detach().norm().clamp_min(1e-30)).item()
-            worst = max(worst, d)
-    print("worst param rel diff", worst)
+    print("graph captured:", gr._graph is not None, "variants:", sorted(gr._graphs))
+    print("reducer buckets:", len(gr.reducer.buckets), "comm dtype:", gr.reducer.comm_dtype)
+    print("eager losses  ", le)
+    print("graph losses  ", lg)
+    # the criteria of tests/test_graph_gpu.py::test_graph_replay_matches_eager: replay vs eager within 4x the
+    # largest eager-vs-eager drift of three eager runs (fp32 atomic order, amplified by Adam) plus a floor
+    ok = gr._graph is not None
+    for s_, b in enumerate(lg):
+        vals = [l[s_] for l in le]
+        ok &= abs(vals[0] - b) <= 1e-3 * max(1.0, abs(b)) + 4 * (max(vals) - min(vals))
+    pe = [dict(t.module.named_parameters()) for t in eager]
+    pg = dict(gr.module.named_parameters())
+    names = [n for n, p in gr.module.named_parameters() if p.requires_grad and not n.endswith("k_proj.bias")]
+    rel = lambda x, y: ((x.detach().float() - y.detach().float()).norm() /  # noqa: E731
+                        y.detach().float().norm().clamp_min(1e-30)).item()
+    pairs = [(0, 1), (0, 2), (1, 2)]
+    worst = []
+    for n in names:
+        e = rel(pg[n], pe[0][n])
+        base = max(rel(pe[i][n], pe[j][n]) for i, j in pairs)
+        floor = 1e-2 if pg[n].dim() == 1 else 5e-3
+        if not e < max(floor, 4 * base):
+            ok = False
+            worst.append((n, e, base))
+    cat = lambda d: torch.cat([d[n].detach().float().flatten() for n in names])  # noqa: E731
+    e_all = rel(cat(pg), cat(pe[0]))
+    base_all = max(rel(cat(pe[i]), cat(pe[j])) for i, j in pairs)
+    ok &= e_all < max(1e-5, 4 * base_all)
+    print("whole-vector rel diff", e_all, "eager-vs-eager", base_all, "violations", worst)
     dist.destroy_process_group()
-    ok = gr._graph is not None and worst < 1e-3 and all(abs(a - b) < 1e-4 for a, b in zip(le, lg))
     print("RCCL_GRAPH_OK" if ok else "RCCL_GRAPH_FAIL")
 
 

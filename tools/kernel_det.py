@@ -74,3 +74,13 @@ for (B, T, H) in [(2, 99, 12), (4, 499, 12), (2, 1999, 12)]:
         return y, mu, rs
 
     check(f"layernorm_fwd M{M}", ln)
+
+# ring GEMM shapes of the Large family (persistent 128 x 256 tiles), with and without row-length zeroing
+for (M, N, Kd) in [(998, 1024, 1024), (998, 1024, 4096), (998, 4096, 1024), (7984, 768, 3072), (7984, 3072, 768)]:
+    x = (torch.randn(M, Kd, device=DEV) * 0.5).to(torch.bfloat16)
+    w = (torch.randn(N, Kd, device=DEV) * 0.05).to(torch.bfloat16)
+    b = torch.randn(N, device=DEV)
+    r = torch.randn(M, N, device=DEV).to(torch.bfloat16)
+    rl = torch.tensor([M // 2 - 7, M // 2], device=DEV, dtype=torch.int64)
+    check(f"gemm {M}x{N}x{Kd} resid", lambda: (K.linear_fwd(x, w, b, residual=r),))
+    check(f"gemm {M}x{N}x{Kd} gelu rowlen", lambda: (K.linear_fwd(x, w, b, act=K.ACT_GELU, row_len=rl, len_rows=M // 2),))

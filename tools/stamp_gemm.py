@@ -42,8 +42,9 @@ else:
     for _ in range(5):
         _lib.call("dph_gemm", C.byref(args), _lib.stream_ptr())
     torch.cuda.synchronize()
-    tiles = ((M + 127) // 128) * ((N + 127) // 128) if os.environ.get("DPH_GEMM_PATH") != "big" else \
-        ((M + 255) // 256) * ((N + 255) // 256)
+    bm, bn = {"big": (256, 256), "wide": (256, 128), "flat": (128, 256), "tall": (256, 64),
+              "half": (128, 64)}.get(os.environ.get("DPH_GEMM_PATH", ""), (128, 128))
+    tiles = ((M + bm - 1) // bm) * ((N + bn - 1) // bn)
     d = ws[: 16 * tiles].view(tiles, 16).cpu().numpy().astype(np.int64)
     t0 = d[:, 0].min()
     st = d[:, :4] - t0
