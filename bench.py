@@ -135,6 +135,28 @@ def pmc_traffic(args):
     return out
 
 
+def bucketed_batches(n: int, seconds_per_batch: float, rank: int, dev):
+    """n batches shaped like distill.py's train loader (data.train_loader): 4000 synthetic utterance lengths
+    uniform in 2-15.6 s (the loader's min_len / max_len), 1000 length buckets, a seconds_per_batch token
+    budget, crop-to-shortest collate; n batches taken evenly over the length range (seeded)."""
+    from dphubert_amd.data import BucketizeBatchSampler
+    g = torch.Generator().manual_seed(2022)
+    lens = torch.randint(32000, 250001, (4000,), generator=g).tolist()
+    bs = BucketizeBatchSampler(lens, num_buckets=1000, max_token_count=int(seconds_per_batch * 16000),
+                               min_len=32000, max_len=250000, shuffle=False)
+    packs = list(bs)
+    pick = [packs[int(i * (len(packs) - 1) / max(n - 1, 1))] for i in range(n)]
+    perm = torch.randperm(n, generator=g).tolist()            # lengths in no particular order over the steps
+    out = []
+    gw = torch.Generator().manual_seed(2022 + rank)
+    for k in perm:
+        idx = pick[k]
+        L = min(lens[i] for i in idx)
+        w = 0.1 * torch.randn(len(idx), L, generator=gw)
+        out.append((w.to(dev), torch.full((len(idx),), L, dtype=torch.int64).to(dev)))
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -153,7 +175,13 @@ def main():
     ap.add_argument("--accum", type=int, default=1, help="micro-batches per optimizer step (a step = one micro-batch)")
     ap.add_argument("--graphs", choices=["on", "off"], default="on",
                     help="on: replay the whole step as one captured HIP graph after the eager warm-up steps")
+    ap.add_argument("--lengths", choices=["fixed", "bucketed"], default="fixed",
+                    help="fixed: B x --seconds utterances (the headline); bucketed: the reference's train loader "
+                         "shapes -- 2-15.6 s utterance lengths, 1000 length buckets, a 160 s token budget per "
+                         "batch, crop-to-shortest collate (lightning.py:306-325) -- one new shape per step, eager")
     args = ap.parse_args()
+    if args.lengths == "bucketed":
+        args.graphs = "off"
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -190,6 +218,9 @@ def main():
     samples = int(args.seconds * 16000)
     wave, lengths = synthetic_batch(args.batch, samples, seed=2022 + rank)
     batch = (wave.to(dev), lengths.to(dev))
+    batches = None
+    if args.lengths == "bucketed":
+        batches = bucketed_batches(args.warmup + args.steps, args.batch * args.seconds, rank, dev)
 
     # warm-up: 2 eager steps, then (graphs) the capture + first replay
     if args.accum < 1 or args.steps < args.accum:
@@ -197,14 +228,16 @@ def main():
     # warm-up in whole optimizer steps (the trainer captures its graphs after 2 eager optimizer steps)
     n_warm = max(args.warmup, 3 if graphs else 1) * args.accum
     for i in range(n_warm):
-        loss = trainer.step(batch)
+        loss = trainer.step(batch if batches is None else batches[i % len(batches)])
     torch.cuda.synchronize()
     graphed = trainer._graph is not None
     log(f"step mode: {'HIP graph replay' if graphed else 'eager'}")
     # GEMM launches of the LAST timed step are bracketed by HIP events on their launch stream (an
     # event marker costs ~3 us of GPU time, so bracketing every step would tax the headline number).
     # With graphs, that step replays a second capture of the same step whose GEMMs carry event nodes.
-    prof = LaunchProfiler() if (rank == 0 and not args.no_roofline) else None
+    # DPH_BENCH_SHAPES=1: key the profiled step's GEMM table by shape / epilogue too (diagnostics, stderr)
+    by_shape = os.environ.get("DPH_BENCH_SHAPES") == "1"
+    prof = LaunchProfiler(by_shape=by_shape) if (rank == 0 and not args.no_roofline) else None
     prof_mode = "timed step" if prof is not None else None
     if prof is not None and graphed:
         try:
@@ -220,11 +253,14 @@ def main():
     t0 = time.perf_counter()
     in_loop = prof is not None and prof_mode != "eager step right after the timed region (same kernels)"
     last_final = (args.steps // args.accum) * args.accum - 1    # the last micro-step that ends an optimizer step
+    audio_timed = 0.0
     for i in range(args.steps):
         last = in_loop and i == last_final
         if last and not graphed:
             prof.__enter__()
-        loss = trainer.step(batch, profiled=last)
+        b = batch if batches is None else batches[args.warmup + i]
+        audio_timed += b[0].shape[0] * b[0].shape[1] / 16000.0
+        loss = trainer.step(b, profiled=last)
     t_host = time.perf_counter() - t0          # host enqueue time (GPU may still be running)
     torch.cuda.synchronize()
     if world > 1:
@@ -236,15 +272,16 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = t.item()
     ms = dt / args.steps * 1e3
-    audio_s = world * args.batch * args.seconds * args.steps
+    audio_s = world * audio_timed            # (every rank processes the same amount: shapes per rank differ)
     value = audio_s / dt
     log(f"host enqueue {t_host / args.steps * 1e3:.2f} ms/step")
     log(f"loss {loss.item():.5f}  step {ms:.2f} ms  {value:.1f} audio-s/s  "
         f"({FLOP_PER_UTT_BASE * args.batch * args.seconds / 10 / (ms / 1e3) / 1e12:.0f} TFLOP/s algorithmic/GPU)")
 
     fam = "WavLM-Base" if args.model == "wavlm-base" else "HuBERT-Base"
+    utts = "10s utts" if batches is None else "bucketed 2-15.6s utts, 160 s/batch"
     out = {
-        "metric": f"audio-seconds/sec/node ({fam} distill step, 10s utts)",
+        "metric": f"audio-seconds/sec/node ({fam} distill step, {utts})",
         "value": round(value, 2),
         "unit": "audio-seconds/sec",
         "n_gpus": world,
@@ -260,7 +297,8 @@ def main():
                                "conv,head,interm, dropout) + L1/cos distill loss + sparsity Lagrangian + AdamW",
                    "utterances_per_gpu": args.batch, "seconds_per_utt": args.seconds,
                    "global_batch_audio_s": world * args.batch * args.seconds, "distill_layers": "0.4,8,12",
-                   "parallelism": f"dp{world}", "accum_grad": args.accum, "grad_comm": args.grad_comm},
+                   "parallelism": f"dp{world}", "accum_grad": args.accum, "grad_comm": args.grad_comm,
+                   "lengths": args.lengths},
         "peak_hbm_gib": round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 2),
         "step_mode": "hip_graph" if graphed else "eager",
     }
@@ -275,6 +313,16 @@ def main():
     if prof is not None:
         prof.__exit__(None, None, None)
         summ = prof.summary()
+        if by_shape:
+            for k, v in sorted(summ.items(), key=lambda kv: -kv[1]["ms"]):
+                log(f"{v['ms']:7.3f} ms {v['launches']:4d}x {v['ms'] / v['launches'] * 1e3:7.1f} us "
+                    f"{v['flops'] / v['ms'] / 1e9:6.0f} TF/s  {k}")
+            agg = {}
+            for k, v in summ.items():
+                d = agg.setdefault(k.split(" M=")[0], {"launches": 0, "ms": 0.0, "flops": 0.0})
+                for f in d:
+                    d[f] += v[f]
+            summ = agg
         top = max(summ.items(), key=lambda kv: kv[1]["ms"])
         name, d = top
         avg_ms = d["ms"] / d["launches"]
@@ -296,7 +344,12 @@ def main():
         if traffic_err:
             out["roofline"]["traffic_error"] = traffic_err
         log(json.dumps({k: v for k, v in summ.items()}))
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if batches is not None:
+        shapes = [tuple(b[0].shape) for b in batches[args.warmup:]]
+        out["config"]["batch_shapes"] = [f"{bb}x{ss / 16000:.2f}s" for bb, ss in shapes]
+        out["data"] = ("synthetic (0.1*randn waveforms; lengths uniform 2-15.6 s, bucketed and cropped like the "
+                       "reference's train loader)")
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and batches is None:
         try:
             out["cpu_baseline"] = cpu_baseline()
         except Exception as e:  # noqa: BLE001 -- baseline is informational

@@ -34,7 +34,7 @@ class DphGemmArgs(C.Structure):
                 ("alpha", f32), ("dropout_p", f32), ("seed", u64), ("bias", vp), ("colmask", vp), ("smask", vp),
                 ("vec_z_inner", i64), ("pre_out", vp), ("aux_in", vp), ("residual", vp), ("colsum_out", vp),
                 ("colsum_aux", vp), ("row_len", vp), ("len_rows", i64), ("drop_row_offset", i64),
-                ("workspace", vp), ("workspace_bytes", i64), ("colsum_n", i64)]
+                ("workspace", vp), ("workspace_bytes", i64), ("colsum_n", i64), ("flags", i64)]
 
 
 class DphTensorSlot(C.Structure):
@@ -95,6 +95,7 @@ _SIGS = {
     "dph_cast_bf16": ([vp, vp, i64, S], C.c_int),
     "dph_transpose_bf16": ([vp, i64, i64, vp, S], C.c_int),
     "dph_cast_bf16_multi": ([vp, i64, S], C.c_int),
+    "dph_copy_f32_multi": ([vp, i64, i64, S], C.c_int),
     "dph_conv_lengths": ([vp, vp, i64, i64, vp, vp, S], C.c_int),
     "dph_conv0_bwd": ([vp, i64, i64, i64, i64, i64, vp, vp, vp, S], C.c_int),
     "dph_gelu_mask_fwd": ([vp, vp, vp, i64, i64, S], C.c_int),
@@ -107,6 +108,8 @@ _SIGS = {
     "dph_branch_bwd": ([vp, vp, i64, i64, f32, u64, vp, vp, i64, vp, vp, vp, S], C.c_int),
     "dph_distill_loss_fwd": ([vp, vp, i64, i64, i64, i64, f32, f32, f32, C.c_int, vp, vp, vp, S], C.c_int),
     "dph_distill_loss_bwd": ([vp, vp, vp, vp, i64, i64, i64, i64, f32, f32, f32, C.c_int, vp, S], C.c_int),
+    "dph_reg_loss_fwd": ([vp, vp, vp, vp, vp, f32, f32, vp, S], C.c_int),
+    "dph_reg_loss_bwd": ([vp, vp, vp, vp, vp, vp, vp, f32, f32, vp, vp, vp, S], C.c_int),
     "dph_hc_sample_fwd": ([vp, vp, vp, vp, i64, u64, f32, f32, f32, f32, S], C.c_int),
     "dph_hc_sample_bwd": ([vp, vp, vp, vp, i64, f32, f32, f32, S], C.c_int),
     "dph_hc_bank_fwd": ([vp, i64, vp, vp, u64, f32, f32, f32, f32, S], C.c_int),
@@ -126,7 +129,7 @@ _SIGS = {
 _lib = None
 # include/dphubert_hip.h layout (3: dph_adamw_step_dev, dph_set_rng_epoch; 4: dph_event_*; 5: LN bwd / colsum
 # workspaces; 12: dph_hc_bank_fwd / dph_hc_bank_bwd)
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 
 class DphError(RuntimeError):

@@ -7,6 +7,8 @@
 //   fp32 master weight -> bf16 GEMM images.
 #include "common.h"
 
+#include <algorithm>
+
 namespace dph {
 namespace {
 
@@ -326,6 +328,22 @@ __global__ void __launch_bounds__(256) cast_bf16_multi_kernel(const int64_t* __r
   }
 }
 
+//   copy:      tab[e] = {src fp32* (0: write zeros), dst fp32*, n}; grid (blocks, entries)
+__global__ void __launch_bounds__(256) copy_f32_multi_kernel(const int64_t* __restrict__ tab) {
+  const int64_t* e = tab + 3 * blockIdx.y;
+  const float* src = reinterpret_cast<const float*>(e[0]);
+  float* dst = reinterpret_cast<float*>(e[1]);
+  const int64_t n = e[2];
+  const bool vec = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0;
+  for (int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4; i < n; i += (int64_t)gridDim.x * 1024) {
+    if (vec && i + 4 <= n) {
+      *reinterpret_cast<float4*>(dst + i) = src ? *reinterpret_cast<const float4*>(src + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+    } else {
+      for (int64_t j = i; j < n && j < i + 4; ++j) dst[j] = src ? src[j] : 0.f;
+    }
+  }
+}
+
 __global__ void __launch_bounds__(256) transpose_bf16_multi_kernel(const int64_t* __restrict__ tab) {
   __shared__ uint16_t t[64][72];
   const int64_t* e = tab + 4 * blockIdx.y;
@@ -369,6 +387,14 @@ extern "C" int dph_cast_bf16_multi(const int64_t* table, int64_t n_entries, hipS
   DPH_REQUIRE(table && n_entries > 0 && n_entries < 65536, "dph_cast_bf16_multi: bad args");
   hipLaunchKernelGGL(dph::cast_bf16_multi_kernel, dim3(64, (unsigned)n_entries), dim3(256), 0, stream, table);
   return check_launch("dph_cast_bf16_multi");
+}
+
+extern "C" int dph_copy_f32_multi(const int64_t* table, int64_t n_entries, int64_t max_n, hipStream_t stream) {
+  DPH_REQUIRE(table && n_entries > 0 && n_entries < 65536 && max_n > 0, "dph_copy_f32_multi: bad args");
+  const int64_t blocks = std::min<int64_t>(std::max<int64_t>(cdiv(max_n, 1024), 1), 2048);
+  hipLaunchKernelGGL(dph::copy_f32_multi_kernel, dim3((unsigned)blocks, (unsigned)n_entries), dim3(256), 0, stream,
+                     table);
+  return check_launch("dph_copy_f32_multi");
 }
 
 extern "C" int dph_transpose_bf16_multi(const int64_t* table, int64_t n_entries, hipStream_t stream) {

@@ -56,6 +56,15 @@ __device__ __forceinline__ int64_t row_addr(const DphMat& d, int64_t r) {
   return r * d.row_stride;
 }
 
+// row_addr for row indices < 2^31 (32-bit division: the 64-bit one is a ~40-instruction routine)
+__device__ __forceinline__ int64_t row_addr32(const DphMat& d, uint32_t r) {
+  if (d.rows_per_batch > 0) {
+    const uint32_t q = r / (uint32_t)d.rows_per_batch;
+    return (int64_t)q * d.batch_stride + (int64_t)(r - q * (uint32_t)d.rows_per_batch) * d.row_stride;
+  }
+  return (int64_t)r * d.row_stride;
+}
+
 __device__ __forceinline__ int64_t z_addr(const DphMat& d, int64_t z) {
   if (d.z_div > 0) return (z / d.z_div) * d.z_outer + (z % d.z_div) * d.z_inner;
   return z * d.z_inner;
@@ -938,8 +947,11 @@ __device__ __forceinline__ float row16_sum(float v) {
   return v;
 }
 
+// Returns true when the check-free copy ran: then the wave issued exactly FM*FN stores of C (plus FM*FN of
+// pre_out when requested) and no other memory operation is left outstanding (the persistent kernel's
+// counted waits rely on it).
 template <class C, int ACT, bool DROP>
-__device__ __forceinline__ void direct_epi_t(const DphGemmArgs& a, int64_t z, int64_t mw, int64_t nw, int lane,
+__device__ __forceinline__ bool direct_epi_t(const DphGemmArgs& a, int64_t z, int64_t mw, int64_t nw, int lane,
                                              const f32x4_t (&acc)[C::FM][C::FN]) {
   constexpr int FM = C::FM, FN = C::FN;
   const int64_t N = a.N;
@@ -975,20 +987,18 @@ __device__ __forceinline__ void direct_epi_t(const DphGemmArgs& a, int64_t z, in
   const uint32_t thr = DROP ? drop_thr(a.dropout_p) : 0u;
   const uint64_t seed = DROP ? epoch_seed(a.seed) : 0;
   // per-element inputs of every fragment, issued together
+  // (loaded two rows ahead inside the fragment loop: at most two rows of inputs are live, 16 VGPRs
+  // instead of 32 -- the persistent kernel's GELU_BWD variant spilled with all of them preloaded)
   uint2 in[FM][FN];
+  const bf16_t* ib = inp + base;
+  auto load_in = [&](int i) {
 #pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) in[i][j] = make_uint2(0, 0);
-  if (has_in) {
-    const bf16_t* ib = inp + base;
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j)
-        if ((mfull || ml + 16 * i < M) && (nfull || nl + 16 * j < N))
-          in[i][j] = *reinterpret_cast<const uint2*>(ib + i * rstep + 16 * j);
-  }
+    for (int j = 0; j < FN; ++j) {
+      in[i][j] = make_uint2(0, 0);
+      if (has_in && (mfull || ml + 16 * i < M) && (nfull || nl + 16 * j < N))
+        in[i][j] = *reinterpret_cast<const uint2*>(ib + i * rstep + 16 * j);
+    }
+  };
   // rows past their row_len segment store zeros: 32-bit segment / remainder of the first row, stepped by 16
   uint32_t zrow = 0;                                   // bit i: row i is a zero row
   if (a.row_len) {
@@ -1020,6 +1030,11 @@ __device__ __forceinline__ void direct_epi_t(const DphGemmArgs& a, int64_t z, in
     const bool obf = !CK || out_bf16;
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
+      if (i == 0) {
+        load_in(0);
+        if (FM > 1) load_in(1);
+      }
+      if (i + 2 < FM) load_in(i + 2);
       if (CK && !mfull && ml + 16 * i >= M) continue;
       const bool zero_row = CK && ((zrow >> i) & 1u);
       char* crow = cb + i * cstep;
@@ -1082,7 +1097,8 @@ __device__ __forceinline__ void direct_epi_t(const DphGemmArgs& a, int64_t z, in
       }
     }
   };
-  if (mfull && nfull && !a.row_len && out_bf16) frags(std::false_type{});
+  const bool lean = mfull && nfull && !a.row_len && out_bf16;
+  if (lean) frags(std::false_type{});
   else frags(std::true_type{});
   if (colsum) {
     // one atomic per column per wave: lanes 0, 16, 32, 48 hold the sums of their 4-column groups
@@ -1106,6 +1122,7 @@ __device__ __forceinline__ void direct_epi_t(const DphGemmArgs& a, int64_t z, in
         }
     }
   }
+  return lean && !colsum;
 }
 
 template <class C>
@@ -1573,13 +1590,13 @@ __global__ void __launch_bounds__(C::NT, C::WPE) ring_persist_kernel(const DphGe
     for (int j = 0; j < C::DMA_A; ++j) {
       const int c = (j * C::NW + wave) * 64 + lane;
       const int r = c >> 2;
-      pa[j] = Ab + min(m0 + r, a.M - 1) * a.A.row_stride + ((c & 3) ^ ring::swz_chunk(r)) * 8;
+      pa[j] = Ab + row_addr32(a.A, (uint32_t)min(m0 + r, a.M - 1)) + ((c & 3) ^ ring::swz_chunk(r)) * 8;
     }
 #pragma unroll
     for (int j = 0; j < C::DMA_B; ++j) {
       const int c = (j * C::NW + wave) * 64 + lane;
       const int r = c >> 2;
-      pb[j] = Bb + min(n0 + r, a.N - 1) * a.B.row_stride + ((c & 3) ^ ring::swz_chunk(r)) * 8;
+      pb[j] = Bb + row_addr32(a.B, (uint32_t)min(n0 + r, a.N - 1)) + ((c & 3) ^ ring::swz_chunk(r)) * 8;
     }
   };
   setup(0);
@@ -1629,8 +1646,17 @@ __global__ void __launch_bounds__(C::NT, C::WPE) ring_persist_kernel(const DphGe
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_sched_barrier(0);
   };
-  auto step_fast = [&](int64_t g, int is, ring::Frags<C>& cur, ring::Frags<C>& nxt) {
-    ring::wait_slices<C::DMA, 2>();
+  // After a lean epilogue the wave has FM*FN (or 2*FM*FN) stores outstanding, issued after the DMAs of the
+  // next tile's slices 0..2 and before those of slice 3 on: the first three steps of the tile then wait
+  // for vmcnt(2*DMA + FM*FN) instead of vmcnt(2*DMA), so the stores drain under those steps' MFMAs
+  // instead of being waited for by the first one (vmcnt retires in order: this still waits for the DMA
+  // the step needs, and at most for the older half of the stores when pre_out doubles them).
+  constexpr int VM_EXTRA = 2 * C::DMA + C::FM * C::FN;
+  static_assert(VM_EXTRA < 64, "vmcnt immediate");
+  constexpr int WAIT_EXTRA = (VM_EXTRA & 15) | ((VM_EXTRA >> 4) << 14) | 0x70 | 0xF00;
+  auto step_fast = [&](int64_t g, int is, ring::Frags<C>& cur, ring::Frags<C>& nxt, bool extra) {
+    if (extra) __builtin_amdgcn_s_waitcnt(WAIT_EXTRA);
+    else ring::wait_slices<C::DMA, 2>();
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
@@ -1674,6 +1700,7 @@ __global__ void __launch_bounds__(C::NT, C::WPE) ring_persist_kernel(const DphGe
   __builtin_amdgcn_s_waitcnt(0xC07F);
   __builtin_amdgcn_sched_barrier(0);
   int64_t g = 0;
+  bool after_lean = false;
 #pragma unroll 1
   for (int64_t k = 0; k < ntiles; ++k) {
     const bool last = k + 1 == ntiles;
@@ -1689,8 +1716,8 @@ __global__ void __launch_bounds__(C::NT, C::WPE) ring_persist_kernel(const DphGe
         is -= H;
         if (is == 0) setup(k + 1);
       }
-      step_fast(g, is, f0, f1);
-      step_fast(g + 1, is + 1, f1, f0);
+      step_fast(g, is, f0, f1, after_lean && i < 3);
+      step_fast(g + 1, is + 1, f1, f0, after_lean && i + 1 < 3);
     }
     if (last) {
       step(g, 0, f0, f1);
@@ -1703,7 +1730,7 @@ __global__ void __launch_bounds__(C::NT, C::WPE) ring_persist_kernel(const DphGe
     tile_of(k, z, m0, n0);
     // (one epilogue variant per kernel: the activation / dropout dispatch happens on the host -- all six
     // inlined into the tile loop spilled ~1000 VGPRs)
-    ring::direct_epi_t<C, ACT, DROP>(a, z, m0 + wr * C::WTM, n0 + wc * C::WTN, lane, acc);
+    after_lean = ring::direct_epi_t<C, ACT, DROP>(a, z, m0 + wr * C::WTM, n0 + wc * C::WTN, lane, acc);
 #pragma unroll
     for (int i = 0; i < C::FM; ++i)
 #pragma unroll
@@ -1870,10 +1897,11 @@ static bool persist_enabled() {
 }
 
 static bool persist_ok(const DphGemmArgs& a) {
-  // (not GELU_BWD: its epilogue in the tile loop spilled ~100 VGPRs)
-  return persist_enabled() && a.act != DPH_ACT_GELU_BWD && a.splits == 1 && a.a_kcontig && a.b_kcontig &&
+  // (not GELU_BWD: its epilogue inside the tile loop spills 40-50 VGPRs)
+  return persist_enabled() && !(a.flags & DPH_GEMM_NO_PERSIST) && a.act != DPH_ACT_GELU_BWD && a.splits == 1 &&
+         a.a_kcontig && a.b_kcontig &&
          a.K % (2 * ring::KS) == 0 &&
-         a.K >= 4 * ring::KS && ring::direct_epi_ok(a) && a.A.rows_per_batch == 0 && a.B.rows_per_batch == 0 &&
+         a.K >= 4 * ring::KS && ring::direct_epi_ok(a) && a.M < ((int64_t)1 << 31) && a.N < ((int64_t)1 << 31) &&
          cdiv(a.M, 128) * cdiv(a.N, 128) * a.batch < ((int64_t)1 << 30);
 }
 

@@ -168,3 +168,58 @@ extern "C" int dph_distill_loss_bwd(const float* s, const void* const* t_layers,
                      T, D, l2w, l1w, cosw, cos_logsig, reinterpret_cast<bf16_t*>(ds));
   return check_launch("dph_distill_loss_bwd");
 }
+
+namespace dph {
+namespace {
+// ---- Lagrangian sparsity regulariser + total loss (lightning.py:221-229) ----------------------------------
+// es = 1 - num / orig, d = es - target, reg = lambda1 * d + lambda2 * d^2, loss = distill + reg: one thread,
+// the fp32 operations in the reference's order (replaces ~10 one-element ATen launches forward and ~12 backward).
+__global__ void reg_fwd_kernel(const float* distill, const float* num, const float* l1, const float* l2,
+                               const float* tgt_dev, float tgt, float orig, float* out) {
+  const float t = tgt_dev ? *tgt_dev : tgt;
+  const float es = 1.0f - *num / orig;
+  const float d = es - t;
+  const float reg = *l1 * d + *l2 * (d * d);
+  out[0] = *distill + reg;
+  out[1] = reg;
+  out[2] = es;
+}
+
+// grads[0..2] = d/dnum, d/dlambda1, d/dlambda2 of (gL * loss + greg * reg + ges * es); the distill loss's
+// gradient is gL itself (the host passes it through)
+__global__ void reg_bwd_kernel(const float* gL, const float* greg, const float* ges, const float* num, const float* l1,
+                               const float* l2, const float* tgt_dev, float tgt, float orig, float* grads,
+                               float* sink_l1, float* sink_l2) {
+  const float t = tgt_dev ? *tgt_dev : tgt;
+  const float es = 1.0f - *num / orig;
+  const float d = es - t;
+  const float gr = (gL ? *gL : 0.0f) + (greg ? *greg : 0.0f);
+  const float gd = gr * *l1 + gr * *l2 * 2.0f * d;
+  const float g_es = gd + (ges ? *ges : 0.0f);
+  grads[0] = -g_es / orig;
+  grads[1] = gr * d;
+  grads[2] = gr * (d * d);
+  if (sink_l1) *sink_l1 += grads[1];
+  if (sink_l2) *sink_l2 += grads[2];
+}
+}  // namespace
+}  // namespace dph
+
+extern "C" int dph_reg_loss_fwd(const float* distill, const float* num, const float* lambda1, const float* lambda2,
+                                const float* target_dev, float target, float orig_params, float* out,
+                                hipStream_t stream) {
+  DPH_REQUIRE(distill && num && lambda1 && lambda2 && out && orig_params > 0.f, "dph_reg_loss_fwd: bad args");
+  hipLaunchKernelGGL(reg_fwd_kernel, dim3(1), dim3(1), 0, stream, distill, num, lambda1, lambda2, target_dev, target,
+                     orig_params, out);
+  return check_launch("dph_reg_loss_fwd");
+}
+
+extern "C" int dph_reg_loss_bwd(const float* g_loss, const float* g_reg, const float* g_es, const float* num,
+                                const float* lambda1, const float* lambda2, const float* target_dev, float target,
+                                float orig_params, float* grads, float* sink_l1, float* sink_l2,
+                                hipStream_t stream) {
+  DPH_REQUIRE(num && lambda1 && lambda2 && grads && orig_params > 0.f, "dph_reg_loss_bwd: bad args");
+  hipLaunchKernelGGL(reg_bwd_kernel, dim3(1), dim3(1), 0, stream, g_loss, g_reg, g_es, num, lambda1, lambda2,
+                     target_dev, target, orig_params, grads, sink_l1, sink_l2);
+  return check_launch("dph_reg_loss_bwd");
+}

@@ -105,6 +105,22 @@ def _variant(args):
     return _lib.lib().dph_gemm_variant(C.byref(args)).decode()
 
 
+GEMM_NO_PERSIST = 1            # DphGemmArgs.flags (include/dphubert_hip.h)
+_SHARED_GPU = [0]
+
+
+class shared_gpu:
+    """GEMMs launched inside the block share the GPU with another stream's kernels (the teacher forward
+    next to the student forward): they get one tile per block instead of the persistent ring grid."""
+
+    def __enter__(self):
+        _SHARED_GPU[0] += 1
+        return self
+
+    def __exit__(self, *exc):
+        _SHARED_GPU[0] -= 1
+
+
 def gemm(A: DphMat, B: DphMat, Cm: DphMat, M: int, N: int, K: int, *, a_kcontig: bool, b_kcontig: bool,
          c_dtype: int = OUT_BF16, act: int = ACT_NONE, alpha: float = 1.0, batch: int = 1, splits: int = 1,
          bias=None, colmask=None, smask=None, vec_z_inner: int = 0, pre_out=None, aux_in=None, residual=None,
@@ -122,7 +138,8 @@ def gemm(A: DphMat, B: DphMat, Cm: DphMat, M: int, N: int, K: int, *, a_kcontig:
     args = DphGemmArgs(M, N, K, batch, splits, int(a_kcontig), int(b_kcontig), A, B, Cm, c_dtype, act, alpha,
                        dropout_p, seed & 0xFFFFFFFFFFFFFFFF, ptr(bias), ptr(colmask), ptr(smask), vec_z_inner,
                        ptr(pre_out), ptr(aux_in), ptr(residual), ptr(colsum_out), ptr(colsum_aux), ptr(row_len),
-                       len_rows, drop_row_offset, ptr(ws), ws_bytes, colsum_n)
+                       len_rows, drop_row_offset, ptr(ws), ws_bytes, colsum_n,
+                       GEMM_NO_PERSIST if _SHARED_GPU[0] else 0)
     prof = LaunchProfiler.active
     if prof is not None:
         e0, e1 = _Event(), _Event()
@@ -132,7 +149,11 @@ def gemm(A: DphMat, B: DphMat, Cm: DphMat, M: int, N: int, K: int, *, a_kcontig:
         e1.record()
         name = _variant(args)
         if prof.by_shape:
-            name = f"{name} M={M} N={N} K={K} b={batch} s={splits} {int(a_kcontig)}{int(b_kcontig)}"
+            al = min((x & -x) if x else 1 << 20 for x in (Cm.ptr or 0, ptr(pre_out) or 0, ptr(aux_in) or 0,
+                                                            ptr(residual) or 0, ptr(bias) or 0))
+            name = (f"{name} M={M} N={N} K={K} b={batch} s={splits} {int(a_kcontig)}{int(b_kcontig)} act={act} "
+                    f"res={residual is not None} rl={row_len is not None} rpbA={A.rows_per_batch} "
+                    f"rsC={Cm.row_stride} align={al}")
         prof.records.append((name, 2.0 * M * N * K * batch, e0, e1))
     return ws  # keep alive until the stream consumes it (caching allocator is stream-ordered)
 

@@ -14,6 +14,7 @@ On the hot path the projection + loss run fused on the GPU
 input, teacher layers are read in place, no ``torch.stack`` copies).
 """
 
+import contextlib
 import math
 import pathlib
 from typing import List, Optional, Union
@@ -180,20 +181,24 @@ class DistillModule(nn.Module):
         waveforms, lengths = batch
         self.teacher_model.eval()
         side = self.teacher_stream if waveforms.is_cuda else None
-        if side is not None:
-            # the frozen teacher runs on its own HIP stream, concurrently with the student forward: its
-            # kernels fill the CUs the student's GEMM tile rounds and latency-bound launches leave idle
-            # (forked / joined with stream waits, so a HIP-graph capture records both branches)
-            main = torch.cuda.current_stream()
-            side.wait_stream(main)
-            with torch.cuda.stream(side), torch.no_grad(), ops.private_zero_arena(self._teacher_arena):
-                teacher_hiddens, teacher_lengths = self.teacher_model.extract_features(waveforms, lengths)
-                t_layers = [teacher_hiddens[idx] for idx in self.distill_layers]
-        else:
-            with torch.no_grad():
-                teacher_hiddens, teacher_lengths = self.teacher_model.extract_features(waveforms, lengths)
-                t_layers = [teacher_hiddens[idx] for idx in self.distill_layers]
-        student_hiddens, student_lengths = self.student_model.extract_features(waveforms, lengths)
+        from . import kernels as K
+        # while the two forwards share the GPU, GEMMs take one tile per block (no persistent grids)
+        shared = K.shared_gpu() if side is not None else contextlib.nullcontext()
+        with shared:
+            if side is not None:
+                # the frozen teacher runs on its own HIP stream, concurrently with the student forward: its
+                # kernels fill the CUs the student's GEMM tile rounds and latency-bound launches leave idle
+                # (forked / joined with stream waits, so a HIP-graph capture records both branches)
+                main = torch.cuda.current_stream()
+                side.wait_stream(main)
+                with torch.cuda.stream(side), torch.no_grad(), ops.private_zero_arena(self._teacher_arena):
+                    teacher_hiddens, teacher_lengths = self.teacher_model.extract_features(waveforms, lengths)
+                    t_layers = [teacher_hiddens[idx] for idx in self.distill_layers]
+            else:
+                with torch.no_grad():
+                    teacher_hiddens, teacher_lengths = self.teacher_model.extract_features(waveforms, lengths)
+                    t_layers = [teacher_hiddens[idx] for idx in self.distill_layers]
+            student_hiddens, student_lengths = self.student_model.extract_features(waveforms, lengths)
         if side is not None:
             main.wait_stream(side)
             for t in t_layers:
@@ -220,13 +225,14 @@ class DistillModule(nn.Module):
             cur_target_sparsity = self._get_target_sparsity()
             # the trainer keeps the target in its per-step device block (HIP-graph replays read it there)
             tgt = cur_target_sparsity if self.target_sparsity_dev is None else self.target_sparsity_dev
-            cur_expected_sparsity = 1. - self.student_model.get_num_params() / self.original_num_params
-            loss_reg = self.lambda1 * (cur_expected_sparsity - tgt) \
-                + self.lambda2 * (cur_expected_sparsity - tgt) ** 2
+            # (lightning.py:221-229 in one kernel pair: ops.RegLossFn)
+            loss, loss_reg, cur_expected_sparsity = ops.RegLossFn.apply(
+                loss_distill, self.student_model.get_num_params(), self.lambda1, self.lambda2, tgt,
+                float(self.original_num_params))
             cur_target_sparsity = tgt
         else:
             loss_reg = 0
-        loss = loss_distill + loss_reg
+            loss = loss_distill
         self.log_dict({f"{mode}_loss": loss, f"{mode}_loss_distill": loss_distill, f"{mode}_loss_mse": loss_mse,
                        f"{mode}_loss_l1": loss_l1, f"{mode}_loss_cos": loss_cos, f"{mode}_loss_reg": loss_reg})
         if mode == "train" and self.use_reg:

@@ -146,7 +146,19 @@ def _table(rows) -> torch.Tensor:
 
 def refresh_images(updated_ids) -> None:
     """Recast every registered image whose sources are all in ``updated_ids`` (ids of parameters
-    the optimizer just wrote), re-transpose their W^T images, and re-key both caches."""
+    the optimizer just wrote), re-transpose their W^T images, re-copy the fp32 concatenations, and
+    re-key the caches."""
+    cats = [e for e in _CAT_REFRESH.values() if all(id(t) in updated_ids for t in e[1])]
+    if cats:
+        crows = []
+        for _owner, ts, out in cats:
+            off = 0
+            for t in ts:
+                crows.append((t.data_ptr(), out.data_ptr() + off * 4, t.numel()))
+                off += t.numel()
+        call("dph_copy_f32_multi", ptr(_table(crows)), len(crows), max(r[2] for r in crows), _s())
+        for owner, ts, out in cats:
+            owner._dph_cat = (("f32cat",) + _version_key(ts), out)
     ents = [e for e in _REFRESH.values() if all(id(t) in updated_ids for t in e[1])]
     if not ents:
         return
@@ -167,15 +179,32 @@ def refresh_images(updated_ids) -> None:
         call("dph_transpose_bf16_multi", ptr(ttab), len(trows), _s())
 
 
+_CAT_REFRESH = {}   # id(concatenation) -> (owner, sources, concatenation)
+
+
 def f32_cat(*ts: torch.Tensor) -> torch.Tensor:
-    """torch.cat of fp32 parameters (e.g. the q/k/v biases), cached like bf16_image."""
+    """Concatenation of fp32 parameters (e.g. the q/k/v biases), cached like bf16_image and refreshed by
+    the optimizer's batched image refresh (one dph_copy_f32_multi launch for all of them)."""
     owner = ts[0]
     key = ("f32cat",) + _version_key(ts)
     hit = getattr(owner, "_dph_cat", None)
     if hit is not None and hit[0] == key:
         return hit[1]
-    out = torch.cat([t.detach() for t in ts])
+    n = sum(t.numel() for t in ts)
+    out = torch.empty(n, dtype=F32, device=ts[0].device)
+    rows, off = [], 0
+    for t in ts:
+        rows.append((t.detach().data_ptr(), out.data_ptr() + off * 4, t.numel()))
+        off += t.numel()
+    if torch.cuda.is_current_stream_capturing():
+        out.copy_(torch.cat([t.detach() for t in ts]))       # (tables are built outside captures)
+    else:
+        call("dph_copy_f32_multi", ptr(_table(rows)), len(rows), max(r[2] for r in rows), _s())
+    if hit is not None:
+        _CAT_REFRESH.pop(id(hit[1]), None)
     owner._dph_cat = (key, out)
+    if all(t.requires_grad for t in ts):
+        _CAT_REFRESH[id(out)] = (owner, ts, out)
     return out
 
 
@@ -422,6 +451,47 @@ class HardConcreteFn(torch.autograd.Function):
         call("dph_hc_sample_bwd", ptr(la), ptr(u), ptr(dmask.contiguous()), ptr(dla), la.numel(), HC_BETA,
              HC_LIMIT_L, HC_LIMIT_R, _s())
         return dla, None
+
+
+class RegLossFn(torch.autograd.Function):
+    """loss = distill + lambda1*(es - t) + lambda2*(es - t)^2 with es = 1 - num/orig (lightning.py:221-229):
+    one single-thread kernel forward (dph_reg_loss_fwd) and one backward, instead of ~10 + ~12 one-element
+    ATen launches.  Returns (loss, loss_reg, expected_sparsity) as 0-d device tensors; ``target`` is a
+    0-d device tensor (the HIP-graph step block) or a float."""
+
+    @staticmethod
+    def forward(ctx, distill, num, lambda1, lambda2, target, orig: float):
+        dev = distill.device
+        out = torch.empty(3, dtype=F32, device=dev)
+        tdev = target if torch.is_tensor(target) else None
+        tval = 0.0 if tdev is not None else float(target)
+        for t in (distill, num, lambda1, lambda2) + ((tdev,) if tdev is not None else ()):
+            if t.dtype != F32 or t.numel() != 1 or not t.is_contiguous():
+                raise ValueError("RegLossFn: fp32 scalar tensors expected")
+        call("dph_reg_loss_fwd", ptr(distill), ptr(num), ptr(lambda1), ptr(lambda2), ptr(tdev), tval, float(orig),
+             ptr(out), _s())
+        ctx.save_for_backward(num, lambda1, lambda2, *((tdev,) if tdev is not None else ()))
+        ctx.tval, ctx.orig, ctx.has_t = tval, float(orig), tdev is not None
+        ctx.lambdas = (lambda1, lambda2)      # the Parameters themselves (their gradient sinks)
+        return out[0], out[1], out[2]
+
+    @staticmethod
+    def backward(ctx, g_loss, g_reg, g_es):
+        saved = ctx.saved_tensors
+        num, l1, l2 = saved[:3]
+        tdev = saved[3] if ctx.has_t else None
+        grads = torch.empty(3, dtype=F32, device=num.device)
+        gs = [g.contiguous() if g is not None else None for g in (g_loss, g_reg, g_es)]
+        sinks = [getattr(p, "_dph_sink", None) for p in ctx.lambdas]
+        direct = all(sk is not None for sk in sinks)
+        sp = [sk[0].data_ptr() + sk[1] * 4 for sk in sinks] if direct else [None, None]
+        call("dph_reg_loss_bwd", ptr(gs[0]), ptr(gs[1]), ptr(gs[2]), ptr(num), ptr(l1), ptr(l2), ptr(tdev), ctx.tval,
+             ctx.orig, ptr(grads), sp[0], sp[1], _s())
+        if direct:
+            for p in ctx.lambdas:
+                p._dph_sink_ready(p)
+            return g_loss, grads[0].view(num.shape), None, None, None, None
+        return g_loss, grads[0].view(num.shape), grads[1].view(l1.shape), grads[2].view(l2.shape), None, None
 
 
 class HardConcreteBank:

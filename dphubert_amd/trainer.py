@@ -188,7 +188,13 @@ class Trainer:
         m = self.module
         self.reducer.prepare(zero=zero, sync=final)
         loss = m.training_step(batch, 0)
-        (loss / self.accum_grad if self.accum_grad > 1 else loss).backward()
+        # backward seeded with a persistent 1/accum_grad scalar: no ones_like fill / division launch per step
+        seed = getattr(self, "_grad_seed", None)
+        if seed is None or seed.device != loss.device:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("Trainer: the backward seed must exist before a graph capture")
+            seed = self._grad_seed = torch.full((), 1.0 / self.accum_grad, dtype=loss.dtype, device=loss.device)
+        loss.backward(seed)
         if final:
             self.reducer.finish()
             self.optimizer.launch()
@@ -202,7 +208,10 @@ class Trainer:
         try:
             if prof is not None:
                 LaunchProfiler.active = prof
-            with torch.cuda.graph(g, pool=self._pool):
+            # thread_local: the process group's watchdog thread keeps polling the events of earlier (eager)
+            # collectives while this thread captures; under the default "global" mode that poll is an illegal
+            # call during capture and aborts the process ("operation not permitted when stream is capturing")
+            with torch.cuda.graph(g, pool=self._pool, capture_error_mode="thread_local"):
                 loss = self._gpu_step(self._static, zero, final)
         finally:
             LaunchProfiler.active = None

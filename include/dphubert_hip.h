@@ -91,7 +91,13 @@ typedef struct DphGemmArgs {
   void* workspace;        /* split-K partials                                  */
   int64_t workspace_bytes;
   int64_t colsum_n;       /* column sums only for n < colsum_n (0: all N); padded-width operands */
+  int64_t flags;          /* DPH_GEMM_* bits below                                */
 } DphGemmArgs;
+
+/* flags: one tile per block even where the persistent ring grid applies -- for GEMMs that share the
+ * GPU with another stream's kernels (the teacher forward runs concurrently with the student forward):
+ * a persistent grid sized to the CUs stalls on the CUs the other kernels hold, a tile grid rebalances */
+#define DPH_GEMM_NO_PERSIST 1
 
 int dph_gemm(const DphGemmArgs* args, hipStream_t stream);
 /* name (as it appears in rocprof kernel names) of the kernel dph_gemm launches for these args */
@@ -274,6 +280,10 @@ int dph_transpose_bf16(const void* src, int64_t R, int64_t C, void* dst, hipStre
  * dph_transpose_bf16 launch per weight): device tables of {src fp32*, dst bf16*, n} resp.
  * {src bf16*, dst bf16*, R, C} int64 entries (R, C multiples of 8) */
 int dph_cast_bf16_multi(const int64_t* table, int64_t n_entries, hipStream_t stream);
+/* batched fp32 copies / zero fills in one launch: device table of {src fp32* (0 = zeros), dst fp32*, n}
+ * int64 entries, max_n >= every n (sizes the grid).  The q/k/v bias concatenations refreshed after an
+ * optimizer step and the gradient buckets zeroed before a backward (replaces an ATen cat / fill each). */
+int dph_copy_f32_multi(const int64_t* table, int64_t n_entries, int64_t max_n, hipStream_t stream);
 /* frame lengths after the conv stack (components.py:179-181, every layer in one launch);
  * kernel_sizes / strides are HOST arrays of n_layers (<= 16) entries, read at call time */
 int dph_conv_lengths(const int64_t* len_in, int64_t* len_out, int64_t n, int64_t n_layers,
@@ -311,6 +321,19 @@ int dph_distill_loss_fwd(const float* s, const void* const* t_layers, int64_t B,
 int dph_distill_loss_bwd(const float* s, const void* const* t_layers, const float* rowstats, const float* dloss,
                          int64_t B, int64_t L, int64_t T, int64_t D, float l2w, float l1w, float cosw,
                          int cos_logsig, void* ds, hipStream_t stream);
+
+/* Lagrangian sparsity regulariser and total loss (lightning.py:221-229, DistillModule._step):
+ * es = 1 - num/orig_params, d = es - target, reg = lambda1*d + lambda2*d^2, out[0..2] = distill + reg,
+ * reg, es.  target from target_dev when non-NULL (the HIP-graph step block), else `target`.  All
+ * pointers are device fp32 scalars. */
+int dph_reg_loss_fwd(const float* distill, const float* num, const float* lambda1, const float* lambda2,
+                     const float* target_dev, float target, float orig_params, float* out, hipStream_t stream);
+/* grads[0..2] = d/d(num, lambda1, lambda2) of g_loss*loss + g_reg*reg + g_es*es (any g may be NULL = 0);
+ * d/d(distill) is g_loss.  sink_l1 / sink_l2 (optional): the lambdas' gradient-bucket slots, += their
+ * gradients (the data-parallel sinks: no AccumulateGrad launch). */
+int dph_reg_loss_bwd(const float* g_loss, const float* g_reg, const float* g_es, const float* num,
+                     const float* lambda1, const float* lambda2, const float* target_dev, float target,
+                     float orig_params, float* grads, float* sink_l1, float* sink_l2, hipStream_t stream);
 
 /* ------------------------------------------------------------------------ *
  * HardConcrete (hardconcrete.py:85-116) + expected parameter count

@@ -232,7 +232,8 @@ def test_model_step_passes_stored_keep_bits(monkeypatch):
     seen.clear()
     with torch.no_grad():
         m(wave)
-    assert [k for _, k in seen] == [None] or [k for _, k in seen] == [0], seen
+    # (a no-grad forward stores no keep bits, whichever attention entry it goes through)
+    assert all(k in (None, 0) for _, k in seen), seen
 
 
 def test_layernorm_branch_dropout_keep_rate_and_scale():

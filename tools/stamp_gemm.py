@@ -38,7 +38,7 @@ else:
     Cm = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
     ws = torch.zeros(8 * 65536 * 8, dtype=torch.int64, device="cuda")
     args = _lib.DphGemmArgs(M, N, Kd, 1, 1, 1, 1, K.dense(A), K.dense(B), K.dense(Cm), 0, 0, 1.0, 0.0, 0, None, None,
-                            None, 0, None, None, None, None, None, None, 0, 0, ws.data_ptr(), ws.numel() * 8, 0)
+                            None, 0, None, None, None, None, None, None, 0, 0, ws.data_ptr(), ws.numel() * 8, 0, 0)
     for _ in range(5):
         _lib.call("dph_gemm", C.byref(args), _lib.stream_ptr())
     torch.cuda.synchronize()
