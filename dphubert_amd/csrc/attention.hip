@@ -410,14 +410,12 @@ __global__ void __launch_bounds__(256) attn_bwd_prep_kernel(const bf16_t* __rest
 // u < NG.  Loops over query steps of 32 rows; Q' and dO' (= hm*dO_m) tiles staged in LDS.
 // ---------------------------------------------------------------------------
 template <bool DROP, bool BIAS, bool KEEP>
-__global__ void __launch_bounds__(256, 2) attn_bwd_dkv_kernel(const bf16_t* __restrict__ qkv,
-                                                           const bf16_t* __restrict__ dom,
-                                                           const float* __restrict__ head_mask,
-                                                           const float* __restrict__ lse,
-                                                           const float* __restrict__ Dv, bf16_t* __restrict__ dqkv,
-                                                           const int64_t* __restrict__ key_len, AttnShape sh,
-                                                           float scale, float drop_p, uint64_t seed, RelBias rb,
-                                                           const uint16_t* __restrict__ keep_in) {
+__device__ __forceinline__ void attn_bwd_dkv_body(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dom,
+                                                  const float* __restrict__ head_mask, const float* __restrict__ lse,
+                                                  const float* __restrict__ Dv, bf16_t* __restrict__ dqkv,
+                                                  const int64_t* __restrict__ key_len, AttnShape sh, float scale,
+                                                  float drop_p, uint64_t seed, RelBias rb,
+                                                  const uint16_t* __restrict__ keep_in, int bx, int64_t h, int64_t b) {
   seed = epoch_seed(seed);   // per-step RNG epoch (graph replays)
   const uint32_t mix = seed_mix(seed);
   constexpr int TB = QT_BWD * 128;   // 4096 B per tile
@@ -427,10 +425,8 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkv_kernel(const bf16_t* __re
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int g = lane >> 4;
-  const int64_t b = blockIdx.z;
-  const int64_t h = blockIdx.y;
   const int64_t T = sh.T, H = sh.H, RS = sh.RS;
-  const int64_t k0 = (int64_t)blockIdx.x * RB + wave * 16 * NG;
+  const int64_t k0 = (int64_t)bx * RB + wave * 16 * NG;
   const bf16_t* rowbase = qkv + b * T * RS;
   const bf16_t* dobase = dom + b * T * (H * HD) + h * HD;
   const int64_t klen = key_len ? key_len[b] : T;
@@ -486,13 +482,13 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkv_kernel(const bf16_t* __re
 #pragma unroll
   for (int u = 0; u < NG; ++u) {
     const int key = (int)kme[u];
-    kt_loc[u] = (key >> 6) - 2 * (int)blockIdx.x;
+    kt_loc[u] = (key >> 6) - 2 * bx;
     const int bit = 16 * ((key >> 2) & 3) + 4 * ((key >> 4) & 3) + (key & 3);
     khalf[u] = bit >> 5;
     kbit[u] = bit & 31;
   }
   extern __shared__ float tw[];   // BIAS: [T + RB - 1] table window (diagonals of this block's keys)
-  const int toff = (int)blockIdx.x * RB;
+  const int toff = bx * RB;
   if constexpr (BIAS) stage_tab_window(tw, rb.tab + h * (2 * T - 1), toff, (int)T);   // ordered by the first barrier
 
   const int nqt = (int)cdiv(T, QT_BWD);
@@ -513,7 +509,7 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkv_kernel(const bf16_t* __re
     if (use_keep && tid >= 64 && tid < 128) {   // (constexpr-false unless KEEP)
       const int r = tid & 31, lt = (tid >> 5) & 1;
       const int64_t q = (int64_t)qt * QT_BWD + r;
-      const int ktile = 2 * (int)blockIdx.x + lt;
+      const int ktile = 2 * bx + lt;
       uint2 wv = make_uint2(0u, 0u);
       if (q < T && ktile < nkt)
         wv = *reinterpret_cast<const uint2*>(keep_in + ((b * H + h) * T + q) * (nkt * 4) + ktile * 4);
@@ -642,14 +638,12 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkv_kernel(const bf16_t* __re
 // backward dQ: block = (128 query rows, h, b), 4 waves x 2 x 16 rows; loops over key tiles.
 // ---------------------------------------------------------------------------
 template <bool DROP, bool BIAS, bool KEEP>
-__global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(const bf16_t* __restrict__ qkv,
-                                                          const bf16_t* __restrict__ dom,
-                                                          const float* __restrict__ head_mask,
-                                                          const float* __restrict__ lse,
-                                                          const float* __restrict__ Dv, bf16_t* __restrict__ dqkv,
-                                                          const int64_t* __restrict__ key_len, AttnShape sh,
-                                                          float scale, float drop_p, uint64_t seed, RelBias rb,
-                                                          const uint16_t* __restrict__ keep_in) {
+__device__ __forceinline__ void attn_bwd_dq_body(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dom,
+                                                 const float* __restrict__ head_mask, const float* __restrict__ lse,
+                                                 const float* __restrict__ Dv, bf16_t* __restrict__ dqkv,
+                                                 const int64_t* __restrict__ key_len, AttnShape sh, float scale,
+                                                 float drop_p, uint64_t seed, RelBias rb,
+                                                 const uint16_t* __restrict__ keep_in, int bx, int64_t h, int64_t b) {
   extern __shared__ float dyn[];   // BIAS: hist [T + RB - 1] (diagonal sums of dS * gate) | table window [T + RB - 1]
   seed = epoch_seed(seed);   // per-step RNG epoch (graph replays)
   const uint32_t mix = seed_mix(seed);
@@ -658,10 +652,8 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(const bf16_t* __res
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int g = lane >> 4;
-  const int64_t b = blockIdx.z;
-  const int64_t h = blockIdx.y;
   const int64_t T = sh.T, H = sh.H, RS = sh.RS;
-  const int64_t q0 = (int64_t)blockIdx.x * RB + wave * 16 * NG;
+  const int64_t q0 = (int64_t)bx * RB + wave * 16 * NG;
   const bf16_t* rowbase = qkv + b * T * RS;
   const int64_t klen = key_len ? key_len[b] : T;
   const float hm = head_mask ? head_mask[h] : 1.0f;
@@ -696,7 +688,7 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(const bf16_t* __res
   }
   float* hist = dyn;
   float* tw = dyn + (T32 + RB - 1);
-  const int qb0 = (int)blockIdx.x * RB;
+  const int qb0 = bx * RB;
   const int toff = T32 - 1 - (qb0 + RB - 1);
   float gq[NG], dg[NG];
 #pragma unroll
@@ -889,6 +881,32 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(const bf16_t* __res
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// backward launch: the dK/dV blocks (z < nbz) and the dQ blocks (z >= nbz) of one layer in ONE grid.  Each
+// kernel alone is 768 blocks at the distill shape (B=16, H=12, T=499) against 512 resident slots (2 per CU),
+// so each ran 1.5 rounds with the last one half empty; in one grid the dQ blocks (about half the work of a
+// dK/dV block) fill the CUs the dK/dV blocks free, longest first (dispatch follows z).
+// mode 1 / 2: dK/dV only / dQ only (A/B timing, DPH_ATTN_SPLIT=1).
+// ---------------------------------------------------------------------------
+template <bool DROP, bool BIAS, bool KEEP>
+__global__ void __launch_bounds__(256, 2) attn_bwd_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dom,
+                                                       const float* __restrict__ head_mask,
+                                                       const float* __restrict__ lse, const float* __restrict__ Dv,
+                                                       bf16_t* __restrict__ dqkv, const int64_t* __restrict__ key_len,
+                                                       AttnShape sh, float scale, float drop_p, uint64_t seed,
+                                                       RelBias rb, const uint16_t* __restrict__ keep_in, int nbz,
+                                                       int mode) {
+  const int z = (int)blockIdx.z;
+  const bool kv = mode == 1 || (mode == 0 && z < nbz);
+  if (kv)
+    attn_bwd_dkv_body<DROP, BIAS, KEEP>(qkv, dom, head_mask, lse, Dv, dqkv, key_len, sh, scale, drop_p, seed, rb,
+                                        keep_in, (int)blockIdx.x, blockIdx.y, z);
+  else
+    attn_bwd_dq_body<DROP, BIAS, KEEP>(qkv, dom, head_mask, lse, Dv, dqkv, key_len, sh, scale, drop_p, seed, rb,
+                                       keep_in, (int)blockIdx.x, blockIdx.y, mode == 0 ? z - nbz : z);
+}
+
 }  // namespace
 }  // namespace dph
 
@@ -910,14 +928,21 @@ void launch_bwd_k(dim3 grid, hipStream_t stream, const void* qkv, const void* do
                   const float* Dvec, void* dqkv, const int64_t* key_len, AttnShape sh, float scale, float p,
                   uint64_t seed, RelBias rb, const void* keep) {
   const size_t tw_bytes = BIAS ? (size_t)(sh.T + RB - 1) * sizeof(float) : 0;
-  hipLaunchKernelGGL((attn_bwd_dkv_kernel<DROP, BIAS, KEEP>), grid, dim3(256), tw_bytes, stream,
+  const char* e = getenv("DPH_ATTN_SPLIT");
+  const int nbz = (int)grid.z;
+  if (e && e[0] == '1') {
+    for (int mode = 1; mode <= 2; ++mode)
+      hipLaunchKernelGGL((attn_bwd_kernel<DROP, BIAS, KEEP>), grid, dim3(256), 2 * tw_bytes, stream,
+                         reinterpret_cast<const bf16_t*>(qkv), reinterpret_cast<const bf16_t*>(dom), hm, lse, Dvec,
+                         reinterpret_cast<bf16_t*>(dqkv), key_len, sh, scale, p, seed, rb,
+                         reinterpret_cast<const uint16_t*>(keep), nbz, mode);
+    return;
+  }
+  const dim3 g2(grid.x, grid.y, 2 * grid.z);
+  hipLaunchKernelGGL((attn_bwd_kernel<DROP, BIAS, KEEP>), g2, dim3(256), 2 * tw_bytes, stream,
                      reinterpret_cast<const bf16_t*>(qkv), reinterpret_cast<const bf16_t*>(dom), hm, lse, Dvec,
                      reinterpret_cast<bf16_t*>(dqkv), key_len, sh, scale, p, seed, rb,
-                     reinterpret_cast<const uint16_t*>(keep));
-  hipLaunchKernelGGL((attn_bwd_dq_kernel<DROP, BIAS, KEEP>), grid, dim3(256), 2 * tw_bytes, stream,
-                     reinterpret_cast<const bf16_t*>(qkv), reinterpret_cast<const bf16_t*>(dom), hm, lse, Dvec,
-                     reinterpret_cast<bf16_t*>(dqkv), key_len, sh, scale, p, seed, rb,
-                     reinterpret_cast<const uint16_t*>(keep));
+                     reinterpret_cast<const uint16_t*>(keep), nbz, 0);
 }
 
 template <bool DROP, bool BIAS>
@@ -963,6 +988,7 @@ static int attention_bwd(const void* qkv, const void* do_masked, const float* he
   const bool bias = rb.tab != nullptr;
   DPH_REQUIRE(dropout_p <= 0.f || pairs_fit(B, T, H), "dph_attention_bwd: B*H*T*ceil(T/2) >= 2^32 dropout pairs");
   DPH_REQUIRE(keep == nullptr || (reinterpret_cast<uintptr_t>(keep) & 7) == 0, "dph_attention_bwd: keep bits not 8-B aligned");
+  DPH_REQUIRE(2 * B < 65536 && H < 65536, "dph_attention_bwd: grid too large (B=%lld H=%lld)", (long long)B, (long long)H);
   if (dropout_p > 0.f) {
     if (bias) launch_bwd<true, true>(grid, stream, qkv, do_masked, head_mask, lse, Dvec, dqkv, key_len, sh, scale, dropout_p, seed, rb, keep);
     else launch_bwd<true, false>(grid, stream, qkv, do_masked, head_mask, lse, Dvec, dqkv, key_len, sh, scale, dropout_p, seed, rb, keep);

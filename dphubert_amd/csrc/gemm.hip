@@ -799,11 +799,13 @@ struct Cfg {
   static constexpr int DMA = DMA_A + DMA_B;                   // per thread per slice
   static_assert(DMA == 2 || DMA == 3 || DMA == 4 || DMA == 5 || DMA == 8,
                 "vmcnt immediates exist for 2, 3, 4, 5 or 8 DMA per thread per slice");
-  static constexpr int EROWS = BM > 128 ? 128 : BM;          // epilogue staging rows per pass
+  static constexpr int EROWS = BM % 128 == 0 ? (BM > 128 ? 128 : BM) : BM / 2;   // epilogue staging rows per pass
   static constexpr int CROW = BN + 4;
   static constexpr int EPI = EROWS * CROW * 4;
   static constexpr int LDS = PIPE > EPI ? PIPE : EPI;
-  static constexpr int MINB = (NW >= 8 && BM * BN > 128 * 128) ? 1 : (BM * BN <= 128 * 64 ? 3 : 2);   // blocks per CU
+  // blocks per CU (the 192-row tile: one, its shapes have about one tile per CU; the persistent loop needs
+  // more than 256 registers for its 96 accumulators + two fragment sets)
+  static constexpr int MINB = (BM % 128 != 0 || (NW >= 8 && BM * BN > 128 * 128)) ? 1 : (BM * BN <= 128 * 64 ? 3 : 2);
   // HIP's second __launch_bounds__ argument is the minimum number of WAVES PER SIMD (not blocks per CU):
   // MINB blocks of NW waves over the 4 SIMDs (caps the VGPRs at 512 / WPE)
   static constexpr int WPE = (MINB * NW + 3) / 4;
@@ -821,6 +823,11 @@ using Mid8 = Cfg<128, 128, 64, 32>;
 // per MFMA; half the L2->LDS bytes per flop of the 128 x 128 tile), one block per CU
 using Wide = Cfg<256, 128, 64, 64>;
 using Flat = Cfg<128, 256, 64, 64>;
+// 192 x 128 tile, 4 waves of 96 x 64 (24 MFMAs per wave per slice, 0.42 fragment reads per MFMA): the
+// M = B*T, N = 768 projections (out-proj / FFN2 forward, QKV / FFN1 / out-proj input gradients) have 189
+// 128 x 256 tiles for 256 CUs (74 % of the chip busy, each CU a full 32 K-output tile); 192 x 128 gives
+// 252 tiles of 24 K outputs (98 % busy, 25 % less work on the critical CU)
+using Tri = Cfg<192, 128, 96, 64>;
 
 // s_waitcnt vmcnt(n * DMA): at most n slices' DMAs still in flight
 template <int DMA, int n>
@@ -1388,7 +1395,7 @@ __global__ void __launch_bounds__(C::NT, C::WPE) ring_gemm_kernel(const DphGemmA
   };
   // (not the 256 x 256 tile: its 128 accumulators leave no room for the epilogue inputs; not the 8-wave
   // 128 x 128 tile: at 4 waves per SIMD its 128-VGPR budget spilled 50 registers)
-  if constexpr (DPH_DIRECT_EPI && C::FM * C::FN <= 16 && C::WPE <= 3) {
+  if constexpr (DPH_DIRECT_EPI && (C::FM * C::FN <= 16 || C::NW == 4) && C::WPE <= 3) {
     if (a.splits == 1 && ring::direct_epi_ok(a)) {
       DPH_TSTAMP(sA);
       sB = sA;
@@ -1784,7 +1791,25 @@ static int small_nt(int64_t kchunk) {
 static int gemm_path_override() {
   const char* e = getenv("DPH_GEMM_PATH");
   if (!e) return 0;
-  return !strcmp(e, "small") ? 1 : !strcmp(e, "big") ? 2 : !strcmp(e, "mid") ? 3 : !strcmp(e, "tall") ? 4 : !strcmp(e, "half") ? 5 : !strcmp(e, "mid8") ? 6 : !strcmp(e, "mid8mn") ? 7 : !strcmp(e, "wide") ? 8 : !strcmp(e, "flat") ? 9 : 0;
+  return !strcmp(e, "small") ? 1 : !strcmp(e, "big") ? 2 : !strcmp(e, "mid") ? 3 : !strcmp(e, "tall") ? 4 : !strcmp(e, "half") ? 5 : !strcmp(e, "mid8") ? 6 : !strcmp(e, "mid8mn") ? 7 : !strcmp(e, "wide") ? 8 : !strcmp(e, "flat") ? 9 : !strcmp(e, "tri") ? 10 : !strcmp(e, "notri") ? 11 : 0;
+}
+
+// the 192 x 128 tile takes the register epilogue only (its staged epilogue is compiled but not routed)
+static bool tri_ok(const DphGemmArgs& a) {
+  return a.splits == 1 && a.a_kcontig && a.b_kcontig && a.K % ring::KS == 0 && ring::direct_epi_ok(a) &&
+         a.act != DPH_ACT_GELU_BWD;
+}
+
+static int num_cus();
+
+// busy-CU model: ceil(tiles / CUs) rounds, each as long as one tile's area (one block per CU)
+static bool tri_better(const DphGemmArgs& a) {
+  const int64_t cus = num_cus();
+  auto cost = [&](int64_t bm, int64_t bn) {
+    const int64_t tiles = cdiv(a.M, bm) * cdiv(a.N, bn) * a.batch;
+    return cdiv(tiles, cus) * bm * bn;
+  };
+  return cost(ring::Tri::BM, ring::Tri::BN) < cost(ring::Flat::BM, ring::Flat::BN);
 }
 
 // an operand the ring kernels can stage: k-contiguous with whole 32-deep k-slices, or mn-contiguous
@@ -1822,6 +1847,8 @@ static int gemm_kind(const DphGemmArgs& a, int64_t kchunk) {
   // slower on 7984 x 768 x 3072 / 2304, the 256 x 256 one 10 % on the 1536-deep conv GEMMs) and N <= 1024
   // (few 128 x 128 tiles per CU: 7984 x 768 x 768 -11 %)
   if (big_ok && a.N > ring::Tall::BN && (kchunk >= 1536 || (a.N <= 1024 && kchunk >= 4 * ring::KS))) kind = 8;
+  // N <= 1024 on the 192 x 128 tile when it fills the CUs better (whole-chip rounds of tiles x tile area)
+  if (kind == 8 && a.N <= 1024 && tri_ok(a) && tri_better(a)) kind = 10;
   const int path = gemm_path_override();
   if (path == 1) kind = 0;
   if (path == 2 && big_ok) kind = 2;
@@ -1832,6 +1859,8 @@ static int gemm_kind(const DphGemmArgs& a, int64_t kchunk) {
   if (path == 7 && ring_ok && !big_ok) kind = 6;     // 8-wave 128x128 tile with mn-contiguous operands
   if (path == 8 && big_ok) kind = 7;
   if (path == 9 && big_ok) kind = 8;
+  if (path == 10 && big_ok && tri_ok(a)) kind = 10;
+  if (path == 11 && kind == 10) kind = 8;     // "notri": the 128 x 256 tile where the 192 x 128 one would run
   return kind;
 }
 
@@ -1846,6 +1875,8 @@ extern "C" const char* dph_gemm_variant(const DphGemmArgs* args) {
   const DphGemmArgs& a = *args;
   const int kind = gemm_kind(a, gemm_kchunk(a));
   if (kind == 6) return a.a_kcontig ? "ring::Cfg<128, 128, 64, 32>, true, false>" : "ring::Cfg<128, 128, 64, 32>, false, false>";
+  if (kind == 10) return persist_ok(a) ? "persist_kernel<dph::(anonymous namespace)::ring::Cfg<192, 128, 96, 64>"
+                                       : "ring::Cfg<192, 128, 96, 64>, true, true>";
   if (kind == 8) return persist_ok(a) ? "persist_kernel<dph::(anonymous namespace)::ring::Cfg<128, 256, 64, 64>"
                                       : "ring::Cfg<128, 256, 64, 64>, true, true>";
   if (kind == 7) return persist_ok(a) ? "persist_kernel<dph::(anonymous namespace)::ring::Cfg<256, 128, 64, 64>"
@@ -1954,7 +1985,10 @@ extern "C" int dph_gemm(const DphGemmArgs* args, hipStream_t stream) {
   // when there are >= ~2 full rounds of tiles over the 256 CUs at one block per CU, else the
   // 128x128 tile (DPH_GEMM_PATH=small|big|mid forces a path, for tests)
   const int kind = gemm_kind(a, kchunk);
-  if (kind == 8) {
+  if (kind == 10) {
+    DPH_REQUIRE(cdiv(a.M, ring::Tri::BM) < 65536 && a.batch * a.splits < 65536, "dph_gemm: grid too large");
+    if (!launch_ring_persist<ring::Tri>(a, stream)) launch_ring<ring::Tri, false>(a, kchunk, stream);
+  } else if (kind == 8) {
     DPH_REQUIRE(cdiv(a.M, ring::Flat::BM) < 65536 && a.batch * a.splits < 65536, "dph_gemm: grid too large");
     if (!launch_ring_persist<ring::Flat>(a, stream)) launch_ring<ring::Flat, false>(a, kchunk, stream);
   } else if (kind == 7) {

@@ -10,10 +10,10 @@ torch.manual_seed(0)
 
 
 @pytest.fixture(autouse=True, params=["small", "mid", "big", "wide", "flat", "flat-np", "tall", "half", "mid8",
-                                     "mid8mn"])
+                                     "mid8mn", "tri", "tri-np"])
 def gemm_path(request, monkeypatch):
     """Run every test on each GEMM path: the 128x128 register-staged kernel and the 128x128 /
-    256x256 / 256x128 / 128x256 / 256x64 LDS-DMA ring kernels (taken where their constraints hold: both operands
+    256x256 / 256x128 / 128x256 / 256x64 / 192x128 LDS-DMA ring kernels (taken where their constraints hold: both operands
     k-contiguous, K % 32 == 0)."""
     path = request.param
     if path.endswith("-np"):            # one tile per block instead of the persistent grid

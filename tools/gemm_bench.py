@@ -19,6 +19,8 @@ SHAPES = [  # (name, M, N, K, a_kcontig, b_kcontig)
     ("ffn2 dgrad", M, 3072, 768, True, False),
     ("ffn1 dgrad", M, 768, 3072, True, False),
     ("qkv dgrad", M, 768, 2304, True, False),
+    ("ffn1 dgrad kk", M, 768, 3072, True, True),
+    ("qkv dgrad kk", M, 768, 2304, True, True),
     ("ffn1 wgrad", 3072, 768, M, False, False),
     ("qkv wgrad", 2304, 768, M, False, False),
     ("sq 4096", 4096, 4096, 4096, True, True),
