@@ -1802,14 +1802,14 @@ static bool tri_ok(const DphGemmArgs& a) {
 
 static int num_cus();
 
-// busy-CU model: ceil(tiles / CUs) rounds, each as long as one tile's area (one block per CU)
+// only where both tilings are a single round over the CUs (one block per CU) and the 192 x 128 one has
+// less area per CU: with several rounds the 128 x 256 tile's two waves per SIMD win (conv1 255984 x 512 x
+// 1536: 553 vs 622 us)
 static bool tri_better(const DphGemmArgs& a) {
   const int64_t cus = num_cus();
-  auto cost = [&](int64_t bm, int64_t bn) {
-    const int64_t tiles = cdiv(a.M, bm) * cdiv(a.N, bn) * a.batch;
-    return cdiv(tiles, cus) * bm * bn;
-  };
-  return cost(ring::Tri::BM, ring::Tri::BN) < cost(ring::Flat::BM, ring::Flat::BN);
+  const int64_t tf = cdiv(a.M, ring::Flat::BM) * cdiv(a.N, ring::Flat::BN) * a.batch;
+  const int64_t tt = cdiv(a.M, ring::Tri::BM) * cdiv(a.N, ring::Tri::BN) * a.batch;
+  return tf <= cus && tt <= cus && ring::Tri::BM * ring::Tri::BN < ring::Flat::BM * ring::Flat::BN;
 }
 
 // an operand the ring kernels can stage: k-contiguous with whole 32-deep k-slices, or mn-contiguous

@@ -19,6 +19,7 @@ Reference semantics followed (file:line of seas2nada/DPHuBERT):
   ExpectedParamsFn     model.py:109-113 + get_num_params chain
 """
 
+import contextlib
 import math
 import os
 from typing import List, Optional, Sequence
@@ -366,6 +367,67 @@ def _zeros(n, like_device, dtype=F32):
 
 
 # ---------------------------------------------------------------------------
+# weight-gradient GEMMs on a side stream (Trainer: wgrad_overlap)
+# ---------------------------------------------------------------------------
+# A layer's weight gradients feed nothing else in the backward (only the optimizer, or the bucket's
+# all-reduce), so they run on a second HIP stream, concurrently with the input-gradient chain: their
+# blocks fill the CUs the chain's N = 768 GEMM rounds, attention tails and latency-bound LayerNorm /
+# reduction launches leave idle (the backward counterpart of the teacher-forward stream).  Only
+# gradients written into bucket sinks move (autograd never reads them); the backward's exit joins the
+# side stream, and GradOut.done() joins it before a bucket's collective is launched.
+_WGRAD_SIDE = [None]
+# which weight gradients move: "all" (encoder layers + conv frontend) or "conv" (DPH_WGRAD_SCOPE)
+_WGRAD_SCOPE = os.environ.get("DPH_WGRAD_SCOPE", "conv")
+
+
+class wgrad_overlap:
+    """Inside the block (one backward), sink-bound weight-gradient GEMMs launch on ``stream``; GEMMs of the
+    main stream take one tile per block meanwhile (a persistent grid would wait for CUs the side stream
+    holds).  Exit: the main stream waits for the side stream."""
+
+    def __init__(self, stream):
+        self.stream = stream
+        share = _WGRAD_SCOPE == "all" and os.environ.get("DPH_WGRAD_PERSIST", "0") != "1"
+        self.shared = K.shared_gpu() if share else contextlib.nullcontext()
+
+    def __enter__(self):
+        if self.stream is not None:
+            self.prev, _WGRAD_SIDE[0] = _WGRAD_SIDE[0], self.stream
+            self.shared.__enter__()
+        return self
+
+    def __exit__(self, *exc):
+        if self.stream is not None:
+            _WGRAD_SIDE[0] = self.prev
+            self.shared.__exit__(*exc)
+            torch.cuda.current_stream().wait_stream(self.stream)
+
+
+class wgrad_side:
+    """Run the block on the weight-gradient side stream when one is active and ``enable`` (the output is a
+    bucket sink): forked from the main stream, and every tensor in ``inputs`` marked as used by the side
+    stream (the caching allocator then keeps it until the side stream's work is done)."""
+
+    def __init__(self, *inputs, enable: bool = True, scope: str = "enc"):
+        self.inputs = inputs
+        self.side = _WGRAD_SIDE[0] if (enable and (_WGRAD_SCOPE == "all" or scope == _WGRAD_SCOPE)) else None
+
+    def __enter__(self):
+        if self.side is not None:
+            self.side.wait_stream(torch.cuda.current_stream())
+            self.ctx = torch.cuda.stream(self.side)
+            self.ctx.__enter__()
+        return self
+
+    def __exit__(self, *exc):
+        if self.side is not None:
+            self.ctx.__exit__(*exc)
+            for t in self.inputs:
+                if t is not None:
+                    t.record_stream(self.side)
+
+
+# ---------------------------------------------------------------------------
 # gradient sinks: weight gradients written straight into the data-parallel buckets
 # ---------------------------------------------------------------------------
 def _sink_view(params) -> Optional[torch.Tensor]:
@@ -422,6 +484,11 @@ class GradOut:
         return self.bufs.get(id(p))
 
     def done(self):
+        side = _WGRAD_SIDE[0]
+        if side is not None and self.sunk_params:
+            red = getattr(self.sunk_params[0]._dph_sink_ready, "__self__", None)
+            if red is not None and red.enabled and red.sync:
+                torch.cuda.current_stream().wait_stream(side)   # the bucket's collective reads these gradients
         for p in self.sunk_params:
             p._dph_sink_ready(p)
 
@@ -821,14 +888,16 @@ class FrontendFn(torch.autograd.Function):
             Cinp = pad8(Cin)
             M = B * Ls[i]
             # weight gradient (packed [O][k*Cinp]) -> [O][Cin][k]
-            dwp = torch.empty(O, k * Cinp, dtype=F32, device=dev)
-            A = K.mat(dz, row_stride=Op)
-            Bm = K.mat(ctx.ys[i - 1], row_stride=s * Cinp, rows_per_batch=Ls[i], batch_stride=Ls[i - 1] * Cinp)
-            splits = K.choose_splits(O, k * Cinp, M)
-            keep.append(K.gemm(A, Bm, K.dense(dwp), O, k * Cinp, M, a_kcontig=False, b_kcontig=False,
-                               c_dtype=K.OUT_F32, splits=splits, device=dev))
             dw, direct = go.buf(pws[i], zero=False)
-            call("dph_conv_weight_unpack_grad", ptr(dwp), ptr(dw), O, Cin, k, Cinp, int(direct), _s())
+            with wgrad_side(dz, ctx.ys[i - 1], enable=direct, scope="conv"):
+                dwp = torch.empty(O, k * Cinp, dtype=F32, device=dev)
+                A = K.mat(dz, row_stride=Op)
+                Bm = K.mat(ctx.ys[i - 1], row_stride=s * Cinp, rows_per_batch=Ls[i], batch_stride=Ls[i - 1] * Cinp)
+                splits = K.choose_splits(O, k * Cinp, M)
+                keep.append(K.gemm(A, Bm, K.dense(dwp), O, k * Cinp, M, a_kcontig=False, b_kcontig=False,
+                                   c_dtype=K.OUT_F32, splits=splits, device=dev))
+                call("dph_conv_weight_unpack_grad", ptr(dwp), ptr(dw), O, Cin, k, Cinp, int(direct), _s())
+                keep.append(dwp)
             # input gradient, fused with the previous layer's GELU/mask backward (i > 1): phase GEMMs
             # writing d_in in place, or the column gradient + col2im for other conv geometries
             wt = t_image(ctx.imgs[i])     # [k*Cinp][Op]: both operands k-contiguous -> ring kernels
@@ -1413,14 +1482,16 @@ class EncoderLayerFn(torch.autograd.Function):
                  ptr(sv["y_pre"]) if has_lmf else None, ptr(g["lmf"]), _s())
             F_ = sv["F"]
             dw2, direct = go.buf(pr["w2"], zero=False)
-            k1 = K.linear_wgrad(dy, sv["f"], dw2, accumulate=direct, k_in=F_)
+            with wgrad_side(dy, sv["f"], enable=direct):
+                k1 = K.linear_wgrad(dy, sv["f"], dw2, accumulate=direct, k_in=F_)
             db1, _ = go.buf(pr["b1"])
             g["im"] = z(F_) if has_im else None
             du = K.linear_dgrad(dy, sv["W2"], w_t=t_image(sv["W2"]), act=K.ACT_GELU_BWD, aux_in=sv["u"], colmask=sv["imp"], colsum_out=db1,
                                 colsum_aux=g["im"] if has_im else z(F_), dropout_p=cfg["p_interm"],
                                 seed=sv["seed_i"], colsum_n=F_)
             dw1, direct = go.buf(pr["w1"], zero=False)
-            k2 = K.linear_wgrad(du, xn2, dw1, accumulate=direct, n_out=F_)
+            with wgrad_side(du, xn2, enable=direct):
+                k2 = K.linear_wgrad(du, xn2, dw1, accumulate=direct, n_out=F_)
             dxn2 = K.linear_dgrad(du, sv["W1"], w_t=t_image(sv["W1"]))
             ds1 = torch.empty_like(dout)
             dln2w, _ = go.buf(pr["ln2_w"])
@@ -1439,7 +1510,8 @@ class EncoderLayerFn(torch.autograd.Function):
             call("dph_branch_bwd", ptr(ds1), ptr(da), M, D, cfg["p_drop"], sv["seed_d"], ptr(lma), None, 0, ptr(dbo),
                  ptr(sv["a_pre"]) if has_lma else None, ptr(g["lma"]), _s())
             dwo, direct = go.buf(pr["wo"], zero=False)
-            k3 = K.linear_wgrad(da, sv["o_m"], dwo, accumulate=direct)
+            with wgrad_side(da, sv["o_m"], enable=direct):
+                k3 = K.linear_wgrad(da, sv["o_m"], dwo, accumulate=direct)
             do_m = K.linear_dgrad(da, sv["Wo"], w_t=t_image(sv["Wo"]))
             Dvec = torch.empty(B * H * T, dtype=F32, device=dev)
             g["hm"] = z(H) if has_hm else None
@@ -1449,7 +1521,8 @@ class EncoderLayerFn(torch.autograd.Function):
             dbqkv, _ = go.buf(pr["bq"], pr["bk"], pr["bv"])
             call("dph_colsum", ptr(dqkv), ptr(dbqkv), M, dqkv.shape[1], *colsum_ws(M, dqkv.shape[1], dev), _s())
             dwqkv, direct = go.buf(pr["wq"], pr["wk"], pr["wv"], zero=False)
-            k4 = K.linear_wgrad(dqkv, xn1, dwqkv, accumulate=direct)
+            with wgrad_side(dqkv, xn1, enable=direct):
+                k4 = K.linear_wgrad(dqkv, xn1, dwqkv, accumulate=direct)
             dxn1 = K.linear_dgrad(dqkv, sv["Wqkv"], w_t=t_image(sv["Wqkv"]))
             EncoderLayerFn._gate_bwd(ctx, cfg, xn1, dxn1, wl_g, go)
             dh = torch.empty_like(dout)
@@ -1566,14 +1639,16 @@ class EncoderLayerFn(torch.autograd.Function):
                  ptr(sv["y_pre"]), ptr(g["lmf"]), *ln_ws(M, D, dev), _s())
             F_ = sv["F"]
             dw2, direct = go.buf(pr["w2"], zero=False)
-            k1 = K.linear_wgrad(dy, sv["f"], dw2, accumulate=direct, k_in=F_)
+            with wgrad_side(dy, sv["f"], enable=direct):
+                k1 = K.linear_wgrad(dy, sv["f"], dw2, accumulate=direct, k_in=F_)
             db1, _ = go.buf(pr["b1"])
             g["im"] = z(F_) if has_im else None
             du = K.linear_dgrad(dy, sv["W2"], w_t=t_image(sv["W2"]), act=K.ACT_GELU_BWD, aux_in=sv["u"], colmask=sv["imp"], colsum_out=db1,
                                 colsum_aux=g["im"] if has_im else z(F_), dropout_p=cfg["p_interm"],
                                 seed=sv["seed_i"], colsum_n=F_)
             dw1, direct = go.buf(pr["w1"], zero=False)
-            k2 = K.linear_wgrad(du, h1, dw1, accumulate=direct, n_out=F_)
+            with wgrad_side(du, h1, enable=direct):
+                k2 = K.linear_wgrad(du, h1, dw1, accumulate=direct, n_out=F_)
             dh1 = K.linear_dgrad(du, sv["W1"], w_t=t_image(sv["W1"]), residual=ds2)
             del k1, k2
         else:
@@ -1593,7 +1668,8 @@ class EncoderLayerFn(torch.autograd.Function):
                  ptr(dln1w), ptr(dln1b), M, D, 0.0, 0, ptr(da), cfg["p_drop"], sv["seed_d"], ptr(lma), ptr(dbo),
                  ptr(sv["a_pre"]), ptr(g["lma"]), *ln_ws(M, D, dev), _s())
             dwo, direct = go.buf(pr["wo"], zero=False)
-            k3 = K.linear_wgrad(da, sv["o_m"], dwo, accumulate=direct)
+            with wgrad_side(da, sv["o_m"], enable=direct):
+                k3 = K.linear_wgrad(da, sv["o_m"], dwo, accumulate=direct)
             do_m = K.linear_dgrad(da, sv["Wo"], w_t=t_image(sv["Wo"]))
             Dvec = torch.empty(B * H * T, dtype=F32, device=dev)
             g["hm"] = z(H) if has_hm else None
@@ -1603,7 +1679,8 @@ class EncoderLayerFn(torch.autograd.Function):
             dbqkv, _ = go.buf(pr["bq"], pr["bk"], pr["bv"])
             call("dph_colsum", ptr(dqkv), ptr(dbqkv), M, dqkv.shape[1], *colsum_ws(M, dqkv.shape[1], dev), _s())
             dwqkv, direct = go.buf(pr["wq"], pr["wk"], pr["wv"], zero=False)
-            k4 = K.linear_wgrad(dqkv, h, dwqkv, accumulate=direct)
+            with wgrad_side(dqkv, h, enable=direct):
+                k4 = K.linear_wgrad(dqkv, h, dwqkv, accumulate=direct)
             dh = K.linear_dgrad(dqkv, sv["Wqkv"], w_t=t_image(sv["Wqkv"]), residual=ds1)
             EncoderLayerFn._gate_bwd(ctx, cfg, h, dh, wl_g, go)
             del k3, k4
