@@ -367,6 +367,206 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(const bf16_t* __restri
 }
 
 // ---------------------------------------------------------------------------
+// forward on v_mfma_f32_32x32x16_bf16 (HuBERT / wav2vec2: no relative-position bias).  Each wave owns 32
+// query rows as the N side of S^T = K Q'^T (a 32 x 32 accumulator: lane l holds query q = l & 31 and keys
+// 8 (r >> 2) + 4 (l >> 5) + (r & 3) of a 32-key subtile), so a row's softmax is in-lane plus one
+// exchange with lane l ^ 32.  The P accumulator registers 8e..8e+7 ARE the B operand of the k-step e of
+// O^T += V^T P^T once the k index is read as that key permutation; the V^T A operand follows it with
+// two transposed LDS reads (rows base + 4 hi + 0..3 and base + 8 + 4 hi + 0..3).  Against the 16 x 16 x 32
+// form: the same MFMA cycles, 16 instead of 24 KB of LDS fragment reads per wave and 64-key tile (V is
+// read once, not once per 16-row group), half the MFMA instructions.
+// LDS: K rows of 128 B with 16-B chunk c at position c ^ ((r >> 1) & 7) (the 32 rows x 2 chunks of a
+// b128 K-fragment read are bank-conflict free), V in the swz128 image of the transposed reads.
+// ---------------------------------------------------------------------------
+typedef __attribute__((ext_vector_type(16))) float f32x16_t;
+
+__device__ __forceinline__ int kswz(int r, int chunk) { return r * 128 + ((chunk ^ ((r >> 1) & 7)) << 4); }
+
+__device__ __forceinline__ bf16x8_t pack8(const f32x16_t& a, int base) {
+  uint4 w;
+  w.x = pack2bf(a[base + 0], a[base + 1]);
+  w.y = pack2bf(a[base + 2], a[base + 3]);
+  w.z = pack2bf(a[base + 4], a[base + 5]);
+  w.w = pack2bf(a[base + 6], a[base + 7]);
+  return __builtin_bit_cast(bf16x8_t, w);
+}
+
+template <bool DROP>
+__global__ void __launch_bounds__(256, 2) attn_fwd32_kernel(const bf16_t* __restrict__ qkv, float* __restrict__ o_u,
+                                                           bf16_t* __restrict__ o_m, float* __restrict__ lse,
+                                                           const float* __restrict__ head_mask,
+                                                           const int64_t* __restrict__ key_len, AttnShape sh,
+                                                           float scale, float drop_p, uint64_t seed,
+                                                           uint16_t* __restrict__ keep_out) {
+  seed = epoch_seed(seed);
+  const uint32_t mix = seed_mix(seed);
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE_SWZ_BYTES];   // [buf][K | V][64 rows x 128 B]
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int hi = lane >> 5;
+  const int b = blockIdx.z;
+  const int h = blockIdx.y;
+  const int T32 = (int)sh.T, H = (int)sh.H;
+  const int64_t RS = sh.RS;
+  const int q = (int)blockIdx.x * RB + wave * 32 + (lane & 31);
+  const bf16_t* rowbase = qkv + (int64_t)b * sh.T * RS;
+  const int klen = (int)(key_len ? key_len[b] : sh.T);
+  const uint32_t half_tp = (uint32_t)(T32 + 1) >> 1;
+  const uint32_t hrow = ((uint32_t)(b * H + h) * (uint32_t)T32 + (uint32_t)q) * half_tp;
+  // Q' = scale * q as the B operand: qf[t] = Q'[q][16 t + 8 hi + 0..7]
+  bf16x8_t qf[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (q < T32) v = *reinterpret_cast<const uint4*>(rowbase + (int64_t)q * RS + h * HD + 16 * t + 8 * hi);
+    qf[t] = __builtin_bit_cast(bf16x8_t, scale_bf16x8(v, scale));
+  }
+  f32x16_t oacc[2];
+#pragma unroll
+  for (int d = 0; d < 2; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) oacc[d][r] = 0.f;
+  float m_run = -INFINITY, l_run = 0.f;
+  const float inv_keep = DROP ? 1.f / (1.f - drop_p) : 1.f;
+  const uint32_t thr = drop_thr(drop_p);
+  const int nkt = (T32 + KT - 1) / KT;
+  uint4 rk[2], rv[2];
+  auto ldsK = [&](int buf) { return smem + buf * 2 * TILE_SWZ_BYTES; };
+  auto ldsV = [&](int buf) { return smem + buf * 2 * TILE_SWZ_BYTES + TILE_SWZ_BYTES; };
+  auto store_kv = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + 256 * i;
+      const int r = c >> 3;
+      *reinterpret_cast<uint4*>(ldsK(buf) + kswz(r, c & 7)) = rk[i];
+      *reinterpret_cast<uint4*>(ldsV(buf) + swz128(r, (c & 7) * 8)) = rv[i];
+    }
+  };
+  stage_load<KT, false>(rk, rowbase + (H + h) * HD, 0, sh.T, RS, 1.0f, tid);
+  stage_load<KT, true>(rv, rowbase + (2 * H + h) * HD, 0, sh.T, RS, 1.0f, tid);
+  store_kv(0);
+  __syncthreads();
+
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int cur = kt & 1;
+    const bool more = kt + 1 < nkt;
+    if (more) {
+      stage_load<KT, false>(rk, rowbase + (H + h) * HD, (int64_t)(kt + 1) * KT, sh.T, RS, 1.0f, tid);
+      stage_load<KT, true>(rv, rowbase + (2 * H + h) * HD, (int64_t)(kt + 1) * KT, sh.T, RS, 1.0f, tid);
+    }
+    const char* K_ = ldsK(cur);
+    const char* V_ = ldsV(cur);
+    f32x16_t sacc[2];
+#pragma unroll
+    for (int k2 = 0; k2 < 2; ++k2) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sacc[k2][r] = 0.f;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const bf16x8_t kf = lds_b128(K_, kswz(32 * k2 + (lane & 31), 2 * t + hi));
+        sacc[k2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[t], sacc[k2], 0, 0, 0);
+      }
+    }
+    const int kb = kt * KT + 4 * hi;   // key of (k2 = 0, r = 0) in this lane
+    auto tile = [&](auto masked_c) {
+      constexpr bool MASKED = decltype(masked_c)::value;
+      float mt = -INFINITY;
+#pragma unroll
+      for (int k2 = 0; k2 < 2; ++k2)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float v = sacc[k2][r];
+          if constexpr (MASKED) {
+            const int key = kb + 32 * k2 + 8 * (r >> 2) + (r & 3);
+            v = key >= klen ? v - 10000.0f : v;
+            v = key >= T32 ? -INFINITY : v;
+          }
+          sacc[k2][r] = v;
+          mt = fmaxf(mt, v);
+        }
+      mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+      const float m_new = fmaxf(m_run, mt);
+      const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * L2E);
+      const float ml = m_new * L2E;
+      float ls = 0.f;
+      uint32_t kw[2] = {0u, 0u};   // stored keep words hi and 2 + hi of this row and tile
+#pragma unroll
+      for (int k2 = 0; k2 < 2; ++k2)
+#pragma unroll
+        for (int rq = 0; rq < 4; ++rq) {
+          uint32_t hb[2] = {0u, 0u};
+          if constexpr (DROP) {
+            const uint32_t pr = hrow + (uint32_t)((kb + 32 * k2 + 8 * rq) >> 1);
+            hb[0] = attn_hash32(mix, pr);
+            hb[1] = attn_hash32(mix, pr + 1);
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int r = 4 * rq + i;
+            const float p = __builtin_amdgcn_exp2f(fmaf(sacc[k2][r], L2E, -ml));
+            ls += p;
+            if constexpr (DROP) {
+              const bool keep = ((i & 1) ? (hb[i >> 1] >> 16) : (hb[i >> 1] & 0xffffu)) >= thr;
+              kw[rq & 1] |= (keep ? 1u : 0u) << (4 * (2 * k2 + (rq >> 1)) + i);
+              sacc[k2][r] = keep ? p * inv_keep : 0.f;
+            } else {
+              sacc[k2][r] = p;
+            }
+          }
+        }
+      if constexpr (DROP) {
+        if (keep_out != nullptr && q < T32) {
+          uint16_t* kp = keep_out + ((int64_t)(b * H + h) * T32 + q) * (nkt * 4) + kt * 4;
+          kp[hi] = (uint16_t)kw[0];
+          kp[2 + hi] = (uint16_t)kw[1];
+        }
+      }
+      ls += __shfl_xor(ls, 32, 64);
+      l_run = l_run * alpha + ls;
+      m_run = m_new;
+#pragma unroll
+      for (int d = 0; d < 2; ++d)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) oacc[d][r] *= alpha;
+#pragma unroll
+      for (int k2 = 0; k2 < 2; ++k2)
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const bf16x8_t pf = pack8(sacc[k2], 8 * e);
+          const int base = 32 * k2 + 16 * e + 4 * hi;
+#pragma unroll
+          for (int d = 0; d < 2; ++d) {
+            const bf16x8_t vf = tr_frag(V_, base, base + 8, 32 * d + 16 * ((lane >> 4) & 1), lane);
+            oacc[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, oacc[d], 0, 0, 0);
+          }
+        }
+    };
+    if ((kt + 1) * KT <= klen && (kt + 1) * KT <= T32) tile(std::integral_constant<bool, false>());
+    else tile(std::integral_constant<bool, true>());
+    if (more) store_kv(cur ^ 1);
+    __syncthreads();
+  }
+
+  if (q >= T32) return;
+  const float hm = head_mask ? head_mask[h] : 1.0f;
+  const float inv_l = 1.0f / l_run;
+  const int64_t obase = ((int64_t)b * T32 + q) * (H * HD) + h * HD;
+#pragma unroll
+  for (int d = 0; d < 2; ++d)
+#pragma unroll
+    for (int rq = 0; rq < 4; ++rq) {
+      const int col = 32 * d + 8 * rq + 4 * hi;
+      float v[4] = {oacc[d][4 * rq] * inv_l, oacc[d][4 * rq + 1] * inv_l, oacc[d][4 * rq + 2] * inv_l,
+                    oacc[d][4 * rq + 3] * inv_l};
+      *reinterpret_cast<float4*>(o_u + obase + col) = make_float4(v[0], v[1], v[2], v[3]);
+      *reinterpret_cast<uint2*>(o_m + obase + col) =
+          make_uint2(pack2bf(v[0] * hm, v[1] * hm), pack2bf(v[2] * hm, v[3] * hm));
+    }
+  if (hi == 0) lse[(int64_t)(b * H + h) * T32 + q] = m_run + __logf(l_run);
+}
+
+// ---------------------------------------------------------------------------
 // backward prep: rowdot[b][h][t] = sum_d dO_m * O_u ; D = hm * rowdot ; dhm[h] += sum rowdot
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) attn_bwd_prep_kernel(const bf16_t* __restrict__ dom,
@@ -914,9 +1114,24 @@ using namespace dph;
 
 namespace {
 
+// DPH_ATTN_FWD=2: the 16 x 16 x 32 forward (two waves per SIMD) for every shape (A/B)
+// DPH_ATTN_FWD=2: the 16 x 16 x 32 forward for every shape (A/B; the WavLM bias always takes it).  Measured
+// and dropped: the 32 x 32 x 16 forward at three waves per SIMD (K / V by LDS-DMA, Q' staged in LDS, 168
+// VGPRs with 14-20 spilled) ran 46 / 58 us against 38 / 51 us at two waves per SIMD.
+static bool fwd32_enabled() {
+  const char* e = getenv("DPH_ATTN_FWD");
+  return !(e && e[0] == '2');
+}
+
 template <bool DROP, bool BIAS>
 void launch_fwd(dim3 grid, hipStream_t stream, const void* qkv, void* o_u, void* o_m, float* lse, const float* hm,
                 const int64_t* key_len, AttnShape sh, float scale, float p, uint64_t seed, RelBias rb, void* keep) {
+  if (!BIAS && fwd32_enabled()) {
+    hipLaunchKernelGGL((attn_fwd32_kernel<DROP>), grid, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(qkv),
+                       reinterpret_cast<float*>(o_u), reinterpret_cast<bf16_t*>(o_m), lse, hm, key_len, sh, scale, p,
+                       seed, reinterpret_cast<uint16_t*>(keep));
+    return;
+  }
   const size_t tw_bytes = BIAS ? (size_t)(sh.T + RB - 1) * sizeof(float) : 0;
   hipLaunchKernelGGL((attn_fwd_kernel<DROP, BIAS>), grid, dim3(256), tw_bytes, stream, reinterpret_cast<const bf16_t*>(qkv),
                      reinterpret_cast<float*>(o_u), reinterpret_cast<bf16_t*>(o_m), lse, hm, key_len, sh, scale, p,
