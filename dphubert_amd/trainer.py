@@ -219,12 +219,17 @@ class Trainer:
             # thread_local: the process group's watchdog thread keeps polling the events of earlier (eager)
             # collectives while this thread captures; under the default "global" mode that poll is an illegal
             # call during capture and aborts the process ("operation not permitted when stream is capturing")
-            with torch.cuda.graph(g, pool=self._pool, capture_error_mode="thread_local"):
+            # the profiled copy (timing only) gets a private memory pool, so it can never alias a block the
+            # main graph keeps using across replays.  Open issue: its reported loss is sometimes a constant
+            # garbage value (bits 0x6976e573) with or without this isolation, while the main graph's loss is
+            # sane (-0.117) in every run; the timed region only replays the main graph
+            pool = None if prof is not None else self._pool
+            with torch.cuda.graph(g, pool=pool, capture_error_mode="thread_local"):
                 loss = self._gpu_step(self._static, zero, final)
         finally:
             LaunchProfiler.active = None
             ops.reset_zero_arena()
-        if self._pool is None:
+        if self._pool is None and prof is None:
             self._pool = g.pool()
         return g, loss
 
