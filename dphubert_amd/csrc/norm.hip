@@ -11,9 +11,18 @@ namespace dph {
 namespace {
 
 constexpr int LN_MAXV = 4;   // up to 4 x (64 lanes x 4 elements) = 1024 columns
-constexpr int LN_FWD_RPW = 2;   // rows per wave, forward (both rows' loads issued before any math)
-constexpr int LN_BWD_RPW = 2;   // rows per wave, backward
-constexpr int LN_BWD_WAVES = 8; // 512-thread backward blocks: 16 rows share one LDS column reduction
+#ifndef DPH_LN_FWD_RPW
+#define DPH_LN_FWD_RPW 2
+#endif
+#ifndef DPH_LN_BWD_RPW
+#define DPH_LN_BWD_RPW 2
+#endif
+#ifndef DPH_LN_BWD_WAVES
+#define DPH_LN_BWD_WAVES 8
+#endif
+constexpr int LN_FWD_RPW = DPH_LN_FWD_RPW;     // rows per wave, forward (all rows' loads issued before any math)
+constexpr int LN_BWD_RPW = DPH_LN_BWD_RPW;     // rows per wave, backward
+constexpr int LN_BWD_WAVES = DPH_LN_BWD_WAVES; // backward block: LN_BWD_WAVES x LN_BWD_RPW rows share one column reduction
 
 __device__ __forceinline__ void unpack4(uint2 r, float (&o)[4]) {
   o[0] = __uint_as_float(r.x << 16);
