@@ -376,11 +376,29 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(const bf16_t* __restri
 // form: the same MFMA cycles, 16 instead of 24 KB of LDS fragment reads per wave and 64-key tile (V is
 // read once, not once per 16-row group), half the MFMA instructions.
 // LDS: K rows of 128 B with 16-B chunk c at position c ^ ((r >> 1) & 7) (the 32 rows x 2 chunks of a
-// b128 K-fragment read are bank-conflict free), V in the swz128 image of the transposed reads.
+// b128 K-fragment read are bank-conflict free), V in the vswz image of its transposed reads.
 // ---------------------------------------------------------------------------
 typedef __attribute__((ext_vector_type(16))) float f32x16_t;
 
 __device__ __forceinline__ int kswz(int r, int chunk) { return r * 128 + ((chunk ^ ((r >> 1) & 7)) << 4); }
+
+// V image of the 32 x 32 forward: 32-B unit u of row r at u ^ (2 ((r >> 1) & 1)).  A transposed A-operand read
+// puts, per half-wave, rows r0..r0+3 (r0 % 4 == 0) x units {2d, 2d+1} in one LDS cycle: these 8 segments land
+// on 8 distinct (row parity, unit) bank groups.  (swz128, the 16 x 16 kernels' image, maps two of them onto
+// one group: 65 % of the LDS cycles were conflict cycles, SQ_LDS_BANK_CONFLICT.)
+__device__ __forceinline__ int vswz(int r, int col) {
+  return r * 128 + ((((col >> 4) ^ (((r >> 1) & 1) << 1)) & 3) * 32) + (col & 15) * 2;
+}
+
+__device__ __forceinline__ bf16x8_t tr_frag_v(const char* lds, int r0, int r1, int c0, int lane) {
+  const int i = lane & 15;
+  const int q = i >> 2;
+  const int p = i & 3;
+  s16x4_t v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + vswz(r0 + q, c0 + 4 * p)));
+  s16x4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + vswz(r1 + q, c0 + 4 * p)));
+  s16x8_t v = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+  return __builtin_bit_cast(bf16x8_t, v);
+}
 
 __device__ __forceinline__ bf16x8_t pack8(const f32x16_t& a, int base) {
   uint4 w;
@@ -440,7 +458,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd32_kernel(const bf16_t* __rest
       const int c = tid + 256 * i;
       const int r = c >> 3;
       *reinterpret_cast<uint4*>(ldsK(buf) + kswz(r, c & 7)) = rk[i];
-      *reinterpret_cast<uint4*>(ldsV(buf) + swz128(r, (c & 7) * 8)) = rv[i];
+      *reinterpret_cast<uint4*>(ldsV(buf) + vswz(r, (c & 7) * 8)) = rv[i];
     }
   };
   stage_load<KT, false>(rk, rowbase + (H + h) * HD, 0, sh.T, RS, 1.0f, tid);
@@ -537,7 +555,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd32_kernel(const bf16_t* __rest
           const int base = 32 * k2 + 16 * e + 4 * hi;
 #pragma unroll
           for (int d = 0; d < 2; ++d) {
-            const bf16x8_t vf = tr_frag(V_, base, base + 8, 32 * d + 16 * ((lane >> 4) & 1), lane);
+            const bf16x8_t vf = tr_frag_v(V_, base, base + 8, 32 * d + 16 * ((lane >> 4) & 1), lane);
             oacc[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, oacc[d], 0, 0, 0);
           }
         }
