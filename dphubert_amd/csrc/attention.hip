@@ -379,6 +379,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(const bf16_t* __restri
 // b128 K-fragment read are bank-conflict free), V in the vswz image of its transposed reads.
 // ---------------------------------------------------------------------------
 typedef __attribute__((ext_vector_type(16))) float f32x16_t;
+constexpr float RESCALE_TH = 8.0f;   // deferred-max threshold of the 32 x 32 forward (score units)
 
 __device__ __forceinline__ int kswz(int r, int chunk) { return r * 128 + ((chunk ^ ((r >> 1) & 7)) << 4); }
 
@@ -504,9 +505,21 @@ __global__ void __launch_bounds__(256, 2) attn_fwd32_kernel(const bf16_t* __rest
           mt = fmaxf(mt, v);
         }
       mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-      const float m_new = fmaxf(m_run, mt);
-      const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * L2E);
-      const float ml = m_new * L2E;
+      // deferred rescale: the running max moves only when a row's tile max exceeds it by more than
+      // RESCALE_TH (p <= e^8 meanwhile: no overflow, the same relative bf16 rounding), and the 32 O
+      // rescale multiplies run only when some row of the wave moved (wave-uniform branch)
+      const bool move = mt > m_run + RESCALE_TH;
+      if (__any(move)) {
+        const float m_new = move ? mt : m_run;
+        const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * L2E);
+        l_run *= alpha;
+        m_run = m_new;
+#pragma unroll
+        for (int d = 0; d < 2; ++d)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) oacc[d][r] *= alpha;
+      }
+      const float ml = m_run * L2E;
       float ls = 0.f;
       uint32_t kw[2] = {0u, 0u};   // stored keep words hi and 2 + hi of this row and tile
 #pragma unroll
@@ -527,7 +540,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd32_kernel(const bf16_t* __rest
             if constexpr (DROP) {
               const bool keep = ((i & 1) ? (hb[i >> 1] >> 16) : (hb[i >> 1] & 0xffffu)) >= thr;
               kw[rq & 1] |= (keep ? 1u : 0u) << (4 * (2 * k2 + (rq >> 1)) + i);
-              sacc[k2][r] = keep ? p * inv_keep : 0.f;
+              sacc[k2][r] = keep ? p : 0.f;   // (1 / (1 - p) applied once to O at the end)
             } else {
               sacc[k2][r] = p;
             }
@@ -541,12 +554,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd32_kernel(const bf16_t* __rest
         }
       }
       ls += __shfl_xor(ls, 32, 64);
-      l_run = l_run * alpha + ls;
-      m_run = m_new;
-#pragma unroll
-      for (int d = 0; d < 2; ++d)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) oacc[d][r] *= alpha;
+      l_run += ls;
 #pragma unroll
       for (int k2 = 0; k2 < 2; ++k2)
 #pragma unroll
@@ -568,7 +576,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd32_kernel(const bf16_t* __rest
 
   if (q >= T32) return;
   const float hm = head_mask ? head_mask[h] : 1.0f;
-  const float inv_l = 1.0f / l_run;
+  const float inv_l = inv_keep / l_run;
   const int64_t obase = ((int64_t)b * T32 + q) * (H * HD) + h * HD;
 #pragma unroll
   for (int d = 0; d < 2; ++d)
