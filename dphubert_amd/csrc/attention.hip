@@ -480,11 +480,10 @@ __global__ void __launch_bounds__(256, 2) attn_fwd32_kernel(const bf16_t* __rest
 #pragma unroll
     for (int k2 = 0; k2 < 2; ++k2) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) sacc[k2][r] = 0.f;
-#pragma unroll
       for (int t = 0; t < 4; ++t) {
         const bf16x8_t kf = lds_b128(K_, kswz(32 * k2 + (lane & 31), 2 * t + hi));
-        sacc[k2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[t], sacc[k2], 0, 0, 0);
+        // (t = 0: the zero accumulator as the MFMA's inline-constant C operand, no register zeroing)
+        sacc[k2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[t], t == 0 ? f32x16_t{} : sacc[k2], 0, 0, 0);
       }
     }
     const int kb = kt * KT + 4 * hi;   // key of (k2 = 0, r = 0) in this lane
