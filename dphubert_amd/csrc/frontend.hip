@@ -153,25 +153,42 @@ __global__ void __launch_bounds__(256) conv0_stats_kernel(const float* __restric
   }
 }
 
-__global__ void conv0_stats_finalize(const float* __restrict__ ws, Conv0 p, int nch, float* __restrict__ mean,
-                                     float* __restrict__ rstd, float eps) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= p.B * p.C) return;
-  const int64_t b = i / p.C;
-  const int64_t c = i % p.C;
-  double n = 0.0, m = 0.0, M2 = 0.0;
-  for (int ch = 0; ch < nch; ++ch) {
-    const double nb = (double)min<int64_t>(STAT_CH, p.L0 - (int64_t)ch * STAT_CH);
-    const float* o = ws + ((b * nch + ch) * p.C + c) * 2;
-    const double mb = o[0], M2b = o[1];
-    const double nn = n + nb;
-    const double d = mb - m;
-    m += d * nb / nn;
-    M2 += M2b + d * d * n * nb / nn;
-    n = nn;
+// GroupNorm statistics of (b, c) from its per-chunk (mean, M2) pairs, in fp64 as shifted sums around the
+// first chunk's mean m0: S1 = sum n_b (m_b - m0), S2 = sum M2_b + n_b (m_b - m0)^2, mean = m0 + S1 / N,
+// M2 = S2 - S1^2 / N (no division per chunk).  A block is 64 channels of one utterance; its 4 waves take
+// every 4th chunk (coalesced 8-B reads along the channels) and are summed through LDS.  (The previous
+// thread-per-(b, c) Chan merge -- 32 blocks, a dependent fp64 division chain over ~125 chunks -- took
+// 48 us per launch.)
+__global__ void __launch_bounds__(256) conv0_stats_finalize(const float* __restrict__ ws, Conv0 p, int nch,
+                                                            float* __restrict__ mean, float* __restrict__ rstd,
+                                                            float eps) {
+  __shared__ double part[4][64][2];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int64_t b = blockIdx.y;
+  const int64_t c = (int64_t)blockIdx.x * 64 + lane;
+  const bool ok = c < p.C;
+  const double m0 = ok ? (double)ws[((b * nch) * p.C + c) * 2] : 0.0;
+  double s1 = 0.0, s2 = 0.0;
+  if (ok) {
+    for (int ch = wv; ch < nch; ch += 4) {
+      const double nb = (double)min<int64_t>(STAT_CH, p.L0 - (int64_t)ch * STAT_CH);
+      const float2 o = *reinterpret_cast<const float2*>(ws + ((b * nch + ch) * p.C + c) * 2);
+      const double d = (double)o.x - m0;
+      s1 = fma(nb, d, s1);
+      s2 += fma(nb * d, d, (double)o.y);
+    }
   }
-  mean[i] = (float)m;
-  rstd[i] = (float)(1.0 / sqrt(M2 / n + (double)eps));
+  part[wv][lane][0] = s1;
+  part[wv][lane][1] = s2;
+  __syncthreads();
+  if (wv != 0 || !ok) return;
+  s1 = part[0][lane][0] + part[1][lane][0] + part[2][lane][0] + part[3][lane][0];
+  s2 = part[0][lane][1] + part[1][lane][1] + part[2][lane][1] + part[3][lane][1];
+  const double N = (double)p.L0;
+  const double M2 = fmax(s2 - s1 * s1 / N, 0.0);
+  mean[b * p.C + c] = (float)(m0 + s1 / N);
+  rstd[b * p.C + c] = (float)(1.0 / sqrt(M2 / N + (double)eps));
 }
 
 template <bool GN>
@@ -634,7 +651,7 @@ extern "C" int dph_conv0_gn_fwd(const float* wave, int64_t B, int64_t S, const f
   const int nch = (int)cdiv(p.L0, STAT_CH);
   DPH_REQUIRE(ws_bytes >= (int64_t)B * nch * C * 2 * 4, "dph_conv0_gn_fwd: workspace too small");
   hipLaunchKernelGGL(conv0_stats_kernel, dim3(nch, (unsigned)B), dim3(256), 0, stream, wave, w, p, ws, nch);
-  hipLaunchKernelGGL(conv0_stats_finalize, dim3((unsigned)cdiv(B * C, 256)), dim3(256), 0, stream, ws, p, nch, mean,
+  hipLaunchKernelGGL(conv0_stats_finalize, dim3((unsigned)cdiv(C, 64), (unsigned)B), dim3(256), 0, stream, ws, p, nch, mean,
                      rstd, 1e-5f);
   hipLaunchKernelGGL(conv0_apply_kernel<true>, dim3((unsigned)cdiv(p.L0, APPLY_ROWS), (unsigned)B), dim3(256), 0,
                      stream, wave, w, (const float*)nullptr, p, gamma, beta, mask, mean, rstd,
