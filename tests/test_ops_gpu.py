@@ -524,3 +524,37 @@ def test_conv_dgrad_phases_match_column_path(monkeypatch):
         grads.append({n: p.grad.detach().float().cpu().clone() for n, p in fe.named_parameters() if p.grad is not None})
     for n in grads[0]:
         assert rel_l2(grads[0][n], grads[1][n]) < 1e-2, n
+
+
+@pytest.mark.parametrize("T,lens,p", [(499, None, 0.1), (499, None, 0.0), (131, [131, 97], 0.1)])
+def test_attention_bwd_merged_grid_matches_split(T, lens, p, monkeypatch):
+    """The dK/dV and dQ blocks launched as ONE grid (default) give bit-identical gradients to two separate
+    launches of the same bodies (DPH_ATTN_SPLIT=1), at the distill shape's T (several rounds of blocks)."""
+    from dphubert_amd import _lib
+    from dphubert_amd._lib import call, ptr
+    torch.manual_seed(8)
+    B, H = 16 if lens is None else 2, 12
+    D = H * 64
+    qkv = (torch.randn(B * T, 3 * D, device=DEV) * 0.5).to(torch.bfloat16)
+    g = torch.randn(B * T, D, device=DEV).to(torch.bfloat16)
+    hm = torch.rand(H, device=DEV)
+    ln = torch.tensor(lens, device=DEV, dtype=torch.int64) if lens else None
+    s = _lib.stream_ptr()
+    keep = torch.zeros(_lib.lib().dph_attention_keep_bytes(B, T, H) // 8, dtype=torch.int64, device=DEV)
+    o_u = torch.empty(B * T, D, device=DEV, dtype=torch.float32)
+    o_m = torch.empty(B * T, D, device=DEV, dtype=torch.bfloat16)
+    lse = torch.empty(B * H * T, device=DEV)
+    kb = keep if p > 0 else None
+    call("dph_attention_fwd", ptr(qkv), ptr(o_u), ptr(o_m), ptr(lse), ptr(hm), ptr(ln), B, T, H, 0.125, p, 5, ptr(kb), s)
+    Dv = torch.empty(B * H * T, device=DEV)
+    call("dph_attention_bwd_prep", ptr(g), ptr(o_u), ptr(hm), ptr(Dv), None, B, T, H, s)
+    outs = []
+    for split in ("0", "1"):
+        monkeypatch.setenv("DPH_ATTN_SPLIT", split)
+        dqkv = torch.full_like(qkv, float("nan"))
+        call("dph_attention_bwd", ptr(qkv), ptr(g), ptr(hm), ptr(lse), ptr(Dv), ptr(dqkv), ptr(ln), B, T, H, 0.125, p,
+             5, ptr(kb), s)
+        torch.cuda.synchronize()
+        outs.append(dqkv)
+    assert torch.isfinite(outs[0].float()).all()
+    assert torch.equal(outs[0], outs[1])
