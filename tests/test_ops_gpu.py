@@ -39,15 +39,20 @@ def _model(cfg, seed=0):
     return m.to(DEV), sd
 
 
-def test_attention_kernel_vs_torch():
+@pytest.mark.parametrize("fwd", ["1", "2"])           # 32x32x16 forward (default) / 16x16x32 forward
+@pytest.mark.parametrize("T,short,amp", [(131, 97, 0.5), (499, 311, 0.5), (499, 499, 3.0)])
+def test_attention_kernel_vs_torch(fwd, T, short, amp, monkeypatch):
+    """amp = 3: scores spread over ~+-40, so row maxima jump by more than the deferred-rescale threshold
+    between key tiles of the 32x32 forward."""
     from dphubert_amd import _lib
     from dphubert_amd._lib import call, ptr
+    monkeypatch.setenv("DPH_ATTN_FWD", fwd)
     torch.manual_seed(0)
-    B, T, H = 2, 131, 3
+    B, H = 2, 3
     D = H * 64
-    qkv = (torch.randn(B * T, 3 * D, device=DEV) * 0.5).to(torch.bfloat16)
+    qkv = (torch.randn(B * T, 3 * D, device=DEV) * amp).to(torch.bfloat16)
     hm = torch.rand(H, device=DEV)
-    lens = torch.tensor([T, 97], device=DEV, dtype=torch.int64)
+    lens = torch.tensor([T, short], device=DEV, dtype=torch.int64)
     o_u = torch.empty(B * T, D, device=DEV, dtype=torch.float32)
     o_m = torch.empty(o_u.shape, device=o_u.device, dtype=torch.bfloat16)
     lse = torch.empty(B * H * T, device=DEV)
