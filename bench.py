@@ -277,6 +277,10 @@ def main():
     log(f"host enqueue {t_host / args.steps * 1e3:.2f} ms/step")
     log(f"loss {loss.item():.5f}  step {ms:.2f} ms  {value:.1f} audio-s/s  "
         f"({FLOP_PER_UTT_BASE * args.batch * args.seconds / 10 / (ms / 1e3) / 1e12:.0f} TFLOP/s algorithmic/GPU)")
+    if os.environ.get("DPH_BENCH_LOGGED") == "1":      # diagnostics: the last replayed graph's logged terms
+        terms = {k: (float(v.float().sum()) if torch.is_tensor(v) else v)
+                 for k, v in getattr(trainer.module, "logged", {}).items()}
+        log(f"logged terms: {terms}")
 
     fam = "WavLM-Base" if args.model == "wavlm-base" else "HuBERT-Base"
     utts = "10s utts" if batches is None else "bucketed 2-15.6s utts, 160 s/batch"
