@@ -742,6 +742,9 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(const DphGemmArgs a, int64_
 #ifndef DPH_ABLATE
 #define DPH_ABLATE 0        // timing ablations of the ring loop (tools/ablate_gemm.py); 0 = production
 #endif
+#ifndef DPH_MID8_MINB
+#define DPH_MID8_MINB 2     // blocks per CU of the 8-wave 128 x 128 tile (A/B builds: 1)
+#endif
 namespace ring {
 constexpr int KS = 32;      // k per slice
 constexpr int NSLOT = 4;
@@ -805,7 +808,8 @@ struct Cfg {
   static constexpr int LDS = PIPE > EPI ? PIPE : EPI;
   // blocks per CU (the 192-row tile: one, its shapes have about one tile per CU; the persistent loop needs
   // more than 256 registers for its 96 accumulators + two fragment sets)
-  static constexpr int MINB = (BM % 128 != 0 || (NW >= 8 && BM * BN > 128 * 128)) ? 1 : (BM * BN <= 128 * 64 ? 3 : 2);
+  static constexpr int MINB = (BM % 128 != 0 || (NW >= 8 && BM * BN > 128 * 128)) ? 1
+                             : (NW >= 8 && BM * BN == 128 * 128) ? DPH_MID8_MINB : (BM * BN <= 128 * 64 ? 3 : 2);
   // HIP's second __launch_bounds__ argument is the minimum number of WAVES PER SIMD (not blocks per CU):
   // MINB blocks of NW waves over the 4 SIMDs (caps the VGPRs at 512 / WPE)
   static constexpr int WPE = (MINB * NW + 3) / 4;
