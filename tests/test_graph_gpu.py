@@ -140,7 +140,9 @@ def test_graph_replay_matches_eager(family, accum):
     cat = lambda d: torch.cat([d[n].detach().float().flatten().cpu() for n in names])  # noqa: E731
     e_all = rel_l2(cat(pg), cat(pe[0]))
     base_all = max(rel_l2(cat(pe[i]), cat(pe[j])) for i, j in pairs)
-    assert e_all < max(1e-5, 4 * base_all), (e_all, base_all)
+    # (floor 1e-4: three eager runs under-estimate the atomic-order spread now and then -- 4.3x once at
+    # accum 3 -- while a stale or missing op in the replay moves the whole vector by > 1e-3)
+    assert e_all < max(1e-4, 4 * base_all), (e_all, base_all)
     # the graph replays follow the LR schedule: optimizer and scheduler state agree
     assert ea.optimizer._step == gr.optimizer._step
     for g1, g2 in zip(ea.optimizer.param_groups, gr.optimizer.param_groups):
