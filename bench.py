@@ -135,6 +135,34 @@ def pmc_traffic(args):
     return out
 
 
+def check_step(loss: float, terms, main_loss):
+    """Refuse to report a throughput measured on a corrupted step: the last timed step's loss must be finite and
+    its logged terms (lightning.py:277-295) self-consistent -- L1 = mean|s - t| > 0, the cosine term in [-1, 1],
+    loss = distill + reg, expected sparsity in [0, 1] -- and, when the last step replayed the profiled graph, its
+    loss must lie near the main graph's (the two replay the same step; the losses differ only by the step's own
+    dropout / HardConcrete draws, |diff| well below 1)."""
+    import math
+    bad = []
+    if not math.isfinite(loss):
+        bad.append(f"loss {loss}")
+    if terms:
+        l1, cos = terms.get("train_loss_l1"), terms.get("train_loss_cos")
+        dist_, reg = terms.get("train_loss_distill"), terms.get("train_loss_reg", 0.0)
+        es = terms.get("sparsity_expected")
+        if l1 is not None and not (0.0 < l1 < 1e3):
+            bad.append(f"l1 {l1}")
+        if cos is not None and not (-1.0 - 1e-5 <= cos <= 1.0 + 1e-5):
+            bad.append(f"cos {cos}")
+        if dist_ is not None and abs(terms.get("train_loss", loss) - (dist_ + reg)) > 1e-4 * max(1.0, abs(loss)):
+            bad.append(f"loss {terms.get('train_loss')} != distill {dist_} + reg {reg}")
+        if es is not None and not (-1e-6 <= es <= 1.0 + 1e-6):
+            bad.append(f"expected sparsity {es}")
+    if main_loss is not None and abs(loss - main_loss) > 0.5:
+        bad.append(f"last step loss {loss} vs main graph {main_loss}")
+    if bad:
+        raise SystemExit("bench.py: the measured step is corrupted: " + "; ".join(bad))
+
+
 def bucketed_batches(n: int, seconds_per_batch: float, rank: int, dev):
     """n batches shaped like distill.py's train loader (data.train_loader): 4000 synthetic utterance lengths
     uniform in 2-15.6 s (the loader's min_len / max_len), 1000 length buckets, a seconds_per_batch token
@@ -277,10 +305,14 @@ def main():
     log(f"host enqueue {t_host / args.steps * 1e3:.2f} ms/step")
     log(f"loss {loss.item():.5f}  step {ms:.2f} ms  {value:.1f} audio-s/s  "
         f"({FLOP_PER_UTT_BASE * args.batch * args.seconds / 10 / (ms / 1e3) / 1e12:.0f} TFLOP/s algorithmic/GPU)")
+    terms = {k: (float(v.float().sum()) if torch.is_tensor(v) else v)
+             for k, v in getattr(trainer.module, "logged", {}).items()}
     if os.environ.get("DPH_BENCH_LOGGED") == "1":      # diagnostics: the last replayed graph's logged terms
-        terms = {k: (float(v.float().sum()) if torch.is_tensor(v) else v)
-                 for k, v in getattr(trainer.module, "logged", {}).items()}
         log(f"logged terms: {terms}")
+    main_loss = None
+    if graphed and trainer._graphs.get((args.accum == 1, True)) is not None:
+        main_loss = trainer._graphs[(args.accum == 1, True)][1].item()     # the last main-graph replay
+    check_step(loss.item(), terms if (graphed or in_loop) else None, main_loss)
 
     fam = "WavLM-Base" if args.model == "wavlm-base" else "HuBERT-Base"
     utts = "10s utts" if batches is None else "bucketed 2-15.6s utts, 160 s/batch"

@@ -69,6 +69,7 @@ _SIGS = {
                               vp, vp, vp, i64, S], C.c_int),
     "dph_wave_layernorm": ([vp, vp, i64, i64, f32, vp, S], C.c_int),
     "dph_colsum": ([vp, vp, i64, i64, vp, i64, S], C.c_int),
+    "dph_colsum3": ([vp, vp, vp, vp, i64, i64, vp, i64, S], C.c_int),
     "dph_colsum_workspace": ([i64, i64], i64),
     "dph_layernorm_bwd_workspace": ([i64, i64], i64),
     "dph_attention_fwd": ([vp, vp, vp, vp, vp, vp, i64, i64, i64, f32, f32, u64, vp, S], C.c_int),
@@ -129,7 +130,7 @@ _SIGS = {
 _lib = None
 # include/dphubert_hip.h layout (3: dph_adamw_step_dev, dph_set_rng_epoch; 4: dph_event_*; 5: LN bwd / colsum
 # workspaces; 12: dph_hc_bank_fwd / dph_hc_bank_bwd)
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 
 class DphError(RuntimeError):

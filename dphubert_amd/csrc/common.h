@@ -188,6 +188,35 @@ __device__ __forceinline__ float wave_max(float v) {
 
 __host__ __device__ __forceinline__ int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// ---- zero fill as a KERNEL node -------------------------------------------------------------
+// The library zeroes its scratch with this kernel, never with hipMemsetAsync: inside a stream capture
+// that also carries the hand-added event-record nodes of the live GEMM timing (runtime.hip), a memset
+// node is the one node kind whose ordering we cannot check, and an accumulator zeroed out of order
+// reads whatever tensor owned the block earlier in the capture.
+namespace {
+__global__ void __launch_bounds__(256) zero_words_kernel(uint32_t* __restrict__ p, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) p[i] = 0u;
+}
+// bytes must be a multiple of 4 (every caller zeroes fp32 / uint32 words)
+inline void zero_async(void* p, int64_t bytes, hipStream_t stream) {
+  const int64_t n = bytes / 4;
+  if (n <= 0) return;
+  const int64_t nb = cdiv(n, 256) < 1024 ? cdiv(n, 256) : 1024;
+  hipLaunchKernelGGL(zero_words_kernel, dim3((unsigned)nb), dim3(256), 0, stream, reinterpret_cast<uint32_t*>(p), n);
+}
+
+// out[0] = sum of n partials part[i * stride + k] ... fixed order (one wave, lane-strided then a shuffle tree):
+// a deterministic replacement for same-address float atomics
+__device__ __forceinline__ float sum_partials_wave(const float* __restrict__ part, int64_t n, int64_t stride) {
+  const int lane = threadIdx.x & 63;
+  float s = 0.f;
+  for (int64_t i = lane; i < n; i += 64) s += part[i * stride];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  return s;
+}
+}  // namespace
+
 // ---- per-step RNG epoch ---------------------------------------------------------------------
 // Every kernel that draws dropout / HardConcrete noise mixes a device-resident epoch word into
 // its seed at entry.  The trainer advances that word with a stream-ordered op once per step, so a

@@ -711,7 +711,7 @@ extern "C" int dph_conv0_gn_bwd(const float* wave, int64_t B, int64_t S, const f
   float* sums = ws;
   const int64_t sums_bytes = cdiv(B * C * NQ * 4, 64) * 64;
   double* gram = reinterpret_cast<double*>(reinterpret_cast<char*>(ws) + sums_bytes);
-  if (hipMemsetAsync(ws, 0, sums_bytes + B * NG * 8, stream) != hipSuccess) return check_launch("dph_conv0_gn_bwd memset");
+  zero_async(ws, sums_bytes + B * NG * 8, stream);
   hipLaunchKernelGGL(conv0_gram_kernel, dim3((unsigned)cdiv(p.L0, GRAM_ROWS), (unsigned)B), dim3(256), 0, stream,
                      wave, p, gram);
   // DPH_C0B_VARIANT (tuning knob): 0 = 4 channels/thread, 4-row dy prefetch, 512 rows/block;

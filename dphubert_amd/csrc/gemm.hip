@@ -2029,7 +2029,7 @@ extern "C" int dph_gemm(const DphGemmArgs* args, hipStream_t stream) {
     const int64_t tiles = (int64_t)grid.x * grid.y * a.batch;
     if (a.workspace_bytes >= slab + tiles * 4) {
       cnt = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(a.workspace) + slab);
-      if (hipMemsetAsync(cnt, 0, tiles * 4, stream) != hipSuccess) return check_launch("dph_gemm split-K ticket memset");
+      zero_async(cnt, tiles * 4, stream);
     }
   }
   if (small_nt(kchunk) == 512) {

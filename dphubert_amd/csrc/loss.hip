@@ -72,17 +72,23 @@ __global__ void __launch_bounds__(256) loss_fwd_kernel(const float* __restrict__
     red[wave][2] = cterm;
   }
   __syncthreads();
-  if (threadIdx.x < 3) {
-    const float v = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
-    atomicAdd(partial + threadIdx.x, v);
-  }
+  // one partial triple per block (no atomics: the finalize kernel sums them in a fixed order)
+  if (threadIdx.x < 3)
+    partial[blockIdx.x * 3 + threadIdx.x] =
+        red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
 }
 
-__global__ void loss_finalize_kernel(const float* __restrict__ partial, int64_t rows, int64_t nel, float l2w, float l1w,
-                                     float cosw, float* __restrict__ out) {
-  const float mse = partial[1] / (float)nel;
-  const float l1 = partial[0] / (float)nel;
-  const float cos = -partial[2] / (float)rows;
+// one wave: sums the nblk partial triples in a fixed order
+__global__ void __launch_bounds__(64) loss_finalize_kernel(const float* __restrict__ partial, int64_t nblk, int64_t rows,
+                                                           int64_t nel, float l2w, float l1w, float cosw,
+                                                           float* __restrict__ out) {
+  const float s_l1 = sum_partials_wave(partial + 0, nblk, 3);
+  const float s_l2 = sum_partials_wave(partial + 1, nblk, 3);
+  const float s_c = sum_partials_wave(partial + 2, nblk, 3);
+  if (threadIdx.x != 0) return;
+  const float mse = s_l2 / (float)nel;
+  const float l1 = s_l1 / (float)nel;
+  const float cos = -s_c / (float)rows;
   out[1] = l2w != 0.f ? mse : 0.f;
   out[2] = l1w != 0.f ? l1 : 0.f;
   out[3] = cosw != 0.f ? cos : 0.f;
@@ -147,12 +153,12 @@ extern "C" int dph_distill_loss_fwd(const float* s, const void* const* t_layers,
               "dph_distill_loss_fwd: unsupported L=%lld D=%lld", (long long)L, (long long)D);
   TPtrs tp;
   for (int i = 0; i < DPH_MAX_DISTILL_LAYERS; ++i) tp.p[i] = i < L ? reinterpret_cast<const bf16_t*>(t_layers[i]) : nullptr;
-  if (hipMemsetAsync(partial, 0, 3 * sizeof(float), stream) != hipSuccess) return check_launch("dph_distill_loss_fwd memset");
   const int64_t rows = B * L * T;
-  hipLaunchKernelGGL(loss_fwd_kernel, dim3((unsigned)std::min<int64_t>(cdiv(rows, 4), 1024)), dim3(256), 0, stream, s,
-                     tp, B, L, T, D,
-                     cos_logsig, rowstats, partial);
-  hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(1), 0, stream, partial, rows, rows * D, l2w, l1w, cosw, out);
+  const int64_t nblk = std::min<int64_t>(cdiv(rows, 4), DPH_LOSS_PARTIAL_FLOATS / 3);
+  hipLaunchKernelGGL(loss_fwd_kernel, dim3((unsigned)nblk), dim3(256), 0, stream, s, tp, B, L, T, D, cos_logsig, rowstats,
+                     partial);
+  hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(64), 0, stream, partial, nblk, rows, rows * D, l2w, l1w, cosw,
+                     out);
   return check_launch("dph_distill_loss_fwd");
 }
 

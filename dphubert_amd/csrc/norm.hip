@@ -564,3 +564,22 @@ extern "C" int dph_colsum(const void* x, float* out, int64_t rows, int64_t cols,
                      stream, ws, nrb, cols, cols, out, (float*)nullptr, (float*)nullptr);
   return check_launch("dph_colsum");
 }
+
+// Column sums of a [rows][3*seg] matrix into three segment outputs (NULL output: segment skipped).  The fused
+// q/k/v projection gradient: the k_proj bias gradient is the column sum of dK, which is exactly zero (each query
+// row's scores are shifted by q.b_k for every key, and softmax is shift invariant, components.py:411-417) -- its
+// fp32 evaluation is rounding noise that AdamW would turn into +-lr steps, so it is not computed (out1 = NULL).
+extern "C" int dph_colsum3(const void* x, float* out0, float* out1, float* out2, int64_t rows, int64_t seg, float* ws,
+                           int64_t ws_bytes, hipStream_t stream) {
+  const int64_t cols = 3 * seg;
+  DPH_REQUIRE(x && rows > 0 && seg > 0, "dph_colsum3: bad args");
+  DPH_REQUIRE(ws && ws_bytes >= dph_colsum_workspace(rows, cols), "dph_colsum3: workspace too small");
+  const int64_t rpb = colsum_rpb(rows);
+  const int64_t nrb = cdiv(rows, rpb);
+  dim3 grid((unsigned)cdiv(cols, 512), (unsigned)nrb);
+  hipLaunchKernelGGL(colsum_kernel, grid, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(x), ws, rows, cols,
+                     rpb);
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)cdiv(cols, 64), (unsigned)slab_groups(nrb)), dim3(256), 0,
+                     stream, ws, nrb, cols, seg, out0, out1, out2);
+  return check_launch("dph_colsum3");
+}

@@ -21,10 +21,11 @@ struct Groups {
 };
 
 // ||g||^2 over every chunk: a fixed grid of at most SUMSQ_BLOCKS blocks walks the chunks, sums in
-// registers (16-B loads where the tensor is 16-B aligned) and adds ONE value per block into *out.
-// (One block per 8192-element chunk meant ~11.7 k same-address float atomics per step: they serialise at
-// the memory side, ~16 ns each -- 0.19 ms for a 382 MB read.)
-constexpr int SUMSQ_BLOCKS = 1024;
+// registers (16-B loads where the tensor is 16-B aligned) and writes ONE partial per block (out[1 + b]);
+// a one-wave kernel sums the partials in a fixed order into out[0] (deterministic clip norm, no memset).
+// (One block per 8192-element chunk with a same-address float atomic each meant ~11.7 k atomics per step:
+// they serialise at the memory side, ~16 ns each -- 0.19 ms for a 382 MB read.)
+constexpr int SUMSQ_BLOCKS = DPH_SUMSQ_FLOATS - 1;
 
 __global__ void __launch_bounds__(256) sumsq_kernel(const DphTensorSlot* __restrict__ slots,
                                                     const int64_t* __restrict__ cslot,
@@ -52,7 +53,12 @@ __global__ void __launch_bounds__(256) sumsq_kernel(const DphTensorSlot* __restr
   s = wave_sum(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
-  if (threadIdx.x == 0) atomicAdd(out, red[0] + red[1] + red[2] + red[3]);
+  if (threadIdx.x == 0) out[1 + blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ void __launch_bounds__(64) sumsq_finalize_kernel(float* __restrict__ out, int64_t nb) {
+  const float s = sum_partials_wave(out + 1, nb, 1);
+  if (threadIdx.x == 0) out[0] = s;
 }
 
 __global__ void __launch_bounds__(256) adamw_kernel(const DphTensorSlot* __restrict__ slots,
@@ -126,10 +132,10 @@ using namespace dph;
 extern "C" int dph_grad_sumsq(const DphTensorSlot* slots, int64_t n_slots, const int64_t* chunk_slot,
                               const int64_t* chunk_start, int64_t n_chunks, float* sumsq, hipStream_t stream) {
   DPH_REQUIRE(slots && chunk_slot && chunk_start && sumsq && n_slots > 0 && n_chunks > 0, "dph_grad_sumsq: bad args");
-  if (hipMemsetAsync(sumsq, 0, sizeof(float), stream) != hipSuccess) return check_launch("dph_grad_sumsq memset");
   const int64_t nb = n_chunks < SUMSQ_BLOCKS ? n_chunks : SUMSQ_BLOCKS;
   hipLaunchKernelGGL(sumsq_kernel, dim3((unsigned)nb), dim3(256), 0, stream, slots, chunk_slot, chunk_start, n_chunks,
                      sumsq);
+  hipLaunchKernelGGL(sumsq_finalize_kernel, dim3(1), dim3(64), 0, stream, sumsq, nb);
   return check_launch("dph_grad_sumsq");
 }
 

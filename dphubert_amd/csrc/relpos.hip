@@ -298,7 +298,7 @@ extern "C" int dph_wavlm_gate_bwd(const void* x, int64_t ldx, const float* w, co
   float* dz = ws;
   float* db0 = ws + 2 * N;          // [8] (entries 0 and 4 used)
   float* part = db0 + 8;            // [nblk][2][64] per-block group rows of dW
-  if (hipMemsetAsync(db0, 0, 8 * sizeof(float), stream) != hipSuccess) return check_launch("dph_wavlm_gate_bwd memset");
+  zero_async(db0, 8 * sizeof(float), stream);
   hipLaunchKernelGGL(wavlm_gate_bwd_kernel, dim3((unsigned)cdiv(N, 256)), dim3(256), 0, stream, a, dgate,
                      reinterpret_cast<bf16_t*>(dx), lddx, dz, db0, dconst);
   hipLaunchKernelGGL(wavlm_gate_wgrad_kernel, dim3((unsigned)nblk), dim3(256), 0, stream, a, dz, part);

@@ -66,7 +66,7 @@ class _LossOnlyFn(torch.autograd.Function):
         L, D = s.shape[0], s.shape[-1]
         dev = s.device
         rowstats = torch.empty(L * B * T * 3, dtype=torch.float32, device=dev)
-        partial = torch.empty(3, dtype=torch.float32, device=dev)
+        partial = torch.empty(ops.LOSS_PARTIAL_FLOATS, dtype=torch.float32, device=dev)
         out = torch.empty(4, dtype=torch.float32, device=dev)
         tptrs = (_C.c_void_p * L)(*[t.data_ptr() for t in t_layers])
         call("dph_distill_loss_fwd", ptr(s), tptrs, B, L, T, D, cfg["l2"], cfg["l1"], cfg["cos"],
@@ -233,6 +233,9 @@ class DistillModule(nn.Module):
         else:
             loss_reg = 0
             loss = loss_distill
+        # the batched gate launch's expected #params belongs to this step only (a later get_num_params() must
+        # recompute it, not return a tensor whose graph this step's backward consumes)
+        self.student_model._bank_num = None
         self.log_dict({f"{mode}_loss": loss, f"{mode}_loss_distill": loss_distill, f"{mode}_loss_mse": loss_mse,
                        f"{mode}_loss_l1": loss_l1, f"{mode}_loss_cos": loss_cos, f"{mode}_loss_reg": loss_reg})
         if mode == "train" and self.use_reg:

@@ -32,6 +32,7 @@ from ._lib import call, ptr
 
 BF16 = torch.bfloat16
 F32 = torch.float32
+LOSS_PARTIAL_FLOATS = 3072      # DPH_LOSS_PARTIAL_FLOATS (include/dphubert_hip.h)
 
 HC_BETA = 2.0 / 3.0
 HC_LIMIT_L = -0.1
@@ -495,6 +496,14 @@ class GradOut:
 
 def _dev(t):
     return t.device
+
+
+def _qkv_bias_grad(dqkv, dbqkv, M, dev):
+    """q / v bias gradients (+=) as column sums of dQ / dV; the k bias gradient is exactly zero (softmax shift
+    invariance, components.py:411-417) and its slot of the fused [3*Dh] buffer is left untouched (zeroed)."""
+    Dh = dqkv.shape[1] // 3
+    base = dbqkv.data_ptr()
+    call("dph_colsum3", ptr(dqkv), base, None, base + 8 * Dh, M, Dh, *colsum_ws(M, 3 * Dh, dev), _s())
 
 
 # ---------------------------------------------------------------------------
@@ -1519,7 +1528,7 @@ class EncoderLayerFn(torch.autograd.Function):
             dqkv = torch.empty_like(sv["qkv"])
             wl_g = EncoderLayerFn._attention_bwd(ctx, cfg, sv, do_m, hm, Dvec, dqkv)
             dbqkv, _ = go.buf(pr["bq"], pr["bk"], pr["bv"])
-            call("dph_colsum", ptr(dqkv), ptr(dbqkv), M, dqkv.shape[1], *colsum_ws(M, dqkv.shape[1], dev), _s())
+            _qkv_bias_grad(dqkv, dbqkv, M, dev)
             dwqkv, direct = go.buf(pr["wq"], pr["wk"], pr["wv"], zero=False)
             with wgrad_side(dqkv, xn1, enable=direct):
                 k4 = K.linear_wgrad(dqkv, xn1, dwqkv, accumulate=direct)
@@ -1677,7 +1686,7 @@ class EncoderLayerFn(torch.autograd.Function):
             dqkv = torch.empty_like(sv["qkv"])
             wl_g = EncoderLayerFn._attention_bwd(ctx, cfg, sv, do_m, hm, Dvec, dqkv)
             dbqkv, _ = go.buf(pr["bq"], pr["bk"], pr["bv"])
-            call("dph_colsum", ptr(dqkv), ptr(dbqkv), M, dqkv.shape[1], *colsum_ws(M, dqkv.shape[1], dev), _s())
+            _qkv_bias_grad(dqkv, dbqkv, M, dev)
             dwqkv, direct = go.buf(pr["wq"], pr["wk"], pr["wv"], zero=False)
             with wgrad_side(dqkv, h, enable=direct):
                 k4 = K.linear_wgrad(dqkv, h, dwqkv, accumulate=direct)
@@ -1729,7 +1738,7 @@ class DistillProjLossFn(torch.autograd.Function):
             else:
                 K.linear_fwd(sh[l], imgs[p], pw[2 * p + 1], out=s[l])
         rowstats = torch.empty(L * M * 3, dtype=F32, device=dev)
-        partial = torch.empty(3, dtype=F32, device=dev)
+        partial = torch.empty(LOSS_PARTIAL_FLOATS, dtype=F32, device=dev)
         out = torch.empty(4, dtype=F32, device=dev)
         tptrs = (_lib.C.c_void_p * L)(*[t.data_ptr() for t in th])
         call("dph_distill_loss_fwd", ptr(s), tptrs, B, L, T, Dt, cfg["l2"], cfg["l1"], cfg["cos"],

@@ -17,6 +17,7 @@ from . import _lib
 from ._lib import DphAdamGroup, DphTensorSlot, call, ptr
 
 CHUNK = 8192   # must match optim.hip
+SUMSQ_FLOATS = 1025   # DPH_SUMSQ_FLOATS (include/dphubert_hip.h)
 
 
 class FusedAdamW(torch.optim.Optimizer):
@@ -60,7 +61,7 @@ class FusedAdamW(torch.optim.Optimizer):
         nbytes = len(plist) * C_SIZEOF_SLOT
         self._pinned = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
         self._slots_dev = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-        self._sumsq = torch.zeros(1, dtype=torch.float32, device=dev)
+        self._sumsq = torch.zeros(SUMSQ_FLOATS, dtype=torch.float32, device=dev)   # [0] = ||g||^2, [1:] partials
         self._chunk_key = key
 
     def _slot_table(self, plist):

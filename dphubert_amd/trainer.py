@@ -150,6 +150,8 @@ class Trainer:
         self._prof_graph = None
         self._static = None
         self._prof_loss = None
+        self._prof = None
+        self._logged_of = {}             # id(graph) -> the module.logged dict its capture produced
         self.scalars = None
         # teacher forward on a side stream (DPH_TEACHER_STREAM=0 keeps one stream)
         if os.environ.get("DPH_TEACHER_STREAM", "1") != "0" and torch.cuda.is_available() and \
@@ -218,11 +220,12 @@ class Trainer:
                 LaunchProfiler.active = prof
             # thread_local: the process group's watchdog thread keeps polling the events of earlier (eager)
             # collectives while this thread captures; under the default "global" mode that poll is an illegal
-            # call during capture and aborts the process ("operation not permitted when stream is capturing")
-            # the profiled copy (timing only) gets a private memory pool, so it can never alias a block the
-            # main graph keeps using across replays.  Open issue: its reported loss is sometimes a constant
-            # garbage value (bits 0x6976e573) with or without this isolation, while the main graph's loss is
-            # sane (-0.117) in every run; the timed region only replays the main graph
+            # call during capture and aborts the process ("operation not permitted when stream is capturing").
+            # The profiled copy (a full training step whose GEMMs carry hand-added event-record nodes; bench.py
+            # replays it as the LAST TIMED step) gets a private memory pool, so it can never alias a block the
+            # main graph keeps using across replays.  Its loss terms are checked by bench.py and
+            # tests/test_fullshape_gpu.py (a round-2 run reported L1 = -2.4e22 for it: an accumulator zeroed by
+            # a memset node; the library zeroes with kernel nodes only since round 3, common.h zero_async)
             pool = None if prof is not None else self._pool
             with torch.cuda.graph(g, pool=pool, capture_error_mode="thread_local"):
                 loss = self._gpu_step(self._static, zero, final)
@@ -231,6 +234,8 @@ class Trainer:
             ops.reset_zero_arena()
         if self._pool is None and prof is None:
             self._pool = g.pool()
+        # the logged terms of this graph are the tensors its capture wrote: a replay of THIS graph refreshes them
+        self._logged_of[id(g)] = dict(self.module.logged)
         return g, loss
 
     def _set_static(self, batch):
@@ -242,6 +247,15 @@ class Trainer:
         if wave.shape != sw.shape or (lengths is None) != (sl is None):
             raise ValueError("Trainer(graphs=True): every batch must have the captured shape "
                              f"{tuple(sw.shape)} (got {tuple(wave.shape)})")
+        if lengths is not None:
+            # normalize_waveform crops the batch to max(lengths) (model.py:96-103); a captured graph replays the
+            # crop of its capture, so a batch with another max(lengths) cannot be replayed (host check: one
+            # small device read per step, only for models that normalize)
+            for mdl in (self.module.teacher_model, self.module.student_model):
+                hint = getattr(mdl, "_lmax_hint", None) if getattr(mdl, "normalize_waveform", False) else None
+                if hint is not None and int(lengths.max()) != hint[1]:
+                    raise ValueError(f"Trainer(graphs=True): max(lengths) = {int(lengths.max())} differs from the "
+                                     f"captured crop length {hint[1]} (normalize_waveform)")
         sw.copy_(wave)
         if lengths is not None:
             sl.copy_(lengths)
@@ -254,6 +268,9 @@ class Trainer:
         # the profiled copy runs the teacher on the main stream: with the side stream, parallel graph branches
         # interleave between an event pair and the pair no longer brackets one kernel (live 75 us vs 58 us in
         # the rocprof trace for the same launches)
+        # the graph's event-record nodes refer to the profiler's hipEvents: keep it (and them) alive as long as
+        # the graph can be replayed (a collected profiler destroys its events -> replay faults on the host)
+        self._prof = prof
         side, self.module.teacher_stream = self.module.teacher_stream, None
         wside, self._wgrad_stream = self._wgrad_stream, None
         try:
@@ -284,11 +301,11 @@ class Trainer:
                     self._graphs = {}
             if key in self._graphs:
                 if profiled and final and self._prof_graph is not None:
-                    self._prof_graph.replay()
-                    loss = self._prof_loss
+                    g, loss = self._prof_graph, self._prof_loss
                 else:
                     g, loss = self._graphs[key]
-                    g.replay()
+                g.replay()
+                m.logged = dict(self._logged_of[id(g)])
         if loss is None:
             loss = self._gpu_step(batch, zero, final)
             if final:

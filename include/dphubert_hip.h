@@ -156,6 +156,11 @@ int dph_wave_layernorm(const float* x, const int64_t* lengths, int64_t B, int64_
  * slab of dph_colsum_workspace(rows, cols) bytes */
 int dph_colsum(const void* x, float* out, int64_t rows, int64_t cols, float* ws, int64_t ws_bytes, hipStream_t stream);
 int64_t dph_colsum_workspace(int64_t rows, int64_t cols);
+/* the same over a [rows][3*seg] matrix into three segment outputs out0/out1/out2 (+=; a NULL output skips its
+ * segment; ws: dph_colsum_workspace(rows, 3*seg) bytes).  q/k/v bias gradients (components.py:406-408): the k
+ * segment is skipped, its gradient is exactly zero by softmax shift invariance (components.py:411-417) */
+int dph_colsum3(const void* x, float* out0, float* out1, float* out2, int64_t rows, int64_t seg, float* ws,
+                int64_t ws_bytes, hipStream_t stream);
 
 /* ------------------------------------------------------------------------ *
  * Fused multi-head self-attention (flash style), head dim 64.
@@ -312,8 +317,11 @@ int dph_add_bf16(const void* a, const void* b, void* out, int64_t n, hipStream_t
  * The loss is a mean over all (l,b,t) rows, so the layer-major order is
  * equivalent to the reference's torch.stack(dim=1) (B,L,T,D).
  * out[0..3] = loss, mse, l1, cos.  rowstats [B*L*T][3] saved for backward.
+ * partial: DPH_LOSS_PARTIAL_FLOATS fp32 of scratch (one (l1, l2, cos) triple per block, summed in a fixed
+ * order by a finalize kernel: deterministic, no atomics, no memset).
  * ------------------------------------------------------------------------ */
 #define DPH_MAX_DISTILL_LAYERS 16
+#define DPH_LOSS_PARTIAL_FLOATS 3072
 int dph_distill_loss_fwd(const float* s, const void* const* t_layers, int64_t B, int64_t L, int64_t T, int64_t D,
                          float l2w, float l1w, float cosw, int cos_logsig, float* rowstats, float* partial,
                          float* out, hipStream_t stream);
@@ -403,7 +411,9 @@ typedef struct DphAdamGroup {
   float pad_[3];
 } DphAdamGroup;
 
-/* sumsq[0] += sum over all slots of grad^2 (fp32 atomics, blocks over chunks) */
+/* sumsq[0] = sum over all slots of grad^2.  sumsq holds DPH_SUMSQ_FLOATS fp32: [0] the result, [1..] one
+ * partial per block, summed in a fixed order by a finalize kernel (deterministic clip norm) */
+#define DPH_SUMSQ_FLOATS 1025
 int dph_grad_sumsq(const DphTensorSlot* slots, int64_t n_slots, const int64_t* chunk_slot,
                    const int64_t* chunk_start, int64_t n_chunks, float* sumsq, hipStream_t stream);
 /* clip coef = min(1, max_norm/(sqrt(sumsq)+1e-6)) applied to grads, then AdamW step `step` (1-based) */
