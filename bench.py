@@ -31,6 +31,60 @@ FLOP_PER_UTT_BASE = 599.6e9      # teacher fwd + 3 x (student fwd +
 MFMA_PEAK_TFLOPS = 2500.0        # MI355X dense bf16 (MI355X_MICROARCH.md)
 
 
+def forward_flops(cfg: dict, samples: int) -> float:
+    """Dense forward FLOPs of one utterance through extract_features: conv frontend, feature
+    projection, positional conv, per layer q/k/v/out projections, QK^T + PV and the FFN, at the config's (possibly
+    pruned, ragged) widths."""
+    L, cin, f = samples, 1, 0.0
+    for cout, k, s_ in cfg["extractor_conv_layer_config"]:
+        L = (L - k) // s_ + 1
+        f += 2.0 * cin * cout * k * L
+        cin = cout
+    T, D = L, cfg["encoder_embed_dim"]
+    f += 2.0 * cin * D * T
+    f += 2.0 * D * (D // cfg["encoder_pos_conv_groups"]) * cfg["encoder_pos_conv_kernel"] * T
+    heads = cfg.get("encoder_num_heads") or [len(h) for h in cfg["encoder_remaining_heads"]]
+    hd = cfg.get("encoder_head_dim", 64)
+    for l in range(cfg["encoder_num_layers"]):
+        if cfg["encoder_use_attention"][l] and heads[l] > 0:
+            e = heads[l] * hd
+            f += 2.0 * T * D * 3 * e + 2.0 * T * e * D + 4.0 * T * T * e
+        if cfg["encoder_use_feed_forward"][l]:
+            f += 4.0 * T * D * cfg["encoder_ff_interm_features"][l]
+    return f
+
+
+def step_flops_per_utt(tcfg: dict, scfg: dict, n_distill: int, samples: int) -> float:
+    """teacher forward + 3 x (student forward + distill projections) per utterance."""
+    T = samples
+    for _, k, s_ in tcfg["extractor_conv_layer_config"]:
+        T = (T - k) // s_ + 1
+    proj = n_distill * 2.0 * T * scfg["encoder_embed_dim"] * tcfg["encoder_embed_dim"]
+    return forward_flops(tcfg, samples) + 3.0 * (forward_flops(scfg, samples) + proj)
+
+
+def workload(args):
+    """(teacher config, student config or None, DistillModule kwargs, description) of the benched step."""
+    from dphubert_amd.synthetic import HUBERT_BASE_CONFIG, WAVLM_BASE_CONFIG, WAV2VEC2_LARGE_CONFIG
+    tcfg = {"wavlm-base": WAVLM_BASE_CONFIG, "large": WAV2VEC2_LARGE_CONFIG}.get(args.model, HUBERT_BASE_CONFIG)
+    layers = "0.4,8,12,16,20,24" if args.model == "large" else "0.4,8,12"       # run_large.sh:13 / run.sh:21
+    if args.student == "pruned":
+        # final_distill.py (run.sh:95-115): the pruned student (prune() of a 0.75-sparsity student, ~23.6 M
+        # params), no HardConcrete units, no regulariser (final_distill.py:115), lr 1e-4
+        from dphubert_amd.synthetic import pruned_student
+        scfg, ssd = pruned_student(tcfg, seed=0)
+        kw = dict(student_config=scfg, student_state=ssd, use_reg=False, learning_rate=1e-4, warmup_updates=5000,
+                  max_updates=25000)
+        desc = "final_distill.py step: {fam} teacher (eval) + pruned student (train, ~23.6 M params, dropout)"
+    else:
+        scfg = dict(tcfg, extractor_prune_conv_channels=True, encoder_prune_attention_heads=True,
+                    encoder_prune_feed_forward_intermediate=True)
+        kw = dict(pruning_units="conv,head,interm", use_reg=True)
+        desc = ("distill.py step: {fam} teacher (eval) + student (train, HardConcrete conv,head,interm, dropout) + "
+                "L1/cos distill loss + sparsity Lagrangian + AdamW")
+    return tcfg, scfg, layers, kw, desc
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -113,7 +167,7 @@ def pmc_traffic(args):
             cmd = [exe, "--pmc", counter, "--kernel-include-regex", "gemm_kernel", "-f", "csv", "-d", d, "-o", "run",
                    "--", sys.executable, os.path.join(here, "bench.py"), "--steps", "1", "--warmup", "1",
                    "--no-cpu-baseline", "--no-roofline", "--traffic", "off", "--graphs", "off", "--batch", str(args.batch),
-                   "--seconds", str(args.seconds)]
+                   "--seconds", str(args.seconds), "--model", args.model, "--student", args.student]
             env = dict(os.environ, TMPDIR="/tmp")
             r = subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
                                timeout=400)
@@ -190,10 +244,16 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=16, help="utterances per GPU (run.sh: 160 s per GPU)")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="utterances per GPU per micro-batch (default: 16 = run.sh's 160 s per GPU; 8 for --student "
+                         "pruned = 640 s over 8 GPUs, SURVEY 8(d) config 4; 6 for --model large = run_large.sh's 60 s)")
     ap.add_argument("--seconds", type=float, default=10.0)
-    ap.add_argument("--model", choices=["hubert-base", "wavlm-base"], default="hubert-base",
-                    help="teacher/student family (the headline metric is quoted on hubert-base)")
+    ap.add_argument("--model", choices=["hubert-base", "wavlm-base", "large"], default="hubert-base",
+                    help="teacher/student family (the headline metric is quoted on hubert-base; large = the "
+                         "wav2vec2-Large teacher of run_large.sh:11, 24 pre-norm layers, distill layers 0.4,8,12,16,20,24)")
+    ap.add_argument("--student", choices=["prune", "pruned"], default="prune",
+                    help="prune: distill.py's joint distill + prune step (HardConcrete units, regulariser); pruned: "
+                         "final_distill.py's step on a pruned ~23.6 M-parameter student (no HardConcrete)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--traffic", choices=["auto", "off"], default="auto",
@@ -210,6 +270,8 @@ def main():
     args = ap.parse_args()
     if args.lengths == "bucketed":
         args.graphs = "off"
+    if args.batch is None:
+        args.batch = 6 if args.model == "large" else (8 if args.student == "pruned" else 16)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -231,13 +293,14 @@ def main():
 
     from dphubert_amd import ops
     from dphubert_amd.kernels import LaunchProfiler
-    from dphubert_amd.synthetic import HUBERT_BASE_CONFIG, WAVLM_BASE_CONFIG, synthetic_batch
+    from dphubert_amd.synthetic import synthetic_batch
     from dphubert_amd.trainer import Trainer, build_distill_module
 
     ops.manual_seed(2022 + rank)
-    model_cfg = WAVLM_BASE_CONFIG if args.model == "wavlm-base" else HUBERT_BASE_CONFIG
-    module = build_distill_module(model_cfg, pruning_units="conv,head,interm", distill_layers="0.4,8,12",
-                                  use_reg=True)
+    tcfg, scfg, distill_layers, mkw, desc = workload(args)
+    module = build_distill_module(tcfg, distill_layers=distill_layers, **mkw)
+    n_student = sum(p.numel() for n, p in module.student_model.named_parameters() if "log_alpha" not in n)
+    flop_utt = step_flops_per_utt(tcfg, scfg, len(module.distill_layers), int(args.seconds * 16000))
     module.global_step = 5000            # target sparsity reached (0.75)
     module = module.to(dev)
     graphs = args.graphs == "on"
@@ -304,7 +367,7 @@ def main():
     value = audio_s / dt
     log(f"host enqueue {t_host / args.steps * 1e3:.2f} ms/step")
     log(f"loss {loss.item():.5f}  step {ms:.2f} ms  {value:.1f} audio-s/s  "
-        f"({FLOP_PER_UTT_BASE * args.batch * args.seconds / 10 / (ms / 1e3) / 1e12:.0f} TFLOP/s algorithmic/GPU)")
+        f"({flop_utt * args.batch / (ms / 1e3) / 1e12:.0f} TFLOP/s algorithmic/GPU)")
     terms = {k: (float(v.float().sum()) if torch.is_tensor(v) else v)
              for k, v in getattr(trainer.module, "logged", {}).items()}
     if os.environ.get("DPH_BENCH_LOGGED") == "1":      # diagnostics: the last replayed graph's logged terms
@@ -314,10 +377,11 @@ def main():
         main_loss = trainer._graphs[(args.accum == 1, True)][1].item()     # the last main-graph replay
     check_step(loss.item(), terms if (graphed or in_loop) else None, main_loss)
 
-    fam = "WavLM-Base" if args.model == "wavlm-base" else "HuBERT-Base"
+    fam = {"wavlm-base": "WavLM-Base", "large": "wav2vec2-Large"}.get(args.model, "HuBERT-Base")
     utts = "10s utts" if batches is None else "bucketed 2-15.6s utts, 160 s/batch"
     out = {
-        "metric": f"audio-seconds/sec/node ({fam} distill step, {utts})",
+        "metric": f"audio-seconds/sec/node ({fam} {'final_distill' if args.student == 'pruned' else 'distill'} step, "
+              f"{utts})",
         "value": round(value, 2),
         "unit": "audio-seconds/sec",
         "n_gpus": world,
@@ -329,10 +393,11 @@ def main():
         "vs_baseline": None,
         "dtype": "bf16",
         "data": f"synthetic (0.1*randn 16 kHz waveforms, seeded random-init {fam} weights)",
-        "config": {"workload": f"distill.py step: {fam} teacher (eval) + student (train, HardConcrete "
-                               "conv,head,interm, dropout) + L1/cos distill loss + sparsity Lagrangian + AdamW",
+        "config": {"workload": desc.format(fam=fam),
                    "utterances_per_gpu": args.batch, "seconds_per_utt": args.seconds,
-                   "global_batch_audio_s": world * args.batch * args.seconds, "distill_layers": "0.4,8,12",
+                   "global_batch_audio_s": world * args.batch * args.seconds * args.accum,
+                   "distill_layers": distill_layers, "student_params": n_student,
+                   "step_gflop_per_utt": round(flop_utt / 1e9, 1),
                    "parallelism": f"dp{world}", "accum_grad": args.accum, "grad_comm": args.grad_comm,
                    "lengths": args.lengths},
         "peak_hbm_gib": round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 2),
@@ -385,7 +450,8 @@ def main():
         out["config"]["batch_shapes"] = [f"{bb}x{ss / 16000:.2f}s" for bb, ss in shapes]
         out["data"] = ("synthetic (0.1*randn waveforms; lengths uniform 2-15.6 s, bucketed and cropped like the "
                        "reference's train loader)")
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and batches is None:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and batches is None and args.model == "hubert-base" \
+            and args.student == "prune":
         try:
             out["cpu_baseline"] = cpu_baseline()
         except Exception as e:  # noqa: BLE001 -- baseline is informational

@@ -22,6 +22,8 @@ import torch
 __all__ = [
     "HUBERT_BASE_CONFIG",
     "HUBERT_LARGE_CONFIG",
+    "WAV2VEC2_LARGE_CONFIG",
+    "pruned_student",
     "seeded_tensor",
     "seeded_state_dict",
     "synthetic_batch",
@@ -82,6 +84,24 @@ HUBERT_LARGE_CONFIG = dict(
 )
 
 
+# the wav2vec2-Large teacher run_large.sh:11 distils (convert_wav2vec2_large_from_fairseq.py:19-40): group_norm
+# extractor without conv bias, 24 pre-norm layers of width 1024 / 16 heads / FFN 4096, normalize_waveform
+WAV2VEC2_LARGE_CONFIG = dict(
+    HUBERT_BASE_CONFIG,
+    encoder_embed_dim=1024,
+    encoder_num_layers=24,
+    encoder_use_attention=[True] * 24,
+    encoder_use_feed_forward=[True] * 24,
+    encoder_num_heads=[16] * 24,
+    encoder_ff_interm_features=[4096] * 24,
+    encoder_layer_norm_first=True,
+    normalize_waveform=True,
+)
+
+# DPHuBERT's published parameter count (README.md:110-111): the student final_distill.py trains
+DPHUBERT_PARAMS = 23_585_946
+
+
 def _gen(seed: int, name: str) -> torch.Generator:
     g = torch.Generator()
     g.manual_seed((int(seed) * 1000003 + zlib.crc32(name.encode())) % (2**63 - 1))
@@ -134,3 +154,75 @@ def synthetic_batch(batch: int, samples: int = 160000, seed: int = 2022):
     wave = 0.1 * torch.randn(batch, samples, generator=g)
     lengths = torch.full((batch,), samples, dtype=torch.int64)
     return wave, lengths
+
+
+def _param_count(config: dict) -> int:
+    from .wav2vec2.model import wav2vec2_model
+    with torch.device("meta"):
+        m = wav2vec2_model(**config)
+    return sum(p.numel() for p in m.parameters())
+
+
+def pruned_student(config: dict, target_params: int = DPHUBERT_PARAMS, seed: int = 0):
+    """A final_distill.py student (final_distill.py:61-65): the reference's own prune() (model.py:115-125) applied to
+    a conv,head,interm student whose HardConcrete logits keep a seeded, per-layer ragged number of conv channels,
+    heads and FFN units, scaled so that the pruned model has ~``target_params`` parameters (23.59 M: DPHuBERT,
+    README.md:110).  Returns (pruned config, pruned state_dict); the weights are the seeded teacher weights that
+    survive the pruning (the student is initialised from the teacher, run.sh:20).
+    """
+    import copy
+    from .wav2vec2.model import wav2vec2_model
+    units = dict(copy.deepcopy(config), extractor_prune_conv_channels=True, encoder_prune_attention_heads=True,
+                 encoder_prune_feed_forward_intermediate=True)
+    g = torch.Generator().manual_seed(1000 + seed)
+    n_layers = config["encoder_num_layers"]
+    convs = [c for c, _, _ in config["extractor_conv_layer_config"]]
+    heads = list(config["encoder_num_heads"])
+    ffs = list(config["encoder_ff_interm_features"])
+    jc = (0.75 + 0.5 * torch.rand(len(convs), generator=g)).tolist()
+    jh = (0.75 + 0.5 * torch.rand(n_layers, generator=g)).tolist()
+    jf = (0.75 + 0.5 * torch.rand(n_layers, generator=g)).tolist()
+
+    def arch(r):
+        kc = [max(8, min(c, round(c * r * j))) for c, j in zip(convs, jc)]
+        kh = [max(1, min(h, round(h * r * j))) for h, j in zip(heads, jh)]
+        kf = [max(8, min(f, round(f * r * j))) for f, j in zip(ffs, jf)]
+        return kc, kh, kf
+
+    def count(r):
+        kc, kh, kf = arch(r)
+        c = copy.deepcopy(config)
+        c["extractor_conv_layer_config"] = [(k, kk, ss) for k, (_, kk, ss) in zip(kc, config["extractor_conv_layer_config"])]
+        c["encoder_num_heads"] = kh
+        c["encoder_ff_interm_features"] = kf
+        return _param_count(c)
+
+    lo, hi = 0.02, 1.0
+    for _ in range(30):
+        mid = 0.5 * (lo + hi)
+        if count(mid) > target_params:
+            hi = mid
+        else:
+            lo = mid
+    kc, kh, kf = arch(lo if abs(count(lo) - target_params) <= abs(count(hi) - target_params) else hi)
+    model = wav2vec2_model(**copy.deepcopy(units))
+    model.load_state_dict(seeded_state_dict([(k, tuple(v.shape)) for k, v in model.state_dict().items()], seed))
+    keep = {}
+    fe = model.feature_extractor.conv_layers
+    for i, k in enumerate(kc):
+        keep[fe[i].hard_concrete] = k
+    for l, layer in enumerate(model.encoder.transformer.layers):
+        keep[layer.attention.hard_concrete_for_heads] = kh[l]
+        keep[layer.feed_forward.hard_concrete_for_intermediate] = kf[l]
+    with torch.no_grad():
+        for hc, k in keep.items():
+            la = torch.full((hc.n_in,), -12.0)
+            la[torch.randperm(hc.n_in, generator=g)[:k]] = 12.0
+            hc.log_alpha.copy_(la)
+    model.eval()
+    conv_config, use_attention, use_feed_forward, num_heads, remaining_heads, ff_interm = model.prune()
+    pruned = copy.deepcopy(config)
+    pruned.update({"extractor_conv_layer_config": conv_config, "encoder_use_attention": use_attention,
+                   "encoder_use_feed_forward": use_feed_forward, "encoder_num_heads": num_heads,
+                   "encoder_ff_interm_features": ff_interm})
+    return pruned, {k: v.detach().clone() for k, v in model.state_dict().items()}

@@ -212,3 +212,12 @@ def test_predlayer_mode_g12():
         # reference heads are nn.Sequential(Linear, GELU): "{i}.0.weight" is the oracle's "{i}.weight"
         e_sample, e_sq = ck_close(out["proj_grads"][n.replace(".0.", ".", 1)], ck)
         assert e_sample < 1e-4 and e_sq < 1e-4, (n, e_sample, e_sq)
+
+
+@pytest.mark.slow
+def test_large_24_layers_g13():
+    """The full wav2vec2-Large depth of run_large.sh (24 pre-norm layers, distill layers 0.4,8,12,16,20,24)."""
+    fx = load_golden("g13_large24.pt")
+    out = _run_fixture(fx)
+    assert len(out["student_hiddens"]) == 25
+    _check_step(fx, out, tol_loss=2e-5, tol_ck=5e-4)

@@ -95,3 +95,58 @@ def test_final_distill_step_pruned_student_vs_oracle():
         assert e < 5e-2, (n, e)
         checked += 1
     assert checked > 20
+
+
+def test_bench_pruned_student_step_vs_oracle():
+    """bench.py --student pruned's final_distill.py step (BASELINE config 4): HuBERT-Base teacher, the ~23.6 M-param
+    student that synthetic.pruned_student prunes with the reference's prune() (ragged conv channels 101-122, 2-3 heads
+    and 522-799 FFN units per layer), 12 layers at the bench's 10 s shape (T = 499), vs the fp32 CPU oracle."""
+    from dphubert_amd.lightning import DistillLoss, DistillModule
+    from dphubert_amd.synthetic import HUBERT_BASE_CONFIG, pruned_student
+    tcfg = copy.deepcopy(HUBERT_BASE_CONFIG)
+    tcfg.update(encoder_projection_dropout=0.0, encoder_attention_dropout=0.0, encoder_ff_interm_dropout=0.0,
+                encoder_dropout=0.0, encoder_layer_drop=0.0)
+    scfg, ssd = pruned_student(tcfg, seed=0)
+    n = sum(v.numel() for v in ssd.values())
+    assert abs(n - 23_585_946) < 0.01 * 23_585_946, n
+    tsd = seeded_sd(tcfg, 0)
+    teacher = wav2vec2_model(**copy.deepcopy(tcfg))
+    teacher.load_state_dict(tsd)
+    for p in teacher.parameters():
+        p.requires_grad = False
+    student = wav2vec2_model(**copy.deepcopy(scfg))
+    student.load_state_dict(ssd, strict=True)
+    psd = proj_sd_from_recipe(2, 768, 3)
+    projs = []
+    for g in range(2):
+        lin = torch.nn.Linear(768, 768)
+        with torch.no_grad():
+            lin.weight.copy_(psd[f"{g}.weight"])
+            lin.bias.copy_(psd[f"{g}.bias"])
+        projs.append(lin)
+    proj_index = [0, 1, 1, 1]
+    layers = [0, 4, 8, 12]
+    dm = DistillModule(teacher_model=teacher, student_model=student, distill_mode="layer2layer", distill_layers=layers,
+                       distill_linear_projs=torch.nn.ModuleList([projs[i] for i in proj_index]),
+                       distill_loss=DistillLoss(0.0, 1.0, 1.0, "raw"), learning_rate=1e-4, weight_decay=0.0,
+                       warmup_updates=5000, max_updates=25000, use_reg=False, reg_learning_rate=None,
+                       target_sparsity=None, sparsity_warmup_updates=None).to(DEV)
+    dm.train()
+    wave, ln = wave_batch(1, 160000, seed=6)
+    loss = dm._step((wave.to(DEV), ln.to(DEV)), 0, "train")
+    loss.backward()
+    torch.cuda.synchronize()
+    want = ref.distill_step(tsd, tcfg, ssd, scfg, psd, layers, proj_index, wave, ln, {}, None, 0)
+    assert abs(loss.item() - want["loss"].item()) <= 1e-3, (loss.item(), want["loss"].item())
+    got = dict(dm.student_model.named_parameters())
+    checked = 0
+    worst = (0.0, None)
+    for n, g in want["grads"].items():
+        if n not in got or got[n].grad is None or n.endswith("k_proj.bias") or g.norm() == 0:
+            continue
+        e = rel_l2(got[n].grad.float().cpu(), g)
+        worst = max(worst, (e, n))
+        assert e < 5e-2, (n, e)
+        checked += 1
+    print("pruned bench student: loss", loss.item(), "oracle", want["loss"].item(), "worst grad", worst)
+    assert checked > 100

@@ -536,6 +536,14 @@ def gen_large_ln():
                     lambdas=(0.3, -0.1), global_step=6000)
 
 
+def gen_large24():
+    """G13: the whole wav2vec2-Large teacher depth of run_large.sh (24 pre-norm layers, D 1024, normalize_waveform,
+    distill layers 0.4,8,12,16,20,24 = run_large.sh:13), 1 x 2 s, conv,head,interm, regulariser active (checksums)."""
+    cfg = large_cfg(24)
+    return run_step(cfg, cfg, "0.4,8,12,16,20,24", B=1, S=32000, units="conv,head,interm", lambdas=(0.2, 0.1),
+                    global_step=5000)
+
+
 def gen_predlayer():
     """G12: predlayer distill mode (distill.py:100-107, lightning.py:259-260) on the 2-layer Base shape, three
     heads (distill layers 0,1,2) on the last hidden state, padded batch, regulariser active."""
@@ -547,7 +555,7 @@ def gen_predlayer():
 def main():
     only = [a[len("--only="):] for a in sys.argv[1:] if a.startswith("--only=")]
     extra = {"g10_large.pt": gen_large, "g11_large_lnext.pt": gen_large_ln, "g12_predlayer.pt": gen_predlayer,
-             "g3_base12.pt": gen_base12}
+             "g3_base12.pt": gen_base12, "g13_large24.pt": gen_large24}
     if only:
         OUT.mkdir(parents=True, exist_ok=True)
         torch.set_num_threads(8)
