@@ -1749,6 +1749,301 @@ __global__ void __launch_bounds__(C::NT, C::WPE) ring_persist_kernel(const DphGe
   }
 }
 
+// =============================================================================================
+// Ping-pong GEMM (both operands k-contiguous, K % 64 == 0, direct-epilogue layouts).
+//
+// 8 waves = two groups of four (wr = 0 / 1; waves w and w + 4 share a SIMD) that run the SAME phase
+// program one barrier interval apart: in every interval one wave of each SIMD multiplies (an MFMA
+// cluster between two barriers) while its partner issues the LDS fragment reads and LDS-DMA stages of
+// its next phase, so the matrix core and the LDS / memory pipes work at once (the guide's 256^2 8-phase
+// structure, cdna_hip_programming.md §5; the ring kernels above run one barrier per 32-deep slice with
+// every wave in the same role, and their main loop measured 1.5-1.6x the MFMA time).
+//
+// Geometry: BM x BN tile, 64-deep K-tiles, waves 2 (M) x 4 (N), each a (BM/2) x (BN/4) output of FM x FN
+// 16x16 accumulators.  A K-tile is staged as four HALF-TILES with their own lifetimes:
+//   A-lo: the first FM/2 fragment rows of both wave rows   (BM/2 rows)
+//   A-hi: the last FM/2                                     (BM/2 rows)
+//   B-n0: the first ceil(FN/2) fragment columns of every wave column, B-n1: the rest
+// Phase j of K-tile u (buffer u & 1) reads / multiplies:
+//   j=0: read A-lo, B-n0 -> MFMA A-lo x B-n0      j=1: read B-n1 -> A-lo x B-n1
+//   j=2: read A-hi       -> A-hi x B-n1           j=3: (no reads)  A-hi x B-n0 (B-n0 kept since j=0)
+// and issues ONE half-tile: j=0 B-n1(u+1), j=1 A-hi(u+1), j=2 A-lo(u+2), j=3 B-n0(u+2).  With the two
+// groups one interval apart, a stage may overwrite a half-tile two phases after its last read (WAR) and a
+// half-tile may be read one phase after the wait that retires it (RAW); the issue order above gives every
+// half-tile exactly that and keeps four half-tiles (G DMAs per thread = one K-tile) in flight across the
+// barriers: each phase waits vmcnt(G), never 0 in the steady state.
+// LDS: two K-tile buffers, each half-tile rows of 128 B whose 16-B chunk p holds k-chunk p ^ ((r>>1)&7)
+// (the swizzle goes on the DMA SOURCE address: LDS-DMA writes lane-linear), conflict-free ds_read_b128.
+// =============================================================================================
+namespace pp {
+constexpr int BK = 64;
+
+template <int BM_, int BN_>
+struct Cfg {
+  static constexpr int BM = BM_, BN = BN_;
+  static constexpr int NW = 8, NT = 512, WGM = 2, WGN = 4;
+  static constexpr int WTM = BM / 2, WTN = BN / 4;
+  static constexpr int FM = WTM / 16, FN = WTN / 16;
+  static constexpr int FM2 = FM / 2, FN0 = (FN + 1) / 2, FN1 = FN / 2;
+  static constexpr int RA = BM / 2, RB0 = 64 * FN0, RB1 = 64 * FN1;     // half-tile rows
+  static constexpr int GA = RA / 64, GB0 = RB0 / 64, GB1 = RB1 / 64;    // LDS-DMA per thread per half-tile
+  static constexpr int G = 2 * GA + GB0 + GB1;                          // per K-tile
+  static constexpr int O_ALO = 0, O_AHI = RA * 128, O_B0 = 2 * RA * 128, O_B1 = O_B0 + RB0 * 128;
+  static constexpr int BUF = (BM + BN) * 128;
+  static constexpr int LDS = 2 * BUF;
+  // two blocks per CU only for the small tiles (the 128 x 192 GELU epilogues spilled at the 128-VGPR cap)
+  static constexpr int MINB = (LDS <= 80 * 1024 && FM * FN <= 8) ? 2 : 1;
+  static constexpr int WPE = MINB * 2;                                  // waves per SIMD
+  static_assert(FM % 2 == 0 && FN >= 2 && RA % 64 == 0 && G < 16, "pp tile geometry");
+};
+using P256 = Cfg<256, 256>;
+using P128x256 = Cfg<128, 256>;
+using P256x128 = Cfg<256, 128>;
+using P128x192 = Cfg<128, 192>;
+using P128 = Cfg<128, 128>;
+
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x70 | 0xF00);
+}
+__device__ __forceinline__ void lgkm0() { __builtin_amdgcn_s_waitcnt(0xC07F); }
+__device__ __forceinline__ void bar() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// 16 x 32 operand fragment of ksub s from a half-tile image: rows rb..rb+15 (rb % 16 == 0)
+__device__ __forceinline__ bf16x8_t hfrag(const char* ht, int rb, int s, int lane) {
+  const int row = rb + (lane & 15);
+  const int phys = (s * 4 + (lane >> 4)) ^ ((lane & 15) >> 1);
+  return *reinterpret_cast<const bf16x8_t*>(ht + row * 128 + phys * 16);
+}
+
+template <class C, int ACT, bool DROP>
+__global__ void __launch_bounds__(C::NT, C::WPE) pp_gemm_kernel(const DphGemmArgs a) {
+  __shared__ __attribute__((aligned(1024))) char smem[C::LDS];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  // tile: the ring kernel's XCD-grouped order (blocks b, b+8, ... share an XCD and get neighbouring tiles)
+  const int64_t z = blockIdx.z;
+  int64_t m0, n0;
+  {
+    const uint32_t ntm = gridDim.y, ntn = gridDim.x, nt = ntm * ntn;
+    const uint32_t bid = blockIdx.y * ntn + blockIdx.x;
+    const uint32_t q = nt >> 3, r = nt & 7;
+    const uint32_t xcd = bid & 7, loc = bid >> 3;
+    const uint32_t t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+    constexpr uint32_t GM = C::BM > 128 ? 4 : 8;
+    const uint32_t gsz = GM * ntn;
+    const uint32_t grp = t / gsz;
+    const uint32_t gm0 = grp * GM;
+    const uint32_t gh = min(GM, ntm - gm0);
+    const uint32_t l = t - grp * gsz;
+    const uint32_t lq = l / gh;
+    m0 = (int64_t)(gm0 + (l - lq * gh)) * C::BM;
+    n0 = (int64_t)lq * C::BN;
+  }
+  const int nk = (int)(a.K / BK);
+  const bf16_t* Ab = reinterpret_cast<const bf16_t*>(a.A.ptr) + z_addr(a.A, z);
+  const bf16_t* Bb = reinterpret_cast<const bf16_t*>(a.B.ptr) + z_addr(a.B, z);
+  // DMA sources (element offsets, < 2^31: checked on the host) of instruction jj of each half-tile kind:
+  // wave instruction gi = jj * 8 + wave fills half-tile rows gi*8 .. +7, lane -> row gi*8 + lane/8,
+  // physical chunk lane % 8 <- logical k-chunk (lane % 8) ^ ((row >> 1) & 7)
+  uint32_t oal[C::GA], oah[C::GA], ob0[C::GB0], ob1[C::GB1];
+  constexpr int HA = C::WTM / 2;
+#pragma unroll
+  for (int jj = 0; jj < C::GA; ++jj) {
+    const int rho = (jj * 8 + wave) * 8 + (lane >> 3);
+    const int lc = (lane & 7) ^ ((rho >> 1) & 7);
+    const int trow = (rho / HA) * C::WTM + rho % HA;
+    oal[jj] = (uint32_t)(row_addr32(a.A, (uint32_t)min<int64_t>(m0 + trow, a.M - 1)) + lc * 8);
+    oah[jj] = (uint32_t)(row_addr32(a.A, (uint32_t)min<int64_t>(m0 + trow + HA, a.M - 1)) + lc * 8);
+  }
+#pragma unroll
+  for (int jj = 0; jj < C::GB0; ++jj) {
+    const int rho = (jj * 8 + wave) * 8 + (lane >> 3);
+    const int lc = (lane & 7) ^ ((rho >> 1) & 7);
+    const int tcol = (rho / (16 * C::FN0)) * C::WTN + rho % (16 * C::FN0);
+    ob0[jj] = (uint32_t)(row_addr32(a.B, (uint32_t)min<int64_t>(n0 + tcol, a.N - 1)) + lc * 8);
+  }
+#pragma unroll
+  for (int jj = 0; jj < C::GB1; ++jj) {
+    const int rho = (jj * 8 + wave) * 8 + (lane >> 3);
+    const int lc = (lane & 7) ^ ((rho >> 1) & 7);
+    const int tcol = (rho / (16 * C::FN1)) * C::WTN + 16 * C::FN0 + rho % (16 * C::FN1);
+    ob1[jj] = (uint32_t)(row_addr32(a.B, (uint32_t)min<int64_t>(n0 + tcol, a.N - 1)) + lc * 8);
+  }
+  auto buf = [&](int u) -> char* { return smem + (u & 1) * C::BUF; };
+  auto st_alo = [&](int u) {
+#pragma unroll
+    for (int jj = 0; jj < C::GA; ++jj) ring::dma16(Ab + oal[jj] + (int64_t)u * BK, buf(u) + C::O_ALO + (jj * 8 + wave) * 1024);
+  };
+  auto st_ahi = [&](int u) {
+#pragma unroll
+    for (int jj = 0; jj < C::GA; ++jj) ring::dma16(Ab + oah[jj] + (int64_t)u * BK, buf(u) + C::O_AHI + (jj * 8 + wave) * 1024);
+  };
+  auto st_b0 = [&](int u) {
+#pragma unroll
+    for (int jj = 0; jj < C::GB0; ++jj) ring::dma16(Bb + ob0[jj] + (int64_t)u * BK, buf(u) + C::O_B0 + (jj * 8 + wave) * 1024);
+  };
+  auto st_b1 = [&](int u) {
+#pragma unroll
+    for (int jj = 0; jj < C::GB1; ++jj) ring::dma16(Bb + ob1[jj] + (int64_t)u * BK, buf(u) + C::O_B1 + (jj * 8 + wave) * 1024);
+  };
+
+  f32x4_t acc[C::FM][C::FN];
+#pragma unroll
+  for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+    for (int j = 0; j < C::FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  bf16x8_t fa[C::FM2][2], fb0[C::FN0][2], fb1[C::FN1][2];
+
+  auto rd_a = [&](const char* ht) {
+#pragma unroll
+    for (int i = 0; i < C::FM2; ++i)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) fa[i][s] = hfrag(ht, wr * HA + 16 * i, s, lane);
+  };
+  auto rd_b0 = [&](const char* bu) {
+#pragma unroll
+    for (int j = 0; j < C::FN0; ++j)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) fb0[j][s] = hfrag(bu + C::O_B0, wc * 16 * C::FN0 + 16 * j, s, lane);
+  };
+  auto rd_b1 = [&](const char* bu) {
+#pragma unroll
+    for (int j = 0; j < C::FN1; ++j)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) fb1[j][s] = hfrag(bu + C::O_B1, wc * 16 * C::FN1 + 16 * j, s, lane);
+  };
+  // MFMA cluster: rows [i0, i0 + FM2) x the given B fragment set
+  auto mm0 = [&](int i0) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < C::FM2; ++i)
+#pragma unroll
+        for (int j = 0; j < C::FN0; ++j)
+          acc[i0 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb0[j][s], fa[i][s], acc[i0 + i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto mm1 = [&](int i0) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < C::FM2; ++i)
+#pragma unroll
+        for (int j = 0; j < C::FN1; ++j)
+          acc[i0 + i][C::FN0 + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb1[j][s], fa[i][s], acc[i0 + i][C::FN0 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  constexpr int G = C::G;
+  // prologue: the half-tiles of "phases" -6 .. -1 (A-lo(0), B-n0(0), B-n1(0), A-hi(0), A-lo(1), B-n0(1)),
+  // then wait for A-lo(0) and B-n0(0)
+  st_alo(0);
+  st_b0(0);
+  st_b1(0);
+  st_ahi(0);
+  st_alo(1);
+  st_b0(1);
+  vm_wait<G>();
+  bar();
+  if (wr == 1) bar();            // group 1 runs one interval behind group 0
+  int u = 0;
+#pragma unroll 1
+  for (; u + 2 < nk; ++u) {
+    const char* bu = buf(u);
+    // j = 0
+    rd_b0(bu);
+    rd_a(bu + C::O_ALO);
+    st_b1(u + 1);
+    vm_wait<G>();
+    bar();
+    lgkm0();
+    __builtin_amdgcn_sched_barrier(0);
+    mm0(0);
+    bar();
+    // j = 1
+    rd_b1(bu);
+    st_ahi(u + 1);
+    vm_wait<G>();
+    bar();
+    lgkm0();
+    __builtin_amdgcn_sched_barrier(0);
+    mm1(0);
+    bar();
+    // j = 2
+    rd_a(bu + C::O_AHI);
+    st_alo(u + 2);
+    vm_wait<G>();
+    bar();
+    lgkm0();
+    __builtin_amdgcn_sched_barrier(0);
+    mm1(C::FM2);
+    bar();
+    // j = 3
+    st_b0(u + 2);
+    vm_wait<G>();
+    bar();
+    mm0(C::FM2);
+    bar();
+  }
+  // the last two K-tiles: nothing staged past nk - 1, the counted waits drain
+#pragma unroll
+  for (int t = 0; t < 2; ++t, ++u) {
+    const bool second_last = t == 0;
+    const char* bu = buf(u);
+    rd_b0(bu);
+    rd_a(bu + C::O_ALO);
+    if (second_last) {
+      st_b1(u + 1);
+      vm_wait<G>();
+    } else {
+      vm_wait<C::GA>();
+    }
+    bar();
+    lgkm0();
+    __builtin_amdgcn_sched_barrier(0);
+    mm0(0);
+    bar();
+    rd_b1(bu);
+    if (second_last) {
+      st_ahi(u + 1);
+      vm_wait<G>();
+    } else {
+      vm_wait<0>();
+    }
+    bar();
+    lgkm0();
+    __builtin_amdgcn_sched_barrier(0);
+    mm1(0);
+    bar();
+    rd_a(bu + C::O_AHI);
+    if (second_last) vm_wait<G - C::GA>();
+    else vm_wait<0>();
+    bar();
+    lgkm0();
+    __builtin_amdgcn_sched_barrier(0);
+    mm1(C::FM2);
+    bar();
+    if (second_last) vm_wait<C::GB1 + C::GA>();
+    else vm_wait<0>();
+    bar();
+    mm0(C::FM2);
+    bar();
+  }
+  if (wr == 0) bar();            // pairs with group 1's extra barrier
+  ring::direct_epi_t<C, ACT, DROP>(a, z, m0 + wr * C::WTM, n0 + wc * C::WTN, lane, acc);
+}
+}  // namespace pp
+
 // split-K reduction + epilogue: one thread per 8 columns of a row
 __global__ void splitk_reduce_kernel(const DphGemmArgs a) {
   const int64_t z = blockIdx.z;
@@ -1795,7 +2090,7 @@ static int small_nt(int64_t kchunk) {
 static int gemm_path_override() {
   const char* e = getenv("DPH_GEMM_PATH");
   if (!e) return 0;
-  return !strcmp(e, "small") ? 1 : !strcmp(e, "big") ? 2 : !strcmp(e, "mid") ? 3 : !strcmp(e, "tall") ? 4 : !strcmp(e, "half") ? 5 : !strcmp(e, "mid8") ? 6 : !strcmp(e, "mid8mn") ? 7 : !strcmp(e, "wide") ? 8 : !strcmp(e, "flat") ? 9 : !strcmp(e, "tri") ? 10 : !strcmp(e, "notri") ? 11 : 0;
+  return !strcmp(e, "small") ? 1 : !strcmp(e, "big") ? 2 : !strcmp(e, "mid") ? 3 : !strcmp(e, "tall") ? 4 : !strcmp(e, "half") ? 5 : !strcmp(e, "mid8") ? 6 : !strcmp(e, "mid8mn") ? 7 : !strcmp(e, "wide") ? 8 : !strcmp(e, "flat") ? 9 : !strcmp(e, "tri") ? 10 : !strcmp(e, "notri") ? 11 : !strcmp(e, "pp256") ? 12 : !strcmp(e, "pp128x256") ? 13 : !strcmp(e, "pp256x128") ? 14 : !strcmp(e, "pp128x192") ? 15 : !strcmp(e, "pp128") ? 16 : 0;
 }
 
 // the 192 x 128 tile takes the register epilogue only (its staged epilogue is compiled but not routed)
@@ -1805,6 +2100,52 @@ static bool tri_ok(const DphGemmArgs& a) {
 }
 
 static int num_cus();
+
+// the ping-pong kernels: both operands k-contiguous with 16-B aligned rows, whole 64-deep K-tiles (at least
+// two), register-epilogue layouts, DMA source offsets within 32 bits
+static bool pp_ok(const DphGemmArgs& a) {
+  if (!(a.splits == 1 && a.a_kcontig && a.b_kcontig && a.K % pp::BK == 0 && a.K >= 2 * pp::BK &&
+        ring::direct_epi_ok(a)))
+    return false;
+  auto op_ok = [&](const DphMat& d, int64_t rows) {
+    const int64_t al = d.row_stride | d.batch_stride | d.z_inner | d.z_outer;
+    if ((al & 7) != 0 || (reinterpret_cast<uintptr_t>(d.ptr) & 15) != 0) return false;
+    const int64_t r = rows - 1;
+    const int64_t last = d.rows_per_batch > 0 ? (r / d.rows_per_batch) * d.batch_stride + (r % d.rows_per_batch) * d.row_stride
+                                              : r * d.row_stride;
+    return last + a.K < ((int64_t)1 << 31) && rows < ((int64_t)1 << 31);
+  };
+  return op_ok(a.A, a.M) && op_ok(a.B, a.N);
+}
+
+// DPH_GEMM_PP=0 keeps every GEMM off the ping-pong kernels (A/B; read per call)
+static bool pp_enabled() {
+  const char* e = getenv("DPH_GEMM_PP");
+  return !(e && e[0] == '0');
+}
+
+// Ping-pong tile choice: estimated time = whole rounds of tiles over the CU slots x one tile's MFMA work at the
+// tile's measured rate (8192^3 random bf16, tools/gemm_ab.py: 256x256 1514, 128x192 1282, 128x256 1221,
+// 256x128 1211, 128x128 1178 TFLOP/s; a 128x128 block shares its CU with a second one).  Picks 256x256 for the
+// many-round conv GEMMs and 128x192 for the M = B*T projections (756 / 252 tiles = whole rounds on 256 CUs).
+static int pp_pick(const DphGemmArgs& a) {
+  struct Opt { int kind, bm, bn, per_cu; double tf; };
+  static const Opt opts[] = {{12, 256, 256, 1, 1514.0}, {15, 128, 192, 1, 1282.0}, {13, 128, 256, 1, 1221.0},
+                             {14, 256, 128, 1, 1211.0}, {16, 128, 128, 2, 1178.0}};
+  const int64_t cus = num_cus();
+  int best = 12;
+  double best_t = 1e300;
+  for (const Opt& o : opts) {
+    const int64_t tiles = cdiv(a.M, o.bm) * cdiv(a.N, o.bn) * a.batch;
+    const int64_t rounds = cdiv(tiles, cus * o.per_cu);
+    const double t = (double)rounds * o.per_cu * (double)o.bm * o.bn / o.tf;
+    if (t < best_t * 0.999) {
+      best_t = t;
+      best = o.kind;
+    }
+  }
+  return best;
+}
 
 // only where both tilings are a single round over the CUs (one block per CU) and the 192 x 128 one has
 // less area per CU: with several rounds the 128 x 256 tile's two waves per SIMD win (conv1 255984 x 512 x
@@ -1853,6 +2194,8 @@ static int gemm_kind(const DphGemmArgs& a, int64_t kchunk) {
   if (big_ok && a.N > ring::Tall::BN && (kchunk >= 1536 || (a.N <= 1024 && kchunk >= 4 * ring::KS))) kind = 8;
   // N <= 1024 on the 192 x 128 tile when it fills the CUs better (whole-chip rounds of tiles x tile area)
   if (kind == 8 && a.N <= 1024 && tri_ok(a) && tri_better(a)) kind = 10;
+  // the ping-pong kernels wherever their layout holds (A/B: DPH_GEMM_PP=0; a forced DPH_GEMM_PATH wins)
+  if (pp_enabled() && pp_ok(a)) kind = pp_pick(a);
   const int path = gemm_path_override();
   if (path == 1) kind = 0;
   if (path == 2 && big_ok) kind = 2;
@@ -1865,6 +2208,7 @@ static int gemm_kind(const DphGemmArgs& a, int64_t kchunk) {
   if (path == 9 && big_ok) kind = 8;
   if (path == 10 && big_ok && tri_ok(a)) kind = 10;
   if (path == 11 && kind == 10) kind = 8;     // "notri": the 128 x 256 tile where the 192 x 128 one would run
+  if (path >= 12 && path <= 16 && pp_ok(a)) kind = path;   // ping-pong tiles (A/B)
   return kind;
 }
 
@@ -1878,6 +2222,11 @@ extern "C" const char* dph_gemm_variant(const DphGemmArgs* args) {
   if (!args) return "";
   const DphGemmArgs& a = *args;
   const int kind = gemm_kind(a, gemm_kchunk(a));
+  if (kind == 12) return "pp_gemm_kernel<dph::(anonymous namespace)::pp::Cfg<256, 256>";
+  if (kind == 13) return "pp_gemm_kernel<dph::(anonymous namespace)::pp::Cfg<128, 256>";
+  if (kind == 14) return "pp_gemm_kernel<dph::(anonymous namespace)::pp::Cfg<256, 128>";
+  if (kind == 15) return "pp_gemm_kernel<dph::(anonymous namespace)::pp::Cfg<128, 192>";
+  if (kind == 16) return "pp_gemm_kernel<dph::(anonymous namespace)::pp::Cfg<128, 128>";
   if (kind == 6) return a.a_kcontig ? "ring::Cfg<128, 128, 64, 32>, true, false>" : "ring::Cfg<128, 128, 64, 32>, false, false>";
   if (kind == 10) return persist_ok(a) ? "persist_kernel<dph::(anonymous namespace)::ring::Cfg<192, 128, 96, 64>"
                                        : "ring::Cfg<192, 128, 96, 64>, true, true>";
@@ -1911,6 +2260,22 @@ static void launch_ring(const DphGemmArgs& a, int64_t kchunk, hipStream_t stream
       hipLaunchKernelGGL((ring_gemm_kernel<Cf, false, false>), g, dim3(Cf::NT), 0, stream, a, kchunk);
   } else {
     hipLaunchKernelGGL((ring_gemm_kernel<Cf, true, true>), g, dim3(Cf::NT), 0, stream, a, kchunk);
+  }
+}
+
+template <class Cf>
+static void launch_pp(const DphGemmArgs& a, hipStream_t stream) {
+  const dim3 g((unsigned)cdiv(a.N, Cf::BN), (unsigned)cdiv(a.M, Cf::BM), (unsigned)a.batch), b(Cf::NT);
+  const bool drop = a.dropout_p > 0.f;
+  if (a.act == DPH_ACT_GELU) {
+    if (drop) hipLaunchKernelGGL((pp::pp_gemm_kernel<Cf, DPH_ACT_GELU, true>), g, b, 0, stream, a);
+    else hipLaunchKernelGGL((pp::pp_gemm_kernel<Cf, DPH_ACT_GELU, false>), g, b, 0, stream, a);
+  } else if (a.act == DPH_ACT_GELU_BWD) {
+    if (drop) hipLaunchKernelGGL((pp::pp_gemm_kernel<Cf, DPH_ACT_GELU_BWD, true>), g, b, 0, stream, a);
+    else hipLaunchKernelGGL((pp::pp_gemm_kernel<Cf, DPH_ACT_GELU_BWD, false>), g, b, 0, stream, a);
+  } else {
+    if (drop) hipLaunchKernelGGL((pp::pp_gemm_kernel<Cf, DPH_ACT_NONE, true>), g, b, 0, stream, a);
+    else hipLaunchKernelGGL((pp::pp_gemm_kernel<Cf, DPH_ACT_NONE, false>), g, b, 0, stream, a);
   }
 }
 
@@ -1989,7 +2354,14 @@ extern "C" int dph_gemm(const DphGemmArgs* args, hipStream_t stream) {
   // when there are >= ~2 full rounds of tiles over the 256 CUs at one block per CU, else the
   // 128x128 tile (DPH_GEMM_PATH=small|big|mid forces a path, for tests)
   const int kind = gemm_kind(a, kchunk);
-  if (kind == 10) {
+  if (kind >= 12 && kind <= 16) {
+    DPH_REQUIRE(cdiv(a.M, 128) < 65536 && a.batch < 65536, "dph_gemm: grid too large");
+    if (kind == 12) launch_pp<pp::P256>(a, stream);
+    else if (kind == 13) launch_pp<pp::P128x256>(a, stream);
+    else if (kind == 14) launch_pp<pp::P256x128>(a, stream);
+    else if (kind == 15) launch_pp<pp::P128x192>(a, stream);
+    else launch_pp<pp::P128>(a, stream);
+  } else if (kind == 10) {
     DPH_REQUIRE(cdiv(a.M, ring::Tri::BM) < 65536 && a.batch * a.splits < 65536, "dph_gemm: grid too large");
     if (!launch_ring_persist<ring::Tri>(a, stream)) launch_ring<ring::Tri, false>(a, kchunk, stream);
   } else if (kind == 8) {

@@ -10,11 +10,11 @@ torch.manual_seed(0)
 
 
 @pytest.fixture(autouse=True, params=["small", "mid", "big", "wide", "flat", "flat-np", "tall", "half", "mid8",
-                                     "mid8mn", "tri", "tri-np"])
+                                     "mid8mn", "tri", "tri-np", "pp256", "pp128x256", "pp256x128", "pp128x192", "pp128"])
 def gemm_path(request, monkeypatch):
     """Run every test on each GEMM path: the 128x128 register-staged kernel and the 128x128 /
     256x256 / 256x128 / 128x256 / 256x64 / 192x128 LDS-DMA ring kernels (taken where their constraints hold: both operands
-    k-contiguous, K % 32 == 0)."""
+    k-contiguous, K % 32 == 0), and the ping-pong kernels (both operands k-contiguous, K % 64 == 0, K >= 128)."""
     path = request.param
     if path.endswith("-np"):            # one tile per block instead of the persistent grid
         monkeypatch.setenv("DPH_GEMM_PERSIST", "0")
