@@ -4,6 +4,7 @@
 # phases (default: parity tests smoke bench prof):
 #   parity  -- tests/test_parity_gpu.py with -s (per-fixture error tables), all cases run; a failure ends the script
 #   tests   -- the whole -m gpu suite, -x
+#   testsall -- the whole -m gpu suite without -x (every failure listed; a failing test does not end the script)
 #   smoke   -- __graft_entry__.smoke()
 #   bench   -- bench.py default line (PMC traffic passes + CPU baseline)
 #   prof    -- rocprofv3 --kernel-trace --stats of a short bench run -> kernel_stats.csv
@@ -45,6 +46,10 @@ for P in $PHASES; do
     tests)
       timeout -k 10 900 $PYT tests -m gpu -x -q > "$O/pytest_gpu.log" 2>&1 || { tail -40 "$O/pytest_gpu.log"; exit 1; }
       tail -3 "$O/pytest_gpu.log" ;;
+    testsall)
+      timeout -k 10 900 $PYT tests -m gpu -q > "$O/pytest_gpu.log" 2>&1; rc=$?
+      grep -E "^(FAILED|ERROR)" "$O/pytest_gpu.log" | head -20; tail -2 "$O/pytest_gpu.log"
+      [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc ;;
     smoke)
       timeout -k 10 180 python -u __graft_entry__.py smoke > "$O/smoke.log" 2>&1 || { tail -30 "$O/smoke.log"; exit 1; }
       tail -1 "$O/smoke.log" ;;
