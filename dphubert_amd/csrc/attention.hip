@@ -433,6 +433,16 @@ __global__ void __launch_bounds__(256, 2) attn_fwd32_kernel(const bf16_t* __rest
   const int klen = (int)(key_len ? key_len[b] : sh.T);
   const uint32_t half_tp = (uint32_t)(T32 + 1) >> 1;
   const uint32_t hrow = ((uint32_t)(b * H + h) * (uint32_t)T32 + (uint32_t)q) * half_tp;
+  // a head whose sampled HardConcrete mask is exactly 0 (clamped, hardconcrete.py:99) contributes nothing and gets no
+  // gradient through its mask: the masked output is 0 and nothing else of it is read (the backward skips it too)
+  if (head_mask != nullptr && head_mask[h] == 0.f) {
+    if (q < T32) {
+      bf16_t* orow = o_m + ((int64_t)b * T32 + q) * (H * HD) + h * HD + 32 * hi;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) *reinterpret_cast<uint4*>(orow + 8 * c) = make_uint4(0, 0, 0, 0);
+    }
+    return;
+  }
   // Q' = scale * q as the B operand: qf[t] = Q'[q][16 t + 8 hi + 0..7]
   bf16x8_t qf[4];
 #pragma unroll
@@ -603,7 +613,11 @@ __global__ void __launch_bounds__(256) attn_bwd_prep_kernel(const bf16_t* __rest
   const int64_t h = blockIdx.y;
   const int64_t bt = (int64_t)blockIdx.x * 256 + threadIdx.x;
   float rd = 0.f;
-  if (bt < B * T) {
+  const float hmh = head_mask ? head_mask[h] : 1.0f;
+  if (bt < B * T && hmh == 0.f) {
+    // skipped head (attn_fwd32_kernel): its unmasked output was never written
+    Dv[(bt / T * H + h) * T + bt % T] = 0.f;
+  } else if (bt < B * T) {
     const bf16_t* a = dom + bt * H * HD + h * HD;
     const float* c = ou + bt * H * HD + h * HD;
 #pragma unroll
@@ -1124,6 +1138,22 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_kernel(const bf16_t* __restri
                                                        int mode) {
   const int z = (int)blockIdx.z;
   const bool kv = mode == 1 || (mode == 0 && z < nbz);
+  if constexpr (!BIAS) {
+    // head with an exactly-zero mask (skipped by the forward): its q / k / v gradients are 0
+    const int64_t h = blockIdx.y;
+    if (head_mask != nullptr && head_mask[h] == 0.f) {
+      const int64_t T = sh.T, H = sh.H, RS = sh.RS;
+      const int64_t b = kv ? z : (mode == 0 ? z - nbz : z);
+      const int64_t r0 = (int64_t)blockIdx.x * RB;
+      for (int c = threadIdx.x; c < RB * 8 * (kv ? 2 : 1); c += 256) {
+        const int64_t r = r0 + (c >> 3) % RB;
+        const int sel = kv ? 1 + (c >> 3) / RB : 0;
+        if (r < T)
+          *reinterpret_cast<uint4*>(dqkv + (b * T + r) * RS + (sel * H + h) * HD + (c & 7) * 8) = make_uint4(0, 0, 0, 0);
+      }
+      return;
+    }
+  }
   if (kv)
     attn_bwd_dkv_body<DROP, BIAS, KEEP>(qkv, dom, head_mask, lse, Dv, dqkv, key_len, sh, scale, drop_p, seed, rb,
                                         keep_in, (int)blockIdx.x, blockIdx.y, z);

@@ -745,6 +745,13 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(const DphGemmArgs a, int64_
 #ifndef DPH_MID8_MINB
 #define DPH_MID8_MINB 2     // blocks per CU of the 8-wave 128 x 128 tile (A/B builds: 1)
 #endif
+// internal epilogue variant: DPH_ACT_GELU under DPH_GEMM_PRE_DGK (pre_out stores gelu'(pre)*mask*keep/(1-p))
+constexpr int ACT_GELU_DGKPRE = 16;
+// internal DphGemmArgs.flags bit set by dph_gemm: the register epilogue writes its per-wave column sums to a
+// workspace slab [2][cdiv(M, WTM)][N] (summed by colsum_slab_reduce_kernel) instead of one same-address float
+// atomic per column per wave (126 -- 2000 adders per address on the FFN / conv input-gradient GEMMs: the
+// atomics, not the MFMAs or the GELU', set those launches' time)
+constexpr int64_t GEMM_COLSUM_SLAB = (int64_t)1 << 20;
 namespace ring {
 constexpr int KS = 32;      // k per slice
 constexpr int NSLOT = 4;
@@ -930,16 +937,17 @@ __device__ __forceinline__ void mfma_slice(f32x4_t (&acc)[C::FM][C::FN], const F
 // main loop).  Every global input (bias / colmask per column group, aux / residual per element) is
 // issued before the first store, so the wait on them never covers a store (gfx9 counts stores in
 // vmcnt).  Preconditions (direct_epi_ok): N % 4 == 0 (a 4-column group is wholly inside or outside N),
-// C rows addressed as m * row_stride (no rows_per_batch), 4-element aligned strides, 16-B aligned
+// C rows addressed as m * row_stride or by the batched row layout, 4-element aligned strides, 16-B aligned
 // pointers, at most one of aux_in / residual, M * N and the row-length segments within 32 bits.
 __host__ __device__ __forceinline__ bool direct_epi_ok(const DphGemmArgs& a) {
   const int64_t calign = a.C.row_stride | a.C.batch_stride | a.C.z_outer | a.C.z_inner | a.N | a.vec_z_inner;
   const uintptr_t palign = reinterpret_cast<uintptr_t>(a.C.ptr) | reinterpret_cast<uintptr_t>(a.pre_out) |
                            reinterpret_cast<uintptr_t>(a.aux_in) | reinterpret_cast<uintptr_t>(a.residual) |
                            reinterpret_cast<uintptr_t>(a.bias) | reinterpret_cast<uintptr_t>(a.colmask);
-  return (calign & 3) == 0 && (palign & 15) == 0 && !(a.aux_in && a.residual) && a.C.rows_per_batch == 0 &&
+  const bool dgk = a.act == DPH_ACT_GELU_BWD_DGK;
+  return (calign & 3) == 0 && (palign & 15) == 0 && (dgk ? (a.aux_in && a.residual) : !(a.aux_in && a.residual)) &&
          a.M < ((int64_t)1 << 31) && (!a.row_len || a.len_rows > 0) &&
-         (a.act == DPH_ACT_GELU_BWD || (!a.colsum_out && !a.colsum_aux));   // column sums: GELU_BWD only
+         (a.act == DPH_ACT_GELU_BWD || dgk || (!a.colsum_out && !a.colsum_aux));   // column sums: GELU backward only
 }
 
 __device__ __forceinline__ void unpack_bf16x4(const uint2 r, float (&o)[4]) {
@@ -973,14 +981,28 @@ __device__ __forceinline__ bool direct_epi_t(const DphGemmArgs& a, int64_t z, in
   const bool nfull = nw + C::WTN <= N;          // wave-uniform: every column group in range
   const bool mfull = mw + C::WTM <= a.M;
   const int64_t voff = (a.C.z_div > 0 ? (z % a.C.z_div) : z) * a.vec_z_inner;
-  const int64_t base = z_addr(a.C, z) + (int64_t)ml * rs + nl;      // element offset of fragment (0, 0)
+  // element offset of fragment row i (columns nl..): rows m * row_stride, or the batched row layout
+  // (b = m / rows_per_batch: the conv input-gradient phase GEMMs write every other row of each utterance)
+  const bool rpb = a.C.rows_per_batch > 0;
+  const int64_t zb = z_addr(a.C, z) + nl;
   const int64_t rstep = 16 * rs;
+  const int64_t r0off = rpb ? 0 : (int64_t)ml * rs;
+  // (the lean copy never has a batched row layout: its rows are a plain stride, no division per row)
+  auto roff = [&](int i, auto ck) -> int64_t {
+    if constexpr (decltype(ck)::value)
+      return zb + (rpb ? row_addr32(a.C, (uint32_t)(ml + 16 * i)) : r0off + i * rstep);
+    else
+      return zb + r0off + i * rstep;
+  };
+  const int64_t base = zb + r0off;   // (rpb == 0)
   // (arithmetic select of the two pointer VALUES, as in tile_epi_rows)
   const uintptr_t ax_p = reinterpret_cast<uintptr_t>(a.aux_in), rs_p = reinterpret_cast<uintptr_t>(a.residual);
   const bf16_t* inp = reinterpret_cast<const bf16_t*>(ax_p | (rs_p & (uintptr_t)(-(intptr_t)(ax_p == 0))));
   const bool has_in = inp != nullptr, has_res = has_in && ax_p == 0;
-  // (column sums are compiled for the GELU_BWD variants only: the only GEMMs that request them)
-  const bool colsum = ACT == DPH_ACT_GELU_BWD && (a.colsum_out || a.colsum_aux);
+  // (column sums are compiled for the GELU backward variants only: the only GEMMs that request them)
+  constexpr bool BWD = ACT == DPH_ACT_GELU_BWD || ACT == DPH_ACT_GELU_BWD_DGK;
+  constexpr bool DGK = ACT == DPH_ACT_GELU_BWD_DGK;
+  const bool colsum = BWD && (a.colsum_out || a.colsum_aux);
   // per-column factors: bias, csm = colmask * layer mask
   float bias[FN][4], csm[FN][4];
   const float sm = a.smask ? *a.smask : 1.0f;
@@ -994,20 +1016,31 @@ __device__ __forceinline__ bool direct_epi_t(const DphGemmArgs& a, int64_t z, in
     bias[j][0] = b.x; bias[j][1] = b.y; bias[j][2] = b.z; bias[j][3] = b.w;
     csm[j][0] = c.x * sm; csm[j][1] = c.y * sm; csm[j][2] = c.z * sm; csm[j][3] = c.w * sm;
   }
+  if constexpr (DGK) {
+    // the mask gradient divides the stored forward output by its column mask (f = gelu * mask * keep/(1-p))
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) csm[j][r] = csm[j][r] != 0.f ? 1.0f / csm[j][r] : 0.f;
+  }
   const float inv_keep = DROP ? 1.0f / (1.0f - a.dropout_p) : 1.0f;
   const uint32_t thr = DROP ? drop_thr(a.dropout_p) : 0u;
   const uint64_t seed = DROP ? epoch_seed(a.seed) : 0;
   // per-element inputs of every fragment, issued together
   // (loaded two rows ahead inside the fragment loop: at most two rows of inputs are live, 16 VGPRs
   // instead of 32 -- the persistent kernel's GELU_BWD variant spilled with all of them preloaded)
-  uint2 in[FM][FN];
-  const bf16_t* ib = inp + base;
-  auto load_in = [&](int i) {
+  uint2 in[FM][FN], in2[DGK ? FM : 1][DGK ? FN : 1];
+  (void)base;
+  const bf16_t* inp2 = reinterpret_cast<const bf16_t*>(rs_p);      // DGK: the forward's output f
+  auto load_in = [&](int i, auto ck) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       in[i][j] = make_uint2(0, 0);
-      if (has_in && (mfull || ml + 16 * i < M) && (nfull || nl + 16 * j < N))
-        in[i][j] = *reinterpret_cast<const uint2*>(ib + i * rstep + 16 * j);
+      if constexpr (DGK) in2[i][j] = make_uint2(0, 0);
+      if (has_in && (mfull || ml + 16 * i < M) && (nfull || nl + 16 * j < N)) {
+        in[i][j] = *reinterpret_cast<const uint2*>(inp + roff(i, ck) + 16 * j);
+        if constexpr (DGK) in2[i][j] = *reinterpret_cast<const uint2*>(inp2 + roff(i, ck) + 16 * j);
+      }
     }
   };
   // rows past their row_len segment store zeros: 32-bit segment / remainder of the first row, stepped by 16
@@ -1030,9 +1063,8 @@ __device__ __forceinline__ bool direct_epi_t(const DphGemmArgs& a, int64_t z, in
 #pragma unroll
     for (int r = 0; r < 4; ++r) cso[j][r] = csa[j][r] = 0.f;
   const bool out_bf16 = a.c_dtype == DPH_OUT_BF16, accum = a.c_dtype == DPH_OUT_F32_ACCUM;
-  char* cb = reinterpret_cast<char*>(a.C.ptr) + base * (out_bf16 ? 2 : 4);
-  char* pb = reinterpret_cast<char*>(a.pre_out) + base * 2;
-  const int64_t cstep = rstep * (out_bf16 ? 2 : 4), pstep = rstep * 2;
+  char* cb = reinterpret_cast<char*>(a.C.ptr);
+  char* pb = reinterpret_cast<char*>(a.pre_out);
   const uint64_t e_base = ((uint64_t)(z * a.M + a.drop_row_offset + ml)) * (uint64_t)N + (uint64_t)nl;
   // CK: bounds and zero-row checks, any output type (edge tiles, row_len, fp32 outputs); interior tiles
   // with a bf16 output run the check-free copy
@@ -1042,19 +1074,21 @@ __device__ __forceinline__ bool direct_epi_t(const DphGemmArgs& a, int64_t z, in
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
       if (i == 0) {
-        load_in(0);
-        if (FM > 1) load_in(1);
+        load_in(0, ck);
+        if (FM > 1) load_in(1, ck);
       }
-      if (i + 2 < FM) load_in(i + 2);
+      if (i + 2 < FM) load_in(i + 2, ck);
       if (CK && !mfull && ml + 16 * i >= M) continue;
       const bool zero_row = CK && ((zrow >> i) & 1u);
-      char* crow = cb + i * cstep;
-      char* prow = pb + i * pstep;
+      const int64_t ro = roff(i, ck);
+      char* crow = cb + ro * (obf ? 2 : 4);
+      char* prow = pb + ro * 2;
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         if (CK && !nfull && nl + 16 * j >= N) continue;
-        float v[4], pre[4], ax[4], xin[4];
+        float v[4], pre[4], ax[4], xin[4], xin2[4];
         unpack_bf16x4(in[i][j], xin);
+        if constexpr (DGK) unpack_bf16x4(in2[i][j], xin2);
         uint32_t keep = 0xfu;
         if constexpr (DROP) {
           // element e_base + 16 i N + 16 j is even (N % 4 == 0, n % 4 == 0): pairs e/2 and e/2 + 1
@@ -1070,6 +1104,16 @@ __device__ __forceinline__ bool direct_epi_t(const DphGemmArgs& a, int64_t z, in
           ax[r] = 0.f;
           if constexpr (ACT == DPH_ACT_GELU) {
             v[r] = k ? gelu_f(pre[r]) * (csm[j][r] * inv_keep) : 0.f;
+          } else if constexpr (ACT == ACT_GELU_DGKPRE) {
+            // the stored "pre" is the backward's factor gelu'(pre) * mask * keep / (1 - p)
+            float g, dg;
+            gelu_and_grad(pre[r], g, dg);
+            const float kk = k ? csm[j][r] * inv_keep : 0.f;
+            v[r] = g * kk;
+            pre[r] = dg * kk;
+          } else if constexpr (DGK) {
+            ax[r] = pre[r] * xin2[r] * csm[j][r];
+            v[r] = pre[r] * xin[r];
           } else if constexpr (ACT == DPH_ACT_GELU_BWD) {
             const float gz = DROP ? (k ? pre[r] * inv_keep : 0.f) : pre[r];
             float g, dg;
@@ -1079,15 +1123,15 @@ __device__ __forceinline__ bool direct_epi_t(const DphGemmArgs& a, int64_t z, in
           } else {
             v[r] = DROP ? (k ? pre[r] * (csm[j][r] * inv_keep) : 0.f) : pre[r] * csm[j][r];
           }
-          // residual: xin is zero without one (GELU_BWD's xin is its aux input, never a residual)
-          if constexpr (ACT != DPH_ACT_GELU_BWD) v[r] += xin[r];
+          // residual: xin is zero without one (the backward variants' xin is their aux input, never a residual)
+          if constexpr (!BWD) v[r] += xin[r];
           if (CK) v[r] = zero_row ? 0.f : v[r];
         }
         if (colsum) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             cso[j][r] += v[r];
-            if constexpr (ACT == DPH_ACT_GELU_BWD) csa[j][r] += ax[r];   // (not zeroed on zero rows, as epilogue8)
+            if constexpr (BWD) csa[j][r] += ax[r];   // (not zeroed on zero rows, as epilogue8)
           }
         }
 #ifdef DPH_EPI_NOSTORE
@@ -1108,19 +1152,36 @@ __device__ __forceinline__ bool direct_epi_t(const DphGemmArgs& a, int64_t z, in
       }
     }
   };
-  const bool lean = mfull && nfull && !a.row_len && out_bf16;
+  const bool lean = mfull && nfull && !a.row_len && out_bf16 && !rpb;
   if (lean) frags(std::false_type{});
   else frags(std::true_type{});
   if (colsum) {
-    // one atomic per column per wave: lanes 0, 16, 32, 48 hold the sums of their 4-column groups
+    // lanes 0, 16, 32, 48 hold the sums of their 4-column groups: one slab entry (COLSUM_SLAB: slab row
+    // mw / WTM, summed by colsum_slab_reduce_kernel) or one atomic per column per wave
 #pragma unroll
     for (int j = 0; j < FN; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         cso[j][r] = row16_sum(cso[j][r]);
-        if constexpr (ACT == DPH_ACT_GELU_BWD) csa[j][r] = row16_sum(csa[j][r]);
+        if constexpr (BWD) csa[j][r] = row16_sum(csa[j][r]);
       }
-    if ((lane & 15) == 0) {
+    if ((lane & 15) == 0 && (a.flags & GEMM_COLSUM_SLAB)) {
+      const int64_t csn = min(a.colsum_n > 0 ? a.colsum_n : N, N);
+      if (mw < a.M) {
+        const int64_t nslots = cdiv(a.M, (int64_t)C::WTM);
+        float* wo = reinterpret_cast<float*>(a.workspace) + (mw / C::WTM) * N;
+        float* wa = wo + nslots * N;
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int64_t n = nl + 16 * j + r;
+            if (n >= csn) continue;
+            wo[n] = cso[j][r];
+            if constexpr (BWD) wa[n] = csa[j][r];
+          }
+      }
+    } else if ((lane & 15) == 0) {
       const int64_t csn = a.colsum_n > 0 ? a.colsum_n : N;
 #pragma unroll
       for (int j = 0; j < FN; ++j)
@@ -1129,7 +1190,7 @@ __device__ __forceinline__ bool direct_epi_t(const DphGemmArgs& a, int64_t z, in
           const int64_t n = nl + 16 * j + r;
           if (n >= csn || n >= N) continue;
           if (a.colsum_out) atomicAdd(a.colsum_out + voff + n, cso[j][r]);
-          if (ACT == DPH_ACT_GELU_BWD && a.colsum_aux) atomicAdd(a.colsum_aux + voff + n, csa[j][r]);
+          if (BWD && a.colsum_aux) atomicAdd(a.colsum_aux + voff + n, csa[j][r]);
         }
     }
   }
@@ -2044,6 +2105,34 @@ __global__ void __launch_bounds__(C::NT, C::WPE) pp_gemm_kernel(const DphGemmArg
 }
 }  // namespace pp
 
+// out[c] += sum_r slab[r][c] (out) and aux[c] += sum_r slab[nrows + r][c]: 64 columns x 4 row phases per block
+// over one of gridDim.y (<= 8) row groups, one atomic per column per group
+__global__ void __launch_bounds__(256) colsum_slab_reduce_kernel(const float* __restrict__ slab, int64_t nrows,
+                                                                 int64_t ncols, int64_t csn, float* __restrict__ out,
+                                                                 float* __restrict__ aux) {
+  __shared__ float red[2][4][64];
+  const int tx = threadIdx.x & 63;
+  const int ty = threadIdx.x >> 6;
+  const int64_t col = (int64_t)blockIdx.x * 64 + tx;
+  const int64_t per = cdiv(nrows, (int64_t)gridDim.y);
+  const int64_t ra = (int64_t)blockIdx.y * per;
+  const int64_t rb = min(nrows, ra + per);
+  float so = 0.f, sa = 0.f;
+  if (col < csn) {
+    for (int64_t r = ra + ty; r < rb; r += 4) {
+      so += slab[r * ncols + col];
+      sa += slab[(nrows + r) * ncols + col];
+    }
+  }
+  red[0][ty][tx] = so;
+  red[1][ty][tx] = sa;
+  __syncthreads();
+  if (ty == 0 && col < csn) {
+    if (out) atomicAdd(out + col, red[0][0][tx] + red[0][1][tx] + red[0][2][tx] + red[0][3][tx]);
+    if (aux) atomicAdd(aux + col, red[1][0][tx] + red[1][1][tx] + red[1][2][tx] + red[1][3][tx]);
+  }
+}
+
 // split-K reduction + epilogue: one thread per 8 columns of a row
 __global__ void splitk_reduce_kernel(const DphGemmArgs a) {
   const int64_t z = blockIdx.z;
@@ -2102,7 +2191,7 @@ static bool tri_ok(const DphGemmArgs& a) {
 static int num_cus();
 
 // the ping-pong kernels: both operands k-contiguous with 16-B aligned rows, whole 64-deep K-tiles (at least
-// two), register-epilogue layouts, DMA source offsets within 32 bits
+// two: the prologue stages two), register-epilogue layouts, DMA source offsets within 32 bits
 static bool pp_ok(const DphGemmArgs& a) {
   if (!(a.splits == 1 && a.a_kcontig && a.b_kcontig && a.K % pp::BK == 0 && a.K >= 2 * pp::BK &&
         ring::direct_epi_ok(a)))
@@ -2221,7 +2310,8 @@ static bool persist_ok(const DphGemmArgs& a);
 extern "C" const char* dph_gemm_variant(const DphGemmArgs* args) {
   if (!args) return "";
   const DphGemmArgs& a = *args;
-  const int kind = gemm_kind(a, gemm_kchunk(a));
+  const bool dgk = a.act == DPH_ACT_GELU_BWD_DGK || (a.act == DPH_ACT_GELU && (a.flags & DPH_GEMM_PRE_DGK));
+  const int kind = dgk ? pp_pick(a) : gemm_kind(a, gemm_kchunk(a));
   if (kind == 12) return "pp_gemm_kernel<dph::(anonymous namespace)::pp::Cfg<256, 256>";
   if (kind == 13) return "pp_gemm_kernel<dph::(anonymous namespace)::pp::Cfg<128, 256>";
   if (kind == 14) return "pp_gemm_kernel<dph::(anonymous namespace)::pp::Cfg<256, 128>";
@@ -2267,7 +2357,12 @@ template <class Cf>
 static void launch_pp(const DphGemmArgs& a, hipStream_t stream) {
   const dim3 g((unsigned)cdiv(a.N, Cf::BN), (unsigned)cdiv(a.M, Cf::BM), (unsigned)a.batch), b(Cf::NT);
   const bool drop = a.dropout_p > 0.f;
-  if (a.act == DPH_ACT_GELU) {
+  if (a.act == DPH_ACT_GELU_BWD_DGK) {
+    hipLaunchKernelGGL((pp::pp_gemm_kernel<Cf, DPH_ACT_GELU_BWD_DGK, false>), g, b, 0, stream, a);
+  } else if (a.act == DPH_ACT_GELU && (a.flags & DPH_GEMM_PRE_DGK)) {
+    if (drop) hipLaunchKernelGGL((pp::pp_gemm_kernel<Cf, ACT_GELU_DGKPRE, true>), g, b, 0, stream, a);
+    else hipLaunchKernelGGL((pp::pp_gemm_kernel<Cf, ACT_GELU_DGKPRE, false>), g, b, 0, stream, a);
+  } else if (a.act == DPH_ACT_GELU) {
     if (drop) hipLaunchKernelGGL((pp::pp_gemm_kernel<Cf, DPH_ACT_GELU, true>), g, b, 0, stream, a);
     else hipLaunchKernelGGL((pp::pp_gemm_kernel<Cf, DPH_ACT_GELU, false>), g, b, 0, stream, a);
   } else if (a.act == DPH_ACT_GELU_BWD) {
@@ -2353,14 +2448,45 @@ extern "C" int dph_gemm(const DphGemmArgs* args, hipStream_t stream) {
   // LDS-DMA ring kernels for k-contiguous A and B with whole 32-deep k-slices: the 256x256 tile
   // when there are >= ~2 full rounds of tiles over the 256 CUs at one block per CU, else the
   // 128x128 tile (DPH_GEMM_PATH=small|big|mid forces a path, for tests)
-  const int kind = gemm_kind(a, kchunk);
+  // the DGK GELU pair (stored gelu' factor / f) exists in the ping-pong kernels' register epilogue only
+  const bool dgk = a.act == DPH_ACT_GELU_BWD_DGK || (a.act == DPH_ACT_GELU && (a.flags & DPH_GEMM_PRE_DGK));
+  if (dgk) {
+    DPH_REQUIRE(pp_ok(a), "dph_gemm: DPH_ACT_GELU_BWD_DGK / DPH_GEMM_PRE_DGK need the ping-pong layout "
+                "(k-contiguous A and B, K %% 64 == 0, dense aligned C): M=%lld N=%lld K=%lld act=%d direct=%d "
+                "A(rs=%lld ptr%%16=%d) B(rs=%lld ptr%%16=%d) C(rs=%lld ptr%%16=%d) aux%%16=%d res%%16=%d pre%%16=%d",
+                (long long)a.M, (long long)a.N, (long long)a.K, a.act, (int)ring::direct_epi_ok(a),
+                (long long)a.A.row_stride, (int)(reinterpret_cast<uintptr_t>(a.A.ptr) & 15), (long long)a.B.row_stride,
+                (int)(reinterpret_cast<uintptr_t>(a.B.ptr) & 15), (long long)a.C.row_stride,
+                (int)(reinterpret_cast<uintptr_t>(a.C.ptr) & 15), (int)(reinterpret_cast<uintptr_t>(a.aux_in) & 15),
+                (int)(reinterpret_cast<uintptr_t>(a.residual) & 15), (int)(reinterpret_cast<uintptr_t>(a.pre_out) & 15));
+    DPH_REQUIRE(a.act != DPH_ACT_GELU_BWD_DGK || (a.dropout_p == 0.f && !a.smask && !a.pre_out),
+                "dph_gemm: DPH_ACT_GELU_BWD_DGK takes no dropout / smask / pre_out");
+    DPH_REQUIRE(a.act != DPH_ACT_GELU || a.pre_out, "dph_gemm: DPH_GEMM_PRE_DGK needs pre_out");
+  }
+  const int kind = dgk ? pp_pick(a) : gemm_kind(a, kchunk);
   if (kind >= 12 && kind <= 16) {
     DPH_REQUIRE(cdiv(a.M, 128) < 65536 && a.batch < 65536, "dph_gemm: grid too large");
-    if (kind == 12) launch_pp<pp::P256>(a, stream);
-    else if (kind == 13) launch_pp<pp::P128x256>(a, stream);
-    else if (kind == 14) launch_pp<pp::P256x128>(a, stream);
-    else if (kind == 15) launch_pp<pp::P128x192>(a, stream);
-    else launch_pp<pp::P128>(a, stream);
+    // column sums through a workspace slab when the caller passed one (kernels.py does for splits == 1)
+    const int64_t wtm = (kind == 12 || kind == 14) ? 128 : 64;
+    const int64_t nslots = cdiv(a.M, wtm);
+    DphGemmArgs b = a;
+    const bool slab = (a.colsum_out || a.colsum_aux) && a.batch == 1 && a.workspace &&
+                      a.workspace_bytes >= 2 * nslots * a.N * 4;
+    if (slab) b.flags |= GEMM_COLSUM_SLAB;
+    if (kind == 12) launch_pp<pp::P256>(b, stream);
+    else if (kind == 13) launch_pp<pp::P128x256>(b, stream);
+    else if (kind == 14) launch_pp<pp::P256x128>(b, stream);
+    else if (kind == 15) launch_pp<pp::P128x192>(b, stream);
+    else launch_pp<pp::P128>(b, stream);
+    if (slab) {
+      int rc = check_launch("dph_gemm");
+      if (rc) return rc;
+      const int64_t csn = std::min<int64_t>(a.colsum_n > 0 ? a.colsum_n : a.N, a.N);
+      const unsigned groups = (unsigned)std::max<int64_t>(1, std::min<int64_t>(8, cdiv(nslots, 64)));
+      hipLaunchKernelGGL(colsum_slab_reduce_kernel, dim3((unsigned)cdiv(csn, 64), groups), dim3(256), 0, stream,
+                         reinterpret_cast<const float*>(a.workspace), nslots, a.N, csn, a.colsum_out, a.colsum_aux);
+      return check_launch("dph_gemm colsum reduce");
+    }
   } else if (kind == 10) {
     DPH_REQUIRE(cdiv(a.M, ring::Tri::BM) < 65536 && a.batch * a.splits < 65536, "dph_gemm: grid too large");
     if (!launch_ring_persist<ring::Tri>(a, stream)) launch_ring<ring::Tri, false>(a, kchunk, stream);

@@ -23,7 +23,7 @@ __global__ void hc_fwd_kernel(const float* __restrict__ la, const float* __restr
   if (u_out) u_out[i] = u;
   const float s = 1.0f / (1.0f + __expf(-((__logf(u / (1.0f - u)) + la[i]) / beta)));
   const float v = s * (hi - lo) + lo;
-  mask[i] = fminf(fmaxf(v, 0.0f), 1.0f);
+  mask[i] = v == 0.0f ? __int_as_float(1) : fminf(fmaxf(v, 0.0f), 1.0f);   // (see hc_bank_fwd_kernel)
 }
 
 __global__ void hc_bwd_kernel(const float* __restrict__ la, const float* __restrict__ u, const float* __restrict__ dm,
@@ -68,7 +68,10 @@ __global__ void __launch_bounds__(256) hc_bank_fwd_kernel(BankArgs a, float* __r
   const float u = a.uin[e] ? a.uin[e][i] : eps + (1.0f - 2.0f * eps) * rand_uniform(seed, (uint64_t)f);
   u_flat[f] = u;
   const float v = hc_s(u, a.la[e][i], beta) * (hi - lo) + lo;
-  mask_flat[f] = fminf(fmaxf(v, 0.0f), 1.0f);
+  // (a pre-clamp value of exactly 0 still passes the clamp's gradient (closed interval, below): its mask is the
+  // smallest subnormal instead of 0, so "mask == 0" means "no gradient through this gate" and the attention
+  // kernels may skip such a head entirely)
+  mask_flat[f] = v == 0.0f ? __int_as_float(1) : fminf(fmaxf(v, 0.0f), 1.0f);
 }
 
 __global__ void __launch_bounds__(256) hc_bank_bwd_kernel(BankArgs a, const float* __restrict__ u_flat, float beta,

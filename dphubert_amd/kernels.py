@@ -18,7 +18,7 @@ BF16 = torch.bfloat16
 F32 = torch.float32
 _SPLITK_INLAUNCH = __import__("os").environ.get("DPH_SPLITK_INLAUNCH", "0") == "1"
 
-ACT_NONE, ACT_GELU, ACT_GELU_BWD = 0, 1, 2
+ACT_NONE, ACT_GELU, ACT_GELU_BWD, ACT_GELU_BWD_DGK = 0, 1, 2, 3
 OUT_BF16, OUT_F32, OUT_F32_ACCUM = 0, 1, 2
 
 
@@ -106,6 +106,7 @@ def _variant(args):
 
 
 GEMM_NO_PERSIST = 1            # DphGemmArgs.flags (include/dphubert_hip.h)
+GEMM_PRE_DGK = 2               # ACT_GELU: pre_out stores gelu'(pre)*colmask*keep/(1-p) (ACT_GELU_BWD_DGK's aux)
 _SHARED_GPU = [0]
 
 
@@ -125,7 +126,7 @@ def gemm(A: DphMat, B: DphMat, Cm: DphMat, M: int, N: int, K: int, *, a_kcontig:
          c_dtype: int = OUT_BF16, act: int = ACT_NONE, alpha: float = 1.0, batch: int = 1, splits: int = 1,
          bias=None, colmask=None, smask=None, vec_z_inner: int = 0, pre_out=None, aux_in=None, residual=None,
          colsum_out=None, colsum_aux=None, row_len=None, len_rows: int = 0, dropout_p: float = 0.0, seed: int = 0,
-         drop_row_offset: int = 0, colsum_n: int = 0, device=None):
+         drop_row_offset: int = 0, colsum_n: int = 0, device=None, flags: int = 0):
     ws = None
     ws_bytes = 0
     if splits > 1:
@@ -135,11 +136,16 @@ def gemm(A: DphMat, B: DphMat, Cm: DphMat, M: int, N: int, K: int, *, a_kcontig:
         n_el = batch * splits * M * N + tiles
         ws_bytes = n_el * 4
         ws = torch.empty(n_el, dtype=F32, device=device or "cuda")
+    elif (colsum_out is not None or colsum_aux is not None) and batch == 1:
+        # per-wave column-sum slab [2][ceil(M/64)][N] (dph_gemm sums it instead of same-address atomics)
+        n_el = 2 * ((M + 63) // 64) * N
+        ws_bytes = n_el * 4
+        ws = torch.empty(n_el, dtype=F32, device=device or Cm_device(colsum_out, colsum_aux))
     args = DphGemmArgs(M, N, K, batch, splits, int(a_kcontig), int(b_kcontig), A, B, Cm, c_dtype, act, alpha,
                        dropout_p, seed & 0xFFFFFFFFFFFFFFFF, ptr(bias), ptr(colmask), ptr(smask), vec_z_inner,
                        ptr(pre_out), ptr(aux_in), ptr(residual), ptr(colsum_out), ptr(colsum_aux), ptr(row_len),
                        len_rows, drop_row_offset, ptr(ws), ws_bytes, colsum_n,
-                       GEMM_NO_PERSIST if _SHARED_GPU[0] else 0)
+                       flags | (GEMM_NO_PERSIST if _SHARED_GPU[0] else 0))
     prof = LaunchProfiler.active
     if prof is not None:
         e0, e1 = _Event(), _Event()
@@ -158,6 +164,13 @@ def gemm(A: DphMat, B: DphMat, Cm: DphMat, M: int, N: int, K: int, *, a_kcontig:
     return ws  # keep alive until the stream consumes it (caching allocator is stream-ordered)
 
 
+def Cm_device(*ts):
+    for t in ts:
+        if t is not None:
+            return t.device
+    return "cuda"
+
+
 def choose_splits(M: int, N: int, K: int, batch: int = 1, target_blocks: int = 512) -> int:
     """Split-K factor so that the grid fills the 256 CUs (weight-gradient GEMMs)."""
     tiles = ((M + 127) // 128) * ((N + 127) // 128) * batch
@@ -169,8 +182,11 @@ def choose_splits(M: int, N: int, K: int, batch: int = 1, target_blocks: int = 5
 
 def linear_fwd(x: torch.Tensor, w_bf16: torch.Tensor, bias: Optional[torch.Tensor] = None, *, out=None,
                out_dtype=BF16, act=ACT_NONE, pre_out=None, colmask=None, smask=None, residual=None,
-               dropout_p=0.0, seed=0, row_len=None, len_rows=0, colsum_out=None):
-    """y = epi(x @ w^T + b); x [M,K] bf16, w [N,K] bf16 (nn.Linear layout)."""
+               dropout_p=0.0, seed=0, row_len=None, len_rows=0, colsum_out=None, pre_dgk=False):
+    """y = epi(x @ w^T + b); x [M,K] bf16, w [N,K] bf16 (nn.Linear layout).
+
+    ``pre_dgk`` (act=ACT_GELU): pre_out receives gelu'(pre)*colmask*keep/(1-p), the aux input of the matching
+    ACT_GELU_BWD_DGK input-gradient GEMM, instead of the pre-activation."""
     _chk(x, BF16, "x")
     _chk(w_bf16, BF16, "w")
     M, K = x.shape
@@ -180,7 +196,8 @@ def linear_fwd(x: torch.Tensor, w_bf16: torch.Tensor, bias: Optional[torch.Tenso
     c_dtype = OUT_BF16 if out.dtype == BF16 else OUT_F32
     gemm(dense(x), dense(w_bf16), dense(out), M, N, K, a_kcontig=True, b_kcontig=True, c_dtype=c_dtype, act=act,
          bias=bias, colmask=colmask, smask=smask, pre_out=pre_out, residual=residual, dropout_p=dropout_p,
-         seed=seed, row_len=row_len, len_rows=len_rows, colsum_out=colsum_out)
+         seed=seed, row_len=row_len, len_rows=len_rows, colsum_out=colsum_out,
+         flags=GEMM_PRE_DGK if pre_dgk else 0)
     return out
 
 

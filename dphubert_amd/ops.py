@@ -579,8 +579,16 @@ class HardConcreteBank:
         self.mods = list(mods)
         self.table = table
         self.sizes = [m.log_alpha.numel() for m in self.mods]
-        self.offsets = _offs(table) if table is not None else []
-        self.total = sum(self.sizes)
+        # each gate's slice of the flat u / mask / gradient buffers starts 16-B aligned: the masks are read as
+        # float4 column vectors by the GEMM register epilogues (a misaligned colmask sends a GEMM off the
+        # ping-pong kernels)
+        self.offsets, o = [], 0
+        for n in self.sizes:
+            self.offsets.append(o)
+            o += (n + 3) // 4 * 4
+        self.total = max(o, 1)
+        dev = table.offsets.device if table is not None else "cpu"
+        self.offsets_dev = torch.tensor(self.offsets or [0], dtype=torch.int64, device=dev)
 
     def noise(self, m):
         """Injected u of a gate (HardConcrete.set_noise) as a device fp32 tensor (converted once), or None."""
@@ -640,7 +648,7 @@ class HardConcreteBankFn(torch.autograd.Function):
             dst = [gflat.data_ptr() + 4 * sk[1] for sk in sinks]
         else:
             gflat = zeros_f32(bank.total, dev)
-            goff = table.offsets
+            goff = bank.offsets_dev
             dst = [gflat.data_ptr() + 4 * o for o in bank.offsets]
         if dnum is not None:
             call("dph_expected_params_bwd", ptr(table.ptr_table(las)), ptr(gflat), ptr(goff), ptr(table.sizes),
@@ -1320,6 +1328,24 @@ class RelPosTableFn(torch.autograd.Function):
         return go.ret(embed), None, None, None
 
 
+def _ffn_dgk(D: int) -> bool:
+    """The FFN intermediate GELU backward from factors the forward stores (K.GEMM_PRE_DGK / K.ACT_GELU_BWD_DGK):
+    the forward GEMM keeps gelu'(pre)*mask*keep/(1-p) instead of pre, so the input-gradient GEMM's epilogue is
+    two multiplies (no erfc, no dropout hash; the mask gradient from the stored output f / mask).  Needs the
+    ping-pong GEMM layout (K = D a multiple of 64, >= 128); DPH_FFN_DGK=0 keeps the recomputing epilogue (A/B)."""
+    return D % 64 == 0 and D >= 128 and os.environ.get("DPH_FFN_DGK", "1") != "0"
+
+
+def _ffn_interm_bwd(dy, sv, db1, dmask, cfg, F_):
+    """du = (dy @ W2) * gelu'(pre) * mask * keep/(1-p); db1 += colsum(du); dmask += colsum((dy @ W2) * gelu(pre) *
+    keep/(1-p)) (components.py:733-739 backward)."""
+    if sv["dgk"]:
+        return K.linear_dgrad(dy, sv["W2"], w_t=t_image(sv["W2"]), act=K.ACT_GELU_BWD_DGK, aux_in=sv["u"],
+                              residual=sv["f"], colmask=sv["imp"], colsum_out=db1, colsum_aux=dmask, colsum_n=F_)
+    return K.linear_dgrad(dy, sv["W2"], w_t=t_image(sv["W2"]), act=K.ACT_GELU_BWD, aux_in=sv["u"], colmask=sv["imp"],
+                          colsum_out=db1, colsum_aux=dmask, dropout_p=cfg["p_interm"], seed=sv["seed_i"], colsum_n=F_)
+
+
 class EncoderLayerFn(torch.autograd.Function):
     """h (B*T, D) bf16 -> layer output (B*T, D) bf16.
 
@@ -1378,12 +1404,13 @@ class EncoderLayerFn(torch.autograd.Function):
             b1p, imp = padded_vec(b1, Fp), padded_vec(im, Fp)
             seed_i = SEEDS.next() if cfg["p_interm"] > 0 else 0
             u = torch.empty(M, Fp, dtype=BF16, device=dev) if need else None
+            dgk = _ffn_dgk(D) and u is not None
             f = K.linear_fwd(h1, W1, b1p, act=K.ACT_GELU, pre_out=u, colmask=imp, dropout_p=cfg["p_interm"],
-                             seed=seed_i)
+                             seed=seed_i, pre_dgk=dgk)
             seed_o = SEEDS.next() if cfg["p_drop"] > 0 else 0
             y_pre = torch.empty(M, D, dtype=BF16, device=dev) if (need and lmf is not None) else None
             s2 = K.linear_fwd(f, W2, b2, smask=lmf, residual=h1, dropout_p=cfg["p_drop"], seed=seed_o, pre_out=y_pre)
-            sv.update(W1=W1, W2=W2, u=u, f=f, y_pre=y_pre, seed_i=seed_i, seed_o=seed_o, F=F_, imp=imp)
+            sv.update(W1=W1, W2=W2, u=u, f=f, y_pre=y_pre, seed_i=seed_i, seed_o=seed_o, F=F_, imp=imp, dgk=dgk)
         else:
             s2 = h1
         out = torch.empty_like(h)
@@ -1449,13 +1476,14 @@ class EncoderLayerFn(torch.autograd.Function):
             b1p, imp = padded_vec(b1, Fp), padded_vec(im, Fp)
             seed_i = SEEDS.next() if cfg["p_interm"] > 0 else 0
             u = torch.empty(M, Fp, dtype=BF16, device=dev) if need else None
+            dgk = _ffn_dgk(D) and u is not None
             f = K.linear_fwd(xn2, W1, b1p, act=K.ACT_GELU, pre_out=u, colmask=imp, dropout_p=cfg["p_interm"],
-                             seed=seed_i)
+                             seed=seed_i, pre_dgk=dgk)
             seed_o = SEEDS.next() if cfg["p_drop"] > 0 else 0
             y_pre = torch.empty(M, D, dtype=BF16, device=dev) if (need and lmf is not None) else None
             out = K.linear_fwd(f, W2, b2, smask=lmf, residual=s1, dropout_p=cfg["p_drop"], seed=seed_o,
                                pre_out=y_pre)
-            sv.update(W1=W1, W2=W2, u=u, f=f, y_pre=y_pre, seed_i=seed_i, seed_o=seed_o, F=F_, imp=imp)
+            sv.update(W1=W1, W2=W2, u=u, f=f, y_pre=y_pre, seed_i=seed_i, seed_o=seed_o, F=F_, imp=imp, dgk=dgk)
         else:
             out = s1.clone() if s1 is h else s1
         if need:
@@ -1495,9 +1523,7 @@ class EncoderLayerFn(torch.autograd.Function):
                 k1 = K.linear_wgrad(dy, sv["f"], dw2, accumulate=direct, k_in=F_)
             db1, _ = go.buf(pr["b1"])
             g["im"] = z(F_) if has_im else None
-            du = K.linear_dgrad(dy, sv["W2"], w_t=t_image(sv["W2"]), act=K.ACT_GELU_BWD, aux_in=sv["u"], colmask=sv["imp"], colsum_out=db1,
-                                colsum_aux=g["im"] if has_im else z(F_), dropout_p=cfg["p_interm"],
-                                seed=sv["seed_i"], colsum_n=F_)
+            du = _ffn_interm_bwd(dy, sv, db1, g["im"] if has_im else z(F_), cfg, F_)
             dw1, direct = go.buf(pr["w1"], zero=False)
             with wgrad_side(du, xn2, enable=direct):
                 k2 = K.linear_wgrad(du, xn2, dw1, accumulate=direct, n_out=F_)
@@ -1652,9 +1678,7 @@ class EncoderLayerFn(torch.autograd.Function):
                 k1 = K.linear_wgrad(dy, sv["f"], dw2, accumulate=direct, k_in=F_)
             db1, _ = go.buf(pr["b1"])
             g["im"] = z(F_) if has_im else None
-            du = K.linear_dgrad(dy, sv["W2"], w_t=t_image(sv["W2"]), act=K.ACT_GELU_BWD, aux_in=sv["u"], colmask=sv["imp"], colsum_out=db1,
-                                colsum_aux=g["im"] if has_im else z(F_), dropout_p=cfg["p_interm"],
-                                seed=sv["seed_i"], colsum_n=F_)
+            du = _ffn_interm_bwd(dy, sv, db1, g["im"] if has_im else z(F_), cfg, F_)
             dw1, direct = go.buf(pr["w1"], zero=False)
             with wgrad_side(du, h1, enable=direct):
                 k2 = K.linear_wgrad(du, h1, dw1, accumulate=direct, n_out=F_)

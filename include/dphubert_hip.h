@@ -59,6 +59,11 @@ typedef struct DphMat {
 #define DPH_ACT_NONE 0
 #define DPH_ACT_GELU 1      /* v = gelu(v), optional pre-activation store        */
 #define DPH_ACT_GELU_BWD 2  /* v = v*drop*colmask*gelu'(aux); colsum_aux += v*drop*gelu(aux) */
+/* GELU backward from what the forward stored: aux_in = the forward's pre_out under DPH_GEMM_PRE_DGK
+ * (gelu'(pre)*colmask*keep/(1-p)), residual = the forward's output f (gelu(pre)*colmask*keep/(1-p)):
+ * v = v*aux; colsum_aux += v*residual/colmask (0 where colmask == 0); colsum_out += stored v.
+ * No dropout / smask arguments (they are folded into aux).  Ping-pong layouts only (dph_gemm checks). */
+#define DPH_ACT_GELU_BWD_DGK 3
 
 #define DPH_OUT_BF16 0
 #define DPH_OUT_F32 1
@@ -98,6 +103,9 @@ typedef struct DphGemmArgs {
  * GPU with another stream's kernels (the teacher forward runs concurrently with the student forward):
  * a persistent grid sized to the CUs stalls on the CUs the other kernels hold, a tile grid rebalances */
 #define DPH_GEMM_NO_PERSIST 1
+/* DPH_ACT_GELU with pre_out: store gelu'(pre)*colmask*keep/(1-p) instead of pre (the aux input of the
+ * matching DPH_ACT_GELU_BWD_DGK input-gradient GEMM).  Ping-pong layouts only. */
+#define DPH_GEMM_PRE_DGK 2
 
 int dph_gemm(const DphGemmArgs* args, hipStream_t stream);
 /* name (as it appears in rocprof kernel names) of the kernel dph_gemm launches for these args */

@@ -208,3 +208,74 @@ def test_transposed_image_dgrad(R, C):
     ref = dy.float() @ img.float()
     close(a, ref, 1e-2)
     close(b, ref, 1e-2)
+
+
+@pytest.mark.parametrize("act", ["none", "gelu_bwd"])
+def test_batched_row_output(act):
+    """C in a batched row layout (the conv input-gradient phase GEMMs: rows m of utterance m // L land on every
+    other row of that utterance, odd phase) with the direct epilogue: GELU' of an aux input in the same layout,
+    column mask, column sums of the stored values and of the mask gradient."""
+    K_ = _k()
+    Bt, L, N, Kd = 3, 333, 192, 256
+    Lin = 2 * L + 1
+    M = Bt * L
+    A, W = rnd(M, Kd), rnd(N, Kd)
+    C = torch.zeros(Bt, Lin, N, device="cuda", dtype=torch.bfloat16)
+    aux = rnd(Bt, Lin, N)
+    cm = (torch.rand(N, device="cuda") > 0.3).float()
+    cso, csa = torch.zeros(N, device="cuda"), torch.zeros(N, device="cuda")
+    kw = {}
+    if act == "gelu_bwd":
+        kw = dict(act=K_.ACT_GELU_BWD, aux_in=aux.view(-1)[N:], colmask=cm, colsum_out=cso, colsum_aux=csa)
+    K_.gemm(K_.dense(A), K_.dense(W), K_.mat(C, 2 * N, rows_per_batch=L, batch_stride=Lin * N, offset=N), M, N, Kd,
+            a_kcontig=True, b_kcontig=True, **kw)
+    torch.cuda.synchronize()
+    y = (A.float() @ W.float().t()).view(Bt, L, N)
+    want = torch.zeros(Bt, Lin, N, device="cuda")
+    if act == "gelu_bwd":
+        z = aux.float()[:, 1:2 * L:2]
+        g = torch.nn.functional.gelu(z)
+        dg = torch.autograd.functional.jacobian(lambda t: torch.nn.functional.gelu(t).sum(), z)
+        v = y * dg * cm
+        want[:, 1:2 * L:2] = v
+        close(cso, v.sum((0, 1)), 2e-2)
+        close(csa, (y * g).sum((0, 1)), 2e-2)
+    else:
+        want[:, 1:2 * L:2] = y
+    close(C, want, 1e-2)
+    assert torch.count_nonzero(C[:, 0:2 * L + 1:2].float()) == 0      # even rows untouched
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_gelu_dgk_pair_matches_recompute(p):
+    """The stored-factor GELU pair (forward pre_out = gelu'(pre)*mask*keep/(1-p), backward v = (dy@W2) * that,
+    mask gradient = (dy@W2) * f / mask) against the recomputing pair (pre stored, GELU' and the dropout hash
+    recomputed in the backward epilogue) on the same inputs and dropout seed."""
+    K_ = _k()
+    M, D, F = 1000, 256, 392
+    x, w1, w2 = rnd(M, D), rnd(F, D, scale=0.1), rnd(D, F, scale=0.1)
+    b1 = torch.randn(F, device="cuda") * 0.1
+    cm = (torch.rand(F, device="cuda") + 0.2).clamp(max=1.0)
+    cm[::7] = 0.0
+    u = torch.empty(M, F, device="cuda", dtype=torch.bfloat16)
+    dgk = torch.empty_like(u)
+    f0 = K_.linear_fwd(x, w1, b1, act=K_.ACT_GELU, pre_out=u, colmask=cm, dropout_p=p, seed=77)
+    f1 = K_.linear_fwd(x, w1, b1, act=K_.ACT_GELU, pre_out=dgk, colmask=cm, dropout_p=p, seed=77, pre_dgk=True)
+    torch.cuda.synchronize()
+    # the same dropout pattern and GELU values (other tile paths may round an element differently by one ulp)
+    assert torch.equal(f0 == 0, f1 == 0)
+    close(f1, f0, 1e-3)
+    dy = rnd(M, D)
+    w2t = w2.t().contiguous()
+    cs0, ca0 = torch.zeros(F, device="cuda"), torch.zeros(F, device="cuda")
+    cs1, ca1 = torch.zeros(F, device="cuda"), torch.zeros(F, device="cuda")
+    d0 = K_.linear_dgrad(dy, w2, w_t=w2t, act=K_.ACT_GELU_BWD, aux_in=u, colmask=cm, colsum_out=cs0, colsum_aux=ca0,
+                         dropout_p=p, seed=77)
+    d1 = K_.linear_dgrad(dy, w2, w_t=w2t, act=K_.ACT_GELU_BWD_DGK, aux_in=dgk, residual=f1, colmask=cm,
+                         colsum_out=cs1, colsum_aux=ca1)
+    torch.cuda.synchronize()
+    close(d1, d0, 1e-2)
+    close(cs1, cs0, 1e-2)
+    live = cm != 0
+    close(ca1[live], ca0[live], 2e-2)
+    assert torch.count_nonzero(ca1[~live]) == 0

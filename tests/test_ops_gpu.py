@@ -39,11 +39,14 @@ def _model(cfg, seed=0):
     return m.to(DEV), sd
 
 
+@pytest.mark.parametrize("zero_head", [False, True])
 @pytest.mark.parametrize("fwd", ["1", "2"])           # 32x32x16 forward (default) / 16x16x32 forward
 @pytest.mark.parametrize("T,short,amp", [(131, 97, 0.5), (499, 311, 0.5), (499, 499, 3.0)])
-def test_attention_kernel_vs_torch(fwd, T, short, amp, monkeypatch):
+def test_attention_kernel_vs_torch(fwd, T, short, amp, zero_head, monkeypatch):
     """amp = 3: scores spread over ~+-40, so row maxima jump by more than the deferred-rescale threshold
-    between key tiles of the 32x32 forward."""
+    between key tiles of the 32x32 forward.  zero_head: head 1's mask is exactly 0 (a clamped HardConcrete gate):
+    the kernels skip it -- masked output and q / k / v gradients exactly 0, no head-mask gradient (its gate passes
+    none: hardconcrete.py:99), the other heads unchanged."""
     from dphubert_amd import _lib
     from dphubert_amd._lib import call, ptr
     monkeypatch.setenv("DPH_ATTN_FWD", fwd)
@@ -52,6 +55,9 @@ def test_attention_kernel_vs_torch(fwd, T, short, amp, monkeypatch):
     D = H * 64
     qkv = (torch.randn(B * T, 3 * D, device=DEV) * amp).to(torch.bfloat16)
     hm = torch.rand(H, device=DEV)
+    if zero_head:
+        hm[1] = 0.0
+    live = (hm != 0).view(1, H, 1).expand(B * T, H, 64).reshape(B * T, H * 64)
     lens = torch.tensor([T, short], device=DEV, dtype=torch.int64)
     o_u = torch.empty(B * T, D, device=DEV, dtype=torch.float32)
     o_m = torch.empty(o_u.shape, device=o_u.device, dtype=torch.bfloat16)
@@ -70,8 +76,9 @@ def test_attention_kernel_vs_torch(fwd, T, short, amp, monkeypatch):
     om = o * hm[None, :, None, None]
     o_ref = o.permute(0, 2, 1, 3).reshape(B * T, D)
     om_ref = om.permute(0, 2, 1, 3).reshape(B * T, D)
-    assert rel_l2(o_u.float(), o_ref.detach()) < 1e-2
+    assert rel_l2(o_u.float()[live], o_ref.detach()[live]) < 1e-2
     assert rel_l2(o_m.float(), om_ref.detach()) < 1e-2
+    assert torch.count_nonzero(o_m.float()[~live]) == 0
     # backward
     g = (torch.randn(B * T, D, device=DEV)).to(torch.bfloat16)
     om_ref.backward(g.float())
@@ -88,7 +95,10 @@ def test_attention_kernel_vs_torch(fwd, T, short, amp, monkeypatch):
         b = gq.view(B * T, 3, D)[:, part]
         assert rel_l2(a, b) < 3e-2, (part, rel_l2(a, b))
     dhm_ref = (g.float().view(B, T, H, 64) * o.detach().permute(0, 2, 1, 3)).sum((0, 1, 3))
-    assert rel_l2(dhm, dhm_ref) < 1e-2
+    hl = hm != 0
+    assert rel_l2(dhm[hl], dhm_ref[hl]) < 1e-2
+    assert torch.count_nonzero(dhm[~hl]) == 0
+    assert torch.count_nonzero(dqkv.float().view(B * T, 3, D)[:, :, ~live[0]]) == 0
 
 
 @pytest.mark.parametrize("sharp", [1.0, 16.0])
