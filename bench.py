@@ -373,8 +373,10 @@ def main():
     if os.environ.get("DPH_BENCH_LOGGED") == "1":      # diagnostics: the last replayed graph's logged terms
         log(f"logged terms: {terms}")
     main_loss = None
-    if graphed and trainer._graphs.get((args.accum == 1, True)) is not None:
-        main_loss = trainer._graphs[(args.accum == 1, True)][1].item()     # the last main-graph replay
+    # (accum 1 only: with accumulation the final micro-step graph's loss output is refreshed by the next
+    # optimizer step's first micro-step replay, so after the loop it no longer holds that step's loss)
+    if graphed and args.accum == 1 and trainer._graphs.get((True, True)) is not None:
+        main_loss = trainer._graphs[(True, True)][1].item()     # the last main-graph replay
     check_step(loss.item(), terms if (graphed or in_loop) else None, main_loss)
 
     fam = {"wavlm-base": "WavLM-Base", "large": "wav2vec2-Large"}.get(args.model, "HuBERT-Base")

@@ -60,6 +60,7 @@ S = vp  # hipStream_t
 _SIGS = {
     "dph_abi_version": ([], C.c_int),
     "dph_gemm": ([C.POINTER(DphGemmArgs), S], C.c_int),
+    "dph_gemm_mn_plan": ([i64, i64, i64, i64], C.c_int),
     "dph_layernorm_fwd": ([vp, vp, vp, vp, vp, vp, vp, i64, i64, f32, f32, u64, S], C.c_int),
     "dph_layernorm_bwd": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, f32, u64, vp, f32, u64, vp, vp, vp, vp, vp, i64,
                            S],
@@ -129,8 +130,8 @@ _SIGS = {
 
 _lib = None
 # include/dphubert_hip.h layout (3: dph_adamw_step_dev, dph_set_rng_epoch; 4: dph_event_*; 5: LN bwd / colsum
-# workspaces; 12: dph_hc_bank_fwd / dph_hc_bank_bwd)
-ABI_VERSION = 14
+# workspaces; 12: dph_hc_bank_fwd / dph_hc_bank_bwd; 15: dph_gemm_mn_plan)
+ABI_VERSION = 15
 
 
 class DphError(RuntimeError):

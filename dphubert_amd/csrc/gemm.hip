@@ -2105,6 +2105,353 @@ __global__ void __launch_bounds__(C::NT, C::WPE) pp_gemm_kernel(const DphGemmArg
 }
 }  // namespace pp
 
+// =============================================================================================
+// Ping-pong weight-gradient kernel: both operands mn-contiguous (A = [K][M], B = [K][N], K = the B*T frames
+// of the batch), split-K over blockIdx.z.  dW = dY^T X of every nn.Linear / conv layer (components.py:107,
+// :272, :406-408, :430, :733, :741; lightning.py:258) without transposing an activation: the LDS-DMA stages
+// each half-tile as a [64 k][R] image (R = 64 or 128 operand rows, 16-B chunk c of k-row r at c ^ fsw(r)),
+// and the MFMA fragments come out of it by ds_read_b64_tr_b16 (two per 16 x 32 fragment; the swizzle puts
+// the 8 k-rows x 2 chunks of a half-wave's transposed read on 16 distinct 4-bank groups).  Same 8-wave
+// schedule as pp_gemm_kernel (two groups one barrier interval apart, four half-tiles per 64-deep K-tile).
+//   * K tail: DMA rows past kend re-read row kend - 1 (finite), the A fragments of the last K-tile zero
+//     their k >= kend elements before the MFMAs;
+//   * BB: B rows in the batched layout (conv weight gradients: row k = output frame, windows of stride s*C
+//     inside each utterance) -- one carry per 64-row tile (rows_per_batch >= 64);
+//   * splits > 1: dph_gemm passes epilogue args whose C is the fp32 workspace slab (z = batch * splits +
+//     split), summed into dW by splitk_reduce_kernel.
+// =============================================================================================
+namespace ppw {
+using pp::BK;
+
+template <int R>
+__device__ __forceinline__ int fsw(int r) { return (2 * ((r >> 1) & 1) + 4 * ((r >> 3) & 1) + 8 * (r & 1)) & (R / 8 - 1); }
+
+// byte offset (k-row 0 .. 3 of the lane's first transposed read, ksub 0) of the fragment with operand rows
+// cb .. cb + 15 (cb % 16 == 0) in a [64][R] half-tile image; ksub s adds 64 R bytes, the second read 8 R
+template <int R>
+__device__ __forceinline__ int tfrag_off(int cb, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int k0 = 8 * g + q;
+  const int c = (cb >> 3) + (p >> 1);
+  return k0 * (2 * R) + ((c ^ fsw<R>(k0)) << 4) + ((p & 1) << 3);
+}
+
+template <int R>
+__device__ __forceinline__ bf16x8_t tfrag(const char* ht, int off, int s) {
+  typedef __attribute__((address_space(3))) s16x4_t lds_s16x4;
+  const char* p0 = ht + off + s * 64 * R;
+  const s16x4_t v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p0);
+  const s16x4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0 + 8 * R));
+  const s16x8_t v = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
+// zero the elements k >= n of a lane's 8 consecutive k values (n <= 0: all, n >= 8: none)
+__device__ __forceinline__ bf16x8_t kmask(bf16x8_t f, int n) {
+  uint4 w = __builtin_bit_cast(uint4, f);
+  auto m = [&](int e) -> uint32_t { return n >= e + 2 ? 0xffffffffu : (n == e + 1 ? 0x0000ffffu : 0u); };
+  w.x &= m(0);
+  w.y &= m(2);
+  w.z &= m(4);
+  w.w &= m(6);
+  return __builtin_bit_cast(bf16x8_t, w);
+}
+
+template <class C, bool BB>
+__global__ void __launch_bounds__(C::NT, C::WPE) ppw_gemm_kernel(const DphGemmArgs a, int64_t kchunk) {
+  __shared__ __attribute__((aligned(1024))) char smem[C::LDS];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int64_t zz = blockIdx.z;
+  const int64_t z = zz / a.splits;
+  const int64_t split = zz - z * a.splits;
+  int64_t m0, n0;
+  {
+    const uint32_t ntm = gridDim.y, ntn = gridDim.x, nt = ntm * ntn;
+    const uint32_t bid = blockIdx.y * ntn + blockIdx.x;
+    const uint32_t q = nt >> 3, r = nt & 7;
+    const uint32_t xcd = bid & 7, loc = bid >> 3;
+    const uint32_t t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+    constexpr uint32_t GM = C::BM > 128 ? 4 : 8;
+    const uint32_t gsz = GM * ntn;
+    const uint32_t grp = t / gsz;
+    const uint32_t gm0 = grp * GM;
+    const uint32_t gh = min(GM, ntm - gm0);
+    const uint32_t l = t - grp * gsz;
+    const uint32_t lq = l / gh;
+    m0 = (int64_t)(gm0 + (l - lq * gh)) * C::BM;
+    n0 = (int64_t)lq * C::BN;
+  }
+  const int32_t kbeg = (int32_t)(split * kchunk);
+  const int32_t kend = (int32_t)min<int64_t>(a.K, kbeg + kchunk);
+  const int nk = (kend - kbeg + BK - 1) / BK;
+  const bf16_t* Ab = reinterpret_cast<const bf16_t*>(a.A.ptr) + z_addr(a.A, z);
+  const bf16_t* Bb = reinterpret_cast<const bf16_t*>(a.B.ptr) + z_addr(a.B, z);
+  const uint32_t rsa = (uint32_t)a.A.row_stride, rsb = (uint32_t)a.B.row_stride;
+  // DMA of a [64][R] half-tile: wave instruction gi = jj * 8 + wave fills k-rows gi * (512 / R) ..; lane ->
+  // k-row gi * (512 / R) + lane / (R / 8), physical chunk lane % (R / 8) <- logical chunk pc ^ fsw(k-row),
+  // i.e. operand rows (columns of the image) 8 lc .. 8 lc + 7, mapped to the tile by the half-tile kind
+  constexpr int HA = C::WTM / 2;
+  const int64_t mpad = ((a.M + 7) & ~(int64_t)7) - 8, npad = ((a.N + 7) & ~(int64_t)7) - 8;
+  uint32_t cal[C::GA], cah[C::GA], cb0[C::GB0], cb1[C::GB1];   // column (operand row) offsets
+  uint8_t kal[C::GA], kb0[C::GB0], kb1[C::GB1];                // k-row within the tile
+  auto krow_of = [&](int jj, int R) { return (jj * 8 + wave) * (512 / R) + lane / (R / 8); };
+#pragma unroll
+  for (int jj = 0; jj < C::GA; ++jj) {
+    constexpr int R = C::RA;
+    const int kr = krow_of(jj, R);
+    const int rho = (((lane % (R / 8)) ^ fsw<R>(kr)) * 8);
+    const int trow = (rho / HA) * C::WTM + rho % HA;
+    kal[jj] = (uint8_t)kr;
+    cal[jj] = (uint32_t)min<int64_t>(m0 + trow, mpad);
+    cah[jj] = (uint32_t)min<int64_t>(m0 + trow + HA, mpad);
+  }
+#pragma unroll
+  for (int jj = 0; jj < C::GB0; ++jj) {
+    constexpr int R = C::RB0;
+    const int kr = krow_of(jj, R);
+    const int rho = (((lane % (R / 8)) ^ fsw<R>(kr)) * 8);
+    const int tcol = (rho / (16 * C::FN0)) * C::WTN + rho % (16 * C::FN0);
+    kb0[jj] = (uint8_t)kr;
+    cb0[jj] = (uint32_t)min<int64_t>(n0 + tcol, npad);
+  }
+#pragma unroll
+  for (int jj = 0; jj < C::GB1; ++jj) {
+    constexpr int R = C::RB1;
+    const int kr = krow_of(jj, R);
+    const int rho = (((lane % (R / 8)) ^ fsw<R>(kr)) * 8);
+    const int tcol = (rho / (16 * C::FN1)) * C::WTN + 16 * C::FN0 + rho % (16 * C::FN1);
+    kb1[jj] = (uint8_t)kr;
+    cb1[jj] = (uint32_t)min<int64_t>(n0 + tcol, npad);
+  }
+  // B rows in the batched layout: (utterance, frame) of each kind's next K-tile start, one carry per tile
+  const uint32_t rpb = BB ? (uint32_t)a.B.rows_per_batch : 0u;
+  const uint32_t bsb = BB ? (uint32_t)a.B.batch_stride : 0u;
+  uint32_t bq[2] = {0u, 0u}, br[2] = {0u, 0u};
+  uint32_t blast = 0u;
+  if constexpr (BB) {
+    bq[0] = bq[1] = (uint32_t)kbeg / rpb;
+    br[0] = br[1] = (uint32_t)kbeg - bq[0] * rpb;
+    const uint32_t kl = (uint32_t)kend - 1u, ql = kl / rpb;
+    blast = ql * bsb + (kl - ql * rpb) * rsb;
+  }
+  auto a_off = [&](int kt, int kr, uint32_t col) -> uint32_t {
+    return __umul24((uint32_t)min(kt + kr, kend - 1), rsa) + col;   // (k, row stride < 2^24: checked on the host)
+  };
+  auto b_off = [&](int kt, int kr, uint32_t col, int kind) -> uint32_t {
+    if constexpr (BB) {
+      uint32_t r = br[kind] + (uint32_t)kr;
+      uint32_t off = bq[kind] * bsb;
+      if (r >= rpb) {
+        r -= rpb;
+        off += bsb;
+      }
+      off += __umul24(r, rsb) + col;
+      return kt + kr < kend ? off : blast + col;
+    } else {
+      return __umul24((uint32_t)min(kt + kr, kend - 1), rsb) + col;
+    }
+  };
+  auto b_adv = [&](int kind) {
+    if constexpr (BB) {
+      br[kind] += BK;
+      if (br[kind] >= rpb) {
+        br[kind] -= rpb;
+        ++bq[kind];
+      }
+    }
+  };
+  auto buf = [&](int u) -> char* { return smem + (u & 1) * C::BUF; };
+  auto st_alo = [&](int u) {
+    const int kt = kbeg + u * BK;
+#pragma unroll
+    for (int jj = 0; jj < C::GA; ++jj) ring::dma16(Ab + a_off(kt, kal[jj], cal[jj]), buf(u) + C::O_ALO + (jj * 8 + wave) * 1024);
+  };
+  auto st_ahi = [&](int u) {
+    const int kt = kbeg + u * BK;
+#pragma unroll
+    for (int jj = 0; jj < C::GA; ++jj) ring::dma16(Ab + a_off(kt, kal[jj], cah[jj]), buf(u) + C::O_AHI + (jj * 8 + wave) * 1024);
+  };
+  auto st_b0 = [&](int u) {
+    const int kt = kbeg + u * BK;
+#pragma unroll
+    for (int jj = 0; jj < C::GB0; ++jj) ring::dma16(Bb + b_off(kt, kb0[jj], cb0[jj], 0), buf(u) + C::O_B0 + (jj * 8 + wave) * 1024);
+    b_adv(0);
+  };
+  auto st_b1 = [&](int u) {
+    const int kt = kbeg + u * BK;
+#pragma unroll
+    for (int jj = 0; jj < C::GB1; ++jj) ring::dma16(Bb + b_off(kt, kb1[jj], cb1[jj], 1), buf(u) + C::O_B1 + (jj * 8 + wave) * 1024);
+    b_adv(1);
+  };
+
+  f32x4_t acc[C::FM][C::FN];
+#pragma unroll
+  for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+    for (int j = 0; j < C::FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  bf16x8_t fa[C::FM2][2], fb0[C::FN0][2], fb1[C::FN1][2];
+  // fragment byte offsets inside their half-tile images (loop invariant)
+  int oa[C::FM2], ob0[C::FN0], ob1[C::FN1];
+#pragma unroll
+  for (int i = 0; i < C::FM2; ++i) oa[i] = tfrag_off<C::RA>(wr * HA + 16 * i, lane);
+#pragma unroll
+  for (int j = 0; j < C::FN0; ++j) ob0[j] = tfrag_off<C::RB0>(wc * 16 * C::FN0 + 16 * j, lane);
+#pragma unroll
+  for (int j = 0; j < C::FN1; ++j) ob1[j] = tfrag_off<C::RB1>(wc * 16 * C::FN1 + 16 * j, lane);
+
+  auto rd_a = [&](const char* ht) {
+#pragma unroll
+    for (int i = 0; i < C::FM2; ++i)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) fa[i][s] = tfrag<C::RA>(ht, oa[i], s);
+  };
+  auto rd_b0 = [&](const char* bu) {
+#pragma unroll
+    for (int j = 0; j < C::FN0; ++j)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) fb0[j][s] = tfrag<C::RB0>(bu + C::O_B0, ob0[j], s);
+  };
+  auto rd_b1 = [&](const char* bu) {
+#pragma unroll
+    for (int j = 0; j < C::FN1; ++j)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) fb1[j][s] = tfrag<C::RB1>(bu + C::O_B1, ob1[j], s);
+  };
+  // the last K-tile's A elements with k >= kend
+  const int kv = kend - (kbeg + (nk - 1) * BK);      // valid k-rows of the last K-tile (1 .. 64)
+  auto mask_a = [&]() {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int n = kv - 32 * s - 8 * (lane >> 4);
+#pragma unroll
+      for (int i = 0; i < C::FM2; ++i) fa[i][s] = kmask(fa[i][s], n);
+    }
+  };
+  auto mm0 = [&](int i0) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < C::FM2; ++i)
+#pragma unroll
+        for (int j = 0; j < C::FN0; ++j)
+          acc[i0 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb0[j][s], fa[i][s], acc[i0 + i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto mm1 = [&](int i0) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < C::FM2; ++i)
+#pragma unroll
+        for (int j = 0; j < C::FN1; ++j)
+          acc[i0 + i][C::FN0 + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb1[j][s], fa[i][s], acc[i0 + i][C::FN0 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  using pp::bar;
+  using pp::lgkm0;
+  using pp::vm_wait;
+  constexpr int G = C::G;
+  st_alo(0);
+  st_b0(0);
+  st_b1(0);
+  st_ahi(0);
+  st_alo(1);
+  st_b0(1);
+  vm_wait<G>();
+  bar();
+  if (wr == 1) bar();
+  int u = 0;
+#pragma unroll 1
+  for (; u + 2 < nk; ++u) {
+    const char* bu = buf(u);
+    rd_b0(bu);
+    rd_a(bu + C::O_ALO);
+    st_b1(u + 1);
+    vm_wait<G>();
+    bar();
+    lgkm0();
+    __builtin_amdgcn_sched_barrier(0);
+    mm0(0);
+    bar();
+    rd_b1(bu);
+    st_ahi(u + 1);
+    vm_wait<G>();
+    bar();
+    lgkm0();
+    __builtin_amdgcn_sched_barrier(0);
+    mm1(0);
+    bar();
+    rd_a(bu + C::O_AHI);
+    st_alo(u + 2);
+    vm_wait<G>();
+    bar();
+    lgkm0();
+    __builtin_amdgcn_sched_barrier(0);
+    mm1(C::FM2);
+    bar();
+    st_b0(u + 2);
+    vm_wait<G>();
+    bar();
+    mm0(C::FM2);
+    bar();
+  }
+#pragma unroll
+  for (int t = 0; t < 2; ++t, ++u) {
+    const bool second_last = t == 0;
+    const bool tail = !second_last && kv < BK;
+    const char* bu = buf(u);
+    rd_b0(bu);
+    rd_a(bu + C::O_ALO);
+    if (second_last) {
+      st_b1(u + 1);
+      vm_wait<G>();
+    } else {
+      vm_wait<C::GA>();
+    }
+    bar();
+    lgkm0();
+    __builtin_amdgcn_sched_barrier(0);
+    if (tail) mask_a();
+    mm0(0);
+    bar();
+    rd_b1(bu);
+    if (second_last) {
+      st_ahi(u + 1);
+      vm_wait<G>();
+    } else {
+      vm_wait<0>();
+    }
+    bar();
+    lgkm0();
+    __builtin_amdgcn_sched_barrier(0);
+    mm1(0);
+    bar();
+    rd_a(bu + C::O_AHI);
+    if (second_last) vm_wait<G - C::GA>();
+    else vm_wait<0>();
+    bar();
+    lgkm0();
+    __builtin_amdgcn_sched_barrier(0);
+    if (tail) mask_a();
+    mm1(C::FM2);
+    bar();
+    if (second_last) vm_wait<C::GB1 + C::GA>();
+    else vm_wait<0>();
+    bar();
+    mm0(C::FM2);
+    bar();
+  }
+  if (wr == 0) bar();
+  ring::direct_epi_t<C, DPH_ACT_NONE, false>(a, zz, m0 + wr * C::WTM, n0 + wc * C::WTN, lane, acc);
+}
+}  // namespace ppw
+
 // out[c] += sum_r slab[r][c] (out) and aux[c] += sum_r slab[nrows + r][c]: 64 columns x 4 row phases per block
 // over one of gridDim.y (<= 8) row groups, one atomic per column per group
 __global__ void __launch_bounds__(256) colsum_slab_reduce_kernel(const float* __restrict__ slab, int64_t nrows,
@@ -2179,7 +2526,7 @@ static int small_nt(int64_t kchunk) {
 static int gemm_path_override() {
   const char* e = getenv("DPH_GEMM_PATH");
   if (!e) return 0;
-  return !strcmp(e, "small") ? 1 : !strcmp(e, "big") ? 2 : !strcmp(e, "mid") ? 3 : !strcmp(e, "tall") ? 4 : !strcmp(e, "half") ? 5 : !strcmp(e, "mid8") ? 6 : !strcmp(e, "mid8mn") ? 7 : !strcmp(e, "wide") ? 8 : !strcmp(e, "flat") ? 9 : !strcmp(e, "tri") ? 10 : !strcmp(e, "notri") ? 11 : !strcmp(e, "pp256") ? 12 : !strcmp(e, "pp128x256") ? 13 : !strcmp(e, "pp256x128") ? 14 : !strcmp(e, "pp128x192") ? 15 : !strcmp(e, "pp128") ? 16 : 0;
+  return !strcmp(e, "small") ? 1 : !strcmp(e, "big") ? 2 : !strcmp(e, "mid") ? 3 : !strcmp(e, "tall") ? 4 : !strcmp(e, "half") ? 5 : !strcmp(e, "mid8") ? 6 : !strcmp(e, "mid8mn") ? 7 : !strcmp(e, "wide") ? 8 : !strcmp(e, "flat") ? 9 : !strcmp(e, "tri") ? 10 : !strcmp(e, "notri") ? 11 : !strcmp(e, "pp256") ? 12 : !strcmp(e, "pp128x256") ? 13 : !strcmp(e, "pp256x128") ? 14 : !strcmp(e, "pp128x192") ? 15 : !strcmp(e, "pp128") ? 16 : !strcmp(e, "ppw") ? 17 : 0;
 }
 
 // the 192 x 128 tile takes the register epilogue only (its staged epilogue is compiled but not routed)
@@ -2234,6 +2581,124 @@ static int pp_pick(const DphGemmArgs& a) {
     }
   }
   return best;
+}
+
+// ---- the weight-gradient ping-pong path (ppw) ----
+// DPH_GEMM_PPW=0 keeps the (mn, mn) GEMMs on the register-staged kernel (A/B; read per call)
+static bool ppw_enabled() {
+  const char* e = getenv("DPH_GEMM_PPW");
+  return !(e && e[0] == '0');
+}
+
+struct PpwPlan {
+  int kind;         // 12 / 13 / 15 / 16 (pp tile ids), 0: none
+  int splits;
+  int64_t kchunk;   // K per split (whole 64-deep K-tiles)
+};
+
+// Tile and split-K choice: whole rounds of (tile, split) blocks over the CU slots x one block's MFMA work at the
+// tile's measured ping-pong rate, plus the fp32 slab the splits write and splitk_reduce_kernel reads back
+// (~4 TB/s) and that launch.  Each split keeps at least eight K-tiles.  The 128 x 192 and 128 x 128 tiles run two
+// blocks per CU here (<= 128 VGPRs, <= 80 KB LDS).  Long-K (conv) shapes: 128 x 192 tiles and ~48 K-tiles per
+// split (up to 32 splits).  Sweep behind both rules: profiles/r3_s9_wgrad_sweep.txt (tools/wgrad_sweep.py).
+static PpwPlan ppw_plan(int64_t M, int64_t N, int64_t K, int64_t batch, int want_splits) {
+  struct Opt { int kind, bm, bn, per_cu; double tf; };
+  static const Opt opts[] = {{12, 256, 256, 1, 1514.0}, {15, 128, 192, 2, 1282.0}, {13, 128, 256, 1, 1221.0},
+                             {16, 128, 128, 2, 1178.0}};
+  const int64_t cus = num_cus();
+  const int64_t nkt = cdiv(K, (int64_t)pp::BK);
+  constexpr int64_t MIN_KT = 8;
+  // DPH_PPW_FORCE="kind:splits" (A/B sweeps, read per call): only that tile, and that split count when free
+  int fk = 0, fs = 0;
+  if (const char* e = getenv("DPH_PPW_FORCE")) sscanf(e, "%d:%d", &fk, &fs);
+  if (want_splits == 0 && fs > 0) want_splits = fs;
+  PpwPlan best{0, 0, 0};
+  double best_t = 1e300;
+  for (const Opt& o : opts) {
+    if (fk && o.kind != fk) continue;
+    const int64_t tiles = cdiv(M, (int64_t)o.bm) * cdiv(N, (int64_t)o.bn) * batch;
+    for (int s = 1; s <= 32; ++s) {
+      if (want_splits > 0 && s != want_splits) continue;
+      const int64_t kct = cdiv(nkt, (int64_t)s);
+      if (kct < 2 || cdiv(nkt, kct) != s || nkt - (s - 1) * kct < 2) continue;
+      if (want_splits == 0 && kct < MIN_KT && s > 1) continue;
+      double t;
+      if (nkt >= 768 && want_splits == 0) {
+        // long K: the measured optimum sits at ~48 K-tiles per split on 128 x 192 (conv1 / conv2 at 32 splits)
+        if (o.kind != 15) continue;
+        t = kct > 48 ? (double)(kct - 48) : (double)(48 - kct);
+      } else {
+        const int64_t rounds = cdiv(tiles * s, cus * o.per_cu);
+        t = (double)rounds * o.per_cu * 2.0 * o.bm * o.bn * (double)(kct * pp::BK) / (o.tf * 1e12 / (double)cus);
+        if (s > 1) t += (double)(s + 1) * batch * M * N * 8.0 / 4.0e12 + 3e-6;
+      }
+      if (t < best_t * 0.999) {
+        best_t = t;
+        best = PpwPlan{o.kind, s, kct * pp::BK};
+      }
+    }
+  }
+  return best;
+}
+
+// operands and epilogue the ppw kernels take: (mn, mn), plain epilogue (alpha, fp32 / accumulating output), dense
+// A rows, B rows dense or batched with >= 64 rows per batch, 16-B aligned rows, DMA offsets and the 24-bit row
+// products within range
+static bool ppw_ok(const DphGemmArgs& a) {
+  if (a.a_kcontig || a.b_kcontig || a.act != DPH_ACT_NONE || a.bias || a.colmask || a.smask || a.pre_out || a.aux_in ||
+      a.residual || a.colsum_out || a.colsum_aux || a.row_len || a.dropout_p != 0.f || a.c_dtype == DPH_OUT_BF16)
+    return false;
+  if (a.M < 64 || a.N < 64 || a.K < 2 * pp::BK || a.K >= (1 << 24)) return false;
+  if (cdiv(a.M, (int64_t)128) >= 65536 || (int64_t)a.batch * a.splits >= 65536) return false;
+  auto op_ok = [&](const DphMat& d, int64_t cols, bool batched_ok) {
+    const int64_t al = d.row_stride | d.batch_stride | d.z_inner | d.z_outer;
+    if ((al & 7) != 0 || (reinterpret_cast<uintptr_t>(d.ptr) & 15) != 0) return false;
+    if (d.row_stride >= (1 << 24) || d.row_stride < ((cols + 7) & ~(int64_t)7)) return false;
+    int64_t last;
+    if (d.rows_per_batch > 0) {
+      if (!batched_ok || d.rows_per_batch < pp::BK || d.rows_per_batch >= (1 << 24)) return false;
+      const int64_t r = a.K - 1;
+      last = (r / d.rows_per_batch) * d.batch_stride + (d.rows_per_batch - 1) * d.row_stride;
+    } else {
+      last = (a.K - 1) * d.row_stride;
+    }
+    return last + cols + 8 < ((int64_t)1 << 31);
+  };
+  return op_ok(a.A, a.M, false) && op_ok(a.B, a.N, true);
+}
+
+// epilogue args of a ppw launch: the real C (splits == 1) or the fp32 slab of the splits (z = batch * splits + split)
+static DphGemmArgs ppw_epi_args(const DphGemmArgs& a) {
+  DphGemmArgs e = a;
+  if (a.splits > 1) {
+    e.C = DphMat{a.workspace, 0, 0, a.N, 0, 0, a.M * a.N};
+    e.c_dtype = DPH_OUT_F32;
+    e.alpha = 1.0f;
+  }
+  return e;
+}
+
+// the plan dph_gemm runs for an eligible (mn, mn) GEMM with these splits (kind 0: the register-staged kernel)
+static PpwPlan ppw_route(const DphGemmArgs& a) {
+  // (a forced DPH_GEMM_PATH other than "ppw" keeps the (mn, mn) GEMMs where it points: tests cover both kernels)
+  const int path = gemm_path_override();
+  if (!ppw_enabled() || (path != 0 && path != 17) || !ppw_ok(a)) return PpwPlan{0, 0, 0};
+  const PpwPlan p = ppw_plan(a.M, a.N, a.K, a.batch, a.splits);
+  if (p.kind == 0 || !ring::direct_epi_ok(ppw_epi_args(a))) return PpwPlan{0, 0, 0};
+  return p;
+}
+
+// split-K factor the ppw plan wants for an (mn, mn) weight-gradient shape (0: no plan; the caller's heuristic)
+extern "C" int dph_gemm_mn_plan(int64_t M, int64_t N, int64_t K, int64_t batch) {
+  if (!ppw_enabled() || M < 64 || N < 64 || K < 2 * pp::BK || batch < 1) return 0;
+  return ppw_plan(M, N, K, batch, 0).splits;
+}
+
+template <class Cf>
+static void launch_ppw(const DphGemmArgs& e, int64_t kchunk, hipStream_t stream) {
+  const dim3 g((unsigned)cdiv(e.N, Cf::BN), (unsigned)cdiv(e.M, Cf::BM), (unsigned)(e.batch * e.splits)), b(Cf::NT);
+  if (e.B.rows_per_batch > 0) hipLaunchKernelGGL((ppw::ppw_gemm_kernel<Cf, true>), g, b, 0, stream, e, kchunk);
+  else hipLaunchKernelGGL((ppw::ppw_gemm_kernel<Cf, false>), g, b, 0, stream, e, kchunk);
 }
 
 // only where both tilings are a single round over the CUs (one block per CU) and the 192 x 128 one has
@@ -2311,6 +2776,11 @@ extern "C" const char* dph_gemm_variant(const DphGemmArgs* args) {
   if (!args) return "";
   const DphGemmArgs& a = *args;
   const bool dgk = a.act == DPH_ACT_GELU_BWD_DGK || (a.act == DPH_ACT_GELU && (a.flags & DPH_GEMM_PRE_DGK));
+  const PpwPlan pw = ppw_route(a);
+  if (pw.kind == 12) return "ppw_gemm_kernel<dph::(anonymous namespace)::pp::Cfg<256, 256>";
+  if (pw.kind == 13) return "ppw_gemm_kernel<dph::(anonymous namespace)::pp::Cfg<128, 256>";
+  if (pw.kind == 15) return "ppw_gemm_kernel<dph::(anonymous namespace)::pp::Cfg<128, 192>";
+  if (pw.kind == 16) return "ppw_gemm_kernel<dph::(anonymous namespace)::pp::Cfg<128, 128>";
   const int kind = dgk ? pp_pick(a) : gemm_kind(a, gemm_kchunk(a));
   if (kind == 12) return "pp_gemm_kernel<dph::(anonymous namespace)::pp::Cfg<256, 256>";
   if (kind == 13) return "pp_gemm_kernel<dph::(anonymous namespace)::pp::Cfg<128, 256>";
@@ -2444,6 +2914,24 @@ extern "C" int dph_gemm(const DphGemmArgs* args, hipStream_t stream) {
     const int64_t need = (int64_t)a.batch * a.splits * a.M * a.N * 4;
     DPH_REQUIRE(a.workspace && a.workspace_bytes >= need, "dph_gemm: split-K workspace too small (%lld < %lld)",
                 (long long)a.workspace_bytes, (long long)need);
+  }
+  // (mn, mn) weight gradients: the ping-pong kernel with its own tile / split plan (the caller sized the workspace
+  // with dph_gemm_mn_plan's splits; any other split count keeps the register-staged kernel)
+  {
+    const PpwPlan pw = ppw_route(a);
+    if (pw.kind) {
+      const DphGemmArgs e = ppw_epi_args(a);
+      if (pw.kind == 12) launch_ppw<pp::P256>(e, pw.kchunk, stream);
+      else if (pw.kind == 13) launch_ppw<pp::P128x256>(e, pw.kchunk, stream);
+      else if (pw.kind == 15) launch_ppw<pp::P128x192>(e, pw.kchunk, stream);
+      else launch_ppw<pp::P128>(e, pw.kchunk, stream);
+      int rc = check_launch("dph_gemm (ppw)");
+      if (rc || a.splits == 1) return rc;
+      const int64_t work = a.M * cdiv(a.N, (int64_t)8);
+      hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)cdiv(work, (int64_t)256), 1, (unsigned)a.batch), dim3(256), 0,
+                         stream, a);
+      return check_launch("dph_gemm (ppw) splitk_reduce");
+    }
   }
   // LDS-DMA ring kernels for k-contiguous A and B with whole 32-deep k-slices: the 256x256 tile
   // when there are >= ~2 full rounds of tiles over the 256 CUs at one block per CU, else the

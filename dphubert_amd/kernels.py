@@ -172,7 +172,11 @@ def Cm_device(*ts):
 
 
 def choose_splits(M: int, N: int, K: int, batch: int = 1, target_blocks: int = 512) -> int:
-    """Split-K factor so that the grid fills the 256 CUs (weight-gradient GEMMs)."""
+    """Split-K factor of an (mn, mn) weight-gradient GEMM: the ping-pong kernel's tile / split plan
+    (dph_gemm_mn_plan), else enough 128x128 register-staged blocks to fill the 256 CUs."""
+    s = _lib.lib().dph_gemm_mn_plan(M, N, K, batch)
+    if s > 0:
+        return int(s)
     tiles = ((M + 127) // 128) * ((N + 127) // 128) * batch
     if tiles >= 256:
         return 1

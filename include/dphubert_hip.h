@@ -110,6 +110,11 @@ typedef struct DphGemmArgs {
 int dph_gemm(const DphGemmArgs* args, hipStream_t stream);
 /* name (as it appears in rocprof kernel names) of the kernel dph_gemm launches for these args */
 const char* dph_gemm_variant(const DphGemmArgs* args);
+/* split-K factor of the ping-pong weight-gradient plan for an (mn, mn) GEMM of this shape (A = [K][M], B = [K][N]:
+ * dW = dY^T X, K = frames of the batch); 0 = no plan.  A dph_gemm with exactly these splits (workspace sized for
+ * them) and an eligible layout runs ppw_gemm_kernel + splitk_reduce; replaces the split heuristic of the
+ * register-staged kernel for the wgrads of components.py:107/:272/:406-408/:430/:733/:741, lightning.py:258 */
+int dph_gemm_mn_plan(int64_t M, int64_t N, int64_t K, int64_t batch);
 
 /* ------------------------------------------------------------------------ *
  * LayerNorm over the last dim (rows x D), fp32 statistics, eps=1e-5.

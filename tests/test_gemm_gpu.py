@@ -10,7 +10,7 @@ torch.manual_seed(0)
 
 
 @pytest.fixture(autouse=True, params=["small", "mid", "big", "wide", "flat", "flat-np", "tall", "half", "mid8",
-                                     "mid8mn", "tri", "tri-np", "pp256", "pp128x256", "pp256x128", "pp128x192", "pp128"])
+                                     "mid8mn", "tri", "tri-np", "pp256", "pp128x256", "pp256x128", "pp128x192", "pp128", "ppw"])
 def gemm_path(request, monkeypatch):
     """Run every test on each GEMM path: the 128x128 register-staged kernel and the 128x128 /
     256x256 / 256x128 / 128x256 / 256x64 / 192x128 LDS-DMA ring kernels (taken where their constraints hold: both operands
@@ -125,6 +125,60 @@ def test_wgrad_splitk(accum):
     K_.linear_wgrad(dy, x, dw, accumulate=accum)
     ref = dy.float().t() @ x.float() + (dw0 if accum else 0)
     close(dw, ref, 1e-5)
+
+
+@pytest.mark.parametrize("N,K,M", [(2304, 768, 7984), (768, 768, 7984), (768, 3072, 7984), (512, 1024, 3000),
+                                   (200, 136, 1000)])
+def test_wgrad_ppw_plan(N, K, M, gemm_path):
+    """(mn, mn) weight gradients on the ping-pong kernel's own tile / split plan (dph_gemm_mn_plan): the
+    step's projection shapes (K = B*T = 7984: a 48-row K tail), fp32 accumulation into an existing gradient."""
+    K_ = _k()
+    if gemm_path != "ppw":
+        pytest.skip("ppw plan only")
+    dy, x = rnd(M, N), rnd(M, K)
+    dw = torch.randn(N, K, device="cuda")
+    dw0 = dw.clone()
+    assert "ppw_gemm_kernel" in K_._variant(_wgrad_args(K_, dy, x, dw))
+    keep = K_.linear_wgrad(dy, x, dw, accumulate=True)
+    torch.cuda.synchronize()
+    del keep
+    ref = dy.double().t() @ x.double() + dw0.double()
+    close(dw, ref, 1e-5)
+
+
+def _wgrad_args(K_, dy, x, dw):
+    from dphubert_amd._lib import DphGemmArgs
+    M, N = dy.shape
+    Kk = x.shape[1]
+    s = K_.choose_splits(N, Kk, M)
+    return DphGemmArgs(N, Kk, M, 1, s, 0, 0, K_.dense(dy), K_.dense(x), K_.dense(dw), K_.OUT_F32_ACCUM, 0, 1.0, 0.0, 0,
+                       None, None, None, 0, None, None, None, None, None, None, 0, 0, None, 4 * s * N * Kk, 0, 0)
+
+
+@pytest.mark.parametrize("B,Lin,Cc,O,k,s", [(2, 301, 64, 128, 3, 2), (16, 999, 512, 512, 2, 2),
+                                             (3, 2001, 512, 512, 3, 2)])
+def test_conv_wgrad_ppw(B, Lin, Cc, O, k, s, gemm_path):
+    """conv weight gradient with the B operand in the batched row layout (overlapping windows of stride s*C inside
+    each utterance): dW[o][j*C + c] = sum_(b,t) dz[b,t,o] x[b, s t + j, c] (components.py:107)."""
+    K_ = _k()
+    if gemm_path not in ("ppw", "small"):
+        pytest.skip("ppw vs the register-staged kernel")
+    Lout = (Lin - k) // s + 1
+    x = rnd(B, Lin, Cc)
+    dz = rnd(B * Lout, O)
+    M = B * Lout
+    dwp = torch.empty(O, k * Cc, device="cuda")
+    A = K_.mat(dz, row_stride=O)
+    Bm = K_.mat(x, row_stride=s * Cc, rows_per_batch=Lout, batch_stride=Lin * Cc)
+    splits = K_.choose_splits(O, k * Cc, M)
+    keep = K_.gemm(A, Bm, K_.dense(dwp), O, k * Cc, M, a_kcontig=False, b_kcontig=False, c_dtype=K_.OUT_F32,
+                   splits=splits)
+    torch.cuda.synchronize()
+    del keep
+    win = x.double().unfold(1, k, s)                     # [B][Lout][C][k]
+    win = win.permute(0, 1, 3, 2).reshape(M, k * Cc)     # [B*Lout][k*C] (j major)
+    ref = dz.double().t() @ win
+    close(dwp, ref, 1e-5)
 
 
 def test_conv_implicit_gemm():

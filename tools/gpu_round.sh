@@ -8,6 +8,8 @@
 #   smoke   -- __graft_entry__.smoke()
 #   bench   -- bench.py default line (PMC traffic passes + CPU baseline)
 #   prof    -- rocprofv3 --kernel-trace --stats of a short bench run -> kernel_stats.csv
+#   gemmtests -- tests/test_gemm_gpu.py (every GEMM path)
+#   wgrad   -- tools/wgrad_ab.py (weight-gradient GEMMs: ppw plan vs the register-staged kernel)
 #   pmcattn -- rocprofv3 --pmc passes over the attention kernels (tools/attn_bench.py)
 #   pmcgemm -- the same over the dominant GEMM shape (7984 x 3072 x 768, tools/gemm_one.py)
 # Every GPU step runs under its own timeout; the first failing step ends the script.
@@ -63,6 +65,12 @@ for P in $PHASES; do
       cat "$O/prof_bench.json"
       f=$(find "$O/prof" -name "*kernel_stats.csv" | head -1)
       cp "$f" "$O/kernel_stats.csv" && python3 tools/stats_csv.py "$O/kernel_stats.csv" 8 40 ;;
+    gemmtests)
+      timeout -k 10 600 $PYT tests/test_gemm_gpu.py -m gpu -x -q > "$O/gemm_tests.log" 2>&1 || { tail -40 "$O/gemm_tests.log"; exit 1; }
+      tail -2 "$O/gemm_tests.log" ;;
+    wgrad)
+      timeout -k 10 300 python -u tools/wgrad_ab.py > "$O/wgrad_ab.log" 2>&1 || { tail -30 "$O/wgrad_ab.log"; exit 1; }
+      cut -c1-220 "$O/wgrad_ab.log" ;;
     pmcattn)
       pmc_run pmcattn attn python3 "$R/tools/attn_bench.py" || exit 1 ;;
     pmcgemm)
