@@ -179,7 +179,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(const bf16_t* __restri
                                                           uint16_t* __restrict__ keep_out) {
   seed = epoch_seed(seed);   // per-step RNG epoch (graph replays)
   const uint32_t mix = seed_mix(seed);
-  __shared__ __attribute__((aligned(16))) char smem[2 * (KTILE_PAD_BYTES + TILE_SWZ_BYTES)];
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE_SWZ_BYTES];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
@@ -231,11 +231,11 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(const bf16_t* __restri
 
   const int nkt = (int)cdiv(T, KT);
   uint4 rk[2], rv[2];
-  auto ldsK = [&](int buf) { return smem + buf * (KTILE_PAD_BYTES + TILE_SWZ_BYTES); };
-  auto ldsV = [&](int buf) { return smem + buf * (KTILE_PAD_BYTES + TILE_SWZ_BYTES) + KTILE_PAD_BYTES; };
-  stage_load<KT, false>(rk, rowbase + (H + h) * HD, 0, T, RS, 1.0f, tid);
+  auto ldsK = [&](int buf) { return smem + buf * 2 * TILE_SWZ_BYTES; };
+  auto ldsV = [&](int buf) { return smem + buf * 2 * TILE_SWZ_BYTES + TILE_SWZ_BYTES; };
+  stage_load<KT, true>(rk, rowbase + (H + h) * HD, 0, T, RS, 1.0f, tid);
   stage_load<KT, true>(rv, rowbase + (2 * H + h) * HD, 0, T, RS, 1.0f, tid);
-  stage_store<KT, false>(ldsK(0), rk, tid);
+  stage_store<KT, true>(ldsK(0), rk, tid);
   stage_store<KT, true>(ldsV(0), rv, tid);
   __syncthreads();
 
@@ -243,7 +243,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(const bf16_t* __restri
     const int cur = kt & 1;
     const bool more = kt + 1 < nkt;
     if (more) {
-      stage_load<KT, false>(rk, rowbase + (H + h) * HD, (int64_t)(kt + 1) * KT, T, RS, 1.0f, tid);
+      stage_load<KT, true>(rk, rowbase + (H + h) * HD, (int64_t)(kt + 1) * KT, T, RS, 1.0f, tid);
       stage_load<KT, true>(rv, rowbase + (2 * H + h) * HD, (int64_t)(kt + 1) * KT, T, RS, 1.0f, tid);
     }
     const char* K_ = ldsK(cur);
@@ -256,7 +256,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(const bf16_t* __restri
       for (int u = 0; u < NG; ++u) sacc[u][s] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        const bf16x8_t kf = lds_b128(K_, ((16 * s + (lane & 15)) * PADROW + ks * 32 + 8 * g) * 2);
+        const bf16x8_t kf = lds_b128(K_, swz128(16 * s + (lane & 15), ks * 32 + 8 * g));
 #pragma unroll
         for (int u = 0; u < NG; ++u) sacc[u][s] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[u][ks], sacc[u][s], 0, 0, 0);
       }
@@ -340,7 +340,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(const bf16_t* __restri
     if (!BIAS && (kt + 1) * KT <= klen && (kt + 1) * KT <= T32) tile(std::integral_constant<bool, BIAS>());
     else tile(std::integral_constant<bool, true>());
     if (more) {
-      stage_store<KT, false>(ldsK(cur ^ 1), rk, tid);
+      stage_store<KT, true>(ldsK(cur ^ 1), rk, tid);
       stage_store<KT, true>(ldsV(cur ^ 1), rv, tid);
     }
     __syncthreads();
@@ -731,28 +731,43 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const bf16_t* __restrict__ qkv
   if constexpr (BIAS) stage_tab_window(tw, rb.tab + h * (2 * T - 1), toff, (int)T);   // ordered by the first barrier
 
   const int nqt = (int)cdiv(T, QT_BWD);
+  // the next query tile's rows AND its per-row words (lse, D, gate, keep bits) are loaded into registers at the
+  // top of an iteration and written to LDS at its end: every global load is a whole iteration of MFMAs ahead of
+  // the barrier that publishes it (the per-row words used to be loaded inside the store step, right before the
+  // barrier, so the block waited one global-load latency per 32-query tile)
   uint4 rq[1], ro[1];
+  float lse_r = 0.f, dv_r = 0.f, g_r = 0.f;
+  uint2 kw_r = make_uint2(0u, 0u);
   auto load_tiles = [&](int qt) {
     stage_load<QT_BWD, true>(rq, rowbase + h * HD, (int64_t)qt * QT_BWD, T, RS, scale, tid);
     stage_load<QT_BWD, true>(ro, dobase, (int64_t)qt * QT_BWD, T, H * HD, hm, tid);
-  };
-  auto store_tiles = [&](int buf, int qt) {
-    stage_store<QT_BWD, true>(ldsQ(buf), rq, tid);
-    stage_store<QT_BWD, true>(ldsO(buf), ro, tid);
     if (tid < QT_BWD) {
       const int64_t q = (int64_t)qt * QT_BWD + tid;
-      lse_s[buf * QT_BWD + tid] = q < T ? lse[(b * H + h) * T + q] * L2E : 0.f;   // log2 units
-      dv_s[buf * QT_BWD + tid] = q < T ? Dv[(b * H + h) * T + q] : 0.f;
-      if constexpr (BIAS) g_s[buf * QT_BWD + tid] = q < T ? rb.gate[(b * H + h) * T + q] : 0.f;
+      lse_r = q < T ? lse[(b * H + h) * T + q] * L2E : 0.f;   // log2 units
+      dv_r = q < T ? Dv[(b * H + h) * T + q] : 0.f;
+      if constexpr (BIAS) g_r = q < T ? rb.gate[(b * H + h) * T + q] : 0.f;
     }
     if (use_keep && tid >= 64 && tid < 128) {   // (constexpr-false unless KEEP)
       const int r = tid & 31, lt = (tid >> 5) & 1;
       const int64_t q = (int64_t)qt * QT_BWD + r;
       const int ktile = 2 * bx + lt;
-      uint2 wv = make_uint2(0u, 0u);
+      kw_r = make_uint2(0u, 0u);
       if (q < T && ktile < nkt)
-        wv = *reinterpret_cast<const uint2*>(keep_in + ((b * H + h) * T + q) * (nkt * 4) + ktile * 4);
-      *reinterpret_cast<uint2*>(kw_s + ((buf * 2 + lt) * QT_BWD + r) * 2) = wv;
+        kw_r = *reinterpret_cast<const uint2*>(keep_in + ((b * H + h) * T + q) * (nkt * 4) + ktile * 4);
+    }
+  };
+  auto store_tiles = [&](int buf, int qt) {
+    (void)qt;
+    stage_store<QT_BWD, true>(ldsQ(buf), rq, tid);
+    stage_store<QT_BWD, true>(ldsO(buf), ro, tid);
+    if (tid < QT_BWD) {
+      lse_s[buf * QT_BWD + tid] = lse_r;
+      dv_s[buf * QT_BWD + tid] = dv_r;
+      if constexpr (BIAS) g_s[buf * QT_BWD + tid] = g_r;
+    }
+    if (use_keep && tid >= 64 && tid < 128) {
+      const int r = tid & 31, lt = (tid >> 5) & 1;
+      *reinterpret_cast<uint2*>(kw_s + ((buf * 2 + lt) * QT_BWD + r) * 2) = kw_r;
     }
   };
   load_tiles(0);
@@ -886,7 +901,10 @@ __device__ __forceinline__ void attn_bwd_dq_body(const bf16_t* __restrict__ qkv,
   extern __shared__ float dyn[];   // BIAS: hist [T + RB - 1] (diagonal sums of dS * gate) | table window [T + RB - 1]
   seed = epoch_seed(seed);   // per-step RNG epoch (graph replays)
   const uint32_t mix = seed_mix(seed);
-  __shared__ __attribute__((aligned(16))) char smem[2 * (TILE_SWZ_BYTES + KTILE_PAD_BYTES)];
+  // K and V tiles both in the swz128 image: the 16-B row reads of a ds_read_b128 lane group (rows 0-3 / 12-15 of
+  // one k-chunk + rows 4-11 of the next) hit 16 distinct 16-B bank groups; the padded [64][72] V image put them
+  // 2-way on 8 of them (SQ_LDS_BANK_CONFLICT 26-32 % of the backward's LDS cycles)
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE_SWZ_BYTES];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
@@ -940,32 +958,39 @@ __device__ __forceinline__ void attn_bwd_dq_body(const bf16_t* __restrict__ qkv,
     stage_tab_window(tw, rb.tab + h * (2 * T - 1), toff, T32);
   }
 
-  auto ldsK = [&](int buf) { return smem + buf * (TILE_SWZ_BYTES + KTILE_PAD_BYTES); };
-  auto ldsV = [&](int buf) { return smem + buf * (TILE_SWZ_BYTES + KTILE_PAD_BYTES) + TILE_SWZ_BYTES; };
+  auto ldsK = [&](int buf) { return smem + buf * 2 * TILE_SWZ_BYTES; };
+  auto ldsV = [&](int buf) { return smem + buf * 2 * TILE_SWZ_BYTES + TILE_SWZ_BYTES; };
   const int nkt = (int)cdiv(T, KT);
   uint4 rk[2], rv[2];
   stage_load<KT, true>(rk, rowbase + (H + h) * HD, 0, T, RS, 1.0f, tid);
-  stage_load<KT, false>(rv, rowbase + (2 * H + h) * HD, 0, T, RS, 1.0f, tid);
+  stage_load<KT, true>(rv, rowbase + (2 * H + h) * HD, 0, T, RS, 1.0f, tid);
   stage_store<KT, true>(ldsK(0), rk, tid);
-  stage_store<KT, false>(ldsV(0), rv, tid);
+  stage_store<KT, true>(ldsV(0), rv, tid);
   __syncthreads();
   const uint32_t thr = drop_thr(drop_p);
   const uint64_t half_tp = (uint64_t)(T + 1) >> 1;
+  uint32_t kw_next[NG];
+#pragma unroll
+  for (int u = 0; u < NG; ++u)
+    kw_next[u] = (DROP && KEEP && !qout[u]) ? keep_in[((b * H + h) * T + qme[u]) * (nkt * 4) + g] : 0u;
   for (int kt = 0; kt < nkt; ++kt) {
     const int cur = kt & 1;
     const bool more = kt + 1 < nkt;
     if (more) {
       stage_load<KT, true>(rk, rowbase + (H + h) * HD, (int64_t)(kt + 1) * KT, T, RS, 1.0f, tid);
-      stage_load<KT, false>(rv, rowbase + (2 * H + h) * HD, (int64_t)(kt + 1) * KT, T, RS, 1.0f, tid);
+      stage_load<KT, true>(rv, rowbase + (2 * H + h) * HD, (int64_t)(kt + 1) * KT, T, RS, 1.0f, tid);
     }
     const char* K_ = ldsK(cur);
     const char* V_ = ldsV(cur);
     f32x4_t ds[NG][4];
-    // stored keep bits of this key tile (16 per lane and row), or the in-kernel hash when none were stored
+    // stored keep bits of this key tile (16 per lane and row; loaded one tile ahead), or the in-kernel hash
     uint32_t kw[NG];
 #pragma unroll
-    for (int u = 0; u < NG; ++u)
-      kw[u] = (DROP && KEEP && !qout[u]) ? keep_in[((b * H + h) * T + qme[u]) * (nkt * 4) + kt * 4 + g] : 0u;
+    for (int u = 0; u < NG; ++u) {
+      kw[u] = kw_next[u];
+      if (DROP && KEEP && more && !qout[u])
+        kw_next[u] = keep_in[((b * H + h) * T + qme[u]) * (nkt * 4) + (kt + 1) * 4 + g];
+    }
     // MASKED: the tile holds padded (>= klen) or missing (>= T) keys.  Elsewhere no per-element compare: rows
     // past T have zero dO and D, so their dS is exactly 0 whatever p is.
     auto tile = [&](auto masked_c) {
@@ -981,7 +1006,7 @@ __device__ __forceinline__ void attn_bwd_dq_body(const bf16_t* __restrict__ qkv,
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
           const bf16x8_t ka = lds_b128(K_, swz128(16 * s + (lane & 15), ks * 32 + 8 * g));
-          const bf16x8_t va = lds_b128(V_, ((16 * s + (lane & 15)) * PADROW + ks * 32 + 8 * g) * 2);
+          const bf16x8_t va = lds_b128(V_, swz128(16 * s + (lane & 15), ks * 32 + 8 * g));
 #pragma unroll
           for (int u = 0; u < NG; ++u) {
             sa[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka, qf[u][ks], sa[u], 0, 0, 0);
@@ -1086,7 +1111,7 @@ __device__ __forceinline__ void attn_bwd_dq_body(const bf16_t* __restrict__ qkv,
     }
     if (more) {
       stage_store<KT, true>(ldsK(cur ^ 1), rk, tid);
-      stage_store<KT, false>(ldsV(cur ^ 1), rv, tid);
+      stage_store<KT, true>(ldsV(cur ^ 1), rv, tid);
     }
     __syncthreads();
   }

@@ -293,6 +293,7 @@ __device__ __forceinline__ void load_dyc(const bf16_t* dyp, int64_t c0, int64_t 
 // their 15 partial sums (P[10], A, Bv, dgamma, dbeta, dmask) into ws with fp32 atomics (63 time
 // blocks per address), conv0_bwd_finalize combines them.  dy is prefetched 4 time steps ahead.
 constexpr int NQ = 15;
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
 
 template <int CPT, int PF>
 __global__ void __launch_bounds__(256) conv0_gn_bwd_kernel(const float* __restrict__ wave,
@@ -332,6 +333,11 @@ __global__ void __launch_bounds__(256) conv0_gn_bwd_kernel(const float* __restri
   for (int i = 0; i < CPT; ++i)
 #pragma unroll
     for (int q = 0; q < NQ; ++q) acc[i][q] = 0.f;
+  f32x2_t acc2[CPT / 2 > 0 ? CPT / 2 : 1][NQ];      // (CPT even: the packed accumulators)
+#pragma unroll
+  for (int i = 0; i < (CPT / 2 > 0 ? CPT / 2 : 1); ++i)
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) acc2[i][q] = f32x2_t{0.f, 0.f};
   const int nper = (nt + L.rpp - 1) / L.rpp;
   const int ta = r0 * nper;
   const int tb = min(nt, ta + nper);
@@ -359,6 +365,33 @@ __global__ void __launch_bounds__(256) conv0_gn_bwd_kernel(const float* __restri
       for (int u = 0; u < PF; ++u) {
         const int t = tg + u;
         if (t < tb) {
+          if constexpr (CPT % 2 == 0) {
+            // channel pairs in packed fp32 (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32: two lanes' worth of the
+            // FIR, the 10 tap sums and the 5 statistics per instruction); the same operations and rounding as the
+            // scalar path, only GELU / GELU' stay per channel
+#pragma unroll
+            for (int pi = 0; pi < CPT / 2; ++pi) {
+              const int i0 = 2 * pi, i1 = 2 * pi + 1;
+              f32x2_t v = {0.f, 0.f};
+#pragma unroll
+              for (int j = 0; j < K0; ++j) v = __builtin_elementwise_fma(f32x2_t{wr[i0][j], wr[i1][j]}, f32x2_t{x[j], x[j]}, v);
+              const f32x2_t xh = (v - f32x2_t{mu[i0], mu[i1]}) * f32x2_t{rs[i0], rs[i1]};
+              const f32x2_t g = __builtin_elementwise_fma(f32x2_t{ga[i0], ga[i1]}, xh, f32x2_t{be[i0], be[i1]});
+              float gl0, gd0, gl1, gd1;
+              gelu_and_grad(g.x, gl0, gd0);
+              gelu_and_grad(g.y, gl1, gd1);
+              const f32x2_t cu = {cur[u][i0], cur[u][i1]};
+              const f32x2_t dg = cu * f32x2_t{mk[i0], mk[i1]} * f32x2_t{gd0, gd1};
+              const f32x2_t dxh = dg * f32x2_t{ga[i0], ga[i1]};
+#pragma unroll
+              for (int j = 0; j < K0; ++j) acc2[pi][j] = __builtin_elementwise_fma(dxh, f32x2_t{x[j], x[j]}, acc2[pi][j]);
+              acc2[pi][10] += dxh;
+              acc2[pi][11] = __builtin_elementwise_fma(dxh, xh, acc2[pi][11]);
+              acc2[pi][12] = __builtin_elementwise_fma(dg, xh, acc2[pi][12]);
+              acc2[pi][13] += dg;
+              acc2[pi][14] = __builtin_elementwise_fma(cu, f32x2_t{gl0, gl1}, acc2[pi][14]);
+            }
+          } else {
           float v[CPT];
           fir<CPT>(wr, x, v);
 #pragma unroll
@@ -377,6 +410,7 @@ __global__ void __launch_bounds__(256) conv0_gn_bwd_kernel(const float* __restri
             acc[i][13] += dg;
             acc[i][14] = fmaf(cur[u][i], gl, acc[i][14]);
           }
+          }
           if (t + 1 < tb) win_advance(x, xs, t);
         }
       }
@@ -385,6 +419,15 @@ __global__ void __launch_bounds__(256) conv0_gn_bwd_kernel(const float* __restri
 #pragma unroll
         for (int i = 0; i < CPT; ++i) cur[u][i] = nxt[u][i];
     }
+  }
+  if constexpr (CPT % 2 == 0) {
+#pragma unroll
+    for (int pi = 0; pi < CPT / 2; ++pi)
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        acc[2 * pi][q] = acc2[pi][q].x;
+        acc[2 * pi + 1][q] = acc2[pi][q].y;
+      }
   }
   // reduce over the rpp thread-rows sharing the same channels, then one atomic per (b, c, q) per block
 #pragma unroll

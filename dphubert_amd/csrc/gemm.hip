@@ -2653,7 +2653,9 @@ static bool ppw_ok(const DphGemmArgs& a) {
   auto op_ok = [&](const DphMat& d, int64_t cols, bool batched_ok) {
     const int64_t al = d.row_stride | d.batch_stride | d.z_inner | d.z_outer;
     if ((al & 7) != 0 || (reinterpret_cast<uintptr_t>(d.ptr) & 15) != 0) return false;
-    if (d.row_stride >= (1 << 24) || d.row_stride < ((cols + 7) & ~(int64_t)7)) return false;
+    // (rows may overlap -- conv windows, row stride s*C < k*C -- when the extent is whole 16-B chunks; a ragged
+    // extent needs rows padded to the chunk, as dph_gemm requires)
+    if (d.row_stride >= (1 << 24) || ((cols & 7) != 0 && d.row_stride < ((cols + 7) & ~(int64_t)7))) return false;
     int64_t last;
     if (d.rows_per_batch > 0) {
       if (!batched_ok || d.rows_per_batch < pp::BK || d.rows_per_batch >= (1 << 24)) return false;

@@ -212,7 +212,9 @@ def test_model_step_passes_stored_keep_bits(monkeypatch):
     from dphubert_amd.synthetic import HUBERT_BASE_CONFIG
     from dphubert_amd.trainer import seeded_model
     cfg = copy.deepcopy(HUBERT_BASE_CONFIG)
-    cfg.update(encoder_num_layers=1, encoder_attention_dropout=0.1)
+    # (layer drop 0: with HuBERT-Base's 0.05 the single layer is skipped in 1 of 20 steps, depending on the global
+    # RNG state the earlier tests of the process left behind)
+    cfg.update(encoder_num_layers=1, encoder_attention_dropout=0.1, encoder_layer_drop=0.0)
     m = seeded_model(cfg, 0).to(DEV).train()
     seen = []
     real = ops.call
