@@ -969,7 +969,12 @@ __device__ __forceinline__ float row16_sum(float v) {
 // Returns true when the check-free copy ran: then the wave issued exactly FM*FN stores of C (plus FM*FN of
 // pre_out when requested) and no other memory operation is left outstanding (the persistent kernel's
 // counted waits rely on it).
-template <class C, int ACT, bool DROP>
+// WIDE (ping-pong kernels): in the check-free bf16 copy, the 4-column groups of fragment pairs (j, j + 1) are
+// exchanged between lane groups g and g ^ 1 (v_permlane16_swap_b32: odd 16-lane rows of the group-j register with
+// the even rows of the group-(j+1) register), so each lane stores 8 consecutive columns with one 16-B store
+// instead of two 8-B ones (the store tail is issue-bound: guide T21).  Not for the persistent ring kernel, whose
+// counted waits assume one store per fragment.
+template <class C, int ACT, bool DROP, bool WIDE = false>
 __device__ __forceinline__ bool direct_epi_t(const DphGemmArgs& a, int64_t z, int64_t mw, int64_t nw, int lane,
                                              const f32x4_t (&acc)[C::FM][C::FN]) {
   constexpr int FM = C::FM, FN = C::FN;
@@ -1068,11 +1073,14 @@ __device__ __forceinline__ bool direct_epi_t(const DphGemmArgs& a, int64_t z, in
   const uint64_t e_base = ((uint64_t)(z * a.M + a.drop_row_offset + ml)) * (uint64_t)N + (uint64_t)nl;
   // CK: bounds and zero-row checks, any output type (edge tiles, row_len, fp32 outputs); interior tiles
   // with a bf16 output run the check-free copy
+  // (WIDE: 16-B aligned rows are needed for the widened stores -- row stride % 8 == 0; wave-uniform)
+  const bool wide = WIDE && (rs & 7) == 0;
   auto frags = [&](auto ck) {
     constexpr bool CK = decltype(ck)::value;
     const bool obf = !CK || out_bf16;
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
+      uint2 opk[FN], ppk[FN];   // (WIDE, !CK: this row's packed outputs, stored after the column loop)
       if (i == 0) {
         load_in(0, ck);
         if (FM > 1) load_in(1, ck);
@@ -1138,6 +1146,11 @@ __device__ __forceinline__ bool direct_epi_t(const DphGemmArgs& a, int64_t z, in
         asm volatile("" ::"v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(pre[0]));
         continue;
 #endif
+        if (WIDE && !CK && wide) {
+          opk[j] = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
+          if (a.pre_out) ppk[j] = make_uint2(pack2bf(pre[0], pre[1]), pack2bf(pre[2], pre[3]));
+          continue;
+        }
         if (a.pre_out) *reinterpret_cast<uint2*>(prow + 32 * j) = make_uint2(pack2bf(pre[0], pre[1]), pack2bf(pre[2], pre[3]));
         if (obf) {
           *reinterpret_cast<uint2*>(crow + 32 * j) = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
@@ -1150,6 +1163,27 @@ __device__ __forceinline__ bool direct_epi_t(const DphGemmArgs& a, int64_t z, in
           *q = make_float4(v[0], v[1], v[2], v[3]);
         }
       }
+#ifndef DPH_EPI_NOSTORE
+      if constexpr (WIDE && !CK) {
+        if (wide) {
+          // lane group g stores columns 16 (j + (g & 1)) + 8 (g >> 1) .. + 7 of the pair (j, j + 1)
+          const int g = lane >> 4;
+          const int off = 32 * (g & 1) + 16 * (g >> 1) - 8 * g;   // bytes, relative to this lane's column nl
+          auto st_pairs = [&](char* rowp, uint2 (&pk)[FN]) {
+#pragma unroll
+            for (int j = 0; j + 1 < FN; j += 2) {
+              const auto rx = __builtin_amdgcn_permlane16_swap(pk[j].x, pk[j + 1].x, false, false);
+              const auto ry = __builtin_amdgcn_permlane16_swap(pk[j].y, pk[j + 1].y, false, false);
+              *reinterpret_cast<uint4*>(rowp + 32 * j + off) = make_uint4(rx[0], ry[0], rx[1], ry[1]);
+            }
+            if constexpr (FN % 2 == 1) *reinterpret_cast<uint2*>(rowp + 32 * (FN - 1)) = pk[FN - 1];
+          };
+          const int64_t ro = roff(i, ck);
+          if (a.pre_out) st_pairs(pb + ro * 2, ppk);
+          st_pairs(cb + ro * 2, opk);
+        }
+      }
+#endif
     }
   };
   const bool lean = mfull && nfull && !a.row_len && out_bf16 && !rpb;
@@ -2101,7 +2135,7 @@ __global__ void __launch_bounds__(C::NT, C::WPE) pp_gemm_kernel(const DphGemmArg
     bar();
   }
   if (wr == 0) bar();            // pairs with group 1's extra barrier
-  ring::direct_epi_t<C, ACT, DROP>(a, z, m0 + wr * C::WTM, n0 + wc * C::WTN, lane, acc);
+  ring::direct_epi_t<C, ACT, DROP, true>(a, z, m0 + wr * C::WTM, n0 + wc * C::WTN, lane, acc);
 }
 }  // namespace pp
 
