@@ -85,6 +85,24 @@ def workload(args):
     return tcfg, scfg, layers, kw, desc
 
 
+def trained_like_masks(student, seed: int = 0):
+    """log_alpha of a prune.py student near its 0.75 target: per layer, a seeded random subset of 4 of 12 heads,
+    768 of 3072 FFN units and 320 of 512 conv channels at log_alpha = +10 (sampled mask 1), the rest at -10
+    (sampled s < 0, clamped to exactly 0 by hardconcrete.py:99 -- the heads the attention kernels skip)."""
+    keep = {"hard_concrete_for_heads": 1 / 3, "hard_concrete_for_intermediate": 0.25, "hard_concrete": 0.625}
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        for name, mod in student.named_modules():
+            frac = keep.get(name.rsplit(".", 1)[-1])
+            if frac is None or getattr(mod, "log_alpha", None) is None:
+                continue
+            n = mod.log_alpha.numel()
+            k = max(1, round(frac * n))
+            la = torch.full((n,), -10.0)
+            la[torch.randperm(n, generator=g)[:k]] = 10.0
+            mod.log_alpha.copy_(la.to(mod.log_alpha.device))
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -261,6 +279,10 @@ def main():
     ap.add_argument("--grad-comm", choices=["fp32", "bf16"], default="fp32",
                     help="payload of the gradient all-reduce at N > 1 (bf16: half the xGMI bytes)")
     ap.add_argument("--accum", type=int, default=1, help="micro-batches per optimizer step (a step = one micro-batch)")
+    ap.add_argument("--masks", choices=["init", "trained"], default="init",
+                    help="student HardConcrete log_alpha: the reference init (hardconcrete.py:70-74; the headline) or "
+                         "trained-like = a prune.py student near its 0.75 target (log_alpha +-10: 4 of 12 heads, 768 of "
+                         "3072 FFN units and 320 of 512 conv channels per layer kept, the rest sampled exactly 0)")
     ap.add_argument("--graphs", choices=["on", "off"], default="on",
                     help="on: replay the whole step as one captured HIP graph after the eager warm-up steps")
     ap.add_argument("--lengths", choices=["fixed", "bucketed"], default="fixed",
@@ -302,6 +324,8 @@ def main():
     n_student = sum(p.numel() for n, p in module.student_model.named_parameters() if "log_alpha" not in n)
     flop_utt = step_flops_per_utt(tcfg, scfg, len(module.distill_layers), int(args.seconds * 16000))
     module.global_step = 5000            # target sparsity reached (0.75)
+    if args.masks == "trained":
+        trained_like_masks(module.student_model)
     module = module.to(dev)
     graphs = args.graphs == "on"
     trainer = Trainer(module, clip_norm=10.0, graphs=graphs, graph_warmup=2, accum_grad=args.accum,
@@ -401,7 +425,7 @@ def main():
                    "distill_layers": distill_layers, "student_params": n_student,
                    "step_gflop_per_utt": round(flop_utt / 1e9, 1),
                    "parallelism": f"dp{world}", "accum_grad": args.accum, "grad_comm": args.grad_comm,
-                   "lengths": args.lengths},
+                   "lengths": args.lengths, "masks": args.masks},
         "peak_hbm_gib": round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 2),
         "step_mode": "hip_graph" if graphed else "eager",
     }
