@@ -34,7 +34,7 @@ class DphGemmArgs(C.Structure):
                 ("alpha", f32), ("dropout_p", f32), ("seed", u64), ("bias", vp), ("colmask", vp), ("smask", vp),
                 ("vec_z_inner", i64), ("pre_out", vp), ("aux_in", vp), ("residual", vp), ("colsum_out", vp),
                 ("colsum_aux", vp), ("row_len", vp), ("len_rows", i64), ("drop_row_offset", i64),
-                ("workspace", vp), ("workspace_bytes", i64), ("colsum_n", i64), ("flags", i64)]
+                ("workspace", vp), ("workspace_bytes", i64), ("colsum_n", i64), ("flags", i64), ("dyn_ext", vp)]
 
 
 class DphTensorSlot(C.Structure):
@@ -61,6 +61,12 @@ _SIGS = {
     "dph_abi_version": ([], C.c_int),
     "dph_gemm": ([C.POINTER(DphGemmArgs), S], C.c_int),
     "dph_gemm_mn_plan": ([i64, i64, i64, i64], C.c_int),
+    "dph_ffn_compact": ([vp, i64, i64, vp, vp, S], C.c_int),
+    "dph_gather_rows_bf16": ([vp, i64, vp, vp, i64, i64, S], C.c_int),
+    "dph_gather_cols_bf16": ([vp, i64, vp, vp, i64, i64, S], C.c_int),
+    "dph_gather_vec_f32": ([vp, vp, vp, i64, S], C.c_int),
+    "dph_scatter_rows_f32": ([vp, vp, vp, i64, i64, i64, C.c_int, S], C.c_int),
+    "dph_scatter_cols_f32": ([vp, vp, vp, i64, i64, i64, C.c_int, S], C.c_int),
     "dph_layernorm_fwd": ([vp, vp, vp, vp, vp, vp, vp, i64, i64, f32, f32, u64, S], C.c_int),
     "dph_layernorm_bwd": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, f32, u64, vp, f32, u64, vp, vp, vp, vp, vp, i64,
                            S],
@@ -130,8 +136,8 @@ _SIGS = {
 
 _lib = None
 # include/dphubert_hip.h layout (3: dph_adamw_step_dev, dph_set_rng_epoch; 4: dph_event_*; 5: LN bwd / colsum
-# workspaces; 12: dph_hc_bank_fwd / dph_hc_bank_bwd; 15: dph_gemm_mn_plan)
-ABI_VERSION = 15
+# workspaces; 12: dph_hc_bank_fwd / dph_hc_bank_bwd; 15: dph_gemm_mn_plan; 16: DphGemmArgs.dyn_ext, dph_ffn_compact + gathers / scatters)
+ABI_VERSION = 16
 
 
 class DphError(RuntimeError):

@@ -1942,7 +1942,15 @@ __global__ void __launch_bounds__(C::NT, C::WPE) pp_gemm_kernel(const DphGemmArg
     m0 = (int64_t)(gm0 + (l - lq * gh)) * C::BM;
     n0 = (int64_t)lq * C::BN;
   }
-  const int nk = (int)(a.K / BK);
+  int nk = (int)(a.K / BK);
+  if (a.dyn_ext != nullptr) {
+    // device-side extents (packed FFN units): whole blocks past m / n return before any barrier, the K loop
+    // stops at k (a multiple of 64, >= 128)
+    const int em = __builtin_amdgcn_readfirstlane(a.dyn_ext[0]), en = __builtin_amdgcn_readfirstlane(a.dyn_ext[1]);
+    const int ek = __builtin_amdgcn_readfirstlane(a.dyn_ext[2]);
+    if ((em > 0 && m0 >= em) || (en > 0 && n0 >= en)) return;
+    if (ek > 0 && ek < a.K) nk = ek / BK;
+  }
   const bf16_t* Ab = reinterpret_cast<const bf16_t*>(a.A.ptr) + z_addr(a.A, z);
   const bf16_t* Bb = reinterpret_cast<const bf16_t*>(a.B.ptr) + z_addr(a.B, z);
   // DMA sources (element offsets, < 2^31: checked on the host) of instruction jj of each half-tile kind:
@@ -2217,6 +2225,10 @@ __global__ void __launch_bounds__(C::NT, C::WPE) ppw_gemm_kernel(const DphGemmAr
     const uint32_t lq = l / gh;
     m0 = (int64_t)(gm0 + (l - lq * gh)) * C::BM;
     n0 = (int64_t)lq * C::BN;
+  }
+  if (a.dyn_ext != nullptr) {   // device-side extents: blocks past m / n return at once (packed FFN units)
+    const int em = __builtin_amdgcn_readfirstlane(a.dyn_ext[0]), en = __builtin_amdgcn_readfirstlane(a.dyn_ext[1]);
+    if ((em > 0 && m0 >= em) || (en > 0 && n0 >= en)) return;
   }
   const int32_t kbeg = (int32_t)(split * kchunk);
   const int32_t kend = (int32_t)min<int64_t>(a.K, kbeg + kchunk);
@@ -2988,6 +3000,12 @@ extern "C" int dph_gemm(const DphGemmArgs* args, hipStream_t stream) {
     DPH_REQUIRE(a.act != DPH_ACT_GELU || a.pre_out, "dph_gemm: DPH_GEMM_PRE_DGK needs pre_out");
   }
   const int kind = dgk ? pp_pick(a) : gemm_kind(a, kchunk);
+  // ((mn, mn) weight gradients off the ppw plan compute the full static extent: correct, only slower -- the packed
+  // FFN operands are finite wherever a product is stored and read)
+  DPH_REQUIRE(!a.dyn_ext || (!a.a_kcontig && !a.b_kcontig) || (kind >= 12 && kind <= 16 && a.splits == 1),
+              "dph_gemm: device-side extents (dyn_ext) need a ping-pong layout (k-contiguous A and B, K %% 64 == 0, dense "
+              "aligned C) or the (mn, mn) weight-gradient plan: M=%lld N=%lld K=%lld", (long long)a.M, (long long)a.N,
+              (long long)a.K);
   if (kind >= 12 && kind <= 16) {
     DPH_REQUIRE(cdiv(a.M, 128) < 65536 && a.batch < 65536, "dph_gemm: grid too large");
     // column sums through a workspace slab when the caller passed one (kernels.py does for splits == 1)

@@ -126,7 +126,8 @@ def gemm(A: DphMat, B: DphMat, Cm: DphMat, M: int, N: int, K: int, *, a_kcontig:
          c_dtype: int = OUT_BF16, act: int = ACT_NONE, alpha: float = 1.0, batch: int = 1, splits: int = 1,
          bias=None, colmask=None, smask=None, vec_z_inner: int = 0, pre_out=None, aux_in=None, residual=None,
          colsum_out=None, colsum_aux=None, row_len=None, len_rows: int = 0, dropout_p: float = 0.0, seed: int = 0,
-         drop_row_offset: int = 0, colsum_n: int = 0, device=None, flags: int = 0):
+         drop_row_offset: int = 0, colsum_n: int = 0, device=None, flags: int = 0, dyn=None):
+    """``dyn``: (int32 device tensor, offset) of a {m, n, k} device-side extent triplet (DphGemmArgs.dyn_ext)."""
     ws = None
     ws_bytes = 0
     if splits > 1:
@@ -145,7 +146,8 @@ def gemm(A: DphMat, B: DphMat, Cm: DphMat, M: int, N: int, K: int, *, a_kcontig:
                        dropout_p, seed & 0xFFFFFFFFFFFFFFFF, ptr(bias), ptr(colmask), ptr(smask), vec_z_inner,
                        ptr(pre_out), ptr(aux_in), ptr(residual), ptr(colsum_out), ptr(colsum_aux), ptr(row_len),
                        len_rows, drop_row_offset, ptr(ws), ws_bytes, colsum_n,
-                       flags | (GEMM_NO_PERSIST if _SHARED_GPU[0] else 0))
+                       flags | (GEMM_NO_PERSIST if _SHARED_GPU[0] else 0),
+                       (dyn[0].data_ptr() + 4 * dyn[1]) if dyn is not None else None)
     prof = LaunchProfiler.active
     if prof is not None:
         e0, e1 = _Event(), _Event()
@@ -186,7 +188,7 @@ def choose_splits(M: int, N: int, K: int, batch: int = 1, target_blocks: int = 5
 
 def linear_fwd(x: torch.Tensor, w_bf16: torch.Tensor, bias: Optional[torch.Tensor] = None, *, out=None,
                out_dtype=BF16, act=ACT_NONE, pre_out=None, colmask=None, smask=None, residual=None,
-               dropout_p=0.0, seed=0, row_len=None, len_rows=0, colsum_out=None, pre_dgk=False):
+               dropout_p=0.0, seed=0, row_len=None, len_rows=0, colsum_out=None, pre_dgk=False, dyn=None):
     """y = epi(x @ w^T + b); x [M,K] bf16, w [N,K] bf16 (nn.Linear layout).
 
     ``pre_dgk`` (act=ACT_GELU): pre_out receives gelu'(pre)*colmask*keep/(1-p), the aux input of the matching
@@ -201,12 +203,12 @@ def linear_fwd(x: torch.Tensor, w_bf16: torch.Tensor, bias: Optional[torch.Tenso
     gemm(dense(x), dense(w_bf16), dense(out), M, N, K, a_kcontig=True, b_kcontig=True, c_dtype=c_dtype, act=act,
          bias=bias, colmask=colmask, smask=smask, pre_out=pre_out, residual=residual, dropout_p=dropout_p,
          seed=seed, row_len=row_len, len_rows=len_rows, colsum_out=colsum_out,
-         flags=GEMM_PRE_DGK if pre_dgk else 0)
+         flags=GEMM_PRE_DGK if pre_dgk else 0, dyn=dyn)
     return out
 
 
 def linear_dgrad(dy: torch.Tensor, w_bf16: torch.Tensor, *, out=None, residual=None, act=ACT_NONE, aux_in=None,
-                 colmask=None, colsum_out=None, colsum_aux=None, dropout_p=0.0, seed=0, colsum_n=0, w_t=None):
+                 colmask=None, colsum_out=None, colsum_aux=None, dropout_p=0.0, seed=0, colsum_n=0, w_t=None, dyn=None):
     """dx = epi(dy @ w); dy [M,N] bf16, w [N,K] bf16 -> [M,K] bf16.
 
     ``w_t``: the [K,N] transposed image of w (ops.t_image): both GEMM operands are then
@@ -223,12 +225,12 @@ def linear_dgrad(dy: torch.Tensor, w_bf16: torch.Tensor, *, out=None, residual=N
         B, bk = dense(w_bf16), False
     gemm(dense(dy), B, dense(out), M, K, N, a_kcontig=True, b_kcontig=bk, residual=residual, act=act,
          aux_in=aux_in, colmask=colmask, colsum_out=colsum_out, colsum_aux=colsum_aux, dropout_p=dropout_p,
-         seed=seed, colsum_n=colsum_n)
+         seed=seed, colsum_n=colsum_n, dyn=dyn)
     return out
 
 
 def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, accumulate: bool = True, n_out: int = 0,
-                 k_in: int = 0):
+                 k_in: int = 0, dyn=None):
     """dw (+)= dy^T @ x; dy [M,N] bf16, x [M,K] bf16, dw [N,K] fp32.
 
     ``n_out`` / ``k_in`` < the operands' widths: only the first n_out x k_in block is produced
@@ -238,5 +240,5 @@ def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, accumulate
     Nw, Kw = (n_out or N), (k_in or K)
     splits = choose_splits(Nw, Kw, M)
     ws = gemm(dense(dy), dense(x), mat(dw, Kw), Nw, Kw, M, a_kcontig=False, b_kcontig=False,
-              c_dtype=OUT_F32_ACCUM if accumulate else OUT_F32, splits=splits, device=dy.device)
+              c_dtype=OUT_F32_ACCUM if accumulate else OUT_F32, splits=splits, device=dy.device, dyn=dyn)
     return ws

@@ -1346,6 +1346,113 @@ def _ffn_interm_bwd(dy, sv, db1, dmask, cfg, F_):
                           colsum_out=db1, colsum_aux=dmask, dropout_p=cfg["p_interm"], seed=sv["seed_i"], colsum_n=F_)
 
 
+
+def _ffn_forward(cfg, xin, w1, b1, w2, b2, im, lmf, resid, need, sv):
+    """FeedForward (components.py:726-748) + dropout + layer mask + residual: resid + drop(FFN(xin)) * lmf.
+
+    Training with sampled intermediate masks (``im``, HardConcrete interm units): the units whose mask is exactly
+    0 (hardconcrete.py:99 clamps) are dropped from every FFN GEMM -- dph_ffn_compact packs the active ones to the
+    front of Fc-wide images (W1 rows, W2 columns, b1, mask) and the GEMMs read the active extent from device
+    memory (DphGemmArgs.dyn_ext), so the captured step graph keeps fixed shapes.  The FFN1 dropout then hashes the
+    packed column index (the same keep rate, another draw than the full-width layout would take).
+    Taken where cfg["ffn_compact"] is set (the trainer's choice from the gate's expected zero fraction: the
+    gathers / scatters cost ~25 us per layer, measured to pay off from ~40 % zero units); DPH_FFN_COMPACT=1 / 0
+    forces it on / off (tests, A/B)."""
+    M, D = xin.shape
+    dev = xin.device
+    # intermediate width F of a pruned student is ragged: stored 8-padded (zero weight rows /
+    # columns, bias and mask padding 0 -> the padding columns of u and f are exactly 0)
+    F_ = w1.shape[0]
+    Fp = pad8(F_)
+    W1 = padded_image(w1, Fp, D)
+    W2 = padded_image(w2, D, Fp)
+    b1p, imp = padded_vec(b1, Fp), padded_vec(im, Fp)
+    seed_i = SEEDS.next() if cfg["p_interm"] > 0 else 0
+    dgk = _ffn_dgk(D) and need
+    seed_o = SEEDS.next() if cfg["p_drop"] > 0 else 0
+    y_pre = torch.empty(M, D, dtype=BF16, device=dev) if (need and lmf is not None) else None
+    mode = os.environ.get("DPH_FFN_COMPACT", "auto")
+    compact = mode == "1" or (mode != "0" and cfg.get("ffn_compact", False))
+    if dgk and im is not None and compact and Fp <= 8192:
+        Fc = max(128, (Fp + 63) // 64 * 64)
+        idx = torch.empty(Fc, dtype=torch.int32, device=dev)
+        ext = torch.empty(10, dtype=torch.int32, device=dev)
+        call("dph_ffn_compact", ptr(imp), Fp, Fc, ptr(idx), ptr(ext), _s())
+        W1g = torch.empty(Fc, D, dtype=BF16, device=dev)
+        call("dph_gather_rows_bf16", ptr(W1), D, ptr(idx), ptr(W1g), Fc, D, _s())
+        W2g = torch.empty(D, Fc, dtype=BF16, device=dev)
+        call("dph_gather_cols_bf16", ptr(W2), Fp, ptr(idx), ptr(W2g), D, Fc, _s())
+        b1g = torch.empty(Fc, dtype=F32, device=dev)
+        call("dph_gather_vec_f32", ptr(b1p), ptr(idx), ptr(b1g), Fc, _s())
+        mg = torch.empty(Fc, dtype=F32, device=dev)
+        call("dph_gather_vec_f32", ptr(imp), ptr(idx), ptr(mg), Fc, _s())
+        u = torch.empty(M, Fc, dtype=BF16, device=dev)
+        f = K.linear_fwd(xin, W1g, b1g, act=K.ACT_GELU, pre_out=u, colmask=mg, dropout_p=cfg["p_interm"],
+                         seed=seed_i, pre_dgk=True, dyn=(ext, 0))
+        out = K.linear_fwd(f, W2g, b2, smask=lmf, residual=resid, dropout_p=cfg["p_drop"], seed=seed_o,
+                           pre_out=y_pre, dyn=(ext, 3))
+        sv.update(W1=W1, W2=W2, W1g=W1g, W2g=W2g, idx=idx, ext=ext, Fc=Fc, u=u, f=f, y_pre=y_pre, seed_i=seed_i,
+                  seed_o=seed_o, F=F_, imp=mg, dgk=True, compact=True)
+        return out
+    u = torch.empty(M, Fp, dtype=BF16, device=dev) if need else None
+    f = K.linear_fwd(xin, W1, b1p, act=K.ACT_GELU, pre_out=u, colmask=imp, dropout_p=cfg["p_interm"],
+                     seed=seed_i, pre_dgk=dgk)
+    out = K.linear_fwd(f, W2, b2, smask=lmf, residual=resid, dropout_p=cfg["p_drop"], seed=seed_o, pre_out=y_pre)
+    sv.update(W1=W1, W2=W2, u=u, f=f, y_pre=y_pre, seed_i=seed_i, seed_o=seed_o, F=F_, imp=imp, dgk=dgk,
+              compact=False)
+    return out
+
+
+def _ffn_backward(cfg, sv, dy, xin, pr, go, dmask, residual=None):
+    """Backward of _ffn_forward from dy = d(FFN2 output) (after the output dropout / layer mask): the W2 / b1 / W1
+    gradients into ``go``'s buffers, the intermediate-mask gradient into ``dmask`` [F], returns d(xin) (+ residual)."""
+    M, D = xin.shape
+    dev = xin.device
+    F_ = sv["F"]
+    if sv["compact"]:
+        Fc, idx, ext = sv["Fc"], sv["idx"], sv["ext"]
+        dw2, direct2 = go.buf(pr["w2"], zero=True)
+        dW2g = torch.empty(D, Fc, dtype=F32, device=dev)
+        k1 = K.linear_wgrad(dy, sv["f"], dW2g, accumulate=False, dyn=(ext, 0))
+        call("dph_scatter_cols_f32", ptr(dW2g), ptr(idx), ptr(dw2), F_, D, Fc, 1, _s())
+        db1, _ = go.buf(pr["b1"])
+        db1g, dmg = zeros_f32(Fc, dev), zeros_f32(Fc, dev)
+        W2t = t_image(sv["W2"])
+        if W2t is not None:
+            W2gT = torch.empty(Fc, D, dtype=BF16, device=dev)
+            call("dph_gather_rows_bf16", ptr(W2t), D, ptr(idx), ptr(W2gT), Fc, D, _s())
+        else:
+            W2gT = sv["W2g"].t().contiguous()
+        du = K.linear_dgrad(dy, sv["W2g"], w_t=W2gT, act=K.ACT_GELU_BWD_DGK, aux_in=sv["u"], residual=sv["f"],
+                            colmask=sv["imp"], colsum_out=db1g, colsum_aux=dmg, colsum_n=Fc, dyn=(ext, 0))
+        call("dph_scatter_cols_f32", ptr(db1g), ptr(idx), ptr(db1), 0, 1, Fc, 1, _s())
+        call("dph_scatter_cols_f32", ptr(dmg), ptr(idx), ptr(dmask), 0, 1, Fc, 1, _s())
+        dw1, _ = go.buf(pr["w1"], zero=True)
+        dW1g = torch.empty(Fc, D, dtype=F32, device=dev)
+        k2 = K.linear_wgrad(du, xin, dW1g, accumulate=False, dyn=(ext, 6))
+        call("dph_scatter_rows_f32", ptr(dW1g), ptr(idx), ptr(dw1), D, Fc, D, 1, _s())
+        W1t = t_image(sv["W1"])
+        if W1t is not None:
+            W1gT = torch.empty(D, Fc, dtype=BF16, device=dev)
+            call("dph_gather_cols_bf16", ptr(W1t), W1t.shape[1], ptr(idx), ptr(W1gT), D, Fc, _s())
+        else:
+            W1gT = sv["W1g"].t().contiguous()
+        dx = K.linear_dgrad(du, sv["W1g"], w_t=W1gT, residual=residual, dyn=(ext, 3))
+        del k1, k2
+        return dx
+    dw2, direct = go.buf(pr["w2"], zero=False)
+    with wgrad_side(dy, sv["f"], enable=direct):
+        k1 = K.linear_wgrad(dy, sv["f"], dw2, accumulate=direct, k_in=F_)
+    db1, _ = go.buf(pr["b1"])
+    du = _ffn_interm_bwd(dy, sv, db1, dmask, cfg, F_)
+    dw1, direct = go.buf(pr["w1"], zero=False)
+    with wgrad_side(du, xin, enable=direct):
+        k2 = K.linear_wgrad(du, xin, dw1, accumulate=direct, n_out=F_)
+    dx = K.linear_dgrad(du, sv["W1"], w_t=t_image(sv["W1"]), residual=residual)
+    del k1, k2
+    return dx
+
+
 class EncoderLayerFn(torch.autograd.Function):
     """h (B*T, D) bf16 -> layer output (B*T, D) bf16.
 
@@ -1395,22 +1502,7 @@ class EncoderLayerFn(torch.autograd.Function):
              0, _s())
         # ---------------- feed-forward block ----------------
         if use_ff:
-            # intermediate width F of a pruned student is ragged: stored 8-padded (zero weight rows /
-            # columns, bias and mask padding 0 -> the padding columns of u and f are exactly 0)
-            F_ = w1.shape[0]
-            Fp = pad8(F_)
-            W1 = padded_image(w1, Fp, D)
-            W2 = padded_image(w2, D, Fp)
-            b1p, imp = padded_vec(b1, Fp), padded_vec(im, Fp)
-            seed_i = SEEDS.next() if cfg["p_interm"] > 0 else 0
-            u = torch.empty(M, Fp, dtype=BF16, device=dev) if need else None
-            dgk = _ffn_dgk(D) and u is not None
-            f = K.linear_fwd(h1, W1, b1p, act=K.ACT_GELU, pre_out=u, colmask=imp, dropout_p=cfg["p_interm"],
-                             seed=seed_i, pre_dgk=dgk)
-            seed_o = SEEDS.next() if cfg["p_drop"] > 0 else 0
-            y_pre = torch.empty(M, D, dtype=BF16, device=dev) if (need and lmf is not None) else None
-            s2 = K.linear_fwd(f, W2, b2, smask=lmf, residual=h1, dropout_p=cfg["p_drop"], seed=seed_o, pre_out=y_pre)
-            sv.update(W1=W1, W2=W2, u=u, f=f, y_pre=y_pre, seed_i=seed_i, seed_o=seed_o, F=F_, imp=imp, dgk=dgk)
+            s2 = _ffn_forward(cfg, h1, w1, b1, w2, b2, im, lmf, h1, need, sv)
         else:
             s2 = h1
         out = torch.empty_like(h)
@@ -1469,21 +1561,7 @@ class EncoderLayerFn(torch.autograd.Function):
             rs2 = torch.empty(M, dtype=F32, device=dev)
             call("dph_layernorm_fwd", ptr(s1), None, ptr(ln2_w), ptr(ln2_b), ptr(xn2), ptr(mu2), ptr(rs2), M, D,
                  1e-5, 0.0, 0, _s())
-            F_ = w1.shape[0]
-            Fp = pad8(F_)
-            W1 = padded_image(w1, Fp, D)
-            W2 = padded_image(w2, D, Fp)
-            b1p, imp = padded_vec(b1, Fp), padded_vec(im, Fp)
-            seed_i = SEEDS.next() if cfg["p_interm"] > 0 else 0
-            u = torch.empty(M, Fp, dtype=BF16, device=dev) if need else None
-            dgk = _ffn_dgk(D) and u is not None
-            f = K.linear_fwd(xn2, W1, b1p, act=K.ACT_GELU, pre_out=u, colmask=imp, dropout_p=cfg["p_interm"],
-                             seed=seed_i, pre_dgk=dgk)
-            seed_o = SEEDS.next() if cfg["p_drop"] > 0 else 0
-            y_pre = torch.empty(M, D, dtype=BF16, device=dev) if (need and lmf is not None) else None
-            out = K.linear_fwd(f, W2, b2, smask=lmf, residual=s1, dropout_p=cfg["p_drop"], seed=seed_o,
-                               pre_out=y_pre)
-            sv.update(W1=W1, W2=W2, u=u, f=f, y_pre=y_pre, seed_i=seed_i, seed_o=seed_o, F=F_, imp=imp, dgk=dgk)
+            out = _ffn_forward(cfg, xn2, w1, b1, w2, b2, im, lmf, s1, need, sv)
         else:
             out = s1.clone() if s1 is h else s1
         if need:
@@ -1518,23 +1596,14 @@ class EncoderLayerFn(torch.autograd.Function):
             call("dph_branch_bwd", ptr(dout), ptr(dy), M, D, cfg["p_drop"], sv["seed_o"], ptr(lmf), None, 0, ptr(db2),
                  ptr(sv["y_pre"]) if has_lmf else None, ptr(g["lmf"]), _s())
             F_ = sv["F"]
-            dw2, direct = go.buf(pr["w2"], zero=False)
-            with wgrad_side(dy, sv["f"], enable=direct):
-                k1 = K.linear_wgrad(dy, sv["f"], dw2, accumulate=direct, k_in=F_)
-            db1, _ = go.buf(pr["b1"])
             g["im"] = z(F_) if has_im else None
-            du = _ffn_interm_bwd(dy, sv, db1, g["im"] if has_im else z(F_), cfg, F_)
-            dw1, direct = go.buf(pr["w1"], zero=False)
-            with wgrad_side(du, xn2, enable=direct):
-                k2 = K.linear_wgrad(du, xn2, dw1, accumulate=direct, n_out=F_)
-            dxn2 = K.linear_dgrad(du, sv["W1"], w_t=t_image(sv["W1"]))
+            dxn2 = _ffn_backward(cfg, sv, dy, xn2, pr, go, g["im"] if has_im else z(F_))
             ds1 = torch.empty_like(dout)
             dln2w, _ = go.buf(pr["ln2_w"])
             dln2b, _ = go.buf(pr["ln2_b"])
             call("dph_layernorm_bwd_ld", ptr(dxn2), ptr(s1), None, ptr(ln2_w), ptr(mu2), ptr(rs2), ptr(ds1),
                  ptr(dln2w), ptr(dln2b), M, D, D, 0.0, 0, None, 0.0, 0, None, None, None, None, ptr(dout),
                  *ln_ws(M, D, dev), _s())
-            del k1, k2
         else:
             ds1 = dout
         # ---- attention branch: s1 = h + drop(attn(LN1(h))) * lma ----
@@ -1673,17 +1742,8 @@ class EncoderLayerFn(torch.autograd.Function):
                  ptr(dln2w), ptr(dln2b), M, D, 0.0, 0, ptr(dy), cfg["p_drop"], sv["seed_o"], ptr(lmf), ptr(db2),
                  ptr(sv["y_pre"]), ptr(g["lmf"]), *ln_ws(M, D, dev), _s())
             F_ = sv["F"]
-            dw2, direct = go.buf(pr["w2"], zero=False)
-            with wgrad_side(dy, sv["f"], enable=direct):
-                k1 = K.linear_wgrad(dy, sv["f"], dw2, accumulate=direct, k_in=F_)
-            db1, _ = go.buf(pr["b1"])
             g["im"] = z(F_) if has_im else None
-            du = _ffn_interm_bwd(dy, sv, db1, g["im"] if has_im else z(F_), cfg, F_)
-            dw1, direct = go.buf(pr["w1"], zero=False)
-            with wgrad_side(du, h1, enable=direct):
-                k2 = K.linear_wgrad(du, h1, dw1, accumulate=direct, n_out=F_)
-            dh1 = K.linear_dgrad(du, sv["W1"], w_t=t_image(sv["W1"]), residual=ds2)
-            del k1, k2
+            dh1 = _ffn_backward(cfg, sv, dy, h1, pr, go, g["im"] if has_im else z(F_), residual=ds2)
         else:
             call("dph_layernorm_bwd", ptr(dout), ptr(s2), None, ptr(ln2_w), ptr(mu2), ptr(rs2), ptr(ds2),
                  ptr(dln2w), ptr(dln2b), M, D, 0.0, 0, None, 0.0, 0, None, None, None, None, *ln_ws(M, D, dev),

@@ -279,10 +279,38 @@ class Trainer:
             self.module.teacher_stream = side
             self._wgrad_stream = wside
 
+    # ---- FFN-unit compaction policy ------------------------------------------------------------
+    FFN_COMPACT_MIN_ZERO = 0.4       # expected fraction of exactly-zero FFN units from which the packed FFN pays
+    FFN_COMPACT_EVERY = 500          # optimizer steps between re-evaluations under graph replay
+
+    def refresh_ffn_compaction(self) -> bool:
+        """Per FFN intermediate HardConcrete gate: run the layer's FFN GEMMs over the active units only
+        (ops._ffn_forward) when the expected fraction of exactly-zero units, 1 - l0_norm / n (hardconcrete.py:62-65:
+        P(mask != 0) = sigmoid(log_alpha - beta log(-l / r))), is >= FFN_COMPACT_MIN_ZERO.  One host read of
+        the expected counts.  Returns whether any gate changed its mode (captured graphs are then stale)."""
+        from .wav2vec2.hardconcrete import HardConcrete
+        mods = [mod for name, mod in self.module.student_model.named_modules()
+                if isinstance(mod, HardConcrete) and name.endswith("hard_concrete_for_intermediate")]
+        if not mods:
+            return False
+        with torch.no_grad():
+            nz = torch.stack([mod.l0_norm() for mod in mods]).float().cpu().tolist()
+        changed = False
+        for mod, k in zip(mods, nz):
+            flag = 1.0 - k / mod.n_in >= self.FFN_COMPACT_MIN_ZERO
+            if bool(getattr(mod, "dph_compact", False)) != flag:
+                mod.dph_compact = flag
+                changed = True
+        return changed
+
     # ---- one step ----------------------------------------------------------------------------
     def step(self, batch, profiled: bool = False):
         m = self.module
         m.train()
+        if self._micro == 0 and (not self._graphs or m.global_step % self.FFN_COMPACT_EVERY == 0):
+            if self.refresh_ffn_compaction() and self._graphs:
+                self._graphs = {}            # recaptured at this step with the new FFN layouts
+                self._prof_graph = None
         dev = batch[0].device
         zero = self._micro == 0
         final = self._micro + 1 == self.accum_grad

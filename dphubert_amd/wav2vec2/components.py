@@ -504,6 +504,10 @@ class EncoderLayer(Module):
             "p_interm": ff.intermediate_dropout.p if (tr and ff is not None) else 0.0,
             "lengths": key_len,
             "pre_norm": bool(self.layer_norm_first),
+            # FFN GEMMs over the active units only (ops._ffn_forward): the trainer sets this per gate from its
+            # expected zero fraction (Trainer.refresh_ffn_compaction)
+            "ffn_compact": bool(getattr(ff.hard_concrete_for_intermediate, "dph_compact", False))
+            if (ff is not None and ff.hard_concrete_for_intermediate is not None) else False,
         }
         if ff is not None and tr and ff.output_dropout.p != self.dropout.p:
             raise NotImplementedError("FFN output dropout != layer dropout")

@@ -97,6 +97,11 @@ typedef struct DphGemmArgs {
   int64_t workspace_bytes;
   int64_t colsum_n;       /* column sums only for n < colsum_n (0: all N); padded-width operands */
   int64_t flags;          /* DPH_GEMM_* bits below                                */
+  /* device-side extents {m, n, k} (int32, <= 0: the static M / N / K): blocks past m / n return at once, the
+   * K loop stops at k (a multiple of 64, >= 128, with zero operand columns up to it).  The FFN GEMMs over the
+   * packed active units (dph_ffn_compact) read the active count this way inside a captured step graph.
+   * Ping-pong kernels only (pp_gemm_kernel: m / n / k, ppw_gemm_kernel: m / n); NULL = static.            */
+  const int32_t* dyn_ext;
 } DphGemmArgs;
 
 /* flags: one tile per block even where the persistent ring grid applies -- for GEMMs that share the
@@ -115,6 +120,25 @@ const char* dph_gemm_variant(const DphGemmArgs* args);
  * them) and an eligible layout runs ppw_gemm_kernel + splitk_reduce; replaces the split heuristic of the
  * register-staged kernel for the wgrads of components.py:107/:272/:406-408/:430/:733/:741, lightning.py:258 */
 int dph_gemm_mn_plan(int64_t M, int64_t N, int64_t K, int64_t batch);
+
+/* ------------------------------------------------------------------------ *
+ * FFN units with an exactly-zero HardConcrete mask (hardconcrete.py:99; components.py:733-741): the layer's FFN
+ * GEMMs run over the active units packed to the front of Fc-wide images (Fc % 64 == 0, Fc >= max(F, 128)).
+ * dph_ffn_compact: idx[Fc] = the active units in order (-1 past them), ext[10] = three {m, n, k} dyn_ext
+ * triplets (N, K, M dynamic = keff = max(128, active count rounded up to 64)) and the active count.
+ * Gathers pack W1 rows / W2 columns / vectors by idx (zero past the active count); scatters add the packed
+ * gradients back to the full-width ones (accumulate = 1) or overwrite their active entries (0).
+ * ------------------------------------------------------------------------ */
+int dph_ffn_compact(const float* mask, int64_t F, int64_t Fc, int32_t* idx, int32_t* ext, hipStream_t stream);
+int dph_gather_rows_bf16(const void* src, int64_t ld_src, const int32_t* idx, void* dst, int64_t rows, int64_t cols,
+                         hipStream_t stream);
+int dph_gather_cols_bf16(const void* src, int64_t ld_src, const int32_t* idx, void* dst, int64_t rows, int64_t Fc,
+                         hipStream_t stream);
+int dph_gather_vec_f32(const float* src, const int32_t* idx, float* dst, int64_t Fc, hipStream_t stream);
+int dph_scatter_rows_f32(const float* src, const int32_t* idx, float* dst, int64_t ld_dst, int64_t rows, int64_t cols,
+                         int accumulate, hipStream_t stream);
+int dph_scatter_cols_f32(const float* src, const int32_t* idx, float* dst, int64_t ld_dst, int64_t rows, int64_t Fc,
+                         int accumulate, hipStream_t stream);
 
 /* ------------------------------------------------------------------------ *
  * LayerNorm over the last dim (rows x D), fp32 statistics, eps=1e-5.

@@ -573,3 +573,53 @@ def test_attention_bwd_merged_grid_matches_split(T, lens, p, monkeypatch):
         outs.append(dqkv)
     assert torch.isfinite(outs[0].float()).all()
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("pre_norm", [False, True])
+def test_ffn_compaction_matches_full_width(monkeypatch, pre_norm):
+    """FFN units whose sampled HardConcrete mask is exactly 0 (hardconcrete.py:99) are dropped from the FFN GEMMs
+    (dph_ffn_compact + device-side extents, ops._ffn_forward / _ffn_backward): the layer output, the input gradient
+    and every parameter / log_alpha gradient equal the full-width computation's (components.py:726-748), with
+    masks exactly 0, exactly 1 and in between, dropout 0, post- and pre-norm layers, an active count that is not a
+    multiple of 64."""
+    import copy
+    from dphubert_amd.synthetic import HUBERT_BASE_CONFIG
+    from dphubert_amd.trainer import seeded_model
+    cfg = copy.deepcopy(HUBERT_BASE_CONFIG)
+    cfg.update(encoder_num_layers=2, encoder_projection_dropout=0.0, encoder_attention_dropout=0.0,
+               encoder_ff_interm_dropout=0.0, encoder_dropout=0.0, encoder_layer_drop=0.0,
+               encoder_prune_feed_forward_intermediate=True, encoder_layer_norm_first=pre_norm)
+    torch.manual_seed(0)
+    wave = (torch.randn(2, 16000 * 2) * 0.1).to(DEV)
+
+    def run(compact):
+        monkeypatch.setenv("DPH_FFN_COMPACT", "1" if compact else "0")
+        m = seeded_model(cfg, 0).to(DEV).train()
+        g = torch.Generator().manual_seed(3)
+        for name, mod in m.named_modules():
+            if name.endswith("hard_concrete_for_intermediate"):
+                n = mod.log_alpha.numel()
+                la = torch.full((n,), -10.0)
+                keep = torch.randperm(n, generator=g)[:701]          # 701 active units: ragged K extent
+                la[keep] = torch.randn(701, generator=g) * 2.0       # masks in (0, 1] and some clamped to 1
+                with torch.no_grad():
+                    mod.log_alpha.copy_(la.to(DEV))
+                mod.set_noise((torch.rand(n, generator=g) * 0.98 + 0.01).to(DEV))
+        x, _ = m(wave)
+        loss = x.float().pow(2).mean()
+        loss.backward()
+        torch.cuda.synchronize()
+        grads = {n: p.grad.detach().float().cpu().clone() for n, p in m.named_parameters() if p.grad is not None}
+        return x.float().cpu(), grads
+
+    x0, g0 = run(False)
+    x1, g1 = run(True)
+    assert (x1 - x0).norm() / x0.norm() < 2e-3
+    assert set(g0) == set(g1)
+    for n in g0:
+        a, b = g1[n], g0[n]
+        den = b.norm().item()
+        if den == 0.0:
+            assert a.norm().item() == 0.0, n
+            continue
+        assert (a - b).norm().item() / den < 2e-2, (n, (a - b).norm().item() / den)
