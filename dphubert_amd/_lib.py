@@ -62,6 +62,8 @@ _SIGS = {
     "dph_gemm": ([C.POINTER(DphGemmArgs), S], C.c_int),
     "dph_gemm_mn_plan": ([i64, i64, i64, i64], C.c_int),
     "dph_ffn_compact": ([vp, i64, i64, vp, vp, S], C.c_int),
+    "dph_ffn_pack": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, i64, S], C.c_int),
+    "dph_ffn_unpack_grads": ([vp, vp, vp, vp, vp, vp, i64, vp, vp, vp, i64, i64, S], C.c_int),
     "dph_gather_rows_bf16": ([vp, i64, vp, vp, i64, i64, S], C.c_int),
     "dph_gather_cols_bf16": ([vp, i64, vp, vp, i64, i64, S], C.c_int),
     "dph_gather_vec_f32": ([vp, vp, vp, i64, S], C.c_int),

@@ -14,6 +14,8 @@
 //   scatters          dW1 rows, dW2 columns, db1 / dmask of the packed units -> the full-width gradients
 #include "common.h"
 
+#include <algorithm>
+
 namespace dph {
 namespace {
 
@@ -128,10 +130,126 @@ __global__ void __launch_bounds__(256) scatter_cols_f32_kernel(const float* __re
   *d = accum ? *d + v : v;
 }
 
+// All packed images of a layer in ONE launch (blockIdx.y = job, grid-stride over blockIdx.x): the FFN GEMM
+// operands of the forward AND the backward (W1 rows, W2 columns, W2^T rows, W1^T columns, b1 / mask), built
+// once per forward -- one launch instead of six (each small gather cost a launch's worth of GPU time).
+struct FfnPack {
+  const bf16_t *w1, *w2, *w2t, *w1t;   // [Fp][D], [D][Fp], [Fp][D], [D][Fp] (w2t / w1t may be null)
+  const float *b1, *mask;              // [Fp] (b1 may be null: zeros)
+  bf16_t *w1g, *w2g, *w2gt, *w1gt;     // [Fc][D], [D][Fc], [Fc][D], [D][Fc]
+  float *b1g, *mg;                     // [Fc]
+  int64_t Fp, Fc, D;
+};
+
+__global__ void __launch_bounds__(256) ffn_pack_kernel(const FfnPack p, const int32_t* __restrict__ idx) {
+  const int job = blockIdx.y;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  const int64_t t0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (job == 0 || job == 2) {                       // row gathers, 16-B chunks
+    const bf16_t* src = job == 0 ? p.w1 : p.w2t;
+    bf16_t* dst = job == 0 ? p.w1g : p.w2gt;
+    if (!src) return;
+    const int64_t c8 = p.D / 8, n = p.Fc * c8;
+    for (int64_t e = t0; e < n; e += stride) {
+      const int64_t j = e / c8, c = (e - j * c8) * 8;
+      const int32_t r = idx[j];
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (r >= 0) v = *reinterpret_cast<const uint4*>(src + (int64_t)r * p.D + c);
+      *reinterpret_cast<uint4*>(dst + j * p.D + c) = v;
+    }
+  } else if (job == 1 || job == 3) {                // column gathers, 2 columns per thread
+    const bf16_t* src = job == 1 ? p.w2 : p.w1t;
+    bf16_t* dst = job == 1 ? p.w2g : p.w1gt;
+    if (!src) return;
+    const int64_t h = p.Fc / 2, n = p.D * h;
+    for (int64_t e = t0; e < n; e += stride) {
+      const int64_t r = e / h, j = (e - r * h) * 2;
+      const int32_t i0 = idx[j], i1 = idx[j + 1];
+      const uint16_t* srow = reinterpret_cast<const uint16_t*>(src + r * p.Fp);
+      const uint32_t lo = i0 >= 0 ? (uint32_t)srow[i0] : 0u, hi = i1 >= 0 ? (uint32_t)srow[i1] : 0u;
+      *reinterpret_cast<uint32_t*>(dst + r * p.Fc + j) = lo | (hi << 16);
+    }
+  } else {                                          // vectors
+    for (int64_t j = t0; j < p.Fc; j += stride) {
+      const int32_t i = idx[j];
+      p.b1g[j] = (i >= 0 && p.b1) ? p.b1[i] : 0.f;
+      p.mg[j] = i >= 0 ? p.mask[i] : 0.f;
+    }
+  }
+}
+
+// The packed gradients back to the full-width ones, one launch: dW2 columns, dW1 rows, db1, dmask (accumulate)
+struct FfnUnpack {
+  const float *dw2g, *dw1g, *db1g, *dmg;   // [D][Fc], [Fc][D], [Fc], [Fc]
+  float *dw2, *dw1, *db1, *dm;             // [D][F] (row stride ld2), [F][D], [F], [F]
+  int64_t ld2, Fc, D;
+};
+
+__global__ void __launch_bounds__(256) ffn_unpack_kernel(const FfnUnpack p, const int32_t* __restrict__ idx) {
+  const int job = blockIdx.y;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  const int64_t t0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (job == 0) {
+    const int64_t n = p.D * p.Fc;
+    for (int64_t e = t0; e < n; e += stride) {
+      const int64_t r = e / p.Fc, j = e - r * p.Fc;
+      const int32_t i = idx[j];
+      if (i >= 0) p.dw2[r * p.ld2 + i] += p.dw2g[e];
+    }
+  } else if (job == 1) {
+    const int64_t c4 = p.D / 4, n = p.Fc * c4;
+    for (int64_t e = t0; e < n; e += stride) {
+      const int64_t j = e / c4, c = (e - j * c4) * 4;
+      const int32_t r = idx[j];
+      if (r < 0) continue;
+      const float4 v = *reinterpret_cast<const float4*>(p.dw1g + j * p.D + c);
+      float4* d = reinterpret_cast<float4*>(p.dw1 + (int64_t)r * p.D + c);
+      float4 o = *d;
+      o.x += v.x; o.y += v.y; o.z += v.z; o.w += v.w;
+      *d = o;
+    }
+  } else {
+    for (int64_t j = t0; j < p.Fc; j += stride) {
+      const int32_t i = idx[j];
+      if (i < 0) continue;
+      if (p.db1) p.db1[i] += p.db1g[j];
+      if (p.dm) p.dm[i] += p.dmg[j];
+    }
+  }
+}
+
 }  // namespace
 }  // namespace dph
 
 using namespace dph;
+
+extern "C" int dph_ffn_pack(const void* w1, const void* w2, const void* w2t, const void* w1t, const float* b1,
+                            const float* mask, const int32_t* idx, void* w1g, void* w2g, void* w2gt, void* w1gt,
+                            float* b1g, float* mg, int64_t Fp, int64_t Fc, int64_t D, hipStream_t stream) {
+  DPH_REQUIRE(w1 && w2 && mask && idx && w1g && w2g && b1g && mg && (!w2t || w2gt) && (!w1t || w1gt),
+              "dph_ffn_pack: null pointer");
+  DPH_REQUIRE(D % 8 == 0 && Fc % 64 == 0 && Fc >= Fp && Fp % 2 == 0, "dph_ffn_pack: D=%lld Fp=%lld Fc=%lld",
+              (long long)D, (long long)Fp, (long long)Fc);
+  const FfnPack p{reinterpret_cast<const bf16_t*>(w1), reinterpret_cast<const bf16_t*>(w2),
+                  reinterpret_cast<const bf16_t*>(w2t), reinterpret_cast<const bf16_t*>(w1t), b1, mask,
+                  reinterpret_cast<bf16_t*>(w1g), reinterpret_cast<bf16_t*>(w2g), reinterpret_cast<bf16_t*>(w2gt),
+                  reinterpret_cast<bf16_t*>(w1gt), b1g, mg, Fp, Fc, D};
+  const int64_t work = std::max<int64_t>(Fc * (D / 8), D * (Fc / 2));
+  const unsigned gx = (unsigned)std::min<int64_t>(cdiv(work, 256), 1024);
+  hipLaunchKernelGGL(ffn_pack_kernel, dim3(gx, 5), dim3(256), 0, stream, p, idx);
+  return check_launch("dph_ffn_pack");
+}
+
+extern "C" int dph_ffn_unpack_grads(const float* dw2g, const float* dw1g, const float* db1g, const float* dmg,
+                                    const int32_t* idx, float* dw2, int64_t ld2, float* dw1, float* db1, float* dm,
+                                    int64_t Fc, int64_t D, hipStream_t stream) {
+  DPH_REQUIRE(dw2g && dw1g && db1g && dmg && idx && dw2 && dw1 && D % 4 == 0,
+              "dph_ffn_unpack_grads: null pointer or D %% 4 != 0");
+  const FfnUnpack p{dw2g, dw1g, db1g, dmg, dw2, dw1, db1, dm, ld2, Fc, D};
+  const unsigned gx = (unsigned)std::min<int64_t>(cdiv(D * Fc, 256), 1024);
+  hipLaunchKernelGGL(ffn_unpack_kernel, dim3(gx, 3), dim3(256), 0, stream, p, idx);
+  return check_launch("dph_ffn_unpack_grads");
+}
 
 extern "C" int dph_ffn_compact(const float* mask, int64_t F, int64_t Fc, int32_t* idx, int32_t* ext,
                                hipStream_t stream) {

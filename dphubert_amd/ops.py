@@ -1356,7 +1356,7 @@ def _ffn_forward(cfg, xin, w1, b1, w2, b2, im, lmf, resid, need, sv):
     memory (DphGemmArgs.dyn_ext), so the captured step graph keeps fixed shapes.  The FFN1 dropout then hashes the
     packed column index (the same keep rate, another draw than the full-width layout would take).
     Taken where cfg["ffn_compact"] is set (the trainer's choice from the gate's expected zero fraction: the
-    gathers / scatters cost ~25 us per layer, measured to pay off from ~40 % zero units); DPH_FFN_COMPACT=1 / 0
+    packing / unpacking launches cost ~10 us per layer, measured to pay off from ~30 % zero units); DPH_FFN_COMPACT=1 / 0
     forces it on / off (tests, A/B)."""
     M, D = xin.shape
     dev = xin.device
@@ -1378,21 +1378,24 @@ def _ffn_forward(cfg, xin, w1, b1, w2, b2, im, lmf, resid, need, sv):
         idx = torch.empty(Fc, dtype=torch.int32, device=dev)
         ext = torch.empty(10, dtype=torch.int32, device=dev)
         call("dph_ffn_compact", ptr(imp), Fp, Fc, ptr(idx), ptr(ext), _s())
+        # every packed operand of the forward AND the backward GEMMs in one launch (W1 rows, W2 columns, the rows /
+        # columns of their transposed images, b1, mask)
+        W1t, W2t = t_image(W1), t_image(W2)
         W1g = torch.empty(Fc, D, dtype=BF16, device=dev)
-        call("dph_gather_rows_bf16", ptr(W1), D, ptr(idx), ptr(W1g), Fc, D, _s())
         W2g = torch.empty(D, Fc, dtype=BF16, device=dev)
-        call("dph_gather_cols_bf16", ptr(W2), Fp, ptr(idx), ptr(W2g), D, Fc, _s())
+        W2gT = torch.empty(Fc, D, dtype=BF16, device=dev) if W2t is not None else None
+        W1gT = torch.empty(D, Fc, dtype=BF16, device=dev) if W1t is not None else None
         b1g = torch.empty(Fc, dtype=F32, device=dev)
-        call("dph_gather_vec_f32", ptr(b1p), ptr(idx), ptr(b1g), Fc, _s())
         mg = torch.empty(Fc, dtype=F32, device=dev)
-        call("dph_gather_vec_f32", ptr(imp), ptr(idx), ptr(mg), Fc, _s())
+        call("dph_ffn_pack", ptr(W1), ptr(W2), ptr(W2t), ptr(W1t), ptr(b1p), ptr(imp), ptr(idx), ptr(W1g), ptr(W2g),
+             ptr(W2gT), ptr(W1gT), ptr(b1g), ptr(mg), Fp, Fc, D, _s())
         u = torch.empty(M, Fc, dtype=BF16, device=dev)
         f = K.linear_fwd(xin, W1g, b1g, act=K.ACT_GELU, pre_out=u, colmask=mg, dropout_p=cfg["p_interm"],
                          seed=seed_i, pre_dgk=True, dyn=(ext, 0))
         out = K.linear_fwd(f, W2g, b2, smask=lmf, residual=resid, dropout_p=cfg["p_drop"], seed=seed_o,
                            pre_out=y_pre, dyn=(ext, 3))
-        sv.update(W1=W1, W2=W2, W1g=W1g, W2g=W2g, idx=idx, ext=ext, Fc=Fc, u=u, f=f, y_pre=y_pre, seed_i=seed_i,
-                  seed_o=seed_o, F=F_, imp=mg, dgk=True, compact=True)
+        sv.update(W1=W1, W2=W2, W1g=W1g, W2g=W2g, W1gT=W1gT, W2gT=W2gT, idx=idx, ext=ext, Fc=Fc, u=u, f=f,
+                  y_pre=y_pre, seed_i=seed_i, seed_o=seed_o, F=F_, imp=mg, dgk=True, compact=True)
         return out
     u = torch.empty(M, Fp, dtype=BF16, device=dev) if need else None
     f = K.linear_fwd(xin, W1, b1p, act=K.ACT_GELU, pre_out=u, colmask=imp, dropout_p=cfg["p_interm"],
@@ -1411,33 +1414,23 @@ def _ffn_backward(cfg, sv, dy, xin, pr, go, dmask, residual=None):
     F_ = sv["F"]
     if sv["compact"]:
         Fc, idx, ext = sv["Fc"], sv["idx"], sv["ext"]
-        dw2, direct2 = go.buf(pr["w2"], zero=True)
         dW2g = torch.empty(D, Fc, dtype=F32, device=dev)
         k1 = K.linear_wgrad(dy, sv["f"], dW2g, accumulate=False, dyn=(ext, 0))
-        call("dph_scatter_cols_f32", ptr(dW2g), ptr(idx), ptr(dw2), F_, D, Fc, 1, _s())
-        db1, _ = go.buf(pr["b1"])
         db1g, dmg = zeros_f32(Fc, dev), zeros_f32(Fc, dev)
-        W2t = t_image(sv["W2"])
-        if W2t is not None:
-            W2gT = torch.empty(Fc, D, dtype=BF16, device=dev)
-            call("dph_gather_rows_bf16", ptr(W2t), D, ptr(idx), ptr(W2gT), Fc, D, _s())
-        else:
-            W2gT = sv["W2g"].t().contiguous()
+        W2gT = sv["W2gT"] if sv["W2gT"] is not None else sv["W2g"].t().contiguous()
         du = K.linear_dgrad(dy, sv["W2g"], w_t=W2gT, act=K.ACT_GELU_BWD_DGK, aux_in=sv["u"], residual=sv["f"],
                             colmask=sv["imp"], colsum_out=db1g, colsum_aux=dmg, colsum_n=Fc, dyn=(ext, 0))
-        call("dph_scatter_cols_f32", ptr(db1g), ptr(idx), ptr(db1), 0, 1, Fc, 1, _s())
-        call("dph_scatter_cols_f32", ptr(dmg), ptr(idx), ptr(dmask), 0, 1, Fc, 1, _s())
-        dw1, _ = go.buf(pr["w1"], zero=True)
         dW1g = torch.empty(Fc, D, dtype=F32, device=dev)
         k2 = K.linear_wgrad(du, xin, dW1g, accumulate=False, dyn=(ext, 6))
-        call("dph_scatter_rows_f32", ptr(dW1g), ptr(idx), ptr(dw1), D, Fc, D, 1, _s())
-        W1t = t_image(sv["W1"])
-        if W1t is not None:
-            W1gT = torch.empty(D, Fc, dtype=BF16, device=dev)
-            call("dph_gather_cols_bf16", ptr(W1t), W1t.shape[1], ptr(idx), ptr(W1gT), D, Fc, _s())
-        else:
-            W1gT = sv["W1g"].t().contiguous()
+        W1gT = sv["W1gT"] if sv["W1gT"] is not None else sv["W1g"].t().contiguous()
         dx = K.linear_dgrad(du, sv["W1g"], w_t=W1gT, residual=residual, dyn=(ext, 3))
+        # the packed gradients back to the full-width (bucket) ones in one launch (accumulating: the buffers are the
+        # zeroed-at-step-start buckets or zero-filled)
+        dw2, _ = go.buf(pr["w2"], zero=True)
+        dw1, _ = go.buf(pr["w1"], zero=True)
+        db1, _ = go.buf(pr["b1"])
+        call("dph_ffn_unpack_grads", ptr(dW2g), ptr(dW1g), ptr(db1g), ptr(dmg), ptr(idx), ptr(dw2), F_, ptr(dw1),
+             ptr(db1), ptr(dmask), Fc, D, _s())
         del k1, k2
         return dx
     dw2, direct = go.buf(pr["w2"], zero=False)

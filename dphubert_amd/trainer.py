@@ -280,7 +280,7 @@ class Trainer:
             self._wgrad_stream = wside
 
     # ---- FFN-unit compaction policy ------------------------------------------------------------
-    FFN_COMPACT_MIN_ZERO = 0.4       # expected fraction of exactly-zero FFN units from which the packed FFN pays
+    FFN_COMPACT_MIN_ZERO = 0.3       # expected fraction of exactly-zero FFN units from which the packed FFN pays
     FFN_COMPACT_EVERY = 500          # optimizer steps between re-evaluations under graph replay
 
     def refresh_ffn_compaction(self) -> bool:

@@ -139,6 +139,16 @@ int dph_scatter_rows_f32(const float* src, const int32_t* idx, float* dst, int64
                          int accumulate, hipStream_t stream);
 int dph_scatter_cols_f32(const float* src, const int32_t* idx, float* dst, int64_t ld_dst, int64_t rows, int64_t Fc,
                          int accumulate, hipStream_t stream);
+/* one launch for every packed FFN operand of a layer (forward and backward GEMMs): W1 rows, W2 columns, the rows
+ * of W2^T and the columns of W1^T (w2t / w1t may be NULL: then w2gt / w1gt are not written), b1 (may be NULL:
+ * zeros) and mask; and one launch adding the packed gradients back: dW2 columns (row stride ld2), dW1 rows, db1,
+ * dmask (db1 / dm may be NULL) */
+int dph_ffn_pack(const void* w1, const void* w2, const void* w2t, const void* w1t, const float* b1, const float* mask,
+                 const int32_t* idx, void* w1g, void* w2g, void* w2gt, void* w1gt, float* b1g, float* mg, int64_t Fp,
+                 int64_t Fc, int64_t D, hipStream_t stream);
+int dph_ffn_unpack_grads(const float* dw2g, const float* dw1g, const float* db1g, const float* dmg, const int32_t* idx,
+                         float* dw2, int64_t ld2, float* dw1, float* db1, float* dm, int64_t Fc, int64_t D,
+                         hipStream_t stream);
 
 /* ------------------------------------------------------------------------ *
  * LayerNorm over the last dim (rows x D), fp32 statistics, eps=1e-5.
