@@ -191,7 +191,8 @@ __global__ void __launch_bounds__(256) conv0_stats_finalize(const float* __restr
   rstd[b * p.C + c] = (float)(1.0 / sqrt(M2 / N + (double)eps));
 }
 
-template <bool GN>
+// VEC: C % 8 == 0, every thread's 8 channels one 16-byte store (no per-row branch)
+template <bool GN, bool VEC>
 __global__ void __launch_bounds__(256) conv0_apply_kernel(const float* __restrict__ wave, const float* __restrict__ w,
                                                           const float* __restrict__ bias, Conv0 p,
                                                           const float* __restrict__ gamma,
@@ -233,7 +234,7 @@ __global__ void __launch_bounds__(256) conv0_apply_kernel(const float* __restric
   if (ta >= tb) return;
   float x[K0];
   win_load(x, xs, ta);
-  const bool vec = c0 + 8 <= p.C && p.C % 8 == 0;
+  // (the window advance past the last row reads xs within its K0 - S0 slack, never used)
   for (int t = ta; t < tb; ++t) {
     float o[CPT];
     fir<CPT>(wr, x, o);
@@ -243,7 +244,7 @@ __global__ void __launch_bounds__(256) conv0_apply_kernel(const float* __restric
       o[i] = GN ? gelu_f(v) * mk[i] : v;
     }
     bf16_t* yp = y + ((b * p.L0) + t0 + t) * p.C + c0;
-    if (vec) {
+    if (VEC) {
       *reinterpret_cast<uint4*>(yp) = make_uint4(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]), pack2bf(o[4], o[5]),
                                                  pack2bf(o[6], o[7]));
     } else {
@@ -251,14 +252,15 @@ __global__ void __launch_bounds__(256) conv0_apply_kernel(const float* __restric
       for (int i = 0; i < CPT; ++i)
         if (c0 + i < p.C) yp[i] = f2bf(o[i]);
     }
-    if (t + 1 < tb) win_advance(x, xs, t);
+    win_advance(x, xs, t);
   }
 }
 
 // CPT consecutive bf16 channels of one dy row -> fp32 (one 4/8/16-byte load when aligned)
-template <int CPT>
+// (VEC: the caller guarantees C % CPT == 0, every row a whole vector -- no per-load branch)
+template <int CPT, bool VEC = false>
 __device__ __forceinline__ void load_dyc(const bf16_t* dyp, int64_t c0, int64_t C, float (&d)[CPT]) {
-  if (c0 + CPT <= C && (C % CPT) == 0) {
+  if (VEC || (c0 + CPT <= C && (C % CPT) == 0)) {
     uint32_t r[CPT / 2];
     if constexpr (CPT == 2) {
       r[0] = *reinterpret_cast<const uint32_t*>(dyp);
@@ -295,7 +297,7 @@ __device__ __forceinline__ void load_dyc(const bf16_t* dyp, int64_t c0, int64_t 
 constexpr int NQ = 15;
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
 
-template <int CPT, int PF>
+template <int CPT, int PF, bool VEC>
 __global__ void __launch_bounds__(256) conv0_gn_bwd_kernel(const float* __restrict__ wave,
                                                            const float* __restrict__ w, Conv0 p,
                                                            const float* __restrict__ gamma,
@@ -341,83 +343,86 @@ __global__ void __launch_bounds__(256) conv0_gn_bwd_kernel(const float* __restri
   const int nper = (nt + L.rpp - 1) / L.rpp;
   const int ta = r0 * nper;
   const int tb = min(nt, ta + nper);
+  // one time step of one thread's CPT channels (d: its dy row)
+  auto step = [&](const float (&x)[K0], const float (&d)[CPT]) {
+    if constexpr (CPT % 2 == 0) {
+      // channel pairs in packed fp32 (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32: two lanes' worth of the
+      // FIR, the 10 tap sums and the 5 statistics per instruction); the same operations and rounding as the
+      // scalar path, only GELU / GELU' stay per channel
+#pragma unroll
+      for (int pi = 0; pi < CPT / 2; ++pi) {
+        const int i0 = 2 * pi, i1 = 2 * pi + 1;
+        f32x2_t v = {0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < K0; ++j) v = __builtin_elementwise_fma(f32x2_t{wr[i0][j], wr[i1][j]}, f32x2_t{x[j], x[j]}, v);
+        const f32x2_t xh = (v - f32x2_t{mu[i0], mu[i1]}) * f32x2_t{rs[i0], rs[i1]};
+        const f32x2_t g = __builtin_elementwise_fma(f32x2_t{ga[i0], ga[i1]}, xh, f32x2_t{be[i0], be[i1]});
+        float gl0, gd0, gl1, gd1;
+        gelu_and_grad(g.x, gl0, gd0);
+        gelu_and_grad(g.y, gl1, gd1);
+        const f32x2_t cu = {d[i0], d[i1]};
+        const f32x2_t dg = cu * f32x2_t{mk[i0], mk[i1]} * f32x2_t{gd0, gd1};
+        const f32x2_t dxh = dg * f32x2_t{ga[i0], ga[i1]};
+#pragma unroll
+        for (int j = 0; j < K0; ++j) acc2[pi][j] = __builtin_elementwise_fma(dxh, f32x2_t{x[j], x[j]}, acc2[pi][j]);
+        acc2[pi][10] += dxh;
+        acc2[pi][11] = __builtin_elementwise_fma(dxh, xh, acc2[pi][11]);
+        acc2[pi][12] = __builtin_elementwise_fma(dg, xh, acc2[pi][12]);
+        acc2[pi][13] += dg;
+        acc2[pi][14] = __builtin_elementwise_fma(cu, f32x2_t{gl0, gl1}, acc2[pi][14]);
+      }
+    } else {
+      float v[CPT];
+      fir<CPT>(wr, x, v);
+#pragma unroll
+      for (int i = 0; i < CPT; ++i) {
+        const float xh = (v[i] - mu[i]) * rs[i];
+        const float g = fmaf(ga[i], xh, be[i]);
+        float gl, gd;
+        gelu_and_grad(g, gl, gd);
+        const float dg = d[i] * mk[i] * gd;
+        const float dxh = dg * ga[i];
+#pragma unroll
+        for (int j = 0; j < K0; ++j) acc[i][j] = fmaf(dxh, x[j], acc[i][j]);
+        acc[i][10] += dxh;
+        acc[i][11] = fmaf(dxh, xh, acc[i][11]);
+        acc[i][12] = fmaf(dg, xh, acc[i][12]);
+        acc[i][13] += dg;
+        acc[i][14] = fmaf(d[i], gl, acc[i][14]);
+      }
+    }
+  };
   if (active && ta < tb) {
     const bf16_t* dyrow = dy + ((b * p.L0) + t0) * p.C + c0;
     float x[K0];
     win_load(x, xs, ta);
+    // dy rows prefetched PF steps ahead; a row past tb is clamped to tb - 1 (loaded, never used) so the loads
+    // carry no branch.  The window advance past the last row reads xs within its K0 - S0 slack (never used).
     float cur[PF][CPT], nxt[PF][CPT];
 #pragma unroll
-    for (int u = 0; u < PF; ++u) {
-      if (ta + u < tb) load_dyc<CPT>(dyrow + (int64_t)(ta + u) * p.C, c0, p.C, cur[u]);
-      else
+    for (int u = 0; u < PF; ++u) load_dyc<CPT, VEC>(dyrow + (int64_t)min(ta + u, tb - 1) * p.C, c0, p.C, cur[u]);
+    int tg = ta;
+    for (; tg + PF <= tb; tg += PF) {
 #pragma unroll
-        for (int i = 0; i < CPT; ++i) cur[u][i] = 0.f;
-    }
-    for (int tg = ta; tg < tb; tg += PF) {
-#pragma unroll
-      for (int u = 0; u < PF; ++u) {
-        if (tg + PF + u < tb) load_dyc<CPT>(dyrow + (int64_t)(tg + PF + u) * p.C, c0, p.C, nxt[u]);
-        else
-#pragma unroll
-          for (int i = 0; i < CPT; ++i) nxt[u][i] = 0.f;
-      }
+      for (int u = 0; u < PF; ++u)
+        load_dyc<CPT, VEC>(dyrow + (int64_t)min(tg + PF + u, tb - 1) * p.C, c0, p.C, nxt[u]);
 #pragma unroll
       for (int u = 0; u < PF; ++u) {
-        const int t = tg + u;
-        if (t < tb) {
-          if constexpr (CPT % 2 == 0) {
-            // channel pairs in packed fp32 (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32: two lanes' worth of the
-            // FIR, the 10 tap sums and the 5 statistics per instruction); the same operations and rounding as the
-            // scalar path, only GELU / GELU' stay per channel
-#pragma unroll
-            for (int pi = 0; pi < CPT / 2; ++pi) {
-              const int i0 = 2 * pi, i1 = 2 * pi + 1;
-              f32x2_t v = {0.f, 0.f};
-#pragma unroll
-              for (int j = 0; j < K0; ++j) v = __builtin_elementwise_fma(f32x2_t{wr[i0][j], wr[i1][j]}, f32x2_t{x[j], x[j]}, v);
-              const f32x2_t xh = (v - f32x2_t{mu[i0], mu[i1]}) * f32x2_t{rs[i0], rs[i1]};
-              const f32x2_t g = __builtin_elementwise_fma(f32x2_t{ga[i0], ga[i1]}, xh, f32x2_t{be[i0], be[i1]});
-              float gl0, gd0, gl1, gd1;
-              gelu_and_grad(g.x, gl0, gd0);
-              gelu_and_grad(g.y, gl1, gd1);
-              const f32x2_t cu = {cur[u][i0], cur[u][i1]};
-              const f32x2_t dg = cu * f32x2_t{mk[i0], mk[i1]} * f32x2_t{gd0, gd1};
-              const f32x2_t dxh = dg * f32x2_t{ga[i0], ga[i1]};
-#pragma unroll
-              for (int j = 0; j < K0; ++j) acc2[pi][j] = __builtin_elementwise_fma(dxh, f32x2_t{x[j], x[j]}, acc2[pi][j]);
-              acc2[pi][10] += dxh;
-              acc2[pi][11] = __builtin_elementwise_fma(dxh, xh, acc2[pi][11]);
-              acc2[pi][12] = __builtin_elementwise_fma(dg, xh, acc2[pi][12]);
-              acc2[pi][13] += dg;
-              acc2[pi][14] = __builtin_elementwise_fma(cu, f32x2_t{gl0, gl1}, acc2[pi][14]);
-            }
-          } else {
-          float v[CPT];
-          fir<CPT>(wr, x, v);
-#pragma unroll
-          for (int i = 0; i < CPT; ++i) {
-            const float xh = (v[i] - mu[i]) * rs[i];
-            const float g = fmaf(ga[i], xh, be[i]);
-            float gl, gd;
-            gelu_and_grad(g, gl, gd);
-            const float dg = cur[u][i] * mk[i] * gd;
-            const float dxh = dg * ga[i];
-#pragma unroll
-            for (int j = 0; j < K0; ++j) acc[i][j] = fmaf(dxh, x[j], acc[i][j]);
-            acc[i][10] += dxh;
-            acc[i][11] = fmaf(dxh, xh, acc[i][11]);
-            acc[i][12] = fmaf(dg, xh, acc[i][12]);
-            acc[i][13] += dg;
-            acc[i][14] = fmaf(cur[u][i], gl, acc[i][14]);
-          }
-          }
-          if (t + 1 < tb) win_advance(x, xs, t);
-        }
+        step(x, cur[u]);
+        win_advance(x, xs, tg + u);
       }
 #pragma unroll
       for (int u = 0; u < PF; ++u)
 #pragma unroll
         for (int i = 0; i < CPT; ++i) cur[u][i] = nxt[u][i];
+    }
+    // ragged tail (< PF steps): its rows are already in cur
+#pragma unroll
+    for (int u = 0; u < PF - 1; ++u) {
+      if (tg + u < tb) {
+        step(x, cur[u]);
+        win_advance(x, xs, tg + u);
+      }
     }
   }
   if constexpr (CPT % 2 == 0) {
@@ -696,9 +701,13 @@ extern "C" int dph_conv0_gn_fwd(const float* wave, int64_t B, int64_t S, const f
   hipLaunchKernelGGL(conv0_stats_kernel, dim3(nch, (unsigned)B), dim3(256), 0, stream, wave, w, p, ws, nch);
   hipLaunchKernelGGL(conv0_stats_finalize, dim3((unsigned)cdiv(C, 64), (unsigned)B), dim3(256), 0, stream, ws, p, nch, mean,
                      rstd, 1e-5f);
-  hipLaunchKernelGGL(conv0_apply_kernel<true>, dim3((unsigned)cdiv(p.L0, APPLY_ROWS), (unsigned)B), dim3(256), 0,
-                     stream, wave, w, (const float*)nullptr, p, gamma, beta, mask, mean, rstd,
-                     reinterpret_cast<bf16_t*>(y));
+  const dim3 grid((unsigned)cdiv(p.L0, APPLY_ROWS), (unsigned)B);
+  if (C % 8 == 0)
+    hipLaunchKernelGGL((conv0_apply_kernel<true, true>), grid, dim3(256), 0, stream, wave, w, (const float*)nullptr, p,
+                       gamma, beta, mask, mean, rstd, reinterpret_cast<bf16_t*>(y));
+  else
+    hipLaunchKernelGGL((conv0_apply_kernel<true, false>), grid, dim3(256), 0, stream, wave, w, (const float*)nullptr, p,
+                       gamma, beta, mask, mean, rstd, reinterpret_cast<bf16_t*>(y));
   return check_launch("dph_conv0_gn_fwd");
 }
 
@@ -712,9 +721,14 @@ extern "C" int dph_conv0_fwd(const float* wave, int64_t B, int64_t S, const floa
   }
   DPH_REQUIRE(S >= K0 && C <= 2048, "dph_conv0_fwd: unsupported");
   Conv0 p = make_conv0(B, S, C);
-  hipLaunchKernelGGL(conv0_apply_kernel<false>, dim3((unsigned)cdiv(p.L0, APPLY_ROWS), (unsigned)B), dim3(256), 0,
-                     stream, wave, w, bias, p, (const float*)nullptr, (const float*)nullptr, (const float*)nullptr,
-                     (const float*)nullptr, (const float*)nullptr, reinterpret_cast<bf16_t*>(y));
+  const dim3 grid((unsigned)cdiv(p.L0, APPLY_ROWS), (unsigned)B);
+  const float* nul = nullptr;
+  if (C % 8 == 0)
+    hipLaunchKernelGGL((conv0_apply_kernel<false, true>), grid, dim3(256), 0, stream, wave, w, bias, p, nul, nul, nul,
+                       nul, nul, reinterpret_cast<bf16_t*>(y));
+  else
+    hipLaunchKernelGGL((conv0_apply_kernel<false, false>), grid, dim3(256), 0, stream, wave, w, bias, p, nul, nul, nul,
+                       nul, nul, reinterpret_cast<bf16_t*>(y));
   return check_launch("dph_conv0_fwd");
 }
 
@@ -766,15 +780,19 @@ extern "C" int dph_conv0_gn_bwd(const float* wave, int64_t B, int64_t S, const f
   const int rows = var == 3 ? BWD_ROWS / 2 : BWD_ROWS;
   dim3 grid((unsigned)cdiv(p.L0, rows), (unsigned)B);
   const bf16_t* dyb = reinterpret_cast<const bf16_t*>(dy);
+  const bool vec = C % 4 == 0;
   if (var == 1 && C <= 512)
-    hipLaunchKernelGGL((conv0_gn_bwd_kernel<2, 4>), grid, dim3(256), 0, stream, wave, w, p, gamma, beta, mask, mean,
+    hipLaunchKernelGGL((conv0_gn_bwd_kernel<2, 4, false>), grid, dim3(256), 0, stream, wave, w, p, gamma, beta, mask, mean,
                        rstd, dyb, sums, rows);
   else if (var == 2)
-    hipLaunchKernelGGL((conv0_gn_bwd_kernel<4, 1>), grid, dim3(256), 0, stream, wave, w, p, gamma, beta, mask, mean,
+    hipLaunchKernelGGL((conv0_gn_bwd_kernel<4, 1, false>), grid, dim3(256), 0, stream, wave, w, p, gamma, beta, mask, mean,
                        rstd, dyb, sums, rows);
+  else if (vec)
+    hipLaunchKernelGGL((conv0_gn_bwd_kernel<4, 4, true>), grid, dim3(256), 0, stream, wave, w, p, gamma, beta, mask,
+                       mean, rstd, dyb, sums, rows);
   else
-    hipLaunchKernelGGL((conv0_gn_bwd_kernel<4, 4>), grid, dim3(256), 0, stream, wave, w, p, gamma, beta, mask, mean,
-                       rstd, dyb, sums, rows);
+    hipLaunchKernelGGL((conv0_gn_bwd_kernel<4, 4, false>), grid, dim3(256), 0, stream, wave, w, p, gamma, beta, mask,
+                       mean, rstd, dyb, sums, rows);
   hipLaunchKernelGGL(conv0_bwd_finalize, dim3((unsigned)cdiv(C, 64)), dim3(64), 0, stream, sums, gram, w, mean, rstd,
                      p, dw, dgamma, dbeta, dmask);
   return check_launch("dph_conv0_gn_bwd");

@@ -476,7 +476,7 @@ def _conv0_gn(wave, w, C, gamma, beta, mask, dy=None):
     return y, dw, dg, db, dm
 
 
-@pytest.mark.parametrize("B,S,C", [(3, 16000, 512), (2, 5003, 200), (1, 47, 36)])
+@pytest.mark.parametrize("B,S,C", [(3, 16000, 512), (2, 5003, 200), (1, 47, 36), (2, 2003, 30)])
 def test_conv0_gn_bwd_fp32_reference(B, S, C):
     """Single-pass conv0/GroupNorm backward (per-(b,c) sums + waveform Gram matrix) against fp32 torch
     autograd of conv1d -> group_norm -> gelu -> *mask (components.py:81-87,107-114); the kernel's only
