@@ -2499,7 +2499,7 @@ __global__ void __launch_bounds__(C::NT, C::WPE) ppw_gemm_kernel(const DphGemmAr
 }  // namespace ppw
 
 // out[c] += sum_r slab[r][c] (out) and aux[c] += sum_r slab[nrows + r][c]: 64 columns x 4 row phases per block
-// over one of gridDim.y (<= 8) row groups, one atomic per column per group
+// over one of gridDim.y (<= 32) row groups, one atomic per column per group
 __global__ void __launch_bounds__(256) colsum_slab_reduce_kernel(const float* __restrict__ slab, int64_t nrows,
                                                                  int64_t ncols, int64_t csn, float* __restrict__ out,
                                                                  float* __restrict__ aux) {
@@ -2512,10 +2512,25 @@ __global__ void __launch_bounds__(256) colsum_slab_reduce_kernel(const float* __
   const int64_t rb = min(nrows, ra + per);
   float so = 0.f, sa = 0.f;
   if (col < csn) {
-    for (int64_t r = ra + ty; r < rb; r += 4) {
+    // four rows' loads in flight per thread (independent partial sums)
+    float so1 = 0.f, sa1 = 0.f, so2 = 0.f, sa2 = 0.f, so3 = 0.f, sa3 = 0.f;
+    int64_t r = ra + ty;
+    for (; r + 12 < rb; r += 16) {
+      so += slab[r * ncols + col];
+      sa += slab[(nrows + r) * ncols + col];
+      so1 += slab[(r + 4) * ncols + col];
+      sa1 += slab[(nrows + r + 4) * ncols + col];
+      so2 += slab[(r + 8) * ncols + col];
+      sa2 += slab[(nrows + r + 8) * ncols + col];
+      so3 += slab[(r + 12) * ncols + col];
+      sa3 += slab[(nrows + r + 12) * ncols + col];
+    }
+    for (; r < rb; r += 4) {
       so += slab[r * ncols + col];
       sa += slab[(nrows + r) * ncols + col];
     }
+    so += (so1 + so2) + so3;
+    sa += (sa1 + sa2) + sa3;
   }
   red[0][ty][tx] = so;
   red[1][ty][tx] = sa;
@@ -3024,7 +3039,8 @@ extern "C" int dph_gemm(const DphGemmArgs* args, hipStream_t stream) {
       int rc = check_launch("dph_gemm");
       if (rc) return rc;
       const int64_t csn = std::min<int64_t>(a.colsum_n > 0 ? a.colsum_n : a.N, a.N);
-      const unsigned groups = (unsigned)std::max<int64_t>(1, std::min<int64_t>(8, cdiv(nslots, 64)));
+      // (>= 16 slab rows per group: a few hundred blocks even at N = 768, each thread's rows in flight together)
+      const unsigned groups = (unsigned)std::max<int64_t>(1, std::min<int64_t>(32, cdiv(nslots, 16)));
       hipLaunchKernelGGL(colsum_slab_reduce_kernel, dim3((unsigned)cdiv(csn, 64), groups), dim3(256), 0, stream,
                          reinterpret_cast<const float*>(a.workspace), nslots, a.N, csn, a.colsum_out, a.colsum_aux);
       return check_launch("dph_gemm colsum reduce");

@@ -378,20 +378,24 @@ __global__ void __launch_bounds__(256) slab_reduce_kernel(const float* __restric
   float s = 0.f;
   if (col < ncols && out) {
     int64_t r = ra + ty;
-    float s1 = 0.f;
-    for (; r + 4 < rb; r += 8) {
+    float s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    for (; r + 12 < rb; r += 16) {
       s += ws[r * ncols + col];
       s1 += ws[(r + 4) * ncols + col];
+      s2 += ws[(r + 8) * ncols + col];
+      s3 += ws[(r + 12) * ncols + col];
     }
-    if (r < rb) s += ws[r * ncols + col];
-    s += s1;
+    for (; r < rb; r += 4) s += ws[r * ncols + col];
+    s += (s1 + s2) + s3;
   }
   red[ty][tx] = s;
   __syncthreads();
   if (ty == 0 && col < ncols && out) atomicAdd(out + (col - (int64_t)q * seg), red[0][tx] + red[1][tx] + red[2][tx] + red[3][tx]);
 }
 
-int64_t slab_groups(int64_t nrows) { return std::max<int64_t>(1, std::min<int64_t>(8, cdiv(nrows, 64))); }
+// row groups of a slab reduction: >= 32 rows (8 per thread phase) per group, up to 32 groups (one atomic per column
+// per group)
+int64_t slab_groups(int64_t nrows) { return std::max<int64_t>(1, std::min<int64_t>(32, cdiv(nrows, 32))); }
 
 int64_t colsum_rpb(int64_t rows) { return std::max<int64_t>(64, cdiv(cdiv(rows, 8192), 4) * 4); }
 
