@@ -37,6 +37,14 @@ class DphGemmArgs(C.Structure):
                 ("workspace", vp), ("workspace_bytes", i64), ("colsum_n", i64), ("flags", i64), ("dyn_ext", vp)]
 
 
+GEMM_GROUP_MAX = 16
+
+
+class DphGemmGroup(C.Structure):
+    _fields_ = [("n", i32), ("reserved", i32), ("a", vp * GEMM_GROUP_MAX), ("b", vp * GEMM_GROUP_MAX),
+                ("c", vp * GEMM_GROUP_MAX)]
+
+
 class DphTensorSlot(C.Structure):
     _fields_ = [("param", vp), ("grad", vp), ("exp_avg", vp), ("exp_avg_sq", vp), ("n", i64), ("group", i32),
                 ("pad_", i32)]
@@ -61,6 +69,7 @@ _SIGS = {
     "dph_abi_version": ([], C.c_int),
     "dph_gemm": ([C.POINTER(DphGemmArgs), S], C.c_int),
     "dph_gemm_mn_plan": ([i64, i64, i64, i64], C.c_int),
+    "dph_gemm_grouped": ([C.POINTER(DphGemmArgs), C.POINTER(DphGemmGroup), S], C.c_int),
     "dph_ffn_compact": ([vp, i64, i64, vp, vp, S], C.c_int),
     "dph_ffn_pack": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, i64, S], C.c_int),
     "dph_ffn_unpack_grads": ([vp, vp, vp, vp, vp, vp, i64, vp, vp, vp, i64, i64, S], C.c_int),
@@ -139,7 +148,7 @@ _SIGS = {
 _lib = None
 # include/dphubert_hip.h layout (3: dph_adamw_step_dev, dph_set_rng_epoch; 4: dph_event_*; 5: LN bwd / colsum
 # workspaces; 12: dph_hc_bank_fwd / dph_hc_bank_bwd; 15: dph_gemm_mn_plan; 16: DphGemmArgs.dyn_ext, dph_ffn_compact + gathers / scatters)
-ABI_VERSION = 16
+ABI_VERSION = 17
 
 
 class DphError(RuntimeError):

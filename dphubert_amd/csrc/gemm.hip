@@ -2200,7 +2200,8 @@ __device__ __forceinline__ bf16x8_t kmask(bf16x8_t f, int n) {
 }
 
 template <class C, bool BB>
-__global__ void __launch_bounds__(C::NT, C::WPE) ppw_gemm_kernel(const DphGemmArgs a, int64_t kchunk) {
+__global__ void __launch_bounds__(C::NT, C::WPE) ppw_gemm_kernel(const DphGemmArgs a, int64_t kchunk,
+                                                                 const DphGemmGroup grp) {
   __shared__ __attribute__((aligned(1024))) char smem[C::LDS];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -2233,8 +2234,9 @@ __global__ void __launch_bounds__(C::NT, C::WPE) ppw_gemm_kernel(const DphGemmAr
   const int32_t kbeg = (int32_t)(split * kchunk);
   const int32_t kend = (int32_t)min<int64_t>(a.K, kbeg + kchunk);
   const int nk = (kend - kbeg + BK - 1) / BK;
-  const bf16_t* Ab = reinterpret_cast<const bf16_t*>(a.A.ptr) + z_addr(a.A, z);
-  const bf16_t* Bb = reinterpret_cast<const bf16_t*>(a.B.ptr) + z_addr(a.B, z);
+  // (grouped launch: problem z's operands; the host zeroed their z offsets)
+  const bf16_t* Ab = reinterpret_cast<const bf16_t*>(grp.n ? grp.a[z] : a.A.ptr) + z_addr(a.A, z);
+  const bf16_t* Bb = reinterpret_cast<const bf16_t*>(grp.n ? grp.b[z] : a.B.ptr) + z_addr(a.B, z);
   const uint32_t rsa = (uint32_t)a.A.row_stride, rsb = (uint32_t)a.B.row_stride;
   // DMA of a [64][R] half-tile: wave instruction gi = jj * 8 + wave fills k-rows gi * (512 / R) ..; lane ->
   // k-row gi * (512 / R) + lane / (R / 8), physical chunk lane % (R / 8) <- logical chunk pc ^ fsw(k-row),
@@ -2494,7 +2496,13 @@ __global__ void __launch_bounds__(C::NT, C::WPE) ppw_gemm_kernel(const DphGemmAr
     bar();
   }
   if (wr == 0) bar();
-  ring::direct_epi_t<C, DPH_ACT_NONE, false>(a, zz, m0 + wr * C::WTM, n0 + wc * C::WTN, lane, acc);
+  if (grp.n && a.splits == 1) {
+    DphGemmArgs e = a;
+    e.C.ptr = grp.c[z];
+    ring::direct_epi_t<C, DPH_ACT_NONE, false>(e, zz, m0 + wr * C::WTM, n0 + wc * C::WTN, lane, acc);
+  } else {
+    ring::direct_epi_t<C, DPH_ACT_NONE, false>(a, zz, m0 + wr * C::WTM, n0 + wc * C::WTN, lane, acc);
+  }
 }
 }  // namespace ppw
 
@@ -2542,7 +2550,9 @@ __global__ void __launch_bounds__(256) colsum_slab_reduce_kernel(const float* __
 }
 
 // split-K reduction + epilogue: one thread per 8 columns of a row
-__global__ void splitk_reduce_kernel(const DphGemmArgs a) {
+__global__ void splitk_reduce_kernel(const DphGemmArgs a0, const DphGemmGroup grp) {
+  DphGemmArgs a = a0;
+  if (grp.n) a.C.ptr = grp.c[blockIdx.z];   // grouped launch: problem z's output (its z offset is 0)
   const int64_t z = blockIdx.z;
   const int64_t n8 = (a.N + 7) / 8;
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2758,10 +2768,25 @@ extern "C" int dph_gemm_mn_plan(int64_t M, int64_t N, int64_t K, int64_t batch) 
 }
 
 template <class Cf>
-static void launch_ppw(const DphGemmArgs& e, int64_t kchunk, hipStream_t stream) {
+static void launch_ppw(const DphGemmArgs& e, int64_t kchunk, const DphGemmGroup& grp, hipStream_t stream) {
   const dim3 g((unsigned)cdiv(e.N, Cf::BN), (unsigned)cdiv(e.M, Cf::BM), (unsigned)(e.batch * e.splits)), b(Cf::NT);
-  if (e.B.rows_per_batch > 0) hipLaunchKernelGGL((ppw::ppw_gemm_kernel<Cf, true>), g, b, 0, stream, e, kchunk);
-  else hipLaunchKernelGGL((ppw::ppw_gemm_kernel<Cf, false>), g, b, 0, stream, e, kchunk);
+  if (e.B.rows_per_batch > 0) hipLaunchKernelGGL((ppw::ppw_gemm_kernel<Cf, true>), g, b, 0, stream, e, kchunk, grp);
+  else hipLaunchKernelGGL((ppw::ppw_gemm_kernel<Cf, false>), g, b, 0, stream, e, kchunk, grp);
+}
+
+// the ppw plan's launch (+ split-K reduce) for args ppw_route accepted
+static int run_ppw(const DphGemmArgs& a, const PpwPlan& pw, const DphGemmGroup& grp, hipStream_t stream) {
+  const DphGemmArgs e = ppw_epi_args(a);
+  if (pw.kind == 12) launch_ppw<pp::P256>(e, pw.kchunk, grp, stream);
+  else if (pw.kind == 13) launch_ppw<pp::P128x256>(e, pw.kchunk, grp, stream);
+  else if (pw.kind == 15) launch_ppw<pp::P128x192>(e, pw.kchunk, grp, stream);
+  else launch_ppw<pp::P128>(e, pw.kchunk, grp, stream);
+  int rc = check_launch("dph_gemm (ppw)");
+  if (rc || a.splits == 1) return rc;
+  const int64_t work = a.M * cdiv(a.N, (int64_t)8);
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)cdiv(work, (int64_t)256), 1, (unsigned)a.batch), dim3(256), 0,
+                     stream, a, grp);
+  return check_launch("dph_gemm (ppw) splitk_reduce");
 }
 
 // only where both tilings are a single round over the CUs (one block per CU) and the 192 x 128 one has
@@ -2982,19 +3007,7 @@ extern "C" int dph_gemm(const DphGemmArgs* args, hipStream_t stream) {
   // with dph_gemm_mn_plan's splits; any other split count keeps the register-staged kernel)
   {
     const PpwPlan pw = ppw_route(a);
-    if (pw.kind) {
-      const DphGemmArgs e = ppw_epi_args(a);
-      if (pw.kind == 12) launch_ppw<pp::P256>(e, pw.kchunk, stream);
-      else if (pw.kind == 13) launch_ppw<pp::P128x256>(e, pw.kchunk, stream);
-      else if (pw.kind == 15) launch_ppw<pp::P128x192>(e, pw.kchunk, stream);
-      else launch_ppw<pp::P128>(e, pw.kchunk, stream);
-      int rc = check_launch("dph_gemm (ppw)");
-      if (rc || a.splits == 1) return rc;
-      const int64_t work = a.M * cdiv(a.N, (int64_t)8);
-      hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)cdiv(work, (int64_t)256), 1, (unsigned)a.batch), dim3(256), 0,
-                         stream, a);
-      return check_launch("dph_gemm (ppw) splitk_reduce");
-    }
+    if (pw.kind) return run_ppw(a, pw, DphGemmGroup{}, stream);
   }
   // LDS-DMA ring kernels for k-contiguous A and B with whole 32-deep k-slices: the 256x256 tile
   // when there are >= ~2 full rounds of tiles over the 256 CUs at one block per CU, else the
@@ -3114,8 +3127,49 @@ extern "C" int dph_gemm(const DphGemmArgs* args, hipStream_t stream) {
   if (a.splits > 1) {
     const int64_t work = a.M * cdiv(a.N, 8);
     dim3 g2((unsigned)cdiv(work, 256), 1, (unsigned)a.batch);
-    hipLaunchKernelGGL(splitk_reduce_kernel, g2, dim3(256), 0, stream, a);
+    hipLaunchKernelGGL(splitk_reduce_kernel, g2, dim3(256), 0, stream, a, DphGemmGroup{});
     rc = check_launch("dph_gemm splitk_reduce");
   }
   return rc;
+}
+
+extern "C" int dph_gemm_grouped(const DphGemmArgs* args, const DphGemmGroup* group, hipStream_t stream) {
+  DPH_REQUIRE(args != nullptr && group != nullptr, "dph_gemm_grouped: null args");
+  const DphGemmGroup& g = *group;
+  DPH_REQUIRE(g.n >= 1 && g.n <= DPH_GEMM_GROUP_MAX, "dph_gemm_grouped: group size %d outside 1..%d", g.n,
+              DPH_GEMM_GROUP_MAX);
+  DphGemmArgs a = *args;
+  DPH_REQUIRE(a.M > 0 && a.N > 0 && a.K > 0 && a.splits >= 1, "dph_gemm_grouped: bad sizes");
+  DPH_REQUIRE(a.batch == g.n, "dph_gemm_grouped: batch (%d) must equal the group size (%d)", a.batch, g.n);
+  DPH_REQUIRE(!a.a_kcontig && !a.b_kcontig, "dph_gemm_grouped: (mn, mn) operands only");
+  uintptr_t al = 0;
+  for (int i = 0; i < g.n; ++i) {
+    DPH_REQUIRE(g.a[i] && g.b[i] && g.c[i], "dph_gemm_grouped: null operand of problem %d", i);
+    al |= reinterpret_cast<uintptr_t>(g.a[i]) | reinterpret_cast<uintptr_t>(g.b[i]) |
+          (a.splits == 1 ? reinterpret_cast<uintptr_t>(g.c[i]) : 0);
+  }
+  if ((al & 15) != 0) {
+    set_error("dph_gemm_grouped: operands not 16-byte aligned");
+    return DPH_EUNSUPPORTED;
+  }
+  for (DphMat* d : {&a.A, &a.B, &a.C}) {
+    d->batch_stride = 0;
+    d->z_div = 0;
+    d->z_outer = 0;
+    d->z_inner = 0;
+  }
+  a.A.ptr = const_cast<void*>(g.a[0]);
+  a.B.ptr = const_cast<void*>(g.b[0]);
+  a.C.ptr = g.c[0];
+  if (a.splits > 1) {
+    const int64_t need = (int64_t)a.batch * a.splits * a.M * a.N * 4;
+    DPH_REQUIRE(a.workspace && a.workspace_bytes >= need, "dph_gemm_grouped: split-K workspace too small (%lld < %lld)",
+                (long long)a.workspace_bytes, (long long)need);
+  }
+  const PpwPlan pw = ppw_route(a);
+  if (!pw.kind || pw.splits != a.splits) {
+    set_error("dph_gemm_grouped: no ping-pong weight-gradient plan for these args");
+    return DPH_EUNSUPPORTED;
+  }
+  return run_ppw(a, pw, g, stream);
 }

@@ -68,14 +68,21 @@ class GradReducer:
         self.params = [p for u in units for p in u]
         cap = int(bucket_mb * 1024 * 1024 / 4)
         self.buckets: List[List[torch.nn.Parameter]] = []
+        # each unit starts on a 16-byte boundary of its bucket (the weight-gradient kernels store whole 16-byte
+        # vectors straight into the bucket; a scalar layer-mask parameter would otherwise shift every later view)
+        pad = lambda n: (n + 3) & ~3  # noqa: E731
+        offsets = {}
         cur, n = [], 0
         for u in units:
             un = sum(p.numel() for p in u)
             if cur and n + un > cap:
                 self.buckets.append(cur)
                 cur, n = [], 0
+            for p in u:
+                offsets[id(p)] = n
+                n += p.numel()
+            n = pad(n)
             cur.extend(u)
-            n += un
         if cur:
             self.buckets.append(cur)
         self.flat = []
@@ -83,17 +90,17 @@ class GradReducer:
         for bi, b in enumerate(self.buckets):
             dev = b[0].device
             dt = b[0].dtype
-            self.flat.append(torch.zeros(sum(p.numel() for p in b), dtype=dt, device=dev))
+            size = pad(max(offsets[id(p)] + p.numel() for p in b))
+            self.flat.append(torch.zeros(size, dtype=dt, device=dev))
             for p in b:
                 self.bucket_of[id(p)] = bi
         self.views = {}
         self.offsets = {}
         for bi, b in enumerate(self.buckets):
-            off = 0
             for p in b:
+                off = offsets[id(p)]
                 self.views[id(p)] = self.flat[bi][off:off + p.numel()].view_as(p)
                 self.offsets[id(p)] = off
-                off += p.numel()
         self.direct = direct
         self._pending = [0] * len(self.buckets)
         self._handles = [None] * len(self.buckets)
@@ -157,7 +164,9 @@ class GradReducer:
         self._ready(p)
 
     def _ready(self, p):
-        if not self.sync or id(p) in self._seen:
+        # (_dph_hold: the parameter's gradient GEMM is queued in an ops.grouped_wgrads block, which notifies again
+        # once it has landed)
+        if not self.sync or id(p) in self._seen or getattr(p, "_dph_hold", False):
             return
         self._seen.add(id(p))
         bi = self.bucket_of[id(p)]

@@ -79,6 +79,7 @@ class LaunchProfiler:
 
     def __init__(self, by_shape: bool = False):
         self.records = []
+        self.keep = []             # events recorded into a graph without a record (kept alive with the graph)
         self.by_shape = by_shape   # key the summary by (kernel, M, N, K, batch, splits) -- diagnostics
 
     def __enter__(self):
@@ -241,4 +242,64 @@ def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, accumulate
     splits = choose_splits(Nw, Kw, M)
     ws = gemm(dense(dy), dense(x), mat(dw, Kw), Nw, Kw, M, a_kcontig=False, b_kcontig=False,
               c_dtype=OUT_F32_ACCUM if accumulate else OUT_F32, splits=splits, device=dy.device, dyn=dyn)
+    return ws
+
+
+EUNSUPPORTED = -3
+
+
+def linear_wgrad_grouped(items: Sequence, accumulate: bool = True) -> Optional[torch.Tensor]:
+    """dw_i (+)= dy_i^T @ x_i for up to 16 problems of ONE shape in one launch (dph_gemm_grouped): the weight
+    gradients of a group of encoder layers, whose blocks together fill the CUs that one layer's GEMM leaves idle
+    without split-K.  ``items``: (dy [M,N] bf16, x [M,K] bf16, dw [N,K] fp32) triples.  Falls back to one
+    linear_wgrad per problem where the grouped kernel does not apply (returns None then)."""
+    n = len(items)
+    if n == 0:
+        return None
+    dy0, x0, dw0 = items[0]
+    M, N = dy0.shape
+    K = x0.shape[1]
+    ok = n <= _lib.GEMM_GROUP_MAX and all(
+        tuple(dy.shape) == (M, N) and tuple(x.shape) == (M, K) and tuple(dw.shape) == (N, K) and
+        dy.dtype == BF16 and x.dtype == BF16 and dw.dtype == F32 and dy.is_contiguous() and x.is_contiguous() and
+        dw.stride() == (K, 1) for dy, x, dw in items)
+    if not ok:
+        for dy, x, dw in items:
+            linear_wgrad(dy, x, dw, accumulate=accumulate)
+        return None
+    splits = choose_splits(N, K, M, batch=n)
+    if splits == 1 and any(dw.data_ptr() % 16 for _, _, dw in items):
+        # (the grouped kernel stores whole 16-byte vectors into each output)
+        for dy, x, dw in items:
+            linear_wgrad(dy, x, dw, accumulate=accumulate)
+        return None
+    ws, ws_bytes = None, 0
+    if splits > 1:
+        ws = torch.empty(n * splits * N * K, dtype=F32, device=dy0.device)
+        ws_bytes = ws.numel() * 4
+    args = DphGemmArgs(N, K, M, n, splits, 0, 0, dense(dy0), dense(x0), mat(dw0, K),
+                       OUT_F32_ACCUM if accumulate else OUT_F32, ACT_NONE, 1.0, 0.0, 0, None, None, None, 0, None,
+                       None, None, None, None, None, 0, 0, ptr(ws), ws_bytes, 0, 0, None)
+    grp = _lib.DphGemmGroup()
+    grp.n = n
+    for i, (dy, x, dw) in enumerate(items):
+        grp.a[i], grp.b[i], grp.c[i] = dy.data_ptr(), x.data_ptr(), dw.data_ptr()
+    prof = LaunchProfiler.active
+    if prof is not None:
+        e0, e1 = _Event(), _Event()
+        e0.record()
+    rc = _lib.lib().dph_gemm_grouped(C.byref(args), C.byref(grp), _stream())
+    if rc == EUNSUPPORTED:
+        if prof is not None:
+            prof.keep.append(e0)   # (a captured event-record node refers to it)
+        for dy, x, dw in items:
+            linear_wgrad(dy, x, dw, accumulate=accumulate)
+        return None
+    _lib.check(rc, "dph_gemm_grouped")
+    if prof is not None:
+        e1.record()
+        name = _variant(args)
+        if prof.by_shape:
+            name = f"{name} grouped M={N} N={K} K={M} b={n} s={splits}"
+        prof.records.append((name, 2.0 * M * N * K * n, e0, e1))
     return ws

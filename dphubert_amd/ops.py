@@ -429,6 +429,80 @@ class wgrad_side:
 
 
 # ---------------------------------------------------------------------------
+# grouped encoder-layer weight gradients (Trainer: wgrad_group)
+# ---------------------------------------------------------------------------
+# One layer's weight-gradient GEMMs (dW = dY^T X, K = the B*T frames) have few output tiles (768 x 768: 18 tiles of
+# 128 x 256), so each needs split-K slices, their fp32 slab and a reduce launch to fill 256 CUs.  Inside a
+# grouped_wgrads block the bucket-sink ones are queued per shape and launched ``group`` layers at a time as ONE
+# grouped GEMM (dph_gemm_grouped: problem z = layer), which fills the CUs with whole-K blocks.  The queued
+# gradients' parameters are held back from the reducer (p._dph_hold) until their group lands, so a bucket's
+# collective still starts only after all its gradients are written; the queue keeps dY / X alive until then.
+_WGRAD_DEFER = [None]
+
+
+class grouped_wgrads:
+    """Queue the encoder layers' bucket-sink weight-gradient GEMMs of one backward and launch them ``group``
+    layers at a time (exit flushes the rest).  ``group`` <= 1: no-op."""
+
+    def __init__(self, group: int = 6):
+        self.group = min(int(group), _lib.GEMM_GROUP_MAX)
+        self.queues = {}
+
+    def __enter__(self):
+        if self.group > 1:
+            self.prev, _WGRAD_DEFER[0] = _WGRAD_DEFER[0], self
+        return self
+
+    def __exit__(self, exc_type, *exc):
+        if self.group > 1:
+            _WGRAD_DEFER[0] = self.prev
+            if exc_type is None:
+                self.flush()
+            else:
+                for items in self.queues.values():
+                    for *_, params in items:
+                        for p in params:
+                            p._dph_hold = False
+                self.queues = {}
+
+    def add(self, dy, x, dw, params):
+        key = (tuple(dy.shape), tuple(x.shape), dy.device)
+        items = self.queues.setdefault(key, [])
+        for p in params:
+            p._dph_hold = True
+        items.append((dy, x, dw, params))
+        if len(items) >= self.group:
+            self._flush(key)
+
+    def _flush(self, key):
+        items = self.queues.pop(key)
+        ws = K.linear_wgrad_grouped([(dy, x, dw) for dy, x, dw, _ in items], accumulate=True)
+        del ws
+        for *_, params in items:
+            for p in params:
+                p._dph_hold = False
+                p._dph_sink_ready(p)
+
+    def flush(self):
+        for key in list(self.queues):
+            self._flush(key)
+
+
+def _layer_wgrad(dy, x, dw, direct, params, **kw):
+    """An encoder layer's weight gradient: queued in the active grouped_wgrads block when it goes straight
+    into the bucket (``direct``) at the operands' full width, else launched now (on the wgrad side stream
+    when one is active)."""
+    q = _WGRAD_DEFER[0]
+    full = tuple(dw.shape) == (dy.shape[1], x.shape[1]) and kw.get("n_out", 0) in (0, dy.shape[1]) and \
+        kw.get("k_in", 0) in (0, x.shape[1])
+    if q is not None and direct and full:
+        q.add(dy, x, dw, params)
+        return None
+    with wgrad_side(dy, x, enable=direct):
+        return K.linear_wgrad(dy, x, dw, accumulate=direct, **kw)
+
+
+# ---------------------------------------------------------------------------
 # gradient sinks: weight gradients written straight into the data-parallel buckets
 # ---------------------------------------------------------------------------
 def _sink_view(params) -> Optional[torch.Tensor]:
@@ -1434,13 +1508,11 @@ def _ffn_backward(cfg, sv, dy, xin, pr, go, dmask, residual=None):
         del k1, k2
         return dx
     dw2, direct = go.buf(pr["w2"], zero=False)
-    with wgrad_side(dy, sv["f"], enable=direct):
-        k1 = K.linear_wgrad(dy, sv["f"], dw2, accumulate=direct, k_in=F_)
+    k1 = _layer_wgrad(dy, sv["f"], dw2, direct, (pr["w2"],), k_in=F_)
     db1, _ = go.buf(pr["b1"])
     du = _ffn_interm_bwd(dy, sv, db1, dmask, cfg, F_)
     dw1, direct = go.buf(pr["w1"], zero=False)
-    with wgrad_side(du, xin, enable=direct):
-        k2 = K.linear_wgrad(du, xin, dw1, accumulate=direct, n_out=F_)
+    k2 = _layer_wgrad(du, xin, dw1, direct, (pr["w1"],), n_out=F_)
     dx = K.linear_dgrad(du, sv["W1"], w_t=t_image(sv["W1"]), residual=residual)
     del k1, k2
     return dx
@@ -1607,8 +1679,7 @@ class EncoderLayerFn(torch.autograd.Function):
             call("dph_branch_bwd", ptr(ds1), ptr(da), M, D, cfg["p_drop"], sv["seed_d"], ptr(lma), None, 0, ptr(dbo),
                  ptr(sv["a_pre"]) if has_lma else None, ptr(g["lma"]), _s())
             dwo, direct = go.buf(pr["wo"], zero=False)
-            with wgrad_side(da, sv["o_m"], enable=direct):
-                k3 = K.linear_wgrad(da, sv["o_m"], dwo, accumulate=direct)
+            k3 = _layer_wgrad(da, sv["o_m"], dwo, direct, (pr["wo"],))
             do_m = K.linear_dgrad(da, sv["Wo"], w_t=t_image(sv["Wo"]))
             Dvec = torch.empty(B * H * T, dtype=F32, device=dev)
             g["hm"] = z(H) if has_hm else None
@@ -1618,8 +1689,7 @@ class EncoderLayerFn(torch.autograd.Function):
             dbqkv, _ = go.buf(pr["bq"], pr["bk"], pr["bv"])
             _qkv_bias_grad(dqkv, dbqkv, M, dev)
             dwqkv, direct = go.buf(pr["wq"], pr["wk"], pr["wv"], zero=False)
-            with wgrad_side(dqkv, xn1, enable=direct):
-                k4 = K.linear_wgrad(dqkv, xn1, dwqkv, accumulate=direct)
+            k4 = _layer_wgrad(dqkv, xn1, dwqkv, direct, (pr["wq"], pr["wk"], pr["wv"]))
             dxn1 = K.linear_dgrad(dqkv, sv["Wqkv"], w_t=t_image(sv["Wqkv"]))
             EncoderLayerFn._gate_bwd(ctx, cfg, xn1, dxn1, wl_g, go)
             dh = torch.empty_like(dout)
@@ -1754,8 +1824,7 @@ class EncoderLayerFn(torch.autograd.Function):
                  ptr(dln1w), ptr(dln1b), M, D, 0.0, 0, ptr(da), cfg["p_drop"], sv["seed_d"], ptr(lma), ptr(dbo),
                  ptr(sv["a_pre"]), ptr(g["lma"]), *ln_ws(M, D, dev), _s())
             dwo, direct = go.buf(pr["wo"], zero=False)
-            with wgrad_side(da, sv["o_m"], enable=direct):
-                k3 = K.linear_wgrad(da, sv["o_m"], dwo, accumulate=direct)
+            k3 = _layer_wgrad(da, sv["o_m"], dwo, direct, (pr["wo"],))
             do_m = K.linear_dgrad(da, sv["Wo"], w_t=t_image(sv["Wo"]))
             Dvec = torch.empty(B * H * T, dtype=F32, device=dev)
             g["hm"] = z(H) if has_hm else None
@@ -1765,8 +1834,7 @@ class EncoderLayerFn(torch.autograd.Function):
             dbqkv, _ = go.buf(pr["bq"], pr["bk"], pr["bv"])
             _qkv_bias_grad(dqkv, dbqkv, M, dev)
             dwqkv, direct = go.buf(pr["wq"], pr["wk"], pr["wv"], zero=False)
-            with wgrad_side(dqkv, h, enable=direct):
-                k4 = K.linear_wgrad(dqkv, h, dwqkv, accumulate=direct)
+            k4 = _layer_wgrad(dqkv, h, dwqkv, direct, (pr["wq"], pr["wk"], pr["wv"]))
             dh = K.linear_dgrad(dqkv, sv["Wqkv"], w_t=t_image(sv["Wqkv"]), residual=ds1)
             EncoderLayerFn._gate_bwd(ctx, cfg, h, dh, wl_g, go)
             del k3, k4

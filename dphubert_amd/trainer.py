@@ -164,6 +164,9 @@ class Trainer:
         if os.environ.get("DPH_WGRAD_STREAM", "0") == "1" and torch.cuda.is_available() and \
                 next(module.parameters()).is_cuda:
             self._wgrad_stream = torch.cuda.Stream()
+        # encoder-layer weight gradients launched this many layers at a time as one grouped GEMM
+        # (ops.grouped_wgrads; DPH_WGRAD_GROUP=1 keeps one launch per layer)
+        self.wgrad_group = int(os.environ.get("DPH_WGRAD_GROUP", "6"))
 
     @property
     def _graph(self):
@@ -203,7 +206,7 @@ class Trainer:
             if torch.cuda.is_current_stream_capturing():
                 raise RuntimeError("Trainer: the backward seed must exist before a graph capture")
             seed = self._grad_seed = torch.full((), 1.0 / self.accum_grad, dtype=loss.dtype, device=loss.device)
-        with ops.wgrad_overlap(self._wgrad_stream):
+        with ops.wgrad_overlap(self._wgrad_stream), ops.grouped_wgrads(self.wgrad_group):
             loss.backward(seed)
         if final:
             self.reducer.finish()

@@ -113,6 +113,22 @@ typedef struct DphGemmArgs {
 #define DPH_GEMM_PRE_DGK 2
 
 int dph_gemm(const DphGemmArgs* args, hipStream_t stream);
+/* Grouped (mn, mn) weight gradients: n <= DPH_GEMM_GROUP_MAX independent dW_i (+)= dY_i^T X_i of ONE shape in one
+ * launch (grid batch z = problem i, operand i at a[i] / b[i] / c[i]).  ``args`` describes every problem: batch == n,
+ * splits = dph_gemm_mn_plan(M, N, K, n) with the workspace sized for n problems, A / B / C ptr ignored, their
+ * z offsets 0.  The per-layer weight-gradient GEMMs of the encoder layers (components.py:406-408, :430, :733,
+ * :741), deferred over a group of layers: the group fills the CUs without (or with fewer) split-K slices.
+ * DPH_EUNSUPPORTED when the layout / alignment is outside the ping-pong weight-gradient kernel (the caller then
+ * runs the problems one dph_gemm at a time). */
+#define DPH_GEMM_GROUP_MAX 16
+typedef struct DphGemmGroup {
+  int32_t n;
+  int32_t reserved;
+  const void* a[DPH_GEMM_GROUP_MAX];
+  const void* b[DPH_GEMM_GROUP_MAX];
+  void* c[DPH_GEMM_GROUP_MAX];
+} DphGemmGroup;
+int dph_gemm_grouped(const DphGemmArgs* args, const DphGemmGroup* group, hipStream_t stream);
 /* name (as it appears in rocprof kernel names) of the kernel dph_gemm launches for these args */
 const char* dph_gemm_variant(const DphGemmArgs* args);
 /* split-K factor of the ping-pong weight-gradient plan for an (mn, mn) GEMM of this shape (A = [K][M], B = [K][N]:

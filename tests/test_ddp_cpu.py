@@ -160,3 +160,17 @@ def test_grad_out_fallback_without_reducer():
     ref(x).backward()
     for (n, p), (_, r) in zip(net.named_parameters(), ref.named_parameters()):
         assert torch.allclose(p.grad, r.grad, rtol=1e-5, atol=1e-6), n
+
+
+def test_bucket_units_16_byte_aligned():
+    """Every parameter unit starts on a 16-byte boundary of its bucket (the weight-gradient kernels store whole
+    16-byte vectors into the bucket), also after odd-sized parameters (a scalar layer mask, a 3-wide bias); a
+    fused group (q / k / v) stays back to back."""
+    ps = [torch.nn.Parameter(torch.zeros(s)) for s in [(1,), (3,), (8, 4), (5,), (6, 2), (6, 2), (6, 2), (1,)]]
+    red = GradReducer(ps, bucket_mb=1e-4, groups=[tuple(ps[4:7])])
+    assert sum(f.numel() for f in red.flat) >= sum(p.numel() for p in ps)
+    for p in ps:
+        assert red.offsets[id(p)] % 4 == 0 or any(p is q for q in ps[5:7]), (p.shape, red.offsets[id(p)])
+    o = [red.offsets[id(p)] for p in ps[4:7]]
+    assert red.bucket_of[id(ps[4])] == red.bucket_of[id(ps[6])] and o[1] == o[0] + 12 and o[2] == o[1] + 12
+    red.remove()

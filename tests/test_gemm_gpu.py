@@ -146,6 +146,56 @@ def test_wgrad_ppw_plan(N, K, M, gemm_path):
     close(dw, ref, 1e-5)
 
 
+@pytest.mark.parametrize("n,N,K,M", [(6, 768, 768, 7984), (3, 2304, 768, 7984), (2, 768, 3072, 1000), (5, 200, 136, 1000),
+                                     (16, 128, 64, 300)])
+def test_wgrad_grouped(n, N, K, M, gemm_path):
+    """dph_gemm_grouped: n independent (mn, mn) weight gradients of one shape in one launch (the deferred encoder
+    layers' dW_i += dY_i^T X_i) against fp64 torch per problem; every output lands in its own buffer.  On the
+    forced non-ppw paths the wrapper falls back to one launch per problem (same results)."""
+    K_ = _k()
+    from dphubert_amd import _lib
+    items = [(rnd(M, N), rnd(M, K), torch.randn(N, K, device="cuda")) for _ in range(n)]
+    ref = [dy.double().t() @ x.double() + dw.double() for dy, x, dw in items]
+    if gemm_path == "ppw":
+        import ctypes as C
+        s = K_.choose_splits(N, K, M, batch=n)
+        ws = torch.empty(max(1, n * s * N * K), device="cuda")
+        dy0, x0, dw0 = items[0]
+        args = _lib.DphGemmArgs(N, K, M, n, s, 0, 0, K_.dense(dy0), K_.dense(x0), K_.dense(dw0), K_.OUT_F32_ACCUM, 0,
+                                1.0, 0.0, 0, None, None, None, 0, None, None, None, None, None, None, 0, 0,
+                                ws.data_ptr(), ws.numel() * 4, 0, 0, None)
+        grp = _lib.DphGemmGroup()
+        grp.n = n
+        for i, (dy, x, dw) in enumerate(items):
+            grp.a[i], grp.b[i], grp.c[i] = dy.data_ptr(), x.data_ptr(), dw.data_ptr()
+        assert "ppw_gemm_kernel" in K_._variant(args)
+        rc = _lib.lib().dph_gemm_grouped(C.byref(args), C.byref(grp), _lib.stream_ptr())
+        assert rc == 0, _lib.lib().dph_last_error()
+    else:
+        keep = K_.linear_wgrad_grouped([(dy, x, dw) for dy, x, dw in items], accumulate=True)
+        del keep
+    torch.cuda.synchronize()
+    for (_, _, dw), r in zip(items, ref):
+        close(dw, r, 1e-5)
+
+
+def test_wgrad_grouped_fallback_misaligned(gemm_path):
+    """A group whose fp32 outputs are not 16-byte aligned (a bucket view after an odd-sized parameter) falls back
+    to per-problem launches where the grouped kernel cannot store them directly; results are the same."""
+    K_ = _k()
+    if gemm_path != "ppw":
+        pytest.skip("ppw path only")
+    n, N, K, M = 4, 256, 192, 2000
+    flat = torch.randn(n * N * K + 1, device="cuda")
+    items = [(rnd(M, N), rnd(M, K), flat[1 + i * N * K:1 + (i + 1) * N * K].view(N, K)) for i in range(n)]
+    ref = [dy.double().t() @ x.double() + dw.double() for dy, x, dw in items]
+    keep = K_.linear_wgrad_grouped(items, accumulate=True)
+    torch.cuda.synchronize()
+    del keep
+    for (_, _, dw), r in zip(items, ref):
+        close(dw, r, 1e-5)
+
+
 def _wgrad_args(K_, dy, x, dw):
     from dphubert_amd._lib import DphGemmArgs
     M, N = dy.shape

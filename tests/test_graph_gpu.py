@@ -196,3 +196,30 @@ def test_graph_replay_with_rccl_allreduce(comm, accum):
     out = r.stdout + r.stderr
     assert r.returncode == 0, out[-3000:]
     assert "RCCL_GRAPH_OK" in out, out[-3000:]
+
+
+def test_grouped_wgrads_match_per_layer(monkeypatch):
+    """Encoder-layer weight gradients deferred and launched as grouped GEMMs (ops.grouped_wgrads: group 2 over the
+    2-layer model, so every layer kind lands in one dph_gemm_grouped launch) against one launch per layer: the
+    same gradient buckets up to fp32 summation order (the grouped plan needs fewer split-K slices)."""
+    from dphubert_amd import kernels as K
+    from dphubert_amd.trainer import Trainer
+    batch = _batch()
+    calls = []
+    orig = K.linear_wgrad_grouped
+
+    def spy(items, **kw):
+        calls.append(len(items))
+        return orig(items, **kw)
+
+    monkeypatch.setattr(K, "linear_wgrad_grouped", spy)
+    res = []
+    for g in (1, 2):
+        monkeypatch.setenv("DPH_WGRAD_GROUP", str(g))
+        tr = Trainer(_module(), clip_norm=10.0)
+        tr.step(batch)
+        torch.cuda.synchronize()
+        res.append(torch.cat([f.detach().float().cpu() for f in tr.reducer.flat]))
+        assert not any(getattr(p, "_dph_hold", False) for p in tr.reducer.params)
+    assert calls == [2, 2, 2, 2], calls     # FFN w2, FFN w1, out-proj, qkv: both layers each
+    assert rel_l2(res[1], res[0]) < 1e-4
