@@ -752,6 +752,10 @@ constexpr int ACT_GELU_DGKPRE = 16;
 // atomic per column per wave (126 -- 2000 adders per address on the FFN / conv input-gradient GEMMs: the
 // atomics, not the MFMAs or the GELU', set those launches' time)
 constexpr int64_t GEMM_COLSUM_SLAB = (int64_t)1 << 20;
+// internal flags bit set by dph_gemm / dph_gemm_grouped on ppw launches with gridDim.z > 1 (problems / split-K
+// slices): the XCD-aware tile order runs over the whole (z, tile) space, so each XCD takes a contiguous range
+// of one slice's / problem's tiles (their shared operand panels stay in that XCD's L2).  DPH_PPW_ZMAP=0: per-z order
+constexpr int64_t GEMM_PPW_ZMAP = (int64_t)1 << 21;
 namespace ring {
 constexpr int KS = 32;      // k per slice
 constexpr int NSLOT = 4;
@@ -2207,16 +2211,22 @@ __global__ void __launch_bounds__(C::NT, C::WPE) ppw_gemm_kernel(const DphGemmAr
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
-  const int64_t zz = blockIdx.z;
-  const int64_t z = zz / a.splits;
-  const int64_t split = zz - z * a.splits;
+  int64_t zz = blockIdx.z;
   int64_t m0, n0;
   {
     const uint32_t ntm = gridDim.y, ntn = gridDim.x, nt = ntm * ntn;
-    const uint32_t bid = blockIdx.y * ntn + blockIdx.x;
-    const uint32_t q = nt >> 3, r = nt & 7;
+    // blocks reach the XCDs round-robin in dispatch order (x fastest, then y, then z); logical tile t = the
+    // block's rank inside its XCD's contiguous share, over one z plane or (ZMAP) over all of them
+    const bool zmap = (a.flags & GEMM_PPW_ZMAP) != 0;
+    const uint32_t total = zmap ? nt * gridDim.z : nt;
+    const uint32_t bid = (zmap ? blockIdx.z * nt : 0u) + blockIdx.y * ntn + blockIdx.x;
+    const uint32_t q = total >> 3, r = total & 7;
     const uint32_t xcd = bid & 7, loc = bid >> 3;
-    const uint32_t t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+    uint32_t t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+    if (zmap) {
+      zz = t / nt;
+      t -= (uint32_t)zz * nt;
+    }
     constexpr uint32_t GM = C::BM > 128 ? 4 : 8;
     const uint32_t gsz = GM * ntn;
     const uint32_t grp = t / gsz;
@@ -2227,6 +2237,9 @@ __global__ void __launch_bounds__(C::NT, C::WPE) ppw_gemm_kernel(const DphGemmAr
     m0 = (int64_t)(gm0 + (l - lq * gh)) * C::BM;
     n0 = (int64_t)lq * C::BN;
   }
+  zz = __builtin_amdgcn_readfirstlane((int)zz);
+  const int64_t z = zz / a.splits;
+  const int64_t split = zz - z * a.splits;
   if (a.dyn_ext != nullptr) {   // device-side extents: blocks past m / n return at once (packed FFN units)
     const int em = __builtin_amdgcn_readfirstlane(a.dyn_ext[0]), en = __builtin_amdgcn_readfirstlane(a.dyn_ext[1]);
     if ((em > 0 && m0 >= em) || (en > 0 && n0 >= en)) return;
@@ -2741,8 +2754,16 @@ static bool ppw_ok(const DphGemmArgs& a) {
 }
 
 // epilogue args of a ppw launch: the real C (splits == 1) or the fp32 slab of the splits (z = batch * splits + split)
+static bool ppw_zmap_enabled() {
+  const char* e = getenv("DPH_PPW_ZMAP");
+  return !(e && e[0] == '0');
+}
+
 static DphGemmArgs ppw_epi_args(const DphGemmArgs& a) {
   DphGemmArgs e = a;
+  if ((int64_t)a.batch * a.splits > 1 && ppw_zmap_enabled() &&
+      cdiv(a.M, (int64_t)64) * cdiv(a.N, (int64_t)64) * a.batch * a.splits < ((int64_t)1 << 31))
+    e.flags |= GEMM_PPW_ZMAP;
   if (a.splits > 1) {
     e.C = DphMat{a.workspace, 0, 0, a.N, 0, 0, a.M * a.N};
     e.c_dtype = DPH_OUT_F32;
