@@ -42,6 +42,43 @@ class SinkLinear(torch.autograd.Function):
         return dy @ w, go.ret(w), go.ret(b)
 
 
+class DeferLinear(torch.autograd.Function):
+    """SinkLinear whose weight gradient goes through ops._layer_wgrad: queued inside an ops.grouped_wgrads block
+    (the encoder layers' path), its parameter held back from the reducer until the group lands."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x)
+        ctx.params = (w, b)
+        return x @ w.t() + b
+
+    @staticmethod
+    def backward(ctx, dy):
+        from dphubert_amd import ops
+        (x,) = ctx.saved_tensors
+        w, b = ctx.params
+        go = GradOut(x.device)
+        dw, direct = go.buf(w, zero=False)
+        if direct:
+            assert ops._layer_wgrad(dy.contiguous(), x, dw, direct, (w,)) is None   # queued, not run
+        else:
+            dw.copy_(dy.t() @ x)
+        db, _ = go.buf(b)
+        db.add_(dy.sum(0))
+        go.done()
+        return dy @ w, go.ret(w), go.ret(b)
+
+
+def _cpu_grouped(items, accumulate=True):
+    """CPU stand-in for kernels.linear_wgrad_grouped (the HIP launch) in the gloo tests."""
+    with torch.no_grad():     # (the HIP launch writes through pointers; the exit flush runs outside the backward)
+        for dy, x, dw in items:
+            if accumulate:
+                dw.add_(dy.t() @ x)
+            else:
+                dw.copy_(dy.t() @ x)
+
+
 class Net(torch.nn.Module):
     def __init__(self, sink: bool):
         super().__init__()
@@ -56,6 +93,8 @@ class Net(torch.nn.Module):
         self.sink = sink
 
     def lin(self, m, x):
+        if self.sink == "defer":
+            return DeferLinear.apply(x, m.weight, m.bias)
         return SinkLinear.apply(x, m.weight, m.bias) if self.sink else m(x)
 
     def forward(self, x):
@@ -99,9 +138,14 @@ def _worker(rank, world, port, sink, accum, bucket_mb, q, comm="fp32"):
         net = Net(sink=sink)
         red = GradReducer(list(net.parameters()), bucket_mb=bucket_mb, groups=net.groups(),
                           comm_dtype=torch.bfloat16 if comm == "bf16" else torch.float32)
+        from dphubert_amd import ops
+        if sink == "defer":
+            ops.K.linear_wgrad_grouped = _cpu_grouped
         for m in range(accum):
             red.prepare(zero=m == 0, sync=m + 1 == accum)
-            (net(_inputs(rank, m)) / accum).backward()
+            with ops.grouped_wgrads(2 if sink == "defer" else 1):
+                (net(_inputs(rank, m)) / accum).backward()
+            assert not any(getattr(p, "_dph_hold", False) for p in net.parameters())
         red.finish()
         # fused groups are laid out back-to-back in one bucket
         for grp in net.groups():
@@ -122,9 +166,11 @@ def _free_port():
 @pytest.mark.parametrize("sink,accum,bucket_mb,comm", [(False, 1, 64.0, "fp32"), (True, 1, 64.0, "fp32"),
                                                        (True, 2, 1e-4, "fp32"), (False, 3, 1e-4, "fp32"),
                                                        (True, 1, 64.0, "bf16"), (True, 3, 1e-4, "bf16"),
-                                                       (False, 2, 64.0, "bf16")])
+                                                       (False, 2, 64.0, "bf16"), ("defer", 1, 1e-4, "fp32"),
+                                                       ("defer", 2, 64.0, "fp32")])
 def test_grad_reducer_gloo_ws2(sink, accum, bucket_mb, comm):
-    """fp32 payload: exact mean of the ranks' accumulated gradients.  bf16 payload (half the link
+    """fp32 payload: exact mean of the ranks' accumulated gradients ("defer": the weight gradients queued by
+    ops.grouped_wgrads and launched two at a time, their buckets' collectives held until they land).  bf16 payload (half the link
     bytes): each rank's accumulated gradient is rounded to bf16 (8 mantissa bits) before the sum, so the mean
     is within 2 bf16 ulps (2 * 2^-8 relative) of the exact one, elementwise."""
     world = 2
