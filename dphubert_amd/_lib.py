@@ -138,6 +138,7 @@ _SIGS = {
     "dph_grad_sumsq": ([vp, i64, vp, vp, i64, vp, S], C.c_int),
     "dph_adamw_step": ([vp, i64, vp, vp, i64, vp, i64, i64, vp, f32, S], C.c_int),
     "dph_adamw_step_dev": ([vp, i64, vp, vp, i64, vp, vp, f32, S], C.c_int),
+    "dph_adamw_step_img": ([vp, i64, vp, vp, i64, vp, vp, i64, i64, vp, f32, vp, S], C.c_int),
     "dph_set_rng_epoch": ([vp], C.c_int),
     "dph_event_create": ([C.POINTER(vp)], C.c_int),
     "dph_event_record": ([vp, S], C.c_int),
@@ -148,7 +149,7 @@ _SIGS = {
 _lib = None
 # include/dphubert_hip.h layout (3: dph_adamw_step_dev, dph_set_rng_epoch; 4: dph_event_*; 5: LN bwd / colsum
 # workspaces; 12: dph_hc_bank_fwd / dph_hc_bank_bwd; 15: dph_gemm_mn_plan; 16: DphGemmArgs.dyn_ext, dph_ffn_compact + gathers / scatters)
-ABI_VERSION = 17
+ABI_VERSION = 18
 
 
 class DphError(RuntimeError):

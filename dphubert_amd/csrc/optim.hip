@@ -65,10 +65,13 @@ __global__ void __launch_bounds__(256) adamw_kernel(const DphTensorSlot* __restr
                                                     const int64_t* __restrict__ cslot,
                                                     const int64_t* __restrict__ cstart, Groups G, float step,
                                                     const DphAdamDyn* __restrict__ dyn,
-                                                    const float* __restrict__ sumsq, float max_norm) {
+                                                    const float* __restrict__ sumsq, float max_norm,
+                                                    const uint64_t* __restrict__ img) {
   const int64_t c = blockIdx.x;
   const DphTensorSlot sl = slots[cslot[c]];
   if (!sl.grad) return;
+  // the parameter's place in its bf16 GEMM image (0: none): the updated master is cast there too
+  bf16_t* const im = img ? reinterpret_cast<bf16_t*>(img[cslot[c]]) : nullptr;
   // device-resident lr / step (HIP-graph replays) or the launch-time values
   const DphAdamGroup gr = dyn ? dyn->g[sl.group] : G.g[sl.group];
   if (dyn) step = dyn->step;
@@ -94,7 +97,8 @@ __global__ void __launch_bounds__(256) adamw_kernel(const DphTensorSlot* __restr
   int64_t i0 = s0;
   // 16-B path over the chunk's whole quads when all four streams are 16-B aligned there
   const uintptr_t al = reinterpret_cast<uintptr_t>(sl.grad + s0) | reinterpret_cast<uintptr_t>(sl.param + s0) |
-                       reinterpret_cast<uintptr_t>(sl.exp_avg + s0) | reinterpret_cast<uintptr_t>(sl.exp_avg_sq + s0);
+                       reinterpret_cast<uintptr_t>(sl.exp_avg + s0) | reinterpret_cast<uintptr_t>(sl.exp_avg_sq + s0) |
+                       (im ? 2 * reinterpret_cast<uintptr_t>(im + s0) : 0);   // (8-B image stores)
   if ((al & 15) == 0) {
     const int64_t n4 = (s1 - s0) >> 2;
     float4* g4 = reinterpret_cast<float4*>(sl.grad + s0);
@@ -111,6 +115,7 @@ __global__ void __launch_bounds__(256) adamw_kernel(const DphTensorSlot* __restr
       m4[j] = m;
       v4[j] = v;
       g4[j] = g;
+      if (im) *reinterpret_cast<uint2*>(im + s0 + 4 * j) = make_uint2(pack2bf(p.x, p.y), pack2bf(p.z, p.w));
     }
     i0 = s0 + 4 * n4;
   }
@@ -121,6 +126,7 @@ __global__ void __launch_bounds__(256) adamw_kernel(const DphTensorSlot* __restr
     sl.exp_avg[i] = m;
     sl.exp_avg_sq[i] = v;
     sl.grad[i] = g;
+    if (im) im[i] = f2bf(p);
   }
 }
 
@@ -148,7 +154,7 @@ extern "C" int dph_adamw_step(const DphTensorSlot* slots, int64_t n_slots, const
   Groups G;
   for (int i = 0; i < MAX_GROUPS; ++i) G.g[i] = groups[i < n_groups ? i : 0];
   hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)n_chunks), dim3(256), 0, stream, slots, chunk_slot, chunk_start, G,
-                     (float)step, (const DphAdamDyn*)nullptr, sumsq, max_norm);
+                     (float)step, (const DphAdamDyn*)nullptr, sumsq, max_norm, (const uint64_t*)nullptr);
   return check_launch("dph_adamw_step");
 }
 
@@ -158,6 +164,21 @@ extern "C" int dph_adamw_step_dev(const DphTensorSlot* slots, int64_t n_slots, c
   DPH_REQUIRE(slots && chunk_slot && chunk_start && dyn && n_chunks > 0, "dph_adamw_step_dev: bad args");
   Groups G = {};
   hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)n_chunks), dim3(256), 0, stream, slots, chunk_slot, chunk_start, G,
-                     1.0f, dyn, sumsq, max_norm);
+                     1.0f, dyn, sumsq, max_norm, (const uint64_t*)nullptr);
   return check_launch("dph_adamw_step_dev");
+}
+
+extern "C" int dph_adamw_step_img(const DphTensorSlot* slots, int64_t n_slots, const int64_t* chunk_slot,
+                                  const int64_t* chunk_start, int64_t n_chunks, const DphAdamDyn* dyn,
+                                  const DphAdamGroup* groups, int64_t n_groups, int64_t step, const float* sumsq,
+                                  float max_norm, const uint64_t* img, hipStream_t stream) {
+  DPH_REQUIRE(slots && chunk_slot && chunk_start && n_chunks > 0, "dph_adamw_step_img: bad args");
+  DPH_REQUIRE(dyn || (groups && n_groups >= 1 && n_groups <= MAX_GROUPS && step >= 1),
+              "dph_adamw_step_img: need dyn or groups/step");
+  Groups G = {};
+  if (!dyn)
+    for (int i = 0; i < MAX_GROUPS; ++i) G.g[i] = groups[i < n_groups ? i : 0];
+  hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)n_chunks), dim3(256), 0, stream, slots, chunk_slot, chunk_start, G,
+                     dyn ? 1.0f : (float)step, dyn, sumsq, max_norm, img);
+  return check_launch("dph_adamw_step_img");
 }

@@ -146,10 +146,27 @@ def _table(rows) -> torch.Tensor:
     return t
 
 
-def refresh_images(updated_ids) -> None:
+def image_targets(updated_ids):
+    """Where the optimizer kernel can write the bf16 casts itself (dph_adamw_step_img): {id(param): address of
+    its rows in a registered image} for the images whose sources are all in ``updated_ids``, and the ids of the
+    images fully covered that way (a parameter feeding two images casts into the first; the second stays with
+    refresh_images)."""
+    dst, covered = {}, set()
+    for _owner, ts, out in _REFRESH.values():
+        if not all(id(t) in updated_ids for t in ts) or any(id(t) in dst for t in ts):
+            continue
+        off = 0
+        for t in ts:
+            dst[id(t)] = out.data_ptr() + off * 2
+            off += t.numel()
+        covered.add(id(out))
+    return dst, covered
+
+
+def refresh_images(updated_ids, cast_done=frozenset()) -> None:
     """Recast every registered image whose sources are all in ``updated_ids`` (ids of parameters
-    the optimizer just wrote), re-transpose their W^T images, re-copy the fp32 concatenations, and
-    re-key the caches."""
+    the optimizer just wrote) -- except the images in ``cast_done`` (ids: the optimizer kernel cast them,
+    image_targets) --, re-transpose their W^T images, re-copy the fp32 concatenations, and re-key the caches."""
     cats = [e for e in _CAT_REFRESH.values() if all(id(t) in updated_ids for t in e[1])]
     if cats:
         crows = []
@@ -166,12 +183,14 @@ def refresh_images(updated_ids) -> None:
         return
     rows = []
     for _owner, ts, out in ents:
+        if id(out) in cast_done:
+            continue
         off = 0
         for t in ts:
             rows.append((t.data_ptr(), out.data_ptr() + off * 2, t.numel()))
             off += t.numel()
-    tab = _table(rows)
-    call("dph_cast_bf16_multi", ptr(tab), len(rows), _s())
+    if rows:
+        call("dph_cast_bf16_multi", ptr(_table(rows)), len(rows), _s())
     for owner, ts, out in ents:
         owner._dph_img = (("cat",) + _version_key(ts), out)
     trows = [(img.data_ptr(), tout.data_ptr(), img.shape[0], img.shape[1])

@@ -125,27 +125,29 @@ class FusedAdamW(torch.optim.Optimizer):
         if clip:
             call("dph_grad_sumsq", ptr(self._slots_dev), len(plist), ptr(self._cslot), ptr(self._cstart),
                  self._nchunks, ptr(self._sumsq), s)
-        if self.dyn_ptr is not None:
-            call("dph_adamw_step_dev", ptr(self._slots_dev), len(plist), ptr(self._cslot), ptr(self._cstart),
-                 self._nchunks, self.dyn_ptr, ptr(self._sumsq) if clip else None, float(self.max_grad_norm or 0.0), s)
-        else:
-            groups = (DphAdamGroup * 4)()
+        from . import ops
+        ids = {id(p) for _, p in plist}
+        # the bf16 GEMM images of the updated weights are written by the AdamW kernel itself (one pass over the
+        # masters instead of a second cast launch re-reading all of them)
+        dst, cast_done = ops.image_targets(ids)
+        img = ops._table([(dst.get(id(p), 0),) for _, p in plist])
+        groups = (DphAdamGroup * 4)()
+        if self.dyn_ptr is None:
             for gi, g in enumerate(self.param_groups):
                 groups[gi].lr = g["lr"]
                 groups[gi].weight_decay = g["weight_decay"]
                 groups[gi].beta1 = g["betas"][0]
                 groups[gi].beta2 = g["betas"][1]
                 groups[gi].eps = g["eps"]
-            call("dph_adamw_step", ptr(self._slots_dev), len(plist), ptr(self._cslot), ptr(self._cstart),
-                 self._nchunks, groups, len(self.param_groups), self._step, ptr(self._sumsq) if clip else None,
-                 float(self.max_grad_norm or 0.0), s)
+        call("dph_adamw_step_img", ptr(self._slots_dev), len(plist), ptr(self._cslot), ptr(self._cstart),
+             self._nchunks, self.dyn_ptr, groups, len(self.param_groups), self._step,
+             ptr(self._sumsq) if clip else None, float(self.max_grad_norm or 0.0), ptr(img), s)
         # the kernel wrote the masters behind autograd's back: bump their version counters so every
         # cached bf16 GEMM image of them (ops.bf16_image & co.) is rebuilt before its next use
         increment_version([p for _, p in plist])
-        # recast (and re-transpose) the bf16 GEMM images of the updated weights in two batched
-        # launches, and move their cache keys to the new versions
-        from . import ops
-        ops.refresh_images({id(p) for _, p in plist})
+        # cast the images the kernel did not cover, re-transpose the W^T images, and move the cache keys to the
+        # new versions
+        ops.refresh_images(ids, cast_done)
 
     @torch.no_grad()
     def step(self, closure=None):

@@ -493,6 +493,14 @@ typedef struct DphAdamDyn {
 int dph_adamw_step_dev(const DphTensorSlot* slots, int64_t n_slots, const int64_t* chunk_slot,
                        const int64_t* chunk_start, int64_t n_chunks, const DphAdamDyn* dyn, const float* sumsq,
                        float max_norm, hipStream_t stream);
+/* either of the above (dyn != NULL: device hyper-parameters, else groups / step) that also writes each updated
+ * master, cast to bf16 (round to nearest even, as dph_cast_bf16), to img[slot] (a device table of n_slots bf16
+ * addresses, 0 = none): the bf16 GEMM images of the weights refreshed by the optimizer kernel itself instead of
+ * a second pass that re-reads every master (replaces the torch param.data -> bf16 copy of the next forward) */
+int dph_adamw_step_img(const DphTensorSlot* slots, int64_t n_slots, const int64_t* chunk_slot,
+                       const int64_t* chunk_start, int64_t n_chunks, const DphAdamDyn* dyn, const DphAdamGroup* groups,
+                       int64_t n_groups, int64_t step, const float* sumsq, float max_norm, const uint64_t* img,
+                       hipStream_t stream);
 
 /* ------------------------------------------------------------------------ *
  * Per-step RNG epoch: every dropout / HardConcrete kernel adds (*epoch) * 0x9E3779B97F4A7C15 to
