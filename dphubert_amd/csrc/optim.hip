@@ -114,7 +114,7 @@ __global__ void __launch_bounds__(256) adamw_kernel(const DphTensorSlot* __restr
       p4[j] = p;
       m4[j] = m;
       v4[j] = v;
-      g4[j] = g;
+      if (clip < 1.0f) g4[j] = g;   // (clip_grad_norm_ scales .grad in place; unscaled, it is already there)
       if (im) *reinterpret_cast<uint2*>(im + s0 + 4 * j) = make_uint2(pack2bf(p.x, p.y), pack2bf(p.z, p.w));
     }
     i0 = s0 + 4 * n4;
@@ -125,7 +125,7 @@ __global__ void __launch_bounds__(256) adamw_kernel(const DphTensorSlot* __restr
     sl.param[i] = p;
     sl.exp_avg[i] = m;
     sl.exp_avg_sq[i] = v;
-    sl.grad[i] = g;
+    if (clip < 1.0f) sl.grad[i] = g;
     if (im) im[i] = f2bf(p);
   }
 }
