@@ -781,7 +781,10 @@ extern "C" int dph_conv0_gn_bwd(const float* wave, int64_t B, int64_t S, const f
   dim3 grid((unsigned)cdiv(p.L0, rows), (unsigned)B);
   const bf16_t* dyb = reinterpret_cast<const bf16_t*>(dy);
   const bool vec = C % 4 == 0;
-  if (var == 1 && C <= 512)
+  if (var == 1 && C <= 512 && vec)
+    hipLaunchKernelGGL((conv0_gn_bwd_kernel<2, 4, true>), grid, dim3(256), 0, stream, wave, w, p, gamma, beta, mask, mean,
+                       rstd, dyb, sums, rows);
+  else if (var == 1 && C <= 512)
     hipLaunchKernelGGL((conv0_gn_bwd_kernel<2, 4, false>), grid, dim3(256), 0, stream, wave, w, p, gamma, beta, mask, mean,
                        rstd, dyb, sums, rows);
   else if (var == 2)
