@@ -28,39 +28,8 @@ import torch
 import torch.distributed as dist
 
 FLOP_PER_UTT_BASE = 599.6e9      # teacher fwd + 3 x (student fwd + projections), 10 s utterance
-MFMA_PEAK_TFLOPS = 2500.0        # MI355X dense bf16 (MI355X_MICROARCH.md)
-
-
-def forward_flops(cfg: dict, samples: int) -> float:
-    """Dense forward FLOPs of one utterance through extract_features: conv frontend, feature
-    projection, positional conv, per layer q/k/v/out projections, QK^T + PV and the FFN, at the config's (possibly
-    pruned, ragged) widths."""
-    L, cin, f = samples, 1, 0.0
-    for cout, k, s_ in cfg["extractor_conv_layer_config"]:
-        L = (L - k) // s_ + 1
-        f += 2.0 * cin * cout * k * L
-        cin = cout
-    T, D = L, cfg["encoder_embed_dim"]
-    f += 2.0 * cin * D * T
-    f += 2.0 * D * (D // cfg["encoder_pos_conv_groups"]) * cfg["encoder_pos_conv_kernel"] * T
-    heads = cfg.get("encoder_num_heads") or [len(h) for h in cfg["encoder_remaining_heads"]]
-    hd = cfg.get("encoder_head_dim", 64)
-    for l in range(cfg["encoder_num_layers"]):
-        if cfg["encoder_use_attention"][l] and heads[l] > 0:
-            e = heads[l] * hd
-            f += 2.0 * T * D * 3 * e + 2.0 * T * e * D + 4.0 * T * T * e
-        if cfg["encoder_use_feed_forward"][l]:
-            f += 4.0 * T * D * cfg["encoder_ff_interm_features"][l]
-    return f
-
-
-def step_flops_per_utt(tcfg: dict, scfg: dict, n_distill: int, samples: int) -> float:
-    """teacher forward + 3 x (student forward + distill projections) per utterance."""
-    T = samples
-    for _, k, s_ in tcfg["extractor_conv_layer_config"]:
-        T = (T - k) // s_ + 1
-    proj = n_distill * 2.0 * T * scfg["encoder_embed_dim"] * tcfg["encoder_embed_dim"]
-    return forward_flops(tcfg, samples) + 3.0 * (forward_flops(scfg, samples) + proj)
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from dphubert_amd.perfmodel import MFMA_PEAK_TFLOPS, forward_flops, step_flops_per_utt  # noqa: E402,F401
 
 
 def workload(args):

@@ -121,12 +121,19 @@ _SIGS = {
     "dph_layernorm_gelu_fwd": ([vp, C.c_int, vp, vp, vp, vp, vp, vp, vp, i64, i64, f32, S], C.c_int),
     "dph_layernorm_bwd_x32": ([vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, vp, i64, S], C.c_int),
     "dph_transpose_bf16_multi": ([vp, i64, S], C.c_int),
+    "dph_layernorm_fwd_x32": ([vp, vp, vp, vp, vp, vp, i64, i64, f32, S], C.c_int),
+    "dph_layernorm_bwd_res32": ([vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, vp, vp, i64, S], C.c_int),
+    "dph_branch_bwd_f32": ([vp, vp, C.c_int, i64, i64, f32, u64, vp, vp, i64, vp, vp, vp, S], C.c_int),
     "dph_conv_weight_pack": ([vp, vp, i64, i64, i64, i64, i64, S], C.c_int),
     "dph_conv_weight_unpack_grad": ([vp, vp, i64, i64, i64, i64, C.c_int, S], C.c_int),
     "dph_add_bf16": ([vp, vp, vp, i64, S], C.c_int),
     "dph_branch_bwd": ([vp, vp, i64, i64, f32, u64, vp, vp, i64, vp, vp, vp, S], C.c_int),
     "dph_distill_loss_fwd": ([vp, vp, i64, i64, i64, i64, f32, f32, f32, C.c_int, vp, vp, vp, S], C.c_int),
     "dph_distill_loss_bwd": ([vp, vp, vp, vp, i64, i64, i64, i64, f32, f32, f32, C.c_int, vp, S], C.c_int),
+    "dph_distill_loss_fwd_ex": ([vp, vp, C.c_uint32, i64, i64, i64, i64, f32, f32, f32, C.c_int, vp, vp, vp, S],
+                                C.c_int),
+    "dph_distill_loss_bwd_ex": ([vp, vp, C.c_uint32, vp, vp, i64, i64, i64, i64, f32, f32, f32, C.c_int, vp, S],
+                                C.c_int),
     "dph_reg_loss_fwd": ([vp, vp, vp, vp, vp, f32, f32, vp, S], C.c_int),
     "dph_reg_loss_bwd": ([vp, vp, vp, vp, vp, vp, vp, f32, f32, vp, vp, vp, S], C.c_int),
     "dph_hc_sample_fwd": ([vp, vp, vp, vp, i64, u64, f32, f32, f32, f32, S], C.c_int),
@@ -148,8 +155,10 @@ _SIGS = {
 
 _lib = None
 # include/dphubert_hip.h layout (3: dph_adamw_step_dev, dph_set_rng_epoch; 4: dph_event_*; 5: LN bwd / colsum
-# workspaces; 12: dph_hc_bank_fwd / dph_hc_bank_bwd; 15: dph_gemm_mn_plan; 16: DphGemmArgs.dyn_ext, dph_ffn_compact + gathers / scatters)
-ABI_VERSION = 18
+# workspaces; 12: dph_hc_bank_fwd / dph_hc_bank_bwd; 15: dph_gemm_mn_plan; 16: DphGemmArgs.dyn_ext, dph_ffn_compact + gathers / scatters;
+# 19: DPH_GEMM_RESID_F32, dph_layernorm_fwd_x32 / _bwd_res32, dph_branch_bwd_f32, dph_distill_loss_*_ex: the fp32
+# pre-norm residual stream)
+ABI_VERSION = 19
 
 
 class DphError(RuntimeError):

@@ -247,12 +247,20 @@ def _train(args, module, world, rank, dev):
         module.global_step = int(ck.get("global_step", 0))
         for _ in range(module.global_step):
             trainer.scheduler.step()
+        trainer.verify_replicas()          # every rank loaded the same state (raises on all ranks otherwise)
     if rank == 0:
         ckpt_dir.mkdir(parents=True, exist_ok=True)
     log_f = open(args.exp_dir / "log.jsonl", "a") if rank == 0 else None
     feed = _batches(args, rank, world, dev)
     t0 = time.time()
     audio = 0.0
+    # algorithmic work of this rank's steps (perfmodel): MFMA FLOPs and the HBM bytes of the
+    # bandwidth-bound kernels -> mfma_util / hbm_gbps next to the reference's log keys (SURVEY 2 "Metrics / logging")
+    from . import perfmodel as PM
+    tcfg = getattr(module.teacher_model, "dph_config", None)
+    scfg = getattr(module.student_model, "dph_config", None)
+    n_train = sum(p.numel() for p in trainer.reducer.params)
+    work_f = work_b = 0.0
     while module.global_step < args.max_updates:
         for _ in range(args.accum_grad):
             batch = next(feed)
@@ -265,11 +273,20 @@ def _train(args, module, world, rank, dev):
                     log_f.flush()
                 batch = next(feed)
             audio += batch[0].shape[0] * batch[0].shape[1] / 16000.0
+            if tcfg is not None and scfg is not None:
+                nb, S = batch[0].shape
+                work_f += nb * PM.step_flops_per_utt(tcfg, scfg, len(module.distill_layers), S)
+                work_b += nb * PM.step_hbm_bytes_per_utt(tcfg, scfg, S)
             loss = trainer.step(batch)
+        work_b += PM.optimizer_hbm_bytes(n_train)
         gs = module.global_step
         if rank == 0 and (gs % args.log_interval == 0 or gs == args.max_updates):
-            rec = {"step": gs, "audio_s_per_s": round(audio * world / max(time.time() - t0, 1e-9), 1),
+            el = max(time.time() - t0, 1e-9)
+            rec = {"step": gs, "audio_s_per_s": round(audio * world / el, 1),
                    "lr": trainer.scheduler.get_last_lr()[0]}
+            if work_f > 0:
+                rec["mfma_util"] = round(work_f / el / (PM.MFMA_PEAK_TFLOPS * 1e12), 4)
+                rec["hbm_gbps"] = round(work_b / el / 1e9, 1)
             rec.update({k: float(v) for k, v in module.logged.items()})
             line = json.dumps(rec)
             print(line, flush=True)

@@ -159,7 +159,11 @@ __global__ void add_bf16_kernel(const bf16_t* __restrict__ a, const bf16_t* __re
 
 // out = dy * drop(p, seed, m*cols+n) * (*smask), rows with (m % len_rows) >= row_len[m / len_rows] zeroed;
 // colsum[n] += out; sdot += sum dy*drop*pre
-__global__ void __launch_bounds__(256) branch_bwd_kernel(const bf16_t* __restrict__ dy, bf16_t* __restrict__ out,
+// DyT / OT: bf16, or fp32 for the pre-norm residual stream (its gradient / the pos-conv output, components.py:846-850)
+__device__ __forceinline__ float to_f(bf16_t v) { return bf2f(v); }
+__device__ __forceinline__ float to_f(float v) { return v; }
+template <typename DyT, typename OT>
+__global__ void __launch_bounds__(256) branch_bwd_kernel(const DyT* __restrict__ dy, OT* __restrict__ out,
                                                          int64_t rows, int64_t cols, float p, uint64_t seed,
                                                          const float* __restrict__ smask,
                                                          const int64_t* __restrict__ row_len, int64_t len_rows,
@@ -186,15 +190,24 @@ __global__ void __launch_bounds__(256) branch_bwd_kernel(const bf16_t* __restric
         const int64_t c = c0 + i;
         float v = 0.f;
         if (c < cols && !zero) {
-          v = bf2f(dy[r * cols + c]) * dropout_scale(seed, (uint64_t)r * cols + c, p, inv_keep);
+          v = to_f(dy[r * cols + c]) * dropout_scale(seed, (uint64_t)r * cols + c, p, inv_keep);
           if (pre) sd += v * bf2f(pre[r * cols + c]);
           v *= sm;
         }
         o[i] = v;
         acc[i] += v;
       }
-      bf16_t* op = out + r * cols + c0;
-      if (c0 + 8 <= cols && cols % 8 == 0) {
+      OT* op = out + r * cols + c0;
+      if constexpr (sizeof(OT) == 4) {
+        if (c0 + 8 <= cols && cols % 8 == 0) {
+          *reinterpret_cast<float4*>(op) = make_float4(o[0], o[1], o[2], o[3]);
+          *reinterpret_cast<float4*>(op + 4) = make_float4(o[4], o[5], o[6], o[7]);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 8; ++i)
+            if (c0 + i < cols) op[i] = o[i];
+        }
+      } else if (c0 + 8 <= cols && cols % 8 == 0) {
         *reinterpret_cast<uint4*>(op) = make_uint4(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]), pack2bf(o[4], o[5]),
                                                    pack2bf(o[6], o[7]));
       } else {
@@ -511,8 +524,27 @@ extern "C" int dph_branch_bwd(const void* dy, void* out, int64_t rows, int64_t c
   DPH_REQUIRE(!sdot || pre, "dph_branch_bwd: sdot needs pre");
   const int64_t rpb = rows_per_block_for(rows);
   dim3 grid((unsigned)cdiv(cols, 512), (unsigned)cdiv(rows, rpb));
-  hipLaunchKernelGGL(branch_bwd_kernel, grid, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(dy),
-                     reinterpret_cast<bf16_t*>(out), rows, cols, p, seed, smask, row_len, len_rows, colsum,
-                     reinterpret_cast<const bf16_t*>(pre), sdot, rpb);
+  hipLaunchKernelGGL((branch_bwd_kernel<bf16_t, bf16_t>), grid, dim3(256), 0, stream,
+                     reinterpret_cast<const bf16_t*>(dy), reinterpret_cast<bf16_t*>(out), rows, cols, p, seed, smask,
+                     row_len, len_rows, colsum, reinterpret_cast<const bf16_t*>(pre), sdot, rpb);
   return check_launch("dph_branch_bwd");
+}
+
+extern "C" int dph_branch_bwd_f32(const float* dy, void* out, int out_f32, int64_t rows, int64_t cols, float p,
+                                  uint64_t seed, const float* smask, const int64_t* row_len, int64_t len_rows,
+                                  float* colsum, const void* pre, float* sdot, hipStream_t stream) {
+  DPH_REQUIRE(dy && out && rows > 0 && cols > 0, "dph_branch_bwd_f32: bad args");
+  DPH_REQUIRE(!row_len || len_rows > 0, "dph_branch_bwd_f32: row_len needs len_rows");
+  DPH_REQUIRE(!sdot || pre, "dph_branch_bwd_f32: sdot needs pre");
+  const int64_t rpb = rows_per_block_for(rows);
+  dim3 grid((unsigned)cdiv(cols, 512), (unsigned)cdiv(rows, rpb));
+  if (out_f32)
+    hipLaunchKernelGGL((branch_bwd_kernel<float, float>), grid, dim3(256), 0, stream, dy,
+                       reinterpret_cast<float*>(out), rows, cols, p, seed, smask, row_len, len_rows, colsum,
+                       reinterpret_cast<const bf16_t*>(pre), sdot, rpb);
+  else
+    hipLaunchKernelGGL((branch_bwd_kernel<float, bf16_t>), grid, dim3(256), 0, stream, dy,
+                       reinterpret_cast<bf16_t*>(out), rows, cols, p, seed, smask, row_len, len_rows, colsum,
+                       reinterpret_cast<const bf16_t*>(pre), sdot, rpb);
+  return check_launch("dph_branch_bwd_f32");
 }

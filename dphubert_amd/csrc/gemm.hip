@@ -234,7 +234,13 @@ __device__ __forceinline__ void epilogue8(const DphGemmArgs& a, int64_t z, int64
   if (a.bias) load8_f32(a.bias + voff + n, vvec, nv, bias);
   if (a.colmask) load8_f32(a.colmask + voff + n, vvec, nv, cm);
   if (a.aux_in) load8_bf16(reinterpret_cast<const bf16_t*>(a.aux_in) + coff, vec, nv, aux);
-  if (a.residual) load8_bf16(reinterpret_cast<const bf16_t*>(a.residual) + coff, vec, nv, res);
+  if (a.residual) {
+    if (a.flags & DPH_GEMM_RESID_F32)   // fp32 residual stream (pre-norm layers)
+      load8_f32(reinterpret_cast<const float*>(a.residual) + coff,
+                (nv == 8) && ((coff & 3) == 0) && ((reinterpret_cast<uintptr_t>(a.residual) & 15) == 0), nv, res);
+    else
+      load8_bf16(reinterpret_cast<const bf16_t*>(a.residual) + coff, vec, nv, res);
+  }
   const float sm = a.smask ? *a.smask : 1.0f;
   float pre[8];
 #pragma unroll
@@ -302,9 +308,10 @@ __device__ __forceinline__ bool tile_epi_ok(const DphGemmArgs& a, int64_t n) {
                            reinterpret_cast<uintptr_t>(a.aux_in) | reinterpret_cast<uintptr_t>(a.residual);
   const uintptr_t valign = reinterpret_cast<uintptr_t>(a.bias) | reinterpret_cast<uintptr_t>(a.colmask);
   // one per-row bf16 input (aux_in OR residual) and a plain (non-accumulating) output
+  // (an fp32 residual takes the generic epilogue8)
   return n + 8 <= a.N && (calign & 7) == 0 && (palign & 15) == 0 && (valign & 15) == 0 &&
          (a.vec_z_inner & 3) == 0 && !(a.aux_in && a.residual) && a.c_dtype != DPH_OUT_F32_ACCUM &&
-         (a.N & 1) == 0;
+         (a.N & 1) == 0 && !(a.flags & DPH_GEMM_RESID_F32);
 }
 
 __device__ __forceinline__ void unpack_bf16x8(const uint4 r, float (&o)[8]) {
@@ -1006,7 +1013,11 @@ __device__ __forceinline__ bool direct_epi_t(const DphGemmArgs& a, int64_t z, in
   const int64_t base = zb + r0off;   // (rpb == 0)
   // (arithmetic select of the two pointer VALUES, as in tile_epi_rows)
   const uintptr_t ax_p = reinterpret_cast<uintptr_t>(a.aux_in), rs_p = reinterpret_cast<uintptr_t>(a.residual);
-  const bf16_t* inp = reinterpret_cast<const bf16_t*>(ax_p | (rs_p & (uintptr_t)(-(intptr_t)(ax_p == 0))));
+  // an fp32 residual (DPH_GEMM_RESID_F32: the pre-norm residual stream) is read in the checked copy below, not
+  // through the bf16 per-element input
+  const bool res32 = (a.flags & DPH_GEMM_RESID_F32) != 0;
+  const uintptr_t rs_b = rs_p & (uintptr_t)(-(intptr_t)!res32);
+  const bf16_t* inp = reinterpret_cast<const bf16_t*>(ax_p | (rs_b & (uintptr_t)(-(intptr_t)(ax_p == 0))));
   const bool has_in = inp != nullptr, has_res = has_in && ax_p == 0;
   // (column sums are compiled for the GELU backward variants only: the only GEMMs that request them)
   constexpr bool BWD = ACT == DPH_ACT_GELU_BWD || ACT == DPH_ACT_GELU_BWD_DGK;
@@ -1101,6 +1112,12 @@ __device__ __forceinline__ bool direct_epi_t(const DphGemmArgs& a, int64_t z, in
         float v[4], pre[4], ax[4], xin[4], xin2[4];
         unpack_bf16x4(in[i][j], xin);
         if constexpr (DGK) unpack_bf16x4(in2[i][j], xin2);
+        if constexpr (!BWD && CK) {
+          if (res32) {
+            const float4 q = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(rs_p) + ro + 16 * j);
+            xin[0] += q.x; xin[1] += q.y; xin[2] += q.z; xin[3] += q.w;
+          }
+        }
         uint32_t keep = 0xfu;
         if constexpr (DROP) {
           // element e_base + 16 i N + 16 j is even (N % 4 == 0, n % 4 == 0): pairs e/2 and e/2 + 1
@@ -1190,7 +1207,7 @@ __device__ __forceinline__ bool direct_epi_t(const DphGemmArgs& a, int64_t z, in
 #endif
     }
   };
-  const bool lean = mfull && nfull && !a.row_len && out_bf16 && !rpb;
+  const bool lean = mfull && nfull && !a.row_len && out_bf16 && !rpb && !res32;
   if (lean) frags(std::false_type{});
   else frags(std::true_type{});
   if (colsum) {
@@ -3016,6 +3033,9 @@ extern "C" int dph_gemm(const DphGemmArgs* args, hipStream_t stream) {
               "dph_gemm: mn-contiguous B needs N %% 8 == 0 or 8-padded rows");
   DPH_REQUIRE(a.act != DPH_ACT_GELU_BWD || a.aux_in, "dph_gemm: GELU_BWD needs aux_in");
   DPH_REQUIRE(!a.row_len || a.len_rows > 0, "dph_gemm: row_len needs len_rows");
+  DPH_REQUIRE(!(a.flags & DPH_GEMM_RESID_F32) ||
+                  (a.residual && a.act != DPH_ACT_GELU_BWD && a.act != DPH_ACT_GELU_BWD_DGK),
+              "dph_gemm: DPH_GEMM_RESID_F32 needs a residual and a forward (non-GELU-backward) epilogue");
   int64_t kchunk = a.K;
   if (a.splits > 1) {
     DPH_REQUIRE(!a.colsum_out && !a.colsum_aux, "dph_gemm: column sums not supported with split-K");

@@ -14,9 +14,22 @@
 namespace dph {
 namespace {
 
+// teacher layer l is bf16, or fp32 when bit l of f32 is set (the fp32 residual stream of pre-norm encoders)
 struct TPtrs {
-  const bf16_t* p[DPH_MAX_DISTILL_LAYERS];
+  const void* p[DPH_MAX_DISTILL_LAYERS];
+  uint32_t f32;
 };
+
+__device__ __forceinline__ void load_t4(const TPtrs& tp, int64_t l, int64_t off, float (&o)[4]) {
+  if ((tp.f32 >> l) & 1u) {
+    const float4 v = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(tp.p[l]) + off);
+    o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+  } else {
+    const uint2 v = *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16_t*>(tp.p[l]) + off);
+    o[0] = __uint_as_float(v.x << 16); o[1] = __uint_as_float(v.x & 0xffff0000u);
+    o[2] = __uint_as_float(v.y << 16); o[3] = __uint_as_float(v.y & 0xffff0000u);
+  }
+}
 
 constexpr float COS_EPS = 1e-8f;
 
@@ -35,14 +48,13 @@ __global__ void __launch_bounds__(256) loss_fwd_kernel(const float* __restrict__
     const int64_t b = (row / T) % B;
     const int64_t l = row / (T * B);
     const float* sr = s + row * D;
-    const bf16_t* tr = tp.p[l] + (b * T + t) * D;
+    const int64_t toff = (b * T + t) * D;
     float dot = 0.f, ns = 0.f, nt = 0.f;
     for (int64_t c = lane * 4; c < D; c += 256) {
       const float4 sv = *reinterpret_cast<const float4*>(sr + c);
-      const uint2 tv = *reinterpret_cast<const uint2*>(tr + c);
       const float a[4] = {sv.x, sv.y, sv.z, sv.w};
-      const float bb[4] = {__uint_as_float(tv.x << 16), __uint_as_float(tv.x & 0xffff0000u),
-                           __uint_as_float(tv.y << 16), __uint_as_float(tv.y & 0xffff0000u)};
+      float bb[4];
+      load_t4(tp, l, toff + c, bb);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const float d = a[i] - bb[i];
@@ -121,14 +133,13 @@ __global__ void __launch_bounds__(256) loss_bwd_kernel(const float* __restrict__
   const float ca = fc / (ns_ * nt_);          // coefficient of t
   const float cb = fc * cs / (ns_ * ns_);     // coefficient of s
   const float* sr = s + row * D;
-  const bf16_t* tr = tp.p[l] + (b * T + t) * D;
+  const int64_t toff = (b * T + t) * D;
   bf16_t* dr = ds + row * D;
   for (int64_t c = lane * 4; c < D; c += 256) {
     const float4 sv = *reinterpret_cast<const float4*>(sr + c);
-    const uint2 tv = *reinterpret_cast<const uint2*>(tr + c);
     const float a[4] = {sv.x, sv.y, sv.z, sv.w};
-    const float bb[4] = {__uint_as_float(tv.x << 16), __uint_as_float(tv.x & 0xffff0000u),
-                         __uint_as_float(tv.y << 16), __uint_as_float(tv.y & 0xffff0000u)};
+    float bb[4];
+    load_t4(tp, l, toff + c, bb);
     float o[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -145,14 +156,16 @@ __global__ void __launch_bounds__(256) loss_bwd_kernel(const float* __restrict__
 
 using namespace dph;
 
-extern "C" int dph_distill_loss_fwd(const float* s, const void* const* t_layers, int64_t B, int64_t L, int64_t T,
-                                    int64_t D, float l2w, float l1w, float cosw, int cos_logsig, float* rowstats,
-                                    float* partial, float* out, hipStream_t stream) {
+extern "C" int dph_distill_loss_fwd_ex(const float* s, const void* const* t_layers, uint32_t t_f32_mask, int64_t B,
+                                       int64_t L, int64_t T, int64_t D, float l2w, float l1w, float cosw,
+                                       int cos_logsig, float* rowstats, float* partial, float* out,
+                                       hipStream_t stream) {
   DPH_REQUIRE(s && t_layers && rowstats && partial && out, "dph_distill_loss_fwd: null pointer");
   DPH_REQUIRE(L >= 1 && L <= DPH_MAX_DISTILL_LAYERS && D % 4 == 0 && B > 0 && T > 0,
               "dph_distill_loss_fwd: unsupported L=%lld D=%lld", (long long)L, (long long)D);
   TPtrs tp;
-  for (int i = 0; i < DPH_MAX_DISTILL_LAYERS; ++i) tp.p[i] = i < L ? reinterpret_cast<const bf16_t*>(t_layers[i]) : nullptr;
+  for (int i = 0; i < DPH_MAX_DISTILL_LAYERS; ++i) tp.p[i] = i < L ? t_layers[i] : nullptr;
+  tp.f32 = t_f32_mask;
   const int64_t rows = B * L * T;
   const int64_t nblk = std::min<int64_t>(cdiv(rows, 4), DPH_LOSS_PARTIAL_FLOATS / 3);
   hipLaunchKernelGGL(loss_fwd_kernel, dim3((unsigned)nblk), dim3(256), 0, stream, s, tp, B, L, T, D, cos_logsig, rowstats,
@@ -162,17 +175,33 @@ extern "C" int dph_distill_loss_fwd(const float* s, const void* const* t_layers,
   return check_launch("dph_distill_loss_fwd");
 }
 
-extern "C" int dph_distill_loss_bwd(const float* s, const void* const* t_layers, const float* rowstats,
-                                    const float* dloss, int64_t B, int64_t L, int64_t T, int64_t D, float l2w,
-                                    float l1w, float cosw, int cos_logsig, void* ds, hipStream_t stream) {
+extern "C" int dph_distill_loss_fwd(const float* s, const void* const* t_layers, int64_t B, int64_t L, int64_t T,
+                                    int64_t D, float l2w, float l1w, float cosw, int cos_logsig, float* rowstats,
+                                    float* partial, float* out, hipStream_t stream) {
+  return dph_distill_loss_fwd_ex(s, t_layers, 0u, B, L, T, D, l2w, l1w, cosw, cos_logsig, rowstats, partial, out,
+                                 stream);
+}
+
+extern "C" int dph_distill_loss_bwd_ex(const float* s, const void* const* t_layers, uint32_t t_f32_mask,
+                                       const float* rowstats, const float* dloss, int64_t B, int64_t L, int64_t T,
+                                       int64_t D, float l2w, float l1w, float cosw, int cos_logsig, void* ds,
+                                       hipStream_t stream) {
   DPH_REQUIRE(s && t_layers && rowstats && ds, "dph_distill_loss_bwd: null pointer");
   DPH_REQUIRE(L >= 1 && L <= DPH_MAX_DISTILL_LAYERS && D % 4 == 0, "dph_distill_loss_bwd: unsupported");
   TPtrs tp;
-  for (int i = 0; i < DPH_MAX_DISTILL_LAYERS; ++i) tp.p[i] = i < L ? reinterpret_cast<const bf16_t*>(t_layers[i]) : nullptr;
+  for (int i = 0; i < DPH_MAX_DISTILL_LAYERS; ++i) tp.p[i] = i < L ? t_layers[i] : nullptr;
+  tp.f32 = t_f32_mask;
   const int64_t rows = B * L * T;
   hipLaunchKernelGGL(loss_bwd_kernel, dim3((unsigned)cdiv(rows, 4)), dim3(256), 0, stream, s, tp, rowstats, dloss, B, L,
                      T, D, l2w, l1w, cosw, cos_logsig, reinterpret_cast<bf16_t*>(ds));
   return check_launch("dph_distill_loss_bwd");
+}
+
+extern "C" int dph_distill_loss_bwd(const float* s, const void* const* t_layers, const float* rowstats,
+                                    const float* dloss, int64_t B, int64_t L, int64_t T, int64_t D, float l2w,
+                                    float l1w, float cosw, int cos_logsig, void* ds, hipStream_t stream) {
+  return dph_distill_loss_bwd_ex(s, t_layers, 0u, rowstats, dloss, B, L, T, D, l2w, l1w, cosw, cos_logsig, ds,
+                                 stream);
 }
 
 namespace dph {

@@ -42,6 +42,15 @@ __device__ __forceinline__ float4 ldx4(const float* p) { return *reinterpret_cas
 __device__ __forceinline__ void unpack4(float4 r, float (&o)[4]) {
   o[0] = r.x; o[1] = r.y; o[2] = r.z; o[3] = r.w;
 }
+// 4-element load / store of a bf16 or fp32 row segment (the pre-norm residual stream's gradient is fp32)
+__device__ __forceinline__ void ld4(const bf16_t* p, float (&o)[4]) { unpack4(*reinterpret_cast<const uint2*>(p), o); }
+__device__ __forceinline__ void ld4(const float* p, float (&o)[4]) { unpack4(*reinterpret_cast<const float4*>(p), o); }
+__device__ __forceinline__ void st4(bf16_t* p, const float (&v)[4]) {
+  *reinterpret_cast<uint2*>(p) = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
+}
+__device__ __forceinline__ void st4(float* p, const float (&v)[4]) {
+  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+}
 
 // per-column vector (gamma / beta / scale) for the NV 4-column chunks a lane owns; 0 past D
 template <int NV>
@@ -148,14 +157,15 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const XT* __restrict__ x, c
 // across the block's waves with LDS atomics, and written as one slab row per block; slab_reduce
 // adds the columns into the outputs.  (One global atomic per column per block -- ~500 blocks onto
 // the same 2304 addresses -- measured 0.09 TB/s: same-address atomics serialise at the memory side.)
-template <int NV, typename XT = bf16_t>
+// XT: the LN input's type; DT: dx / dx_add (fp32 for the pre-norm residual stream, components.py:846-850)
+template <int NV, typename XT = bf16_t, typename DT = bf16_t>
 __global__ void __launch_bounds__(64 * LN_BWD_WAVES) ln_bwd_kernel(
     const bf16_t* __restrict__ dy, const XT* __restrict__ x, const float* __restrict__ xscale,
     const float* __restrict__ gamma, const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
-    bf16_t* __restrict__ dx, float* __restrict__ dgamma, float* __restrict__ dbeta, int64_t rows, int D, int ld,
+    DT* __restrict__ dx, float* __restrict__ dgamma, float* __restrict__ dbeta, int64_t rows, int D, int ld,
     float drop_p, uint64_t seed, bf16_t* __restrict__ branch, float branch_p, uint64_t branch_seed,
     const float* __restrict__ branch_smask, float* __restrict__ branch_colsum, const bf16_t* __restrict__ branch_pre,
-    float* __restrict__ branch_sdot, const bf16_t* __restrict__ dx_add, float* __restrict__ ws) {
+    float* __restrict__ branch_sdot, const DT* __restrict__ dx_add, float* __restrict__ ws) {
   seed = epoch_seed(seed); branch_seed = epoch_seed(branch_seed);   // per-step RNG epoch (graph replays)
   __shared__ float4 red[LN_BWD_WAVES][NV * 64];
   const int lane = threadIdx.x & 63;
@@ -225,11 +235,11 @@ __global__ void __launch_bounds__(64 * LN_BWD_WAVES) ln_bwd_kernel(
         // other gradient paths into the LN input (pre-norm residual); the branch output below
         // stays the LN-path gradient only
         float ad[4];
-        unpack4(*reinterpret_cast<const uint2*>(dx_add + row * ld + col), ad);
-        *reinterpret_cast<uint2*>(dx + row * ld + col) =
-            make_uint2(pack2bf(o[0] + ad[0], o[1] + ad[1]), pack2bf(o[2] + ad[2], o[3] + ad[3]));
+        ld4(dx_add + row * ld + col, ad);
+        const float s[4] = {o[0] + ad[0], o[1] + ad[1], o[2] + ad[2], o[3] + ad[3]};
+        st4(dx + row * ld + col, s);
       } else {
-        *reinterpret_cast<uint2*>(dx + row * ld + col) = make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
+        st4(dx + row * ld + col, o);
       }
       if (branch) {
         float pre[4] = {0.f, 0.f, 0.f, 0.f}, z[4], bo[4];
@@ -531,6 +541,58 @@ extern "C" int dph_layernorm_bwd_x32(const void* dy, const float* x, const float
                        0, stream, ws, nblk, 3 * D, D, dgamma, dbeta, (float*)nullptr);
   }
   return check_launch("dph_layernorm_bwd_x32");
+}
+
+extern "C" int dph_layernorm_fwd_x32(const float* x, const float* gamma, const float* beta, void* y, float* mean,
+                                     float* rstd, int64_t rows, int64_t D, float eps, hipStream_t stream) {
+  DPH_REQUIRE(x && gamma && beta && y && mean && rstd, "dph_layernorm_fwd_x32: null pointer");
+  DPH_REQUIRE(D >= 1 && D % 4 == 0 && D <= LN_MAXV * 256 && rows > 0, "dph_layernorm_fwd_x32: unsupported D=%lld",
+              (long long)D);
+  const dim3 grid((unsigned)cdiv(rows, 4 * LN_FWD_RPW));
+#define LN_FWD32_LAUNCH(NV)                                                                                      \
+  hipLaunchKernelGGL((ln_fwd_kernel<NV, false, float>), grid, dim3(256), 0, stream, x, (const float*)nullptr,    \
+                     gamma, beta, reinterpret_cast<bf16_t*>(y), mean, rstd, rows, (int)D, (int)D, eps, 0.f,       \
+                     (uint64_t)0, (const float*)nullptr, (bf16_t*)nullptr)
+  switch (cdiv(D, 256)) {
+    case 1: LN_FWD32_LAUNCH(1); break;
+    case 2: LN_FWD32_LAUNCH(2); break;
+    case 3: LN_FWD32_LAUNCH(3); break;
+    default: LN_FWD32_LAUNCH(4); break;
+  }
+#undef LN_FWD32_LAUNCH
+  return check_launch("dph_layernorm_fwd_x32");
+}
+
+extern "C" int dph_layernorm_bwd_res32(const void* dy, const float* x, const float* gamma, const float* mean,
+                                       const float* rstd, float* dx, float* dgamma, float* dbeta, int64_t rows,
+                                       int64_t D, const float* dx_add, float* ws, int64_t ws_bytes,
+                                       hipStream_t stream) {
+  DPH_REQUIRE(dy && x && gamma && mean && rstd && dx, "dph_layernorm_bwd_res32: null pointer");
+  DPH_REQUIRE(D >= 1 && D % 4 == 0 && D <= LN_MAXV * 256 && rows > 0, "dph_layernorm_bwd_res32: unsupported D=%lld",
+              (long long)D);
+  const bool sums = dgamma || dbeta;
+  DPH_REQUIRE(!sums || (ws && ws_bytes >= dph_layernorm_bwd_workspace(rows, D)),
+              "dph_layernorm_bwd_res32: workspace too small (%lld < %lld bytes)", (long long)ws_bytes,
+              (long long)dph_layernorm_bwd_workspace(rows, D));
+  const dim3 grid((unsigned)cdiv(rows, LN_BWD_WAVES * LN_BWD_RPW));
+#define LN_BWDR_LAUNCH(NV)                                                                                       \
+  hipLaunchKernelGGL((ln_bwd_kernel<NV, float, float>), grid, dim3(64 * LN_BWD_WAVES), 0, stream,                \
+                     reinterpret_cast<const bf16_t*>(dy), x, (const float*)nullptr, gamma, mean, rstd, dx, dgamma, \
+                     dbeta, rows, (int)D, (int)D, 0.f, (uint64_t)0, (bf16_t*)nullptr, 0.f, (uint64_t)0,           \
+                     (const float*)nullptr, (float*)nullptr, (const bf16_t*)nullptr, (float*)nullptr, dx_add, ws)
+  switch (cdiv(D, 256)) {
+    case 1: LN_BWDR_LAUNCH(1); break;
+    case 2: LN_BWDR_LAUNCH(2); break;
+    case 3: LN_BWDR_LAUNCH(3); break;
+    default: LN_BWDR_LAUNCH(4); break;
+  }
+#undef LN_BWDR_LAUNCH
+  if (sums) {
+    const int64_t nblk = grid.x;
+    hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)cdiv(3 * D, 64), (unsigned)slab_groups(nblk)), dim3(256),
+                       0, stream, ws, nblk, 3 * D, D, dgamma, dbeta, (float*)nullptr);
+  }
+  return check_launch("dph_layernorm_bwd_res32");
 }
 
 extern "C" int dph_wave_layernorm(const float* x, const int64_t* lengths, int64_t B, int64_t S, float eps, float* y,

@@ -34,7 +34,7 @@ int check_launch(const char* what) {
 }  // namespace dph
 
 extern "C" const char* dph_last_error(void) { return dph::g_err; }
-extern "C" int dph_abi_version(void) { return 18; }
+extern "C" int dph_abi_version(void) { return 19; }
 
 // Point every kernel's RNG epoch at the device word `epoch` (uint64, device memory) on the current
 // device, or detach it (NULL: seeds are used as passed).  Not stream-ordered: call outside any

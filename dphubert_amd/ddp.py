@@ -18,7 +18,10 @@ NCCL).  Design for one 8x MI355X node:
 * ``comm_dtype=torch.bfloat16`` halves the payload on the links (191 MB
   instead of 382 MB per step): each bucket is cast to a persistent bf16 buffer right
   before its collective and cast back into the fp32 bucket after it; the optimizer
-  still reads fp32 gradients (masters and moments stay fp32).
+  still reads fp32 gradients (masters and moments stay fp32);
+* replicas start identical: ``broadcast_module`` sends rank 0's parameters and buffers at
+  trainer construction (DDP's construction-time broadcast), ``verify_replicas`` checks them
+  after a checkpoint load.
 """
 
 from typing import Iterable, List, Optional, Sequence
@@ -207,3 +210,61 @@ class GradReducer:
             for a in ("_dph_sink", "_dph_sink_ready"):
                 if hasattr(p, a):
                     delattr(p, a)
+
+
+# ---------------------------------------------------------------------------------------------
+# replica consistency (torch DDP's construction-time broadcast, distill.py:41 strategy="ddp")
+# ---------------------------------------------------------------------------------------------
+def _module_tensors(module: torch.nn.Module):
+    """(name, tensor) of every parameter and buffer, each storage once."""
+    seen, out = set(), []
+    for n, t in list(module.named_parameters()) + list(module.named_buffers()):
+        if t is None or t.data_ptr() in seen or t.numel() == 0:
+            continue
+        seen.add(t.data_ptr())
+        out.append((n, t))
+    return out
+
+
+def broadcast_module(module: torch.nn.Module, src: int = 0, process_group=None):
+    """Every parameter and buffer of ``module`` from rank ``src``: flattened per (device, dtype) into one buffer and
+    broadcast once each (a few large collectives, not one per tensor), then copied back in place under no_grad so
+    each parameter's version moves (the cached bf16 GEMM images, keyed by version, are rebuilt)."""
+    if not dist.is_initialized() or dist.get_world_size(process_group) == 1:
+        return
+    from torch._utils import _flatten_dense_tensors, _unflatten_dense_tensors
+    by = {}
+    for _, t in _module_tensors(module):
+        by.setdefault((t.device, t.dtype), []).append(t)
+    with torch.no_grad():
+        for ts in by.values():
+            flat = _flatten_dense_tensors([t.detach() for t in ts])
+            dist.broadcast(flat, src, group=process_group)
+            for t, v in zip(ts, _unflatten_dense_tensors(flat, ts)):
+                t.copy_(v)
+
+
+def replica_checksums(module: torch.nn.Module) -> torch.Tensor:
+    """[2 * n_tensors] fp64: per tensor its sum and a position-weighted sum (weights 1..97 cycling, so a permutation
+    or a shifted copy changes it)."""
+    vals = []
+    for _, t in _module_tensors(module):
+        x = t.detach().reshape(-1).double()
+        w = torch.arange(x.numel(), device=x.device, dtype=torch.float64).remainder_(97).add_(1.0)
+        vals.append(torch.stack([x.sum(), (x * w).sum()]))
+    return torch.cat(vals) if vals else torch.zeros(0, dtype=torch.float64)
+
+
+def verify_replicas(module: torch.nn.Module, process_group=None, rtol: float = 0.0):
+    """Raise on every rank if any parameter / buffer differs between ranks (checksums all-reduced MAX and MIN): after
+    a checkpoint load (cli --resume_checkpoint) every rank must hold rank 0's state."""
+    if not dist.is_initialized() or dist.get_world_size(process_group) == 1:
+        return
+    cs = replica_checksums(module)
+    hi, lo = cs.clone(), cs.clone()
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=process_group)
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=process_group)
+    bad = ((hi - lo).abs() > rtol * hi.abs()).reshape(-1, 2).any(1).nonzero().flatten().tolist()
+    if bad:
+        names = [n for n, _ in _module_tensors(module)]
+        raise RuntimeError(f"replicas differ across ranks in {len(bad)} tensors: {[names[i] for i in bad[:8]]}")

@@ -79,8 +79,19 @@ class LaunchProfiler:
 
     def __init__(self, by_shape: bool = False):
         self.records = []
-        self.keep = []             # events recorded into a graph without a record (kept alive with the graph)
+        # every event this profiler handed out.  Inside a capture each one becomes an event-record node of the graph,
+        # which hipGraphLaunch records on every replay: the event must outlive the graph.  A launch that fails after
+        # its first event was recorded (the grouped weight-gradient GEMM returning DPH_EUNSUPPORTED and falling back
+        # to per-layer launches) used to drop that event with its Python wrapper -> hipEventDestroy -> the next
+        # replay recorded a freed event and segfaulted on the host (round 3, gpurun_out/r3_s25).  Owned here, no
+        # event can be collected before the profiler (kept by Trainer with the profiled graph).
+        self.events = []
         self.by_shape = by_shape   # key the summary by (kernel, M, N, K, batch, splits) -- diagnostics
+
+    def event(self) -> "_Event":
+        e = _Event()
+        self.events.append(e)
+        return e
 
     def __enter__(self):
         LaunchProfiler.active = self
@@ -108,6 +119,7 @@ def _variant(args):
 
 GEMM_NO_PERSIST = 1            # DphGemmArgs.flags (include/dphubert_hip.h)
 GEMM_PRE_DGK = 2               # ACT_GELU: pre_out stores gelu'(pre)*colmask*keep/(1-p) (ACT_GELU_BWD_DGK's aux)
+GEMM_RESID_F32 = 4             # the residual is fp32 (the pre-norm residual stream); set from the tensor's dtype
 _SHARED_GPU = [0]
 
 
@@ -129,6 +141,8 @@ def gemm(A: DphMat, B: DphMat, Cm: DphMat, M: int, N: int, K: int, *, a_kcontig:
          colsum_out=None, colsum_aux=None, row_len=None, len_rows: int = 0, dropout_p: float = 0.0, seed: int = 0,
          drop_row_offset: int = 0, colsum_n: int = 0, device=None, flags: int = 0, dyn=None):
     """``dyn``: (int32 device tensor, offset) of a {m, n, k} device-side extent triplet (DphGemmArgs.dyn_ext)."""
+    if residual is not None and residual.dtype == F32:
+        flags |= GEMM_RESID_F32
     ws = None
     ws_bytes = 0
     if splits > 1:
@@ -151,7 +165,7 @@ def gemm(A: DphMat, B: DphMat, Cm: DphMat, M: int, N: int, K: int, *, a_kcontig:
                        (dyn[0].data_ptr() + 4 * dyn[1]) if dyn is not None else None)
     prof = LaunchProfiler.active
     if prof is not None:
-        e0, e1 = _Event(), _Event()
+        e0, e1 = prof.event(), prof.event()
         e0.record()
     call("dph_gemm", C.byref(args), _stream())
     if prof is not None:
@@ -199,7 +213,9 @@ def linear_fwd(x: torch.Tensor, w_bf16: torch.Tensor, bias: Optional[torch.Tenso
     M, K = x.shape
     N = w_bf16.shape[0]
     if out is None:
-        out = torch.empty(M, N, dtype=out_dtype, device=x.device)
+        # (an fp32 residual -- the pre-norm residual stream -- keeps its sum in fp32)
+        dt = F32 if (residual is not None and residual.dtype == F32) else out_dtype
+        out = torch.empty(M, N, dtype=dt, device=x.device)
     c_dtype = OUT_BF16 if out.dtype == BF16 else OUT_F32
     gemm(dense(x), dense(w_bf16), dense(out), M, N, K, a_kcontig=True, b_kcontig=True, c_dtype=c_dtype, act=act,
          bias=bias, colmask=colmask, smask=smask, pre_out=pre_out, residual=residual, dropout_p=dropout_p,
@@ -210,14 +226,15 @@ def linear_fwd(x: torch.Tensor, w_bf16: torch.Tensor, bias: Optional[torch.Tenso
 
 def linear_dgrad(dy: torch.Tensor, w_bf16: torch.Tensor, *, out=None, residual=None, act=ACT_NONE, aux_in=None,
                  colmask=None, colsum_out=None, colsum_aux=None, dropout_p=0.0, seed=0, colsum_n=0, w_t=None, dyn=None):
-    """dx = epi(dy @ w); dy [M,N] bf16, w [N,K] bf16 -> [M,K] bf16.
+    """dx = epi(dy @ w); dy [M,N] bf16, w [N,K] bf16 -> [M,K] bf16 (fp32 with an fp32 ``out`` / ``residual``).
 
     ``w_t``: the [K,N] transposed image of w (ops.t_image): both GEMM operands are then
     k-contiguous and the LDS-DMA ring kernels take the GEMM."""
     M, N = dy.shape
     K = w_bf16.shape[1]
     if out is None:
-        out = torch.empty(M, K, dtype=BF16, device=dy.device)
+        dt = F32 if (residual is not None and residual.dtype == F32) else BF16
+        out = torch.empty(M, K, dtype=dt, device=dy.device)
     if w_t is not None:
         if tuple(w_t.shape) != (K, N):
             raise ValueError(f"w_t must be [{K},{N}], got {tuple(w_t.shape)}")
@@ -225,6 +242,7 @@ def linear_dgrad(dy: torch.Tensor, w_bf16: torch.Tensor, *, out=None, residual=N
     else:
         B, bk = dense(w_bf16), False
     gemm(dense(dy), B, dense(out), M, K, N, a_kcontig=True, b_kcontig=bk, residual=residual, act=act,
+         c_dtype=OUT_BF16 if out.dtype == BF16 else OUT_F32,
          aux_in=aux_in, colmask=colmask, colsum_out=colsum_out, colsum_aux=colsum_aux, dropout_p=dropout_p,
          seed=seed, colsum_n=colsum_n, dyn=dyn)
     return out
@@ -286,12 +304,10 @@ def linear_wgrad_grouped(items: Sequence, accumulate: bool = True) -> Optional[t
         grp.a[i], grp.b[i], grp.c[i] = dy.data_ptr(), x.data_ptr(), dw.data_ptr()
     prof = LaunchProfiler.active
     if prof is not None:
-        e0, e1 = _Event(), _Event()
+        e0, e1 = prof.event(), prof.event()   # (owned by the profiler: e0 is recorded even if the launch falls back)
         e0.record()
     rc = _lib.lib().dph_gemm_grouped(C.byref(args), C.byref(grp), _stream())
     if rc == EUNSUPPORTED:
-        if prof is not None:
-            prof.keep.append(e0)   # (a captured event-record node refers to it)
         for dy, x, dw in items:
             linear_wgrad(dy, x, dw, accumulate=accumulate)
         return None

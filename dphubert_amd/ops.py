@@ -507,6 +507,24 @@ class grouped_wgrads:
             self._flush(key)
 
 
+def _flush_wgrads_hook(grad):
+    q = _WGRAD_DEFER[0]
+    if q is not None:
+        q.flush()
+    return None
+
+
+def mark_encoder_input(x: torch.Tensor) -> torch.Tensor:
+    """Hook the first encoder layer's input (Transformer._preprocess's output): its gradient is computed when the
+    encoder backward ends, and the hook launches the layer weight gradients still queued in a grouped_wgrads block
+    right then -- so every encoder bucket's collective is issued before the frontend backward (pos-conv, feature
+    projection, conv stack) instead of at the end of the whole backward when the group size does not divide the
+    layer count."""
+    if x.requires_grad:
+        x.register_hook(_flush_wgrads_hook)
+    return x
+
+
 def _layer_wgrad(dy, x, dw, direct, params, **kw):
     """An encoder layer's weight gradient: queued in the active grouped_wgrads block when it goes straight
     into the bucket (``direct``) at the operands' full width, else launched now (on the wgrad side stream
@@ -591,12 +609,21 @@ def _dev(t):
     return t.device
 
 
+# k_proj.bias gradient: mathematically exactly zero (below), so it is not computed by default.  The reference's
+# autograd evaluates it in floating point -- rounding noise of a sum that cancels to 0 -- and AdamW turns that noise
+# into +-lr steps, so a reference-trained checkpoint's k_proj.bias drifts where ours stays put (the model output is
+# unchanged either way).  DPH_KBIAS_GRAD=1 computes the column sum of dK as the reference does (checkpoint-matching
+# runs; its values are noise and are not parity-pinned).
+_KBIAS_GRAD = os.environ.get("DPH_KBIAS_GRAD", "0") == "1"
+
+
 def _qkv_bias_grad(dqkv, dbqkv, M, dev):
     """q / v bias gradients (+=) as column sums of dQ / dV; the k bias gradient is exactly zero (softmax shift
     invariance, components.py:411-417) and its slot of the fused [3*Dh] buffer is left untouched (zeroed)."""
     Dh = dqkv.shape[1] // 3
     base = dbqkv.data_ptr()
-    call("dph_colsum3", ptr(dqkv), base, None, base + 8 * Dh, M, Dh, *colsum_ws(M, 3 * Dh, dev), _s())
+    call("dph_colsum3", ptr(dqkv), base, base + 4 * Dh if _KBIAS_GRAD else None, base + 8 * Dh, M, Dh,
+         *colsum_ws(M, 3 * Dh, dev), _s())
 
 
 # ---------------------------------------------------------------------------
@@ -1316,21 +1343,27 @@ class PosConvFn(torch.autograd.Function):
         xg = torch.empty(B * G * Tp * Cg, dtype=BF16, device=dev)
         call("dph_regroup_pad", ptr(x), ptr(xg), B, T, G, Cg, P, Q, _s())
         need = cfg["need_grad"]
-        s0 = torch.empty_like(x)
+        ln = cfg.get("ln", True)
+        # pre-norm Transformer: s0 = x + pos_conv(x) starts the fp32 residual stream of the layers (EncoderLayerFn)
+        s0 = torch.empty_like(x) if ln else torch.empty(M, D, dtype=F32, device=dev)
         z = torch.empty_like(x) if need else None
         Cm = K.mat(s0, D, z_div=G, z_outer=T * D, z_inner=Cg)
         K.gemm(K.mat(xg, Cg, z_inner=Tp * Cg), K.mat(wk, Kk * Cg, z_div=G, z_outer=0, z_inner=Cg * Kk * Cg), Cm, T,
                Cg, Kk * Cg, a_kcontig=True, b_kcontig=True, batch=B * G, act=K.ACT_GELU, bias=bias, vec_z_inner=Cg,
-               pre_out=z, residual=x)
-        h = torch.empty_like(x)
+               pre_out=z, residual=x, c_dtype=K.OUT_BF16 if ln else K.OUT_F32)
         mu = torch.empty(M, dtype=F32, device=dev)
         rs = torch.empty(M, dtype=F32, device=dev)
         seed = SEEDS.next() if cfg["p"] > 0 else 0
-        if cfg.get("ln", True):
+        if ln:
+            h = torch.empty_like(x)
             call("dph_layernorm_fwd", ptr(s0), None, ptr(ln_w), ptr(ln_b), ptr(h), ptr(mu), ptr(rs), M, D, 1e-5,
                  cfg["p"], seed, _s())
-        else:   # pre-norm Transformer (components.py:1283 flag): no LayerNorm here, dropout only
-            call("dph_branch_bwd", ptr(s0), ptr(h), M, D, cfg["p"], seed, None, None, 0, None, None, None, _s())
+        elif cfg["p"] > 0:   # pre-norm Transformer (components.py:1283 flag): no LayerNorm here, dropout only
+            h = torch.empty(M, D, dtype=F32, device=dev)
+            call("dph_branch_bwd_f32", ptr(s0), ptr(h), 1, M, D, cfg["p"], seed, None, None, 0, None, None, None,
+                 _s())
+        else:
+            h = s0
         if need:
             ctx.cfg = cfg
             ctx.seed = seed
@@ -1348,7 +1381,7 @@ class PosConvFn(torch.autograd.Function):
         Cg = D // G
         dev = x.device
         dh = dh.contiguous()
-        ds0 = torch.empty_like(dh)
+        ds0 = torch.empty(M, D, dtype=BF16, device=dev)
         p_bias, p_lw, p_lb = ctx.params
         go = GradOut(dev)
         if cfg.get("ln", True):
@@ -1356,8 +1389,10 @@ class PosConvFn(torch.autograd.Function):
             dlb, _ = go.buf(p_lb)
             call("dph_layernorm_bwd", ptr(dh), ptr(s0), None, ptr(ln_w), ptr(mu), ptr(rs), ptr(ds0), ptr(dlw),
                  ptr(dlb), M, D, cfg["p"], ctx.seed, None, 0.0, 0, None, None, None, None, *ln_ws(M, D, dev), _s())
-        else:
-            call("dph_branch_bwd", ptr(dh), ptr(ds0), M, D, cfg["p"], ctx.seed, None, None, 0, None, None, None, _s())
+        else:   # (the fp32 residual stream's gradient)
+            dh = dh if dh.dtype == F32 else dh.float()
+            call("dph_branch_bwd_f32", ptr(dh), ptr(ds0), 0, M, D, cfg["p"], ctx.seed, None, None, 0, None, None,
+                 None, _s())
         dz = torch.empty_like(ds0)
         call("dph_gelu_mask_bwd", ptr(ds0), ptr(z), None, ptr(dz), None, M, D, _s())
         db, _ = go.buf(p_bias)
@@ -1425,8 +1460,10 @@ def _ffn_dgk(D: int) -> bool:
     """The FFN intermediate GELU backward from factors the forward stores (K.GEMM_PRE_DGK / K.ACT_GELU_BWD_DGK):
     the forward GEMM keeps gelu'(pre)*mask*keep/(1-p) instead of pre, so the input-gradient GEMM's epilogue is
     two multiplies (no erfc, no dropout hash; the mask gradient from the stored output f / mask).  Needs the
-    ping-pong GEMM layout (K = D a multiple of 64, >= 128); DPH_FFN_DGK=0 keeps the recomputing epilogue (A/B)."""
-    return D % 64 == 0 and D >= 128 and os.environ.get("DPH_FFN_DGK", "1") != "0"
+    ping-pong GEMM layout (K = D a multiple of 64, >= 128) for both operands k-contiguous -- so the transposed
+    weight images too (DPH_DGRAD_T=0 turns them off, and with them this path); DPH_FFN_DGK=0 keeps the recomputing
+    epilogue (A/B)."""
+    return _DGRAD_T and D % 64 == 0 and D >= 128 and os.environ.get("DPH_FFN_DGK", "1") != "0"
 
 
 def _ffn_interm_bwd(dy, sv, db1, dmask, cfg, F_):
@@ -1606,9 +1643,14 @@ class EncoderLayerFn(torch.autograd.Function):
     # ---------------- pre-norm (wav2vec2 / HuBERT Large, components.py:835-845) ----------------
     #   s1  = h + drop(attn(LN1(h))) * layer_mask_att
     #   out = s1 + FFN(LN2(s1)) * layer_mask_ffn        (no LayerNorm after the block)
+    # The residual stream h -> s1 -> out is fp32 (and so is its gradient): a bf16 stream takes two roundings per
+    # layer of an un-normalised sum (48 over wav2vec2-Large's 24 layers) -- the GEMM epilogues add the branch to the
+    # fp32 residual (DPH_GEMM_RESID_F32), the LayerNorms read it in fp32 and write the bf16 GEMM operand.
     @staticmethod
     def _forward_pre(ctx, cfg, h, wq, wk, wv, bq, bk, bv, wo, bo, ln1_w, ln1_b, w1, b1, w2, b2, ln2_w, ln2_b, hm,
                      lma, im, lmf):
+        if h.dtype != F32:
+            raise ValueError("pre-norm encoder layers carry the residual stream in fp32 (got %s)" % h.dtype)
         M, D = h.shape
         dev = h.device
         need = cfg["need_grad"]
@@ -1618,11 +1660,11 @@ class EncoderLayerFn(torch.autograd.Function):
         sv = {}
         xn1 = mu1 = rs1 = xn2 = mu2 = rs2 = None
         if use_att:
-            xn1 = torch.empty_like(h)
+            xn1 = torch.empty(M, D, dtype=BF16, device=dev)
             mu1 = torch.empty(M, dtype=F32, device=dev)
             rs1 = torch.empty(M, dtype=F32, device=dev)
-            call("dph_layernorm_fwd", ptr(h), None, ptr(ln1_w), ptr(ln1_b), ptr(xn1), ptr(mu1), ptr(rs1), M, D, 1e-5,
-                 0.0, 0, _s())
+            call("dph_layernorm_fwd_x32", ptr(h), ptr(ln1_w), ptr(ln1_b), ptr(xn1), ptr(mu1), ptr(rs1), M, D, 1e-5,
+                 _s())
             Dh = wq.shape[0]
             Wqkv = bf16_image(wq, wk, wv)
             qkv = K.linear_fwd(xn1, Wqkv, f32_cat(bq, bk, bv))
@@ -1635,16 +1677,16 @@ class EncoderLayerFn(torch.autograd.Function):
             seed_d = SEEDS.next() if cfg["p_drop"] > 0 else 0
             a_pre = torch.empty(M, D, dtype=BF16, device=dev) if (need and lma is not None) else None
             s1 = K.linear_fwd(o_m, Wo, bo, smask=lma, residual=h, dropout_p=cfg["p_drop"], seed=seed_d,
-                              pre_out=a_pre)
+                              pre_out=a_pre)                  # fp32 (fp32 residual)
             sv.update(Wqkv=Wqkv, qkv=qkv, o_u=o_u, o_m=o_m, lse=lse, Wo=Wo, a_pre=a_pre, seed_a=seed_a, seed_d=seed_d)
         else:
             s1 = h
         if use_ff:
-            xn2 = torch.empty_like(h)
+            xn2 = torch.empty(M, D, dtype=BF16, device=dev)
             mu2 = torch.empty(M, dtype=F32, device=dev)
             rs2 = torch.empty(M, dtype=F32, device=dev)
-            call("dph_layernorm_fwd", ptr(s1), None, ptr(ln2_w), ptr(ln2_b), ptr(xn2), ptr(mu2), ptr(rs2), M, D,
-                 1e-5, 0.0, 0, _s())
+            call("dph_layernorm_fwd_x32", ptr(s1), ptr(ln2_w), ptr(ln2_b), ptr(xn2), ptr(mu2), ptr(rs2), M, D, 1e-5,
+                 _s())
             out = _ffn_forward(cfg, xn2, w1, b1, w2, b2, im, lmf, s1, need, sv)
         else:
             out = s1.clone() if s1 is h else s1
@@ -1668,35 +1710,36 @@ class EncoderLayerFn(torch.autograd.Function):
         M, D = h.shape
         dev = h.device
         dout = dout.contiguous()
+        if dout.dtype != F32:
+            dout = dout.float()
         z = lambda n: zeros_f32(n, dev)  # noqa: E731
         pr = ctx.params
         go = GradOut(dev)
         g = {}
-        # ---- FFN branch: out = s1 + drop(FFN(LN2(s1))) * lmf ----
+        # ---- FFN branch: out = s1 + drop(FFN(LN2(s1))) * lmf  (dout, ds1: fp32 residual-stream gradients) ----
         if use_ff:
-            dy = torch.empty_like(dout)
+            dy = torch.empty(M, D, dtype=BF16, device=dev)
             db2, _ = go.buf(pr["b2"])
             g["lmf"] = z(1) if has_lmf else None
-            call("dph_branch_bwd", ptr(dout), ptr(dy), M, D, cfg["p_drop"], sv["seed_o"], ptr(lmf), None, 0, ptr(db2),
-                 ptr(sv["y_pre"]) if has_lmf else None, ptr(g["lmf"]), _s())
+            call("dph_branch_bwd_f32", ptr(dout), ptr(dy), 0, M, D, cfg["p_drop"], sv["seed_o"], ptr(lmf), None, 0,
+                 ptr(db2), ptr(sv["y_pre"]) if has_lmf else None, ptr(g["lmf"]), _s())
             F_ = sv["F"]
             g["im"] = z(F_) if has_im else None
             dxn2 = _ffn_backward(cfg, sv, dy, xn2, pr, go, g["im"] if has_im else z(F_))
-            ds1 = torch.empty_like(dout)
+            ds1 = torch.empty(M, D, dtype=F32, device=dev)
             dln2w, _ = go.buf(pr["ln2_w"])
             dln2b, _ = go.buf(pr["ln2_b"])
-            call("dph_layernorm_bwd_ld", ptr(dxn2), ptr(s1), None, ptr(ln2_w), ptr(mu2), ptr(rs2), ptr(ds1),
-                 ptr(dln2w), ptr(dln2b), M, D, D, 0.0, 0, None, 0.0, 0, None, None, None, None, ptr(dout),
-                 *ln_ws(M, D, dev), _s())
+            call("dph_layernorm_bwd_res32", ptr(dxn2), ptr(s1), ptr(ln2_w), ptr(mu2), ptr(rs2), ptr(ds1), ptr(dln2w),
+                 ptr(dln2b), M, D, ptr(dout), *ln_ws(M, D, dev), _s())
         else:
             ds1 = dout
         # ---- attention branch: s1 = h + drop(attn(LN1(h))) * lma ----
         if use_att:
-            da = torch.empty_like(dout)
+            da = torch.empty(M, D, dtype=BF16, device=dev)
             dbo, _ = go.buf(pr["bo"])
             g["lma"] = z(1) if has_lma else None
-            call("dph_branch_bwd", ptr(ds1), ptr(da), M, D, cfg["p_drop"], sv["seed_d"], ptr(lma), None, 0, ptr(dbo),
-                 ptr(sv["a_pre"]) if has_lma else None, ptr(g["lma"]), _s())
+            call("dph_branch_bwd_f32", ptr(ds1), ptr(da), 0, M, D, cfg["p_drop"], sv["seed_d"], ptr(lma), None, 0,
+                 ptr(dbo), ptr(sv["a_pre"]) if has_lma else None, ptr(g["lma"]), _s())
             dwo, direct = go.buf(pr["wo"], zero=False)
             k3 = _layer_wgrad(da, sv["o_m"], dwo, direct, (pr["wo"],))
             do_m = K.linear_dgrad(da, sv["Wo"], w_t=t_image(sv["Wo"]))
@@ -1711,12 +1754,11 @@ class EncoderLayerFn(torch.autograd.Function):
             k4 = _layer_wgrad(dqkv, xn1, dwqkv, direct, (pr["wq"], pr["wk"], pr["wv"]))
             dxn1 = K.linear_dgrad(dqkv, sv["Wqkv"], w_t=t_image(sv["Wqkv"]))
             EncoderLayerFn._gate_bwd(ctx, cfg, xn1, dxn1, wl_g, go)
-            dh = torch.empty_like(dout)
+            dh = torch.empty(M, D, dtype=F32, device=dev)
             dln1w, _ = go.buf(pr["ln1_w"])
             dln1b, _ = go.buf(pr["ln1_b"])
-            call("dph_layernorm_bwd_ld", ptr(dxn1), ptr(h), None, ptr(ln1_w), ptr(mu1), ptr(rs1), ptr(dh),
-                 ptr(dln1w), ptr(dln1b), M, D, D, 0.0, 0, None, 0.0, 0, None, None, None, None, ptr(ds1),
-                 *ln_ws(M, D, dev), _s())
+            call("dph_layernorm_bwd_res32", ptr(dxn1), ptr(h), ptr(ln1_w), ptr(mu1), ptr(rs1), ptr(dh), ptr(dln1w),
+                 ptr(dln1b), M, D, ptr(ds1), *ln_ws(M, D, dev), _s())
             del k3, k4
         else:
             dh = ds1
@@ -1872,11 +1914,30 @@ class EncoderLayerFn(torch.autograd.Function):
 # ---------------------------------------------------------------------------
 # Distill projections + DistillLoss (fused)
 # ---------------------------------------------------------------------------
+def _bf16_rows(xs):
+    """bf16 copies of the fp32 tensors of ``xs`` (one per distinct tensor; bf16 ones pass through)."""
+    done = {}
+    out = []
+    for x in xs:
+        if x.dtype == BF16:
+            out.append(x)
+            continue
+        if id(x) not in done:
+            y = torch.empty(x.shape, dtype=BF16, device=x.device)
+            call("dph_cast_bf16", ptr(x.contiguous()), ptr(y), x.numel(), _s())
+            done[id(x)] = y
+        out.append(done[id(x)])
+    return out
+
+
 class DistillProjLossFn(torch.autograd.Function):
     """student hidden list -> per-layer Linear (shared per group) -> loss terms.
 
     args: cfg, then L student hiddens (B*T, Ds) bf16, then P projection (weight, bias) pairs,
     then L teacher hiddens (B*T, Dt) bf16.  Returns (loss, mse, l1, cos) 0-d fp32.
+    Hiddens of pre-norm encoders are the fp32 residual stream (EncoderLayerFn._forward_pre): the student's are
+    rounded to bf16 once here (the projection GEMM's operand) and their gradients are fp32; the loss kernel reads
+    the teacher's in fp32.
     """
 
     @staticmethod
@@ -1889,6 +1950,10 @@ class DistillProjLossFn(torch.autograd.Function):
         M, Ds = sh[0].shape
         Dt = pw[0].shape[0]
         dev = sh[0].device
+        ctx.in_f32 = [x.dtype == F32 for x in sh]
+        sh = _bf16_rows(sh)          # (the projection GEMM's operand; the teacher rows are read in their dtype)
+        tmask = sum(1 << l for l, t in enumerate(th) if t.dtype == F32)
+        ctx.tmask = tmask
         s = torch.empty(L, M, Dt, dtype=F32, device=dev)
         imgs = [bf16_image(pw[2 * p]) for p in range(P)]
         # predlayer heads (distill.py:100-107): Linear + exact-erf GELU in the GEMM epilogue, the pre-activation
@@ -1905,7 +1970,7 @@ class DistillProjLossFn(torch.autograd.Function):
         partial = torch.empty(LOSS_PARTIAL_FLOATS, dtype=F32, device=dev)
         out = torch.empty(4, dtype=F32, device=dev)
         tptrs = (_lib.C.c_void_p * L)(*[t.data_ptr() for t in th])
-        call("dph_distill_loss_fwd", ptr(s), tptrs, B, L, T, Dt, cfg["l2"], cfg["l1"], cfg["cos"],
+        call("dph_distill_loss_fwd_ex", ptr(s), tptrs, tmask, B, L, T, Dt, cfg["l2"], cfg["l1"], cfg["cos"],
              int(cfg["cos_type"] == "log_sig"), ptr(rowstats), ptr(partial), ptr(out), _s())
         ctx.cfg = cfg
         ctx.params = pw
@@ -1928,8 +1993,8 @@ class DistillProjLossFn(torch.autograd.Function):
         ds = torch.empty(L, M, Dt, dtype=BF16, device=dev)
         tptrs = (_lib.C.c_void_p * L)(*[t.data_ptr() for t in th])
         dl = dloss.contiguous() if dloss is not None else torch.ones((), dtype=F32, device=dev)
-        call("dph_distill_loss_bwd", ptr(s), tptrs, ptr(rowstats), ptr(dl), B, L, T, Dt, cfg["l2"], cfg["l1"],
-             cfg["cos"], int(cfg["cos_type"] == "log_sig"), ptr(ds), _s())
+        call("dph_distill_loss_bwd_ex", ptr(s), tptrs, ctx.tmask, ptr(rowstats), ptr(dl), B, L, T, Dt, cfg["l2"],
+             cfg["l1"], cfg["cos"], int(cfg["cos_type"] == "log_sig"), ptr(ds), _s())
         go = GradOut(dev)
         pw = ctx.params
         dW = [go.buf(pw[2 * p])[0] for p in range(P)]
@@ -1947,10 +2012,11 @@ class DistillProjLossFn(torch.autograd.Function):
             p = cfg["proj_index"][l]
             keep.append(K.linear_wgrad(ds[l], sh[l], dW[p], accumulate=True))
             call("dph_colsum", ptr(ds[l]), ptr(db[p]), M, Dt, *colsum_ws(M, Dt, dev), _s())
+            o = torch.empty(M, Ds, dtype=F32, device=dev) if ctx.in_f32[l] else None
             if shared:
-                acc = K.linear_dgrad(ds[l], imgs[p], w_t=t_image(imgs[p]), residual=acc)
+                acc = K.linear_dgrad(ds[l], imgs[p], w_t=t_image(imgs[p]), residual=acc, out=o if acc is None else None)
             else:
-                dh.append(K.linear_dgrad(ds[l], imgs[p], w_t=t_image(imgs[p])))
+                dh.append(K.linear_dgrad(ds[l], imgs[p], w_t=t_image(imgs[p]), out=o))
         if shared:
             dh = [acc] + [None] * (L - 1)
         go.done()

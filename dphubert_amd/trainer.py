@@ -116,6 +116,105 @@ def fused_grad_groups(model) -> List[tuple]:
     return groups
 
 
+# ---- weight-gradient group plan at world size > 1 ---------------------------------------------------------------
+# Measured on one MI355X (profiles/r3_s29 kernel trace, one replayed step at B = 16 x 10 s = 7984 frames, HuBERT-Base
+# with 7 087 872 parameters per encoder layer): the encoder backward without its weight gradients 4.2 ms for 12 layers;
+# the grouped weight-gradient GEMMs 2.0 ms for 12 layers at 12 per launch, +0.30 / +0.46 / +0.49 / +1.39 ms at groups
+# of 6 / 4 / 3 / 1 (profiles/r3_s26_*, r3_s27_*); the conv-frontend backward (pos-conv .. conv0) 3.9 ms.
+WG_FRAMES = 7984
+WG_LAYER_PARAMS = 7087872
+WG_T_LAYER_MS = 4.2 / 12
+WG_WGRAD_MS = {1: 3.39, 2: 2.9, 3: 2.49, 4: 2.46, 6: 2.30, 8: 2.2, 12: 2.0, 16: 2.0}   # per 12 layers, by group
+WG_FRONTEND_MS = 3.9
+XGMI_BUS_GBPS = 150.0   # ring all-reduce bus bandwidth of one xGMI ring (382 MB in ~4.4 ms at N = 8)
+
+
+def grad_ready_times(model, frames: float, group: int, proj_params=()):
+    """Predicted gradient-ready time (ms from the start of the encoder backward) of every student parameter with the
+    encoder layers' weight gradients launched ``group`` layers at a time (ops.grouped_wgrads, flushed at the
+    encoder's end too), from the measured per-layer costs above scaled by the frames and by each layer's parameter
+    count.  Returns (ready {id(param): ms}, encoder end, backward end)."""
+    sc = frames / WG_FRAMES
+    layers = list(model.encoder.transformer.layers)
+    L = len(layers)
+    wg = WG_WGRAD_MS[max(k for k in WG_WGRAD_MS if k <= max(1, group))] / 12.0
+    ready = {}
+    t, queue = 0.0, []
+    for li in reversed(range(L)):
+        lay = layers[li]
+        r = sum(p.numel() for n, p in lay.named_parameters() if "log_alpha" not in n) / WG_LAYER_PARAMS
+        t += WG_T_LAYER_MS * sc * r
+        deferred = []
+        for n, p in lay.named_parameters():
+            if "log_alpha" in n:
+                continue
+            if p.dim() == 2 and ("attention" in n or "feed_forward" in n):
+                deferred.append(p)
+            else:
+                ready[id(p)] = t
+        queue.append((r, deferred))
+        if len(queue) >= group or li == 0:
+            t += sum(wg * sc * rr for rr, _ in queue)
+            for _, ds in queue:
+                for p in ds:
+                    ready[id(p)] = t
+            queue = []
+    t_enc = t
+    t_end = t_enc + WG_FRONTEND_MS * sc
+    for n, p in model.named_parameters():
+        if id(p) in ready:
+            continue
+        # encoder-level (pos-conv, its LayerNorm, feature projection): early in the frontend window; conv stack,
+        # HardConcrete logits (one bank backward at the end): at its end
+        early = n.startswith("encoder.") and "log_alpha" not in n
+        ready[id(p)] = t_enc + 0.1 * WG_FRONTEND_MS * sc if early else t_end
+    for p in proj_params:
+        ready[id(p)] = 0.0
+    return ready, t_enc, t_end
+
+
+def wgrad_group_timeline(model, buckets, world: int, frames: float, group: int, bus_gbps: float = XGMI_BUS_GBPS,
+                         comm_bytes: int = 4, proj_params=()):
+    """Predicted backward of one optimizer step (grad_ready_times): each bucket's ring all-reduce -- 2 (N-1)/N x its
+    bytes at ``bus_gbps`` -- starts when its last gradient is ready and after the previous collective (one RCCL
+    stream).  Returns (compute end, last collective's end) in ms."""
+    ready, _, t_end = grad_ready_times(model, frames, group, proj_params)
+    comm_end = 0.0
+    f = 2.0 * (world - 1) / world
+    for rt, n in sorted((max(ready.get(id(p), t_end) for p in b), sum(p.numel() for p in b)) for b in buckets):
+        comm_end = max(comm_end, rt) + f * n * comm_bytes / (bus_gbps * 1e6)
+    return t_end, comm_end
+
+
+def grad_ready_order(module, params):
+    """``params`` in predicted gradient-ready order (grad_ready_times at the bench shape, B = 16 x 10 s): the
+    buckets then fill in the order the backward produces them -- distill projections first, encoder layers last to
+    first, the frontend, and the HardConcrete logits and Lagrange multipliers (whose gradients land at the very end
+    of the backward) in the last bucket instead of the first."""
+    proj = list(module.distill_linear_projs.parameters())
+    ready, _, t_end = grad_ready_times(module.student_model, WG_FRAMES, 12, proj)
+    idx = {id(p): i for i, p in enumerate(params)}
+    return sorted(params, key=lambda p: (ready.get(id(p), t_end + 1.0), idx[id(p)]))
+
+
+def plan_wgrad_group(model, buckets, world: int, frames: float, bus_gbps: float = XGMI_BUS_GBPS,
+                     comm_bytes: int = 4, proj_params=()) -> int:
+    """The group size (layers per grouped weight-gradient launch) that minimises the predicted step end
+    max(compute end, last collective end) of wgrad_group_timeline; the largest group on ties and at world size 1."""
+    from . import _lib
+    L = len(model.encoder.transformer.layers)
+    cands = [g for g in sorted(WG_WGRAD_MS) if g <= min(L, _lib.GEMM_GROUP_MAX)] or [1]
+    if world <= 1:
+        return cands[-1]
+    best, best_t = cands[-1], None
+    for g in reversed(cands):
+        te, ce = wgrad_group_timeline(model, buckets, world, frames, g, bus_gbps, comm_bytes, proj_params)
+        t = max(te, ce)
+        if best_t is None or t < best_t - 1e-9:
+            best, best_t = g, t
+    return best
+
+
 class Trainer:
     """One process per GPU; call ``step(batch)`` per micro-batch (optimizer update every
     ``accum_grad`` calls).
@@ -136,6 +235,8 @@ class Trainer:
         self.optimizer = opt["optimizer"]
         self.scheduler = opt["lr_scheduler"]["scheduler"]
         params = [p for g in self.optimizer.param_groups for p in g["params"]]
+        # (GradReducer fills its buckets in reverse registration order: hand it the reverse of the ready order)
+        params = list(reversed(grad_ready_order(module, params)))
         self.reducer = GradReducer(params, bucket_mb=bucket_mb, groups=fused_grad_groups(module.student_model),
                                    comm_dtype=grad_dtype)
         if accum_grad < 1:
@@ -152,6 +253,8 @@ class Trainer:
         self._prof_loss = None
         self._prof = None
         self._logged_of = {}             # id(graph) -> the module.logged dict its capture produced
+        self._ffn_at = None              # global step of the last FFN compaction decision
+        self._eager_until = 0            # optimizer steps before this global step run eagerly (after a layout change)
         self.scalars = None
         # teacher forward on a side stream (DPH_TEACHER_STREAM=0 keeps one stream)
         if os.environ.get("DPH_TEACHER_STREAM", "1") != "0" and torch.cuda.is_available() and \
@@ -166,9 +269,18 @@ class Trainer:
             self._wgrad_stream = torch.cuda.Stream()
         # encoder-layer weight gradients launched this many layers at a time as one grouped GEMM (12: the whole
         # HuBERT-Base encoder in one launch per layer kind, 19.28 ms per step against 19.58 at 6, 19.74 at 4 and
-        # 20.67 ungrouped, profiles/r3_s27_*; the buckets' collectives then overlap the conv-frontend backward)
-        # (ops.grouped_wgrads; DPH_WGRAD_GROUP=1 keeps one launch per layer)
-        self.wgrad_group = int(os.environ.get("DPH_WGRAD_GROUP", "12"))
+        # 20.67 ungrouped, profiles/r3_s27_*) (ops.grouped_wgrads; DPH_WGRAD_GROUP=1 keeps one launch per layer).
+        # At world size > 1 the group is planned at the first step from the measured backward costs against the
+        # buckets' all-reduce time over xGMI (plan_wgrad_group; DPH_XGMI_BUS_GBPS overrides the link rate), unless
+        # DPH_WGRAD_GROUP fixes it.
+        env_group = os.environ.get("DPH_WGRAD_GROUP")
+        self.wgrad_group = int(env_group) if env_group else 12
+        self._plan_group = env_group is None and self.reducer.world > 1
+        self.wgrad_plan = None
+        # replicas start from rank 0's parameters and buffers (torch DDP broadcasts at construction, distill.py:41)
+        if self.reducer.world > 1:
+            from .ddp import broadcast_module
+            broadcast_module(module, process_group=self.reducer.group)
 
     @property
     def _graph(self):
@@ -308,21 +420,48 @@ class Trainer:
                 changed = True
         return changed
 
+    def verify_replicas(self):
+        """Raise if any parameter / buffer differs across ranks (after a checkpoint load: cli --resume_checkpoint)."""
+        from .ddp import verify_replicas
+        verify_replicas(self.module, process_group=self.reducer.group)
+
+    def _plan(self, batch):
+        """World size > 1: the weight-gradient group from the step's frames (B x ~S / 320) and the bucket layout."""
+        self._plan_group = False
+        frames = batch[0].shape[0] * batch[0].shape[1] / 320.0
+        proj = list(self.module.distill_linear_projs.parameters())
+        bus = float(os.environ.get("DPH_XGMI_BUS_GBPS", XGMI_BUS_GBPS))
+        cb = 2 if self.reducer.comm_dtype == torch.bfloat16 else 4
+        self.wgrad_group = plan_wgrad_group(self.module.student_model, self.reducer.buckets, self.reducer.world,
+                                            frames, bus, cb, proj)
+        self.wgrad_plan = {"group": self.wgrad_group, "world": self.reducer.world, "frames": frames, "bus_gbps": bus,
+                           "timeline_ms": wgrad_group_timeline(self.module.student_model, self.reducer.buckets,
+                                                               self.reducer.world, frames, self.wgrad_group, bus, cb,
+                                                               proj)}
+
     # ---- one step ----------------------------------------------------------------------------
     def step(self, batch, profiled: bool = False):
         m = self.module
         m.train()
-        if self._micro == 0 and (not self._graphs or m.global_step % self.FFN_COMPACT_EVERY == 0):
+        if self._plan_group:
+            self._plan(batch)
+        # FFN compaction policy: at the first step and every FFN_COMPACT_EVERY optimizer steps after it, eager or
+        # replayed alike (one host read of the gates' expected counts: not on every eager step)
+        if self._micro == 0 and (self._ffn_at is None or m.global_step - self._ffn_at >= self.FFN_COMPACT_EVERY):
+            self._ffn_at = m.global_step
             if self.refresh_ffn_compaction() and self._graphs:
-                self._graphs = {}            # recaptured at this step with the new FFN layouts
+                # stale graphs: this optimizer step runs eagerly in the new FFN layouts (their packed buffers and
+                # cached images are built outside any capture), the next one recaptures
+                self._graphs = {}
                 self._prof_graph = None
+                self._eager_until = m.global_step + 1
         dev = batch[0].device
         zero = self._micro == 0
         final = self._micro + 1 == self.accum_grad
         adam_step = self.optimizer.begin_step() if final else self.optimizer._step + 1
         self._upload(dev, adam_step)
         loss = None
-        if self.graphs and self._n_eager >= self.graph_warmup:
+        if self.graphs and self._n_eager >= self.graph_warmup and m.global_step >= self._eager_until:
             self._set_static(batch)
             key = (zero, final)
             if key not in self._graphs:
@@ -334,6 +473,9 @@ class Trainer:
                     self._graphs = {}
             if key in self._graphs:
                 if profiled and final and self._prof_graph is not None:
+                    # the profiled graph's event-record nodes refer to the profiler's events (LaunchProfiler.events)
+                    if self._prof is None or not self._prof.events:
+                        raise RuntimeError("profiled graph without its LaunchProfiler: its events would be freed")
                     g, loss = self._prof_graph, self._prof_loss
                 else:
                     g, loss = self._graphs[key]

@@ -577,7 +577,7 @@ class Transformer(Module):
 
     def forward(self, x: Tensor, attention_mask=None, position_bias=None, key_len=None) -> Tensor:
         import random
-        x = self._preprocess(x)
+        x = ops.mark_encoder_input(self._preprocess(x))
         for layer in self.layers:
             if not (self.training and random.random() <= self.layer_drop):
                 x, position_bias = layer(x, attention_mask, position_bias=position_bias, key_len=key_len)
@@ -592,7 +592,7 @@ class Transformer(Module):
             if not 0 < num_layers <= len(self.layers):
                 raise ValueError(f"`num_layers` must be between [1, {len(self.layers)}]")
         ret: List[Tensor] = []
-        x = self._preprocess(x)
+        x = ops.mark_encoder_input(self._preprocess(x))
         for layer in self.layers:
             x, position_bias = layer(x, attention_mask, position_bias=position_bias, key_len=key_len)
             ret.append(x)

@@ -84,7 +84,8 @@ class Wav2Vec2Model(Module):
 
     def extract_features(self, waveforms: Tensor, lengths: Optional[Tensor] = None,
                          num_layers: Optional[int] = None) -> Tuple[List[Tensor], Optional[Tensor]]:
-        """model.py:57-107.  Returns the N+1 hidden states (B, T, D) (bf16) and the frame lengths."""
+        """model.py:57-107.  Returns the N+1 hidden states (B, T, D) and the frame lengths: bf16, and fp32 for the
+        layers of a pre-norm encoder (its residual stream, ops.EncoderLayerFn._forward_pre)."""
         if self.normalize_waveform:
             waveforms = self._normalize(waveforms, lengths)
         self._sample_gates()
@@ -161,9 +162,9 @@ class Wav2Vec2Model(Module):
 
 def wav2vec2_model(**configs) -> Wav2Vec2Model:
     """Wraps the original wav2vec2_model (model.py:172-178)."""
-    if "encoder_remaining_heads" in configs:
-        return wavlm_model(**configs)
-    return wav2vec2_model_original(**configs)
+    m = wavlm_model(**configs) if "encoder_remaining_heads" in configs else wav2vec2_model_original(**configs)
+    m.dph_config = dict(configs)       # (its FLOP / byte accounting in the training log: perfmodel)
+    return m
 
 
 def wavlm_model(

@@ -111,6 +111,10 @@ typedef struct DphGemmArgs {
 /* DPH_ACT_GELU with pre_out: store gelu'(pre)*colmask*keep/(1-p) instead of pre (the aux input of the
  * matching DPH_ACT_GELU_BWD_DGK input-gradient GEMM).  Ping-pong layouts only. */
 #define DPH_GEMM_PRE_DGK 2
+/* residual is fp32 (same element layout as C): the pre-norm residual stream x + f(LN(x)) carried in fp32 across
+ * the layers (components.py:846, :850), whose 2 x L bf16 roundings would otherwise accumulate.  Forward epilogues
+ * only (not with DPH_ACT_GELU_BWD / _DGK). */
+#define DPH_GEMM_RESID_F32 4
 
 int dph_gemm(const DphGemmArgs* args, hipStream_t stream);
 /* Grouped (mn, mn) weight gradients: n <= DPH_GEMM_GROUP_MAX independent dW_i (+)= dY_i^T X_i of ONE shape in one
@@ -209,6 +213,15 @@ int dph_layernorm_bwd_ld(const void* dy, const void* x, const float* xscale, con
                          float dropout_p, uint64_t seed, void* branch, float branch_p, uint64_t branch_seed,
                          const float* branch_smask, float* branch_colsum, const void* branch_pre, float* branch_sdot,
                          const void* dx_add, float* ws, int64_t ws_bytes, hipStream_t stream);
+/* pre-norm residual stream in fp32 (components.py:835-850: x + attn(LN(x)), x + FFN(LN(x)) carried across the layers
+ * without a bf16 rounding per add): LN forward of an fp32 x (y bf16: the next GEMM's operand), and the LN backward
+ * whose input gradient is the fp32 stream's: dx (fp32) = LN backward of dy (bf16) + dx_add (fp32, optional: the
+ * residual path's gradient); dgamma / dbeta accumulate (ws: dph_layernorm_bwd_workspace bytes). */
+int dph_layernorm_fwd_x32(const float* x, const float* gamma, const float* beta, void* y, float* mean, float* rstd,
+                          int64_t rows, int64_t D, float eps, hipStream_t stream);
+int dph_layernorm_bwd_res32(const void* dy, const float* x, const float* gamma, const float* mean, const float* rstd,
+                            float* dx, float* dgamma, float* dbeta, int64_t rows, int64_t D, const float* dx_add,
+                            float* ws, int64_t ws_bytes, hipStream_t stream);
 /* per-utterance waveform LayerNorm, model.py:96-103 (normalize_waveform, wav2vec2-Large):
  * y[b][:len_b] = (x - mean) / sqrt(var + eps) over the first len_b samples, y[b][len_b:] = 0
  * (lengths == NULL: full rows) */
@@ -370,6 +383,11 @@ int dph_conv_weight_unpack_grad(const float* g, float* dst, int64_t O, int64_t C
 int dph_branch_bwd(const void* dy, void* out, int64_t rows, int64_t cols, float p, uint64_t seed, const float* smask,
                    const int64_t* row_len, int64_t len_rows, float* colsum, const void* pre, float* sdot,
                    hipStream_t stream);
+/* the same with an fp32 dy (the pre-norm residual stream's gradient); out is bf16, or fp32 when out_f32 (the
+ * pre-norm pos-conv output's dropout, components.py:891, forward) */
+int dph_branch_bwd_f32(const float* dy, void* out, int out_f32, int64_t rows, int64_t cols, float p, uint64_t seed,
+                       const float* smask, const int64_t* row_len, int64_t len_rows, float* colsum, const void* pre,
+                       float* sdot, hipStream_t stream);
 /* bf16 -> f32 copy / accumulate helpers */
 int dph_add_bf16(const void* a, const void* b, void* out, int64_t n, hipStream_t stream);
 
@@ -392,6 +410,15 @@ int dph_distill_loss_fwd(const float* s, const void* const* t_layers, int64_t B,
 int dph_distill_loss_bwd(const float* s, const void* const* t_layers, const float* rowstats, const float* dloss,
                          int64_t B, int64_t L, int64_t T, int64_t D, float l2w, float l1w, float cosw,
                          int cos_logsig, void* ds, hipStream_t stream);
+
+/* the same with per-layer teacher dtypes: layer l is fp32 when bit l of t_f32_mask is set, else bf16 (the
+ * hiddens of pre-norm encoders are their fp32 residual stream, components.py:846-850: read unrounded) */
+int dph_distill_loss_fwd_ex(const float* s, const void* const* t_layers, uint32_t t_f32_mask, int64_t B, int64_t L,
+                            int64_t T, int64_t D, float l2w, float l1w, float cosw, int cos_logsig, float* rowstats,
+                            float* partial, float* out, hipStream_t stream);
+int dph_distill_loss_bwd_ex(const float* s, const void* const* t_layers, uint32_t t_f32_mask, const float* rowstats,
+                            const float* dloss, int64_t B, int64_t L, int64_t T, int64_t D, float l2w, float l1w,
+                            float cosw, int cos_logsig, void* ds, hipStream_t stream);
 
 /* Lagrangian sparsity regulariser and total loss (lightning.py:221-229, DistillModule._step):
  * es = 1 - num/orig_params, d = es - target, reg = lambda1*d + lambda2*d^2, out[0..2] = distill + reg,

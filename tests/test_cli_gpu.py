@@ -2,6 +2,7 @@
 final_distill.py -> save_final_ckpt.py, each as its own process with the reference's flags, on a 2-layer
 HuBERT-Base-width model and a 16 kHz WAV manifest in prepare_data.py's tsv format (scipy-written files)."""
 import copy
+import json
 import os
 import subprocess
 import sys
@@ -52,6 +53,11 @@ def test_distill_prune_final_distill_save(tmp_path):
     assert ck.exists()
     state = torch.load(ck, map_location="cpu", weights_only=True)
     assert state["global_step"] == 3
+    # the reference's log keys (lightning.py:277-295) plus the roofline keys of SURVEY 2 "Metrics / logging"
+    recs = [json.loads(x) for x in (exp / "log.jsonl").read_text().splitlines() if x.strip()]
+    train = [r for r in recs if "train_loss" in r]
+    assert train and all(0.0 < r["mfma_util"] < 1.0 and r["hbm_gbps"] > 0.0 and "audio_s_per_s" in r
+                         for r in train), train
     _run(["prune.py", "--distilled_ckpt", ck, "--original_ckpt", teacher])
     pruned = exp / "ckpts" / "pruned_hubert_base.pth"
     pk = torch.load(pruned, map_location="cpu", weights_only=True)

@@ -220,3 +220,163 @@ def test_bucket_units_16_byte_aligned():
     o = [red.offsets[id(p)] for p in ps[4:7]]
     assert red.bucket_of[id(ps[4])] == red.bucket_of[id(ps[6])] and o[1] == o[0] + 12 and o[2] == o[1] + 12
     red.remove()
+
+
+# ---------------------------------------------------------------------------------------------
+# the comm window: encoder buckets' collectives before the frontend backward
+# ---------------------------------------------------------------------------------------------
+_EVENTS = []
+
+
+class FrontLinear(SinkLinear):
+    """The 'frontend' below the encoder: its backward start is recorded."""
+
+    @staticmethod
+    def backward(ctx, dy):
+        _EVENTS.append(("frontend",))
+        return SinkLinear.backward(ctx, dy)
+
+
+class Stack(torch.nn.Module):
+    """frontend -> ops.mark_encoder_input -> 12 'encoder layers' whose weight gradients are deferred (DeferLinear)."""
+
+    def __init__(self, n_layers=12):
+        super().__init__()
+        g = torch.Generator().manual_seed(1)
+        self.front = torch.nn.Linear(6, 8)
+        self.layers = torch.nn.ModuleList([torch.nn.Linear(8, 8) for _ in range(n_layers)])
+        for p in self.parameters():
+            with torch.no_grad():
+                p.copy_(torch.randn(p.shape, generator=g) * 0.5)
+
+    def forward(self, x):
+        from dphubert_amd import ops
+        h = ops.mark_encoder_input(FrontLinear.apply(x, self.front.weight, self.front.bias))
+        for lay in self.layers:
+            h = torch.tanh(DeferLinear.apply(h, lay.weight, lay.bias))
+        return (h ** 2).mean()
+
+
+def _window_worker(rank, world, port, group, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from dphubert_amd import ops
+        ops.K.linear_wgrad_grouped = _cpu_grouped
+        net = Stack()
+        # one bucket per layer (8x8 + 8 floats = 288 B): each layer's collective is its own event
+        red = GradReducer(list(net.parameters()), bucket_mb=300 / 2 ** 20)
+        orig = red._launch
+
+        def launch(bi):
+            _EVENTS.append(("launch", bi))
+            return orig(bi)
+
+        red._launch = launch
+        red.prepare()
+        with ops.grouped_wgrads(group):
+            net(_inputs(rank, 0)[:, :6]).backward()
+        red.finish()
+        enc = {red.bucket_of[id(lay.weight)] for lay in net.layers}
+        q.put((rank, list(_EVENTS), sorted(enc)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("group", [6, 5])
+def test_encoder_buckets_reduce_before_frontend_backward(group):
+    """DPH_WGRAD_GROUP=6 (and 5, which does not divide the 12 layers): every encoder bucket's all-reduce is issued
+    before the frontend backward starts -- the last partial group is flushed by the hook on the encoder input
+    (ops.mark_encoder_input), not at the end of the backward -- so the collectives overlap the frontend backward."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_window_worker, args=(r, world, port, group, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, ev, enc in res:
+        front = ev.index(("frontend",))
+        launched = {e[1] for e in ev[:front] if e[0] == "launch"}
+        assert set(enc) <= launched, (rank, group, ev)
+
+
+def _replica_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from dphubert_amd.ddp import broadcast_module, verify_replicas
+        torch.manual_seed(10 + rank)                   # every rank initialises differently
+        net = torch.nn.Sequential(torch.nn.Linear(6, 5), torch.nn.BatchNorm1d(5), torch.nn.Linear(5, 3))
+        net[1].running_mean.normal_()
+        v0 = net[0].weight._version
+        broadcast_module(net)
+        assert net[0].weight._version > v0             # the bf16 image caches key on the version
+        verify_replicas(net)                           # identical now: no error
+        state = {k: v.clone() for k, v in net.state_dict().items()}
+        if rank == 1:
+            with torch.no_grad():
+                net[2].weight[0, 0] += 1e-6            # one element on one rank
+        try:
+            verify_replicas(net)
+            mismatch = None
+        except RuntimeError as e:
+            mismatch = str(e)
+        q.put((rank, state, mismatch))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_broadcast_and_verify_replicas_gloo_ws2():
+    """Trainer construction broadcasts rank 0's parameters and buffers (torch DDP's construction-time broadcast,
+    distill.py:41); verify_replicas (run after a checkpoint load) fails on every rank when one element differs."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_replica_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict((r, (s, m)) for r, s, m in (q.get(timeout=120) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for k in res[0][0]:
+        assert torch.equal(res[0][0][k], res[1][0][k]), k
+    for r in range(world):
+        assert res[r][1] is not None and "2.weight" in res[r][1], res[r][1]
+
+
+def test_wgrad_group_plan_and_bucket_order():
+    """The bucket layout follows the predicted gradient-ready order (distill projections first; HardConcrete logits
+    and Lagrange multipliers, whose gradients land at the end of the backward, in the last bucket), and the planned
+    weight-gradient group minimises the modelled step end: the whole encoder at world size 1, no larger a group on a
+    slow link than on a fast one."""
+    from dphubert_amd.synthetic import HUBERT_BASE_CONFIG
+    from dphubert_amd import trainer as T
+    dm = T.build_distill_module(HUBERT_BASE_CONFIG, distill_layers="0.4,8,12")
+    opt = dm.configure_optimizers(clip_norm=10.0)["optimizer"]
+    params = [p for g in opt.param_groups for p in g["params"]]
+    red = GradReducer(list(reversed(T.grad_ready_order(dm, params))), groups=T.fused_grad_groups(dm.student_model))
+    names = {id(p): n for n, p in dm.named_parameters()}
+    first, last = [names[id(p)] for p in red.buckets[0]], [names[id(p)] for p in red.buckets[-1]]
+    assert any(n.startswith("distill_linear_projs") for n in first)
+    assert all("log_alpha" in n or n.startswith("lambda") or "feature_extractor" in n or "encoder." in n for n in last)
+    assert sum("log_alpha" in n for n in last) == sum("log_alpha" in n for n in names.values())
+    proj = list(dm.distill_linear_projs.parameters())
+    frames = 16 * 160000 / 320
+    assert T.plan_wgrad_group(dm.student_model, red.buckets, 1, frames) == 12
+    picks = {}
+    for bus in (150.0, 20.0):
+        g = T.plan_wgrad_group(dm.student_model, red.buckets, 8, frames, bus, 4, proj)
+        ends = {c: max(T.wgrad_group_timeline(dm.student_model, red.buckets, 8, frames, c, bus, 4, proj))
+                for c in (1, 2, 3, 4, 6, 8, 12)}
+        assert ends[g] <= min(ends.values()) + 1e-9, (bus, g, ends)
+        picks[bus] = g
+    assert picks[20.0] <= picks[150.0], picks

@@ -150,13 +150,98 @@ def test_graph_replay_matches_eager(family, accum):
     cat = lambda d: torch.cat([d[n].detach().float().flatten().cpu() for n in names])  # noqa: E731
     e_all = rel_l2(cat(pg), cat(pe[0]))
     base_all = max(rel_l2(cat(pe[i]), cat(pe[j])) for i, j in pairs)
-    # (floor 1e-4: three eager runs under-estimate the atomic-order spread now and then -- 4.3x once at
-    # accum 3 -- while a stale or missing op in the replay moves the whole vector by > 1e-3)
-    assert e_all < max(1e-4, 4 * base_all), (e_all, base_all)
+    # (floor 1e-5, as tools/graph_rccl_probe.py: with the student offset from the teacher (_module) the gradients
+    # are smooth in the weights and the eager spread is a fair estimate; a stale or missing op in the replay moves
+    # the whole vector by > 1e-3)
+    assert e_all < max(1e-5, 4 * base_all), (e_all, base_all)
     # the graph replays follow the LR schedule: optimizer and scheduler state agree
     assert ea.optimizer._step == gr.optimizer._step
     for g1, g2 in zip(ea.optimizer.param_groups, gr.optimizer.param_groups):
         assert g1["lr"] == g2["lr"]
+
+
+def _assert_tracks_eager(eager, gr, le, lg):
+    """The graph trainer's losses and parameters within 4x the eager-vs-eager spread (test_graph_replay_matches_eager's
+    rule)."""
+    for s_, b in enumerate(lg):
+        vals = [l[s_] for l in le]
+        spread = max(vals) - min(vals)
+        assert abs(vals[0] - b) <= 1e-3 * max(1.0, abs(b)) + 4 * spread, (le, lg)
+    pe = [dict(t.module.named_parameters()) for t in eager]
+    names = [n for n, p in gr.module.named_parameters() if p.requires_grad and not n.endswith("k_proj.bias")]
+    pg = dict(gr.module.named_parameters())
+    pairs = [(0, 1), (0, 2), (1, 2)]
+    for n in names:
+        e = rel_l2(pg[n].detach().cpu(), pe[0][n].detach().cpu())
+        base = max(rel_l2(pe[i][n].detach().cpu(), pe[j][n].detach().cpu()) for i, j in pairs)
+        assert e < max(1e-2 if pg[n].dim() == 1 else 5e-3, 4 * base), (n, e, base)
+    cat = lambda d: torch.cat([d[n].detach().float().flatten().cpu() for n in names])  # noqa: E731
+    e_all = rel_l2(cat(pg), cat(pe[0]))
+    base_all = max(rel_l2(cat(pe[i]), cat(pe[j])) for i, j in pairs)
+    assert e_all < max(1e-5, 4 * base_all), (e_all, base_all)
+
+
+def test_ffn_compaction_switch_under_graphs():
+    """A gate whose expected zero fraction crosses Trainer.FFN_COMPACT_MIN_ZERO at a re-evaluation step under graph
+    replay (a prune.py run toward 0.75 sparsity reaches it): the stale graphs are dropped, that optimizer step runs
+    eagerly in the packed FFN layout, the next one recaptures -- and the trajectory tracks eager trainers making the
+    same switch (losses and every parameter within 4x the eager-vs-eager spread)."""
+    from dphubert_amd.trainer import Trainer
+    batch = _batch()
+    mk = lambda graphs: Trainer(_module(), clip_norm=10.0, graphs=graphs, graph_warmup=1)  # noqa: E731
+    eager = [mk(False) for _ in range(3)]
+    gr = mk(True)
+    for t in eager + [gr]:
+        t.FFN_COMPACT_EVERY = 3          # decisions at global steps 1, 4, 7 (_module() starts at 1)
+    le = [[] for _ in eager]
+    lg = []
+    g = torch.Generator().manual_seed(5)
+    for step in range(6):
+        if step == 2:                    # before global step 3: half of layer 0's FFN units pushed to exact zeros
+            n = gr.module.student_model.encoder.transformer.layers[0].feed_forward.hard_concrete_for_intermediate \
+                .log_alpha.numel()
+            idx = torch.randperm(n, generator=g)[: n // 2].to(DEV)
+            for t in eager + [gr]:
+                hc = t.module.student_model.encoder.transformer.layers[0].feed_forward.hard_concrete_for_intermediate
+                with torch.no_grad():
+                    hc.log_alpha[idx] = -10.0
+        for t, l in zip(eager, le):
+            l.append(t.step(batch).item())
+        lg.append(gr.step(batch).item())
+        if step == 3:                    # global step 4: the switch -- graphs dropped, this step eager
+            assert not gr._graphs and gr._eager_until == 5
+    torch.cuda.synchronize()
+    hc = gr.module.student_model.encoder.transformer.layers[0].feed_forward.hard_concrete_for_intermediate
+    assert getattr(hc, "dph_compact", False), "the gate did not switch to the packed FFN"
+    assert gr._graph is not None, "no graph recaptured after the switch"
+    _assert_tracks_eager(eager, gr, le, lg)
+
+
+def test_profiled_graph_survives_grouped_fallback(monkeypatch):
+    """Round-3 host segfault in the profiled step replay (gpurun_out/r3_s25): a grouped weight-gradient launch that
+    returned DPH_EUNSUPPORTED after its start event was recorded into the graph dropped that event, and the replay
+    recorded a destroyed hipEvent.  Every grouped launch is forced to fall back here; the profiler owns its events,
+    so the replays after a garbage collection run and time every GEMM."""
+    import gc
+    from dphubert_amd import _lib
+    from dphubert_amd import kernels as K
+    from dphubert_amd.kernels import LaunchProfiler
+    from dphubert_amd.trainer import Trainer
+    batch = _batch()
+    tr = Trainer(_module(), clip_norm=10.0, graphs=True, graph_warmup=1)
+    for _ in range(2):
+        tr.step(batch)
+    monkeypatch.setattr(_lib.lib(), "dph_gemm_grouped", lambda *a: K.EUNSUPPORTED)
+    prof = LaunchProfiler()
+    tr.prepare_profiled_step(prof)
+    assert len(prof.events) > 2 * len(prof.records), "no grouped launch fell back"
+    gc.collect()
+    for _ in range(2):
+        loss = tr.step(batch, profiled=True)
+    torch.cuda.synchronize()
+    assert torch.isfinite(loss).item()
+    summ = prof.summary()
+    assert summ and all(v["ms"] > 0 for v in summ.values()), summ
 
 
 def test_graph_profiled_step_events():
