@@ -89,6 +89,7 @@ _SIGS = {
     "dph_colsum": ([vp, vp, i64, i64, vp, i64, S], C.c_int),
     "dph_colsum3": ([vp, vp, vp, vp, i64, i64, vp, i64, S], C.c_int),
     "dph_colsum_workspace": ([i64, i64], i64),
+    "dph_colprod": ([vp, i64, vp, i64, vp, vp, i64, i64, S], C.c_int),
     "dph_layernorm_bwd_workspace": ([i64, i64], i64),
     "dph_attention_fwd": ([vp, vp, vp, vp, vp, vp, i64, i64, i64, f32, f32, u64, vp, S], C.c_int),
     "dph_attention_keep_bytes": ([i64, i64, i64], i64),

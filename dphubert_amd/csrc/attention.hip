@@ -602,6 +602,219 @@ __global__ void __launch_bounds__(256, 2) attn_fwd32_kernel(const bf16_t* __rest
 }
 
 // ---------------------------------------------------------------------------
+// The 32 x 32 forward, restructured for VALU issue (PMC, profiles/r4_s2_pmcattn_summary.txt: 18.4 VALU
+// instructions per MFMA at p = 0, 34.6 at p = 0.1, MFMA busy 10-13 %: the kernel is VALU-issue bound):
+//  * key tiles that need no mask run in a loop of their own and the masked tile(s) after it, so the O
+//    accumulators flow straight from one loop into the next (the old single loop with a masked / unmasked
+//    branch inside compiled to 32 v_mov_b64 phi copies of the accumulators per tile);
+//  * tiles wholly past the key length are skipped: their scores carry the -1e4 key mask
+//    (components.py:411-415) and exp2 of (s - 1e4 - max) * log2(e) is exactly 0 in fp32, so they add
+//    nothing to O or to the row sum (when every key is masked -- key_len 0 -- all tiles run masked);
+//  * K / V tile loads clamp their rows to T - 1 instead of branching per row (rows past T only feed keys
+//    the mask zeroes);
+//  * the eight K fragments of a tile are read before its first MFMA (the compiler otherwise waited
+//    lgkmcnt(0) on each read in front of its MFMA);
+//  * the row sum is four interleaved chains instead of one 32-deep dependent chain.
+// Same arithmetic per score as attn_fwd32_kernel; keep bits in the same layout (tiles past the key length
+// are not written: their probabilities are 0 and the backward multiplies whatever it reads there by 0).
+// ---------------------------------------------------------------------------
+template <bool DROP>
+__global__ void __launch_bounds__(256, 3) attn_fwd32v2_kernel(const bf16_t* __restrict__ qkv, float* __restrict__ o_u,
+                                                             bf16_t* __restrict__ o_m, float* __restrict__ lse,
+                                                             const float* __restrict__ head_mask,
+                                                             const int64_t* __restrict__ key_len, AttnShape sh,
+                                                             float scale, float drop_p, uint64_t seed,
+                                                             uint16_t* __restrict__ keep_out) {
+  seed = epoch_seed(seed);
+  const uint32_t mix = seed_mix(seed);
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE_SWZ_BYTES];   // [buf][K | V][64 rows x 128 B]
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int hi = lane >> 5;
+  const int b = blockIdx.z;
+  const int h = blockIdx.y;
+  const int T32 = (int)sh.T, H = (int)sh.H;
+  const int64_t RS = sh.RS;
+  const int q = (int)blockIdx.x * RB + wave * 32 + (lane & 31);
+  const bf16_t* rowbase = qkv + (int64_t)b * sh.T * RS;
+  const int klen = (int)(key_len ? key_len[b] : sh.T);
+  const uint32_t half_tp = (uint32_t)(T32 + 1) >> 1;
+  const uint32_t hrow = ((uint32_t)(b * H + h) * (uint32_t)T32 + (uint32_t)q) * half_tp;
+  if (head_mask != nullptr && head_mask[h] == 0.f) {
+    if (q < T32) {
+      bf16_t* orow = o_m + ((int64_t)b * T32 + q) * (H * HD) + h * HD + 32 * hi;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) *reinterpret_cast<uint4*>(orow + 8 * c) = make_uint4(0, 0, 0, 0);
+    }
+    return;
+  }
+  bf16x8_t qf[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (q < T32) v = *reinterpret_cast<const uint4*>(rowbase + (int64_t)q * RS + h * HD + 16 * t + 8 * hi);
+    qf[t] = __builtin_bit_cast(bf16x8_t, scale_bf16x8(v, scale));
+  }
+  f32x16_t oacc[2];
+#pragma unroll
+  for (int d = 0; d < 2; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) oacc[d][r] = 0.f;
+  float m_run = -INFINITY, l_run = 0.f;
+  const float inv_keep = DROP ? 1.f / (1.f - drop_p) : 1.f;
+  const uint32_t thr = drop_thr(drop_p);
+  const int nkt = (T32 + KT - 1) / KT;                      // keep-word stride (layout of every tile)
+  const int kend = (klen >= 1 && klen < T32) ? klen : T32;  // keys that can carry probability
+  const int ntile = (kend + KT - 1) / KT;
+  const int nfull = klen >= 1 ? kend / KT : 0;              // tiles with no masked key
+  uint4 rk[2], rv[2];
+  auto ldsK = [&](int buf) { return smem + buf * 2 * TILE_SWZ_BYTES; };
+  auto ldsV = [&](int buf) { return smem + buf * 2 * TILE_SWZ_BYTES + TILE_SWZ_BYTES; };
+  // K / V rows of key tile kt (rows clamped to T - 1: no per-row branch)
+  auto load_kv = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + 256 * i;
+      const int r = min(kt * KT + (c >> 3), T32 - 1);
+      const int c8 = (c & 7) * 8;
+      rk[i] = *reinterpret_cast<const uint4*>(rowbase + (int64_t)r * RS + (H + h) * HD + c8);
+      rv[i] = *reinterpret_cast<const uint4*>(rowbase + (int64_t)r * RS + (2 * H + h) * HD + c8);
+    }
+  };
+  auto store_kv = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + 256 * i;
+      const int r = c >> 3;
+      *reinterpret_cast<uint4*>(ldsK(buf) + kswz(r, c & 7)) = rk[i];
+      *reinterpret_cast<uint4*>(ldsV(buf) + vswz(r, (c & 7) * 8)) = rv[i];
+    }
+  };
+  load_kv(0);
+  store_kv(0);
+  __syncthreads();
+
+  auto body = [&](int kt, auto masked_c) {
+    constexpr bool MASKED = decltype(masked_c)::value;
+    const int cur = kt & 1;
+    const bool more = kt + 1 < ntile;
+    if (more) load_kv(kt + 1);
+    const char* K_ = ldsK(cur);
+    const char* V_ = ldsV(cur);
+    bf16x8_t kf[2][4];
+#pragma unroll
+    for (int k2 = 0; k2 < 2; ++k2)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) kf[k2][t] = lds_b128(K_, kswz(32 * k2 + (lane & 31), 2 * t + hi));
+    f32x16_t sacc[2];
+#pragma unroll
+    for (int k2 = 0; k2 < 2; ++k2)
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        sacc[k2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[k2][t], qf[t], t == 0 ? f32x16_t{} : sacc[k2], 0, 0, 0);
+    const int kb = kt * KT + 4 * hi;   // key of (k2 = 0, r = 0) in this lane
+    float mt = -INFINITY;
+#pragma unroll
+    for (int k2 = 0; k2 < 2; ++k2)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float v = sacc[k2][r];
+        if constexpr (MASKED) {
+          const int key = kb + 32 * k2 + 8 * (r >> 2) + (r & 3);
+          v = key >= klen ? v - 10000.0f : v;
+          v = key >= T32 ? -INFINITY : v;
+          sacc[k2][r] = v;
+        }
+        mt = fmaxf(mt, v);
+      }
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    const bool move = mt > m_run + RESCALE_TH;
+    if (__any(move)) {
+      const float m_new = move ? mt : m_run;
+      const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * L2E);
+      l_run *= alpha;
+      m_run = m_new;
+#pragma unroll
+      for (int d = 0; d < 2; ++d)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) oacc[d][r] *= alpha;
+    }
+    const float ml = m_run * L2E;
+    float ls[4] = {0.f, 0.f, 0.f, 0.f};
+    uint32_t kw[2] = {0u, 0u};
+#pragma unroll
+    for (int k2 = 0; k2 < 2; ++k2)
+#pragma unroll
+      for (int rq = 0; rq < 4; ++rq) {
+        uint32_t hb[2] = {0u, 0u};
+        if constexpr (DROP) {
+          const uint32_t pr = hrow + (uint32_t)((kb + 32 * k2 + 8 * rq) >> 1);
+          hb[0] = attn_hash32(mix, pr);
+          hb[1] = attn_hash32(mix, pr + 1);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = 4 * rq + i;
+          const float p = __builtin_amdgcn_exp2f(fmaf(sacc[k2][r], L2E, -ml));
+          ls[i] += p;
+          if constexpr (DROP) {
+            const bool keep = ((i & 1) ? (hb[i >> 1] >> 16) : (hb[i >> 1] & 0xffffu)) >= thr;
+            kw[rq & 1] |= (keep ? 1u : 0u) << (4 * (2 * k2 + (rq >> 1)) + i);
+            sacc[k2][r] = keep ? p : 0.f;
+          } else {
+            sacc[k2][r] = p;
+          }
+        }
+      }
+    if constexpr (DROP) {
+      if (keep_out != nullptr && q < T32) {
+        uint16_t* kp = keep_out + ((int64_t)(b * H + h) * T32 + q) * (nkt * 4) + kt * 4;
+        kp[hi] = (uint16_t)kw[0];
+        kp[2 + hi] = (uint16_t)kw[1];
+      }
+    }
+    float lsum = (ls[0] + ls[1]) + (ls[2] + ls[3]);
+    lsum += __shfl_xor(lsum, 32, 64);
+    l_run += lsum;
+#pragma unroll
+    for (int k2 = 0; k2 < 2; ++k2)
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const bf16x8_t pf = pack8(sacc[k2], 8 * e);
+        const int base = 32 * k2 + 16 * e + 4 * hi;
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+          const bf16x8_t vf = tr_frag_v(V_, base, base + 8, 32 * d + 16 * ((lane >> 4) & 1), lane);
+          oacc[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, oacc[d], 0, 0, 0);
+        }
+      }
+    if (more) store_kv(cur ^ 1);
+    __syncthreads();
+  };
+  int kt = 0;
+  for (; kt < nfull; ++kt) body(kt, std::integral_constant<bool, false>());
+  for (; kt < ntile; ++kt) body(kt, std::integral_constant<bool, true>());
+
+  if (q >= T32) return;
+  const float hm = head_mask ? head_mask[h] : 1.0f;
+  const float inv_l = inv_keep / l_run;
+  const int64_t obase = ((int64_t)b * T32 + q) * (H * HD) + h * HD;
+#pragma unroll
+  for (int d = 0; d < 2; ++d)
+#pragma unroll
+    for (int rq = 0; rq < 4; ++rq) {
+      const int col = 32 * d + 8 * rq + 4 * hi;
+      float v[4] = {oacc[d][4 * rq] * inv_l, oacc[d][4 * rq + 1] * inv_l, oacc[d][4 * rq + 2] * inv_l,
+                    oacc[d][4 * rq + 3] * inv_l};
+      *reinterpret_cast<float4*>(o_u + obase + col) = make_float4(v[0], v[1], v[2], v[3]);
+      *reinterpret_cast<uint2*>(o_m + obase + col) =
+          make_uint2(pack2bf(v[0] * hm, v[1] * hm), pack2bf(v[2] * hm, v[3] * hm));
+    }
+  if (hi == 0) lse[(int64_t)(b * H + h) * T32 + q] = m_run + __logf(l_run);
+}
+
+// ---------------------------------------------------------------------------
 // backward prep: rowdot[b][h][t] = sum_d dO_m * O_u ; D = hm * rowdot ; dhm[h] += sum rowdot
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) attn_bwd_prep_kernel(const bf16_t* __restrict__ dom,
@@ -1194,19 +1407,26 @@ using namespace dph;
 
 namespace {
 
-// DPH_ATTN_FWD=2: the 16 x 16 x 32 forward (two waves per SIMD) for every shape (A/B)
-// DPH_ATTN_FWD=2: the 16 x 16 x 32 forward for every shape (A/B; the WavLM bias always takes it).  Measured
+// DPH_ATTN_FWD=2: the 16 x 16 x 32 forward for every shape (A/B; the WavLM bias always takes it); =1: the first
+// 32 x 32 forward (attn_fwd32_kernel, A/B against the restructured attn_fwd32v2_kernel, the default).  Measured
 // and dropped: the 32 x 32 x 16 forward at three waves per SIMD (K / V by LDS-DMA, Q' staged in LDS, 168
 // VGPRs with 14-20 spilled) ran 46 / 58 us against 38 / 51 us at two waves per SIMD.
-static bool fwd32_enabled() {
+static int fwd32_mode() {
   const char* e = getenv("DPH_ATTN_FWD");
-  return !(e && e[0] == '2');
+  return (e && e[0] == '2') ? 0 : ((e && e[0] == '1') ? 1 : 2);
 }
 
 template <bool DROP, bool BIAS>
 void launch_fwd(dim3 grid, hipStream_t stream, const void* qkv, void* o_u, void* o_m, float* lse, const float* hm,
                 const int64_t* key_len, AttnShape sh, float scale, float p, uint64_t seed, RelBias rb, void* keep) {
-  if (!BIAS && fwd32_enabled()) {
+  const int mode = BIAS ? 0 : fwd32_mode();
+  if (mode == 2) {
+    hipLaunchKernelGGL((attn_fwd32v2_kernel<DROP>), grid, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(qkv),
+                       reinterpret_cast<float*>(o_u), reinterpret_cast<bf16_t*>(o_m), lse, hm, key_len, sh, scale, p,
+                       seed, reinterpret_cast<uint16_t*>(keep));
+    return;
+  }
+  if (mode == 1) {
     hipLaunchKernelGGL((attn_fwd32_kernel<DROP>), grid, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(qkv),
                        reinterpret_cast<float*>(o_u), reinterpret_cast<bf16_t*>(o_m), lse, hm, key_len, sh, scale, p,
                        seed, reinterpret_cast<uint16_t*>(keep));

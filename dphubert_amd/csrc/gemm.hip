@@ -956,7 +956,7 @@ __host__ __device__ __forceinline__ bool direct_epi_ok(const DphGemmArgs& a) {
                            reinterpret_cast<uintptr_t>(a.aux_in) | reinterpret_cast<uintptr_t>(a.residual) |
                            reinterpret_cast<uintptr_t>(a.bias) | reinterpret_cast<uintptr_t>(a.colmask);
   const bool dgk = a.act == DPH_ACT_GELU_BWD_DGK;
-  return (calign & 3) == 0 && (palign & 15) == 0 && (dgk ? (a.aux_in && a.residual) : !(a.aux_in && a.residual)) &&
+  return (calign & 3) == 0 && (palign & 15) == 0 && (dgk ? a.aux_in != nullptr : !(a.aux_in && a.residual)) &&
          a.M < ((int64_t)1 << 31) && (!a.row_len || a.len_rows > 0) &&
          (a.act == DPH_ACT_GELU_BWD || dgk || (!a.colsum_out && !a.colsum_aux));   // column sums: GELU backward only
 }
@@ -1051,7 +1051,8 @@ __device__ __forceinline__ bool direct_epi_t(const DphGemmArgs& a, int64_t z, in
   // instead of 32 -- the persistent kernel's GELU_BWD variant spilled with all of them preloaded)
   uint2 in[FM][FN], in2[DGK ? FM : 1][DGK ? FN : 1];
   (void)base;
-  const bf16_t* inp2 = reinterpret_cast<const bf16_t*>(rs_p);      // DGK: the forward's output f
+  const bf16_t* inp2 = reinterpret_cast<const bf16_t*>(rs_p);      // DGK: the forward's output f (optional)
+  const bool has_in2 = DGK && inp2 != nullptr;
   auto load_in = [&](int i, auto ck) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
@@ -1059,7 +1060,9 @@ __device__ __forceinline__ bool direct_epi_t(const DphGemmArgs& a, int64_t z, in
       if constexpr (DGK) in2[i][j] = make_uint2(0, 0);
       if (has_in && (mfull || ml + 16 * i < M) && (nfull || nl + 16 * j < N)) {
         in[i][j] = *reinterpret_cast<const uint2*>(inp + roff(i, ck) + 16 * j);
-        if constexpr (DGK) in2[i][j] = *reinterpret_cast<const uint2*>(inp2 + roff(i, ck) + 16 * j);
+        if constexpr (DGK) {
+          if (has_in2) in2[i][j] = *reinterpret_cast<const uint2*>(inp2 + roff(i, ck) + 16 * j);
+        }
       }
     }
   };

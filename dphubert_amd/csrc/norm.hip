@@ -370,6 +370,55 @@ __global__ void __launch_bounds__(256) colsum_kernel(const bf16_t* __restrict__ 
   }
 }
 
+// out[n] += s(n) * sum_r a[r][n] * b[r][n] (dph_colprod): block = 64 x 4 threads, 8 columns per thread over a
+// range of rows, the 4 row phases summed in LDS, one atomic per column per block
+__global__ void __launch_bounds__(256) colprod_kernel(const bf16_t* __restrict__ a, int64_t lda,
+                                                      const float* __restrict__ b, int64_t ldb,
+                                                      const float* __restrict__ colmask, float* __restrict__ out,
+                                                      int64_t R, int64_t N, int64_t rows_per_block) {
+  __shared__ float red[4][512];
+  const int tx = threadIdx.x & 63;
+  const int ty = threadIdx.x >> 6;
+  const int64_t c0 = (int64_t)blockIdx.x * 512 + tx * 8;
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per_block;
+  const int64_t r1 = min(R, r0 + rows_per_block);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const bool vec = c0 + 8 <= N && (lda % 8) == 0 && (ldb % 4) == 0;
+  for (int64_t r = r0 + ty; r < r1; r += 4) {
+    const bf16_t* pa = a + r * lda + c0;
+    const float* pb = b + r * ldb + c0;
+    if (vec) {
+      const uint4 ra = *reinterpret_cast<const uint4*>(pa);
+      const float4 b0 = *reinterpret_cast<const float4*>(pb);
+      const float4 b1 = *reinterpret_cast<const float4*>(pb + 4);
+      const uint32_t w[4] = {ra.x, ra.y, ra.z, ra.w};
+      const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        acc[2 * i] = fmaf(__uint_as_float(w[i] << 16), bv[2 * i], acc[2 * i]);
+        acc[2 * i + 1] = fmaf(__uint_as_float(w[i] & 0xffff0000u), bv[2 * i + 1], acc[2 * i + 1]);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        if (c0 + i < N) acc[i] = fmaf(bf2f(pa[i]), pb[i], acc[i]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) red[ty][tx * 8 + i] = acc[i];
+  __syncthreads();
+  for (int c = threadIdx.x; c < 512; c += 256) {
+    const int64_t col = (int64_t)blockIdx.x * 512 + c;
+    if (col >= N) continue;
+    float sc = 1.f;
+    if (colmask) {
+      const float m = colmask[col];
+      sc = m != 0.f ? 1.0f / m : 0.f;
+    }
+    atomicAdd(out + col, sc * (red[0][c] + red[1][c] + red[2][c] + red[3][c]));
+  }
+}
+
 // out_q[c] += sum_r ws[r][q * seg + c] for the (up to 3) column segments q of width seg (null outputs
 // skipped).  Block = 64 columns x 4 row phases over one of gridDim.y row groups; one atomic per column
 // per group (a handful of adders per address).
@@ -611,6 +660,16 @@ extern "C" int dph_layernorm_bwd(const void* dy, const void* x, const float* xsc
   return dph_layernorm_bwd_ld(dy, x, xscale, gamma, mean, rstd, dx, dgamma, dbeta, rows, D, D, dropout_p, seed,
                               branch, branch_p, branch_seed, branch_smask, branch_colsum, branch_pre, branch_sdot,
                               nullptr, ws, ws_bytes, stream);
+}
+
+extern "C" int dph_colprod(const void* a, int64_t lda, const float* b, int64_t ldb, const float* colmask, float* out,
+                           int64_t R, int64_t N, hipStream_t stream) {
+  DPH_REQUIRE(a && b && out && R > 0 && N > 0 && lda >= N && ldb >= N, "dph_colprod: bad args");
+  const int64_t rpb = 32;
+  dim3 grid((unsigned)cdiv(N, 512), (unsigned)cdiv(R, rpb));
+  hipLaunchKernelGGL(colprod_kernel, grid, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(a), lda, b, ldb,
+                     colmask, out, R, N, rpb);
+  return check_launch("dph_colprod");
 }
 
 extern "C" int64_t dph_colsum_workspace(int64_t rows, int64_t cols) {

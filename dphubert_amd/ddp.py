@@ -130,6 +130,8 @@ class GradReducer:
         """
         if zero:
             self._zero_buckets()
+        # buckets hold only this micro-batch's gradients (kernels may read a fresh weight gradient back: ops)
+        self.fresh = bool(zero)
         for p in self.params:
             p.grad = self.views[id(p)]
             if self.direct:

@@ -28,6 +28,8 @@ from .wav2vec2.model import Wav2Vec2Model
 
 __all__ = ["DistillLoss", "DistillModule", "LinearDecayLRScheduler"]
 
+_TEACHER_AFTER = __import__("os").environ.get("DPH_TEACHER_ORDER", "before") == "after"
+
 
 class DistillLoss(nn.Module):
     """lightning.py:91-139: ``loss = l2*MSE + l1*L1 + cos*(-mean cos)`` (or the ``log_sig`` variant)."""
@@ -184,13 +186,21 @@ class DistillModule(nn.Module):
         from . import kernels as K
         # while the two forwards share the GPU, GEMMs take one tile per block (no persistent grids)
         shared = K.shared_gpu() if side is not None else contextlib.nullcontext()
+        # DPH_TEACHER_ORDER=after (A/B): record the teacher branch after the student forward instead of before it
+        # (a captured graph launches its nodes in recording order)
+        after = side is not None and _TEACHER_AFTER
         with shared:
+            if after:
+                main = torch.cuda.current_stream()
+                side.wait_stream(main)
+                student_hiddens, student_lengths = self.student_model.extract_features(waveforms, lengths)
             if side is not None:
                 # the frozen teacher runs on its own HIP stream, concurrently with the student forward: its
                 # kernels fill the CUs the student's GEMM tile rounds and latency-bound launches leave idle
                 # (forked / joined with stream waits, so a HIP-graph capture records both branches)
                 main = torch.cuda.current_stream()
-                side.wait_stream(main)
+                if not after:
+                    side.wait_stream(main)
                 with torch.cuda.stream(side), torch.no_grad(), ops.private_zero_arena(self._teacher_arena):
                     teacher_hiddens, teacher_lengths = self.teacher_model.extract_features(waveforms, lengths)
                     t_layers = [teacher_hiddens[idx] for idx in self.distill_layers]
@@ -198,7 +208,8 @@ class DistillModule(nn.Module):
                 with torch.no_grad():
                     teacher_hiddens, teacher_lengths = self.teacher_model.extract_features(waveforms, lengths)
                     t_layers = [teacher_hiddens[idx] for idx in self.distill_layers]
-            student_hiddens, student_lengths = self.student_model.extract_features(waveforms, lengths)
+            if not after:
+                student_hiddens, student_lengths = self.student_model.extract_features(waveforms, lengths)
         if side is not None:
             main.wait_stream(side)
             for t in t_layers:

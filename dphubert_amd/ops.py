@@ -479,25 +479,27 @@ class grouped_wgrads:
                 self.flush()
             else:
                 for items in self.queues.values():
-                    for *_, params in items:
+                    for *_, params, _post in items:
                         for p in params:
                             p._dph_hold = False
                 self.queues = {}
 
-    def add(self, dy, x, dw, params):
+    def add(self, dy, x, dw, params, post=None):
         key = (tuple(dy.shape), tuple(x.shape), dy.device)
         items = self.queues.setdefault(key, [])
         for p in params:
             p._dph_hold = True
-        items.append((dy, x, dw, params))
+        items.append((dy, x, dw, params, post))
         if len(items) >= self.group:
             self._flush(key)
 
     def _flush(self, key):
         items = self.queues.pop(key)
-        ws = K.linear_wgrad_grouped([(dy, x, dw) for dy, x, dw, _ in items], accumulate=True)
+        ws = K.linear_wgrad_grouped([(dy, x, dw) for dy, x, dw, _, _ in items], accumulate=True)
         del ws
-        for *_, params in items:
+        for *_, params, post in items:
+            if post is not None:
+                post()           # reads the landed weight gradient (stream-ordered after the grouped launch)
             for p in params:
                 p._dph_hold = False
                 p._dph_sink_ready(p)
@@ -525,18 +527,33 @@ def mark_encoder_input(x: torch.Tensor) -> torch.Tensor:
     return x
 
 
-def _layer_wgrad(dy, x, dw, direct, params, **kw):
+def _layer_wgrad(dy, x, dw, direct, params, post=None, **kw):
     """An encoder layer's weight gradient: queued in the active grouped_wgrads block when it goes straight
     into the bucket (``direct``) at the operands' full width, else launched now (on the wgrad side stream
-    when one is active)."""
+    when one is active).  ``post()`` runs once the gradient has landed (after its launch, or after the grouped
+    launch that carries it)."""
     q = _WGRAD_DEFER[0]
     full = tuple(dw.shape) == (dy.shape[1], x.shape[1]) and kw.get("n_out", 0) in (0, dy.shape[1]) and \
         kw.get("k_in", 0) in (0, x.shape[1])
     if q is not None and direct and full:
-        q.add(dy, x, dw, params)
+        q.add(dy, x, dw, params, post)
         return None
     with wgrad_side(dy, x, enable=direct):
-        return K.linear_wgrad(dy, x, dw, accumulate=direct, **kw)
+        ws = K.linear_wgrad(dy, x, dw, accumulate=direct, **kw)
+    if post is not None:
+        post()
+    return ws
+
+
+def _bucket_fresh(p) -> bool:
+    """The gradient bucket behind ``p``'s sink holds this micro-batch's gradient alone (zeroed at its start)."""
+    red = getattr(getattr(p, "_dph_sink_ready", None), "__self__", None)
+    return red is not None and bool(getattr(red, "fresh", False))
+
+
+# FFN intermediate-mask gradient from the FFN2 weight gradient (dph_colprod: sum_o W2[o][n] dW2[o][n] / mask_n)
+# instead of re-reading the forward's f in the FFN2 input-gradient epilogue; DPH_FFN_COLPROD=0 keeps the epilogue
+_FFN_COLPROD = os.environ.get("DPH_FFN_COLPROD", "1") != "0"
 
 
 # ---------------------------------------------------------------------------
@@ -1470,8 +1487,10 @@ def _ffn_interm_bwd(dy, sv, db1, dmask, cfg, F_):
     """du = (dy @ W2) * gelu'(pre) * mask * keep/(1-p); db1 += colsum(du); dmask += colsum((dy @ W2) * gelu(pre) *
     keep/(1-p)) (components.py:733-739 backward)."""
     if sv["dgk"]:
+        # dmask None: the mask gradient comes from the FFN2 weight gradient (dph_colprod), f is not read here
         return K.linear_dgrad(dy, sv["W2"], w_t=t_image(sv["W2"]), act=K.ACT_GELU_BWD_DGK, aux_in=sv["u"],
-                              residual=sv["f"], colmask=sv["imp"], colsum_out=db1, colsum_aux=dmask, colsum_n=F_)
+                              residual=sv["f"] if dmask is not None else None, colmask=sv["imp"], colsum_out=db1,
+                              colsum_aux=dmask, colsum_n=F_)
     return K.linear_dgrad(dy, sv["W2"], w_t=t_image(sv["W2"]), act=K.ACT_GELU_BWD, aux_in=sv["u"], colmask=sv["imp"],
                           colsum_out=db1, colsum_aux=dmask, dropout_p=cfg["p_interm"], seed=sv["seed_i"], colsum_n=F_)
 
@@ -1538,7 +1557,8 @@ def _ffn_forward(cfg, xin, w1, b1, w2, b2, im, lmf, resid, need, sv):
 
 def _ffn_backward(cfg, sv, dy, xin, pr, go, dmask, residual=None):
     """Backward of _ffn_forward from dy = d(FFN2 output) (after the output dropout / layer mask): the W2 / b1 / W1
-    gradients into ``go``'s buffers, the intermediate-mask gradient into ``dmask`` [F], returns d(xin) (+ residual)."""
+    gradients into ``go``'s buffers, the intermediate-mask gradient into ``dmask`` [F] (None: no intermediate mask,
+    not computed), returns d(xin) (+ residual)."""
     M, D = xin.shape
     dev = xin.device
     F_ = sv["F"]
@@ -1564,9 +1584,19 @@ def _ffn_backward(cfg, sv, dy, xin, pr, go, dmask, residual=None):
         del k1, k2
         return dx
     dw2, direct = go.buf(pr["w2"], zero=False)
-    k1 = _layer_wgrad(dy, sv["f"], dw2, direct, (pr["w2"],), k_in=F_)
+    # the mask gradient as sum_o W2[o][n] dW2[o][n] / mask_n over THIS micro-batch's dW2 = dY^T f: a fresh buffer,
+    # or a bucket zeroed at this micro-batch's start (gradient accumulation past the first micro-batch, and the
+    # weight-gradient side stream, keep the f-reading epilogue)
+    colprod = (_FFN_COLPROD and sv["dgk"] and dmask is not None and _WGRAD_SIDE[0] is None
+               and ((not direct) or _bucket_fresh(pr["w2"])))
+    post = None
+    if colprod:
+        W2i, imp = sv["W2"], sv["imp"]
+        post = lambda: call("dph_colprod", ptr(W2i), W2i.shape[1], ptr(dw2), F_, ptr(imp), ptr(dmask), D, F_,  # noqa
+                            _s())
+    k1 = _layer_wgrad(dy, sv["f"], dw2, direct, (pr["w2"],), post=post, k_in=F_)
     db1, _ = go.buf(pr["b1"])
-    du = _ffn_interm_bwd(dy, sv, db1, dmask, cfg, F_)
+    du = _ffn_interm_bwd(dy, sv, db1, None if colprod else dmask, cfg, F_)
     dw1, direct = go.buf(pr["w1"], zero=False)
     k2 = _layer_wgrad(du, xin, dw1, direct, (pr["w1"],), n_out=F_)
     dx = K.linear_dgrad(du, sv["W1"], w_t=t_image(sv["W1"]), residual=residual)
@@ -1725,7 +1755,7 @@ class EncoderLayerFn(torch.autograd.Function):
                  ptr(db2), ptr(sv["y_pre"]) if has_lmf else None, ptr(g["lmf"]), _s())
             F_ = sv["F"]
             g["im"] = z(F_) if has_im else None
-            dxn2 = _ffn_backward(cfg, sv, dy, xn2, pr, go, g["im"] if has_im else z(F_))
+            dxn2 = _ffn_backward(cfg, sv, dy, xn2, pr, go, g["im"])
             ds1 = torch.empty(M, D, dtype=F32, device=dev)
             dln2w, _ = go.buf(pr["ln2_w"])
             dln2b, _ = go.buf(pr["ln2_b"])
@@ -1867,7 +1897,7 @@ class EncoderLayerFn(torch.autograd.Function):
                  ptr(sv["y_pre"]), ptr(g["lmf"]), *ln_ws(M, D, dev), _s())
             F_ = sv["F"]
             g["im"] = z(F_) if has_im else None
-            dh1 = _ffn_backward(cfg, sv, dy, h1, pr, go, g["im"] if has_im else z(F_), residual=ds2)
+            dh1 = _ffn_backward(cfg, sv, dy, h1, pr, go, g["im"], residual=ds2)
         else:
             call("dph_layernorm_bwd", ptr(dout), ptr(s2), None, ptr(ln2_w), ptr(mu2), ptr(rs2), ptr(ds2),
                  ptr(dln2w), ptr(dln2b), M, D, 0.0, 0, None, 0.0, 0, None, None, None, None, *ln_ws(M, D, dev),

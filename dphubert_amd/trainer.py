@@ -420,6 +420,16 @@ class Trainer:
                 changed = True
         return changed
 
+    def _drop_graphs(self):
+        """Forget every captured graph AND their shared memory pool: the pool dies with its last graph, so a later
+        capture into the stale pool handle trips the caching allocator (use_count assert); the next capture
+        starts a new one."""
+        self._graphs = {}
+        self._prof_graph = None
+        self._prof_loss = None
+        self._logged_of = {}
+        self._pool = None
+
     def verify_replicas(self):
         """Raise if any parameter / buffer differs across ranks (after a checkpoint load: cli --resume_checkpoint)."""
         from .ddp import verify_replicas
@@ -452,8 +462,7 @@ class Trainer:
             if self.refresh_ffn_compaction() and self._graphs:
                 # stale graphs: this optimizer step runs eagerly in the new FFN layouts (their packed buffers and
                 # cached images are built outside any capture), the next one recaptures
-                self._graphs = {}
-                self._prof_graph = None
+                self._drop_graphs()
                 self._eager_until = m.global_step + 1
         dev = batch[0].device
         zero = self._micro == 0
@@ -470,7 +479,7 @@ class Trainer:
                 except Exception as e:  # noqa: BLE001 -- uncapturable op: stay eager
                     warnings.warn(f"HIP graph capture failed, running eagerly: {e!r}")
                     self.graphs = False
-                    self._graphs = {}
+                    self._drop_graphs()
             if key in self._graphs:
                 if profiled and final and self._prof_graph is not None:
                     # the profiled graph's event-record nodes refer to the profiler's events (LaunchProfiler.events)

@@ -62,6 +62,8 @@ typedef struct DphMat {
 /* GELU backward from what the forward stored: aux_in = the forward's pre_out under DPH_GEMM_PRE_DGK
  * (gelu'(pre)*colmask*keep/(1-p)), residual = the forward's output f (gelu(pre)*colmask*keep/(1-p)):
  * v = v*aux; colsum_aux += v*residual/colmask (0 where colmask == 0); colsum_out += stored v.
+ * residual may be NULL (then colsum_aux gets zeros): the mask gradient comes from dph_colprod over the FFN2
+ * weight gradient instead, and this epilogue reads one input less.
  * No dropout / smask arguments (they are folded into aux).  Ping-pong layouts only (dph_gemm checks). */
 #define DPH_ACT_GELU_BWD_DGK 3
 
@@ -228,6 +230,12 @@ int dph_layernorm_bwd_res32(const void* dy, const float* x, const float* gamma, 
 int dph_wave_layernorm(const float* x, const int64_t* lengths, int64_t B, int64_t S, float eps, float* y,
                        hipStream_t stream);
 
+/* out[n] += s(n) * sum_r a[r][n] * b[r][n], s(n) = 1/colmask[n] (0 where colmask[n] == 0; colmask NULL: 1), for
+ * a bf16 [R][lda] and b fp32 [R][ldb], n < N.  The FFN intermediate-mask gradient from the FFN2 weight gradient
+ * (components.py:733-741): d loss/d mask_n = sum_o W2[o][n] dW2[o][n] / mask_n, dW2 = dY^T f of this micro-batch --
+ * the contraction the FFN2 input-gradient epilogue otherwise evaluates by re-reading f */
+int dph_colprod(const void* a, int64_t lda, const float* b, int64_t ldb, const float* colmask, float* out, int64_t R,
+                int64_t N, hipStream_t stream);
 /* column sums of a bf16 matrix (bias gradients): out[n] += sum_m x[m][n]; ws: per-row-block partial
  * slab of dph_colsum_workspace(rows, cols) bytes */
 int dph_colsum(const void* x, float* out, int64_t rows, int64_t cols, float* ws, int64_t ws_bytes, hipStream_t stream);
