@@ -668,28 +668,29 @@ __global__ void __launch_bounds__(256, 3) attn_fwd32v2_kernel(const bf16_t* __re
   const int kend = (klen >= 1 && klen < T32) ? klen : T32;  // keys that can carry probability
   const int ntile = (kend + KT - 1) / KT;
   const int nfull = klen >= 1 ? kend / KT : 0;              // tiles with no masked key
-  uint4 rk[2], rv[2];
+  // staged K / V rows as four named registers (an array of them, captured by the lambdas, was demoted to
+  // scratch memory: 80 bytes per lane of scratch stores and loads per tile)
+  uint4 rk0, rk1, rv0, rv1;
   auto ldsK = [&](int buf) { return smem + buf * 2 * TILE_SWZ_BYTES; };
   auto ldsV = [&](int buf) { return smem + buf * 2 * TILE_SWZ_BYTES + TILE_SWZ_BYTES; };
   // K / V rows of key tile kt (rows clamped to T - 1: no per-row branch)
+  const int c8 = (tid & 7) * 8;
   auto load_kv = [&](int kt) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int c = tid + 256 * i;
-      const int r = min(kt * KT + (c >> 3), T32 - 1);
-      const int c8 = (c & 7) * 8;
-      rk[i] = *reinterpret_cast<const uint4*>(rowbase + (int64_t)r * RS + (H + h) * HD + c8);
-      rv[i] = *reinterpret_cast<const uint4*>(rowbase + (int64_t)r * RS + (2 * H + h) * HD + c8);
-    }
+    const int r0 = min(kt * KT + (tid >> 3), T32 - 1);
+    const int r1 = min(kt * KT + 32 + (tid >> 3), T32 - 1);
+    const bf16_t* kb0 = rowbase + (int64_t)r0 * RS + (H + h) * HD + c8;
+    const bf16_t* kb1 = rowbase + (int64_t)r1 * RS + (H + h) * HD + c8;
+    rk0 = *reinterpret_cast<const uint4*>(kb0);
+    rk1 = *reinterpret_cast<const uint4*>(kb1);
+    rv0 = *reinterpret_cast<const uint4*>(kb0 + H * HD);
+    rv1 = *reinterpret_cast<const uint4*>(kb1 + H * HD);
   };
   auto store_kv = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int c = tid + 256 * i;
-      const int r = c >> 3;
-      *reinterpret_cast<uint4*>(ldsK(buf) + kswz(r, c & 7)) = rk[i];
-      *reinterpret_cast<uint4*>(ldsV(buf) + vswz(r, (c & 7) * 8)) = rv[i];
-    }
+    const int r = tid >> 3;
+    *reinterpret_cast<uint4*>(ldsK(buf) + kswz(r, tid & 7)) = rk0;
+    *reinterpret_cast<uint4*>(ldsV(buf) + vswz(r, c8)) = rv0;
+    *reinterpret_cast<uint4*>(ldsK(buf) + kswz(r + 32, tid & 7)) = rk1;
+    *reinterpret_cast<uint4*>(ldsV(buf) + vswz(r + 32, c8)) = rv1;
   };
   load_kv(0);
   store_kv(0);

@@ -1314,16 +1314,19 @@ def _weight_norm_ws(R: int, K: int, dev):
 
 
 class LayerNormFn(torch.autograd.Function):
-    """Plain nn.LayerNorm over the last dim of (rows, D) bf16 (the final LN of a pre-norm
-    Transformer.forward, components.py:903-904)."""
+    """Plain nn.LayerNorm over the last dim of (rows, D) (the final LN of a pre-norm Transformer.forward,
+    components.py:903-904): x bf16, or fp32 -- the pre-norm layers' fp32 residual stream -- with a bf16 output."""
 
     @staticmethod
     def forward(ctx, x, w, b):
         M, D = x.shape
-        y = torch.empty_like(x)
+        y = torch.empty(M, D, dtype=BF16, device=x.device)
         mu = torch.empty(M, dtype=F32, device=x.device)
         rs = torch.empty(M, dtype=F32, device=x.device)
-        call("dph_layernorm_fwd", ptr(x), None, ptr(w), ptr(b), ptr(y), ptr(mu), ptr(rs), M, D, 1e-5, 0.0, 0, _s())
+        if x.dtype == F32:
+            call("dph_layernorm_fwd_x32", ptr(x), ptr(w), ptr(b), ptr(y), ptr(mu), ptr(rs), M, D, 1e-5, _s())
+        else:
+            call("dph_layernorm_fwd", ptr(x), None, ptr(w), ptr(b), ptr(y), ptr(mu), ptr(rs), M, D, 1e-5, 0.0, 0, _s())
         ctx.save_for_backward(x, w, mu, rs)
         return y
 
@@ -1331,11 +1334,18 @@ class LayerNormFn(torch.autograd.Function):
     def backward(ctx, dy):
         x, w, mu, rs = ctx.saved_tensors
         M, D = x.shape
+        dy = dy.contiguous()
+        if dy.dtype != BF16:
+            dy = dy.to(BF16)
         dx = torch.empty_like(x)
         dw = zeros_f32(D, x.device)
         db = zeros_f32(D, x.device)
-        call("dph_layernorm_bwd", ptr(dy.contiguous()), ptr(x), None, ptr(w), ptr(mu), ptr(rs), ptr(dx), ptr(dw),
-             ptr(db), M, D, 0.0, 0, None, 0.0, 0, None, None, None, None, *ln_ws(M, D, x.device), _s())
+        if x.dtype == F32:
+            call("dph_layernorm_bwd_res32", ptr(dy), ptr(x), ptr(w), ptr(mu), ptr(rs), ptr(dx), ptr(dw), ptr(db), M, D,
+                 None, *ln_ws(M, D, x.device), _s())
+        else:
+            call("dph_layernorm_bwd", ptr(dy), ptr(x), None, ptr(w), ptr(mu), ptr(rs), ptr(dx), ptr(dw), ptr(db), M, D,
+                 0.0, 0, None, 0.0, 0, None, None, None, None, *ln_ws(M, D, x.device), _s())
         return dx, dw, db
 
 

@@ -319,7 +319,9 @@ def _replica_worker(rank, world, port, q):
         broadcast_module(net)
         assert net[0].weight._version > v0             # the bf16 image caches key on the version
         verify_replicas(net)                           # identical now: no error
-        state = {k: v.clone() for k, v in net.state_dict().items()}
+        # numpy copies travel through the queue by value (torch tensors go by shared-memory handle, which a worker
+        # that has exited no longer holds)
+        state = {k: v.detach().numpy().copy() for k, v in net.state_dict().items()}
         if rank == 1:
             with torch.no_grad():
                 net[2].weight[0, 0] += 1e-6            # one element on one rank
@@ -348,7 +350,7 @@ def test_broadcast_and_verify_replicas_gloo_ws2():
         p.join(timeout=60)
         assert p.exitcode == 0
     for k in res[0][0]:
-        assert torch.equal(res[0][0][k], res[1][0][k]), k
+        assert (res[0][0][k] == res[1][0][k]).all(), k
     for r in range(world):
         assert res[r][1] is not None and "2.weight" in res[r][1], res[r][1]
 

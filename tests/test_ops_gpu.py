@@ -215,9 +215,14 @@ def test_attention_stored_keep_bits_match_rehash(T, lens):
     o2, d2 = run(keep)
     assert torch.equal(o1, o2)
     assert torch.equal(d1, d2)
-    # the stored bits are the dropout draws (keep rate 1 - p = 0.9; the slots of keys past T are drawn too)
+    # the stored bits are the dropout draws (keep rate 1 - p = 0.9). Layout: [b, h, query row][key tile of 64][64
+    # bits]; the forward draws every key of a tile it visits (keys past T or the length inside the last tile too)
+    # and skips tiles wholly past the length, whose words the backward never reads (their P is 0).
     import numpy as np
-    frac = np.unpackbits(keep.view(torch.uint8).cpu().numpy()).mean()
+    nkt = (T + 63) // 64
+    words = keep.view(torch.uint8).cpu().numpy().reshape(B, H, T, nkt, 8)
+    seen = [words[b, :, :, :(((lens[b] if lens else T) + 63) // 64)] for b in range(B)]
+    frac = np.concatenate([np.unpackbits(w.reshape(-1)) for w in seen]).mean()
     assert 0.88 < frac < 0.92, frac
 
 

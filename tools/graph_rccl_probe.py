@@ -71,6 +71,13 @@ def main():
     base_all = max(rel(cat(pe[i]), cat(pe[j])) for i, j in pairs)
     ok &= e_all < max(1e-5, 4 * base_all)
     print("whole-vector rel diff", e_all, "eager-vs-eager", base_all, "violations", worst)
+    # the parameters carrying most of the replay-vs-eager difference (squared-norm share) beside their eager spread
+    sq = lambda x, y: (x.detach().float() - y.detach().float()).norm().item() ** 2  # noqa: E731
+    share = sorted(((sq(pg[n], pe[0][n]), n) for n in names), reverse=True)[:6]
+    tot = sum(sq(pg[n], pe[0][n]) for n in names) or 1.0
+    for d, n in share:
+        print(f"   {n}: share {d / tot:.3f} rel {rel(pg[n], pe[0][n]):.3g} "
+              f"eager spread {max(rel(pe[i][n], pe[j][n]) for i, j in pairs):.3g}")
     dist.destroy_process_group()
     print("RCCL_GRAPH_OK" if ok else "RCCL_GRAPH_FAIL")
 
