@@ -110,9 +110,8 @@ def test_graph_replay_matches_eager(family, accum):
     (run_large.sh:54 --accum_grad 3)."""
     from dphubert_amd.trainer import Trainer
     batch = _batch()
-    # three eager runs estimate the run-to-run spread (one pair is a noisy estimate: graph-vs-eager drifts
-    # of 3-8x a single eager pair's showed up in both graph and eager-only variants of the kernels)
-    eager = [Trainer(_module(family=family), clip_norm=10.0, accum_grad=accum) for _ in range(3)]
+    # four eager runs sample the run-to-run spread (tracks_eager_report)
+    eager = [Trainer(_module(family=family), clip_norm=10.0, accum_grad=accum) for _ in range(4)]
     gr = Trainer(_module(family=family), clip_norm=10.0, graphs=True, graph_warmup=1, accum_grad=accum)
     le = [[] for _ in eager]
     lg = []
@@ -125,60 +124,59 @@ def test_graph_replay_matches_eager(family, accum):
     assert gr._graph is not None, "graph capture fell back to eager"
     assert len(gr._graphs) == min(accum, 3), sorted(gr._graphs)
     assert ea.module.global_step == gr.module.global_step == 1 + 5   # _module() starts at global_step 1
-    # losses: within 4x the largest eager-vs-eager difference (fp32 atomic order in gradient reductions,
-    # amplified by Adam over the steps) plus 1e-3 relative; a stale or missing op in the replay moves
-    # the loss by > 1e-2
-    for s_, b in enumerate(lg):
-        vals = [l[s_] for l in le]
-        spread = max(vals) - min(vals)
-        assert abs(vals[0] - b) <= 1e-3 * max(1.0, abs(b)) + 4 * spread, (le, lg)
     assert len(set(round(x, 6) for x in lg)) > 1, "replayed steps did not train"
-    pe = [dict(t.module.named_parameters()) for t in eager]
-    names = [n for n, p in gr.module.named_parameters() if p.requires_grad and not n.endswith("k_proj.bias")]
-    # k_proj.bias has an exactly-zero gradient (softmax shift invariance): Adam turns the fp32
-    # atomic-order noise of that zero into +-lr steps, so it is not comparable run to run.
-    # Per parameter: within 4x the largest eager-vs-eager drift of the same parameter, or 5e-3 (1-D
-    # biases 1e-2: their gradients are column sums with heavy cancellation); all parameters together:
-    # within 4x the largest eager-vs-eager drift of the whole parameter vector.
-    pg = dict(gr.module.named_parameters())
-    pairs = [(0, 1), (0, 2), (1, 2)]
-    for n in names:
-        e = rel_l2(pg[n].detach().cpu(), pe[0][n].detach().cpu())
-        base = max(rel_l2(pe[i][n].detach().cpu(), pe[j][n].detach().cpu()) for i, j in pairs)
-        floor = 1e-2 if pg[n].dim() == 1 else 5e-3
-        assert e < max(floor, 4 * base), (n, e, base)
-    cat = lambda d: torch.cat([d[n].detach().float().flatten().cpu() for n in names])  # noqa: E731
-    e_all = rel_l2(cat(pg), cat(pe[0]))
-    base_all = max(rel_l2(cat(pe[i]), cat(pe[j])) for i, j in pairs)
-    # (floor 1e-5, as tools/graph_rccl_probe.py: with the student offset from the teacher (_module) the gradients
-    # are smooth in the weights and the eager spread is a fair estimate; a stale or missing op in the replay moves
-    # the whole vector by > 1e-3)
-    assert e_all < max(1e-5, 4 * base_all), (e_all, base_all)
+    _assert_tracks_eager(eager, gr, le, lg)
     # the graph replays follow the LR schedule: optimizer and scheduler state agree
     assert ea.optimizer._step == gr.optimizer._step
     for g1, g2 in zip(ea.optimizer.param_groups, gr.optimizer.param_groups):
         assert g1["lr"] == g2["lr"]
 
 
-def _assert_tracks_eager(eager, gr, le, lg):
-    """The graph trainer's losses and parameters within 4x the eager-vs-eager spread (test_graph_replay_matches_eager's
-    rule)."""
+def tracks_eager_report(eager, gr, le, lg):
+    """Does the graph trainer track the eager ones?  Returns (ok, report lines).
+
+    The eager runs sample the run-to-run spread (fp32 atomic order in gradient reductions, amplified by AdamW on
+    tiny gradients; it is not Gaussian: at a step where some gradient is a cancellation-dominated sum the runs
+    split into two or three clusters, tools/graph_diag.py, profiles/r4_graph_diag_rccl.txt).  The replay is
+    compared with the NEAREST eager run (whole-vector distance) -- one more draw from the same distribution lies
+    within the spread of the others, wherever its cluster -- and must sit within 4x the largest eager-vs-eager
+    difference:
+      * losses: that, plus 1e-3 relative (a stale or missing op in the replay moves the loss by > 1e-2);
+      * each parameter: that, or 5e-3 (1-D biases 1e-2: cancellation-heavy column sums); k_proj.bias is left out
+        (its gradient is exactly zero by softmax shift invariance, so Adam turns the atomic-order noise of that
+        zero into +-lr steps);
+      * the whole parameter vector: that, or 1e-5 (with the student offset from the teacher, _module, the
+        gradients are smooth in the weights; a stale op moves the whole vector by > 1e-3)."""
+    pe = [dict(t.module.named_parameters()) for t in eager]
+    pg = dict(gr.module.named_parameters())
+    names = [n for n, p in gr.module.named_parameters() if p.requires_grad and not n.endswith("k_proj.bias")]
+    cat = lambda d: torch.cat([d[n].detach().float().flatten().cpu() for n in names])  # noqa: E731
+    vg, ve = cat(pg), [cat(d) for d in pe]
+    pairs = [(i, j) for i in range(len(eager)) for j in range(i + 1, len(eager))]
+    near = min(range(len(eager)), key=lambda i: rel_l2(vg, ve[i]))
+    ok, lines = True, []
     for s_, b in enumerate(lg):
         vals = [l[s_] for l in le]
-        spread = max(vals) - min(vals)
-        assert abs(vals[0] - b) <= 1e-3 * max(1.0, abs(b)) + 4 * spread, (le, lg)
-    pe = [dict(t.module.named_parameters()) for t in eager]
-    names = [n for n, p in gr.module.named_parameters() if p.requires_grad and not n.endswith("k_proj.bias")]
-    pg = dict(gr.module.named_parameters())
-    pairs = [(0, 1), (0, 2), (1, 2)]
+        if not abs(vals[near] - b) <= 1e-3 * max(1.0, abs(b)) + 4 * (max(vals) - min(vals)):
+            ok = False
+            lines.append(f"loss step {s_}: graph {b} eager {vals}")
     for n in names:
-        e = rel_l2(pg[n].detach().cpu(), pe[0][n].detach().cpu())
+        e = rel_l2(pg[n].detach().cpu(), pe[near][n].detach().cpu())
         base = max(rel_l2(pe[i][n].detach().cpu(), pe[j][n].detach().cpu()) for i, j in pairs)
-        assert e < max(1e-2 if pg[n].dim() == 1 else 5e-3, 4 * base), (n, e, base)
-    cat = lambda d: torch.cat([d[n].detach().float().flatten().cpu() for n in names])  # noqa: E731
-    e_all = rel_l2(cat(pg), cat(pe[0]))
-    base_all = max(rel_l2(cat(pe[i]), cat(pe[j])) for i, j in pairs)
-    assert e_all < max(1e-5, 4 * base_all), (e_all, base_all)
+        if not e < max(1e-2 if pg[n].dim() == 1 else 5e-3, 4 * base):
+            ok = False
+            lines.append(f"param {n}: graph-vs-eager {e:.3g} eager spread {base:.3g}")
+    e_all = rel_l2(vg, ve[near])
+    base_all = max(rel_l2(ve[i], ve[j]) for i, j in pairs)
+    ok &= e_all < max(1e-5, 4 * base_all)
+    lines.append(f"whole vector: graph vs nearest eager run ({near}) {e_all:.3g}, largest eager-vs-eager "
+                 f"{base_all:.3g}, eager runs to run 0 {[round(rel_l2(v, ve[0]), 8) for v in ve[1:]]}")
+    return ok, lines
+
+
+def _assert_tracks_eager(eager, gr, le, lg):
+    ok, lines = tracks_eager_report(eager, gr, le, lg)
+    assert ok, "\n".join(lines + [f"eager losses {le}", f"graph losses {lg}"])
 
 
 def test_ffn_compaction_switch_under_graphs():
@@ -189,7 +187,7 @@ def test_ffn_compaction_switch_under_graphs():
     from dphubert_amd.trainer import Trainer
     batch = _batch()
     mk = lambda graphs: Trainer(_module(), clip_norm=10.0, graphs=graphs, graph_warmup=1)  # noqa: E731
-    eager = [mk(False) for _ in range(3)]
+    eager = [mk(False) for _ in range(4)]
     gr = mk(True)
     for t in eager + [gr]:
         t.FFN_COMPACT_EVERY = 3          # decisions at global steps 1, 4, 7 (_module() starts at 1)
