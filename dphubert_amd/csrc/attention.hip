@@ -115,6 +115,19 @@ __device__ __forceinline__ uint32_t seed_mix(uint64_t seed) {
 }
 __device__ __forceinline__ uint32_t attn_hash32(uint32_t mix, uint32_t pair) { return hash32(pair ^ mix); }
 
+// packed-16 dropout test of one pair hash: 0xffff in each half whose 16 bits are below thr (dropped), else 0.
+// (bits ^ 0x8000) - (thr - 0x8000) is the signed difference bits - thr shifted into int16 range; the saturating
+// subtract keeps its sign, the arithmetic shift spreads it.  thr <= 65535 (p < 1).
+typedef short s16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ s16x2_t drop_thr2(uint32_t thr) {
+  const short t = (short)((int)min(thr, 65535u) - 32768);
+  return s16x2_t{t, t};
+}
+__device__ __forceinline__ uint32_t drop_mask2(uint32_t bits, s16x2_t thr2) {
+  const s16x2_t d = __builtin_elementwise_sub_sat(__builtin_bit_cast(s16x2_t, bits ^ 0x80008000u), thr2);
+  return __builtin_bit_cast(uint32_t, d >> (short)15);
+}
+
 // Stored keep bits (forward -> backward): uint16 word (row, key tile kt, lane group g) holds the keep bit of
 // key kt*64 + 16 s + 4 g + i at bit 4 s + i -- exactly the 16 keys lane group g of a row owns in the forward
 // and dQ MFMA layouts, so those kernels move one aligned uint16 per row and tile, and the dK/dV kernel reads
@@ -614,7 +627,14 @@ __global__ void __launch_bounds__(256, 2) attn_fwd32_kernel(const bf16_t* __rest
 //    the mask zeroes);
 //  * the eight K fragments of a tile are read before its first MFMA (the compiler otherwise waited
 //    lgkmcnt(0) on each read in front of its MFMA);
-//  * the row sum is four interleaved chains instead of one 32-deep dependent chain.
+//  * the row sum is four interleaved chains instead of one 32-deep dependent chain;
+//  * P is packed to bf16 pairs as soon as it is computed and the dropout is applied to the packed word
+//    (drop_mask2: three packed-16 ops per hashed key pair, 41 -> 40.8 us with stored keep bits);
+//  * the staged K / V rows live in four named registers (as an array captured by the lambdas they were
+//    demoted to 80 B per lane of scratch: 47.4 -> 31.1 us at p = 0, profiles/r4_s4_attn_fwd_ab.txt).
+// Where the rest goes (B = 16, T = 499, p = 0, profiles/r4_s6_attn_fwd_breakdown.txt, knobs since removed):
+// without the fp32 o_u store 27.2 us, without any output store 24.2, without the K / V loads past the first
+// tile 27.9, with exp2 replaced by its argument 29.1, with all of these 20.3 -- the MFMA work alone is 4.9 us.
 // Same arithmetic per score as attn_fwd32_kernel; keep bits in the same layout (tiles past the key length
 // are not written: their probabilities are 0 and the backward multiplies whatever it reads there by 0).
 // ---------------------------------------------------------------------------
@@ -664,6 +684,7 @@ __global__ void __launch_bounds__(256, 3) attn_fwd32v2_kernel(const bf16_t* __re
   float m_run = -INFINITY, l_run = 0.f;
   const float inv_keep = DROP ? 1.f / (1.f - drop_p) : 1.f;
   const uint32_t thr = drop_thr(drop_p);
+  const s16x2_t thr2 = drop_thr2(thr);
   const int nkt = (T32 + KT - 1) / KT;                      // keep-word stride (layout of every tile)
   const int kend = (klen >= 1 && klen < T32) ? klen : T32;  // keys that can carry probability
   const int ntile = (kend + KT - 1) / KT;
@@ -743,36 +764,41 @@ __global__ void __launch_bounds__(256, 3) attn_fwd32v2_kernel(const bf16_t* __re
     }
     const float ml = m_run * L2E;
     float ls[4] = {0.f, 0.f, 0.f, 0.f};
-    uint32_t kw[2] = {0u, 0u};
+    // P packed to bf16 pairs right away (keys 2m, 2m+1 -- the pair one hash draws for), the dropout applied
+    // to the packed word: per 16-bit half, (bits ^ 0x8000) - (thr - 0x8000) saturating is negative exactly when
+    // bits < thr, and its arithmetic shift by 15 is the half's drop mask.  Three packed-16 ops and two bitops
+    // per PAIR instead of an extract / compare / select / bit-insert per score.
+    uint32_t pw[2][4][2];
+    uint32_t kd[2] = {0u, 0u};   // DROP bits of the rq-even / rq-odd stored words: even key low half, odd high
 #pragma unroll
     for (int k2 = 0; k2 < 2; ++k2)
 #pragma unroll
       for (int rq = 0; rq < 4; ++rq) {
-        uint32_t hb[2] = {0u, 0u};
-        if constexpr (DROP) {
-          const uint32_t pr = hrow + (uint32_t)((kb + 32 * k2 + 8 * rq) >> 1);
-          hb[0] = attn_hash32(mix, pr);
-          hb[1] = attn_hash32(mix, pr + 1);
-        }
+        float pv[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int r = 4 * rq + i;
-          const float p = __builtin_amdgcn_exp2f(fmaf(sacc[k2][r], L2E, -ml));
-          ls[i] += p;
+          pv[i] = __builtin_amdgcn_exp2f(fmaf(sacc[k2][r], L2E, -ml));
+          ls[i] += pv[i];
+        }
+#pragma unroll
+        for (int pi = 0; pi < 2; ++pi) {
+          uint32_t w = pack2bf(pv[2 * pi], pv[2 * pi + 1]);
           if constexpr (DROP) {
-            const bool keep = ((i & 1) ? (hb[i >> 1] >> 16) : (hb[i >> 1] & 0xffffu)) >= thr;
-            kw[rq & 1] |= (keep ? 1u : 0u) << (4 * (2 * k2 + (rq >> 1)) + i);
-            sacc[k2][r] = keep ? p : 0.f;
-          } else {
-            sacc[k2][r] = p;
+            const uint32_t hsh = attn_hash32(mix, hrow + (uint32_t)((kb + 32 * k2 + 8 * rq) >> 1) + pi);
+            const uint32_t m = drop_mask2(hsh, thr2);
+            w &= ~m;
+            const int bt = 4 * (2 * k2 + (rq >> 1)) + 2 * pi;
+            kd[rq & 1] |= m & ((1u << bt) | (1u << (17 + bt)));
           }
+          pw[k2][rq][pi] = w;
         }
       }
     if constexpr (DROP) {
       if (keep_out != nullptr && q < T32) {
         uint16_t* kp = keep_out + ((int64_t)(b * H + h) * T32 + q) * (nkt * 4) + kt * 4;
-        kp[hi] = (uint16_t)kw[0];
-        kp[2 + hi] = (uint16_t)kw[1];
+        kp[hi] = (uint16_t)~(kd[0] | (kd[0] >> 16));
+        kp[2 + hi] = (uint16_t)~(kd[1] | (kd[1] >> 16));
       }
     }
     float lsum = (ls[0] + ls[1]) + (ls[2] + ls[3]);
@@ -782,7 +808,8 @@ __global__ void __launch_bounds__(256, 3) attn_fwd32v2_kernel(const bf16_t* __re
     for (int k2 = 0; k2 < 2; ++k2)
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
-        const bf16x8_t pf = pack8(sacc[k2], 8 * e);
+        const uint4 pq = make_uint4(pw[k2][2 * e][0], pw[k2][2 * e][1], pw[k2][2 * e + 1][0], pw[k2][2 * e + 1][1]);
+        const bf16x8_t pf = __builtin_bit_cast(bf16x8_t, pq);
         const int base = 32 * k2 + 16 * e + 4 * hi;
 #pragma unroll
         for (int d = 0; d < 2; ++d) {

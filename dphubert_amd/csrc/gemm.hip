@@ -2673,6 +2673,17 @@ static int pp_pick(const DphGemmArgs& a) {
   static const Opt opts[] = {{12, 256, 256, 1, 1514.0}, {15, 128, 192, 1, 1282.0}, {13, 128, 256, 1, 1221.0},
                              {14, 256, 128, 1, 1211.0}, {16, 128, 128, 2, 1178.0}};
   const int64_t cus = num_cus();
+  // DPH_PP_FORCE=kind (A/B sweeps, read per call): that tile whenever the ping-pong path runs
+  if (const char* e = getenv("DPH_PP_FORCE")) {
+    const int fk = atoi(e);
+    for (const Opt& o : opts)
+      if (o.kind == fk) return fk;
+  }
+  // FFN-width GELU epilogues (the intermediate forward with its stored factor, the DGK input gradient): the
+  // epilogue outweighs the 12 K-tiles of MFMA work, and the two-blocks-per-CU 128 x 128 tile runs one block's
+  // epilogue beside the other's main loop: 62.5 / 57.6 / 54.3 us vs 70.2 / 64.3 / 61.9 on 128 x 192
+  // (student FFN1 / teacher FFN1 / FFN2 DGK dgrad at 7984 x 3072 x 768, profiles/r4_s8_pp_tile_ab.txt)
+  if (a.act != DPH_ACT_NONE && a.N >= 2048 && a.K <= 1024 && a.batch == 1) return 16;
   int best = 12;
   double best_t = 1e300;
   for (const Opt& o : opts) {

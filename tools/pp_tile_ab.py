@@ -1,0 +1,78 @@
+"""Ping-pong tile A/B on the step's projection GEMMs WITH their epilogues (GELU + stored factor + dropout, fp32
+residual stream, DGK input gradient): every tile kind forced through DPH_PP_FORCE (read per call), interleaved
+rounds, median us per (shape, tile).  usage: python tools/pp_tile_ab.py [rounds] [kind ...]
+kinds: 12 = 256x256, 13 = 128x256, 14 = 256x128, 15 = 128x192, 16 = 128x128 (two blocks per CU)."""
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+from dphubert_amd import kernels as K  # noqa: E402
+
+M = 16 * 499
+dev = "cuda"
+bf = lambda *s: (torch.rand(*s, device=dev) * 2 - 1).to(torch.bfloat16)  # noqa: E731
+
+
+def case(name, n, k, **epi):
+    return name, n, k, epi
+
+
+u = torch.empty(M, 3072, device=dev, dtype=torch.bfloat16)
+cm = torch.rand(3072, device=dev) + 0.5
+res32 = torch.randn(M, 768, device=dev)
+CASES = [
+    case("ffn1 fwd student (gelu, gelu' factor, mask, dropout)", 3072, 768, act=K.ACT_GELU, pre_out=u, colmask=cm,
+         dropout_p=0.1, seed=3, flags=K.GEMM_PRE_DGK, bias=True),
+    case("ffn1 fwd teacher (gelu, pre)", 3072, 768, act=K.ACT_GELU, pre_out=u, bias=True),
+    case("ffn2 dgrad DGK", 3072, 768, act=K.ACT_GELU_BWD_DGK, aux_in=u),
+    case("qkv fwd", 2304, 768, bias=True),
+    case("ffn2 fwd (fp32 residual)", 768, 3072, residual=res32, c_dtype=K.OUT_F32, bias=True),
+    case("oproj fwd (fp32 residual)", 768, 768, residual=res32, c_dtype=K.OUT_F32, bias=True),
+    case("ffn1 dgrad", 768, 3072),
+    case("qkv dgrad", 768, 2304),
+]
+rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+kinds = sys.argv[2:] or ["auto", "15", "16", "13", "12", "14"]
+data = {}
+for name, n, k, epi in CASES:
+    A, B = bf(M, k), bf(n, k)
+    odt = torch.float32 if epi.get("c_dtype") == K.OUT_F32 else torch.bfloat16
+    C = torch.empty(M, n, device=dev, dtype=odt)
+    kw = dict(epi)
+    if kw.pop("bias", False):
+        kw["bias"] = torch.randn(n, device=dev)
+    data[name] = (A, B, C, n, k, kw)
+
+
+def run(name, kind, iters=20):
+    if kind == "auto":
+        os.environ.pop("DPH_PP_FORCE", None)
+    else:
+        os.environ["DPH_PP_FORCE"] = kind
+    A, B, C, n, k, kw = data[name]
+    f = lambda: K.gemm(K.dense(A), K.dense(B), K.dense(C), M, n, k, a_kcontig=True, b_kcontig=True, **kw)  # noqa
+    f()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        f()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters * 1e3
+
+
+res = {}
+for _ in range(rounds):
+    for name, *_r in CASES:
+        for kd in kinds:
+            res.setdefault((name, kd), []).append(run(name, kd))
+os.environ.pop("DPH_PP_FORCE", None)
+for name, n, k, _e in CASES:
+    fl = 2.0 * M * n * k
+    row = " | ".join(f"{kd} {statistics.median(res[(name, kd)]):6.1f}" for kd in kinds)
+    best = min(kinds, key=lambda kd: statistics.median(res[(name, kd)]))
+    print(f"{name:52s} {M}x{n}x{k}: {row}  (best {best}: "
+          f"{fl / statistics.median(res[(name, best)]) / 1e6:5.0f} TF/s)", flush=True)
