@@ -8,9 +8,9 @@
 // instead of ever storing its pre-norm output, so the only HBM traffic is the
 // bf16 layer output (and its gradient in backward).
 //
-// Statistics: per (utterance, channel) over L0 = floor((S-k0)/s0)+1 steps,
-// chunk-local two-pass (mean, M2) merged with Chan's formula -> torch
-// group_norm numerics (biased variance, eps=1e-5).
+// Statistics: per (utterance, channel) over L0 = floor((S-k0)/s0)+1 steps, in closed form
+// from the waveform's per-utterance tap sums and 10 x 10 Gram matrix (fp64, conv0_gram_reduce):
+// biased variance, eps = 1e-5, as torch.group_norm.
 //
 // Weight norm (components.py:306, dim=2): w = g * v / ||v||_(dims 0,1).
 #include "common.h"
@@ -24,7 +24,6 @@ namespace {
 constexpr int K0 = 10;
 constexpr int S0 = 5;
 static_assert(K0 == 2 * S0, "sliding window assumes k0 = 2*s0");
-constexpr int STAT_CH = 256;     // time steps per stats chunk
 constexpr int APPLY_ROWS = 256;  // time steps per apply block
 constexpr int BWD_ROWS = 512;    // time steps per backward block
 
@@ -83,112 +82,6 @@ __device__ __forceinline__ int stage_wave(float* xs, const float* wave, const Co
   for (int i = threadIdx.x; i < nsamp; i += blockDim.x) xs[i] = xw[i];
   __syncthreads();
   return nsamp;
-}
-
-// Partial statistics per (utterance, chunk of STAT_CH steps, channel): shifted sums around the
-// chunk's first conv value (stable), written as (chunk mean, M2) for a Chan merge.
-// ws[((b*nch + ch)*C + c)*2 + {0,1}]
-__global__ void __launch_bounds__(256) conv0_stats_kernel(const float* __restrict__ wave, const float* __restrict__ w,
-                                                          Conv0 p, float* __restrict__ ws, int nch) {
-  constexpr int CPT = 8;
-  __shared__ float xs[STAT_CH * S0 + K0];
-  __shared__ float red[256 * CPT * 2];
-  const int64_t b = blockIdx.y;
-  const int ch = blockIdx.x;
-  const int64_t t0 = (int64_t)ch * STAT_CH;
-  const int nt = (int)min<int64_t>(STAT_CH, p.L0 - t0);
-  stage_wave(xs, wave, p, b, t0, nt);
-  RowLayout<CPT> L(p.C);
-  const int tid = threadIdx.x;
-  const bool active = tid < L.tpr * L.rpp;
-  const int64_t c0 = active ? (int64_t)(tid % L.tpr) * CPT : 0;
-  const int r0 = active ? tid / L.tpr : 0;
-  float wr[CPT][K0];
-  load_taps<CPT>(wr, w, c0, p.C, active);
-  float x[K0], sh[CPT], s1[CPT], s2[CPT];
-  win_load(x, xs, 0);
-  fir<CPT>(wr, x, sh);          // shift = conv value at the chunk's first step
-#pragma unroll
-  for (int i = 0; i < CPT; ++i) s1[i] = s2[i] = 0.f;
-  const int nper = (nt + L.rpp - 1) / L.rpp;
-  const int ta = r0 * nper;
-  const int tb = min(nt, ta + nper);
-  if (active && ta < tb) {
-    win_load(x, xs, ta);
-    for (int t = ta; t < tb; ++t) {
-      float v[CPT];
-      fir<CPT>(wr, x, v);
-#pragma unroll
-      for (int i = 0; i < CPT; ++i) {
-        const float d = v[i] - sh[i];
-        s1[i] += d;
-        s2[i] = fmaf(d, d, s2[i]);
-      }
-      if (t + 1 < tb) win_advance(x, xs, t);
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < CPT; ++i) {
-    red[(tid * CPT + i) * 2 + 0] = s1[i];
-    red[(tid * CPT + i) * 2 + 1] = s2[i];
-  }
-  __syncthreads();
-  if (active && r0 == 0) {
-#pragma unroll
-    for (int i = 0; i < CPT; ++i) {
-      float a = 0.f, q = 0.f;
-      for (int r = 0; r < L.rpp; ++r) {
-        const int tt = r * L.tpr + (tid % L.tpr);
-        a += red[(tt * CPT + i) * 2 + 0];
-        q += red[(tt * CPT + i) * 2 + 1];
-      }
-      const int64_t c = c0 + i;
-      if (c < p.C) {
-        const float m = a / nt;
-        float* o = ws + ((b * nch + ch) * p.C + c) * 2;
-        o[0] = sh[i] + m;
-        o[1] = fmaxf(q - a * m, 0.f);
-      }
-    }
-  }
-}
-
-// GroupNorm statistics of (b, c) from its per-chunk (mean, M2) pairs, in fp64 as shifted sums around the
-// first chunk's mean m0: S1 = sum n_b (m_b - m0), S2 = sum M2_b + n_b (m_b - m0)^2, mean = m0 + S1 / N,
-// M2 = S2 - S1^2 / N (no division per chunk).  A block is 64 channels of one utterance; its 4 waves take
-// every 4th chunk (coalesced 8-B reads along the channels) and are summed through LDS.  (The previous
-// thread-per-(b, c) Chan merge -- 32 blocks, a dependent fp64 division chain over ~125 chunks -- took
-// 48 us per launch.)
-__global__ void __launch_bounds__(256) conv0_stats_finalize(const float* __restrict__ ws, Conv0 p, int nch,
-                                                            float* __restrict__ mean, float* __restrict__ rstd,
-                                                            float eps) {
-  __shared__ double part[4][64][2];
-  const int lane = threadIdx.x & 63;
-  const int wv = threadIdx.x >> 6;
-  const int64_t b = blockIdx.y;
-  const int64_t c = (int64_t)blockIdx.x * 64 + lane;
-  const bool ok = c < p.C;
-  const double m0 = ok ? (double)ws[((b * nch) * p.C + c) * 2] : 0.0;
-  double s1 = 0.0, s2 = 0.0;
-  if (ok) {
-    for (int ch = wv; ch < nch; ch += 4) {
-      const double nb = (double)min<int64_t>(STAT_CH, p.L0 - (int64_t)ch * STAT_CH);
-      const float2 o = *reinterpret_cast<const float2*>(ws + ((b * nch + ch) * p.C + c) * 2);
-      const double d = (double)o.x - m0;
-      s1 = fma(nb, d, s1);
-      s2 += fma(nb * d, d, (double)o.y);
-    }
-  }
-  part[wv][lane][0] = s1;
-  part[wv][lane][1] = s2;
-  __syncthreads();
-  if (wv != 0 || !ok) return;
-  s1 = part[0][lane][0] + part[1][lane][0] + part[2][lane][0] + part[3][lane][0];
-  s2 = part[0][lane][1] + part[1][lane][1] + part[2][lane][1] + part[3][lane][1];
-  const double N = (double)p.L0;
-  const double M2 = fmax(s2 - s1 * s1 / N, 0.0);
-  mean[b * p.C + c] = (float)(m0 + s1 / N);
-  rstd[b * p.C + c] = (float)(1.0 / sqrt(M2 / N + (double)eps));
 }
 
 // VEC: C % 8 == 0, every thread's 8 channels one 16-byte store (no per-row branch)
@@ -290,7 +183,7 @@ __device__ __forceinline__ void load_dyc(const bf16_t* dyp, int64_t c0, int64_t 
 //   dw[c][j] = sum_b rstd*(P_j - (A/N)*S_j - (Bv/N)*Q_j),
 //   P_j = sum_t dxh*x_j (accumulated here), S_j = sum_t x_j and
 //   Q_j = sum_t xh*x_j = rstd*(sum_k w[c][k]*G[k][j] - mean*S_j) from the per-utterance Gram matrix
-//   G[k][j] = sum_t x_k*x_j of the waveform (conv0_gram_kernel).
+//   G[k][j] = sum_t x_k*x_j of the waveform (conv0_gram_part_kernel + conv0_gram_reduce).
 // So the old second pass (recompute conv0 + GELU' + dconv) disappears.  Per (b, c) the blocks add
 // their 15 partial sums (P[10], A, Bv, dgamma, dbeta, dmask) into ws with fp32 atomics (63 time
 // blocks per address), conv0_bwd_finalize combines them.  dy is prefetched 4 time steps ahead.
@@ -361,14 +254,12 @@ __global__ void __launch_bounds__(256) conv0_gn_bwd_kernel(const float* __restri
         gelu_and_grad(g.x, gl0, gd0);
         gelu_and_grad(g.y, gl1, gd1);
         const f32x2_t cu = {d[i0], d[i1]};
-        const f32x2_t dg = cu * f32x2_t{mk[i0], mk[i1]} * f32x2_t{gd0, gd1};
-        const f32x2_t dxh = dg * f32x2_t{ga[i0], ga[i1]};
+        // dg' = dy GELU'(g): the channel's mask and gamma are factored out of every sum (applied per block)
+        const f32x2_t dgp = cu * f32x2_t{gd0, gd1};
 #pragma unroll
-        for (int j = 0; j < K0; ++j) acc2[pi][j] = __builtin_elementwise_fma(dxh, f32x2_t{x[j], x[j]}, acc2[pi][j]);
-        acc2[pi][10] += dxh;
-        acc2[pi][11] = __builtin_elementwise_fma(dxh, xh, acc2[pi][11]);
-        acc2[pi][12] = __builtin_elementwise_fma(dg, xh, acc2[pi][12]);
-        acc2[pi][13] += dg;
+        for (int j = 0; j < K0; ++j) acc2[pi][j] = __builtin_elementwise_fma(dgp, f32x2_t{x[j], x[j]}, acc2[pi][j]);
+        acc2[pi][10] += dgp;
+        acc2[pi][11] = __builtin_elementwise_fma(dgp, xh, acc2[pi][11]);
         acc2[pi][14] = __builtin_elementwise_fma(cu, f32x2_t{gl0, gl1}, acc2[pi][14]);
       }
     } else {
@@ -380,14 +271,11 @@ __global__ void __launch_bounds__(256) conv0_gn_bwd_kernel(const float* __restri
         const float g = fmaf(ga[i], xh, be[i]);
         float gl, gd;
         gelu_and_grad(g, gl, gd);
-        const float dg = d[i] * mk[i] * gd;
-        const float dxh = dg * ga[i];
+        const float dgp = d[i] * gd;
 #pragma unroll
-        for (int j = 0; j < K0; ++j) acc[i][j] = fmaf(dxh, x[j], acc[i][j]);
-        acc[i][10] += dxh;
-        acc[i][11] = fmaf(dxh, xh, acc[i][11]);
-        acc[i][12] = fmaf(dg, xh, acc[i][12]);
-        acc[i][13] += dg;
+        for (int j = 0; j < K0; ++j) acc[i][j] = fmaf(dgp, x[j], acc[i][j]);
+        acc[i][10] += dgp;
+        acc[i][11] = fmaf(dgp, xh, acc[i][11]);
         acc[i][14] = fmaf(d[i], gl, acc[i][14]);
       }
     }
@@ -437,6 +325,7 @@ __global__ void __launch_bounds__(256) conv0_gn_bwd_kernel(const float* __restri
   // reduce over the rpp thread-rows sharing the same channels, then one atomic per (b, c, q) per block
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
+    if (q == 12 || q == 13) continue;   // derived from 10 / 11 below
 #pragma unroll
     for (int i = 0; i < CPT; ++i) red[tid * CPT + i] = acc[i][q];
     __syncthreads();
@@ -446,7 +335,24 @@ __global__ void __launch_bounds__(256) conv0_gn_bwd_kernel(const float* __restri
         float s = 0.f;
         for (int r = 0; r < L.rpp; ++r) s += red[(r * L.tpr + (tid % L.tpr)) * CPT + i];
         const int64_t c = c0 + i;
-        if (c < p.C) atomicAdd(sums + (b * p.C + c) * NQ + q, s);
+        // acc q: 0-9 sum dg' x_j, 10 sum dg', 11 sum dg' xh, 14 sum dy GELU(g) (12, 13 unused) -> the 15 sums
+        // conv0_bwd_finalize reads: P_j = ga mk (0-9), A = ga mk S1, Bv = ga mk T2, dgamma = mk T2,
+        // dbeta = mk S1, dmask
+        if (c < p.C && q != 12 && q != 13) {
+          const float gm = ga[i] * mk[i];
+          float* o = sums + (b * p.C + c) * NQ;
+          if (q < 10) {
+            atomicAdd(o + q, gm * s);
+          } else if (q == 10) {
+            atomicAdd(o + 10, gm * s);
+            atomicAdd(o + 13, mk[i] * s);
+          } else if (q == 11) {
+            atomicAdd(o + 11, gm * s);
+            atomicAdd(o + 12, mk[i] * s);
+          } else {
+            atomicAdd(o + 14, s);
+          }
+        }
       }
     }
     __syncthreads();
@@ -518,25 +424,28 @@ __global__ void __launch_bounds__(256) conv0_plain_bwd_kernel(const float* __res
 }
 
 // per utterance: S[j] = sum_t x_j[t], G[k][j] = sum_t x_k[t] x_j[t] (x_j[t] = wave[s0*t + j], t < L0),
-// fp64, packed: gram[b][0..9] = S, gram[b][10 + j*(j+1)/2 + k] = G[k][j] (k <= j).  Grid (chunks of
-// GRAM_ROWS time steps, B); blocks add their partial sums with fp64 atomics (gram zeroed first).
+// fp64, packed: gram[b][0..9] = S, gram[b][10 + j*(j+1)/2 + k] = G[k][j] (k <= j).
 constexpr int NG = K0 + K0 * (K0 + 1) / 2;   // 65
-constexpr int GRAM_ROWS = 2048;
+constexpr int GRAM_CHUNKS = 16;   // fixed split of an utterance's steps (the workspace size does not depend on S)
 
 __device__ __forceinline__ int gram_idx(int k, int j) {   // symmetric
   return k <= j ? K0 + j * (j + 1) / 2 + k : K0 + k * (k + 1) / 2 + j;
 }
 
-__global__ void __launch_bounds__(256) conv0_gram_kernel(const float* __restrict__ wave, Conv0 p,
-                                                         double* __restrict__ gram) {
+// Block (chunk, b) of a fixed GRAM_CHUNKS-way split of utterance b's steps writes its partial sums to
+// gpart[(b * GRAM_CHUNKS + chunk) * NG + q]; conv0_gram_reduce adds them in chunk order (no atomics: the forward's
+// GroupNorm statistics below are bitwise reproducible).
+__global__ void __launch_bounds__(256) conv0_gram_part_kernel(const float* __restrict__ wave, Conv0 p,
+                                                              double* __restrict__ gpart) {
   __shared__ double red[4][NG];
   const int64_t b = blockIdx.y;
   const float* xw = wave + b * p.S;
-  const int64_t t1 = min<int64_t>(p.L0, (int64_t)(blockIdx.x + 1) * GRAM_ROWS);
+  const int64_t per = cdiv(p.L0, (int64_t)GRAM_CHUNKS);
+  const int64_t t1 = min<int64_t>(p.L0, (int64_t)(blockIdx.x + 1) * per);
   double acc[NG];
 #pragma unroll
   for (int q = 0; q < NG; ++q) acc[q] = 0.0;
-  for (int64_t t = (int64_t)blockIdx.x * GRAM_ROWS + threadIdx.x; t < t1; t += 256) {
+  for (int64_t t = (int64_t)blockIdx.x * per + threadIdx.x; t < t1; t += 256) {
     float x[K0];
 #pragma unroll
     for (int j = 0; j < K0; ++j) x[j] = xw[t * S0 + j];
@@ -556,7 +465,46 @@ __global__ void __launch_bounds__(256) conv0_gram_kernel(const float* __restrict
   }
   __syncthreads();
   for (int q = threadIdx.x; q < NG; q += 256)
-    atomicAdd(gram + b * NG + q, (red[0][q] + red[1][q]) + (red[2][q] + red[3][q]));
+    gpart[(b * GRAM_CHUNKS + blockIdx.x) * NG + q] = (red[0][q] + red[1][q]) + (red[2][q] + red[3][q]);
+}
+
+// One block per utterance: gram[b] = the chunk partials summed in order (optional output), and -- with mean / rstd
+// given -- the GroupNorm(C, C) statistics of conv0's output in closed form.  Channel c's conv value at step t is
+// v = sum_j w[c][j] x_j[t], so over the N = L0 steps (the whole padded sequence, as torch.group_norm takes it)
+//   mean = sum_j w_j S_j / N,   E[v^2] = sum_jk w_j w_k G_jk / N,   var = E[v^2] - mean^2   (biased, fp64)
+// from the waveform's per-utterance sums S_j and Gram matrix G_jk: no pass over the B x L0 x C conv outputs.
+__global__ void __launch_bounds__(256) conv0_gram_reduce(const double* __restrict__ gpart, const float* __restrict__ w,
+                                                         Conv0 p, double* __restrict__ gram, float* __restrict__ mean,
+                                                         float* __restrict__ rstd, float eps) {
+  __shared__ double g[NG];
+  const int64_t b = blockIdx.x;
+  for (int q = threadIdx.x; q < NG; q += 256) {
+    double v = 0.0;
+    for (int ch = 0; ch < GRAM_CHUNKS; ++ch) v += gpart[(b * GRAM_CHUNKS + ch) * NG + q];
+    g[q] = v;
+    if (gram) gram[b * NG + q] = v;
+  }
+  __syncthreads();
+  if (!mean) return;
+  const double N = (double)p.L0;
+  for (int64_t c = threadIdx.x; c < p.C; c += 256) {
+    double wj[K0];
+#pragma unroll
+    for (int j = 0; j < K0; ++j) wj[j] = (double)w[c * K0 + j];
+    double m = 0.0, e2 = 0.0;
+#pragma unroll
+    for (int j = 0; j < K0; ++j) {
+      m = fma(wj[j], g[j], m);
+      double r = 0.0;
+#pragma unroll
+      for (int k = 0; k < j; ++k) r = fma(wj[k], g[K0 + j * (j + 1) / 2 + k], r);
+      e2 = fma(wj[j], fma(2.0, r, wj[j] * g[K0 + j * (j + 1) / 2 + j]), e2);
+    }
+    m /= N;
+    const double var = fmax(e2 / N - m * m, 0.0);
+    mean[b * p.C + c] = (float)m;
+    rstd[b * p.C + c] = (float)(1.0 / sqrt(var + (double)eps));
+  }
 }
 
 // one thread per channel: combine the per-(b,c) sums into dw[c][j], dgamma, dbeta, dmask (accumulate)
@@ -696,10 +644,11 @@ extern "C" int dph_conv0_gn_fwd(const float* wave, int64_t B, int64_t S, const f
   }
   DPH_REQUIRE(S >= K0 && C <= 2048, "dph_conv0_gn_fwd: unsupported S=%lld C=%lld", (long long)S, (long long)C);
   Conv0 p = make_conv0(B, S, C);
-  const int nch = (int)cdiv(p.L0, STAT_CH);
-  DPH_REQUIRE(ws_bytes >= (int64_t)B * nch * C * 2 * 4, "dph_conv0_gn_fwd: workspace too small");
-  hipLaunchKernelGGL(conv0_stats_kernel, dim3(nch, (unsigned)B), dim3(256), 0, stream, wave, w, p, ws, nch);
-  hipLaunchKernelGGL(conv0_stats_finalize, dim3((unsigned)cdiv(C, 64), (unsigned)B), dim3(256), 0, stream, ws, p, nch, mean,
+  DPH_REQUIRE(ws_bytes >= (int64_t)B * GRAM_CHUNKS * NG * 8, "dph_conv0_gn_fwd: workspace too small (%lld < %lld)",
+              (long long)ws_bytes, (long long)(B * GRAM_CHUNKS * NG * 8));
+  double* gpart = reinterpret_cast<double*>(ws);
+  hipLaunchKernelGGL(conv0_gram_part_kernel, dim3(GRAM_CHUNKS, (unsigned)B), dim3(256), 0, stream, wave, p, gpart);
+  hipLaunchKernelGGL(conv0_gram_reduce, dim3((unsigned)B), dim3(256), 0, stream, gpart, w, p, (double*)nullptr, mean,
                      rstd, 1e-5f);
   const dim3 grid((unsigned)cdiv(p.L0, APPLY_ROWS), (unsigned)B);
   if (C % 8 == 0)
@@ -748,7 +697,7 @@ extern "C" int dph_conv0_bwd(const float* wave, int64_t B, int64_t S, int64_t C,
 }
 
 extern "C" int64_t dph_conv0_gn_bwd_workspace(int64_t B, int64_t C) {
-  return cdiv(B * C * NQ * 4, 64) * 64 + B * NG * 8;
+  return cdiv(B * C * NQ * 4, 64) * 64 + B * NG * 8 + B * GRAM_CHUNKS * NG * 8;
 }
 
 extern "C" int dph_conv0_gn_bwd(const float* wave, int64_t B, int64_t S, const float* w, int64_t C, int64_t k0,
@@ -768,11 +717,13 @@ extern "C" int dph_conv0_gn_bwd(const float* wave, int64_t B, int64_t S, const f
   float* sums = ws;
   const int64_t sums_bytes = cdiv(B * C * NQ * 4, 64) * 64;
   double* gram = reinterpret_cast<double*>(reinterpret_cast<char*>(ws) + sums_bytes);
-  zero_async(ws, sums_bytes + B * NG * 8, stream);
-  hipLaunchKernelGGL(conv0_gram_kernel, dim3((unsigned)cdiv(p.L0, GRAM_ROWS), (unsigned)B), dim3(256), 0, stream,
-                     wave, p, gram);
-  // DPH_C0B_VARIANT (tuning knob): 0 = 4 channels/thread, 4-row dy prefetch, 512 rows/block;
-  // 1 = 2 ch/thread; 2 = 4 ch, 1-row prefetch; 3 = 4 ch, 256 rows/block
+  double* gpart = gram + B * NG;
+  zero_async(ws, sums_bytes, stream);
+  hipLaunchKernelGGL(conv0_gram_part_kernel, dim3(GRAM_CHUNKS, (unsigned)B), dim3(256), 0, stream, wave, p, gpart);
+  hipLaunchKernelGGL(conv0_gram_reduce, dim3((unsigned)B), dim3(256), 0, stream, gpart, w, p, gram, (float*)nullptr,
+                     (float*)nullptr, 0.f);
+  // DPH_C0B_VARIANT (tuning knob): 0 = 4 channels/thread, 4-row dy prefetch, 512 rows/block; 1 = 2 ch/thread;
+  // 2 = 4 ch, 1-row prefetch; 3 = 4 ch, 256 rows/block
   static const int var = [] {
     const char* e = getenv("DPH_C0B_VARIANT");
     return e ? atoi(e) : 0;

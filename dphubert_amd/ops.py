@@ -971,8 +971,7 @@ class FrontendFn(torch.autograd.Function):
         y = torch.empty(B * Ls[0], C0p, dtype=BF16, device=dev)
         mean = torch.empty(B, C0p, dtype=F32, device=dev)
         rstd = torch.empty(B, C0p, dtype=F32, device=dev)
-        nch = -(-Ls[0] // 256)
-        ws = torch.empty(B * nch * C0p * 2, dtype=F32, device=dev)
+        ws = torch.empty(B * 16 * 65 * 2, dtype=F32, device=dev)   # per-(utterance, chunk) fp64 Gram partials
         call("dph_conv0_gn_fwd", ptr(wave), B, S, ptr(w0), C0p, k0, s0, ptr(g0), ptr(b0), ptr(m0),
              ptr(y), ptr(mean), ptr(rstd), ptr(ws), ws.numel() * 4, _s())
         ys, zs, imgs, cms = [y], [None], [None], [m0]

@@ -314,6 +314,8 @@ int dph_wavlm_gate_bwd(const void* x, int64_t ldx, const float* w, const float* 
  * 1071-1076): conv0 (1 -> C, kernel k0, stride s0, no bias) + GroupNorm(C,C)
  * + GELU + HardConcrete channel mask, output channels-last bf16 [B][L][C].
  * ------------------------------------------------------------------------ */
+/* mean / rstd [B][C]: the GroupNorm statistics, computed in closed form from the waveform's per-utterance tap
+ * sums and Gram matrix (fp64); ws: >= B * 16 * 65 * 8 bytes (per-chunk Gram partials) */
 int dph_conv0_gn_fwd(const float* wave, int64_t B, int64_t S, const float* w, int64_t C, int64_t k0, int64_t s0,
                      const float* gamma, const float* beta, const float* mask, void* y, float* mean, float* rstd,
                      float* ws, int64_t ws_bytes, hipStream_t stream);

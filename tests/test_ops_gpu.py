@@ -466,7 +466,7 @@ def _conv0_gn(wave, w, C, gamma, beta, mask, dy=None):
     y = torch.empty(B * L0, C, dtype=torch.bfloat16, device=DEV)
     mean = torch.empty(B, C, device=DEV)
     rstd = torch.empty(B, C, device=DEV)
-    ws = torch.empty(B * (-(-L0 // 256)) * C * 2, device=DEV)
+    ws = torch.empty(B * 16 * 65 * 2, device=DEV)   # per-(utterance, chunk) fp64 Gram partials
     st = _lib.stream_ptr()
     call("dph_conv0_gn_fwd", ptr(wave), B, S, ptr(w), C, 10, 5, ptr(gamma), ptr(beta), ptr(mask), ptr(y),
          ptr(mean), ptr(rstd), ptr(ws), ws.numel() * 4, st)

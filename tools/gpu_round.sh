@@ -12,6 +12,7 @@
 #   wgrad   -- tools/wgrad_ab.py (weight-gradient GEMMs: ppw plan vs the register-staged kernel)
 #   pmcattn -- rocprofv3 --pmc passes over the attention kernels (tools/attn_bench.py)
 #   pmcgemm -- the same over the dominant GEMM shape (7984 x 3072 x 768, tools/gemm_one.py)
+#   pmcconv0 -- the same over the conv0 GroupNorm kernels (tools/conv0_bench.py)
 # Every GPU step runs under its own timeout; the first failing step ends the script.
 set -o pipefail
 TAG=${1:-run}; shift
@@ -75,6 +76,8 @@ for P in $PHASES; do
       pmc_run pmcattn attn python3 "$R/tools/attn_bench.py" || exit 1 ;;
     pmcgemm)
       pmc_run pmcgemm gemm python3 "$R/tools/gemm_one.py" 7984 3072 768 5 || exit 1 ;;
+    pmcconv0)
+      pmc_run pmcconv0 conv0 python3 "$R/tools/conv0_bench.py" 0 3 || exit 1 ;;
     *) echo "unknown phase $P"; exit 2 ;;
   esac
 done
