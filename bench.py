@@ -29,7 +29,7 @@ import torch.distributed as dist
 
 FLOP_PER_UTT_BASE = 599.6e9      # teacher fwd + 3 x (student fwd + projections), 10 s utterance
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-from dphubert_amd.perfmodel import MFMA_PEAK_TFLOPS, forward_flops, step_flops_per_utt  # noqa: E402,F401
+from dphubert_amd.perfmodel import HBM_PEAK_GBPS, MFMA_PEAK_TFLOPS, forward_flops, step_flops_per_utt  # noqa: E402,F401,E501
 
 
 def workload(args):
@@ -440,6 +440,21 @@ def main():
         if traffic_err:
             out["roofline"]["traffic_error"] = traffic_err
         log(json.dumps({k: v for k, v in summ.items()}))
+        # the non-GEMM kernels of the same profiled step against their own roof: attention on the MFMA peak
+        # (algorithmic FLOPs), conv0 / LayerNorm / AdamW on HBM (the bytes each launch must move once)
+        table = []
+        for label, d in sorted(prof.span_summary().items(), key=lambda kv: -kv[1]["ms"]):
+            avg_s = d["ms"] / d["launches"] / 1e3
+            per = d["work"] / d["launches"]
+            if d["unit"] == "flop":
+                ach, peak, unit = per / avg_s / 1e12, MFMA_PEAK_TFLOPS, "TFLOP/s"
+            else:
+                ach, peak, unit = per / avg_s / 1e9, HBM_PEAK_GBPS, "GB/s"
+            table.append({"kernel": label, "bound": "mfma" if d["unit"] == "flop" else "hbm",
+                          "launches_per_step": d["launches"], "avg_launch_us": round(avg_s * 1e6, 2),
+                          "work_per_launch": per, "work_unit": d["unit"], "achieved": round(ach, 1), "peak": peak,
+                          "unit": unit, "frac": round(ach / peak, 4), "ms_per_step": round(d["ms"], 3)})
+        out["kernel_table"] = table
     if batches is not None:
         shapes = [tuple(b[0].shape) for b in batches[args.warmup:]]
         out["config"]["batch_shapes"] = [f"{bb}x{ss / 16000:.2f}s" for bb, ss in shapes]

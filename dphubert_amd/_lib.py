@@ -216,7 +216,12 @@ def ptr(t):
     return t.data_ptr()
 
 
+# set by kernels.LaunchProfiler while it is active: brackets the non-GEMM launches its table covers
+CALL_HOOK = [None]
+
+
 def call(name: str, *args):
     fn = getattr(lib(), name)
-    rc = fn(*args)
+    hook = CALL_HOOK[0]
+    rc = hook(name, fn, args) if hook is not None else fn(*args)
     check(rc, name)

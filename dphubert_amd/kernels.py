@@ -70,6 +70,40 @@ class _Event:
             pass
 
 
+def _attn_work(a, off, label, mult):
+    B, T, H, p = a[off], a[off + 1], a[off + 2], a[off + 4]
+    return label + ("_drop" if p > 0 else ""), mult * B * H * T * T * 64, "flop"
+
+
+def _conv0_bytes(a):
+    B, S, C = a[1], a[2], a[4]
+    L0 = (S - 10) // 5 + 1
+    return 2.0 * B * L0 * C + 2.0 * 4 * B * S   # the bf16 output (its gradient) once + the waveform twice
+
+
+# Algorithmic work of the non-GEMM launches bench.py tabulates (the argument order of include/dphubert_hip.h):
+# attention in FLOPs (forward 4 B H T^2 64: Q K^T and P V; backward 2.5x that: dV, dP, dQ, dK plus the recomputed
+# S), the memory-bound kernels in bytes of the tensors they must read / write once.
+SPAN_WORK = {
+    "dph_attention_fwd": lambda a: _attn_work(a, 6, "attn_fwd", 4.0),
+    "dph_attention_fwd_relpos": lambda a: _attn_work(a, 8, "attn_fwd_relpos", 4.0),
+    "dph_attention_bwd": lambda a: _attn_work(a, 7, "attn_bwd", 10.0),
+    "dph_attention_bwd_relpos": lambda a: _attn_work(a, 11, "attn_bwd_relpos", 10.0),
+    "dph_conv0_gn_fwd": lambda a: ("conv0_gn_fwd", _conv0_bytes(a), "byte"),
+    "dph_conv0_gn_bwd": lambda a: ("conv0_gn_bwd", _conv0_bytes(a), "byte"),
+    # x, y bf16 (+ the scaled input)
+    "dph_layernorm_fwd": lambda a: ("ln_fwd", a[7] * a[8] * (4.0 + 2.0 * (a[1] is not None)), "byte"),
+    "dph_layernorm_fwd_x32": lambda a: ("ln_fwd", a[6] * a[7] * 6.0, "byte"),
+    # dy, x, dx bf16 (+ the branch gradient written, + its stored pre-activation read)
+    "dph_layernorm_bwd": lambda a: ("ln_bwd", a[9] * a[10] * (6.0 + 2.0 * (a[13] is not None) +
+                                                            2.0 * (a[18] is not None)), "byte"),
+    "dph_layernorm_bwd_res32": lambda a: ("ln_bwd", a[8] * a[9] * (10.0 + 4.0 * (a[10] is not None)), "byte"),
+    # 30 B per updated parameter (optim.FusedAdamW sets the count): p, g, m, v read, p, m, v + bf16 image written
+    "dph_adamw_step_img": lambda a: ("adamw", 30.0 * SPAN_HINT.get("adamw_params", 0), "byte"),
+}
+SPAN_HINT = {}
+
+
 class LaunchProfiler:
     """Brackets every GEMM launch with HIP events on the launch stream (used by bench.py to
     measure per-kernel average durations live; off by default).  Works eagerly and inside a HIP
@@ -87,6 +121,7 @@ class LaunchProfiler:
         # event can be collected before the profiler (kept by Trainer with the profiled graph).
         self.events = []
         self.by_shape = by_shape   # key the summary by (kernel, M, N, K, batch, splits) -- diagnostics
+        self.spans = []            # (label, work, unit, e0, e1) of the SPAN_WORK launches
 
     def event(self) -> "_Event":
         e = _Event()
@@ -95,10 +130,35 @@ class LaunchProfiler:
 
     def __enter__(self):
         LaunchProfiler.active = self
+        _lib.CALL_HOOK[0] = self._span
         return self
 
     def __exit__(self, *exc):
         LaunchProfiler.active = None
+        _lib.CALL_HOOK[0] = None
+
+    def _span(self, name, fn, args):
+        wk = SPAN_WORK.get(name)
+        if wk is None:
+            return fn(*args)
+        e0, e1 = self.event(), self.event()
+        e0.record()
+        rc = fn(*args)
+        e1.record()
+        label, work, unit = wk(args)
+        self.spans.append((label, float(work), unit, e0, e1))
+        return rc
+
+    def span_summary(self):
+        """{label: {launches, ms, work, unit}} of the bracketed non-GEMM launches."""
+        torch.cuda.synchronize()
+        out = {}
+        for label, work, unit, e0, e1 in self.spans:
+            d = out.setdefault(label, {"launches": 0, "ms": 0.0, "work": 0.0, "unit": unit})
+            d["launches"] += 1
+            d["ms"] += e0.elapsed_time(e1)
+            d["work"] += work
+        return out
 
     def summary(self):
         torch.cuda.synchronize()

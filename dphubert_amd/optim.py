@@ -139,6 +139,8 @@ class FusedAdamW(torch.optim.Optimizer):
                 groups[gi].beta1 = g["betas"][0]
                 groups[gi].beta2 = g["betas"][1]
                 groups[gi].eps = g["eps"]
+        from .kernels import SPAN_HINT
+        SPAN_HINT["adamw_params"] = sum(p.numel() for _, p in plist)   # bench.py's kernel table (bytes per launch)
         call("dph_adamw_step_img", ptr(self._slots_dev), len(plist), ptr(self._cslot), ptr(self._cstart),
              self._nchunks, self.dyn_ptr, groups, len(self.param_groups), self._step,
              ptr(self._sumsq) if clip else None, float(self.max_grad_norm or 0.0), ptr(img), s)

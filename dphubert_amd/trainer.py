@@ -334,7 +334,7 @@ class Trainer:
         g = torch.cuda.CUDAGraph()
         try:
             if prof is not None:
-                LaunchProfiler.active = prof
+                prof.__enter__()         # GEMM brackets + the non-GEMM span hook (kernels.SPAN_WORK)
             # thread_local: the process group's watchdog thread keeps polling the events of earlier (eager)
             # collectives while this thread captures; under the default "global" mode that poll is an illegal
             # call during capture and aborts the process ("operation not permitted when stream is capturing").
@@ -348,6 +348,8 @@ class Trainer:
                 loss = self._gpu_step(self._static, zero, final)
         finally:
             LaunchProfiler.active = None
+            if prof is not None:
+                prof.__exit__(None, None, None)
             ops.reset_zero_arena()
         if self._pool is None and prof is None:
             self._pool = g.pool()
