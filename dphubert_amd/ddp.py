@@ -180,6 +180,12 @@ class GradReducer:
             self._launch(bi)
 
     def _launch(self, bi):
+        # a bucket may hold gradients written on the weight-gradient side stream (ops.wgrad_side): its collective
+        # starts after them too
+        from .ops import _WGRAD_SIDE
+        side = _WGRAD_SIDE[0]
+        if side is not None and side != torch.cuda.current_stream():
+            torch.cuda.current_stream().wait_stream(side)
         f = self.flat[bi]
         if self.payload[bi] is not None:
             f = self.payload[bi]

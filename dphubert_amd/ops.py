@@ -495,14 +495,20 @@ class grouped_wgrads:
 
     def _flush(self, key):
         items = self.queues.pop(key)
-        ws = K.linear_wgrad_grouped([(dy, x, dw) for dy, x, dw, _, _ in items], accumulate=True)
-        del ws
-        for *_, params, post in items:
-            if post is not None:
-                post()           # reads the landed weight gradient (stream-ordered after the grouped launch)
-            for p in params:
-                p._dph_hold = False
-                p._dph_sink_ready(p)
+        # a group whose gradients nothing else in the backward reads (no post(): the FFN2 group's feeds the FFN
+        # mask gradient the HardConcrete backward consumes) may run on the weight-gradient side stream
+        # (DPH_WGRAD_STREAM=1 with DPH_WGRAD_SCOPE=group / all), beside the rest of the backward
+        side_ok = all(post is None for *_, post in items)
+        ins = [t for dy, x, *_ in items for t in (dy, x)]
+        with wgrad_side(*ins, enable=side_ok, scope="group"):
+            ws = K.linear_wgrad_grouped([(dy, x, dw) for dy, x, dw, _, _ in items], accumulate=True)
+            del ws
+            for *_, params, post in items:
+                if post is not None:
+                    post()       # reads the landed weight gradient (stream-ordered after the grouped launch)
+                for p in params:
+                    p._dph_hold = False
+                    p._dph_sink_ready(p)
 
     def flush(self):
         for key in list(self.queues):
