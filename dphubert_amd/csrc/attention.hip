@@ -371,11 +371,11 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(const bf16_t* __restri
       float v[4] = {oacc[u][d][0] * inv_l, oacc[u][d][1] * inv_l, oacc[u][d][2] * inv_l, oacc[u][d][3] * inv_l};
       // fp32: the backward's D = rowsum(dO * O) must cancel against sum_j P_j dP_j to fp32 accuracy (a bf16 O
       // leaves 2^-9 |dO||v| of noise in every dS, which dominates dQ / dK where the softmax saturates)
-      *reinterpret_cast<float4*>(o_u + obase + col) = make_float4(v[0], v[1], v[2], v[3]);
+      if (o_u) *reinterpret_cast<float4*>(o_u + obase + col) = make_float4(v[0], v[1], v[2], v[3]);
       *reinterpret_cast<uint2*>(o_m + obase + col) =
           make_uint2(pack2bf(v[0] * hm, v[1] * hm), pack2bf(v[2] * hm, v[3] * hm));
     }
-    if (g == 0) lse[(b * H + h) * T + qme[u]] = m_run[u] + __logf(l_run[u]);
+    if (g == 0 && lse) lse[(b * H + h) * T + qme[u]] = m_run[u] + __logf(l_run[u]);
   }
 }
 
@@ -607,11 +607,11 @@ __global__ void __launch_bounds__(256, 2) attn_fwd32_kernel(const bf16_t* __rest
       const int col = 32 * d + 8 * rq + 4 * hi;
       float v[4] = {oacc[d][4 * rq] * inv_l, oacc[d][4 * rq + 1] * inv_l, oacc[d][4 * rq + 2] * inv_l,
                     oacc[d][4 * rq + 3] * inv_l};
-      *reinterpret_cast<float4*>(o_u + obase + col) = make_float4(v[0], v[1], v[2], v[3]);
+      if (o_u) *reinterpret_cast<float4*>(o_u + obase + col) = make_float4(v[0], v[1], v[2], v[3]);
       *reinterpret_cast<uint2*>(o_m + obase + col) =
           make_uint2(pack2bf(v[0] * hm, v[1] * hm), pack2bf(v[2] * hm, v[3] * hm));
     }
-  if (hi == 0) lse[(int64_t)(b * H + h) * T32 + q] = m_run + __logf(l_run);
+  if (hi == 0 && lse) lse[(int64_t)(b * H + h) * T32 + q] = m_run + __logf(l_run);
 }
 
 // ---------------------------------------------------------------------------
@@ -835,11 +835,11 @@ __global__ void __launch_bounds__(256, 3) attn_fwd32v2_kernel(const bf16_t* __re
       const int col = 32 * d + 8 * rq + 4 * hi;
       float v[4] = {oacc[d][4 * rq] * inv_l, oacc[d][4 * rq + 1] * inv_l, oacc[d][4 * rq + 2] * inv_l,
                     oacc[d][4 * rq + 3] * inv_l};
-      *reinterpret_cast<float4*>(o_u + obase + col) = make_float4(v[0], v[1], v[2], v[3]);
+      if (o_u) *reinterpret_cast<float4*>(o_u + obase + col) = make_float4(v[0], v[1], v[2], v[3]);
       *reinterpret_cast<uint2*>(o_m + obase + col) =
           make_uint2(pack2bf(v[0] * hm, v[1] * hm), pack2bf(v[2] * hm, v[3] * hm));
     }
-  if (hi == 0) lse[(int64_t)(b * H + h) * T32 + q] = m_run + __logf(l_run);
+  if (hi == 0 && lse) lse[(int64_t)(b * H + h) * T32 + q] = m_run + __logf(l_run);
 }
 
 // ---------------------------------------------------------------------------
@@ -1545,7 +1545,7 @@ static int attention_bwd(const void* qkv, const void* do_masked, const float* he
 extern "C" int dph_attention_fwd(const void* qkv, void* o_unmasked, void* o_masked, float* lse,
                                  const float* head_mask, const int64_t* key_len, int64_t B, int64_t T, int64_t H,
                                  float scale, float dropout_p, uint64_t seed, void* keep_bits, hipStream_t stream) {
-  DPH_REQUIRE(qkv && o_unmasked && o_masked && lse && B > 0 && T > 0 && H > 0, "dph_attention_fwd: bad args");
+  DPH_REQUIRE(qkv && o_masked && B > 0 && T > 0 && H > 0, "dph_attention_fwd: bad args");
   return attention_fwd(qkv, o_unmasked, o_masked, lse, head_mask, key_len, B, T, H, scale, dropout_p, seed,
                        RelBias{nullptr, nullptr, nullptr, nullptr}, keep_bits, stream);
 }
@@ -1554,7 +1554,7 @@ extern "C" int dph_attention_fwd_relpos(const void* qkv, void* o_unmasked, void*
                                         const float* head_mask, const int64_t* key_len, const float* rel_tab,
                                         const float* gate, int64_t B, int64_t T, int64_t H, float scale,
                                         float dropout_p, uint64_t seed, void* keep_bits, hipStream_t stream) {
-  DPH_REQUIRE(qkv && o_unmasked && o_masked && lse && rel_tab && gate && B > 0 && T > 0 && T <= 3584 && H > 0,
+  DPH_REQUIRE(qkv && o_masked && rel_tab && gate && B > 0 && T > 0 && T <= 3584 && H > 0,
               "dph_attention_fwd_relpos: bad args (T <= 3584)");
   return attention_fwd(qkv, o_unmasked, o_masked, lse, head_mask, key_len, B, T, H, scale, dropout_p, seed,
                        RelBias{rel_tab, gate, nullptr, nullptr}, keep_bits, stream);

@@ -1648,9 +1648,11 @@ class EncoderLayerFn(torch.autograd.Function):
             Wqkv = bf16_image(wq, wk, wv)
             bqkv = f32_cat(bq, bk, bv)
             qkv = K.linear_fwd(h, Wqkv, bqkv)
-            o_u = torch.empty(M, Dh, dtype=F32, device=dev)     # fp32: the backward's D (attention.hip)
+            # fp32 unmasked output: the backward's D (attention.hip); neither it nor the LSE is written without a
+            # backward (the teacher)
+            o_u = torch.empty(M, Dh, dtype=F32, device=dev) if need else None
             o_m = torch.empty(M, Dh, dtype=BF16, device=dev)
-            lse = torch.empty(B * H * T, dtype=F32, device=dev)
+            lse = torch.empty(B * H * T, dtype=F32, device=dev) if need else None
             seed_a = SEEDS.next() if cfg["p_attn"] > 0 else 0
             sv["gate"] = EncoderLayerFn._attention_fwd(ctx, cfg, h, qkv, o_u, o_m, lse, hm, seed_a)
             Wo = bf16_image(wo)
@@ -1713,9 +1715,9 @@ class EncoderLayerFn(torch.autograd.Function):
             Dh = wq.shape[0]
             Wqkv = bf16_image(wq, wk, wv)
             qkv = K.linear_fwd(xn1, Wqkv, f32_cat(bq, bk, bv))
-            o_u = torch.empty(M, Dh, dtype=F32, device=dev)     # fp32: the backward's D (attention.hip)
+            o_u = torch.empty(M, Dh, dtype=F32, device=dev) if need else None   # (as the post-norm forward)
             o_m = torch.empty(M, Dh, dtype=BF16, device=dev)
-            lse = torch.empty(B * H * T, dtype=F32, device=dev)
+            lse = torch.empty(B * H * T, dtype=F32, device=dev) if need else None
             seed_a = SEEDS.next() if cfg["p_attn"] > 0 else 0
             sv["gate"] = EncoderLayerFn._attention_fwd(ctx, cfg, xn1, qkv, o_u, o_m, lse, hm, seed_a)
             Wo = bf16_image(wo)

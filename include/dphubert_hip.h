@@ -252,7 +252,8 @@ int dph_colsum3(const void* x, float* out0, float* out1, float* out2, int64_t ro
  * [B*T][3*H*64] (q | k | v), scores (scale*q)k^T + (-1e4 key padding),
  * softmax, dropout(p), @v, x head_mask.  Writes o_unmasked ([B*T][H*64] fp32:
  * the backward's D = rowsum(dO*O) must cancel sum_j P_j dP_j to fp32 accuracy), o_masked
- * ([B*T][H*64] bf16, the out_proj input) and the per-row log-sum-exp [B][H][T].
+ * ([B*T][H*64] bf16, the out_proj input) and the per-row log-sum-exp [B][H][T].  o_unmasked and lse may be
+ * NULL (a forward without backward: the teacher) -- not written then.
  * ------------------------------------------------------------------------ */
 int dph_attention_fwd(const void* qkv, void* o_unmasked, void* o_masked, float* lse, const float* head_mask,
                       const int64_t* key_len, int64_t B, int64_t T, int64_t H, float scale, float dropout_p,
