@@ -560,6 +560,7 @@ def _bucket_fresh(p) -> bool:
 # FFN intermediate-mask gradient from the FFN2 weight gradient (dph_colprod: sum_o W2[o][n] dW2[o][n] / mask_n)
 # instead of re-reading the forward's f in the FFN2 input-gradient epilogue; DPH_FFN_COLPROD=0 keeps the epilogue
 _FFN_COLPROD = os.environ.get("DPH_FFN_COLPROD", "1") != "0"
+_TEACHER_OU = os.environ.get("DPH_TEACHER_OU", "0") == "1"   # A/B: the no-grad attention forward writes o_u / lse
 
 
 # ---------------------------------------------------------------------------
@@ -1650,9 +1651,9 @@ class EncoderLayerFn(torch.autograd.Function):
             qkv = K.linear_fwd(h, Wqkv, bqkv)
             # fp32 unmasked output: the backward's D (attention.hip); neither it nor the LSE is written without a
             # backward (the teacher)
-            o_u = torch.empty(M, Dh, dtype=F32, device=dev) if need else None
+            o_u = torch.empty(M, Dh, dtype=F32, device=dev) if (need or _TEACHER_OU) else None
             o_m = torch.empty(M, Dh, dtype=BF16, device=dev)
-            lse = torch.empty(B * H * T, dtype=F32, device=dev) if need else None
+            lse = torch.empty(B * H * T, dtype=F32, device=dev) if (need or _TEACHER_OU) else None
             seed_a = SEEDS.next() if cfg["p_attn"] > 0 else 0
             sv["gate"] = EncoderLayerFn._attention_fwd(ctx, cfg, h, qkv, o_u, o_m, lse, hm, seed_a)
             Wo = bf16_image(wo)

@@ -145,8 +145,10 @@ def tracks_eager_report(eager, gr, le, lg):
       * each parameter: that, or 5e-3 (1-D biases 1e-2: cancellation-heavy column sums); k_proj.bias is left out
         (its gradient is exactly zero by softmax shift invariance, so Adam turns the atomic-order noise of that
         zero into +-lr steps);
-      * the whole parameter vector: that, or 1e-5 (with the student offset from the teacher, _module, the
-        gradients are smooth in the weights; a stale op moves the whole vector by > 1e-3)."""
+      * the whole parameter vector: that, or 1e-4.  The eager runs themselves split into branches ~1e-5 and
+        ~5.4e-5 apart in this configuration (profiles/r4_s25_graph_flake.txt: tools/graph_flake_probe.py, six trials in
+        one process), so four eager runs that all took one branch cannot bound a replay that took the other (r4_s23:
+        5.38e-5 against 4 x 1.21e-5); a stale or missing op in the replay moves the whole vector by > 1e-3."""
     pe = [dict(t.module.named_parameters()) for t in eager]
     pg = dict(gr.module.named_parameters())
     names = [n for n, p in gr.module.named_parameters() if p.requires_grad and not n.endswith("k_proj.bias")]
@@ -168,7 +170,7 @@ def tracks_eager_report(eager, gr, le, lg):
             lines.append(f"param {n}: graph-vs-eager {e:.3g} eager spread {base:.3g}")
     e_all = rel_l2(vg, ve[near])
     base_all = max(rel_l2(ve[i], ve[j]) for i, j in pairs)
-    ok &= e_all < max(1e-5, 4 * base_all)
+    ok &= e_all < max(1e-4, 4 * base_all)
     lines.append(f"whole vector: graph vs nearest eager run ({near}) {e_all:.3g}, largest eager-vs-eager "
                  f"{base_all:.3g}, eager runs to run 0 {[round(rel_l2(v, ve[0]), 8) for v in ve[1:]]}")
     return ok, lines
