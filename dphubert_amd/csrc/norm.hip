@@ -287,8 +287,16 @@ __global__ void __launch_bounds__(64 * LN_BWD_WAVES) ln_bwd_kernel(
     }
   }
   if (branch_sdot) {
+    // one same-address atomic per BLOCK (per wave: 66 us for a 7984 x 768 launch, profiles/r4_s28_ln_ab.txt)
+    __shared__ float sdot_s[16];
     sdot = wave_sum(sdot);
-    if (lane == 0) atomicAdd(branch_sdot, sdot);
+    if (lane == 0) sdot_s[wave] = sdot;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float t = 0.f;
+      for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += sdot_s[w];
+      atomicAdd(branch_sdot, t);
+    }
   }
 }
 
@@ -458,6 +466,227 @@ int64_t slab_groups(int64_t nrows) { return std::max<int64_t>(1, std::min<int64_
 
 int64_t colsum_rpb(int64_t rows) { return std::max<int64_t>(64, cdiv(cdiv(rows, 8192), 4) * 4); }
 
+// Forward, the common case (bf16 rows of D = 256 * k <= 1024 with no row padding, no input scale, no dropout --
+// every post-norm encoder LayerNorm, components.py:853,856): a HALF wave per row, 16-byte loads and stores
+// (NE = D / 32 elements per lane: NE / 8 vector accesses), sums over the 32 lanes of the half.  Half the memory
+// instructions of ln_fwd_kernel's 8-byte quads; otherwise the same fp32 two-pass statistics per row.
+template <int NE>
+__global__ void __launch_bounds__(256) ln_fwd16_kernel(const bf16_t* __restrict__ x, const float* __restrict__ gamma,
+                                                       const float* __restrict__ beta, bf16_t* __restrict__ y,
+                                                       float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                       int64_t rows, float eps) {
+  constexpr int NC = NE / 8;                 // 16-B chunks per lane
+  constexpr int D = NE * 32;
+  const int lane = threadIdx.x & 63;
+  const int hl = lane & 31;
+  const int64_t row = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5);
+  const bool ok = row < rows;
+  uint4 raw[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+    raw[c] = ok ? *reinterpret_cast<const uint4*>(x + row * D + (c * 32 + hl) * 8) : make_uint4(0, 0, 0, 0);
+  float v[NC][8];
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const uint32_t w[4] = {raw[c].x, raw[c].y, raw[c].z, raw[c].w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[c][2 * i] = __uint_as_float(w[i] << 16);
+      v[c][2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s += v[c][i];
+  }
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  const float mean = s * (1.0f / (float)D);
+  float q = 0.f;
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float d = v[c][i] - mean;
+      q += d * d;
+    }
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
+  const float rstd = rsqrtf(q * (1.0f / (float)D) + eps);
+  if (!ok) return;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int col = (c * 32 + hl) * 8;
+    const float4 g0 = *reinterpret_cast<const float4*>(gamma + col), g1 = *reinterpret_cast<const float4*>(gamma + col + 4);
+    const float4 b0 = *reinterpret_cast<const float4*>(beta + col), b1 = *reinterpret_cast<const float4*>(beta + col + 4);
+    const float ga[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+    const float be[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+    float o[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = (v[c][i] - mean) * rstd * ga[i] + be[i];
+    *reinterpret_cast<uint4*>(y + row * D + col) =
+        make_uint4(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]), pack2bf(o[4], o[5]), pack2bf(o[6], o[7]));
+  }
+  if (hl == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+}
+
+// Backward, the common case of the post-norm layers (bf16 dy / x / dx of D = 256 * k <= 1024, no row padding, no
+// input scale, no dropout on the LN input, no dx_add; the branch gradient -- dropout, layer mask, its column sums
+// and mask-gradient dot -- as ln_bwd_kernel): a HALF wave per row with 16-byte accesses, 8 waves x 2 rows per block
+// and the same per-block slab row ws[block][3][D] for slab_reduce.  The two halves of a wave (two rows, same
+// columns) combine their column partials with one lane ^ 32 exchange before the cross-wave LDS sum.
+template <int NE>
+__global__ void __launch_bounds__(512) ln_bwd16_kernel(
+    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const float* __restrict__ gamma,
+    const float* __restrict__ mean_in, const float* __restrict__ rstd_in, bf16_t* __restrict__ dx,
+    float* __restrict__ dgamma, float* __restrict__ dbeta, int64_t rows, bf16_t* __restrict__ branch, float branch_p,
+    uint64_t branch_seed, const float* __restrict__ branch_smask, float* __restrict__ branch_colsum,
+    const bf16_t* __restrict__ branch_pre, float* __restrict__ branch_sdot, float* __restrict__ ws) {
+  constexpr int NC = NE / 8;
+  constexpr int D = NE * 32;
+  static_assert(LN_BWD_WAVES == 8 && LN_BWD_RPW == 2, "ln_bwd16: the slab layout assumes 16 rows per block");
+  branch_seed = epoch_seed(branch_seed);
+  __shared__ float4 red[8][NC * 32][2];
+  const int lane = threadIdx.x & 63;
+  const int hl = lane & 31;
+  const int wave = threadIdx.x >> 6;
+  const int64_t row = ((int64_t)blockIdx.x * 8 + wave) * 2 + (lane >> 5);
+  const bool ok = row < rows;
+  uint4 rx[NC], rd[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int64_t off = row * D + (c * 32 + hl) * 8;
+    rx[c] = ok ? *reinterpret_cast<const uint4*>(x + off) : make_uint4(0, 0, 0, 0);
+    rd[c] = ok ? *reinterpret_cast<const uint4*>(dy + off) : make_uint4(0, 0, 0, 0);
+  }
+  const float mean = ok ? mean_in[row] : 0.f;
+  const float rstd = ok ? rstd_in[row] : 0.f;
+  const float binv_keep = branch_p > 0.f ? 1.f / (1.f - branch_p) : 1.f;
+  const float bsm = branch_smask ? *branch_smask : 1.0f;
+  float xh[NC][8], g[NC][8], dyv[NC][8], ga[NC][8];
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int col = (c * 32 + hl) * 8;
+    const float4 g0 = *reinterpret_cast<const float4*>(gamma + col), g1 = *reinterpret_cast<const float4*>(gamma + col + 4);
+    ga[c][0] = g0.x; ga[c][1] = g0.y; ga[c][2] = g0.z; ga[c][3] = g0.w;
+    ga[c][4] = g1.x; ga[c][5] = g1.y; ga[c][6] = g1.z; ga[c][7] = g1.w;
+    const uint32_t wx[4] = {rx[c].x, rx[c].y, rx[c].z, rx[c].w};
+    const uint32_t wd[4] = {rd[c].x, rd[c].y, rd[c].z, rd[c].w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      xh[c][2 * i] = (__uint_as_float(wx[i] << 16) - mean) * rstd;
+      xh[c][2 * i + 1] = (__uint_as_float(wx[i] & 0xffff0000u) - mean) * rstd;
+      dyv[c][2 * i] = __uint_as_float(wd[i] << 16);
+      dyv[c][2 * i + 1] = __uint_as_float(wd[i] & 0xffff0000u);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      g[c][i] = dyv[c][i] * ga[c][i];
+      s1 += g[c][i];
+      s2 += g[c][i] * xh[c][i];
+    }
+  }
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) {
+    s1 += __shfl_xor(s1, o, 64);
+    s2 += __shfl_xor(s2, o, 64);
+  }
+  s1 *= 1.0f / (float)D;
+  s2 *= 1.0f / (float)D;
+  float sdot = 0.f;
+  float pc[NC][8];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int col = (c * 32 + hl) * 8;
+    float o[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = rstd * (g[c][i] - s1 - xh[c][i] * s2);
+    if (ok)
+      *reinterpret_cast<uint4*>(dx + row * D + col) =
+          make_uint4(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]), pack2bf(o[4], o[5]), pack2bf(o[6], o[7]));
+#pragma unroll
+    for (int i = 0; i < 8; ++i) pc[c][i] = 0.f;
+    if (branch) {
+      float pre[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, z[8], bo[8];
+      if (branch_sdot && ok) {
+        const uint4 rp = *reinterpret_cast<const uint4*>(branch_pre + row * D + col);
+        const uint32_t wp[4] = {rp.x, rp.y, rp.z, rp.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          pre[2 * i] = __uint_as_float(wp[i] << 16);
+          pre[2 * i + 1] = __uint_as_float(wp[i] & 0xffff0000u);
+        }
+      }
+      float z0[4], z1[4];
+      dropout_scale4(branch_seed, (uint64_t)row * D + col, branch_p, binv_keep, z0);
+      dropout_scale4(branch_seed, (uint64_t)row * D + col + 4, branch_p, binv_keep, z1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        z[i] = z0[i];
+        z[4 + i] = z1[i];
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float zz = ok ? o[i] * z[i] : 0.f;
+        sdot += zz * pre[i];
+        bo[i] = zz * bsm;
+        pc[c][i] = bo[i];
+      }
+      if (ok)
+        *reinterpret_cast<uint4*>(branch + row * D + col) =
+            make_uint4(pack2bf(bo[0], bo[1]), pack2bf(bo[2], bo[3]), pack2bf(bo[4], bo[5]), pack2bf(bo[6], bo[7]));
+    }
+  }
+  // column partials of this row: dgamma = dy * xh, dbeta = dy, branch colsum = bo (rows past `rows` are zero)
+  float* wrow = ws + (int64_t)blockIdx.x * 3 * D;
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const bool want = q == 0 ? dgamma != nullptr : (q == 1 ? dbeta != nullptr : branch_colsum != nullptr);
+    if (!want) continue;
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      float t[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float vq = q == 0 ? (ok ? dyv[c][i] * xh[c][i] : 0.f) : (q == 1 ? (ok ? dyv[c][i] : 0.f) : pc[c][i]);
+        t[i] = vq + __shfl_xor(vq, 32, 64);
+      }
+      if (lane < 32) {
+        red[wave][c * 32 + hl][0] = make_float4(t[0], t[1], t[2], t[3]);
+        red[wave][c * 32 + hl][1] = make_float4(t[4], t[5], t[6], t[7]);
+      }
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < NC * 32 * 2; j += 512) {
+      const int cj = j >> 1, hh = j & 1;
+      float4 acc = red[0][cj][hh];
+#pragma unroll
+      for (int w = 1; w < 8; ++w) {
+        const float4 u = red[w][cj][hh];
+        acc.x += u.x; acc.y += u.y; acc.z += u.z; acc.w += u.w;
+      }
+      // (cj = c * 32 + hl owns columns (c * 32 + hl) * 8 .. + 7; hh picks the half)
+      *reinterpret_cast<float4*>(wrow + q * D + cj * 8 + hh * 4) = acc;
+    }
+  }
+  if (branch_sdot) {
+    // one same-address atomic per BLOCK (per wave: 66 us for a 7984 x 768 launch, profiles/r4_s28_ln_ab.txt)
+    __shared__ float sdot_s[16];
+    sdot = wave_sum(sdot);
+    if (lane == 0) sdot_s[wave] = sdot;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float t = 0.f;
+      for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += sdot_s[w];
+      atomicAdd(branch_sdot, t);
+    }
+  }
+}
+
 }  // namespace
 }  // namespace dph
 
@@ -470,6 +699,24 @@ extern "C" int dph_layernorm_fwd_ld(const void* x, const float* xscale, const fl
   if (ld == 0) ld = D;
   DPH_REQUIRE(D >= 1 && ld >= D && ld % 4 == 0 && ld <= LN_MAXV * 256 && rows > 0,
               "dph_layernorm_fwd: unsupported D=%lld ld=%lld", (long long)D, (long long)ld);
+  static const bool ln16 = [] {
+    const char* e = getenv("DPH_LN_FWD16");
+    return !(e && e[0] == '0');
+  }();
+  if (ln16 && !xscale && dropout_p <= 0.f && ld == D && D % 256 == 0 && D <= 1024 &&
+      (reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0 &&
+      (reinterpret_cast<uintptr_t>(gamma) & 15) == 0 && (reinterpret_cast<uintptr_t>(beta) & 15) == 0) {
+    const dim3 g16((unsigned)cdiv(rows, 8));
+    const bf16_t* xb = reinterpret_cast<const bf16_t*>(x);
+    bf16_t* yb = reinterpret_cast<bf16_t*>(y);
+    switch (D / 256) {
+      case 1: hipLaunchKernelGGL(ln_fwd16_kernel<8>, g16, dim3(256), 0, stream, xb, gamma, beta, yb, mean, rstd, rows, eps); break;
+      case 2: hipLaunchKernelGGL(ln_fwd16_kernel<16>, g16, dim3(256), 0, stream, xb, gamma, beta, yb, mean, rstd, rows, eps); break;
+      case 3: hipLaunchKernelGGL(ln_fwd16_kernel<24>, g16, dim3(256), 0, stream, xb, gamma, beta, yb, mean, rstd, rows, eps); break;
+      default: hipLaunchKernelGGL(ln_fwd16_kernel<32>, g16, dim3(256), 0, stream, xb, gamma, beta, yb, mean, rstd, rows, eps); break;
+    }
+    return check_launch("dph_layernorm_fwd");
+  }
   const dim3 grid((unsigned)cdiv(rows, 4 * LN_FWD_RPW));
 #define LN_FWD_LAUNCH(NV)                                                                                    \
   hipLaunchKernelGGL(ln_fwd_kernel<NV>, grid, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(x), xscale, \
@@ -538,6 +785,28 @@ extern "C" int dph_layernorm_bwd_ld(const void* dy, const void* x, const float* 
               "dph_layernorm_bwd: workspace too small (%lld < %lld bytes)", (long long)ws_bytes,
               (long long)dph_layernorm_bwd_workspace(rows, D));
   const dim3 grid((unsigned)cdiv(rows, LN_BWD_WAVES * LN_BWD_RPW));
+  static const bool ln16 = [] {
+    const char* e = getenv("DPH_LN_BWD16");
+    return !(e && e[0] == '0');
+  }();
+  auto a16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  if (ln16 && !xscale && dropout_p <= 0.f && !dx_add && ld == D && D % 256 == 0 && D <= 1024 && a16(dy) && a16(x) &&
+      a16(dx) && a16(gamma) && (!branch || a16(branch)) && (!branch_pre || a16(branch_pre))) {
+    const bf16_t* dyb = reinterpret_cast<const bf16_t*>(dy);
+    const bf16_t* xb = reinterpret_cast<const bf16_t*>(x);
+#define LN_BWD16_LAUNCH(NE)                                                                                       \
+  hipLaunchKernelGGL(ln_bwd16_kernel<NE>, grid, dim3(512), 0, stream, dyb, xb, gamma, mean, rstd,                 \
+                     reinterpret_cast<bf16_t*>(dx), dgamma, dbeta, rows, reinterpret_cast<bf16_t*>(branch), branch_p, \
+                     branch_seed, branch_smask, branch_colsum, reinterpret_cast<const bf16_t*>(branch_pre),           \
+                     branch_sdot, ws)
+    switch (D / 256) {
+      case 1: LN_BWD16_LAUNCH(8); break;
+      case 2: LN_BWD16_LAUNCH(16); break;
+      case 3: LN_BWD16_LAUNCH(24); break;
+      default: LN_BWD16_LAUNCH(32); break;
+    }
+#undef LN_BWD16_LAUNCH
+  } else {
 #define LN_BWD_LAUNCH(NV)                                                                                        \
   hipLaunchKernelGGL(ln_bwd_kernel<NV>, grid, dim3(64 * LN_BWD_WAVES), 0, stream,                                \
                      reinterpret_cast<const bf16_t*>(dy), reinterpret_cast<const bf16_t*>(x), xscale, gamma, mean, \
@@ -552,6 +821,7 @@ extern "C" int dph_layernorm_bwd_ld(const void* dy, const void* x, const float* 
     default: LN_BWD_LAUNCH(4); break;
   }
 #undef LN_BWD_LAUNCH
+  }
   if (sums) {
     const int64_t nblk = grid.x;
     hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)cdiv(3 * D, 64), (unsigned)slab_groups(nblk)), dim3(256),
