@@ -415,7 +415,7 @@ def main():
                     f"{v['flops'] / v['ms'] / 1e9:6.0f} TF/s  {k}")
             agg = {}
             for k, v in summ.items():
-                d = agg.setdefault(k.split(" M=")[0], {"launches": 0, "ms": 0.0, "flops": 0.0})
+                d = agg.setdefault(k.split(" M=")[0], {"launches": 0, "ms": 0.0, "flops": 0.0, "bytes": 0.0})
                 for f in d:
                     d[f] += v[f]
             summ = agg
@@ -430,9 +430,12 @@ def main():
         if traffic:
             hits = [v for k, v in traffic.items() if name in k]
             tr = round(hits[0]) if hits else None
+        alg_b = d["bytes"] / d["launches"]
         out["roofline"] = {"bound": "mfma", "kernel": name, "achieved": round(achieved, 1),
                            "peak": MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / MFMA_PEAK_TFLOPS, 4),
                            "traffic": tr, "traffic_unit": "bytes/launch (HBM, PMC FETCH_SIZE*2 + WRITE_SIZE)",
+                           "algorithmic_bytes": round(alg_b),
+                           "traffic_ratio": round(tr / alg_b, 3) if tr else None,
                            "launches_per_step": d["launches"],
                            "avg_launch_us": round(avg_ms * 1e3, 2), "flop_per_launch": flops_per_launch,
                            "all_gemm_tflops": round(all_fl / (all_ms / 1e3) / 1e12, 1),

@@ -163,12 +163,13 @@ class LaunchProfiler:
     def summary(self):
         torch.cuda.synchronize()
         out = {}
-        for name, flops, e0, e1 in self.records:
+        for name, flops, e0, e1, byt in self.records:
             ms = e0.elapsed_time(e1)
-            d = out.setdefault(name, {"launches": 0, "ms": 0.0, "flops": 0.0})
+            d = out.setdefault(name, {"launches": 0, "ms": 0.0, "flops": 0.0, "bytes": 0.0})
             d["launches"] += 1
             d["ms"] += ms
             d["flops"] += flops
+            d["bytes"] += byt
         return out
 
 
@@ -237,7 +238,13 @@ def gemm(A: DphMat, B: DphMat, Cm: DphMat, M: int, N: int, K: int, *, a_kcontig:
             name = (f"{name} M={M} N={N} K={K} b={batch} s={splits} {int(a_kcontig)}{int(b_kcontig)} act={act} "
                     f"res={residual is not None} rl={row_len is not None} rpbA={A.rows_per_batch} "
                     f"rsC={Cm.row_stride} align={al}")
-        prof.records.append((name, 2.0 * M * N * K * batch, e0, e1))
+        # algorithmic HBM bytes: A, B and C once, plus every epilogue operand the call reads or writes
+        ob = 2 if c_dtype == OUT_BF16 else (8 if c_dtype == OUT_F32_ACCUM else 4)
+        byt = batch * (2.0 * (M * K + N * K) + ob * M * N)
+        for t, rw in ((pre_out, 1), (aux_in, 1), (residual, 1)):
+            if t is not None:
+                byt += rw * batch * M * N * t.element_size()
+        prof.records.append((name, 2.0 * M * N * K * batch, e0, e1, byt))
     return ws  # keep alive until the stream consumes it (caching allocator is stream-ordered)
 
 
@@ -377,5 +384,5 @@ def linear_wgrad_grouped(items: Sequence, accumulate: bool = True) -> Optional[t
         name = _variant(args)
         if prof.by_shape:
             name = f"{name} grouped M={N} N={K} K={M} b={n} s={splits}"
-        prof.records.append((name, 2.0 * M * N * K * n, e0, e1))
+        prof.records.append((name, 2.0 * M * N * K * n, e0, e1, n * (2.0 * (M * N + M * K) + 8.0 * N * K)))
     return ws
