@@ -2683,7 +2683,10 @@ static int pp_pick(const DphGemmArgs& a) {
   // epilogue outweighs the 12 K-tiles of MFMA work, and the two-blocks-per-CU 128 x 128 tile runs one block's
   // epilogue beside the other's main loop: 62.5 / 57.6 / 54.3 us vs 70.2 / 64.3 / 61.9 on 128 x 192
   // (student FFN1 / teacher FFN1 / FFN2 DGK dgrad at 7984 x 3072 x 768, profiles/r4_s8_pp_tile_ab.txt)
-  if (a.act != DPH_ACT_NONE && a.N >= 2048 && a.K <= 1024 && a.batch == 1) return 16;
+  // (the Large shape, 5988 x 4096 x 1024, measured the same with and without the rule: 23.21 / 23.23 ms per step,
+  // profiles/r4_s33_large_gelu128_ab.txt.)  DPH_PP_GELU128=0 drops the rule (A/B, read per call)
+  const char* g128 = getenv("DPH_PP_GELU128");
+  if (!(g128 && g128[0] == '0') && a.act != DPH_ACT_NONE && a.N >= 2048 && a.K <= 1024 && a.batch == 1) return 16;
   int best = 12;
   double best_t = 1e300;
   for (const Opt& o : opts) {

@@ -6,6 +6,7 @@
 // channel LayerNorm of layer_norm-mode extractors (:54-61).  torch semantics:
 // biased variance, eps inside the sqrt.
 #include "common.h"
+#include <initializer_list>
 
 namespace dph {
 namespace {
@@ -470,34 +471,60 @@ int64_t colsum_rpb(int64_t rows) { return std::max<int64_t>(64, cdiv(cdiv(rows, 
 // every post-norm encoder LayerNorm, components.py:853,856): a HALF wave per row, 16-byte loads and stores
 // (NE = D / 32 elements per lane: NE / 8 vector accesses), sums over the 32 lanes of the half.  Half the memory
 // instructions of ln_fwd_kernel's 8-byte quads; otherwise the same fp32 two-pass statistics per row.
-template <int NE>
-__global__ void __launch_bounds__(256) ln_fwd16_kernel(const bf16_t* __restrict__ x, const float* __restrict__ gamma,
+__device__ __forceinline__ void ld8(const bf16_t* p, float (&o)[8]) {
+  const uint4 r = *reinterpret_cast<const uint4*>(p);
+  const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    o[2 * i] = __uint_as_float(w[i] << 16);
+    o[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ void ld8(const float* p, float (&o)[8]) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w;
+  o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
+}
+__device__ __forceinline__ void st8(bf16_t* p, const float (&o)[8]) {
+  *reinterpret_cast<uint4*>(p) =
+      make_uint4(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]), pack2bf(o[4], o[5]), pack2bf(o[6], o[7]));
+}
+__device__ __forceinline__ void st8(float* p, const float (&o)[8]) {
+  *reinterpret_cast<float4*>(p) = make_float4(o[0], o[1], o[2], o[3]);
+  *reinterpret_cast<float4*>(p + 4) = make_float4(o[4], o[5], o[6], o[7]);
+}
+
+// Forward, the common case (rows of D = 256 * k <= 1024 with no row padding, no input scale, no dropout -- every
+// post-norm encoder LayerNorm, components.py:853,856, with bf16 x, and the pre-norm layers' LN1 / LN2 over the fp32
+// residual stream, components.py:846-850): a HALF wave per row, 16-byte loads and stores (NE = D / 32 elements per
+// lane: NE / 8 vector accesses of bf16, twice that of fp32), sums over the 32 lanes of the half.  Half the memory
+// instructions of ln_fwd_kernel's 8-byte quads; otherwise the same fp32 two-pass statistics per row.
+template <int NE, typename XT = bf16_t>
+__global__ void __launch_bounds__(256) ln_fwd16_kernel(const XT* __restrict__ x, const float* __restrict__ gamma,
                                                        const float* __restrict__ beta, bf16_t* __restrict__ y,
                                                        float* __restrict__ mean_out, float* __restrict__ rstd_out,
                                                        int64_t rows, float eps) {
-  constexpr int NC = NE / 8;                 // 16-B chunks per lane
+  constexpr int NC = NE / 8;                 // 8-element chunks per lane
   constexpr int D = NE * 32;
   const int lane = threadIdx.x & 63;
   const int hl = lane & 31;
   const int64_t row = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5);
   const bool ok = row < rows;
-  uint4 raw[NC];
-#pragma unroll
-  for (int c = 0; c < NC; ++c)
-    raw[c] = ok ? *reinterpret_cast<const uint4*>(x + row * D + (c * 32 + hl) * 8) : make_uint4(0, 0, 0, 0);
   float v[NC][8];
-  float s = 0.f;
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
-    const uint32_t w[4] = {raw[c].x, raw[c].y, raw[c].z, raw[c].w};
+    if (ok) {
+      ld8(x + row * D + (c * 32 + hl) * 8, v[c]);
+    } else {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      v[c][2 * i] = __uint_as_float(w[i] << 16);
-      v[c][2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+      for (int i = 0; i < 8; ++i) v[c][i] = 0.f;
     }
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
 #pragma unroll
     for (int i = 0; i < 8; ++i) s += v[c][i];
-  }
 #pragma unroll
   for (int o = 16; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
   const float mean = s * (1.0f / (float)D);
@@ -523,8 +550,7 @@ __global__ void __launch_bounds__(256) ln_fwd16_kernel(const bf16_t* __restrict_
     float o[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) o[i] = (v[c][i] - mean) * rstd * ga[i] + be[i];
-    *reinterpret_cast<uint4*>(y + row * D + col) =
-        make_uint4(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]), pack2bf(o[4], o[5]), pack2bf(o[6], o[7]));
+    st8(y + row * D + col, o);
   }
   if (hl == 0) {
     mean_out[row] = mean;
@@ -532,18 +558,20 @@ __global__ void __launch_bounds__(256) ln_fwd16_kernel(const bf16_t* __restrict_
   }
 }
 
-// Backward, the common case of the post-norm layers (bf16 dy / x / dx of D = 256 * k <= 1024, no row padding, no
-// input scale, no dropout on the LN input, no dx_add; the branch gradient -- dropout, layer mask, its column sums
-// and mask-gradient dot -- as ln_bwd_kernel): a HALF wave per row with 16-byte accesses, 8 waves x 2 rows per block
-// and the same per-block slab row ws[block][3][D] for slab_reduce.  The two halves of a wave (two rows, same
-// columns) combine their column partials with one lane ^ 32 exchange before the cross-wave LDS sum.
-template <int NE>
+// Backward, the common case (bf16 dy of D = 256 * k <= 1024, no row padding, no input scale, no dropout on the LN
+// input): the post-norm layers (bf16 x / dx; the branch gradient -- dropout, layer mask, its column sums and
+// mask-gradient dot -- as ln_bwd_kernel) and the pre-norm layers (fp32 x / dx / dx_add, the residual stream,
+// components.py:846-850): a HALF wave per row with 16-byte accesses, 8 waves x 2 rows per block and the same
+// per-block slab row ws[block][3][D] for slab_reduce.  The two halves of a wave (two rows, same columns) combine
+// their column partials with one lane ^ 32 exchange before the cross-wave LDS sum.
+template <int NE, typename XT = bf16_t, typename DT = bf16_t>
 __global__ void __launch_bounds__(512) ln_bwd16_kernel(
-    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const float* __restrict__ gamma,
-    const float* __restrict__ mean_in, const float* __restrict__ rstd_in, bf16_t* __restrict__ dx,
+    const bf16_t* __restrict__ dy, const XT* __restrict__ x, const float* __restrict__ gamma,
+    const float* __restrict__ mean_in, const float* __restrict__ rstd_in, DT* __restrict__ dx,
     float* __restrict__ dgamma, float* __restrict__ dbeta, int64_t rows, bf16_t* __restrict__ branch, float branch_p,
     uint64_t branch_seed, const float* __restrict__ branch_smask, float* __restrict__ branch_colsum,
-    const bf16_t* __restrict__ branch_pre, float* __restrict__ branch_sdot, float* __restrict__ ws) {
+    const bf16_t* __restrict__ branch_pre, float* __restrict__ branch_sdot, const DT* __restrict__ dx_add,
+    float* __restrict__ ws) {
   constexpr int NC = NE / 8;
   constexpr int D = NE * 32;
   static_assert(LN_BWD_WAVES == 8 && LN_BWD_RPW == 2, "ln_bwd16: the slab layout assumes 16 rows per block");
@@ -554,18 +582,22 @@ __global__ void __launch_bounds__(512) ln_bwd16_kernel(
   const int wave = threadIdx.x >> 6;
   const int64_t row = ((int64_t)blockIdx.x * 8 + wave) * 2 + (lane >> 5);
   const bool ok = row < rows;
-  uint4 rx[NC], rd[NC];
+  float xh[NC][8], g[NC][8], dyv[NC][8], ga[NC][8];
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
     const int64_t off = row * D + (c * 32 + hl) * 8;
-    rx[c] = ok ? *reinterpret_cast<const uint4*>(x + off) : make_uint4(0, 0, 0, 0);
-    rd[c] = ok ? *reinterpret_cast<const uint4*>(dy + off) : make_uint4(0, 0, 0, 0);
+    if (ok) {
+      ld8(x + off, xh[c]);
+      ld8(dy + off, dyv[c]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) xh[c][i] = dyv[c][i] = 0.f;
+    }
   }
   const float mean = ok ? mean_in[row] : 0.f;
   const float rstd = ok ? rstd_in[row] : 0.f;
   const float binv_keep = branch_p > 0.f ? 1.f / (1.f - branch_p) : 1.f;
   const float bsm = branch_smask ? *branch_smask : 1.0f;
-  float xh[NC][8], g[NC][8], dyv[NC][8], ga[NC][8];
   float s1 = 0.f, s2 = 0.f;
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
@@ -573,17 +605,9 @@ __global__ void __launch_bounds__(512) ln_bwd16_kernel(
     const float4 g0 = *reinterpret_cast<const float4*>(gamma + col), g1 = *reinterpret_cast<const float4*>(gamma + col + 4);
     ga[c][0] = g0.x; ga[c][1] = g0.y; ga[c][2] = g0.z; ga[c][3] = g0.w;
     ga[c][4] = g1.x; ga[c][5] = g1.y; ga[c][6] = g1.z; ga[c][7] = g1.w;
-    const uint32_t wx[4] = {rx[c].x, rx[c].y, rx[c].z, rx[c].w};
-    const uint32_t wd[4] = {rd[c].x, rd[c].y, rd[c].z, rd[c].w};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      xh[c][2 * i] = (__uint_as_float(wx[i] << 16) - mean) * rstd;
-      xh[c][2 * i + 1] = (__uint_as_float(wx[i] & 0xffff0000u) - mean) * rstd;
-      dyv[c][2 * i] = __uint_as_float(wd[i] << 16);
-      dyv[c][2 * i + 1] = __uint_as_float(wd[i] & 0xffff0000u);
-    }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
+      xh[c][i] = (xh[c][i] - mean) * rstd;
       g[c][i] = dyv[c][i] * ga[c][i];
       s1 += g[c][i];
       s2 += g[c][i] * xh[c][i];
@@ -604,9 +628,18 @@ __global__ void __launch_bounds__(512) ln_bwd16_kernel(
     float o[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) o[i] = rstd * (g[c][i] - s1 - xh[c][i] * s2);
-    if (ok)
-      *reinterpret_cast<uint4*>(dx + row * D + col) =
-          make_uint4(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]), pack2bf(o[4], o[5]), pack2bf(o[6], o[7]));
+    if (ok) {
+      if (dx_add) {
+        // other gradient paths into the LN input (pre-norm residual); the branch below stays the LN-path gradient
+        float ad[8], sm[8];
+        ld8(dx_add + row * D + col, ad);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) sm[i] = o[i] + ad[i];
+        st8(dx + row * D + col, sm);
+      } else {
+        st8(dx + row * D + col, o);
+      }
+    }
 #pragma unroll
     for (int i = 0; i < 8; ++i) pc[c][i] = 0.f;
     if (branch) {
@@ -768,6 +801,37 @@ extern "C" int64_t dph_layernorm_bwd_workspace(int64_t rows, int64_t D) {
   return cdiv(rows, (int64_t)LN_BWD_WAVES * LN_BWD_RPW) * 3 * D * 4;
 }
 
+namespace {
+bool ln16_env(const char* name) {
+  const char* e = getenv(name);
+  return !(e && e[0] == '0');
+}
+bool ln16_shape(int64_t D, std::initializer_list<const void*> ps) {
+  if (D % 256 != 0 || D > 1024) return false;
+  for (const void* q : ps)
+    if (q && (reinterpret_cast<uintptr_t>(q) & 15) != 0) return false;
+  return true;
+}
+// the 16-byte backward over fp32 x (XT) with bf16 (x32) or fp32 (res32) dx; no branch outputs
+template <typename DT>
+void ln_bwd16_f32x(const void* dy, const float* x, const float* gamma, const float* mean, const float* rstd, DT* dx,
+                   float* dgamma, float* dbeta, int64_t rows, int64_t D, const DT* dx_add, float* ws, dim3 grid,
+                   hipStream_t stream) {
+  const bf16_t* dyb = reinterpret_cast<const bf16_t*>(dy);
+#define LN_BWD16F_LAUNCH(NE)                                                                                     \
+  hipLaunchKernelGGL((ln_bwd16_kernel<NE, float, DT>), grid, dim3(512), 0, stream, dyb, x, gamma, mean, rstd, dx,  \
+                     dgamma, dbeta, rows, (bf16_t*)nullptr, 0.f, (uint64_t)0, (const float*)nullptr,              \
+                     (float*)nullptr, (const bf16_t*)nullptr, (float*)nullptr, dx_add, ws)
+  switch (D / 256) {
+    case 1: LN_BWD16F_LAUNCH(8); break;
+    case 2: LN_BWD16F_LAUNCH(16); break;
+    case 3: LN_BWD16F_LAUNCH(24); break;
+    default: LN_BWD16F_LAUNCH(32); break;
+  }
+#undef LN_BWD16F_LAUNCH
+}
+}  // namespace
+
 extern "C" int dph_layernorm_bwd_ld(const void* dy, const void* x, const float* xscale, const float* gamma,
                                     const float* mean, const float* rstd, void* dx, float* dgamma, float* dbeta,
                                     int64_t rows, int64_t D, int64_t ld, float dropout_p, uint64_t seed, void* branch,
@@ -790,15 +854,16 @@ extern "C" int dph_layernorm_bwd_ld(const void* dy, const void* x, const float* 
     return !(e && e[0] == '0');
   }();
   auto a16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
-  if (ln16 && !xscale && dropout_p <= 0.f && !dx_add && ld == D && D % 256 == 0 && D <= 1024 && a16(dy) && a16(x) &&
-      a16(dx) && a16(gamma) && (!branch || a16(branch)) && (!branch_pre || a16(branch_pre))) {
+  if (ln16 && !xscale && dropout_p <= 0.f && ld == D && D % 256 == 0 && D <= 1024 && a16(dy) && a16(x) &&
+      a16(dx) && a16(gamma) && (!branch || a16(branch)) && (!branch_pre || a16(branch_pre)) &&
+      (!dx_add || a16(dx_add))) {
     const bf16_t* dyb = reinterpret_cast<const bf16_t*>(dy);
     const bf16_t* xb = reinterpret_cast<const bf16_t*>(x);
 #define LN_BWD16_LAUNCH(NE)                                                                                       \
   hipLaunchKernelGGL(ln_bwd16_kernel<NE>, grid, dim3(512), 0, stream, dyb, xb, gamma, mean, rstd,                 \
                      reinterpret_cast<bf16_t*>(dx), dgamma, dbeta, rows, reinterpret_cast<bf16_t*>(branch), branch_p, \
                      branch_seed, branch_smask, branch_colsum, reinterpret_cast<const bf16_t*>(branch_pre),           \
-                     branch_sdot, ws)
+                     branch_sdot, reinterpret_cast<const bf16_t*>(dx_add), ws)
     switch (D / 256) {
       case 1: LN_BWD16_LAUNCH(8); break;
       case 2: LN_BWD16_LAUNCH(16); break;
@@ -841,6 +906,11 @@ extern "C" int dph_layernorm_bwd_x32(const void* dy, const float* x, const float
               "dph_layernorm_bwd_x32: workspace too small (%lld < %lld bytes)", (long long)ws_bytes,
               (long long)dph_layernorm_bwd_workspace(rows, D));
   const dim3 grid((unsigned)cdiv(rows, LN_BWD_WAVES * LN_BWD_RPW));
+  static const bool ln16 = ln16_env("DPH_LN_BWD16");
+  if (ln16 && ln16_shape(D, {dy, x, dx, gamma})) {
+    ln_bwd16_f32x<bf16_t>(dy, x, gamma, mean, rstd, reinterpret_cast<bf16_t*>(dx), dgamma, dbeta, rows, D,
+                          (const bf16_t*)nullptr, ws, grid, stream);
+  } else {
 #define LN_BWD32_LAUNCH(NV)                                                                                      \
   hipLaunchKernelGGL((ln_bwd_kernel<NV, float>), grid, dim3(64 * LN_BWD_WAVES), 0, stream,                       \
                      reinterpret_cast<const bf16_t*>(dy), x, (const float*)nullptr, gamma, mean, rstd,           \
@@ -854,6 +924,7 @@ extern "C" int dph_layernorm_bwd_x32(const void* dy, const float* x, const float
     default: LN_BWD32_LAUNCH(4); break;
   }
 #undef LN_BWD32_LAUNCH
+  }
   if (sums) {
     const int64_t nblk = grid.x;
     hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)cdiv(3 * D, 64), (unsigned)slab_groups(nblk)), dim3(256),
@@ -867,6 +938,18 @@ extern "C" int dph_layernorm_fwd_x32(const float* x, const float* gamma, const f
   DPH_REQUIRE(x && gamma && beta && y && mean && rstd, "dph_layernorm_fwd_x32: null pointer");
   DPH_REQUIRE(D >= 1 && D % 4 == 0 && D <= LN_MAXV * 256 && rows > 0, "dph_layernorm_fwd_x32: unsupported D=%lld",
               (long long)D);
+  static const bool ln16 = ln16_env("DPH_LN_FWD16");
+  if (ln16 && ln16_shape(D, {x, y, gamma, beta})) {
+    const dim3 g16((unsigned)cdiv(rows, 8));
+    bf16_t* yb = reinterpret_cast<bf16_t*>(y);
+    switch (D / 256) {
+      case 1: hipLaunchKernelGGL((ln_fwd16_kernel<8, float>), g16, dim3(256), 0, stream, x, gamma, beta, yb, mean, rstd, rows, eps); break;
+      case 2: hipLaunchKernelGGL((ln_fwd16_kernel<16, float>), g16, dim3(256), 0, stream, x, gamma, beta, yb, mean, rstd, rows, eps); break;
+      case 3: hipLaunchKernelGGL((ln_fwd16_kernel<24, float>), g16, dim3(256), 0, stream, x, gamma, beta, yb, mean, rstd, rows, eps); break;
+      default: hipLaunchKernelGGL((ln_fwd16_kernel<32, float>), g16, dim3(256), 0, stream, x, gamma, beta, yb, mean, rstd, rows, eps); break;
+    }
+    return check_launch("dph_layernorm_fwd_x32");
+  }
   const dim3 grid((unsigned)cdiv(rows, 4 * LN_FWD_RPW));
 #define LN_FWD32_LAUNCH(NV)                                                                                      \
   hipLaunchKernelGGL((ln_fwd_kernel<NV, false, float>), grid, dim3(256), 0, stream, x, (const float*)nullptr,    \
@@ -894,6 +977,10 @@ extern "C" int dph_layernorm_bwd_res32(const void* dy, const float* x, const flo
               "dph_layernorm_bwd_res32: workspace too small (%lld < %lld bytes)", (long long)ws_bytes,
               (long long)dph_layernorm_bwd_workspace(rows, D));
   const dim3 grid((unsigned)cdiv(rows, LN_BWD_WAVES * LN_BWD_RPW));
+  static const bool ln16 = ln16_env("DPH_LN_BWD16");
+  if (ln16 && ln16_shape(D, {dy, x, dx, gamma, dx_add})) {
+    ln_bwd16_f32x<float>(dy, x, gamma, mean, rstd, dx, dgamma, dbeta, rows, D, dx_add, ws, grid, stream);
+  } else {
 #define LN_BWDR_LAUNCH(NV)                                                                                       \
   hipLaunchKernelGGL((ln_bwd_kernel<NV, float, float>), grid, dim3(64 * LN_BWD_WAVES), 0, stream,                \
                      reinterpret_cast<const bf16_t*>(dy), x, (const float*)nullptr, gamma, mean, rstd, dx, dgamma, \
@@ -906,6 +993,7 @@ extern "C" int dph_layernorm_bwd_res32(const void* dy, const float* x, const flo
     default: LN_BWDR_LAUNCH(4); break;
   }
 #undef LN_BWDR_LAUNCH
+  }
   if (sums) {
     const int64_t nblk = grid.x;
     hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)cdiv(3 * D, 64), (unsigned)slab_groups(nblk)), dim3(256),

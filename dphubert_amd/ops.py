@@ -941,9 +941,15 @@ def conv_dgrad_phases(dz: torch.Tensor, wt: torch.Tensor, B: int, Lout: int, Lin
         weven = torch.cat([wt[2 * Cin:3 * Cin], wt[:Cin]], dim=1)
         gemm(K.mat(dz, O, rows_per_batch=Lout - 1, batch_stride=Lout * O), K.dense(weven), 2 * Cin, Lout - 1,
              B * (Lout - 1), Cin, 2 * O, cm, dmask)
-    gemm(K.mat(dz, O, rows_per_batch=1, batch_stride=Lout * O), K.mat(wt, O), 0, 1, B, Cin, O, cm, dmask)
-    gemm(K.mat(dz, O, rows_per_batch=1, batch_stride=Lout * O, offset=(Lout - 1) * O), K.mat(wt, O, offset=2 * Cin * O),
-         2 * Lout * Cin, 1, B, Cin, O, cm, dmask)
+    # the two edge-row GEMMs (B rows each) in ONE launch: grid batch z = 0 / 1 picks dz row 0 / Lout - 1, tap
+    # W_0 / W_2 and output row 0 / 2 Lout (the z offsets), aux_in following the C layout
+    kw = {}
+    if z_pre is not None:
+        kw = dict(act=K.ACT_GELU_BWD, aux_in=zflat, colmask=cm, colsum_aux=dmask)
+    K.gemm(K.mat(dz, O, rows_per_batch=1, batch_stride=Lout * O, z_inner=(Lout - 1) * O),
+           K.mat(wt, O, z_inner=2 * Cin * O),
+           K.mat(d, Cin, rows_per_batch=1, batch_stride=Lin * Cin, z_inner=2 * Lout * Cin), B, Cin, O,
+           a_kcontig=True, b_kcontig=True, batch=2, **kw)
     if Lin > 2 * Lout + 1:
         d.view(B, Lin, Cin)[:, 2 * Lout + 1:].zero_()
     return d
