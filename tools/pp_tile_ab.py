@@ -1,7 +1,9 @@
 """Ping-pong tile A/B on the step's projection GEMMs WITH their epilogues (GELU + stored factor + dropout, fp32
 residual stream, DGK input gradient): every tile kind forced through DPH_PP_FORCE (read per call), interleaved
 rounds, median us per (shape, tile).  usage: python tools/pp_tile_ab.py [rounds] [kind ...]
-kinds: 12 = 256x256, 13 = 128x256, 14 = 256x128, 15 = 128x192, 16 = 128x128 (two blocks per CU)."""
+kinds: 12 = 256x256, 13 = 128x256, 14 = 256x128, 15 = 128x192, 16 = 128x128 (two blocks per CU).
+DPH_AB_SET=conv: the conv extractor's input-gradient GEMMs with the previous layer's GELU backward in the epilogue
+(ops.conv_dgrad_phases: M = B x L rows, N = Cin = 512, K = 512 / 1024) instead of the encoder projections."""
 import os
 import statistics
 import sys
@@ -16,13 +18,26 @@ dev = "cuda"
 bf = lambda *s: (torch.rand(*s, device=dev) * 2 - 1).to(torch.bfloat16)  # noqa: E731
 
 
-def case(name, n, k, **epi):
-    return name, n, k, epi
+def case(name, n, k, m=M, **epi):
+    return name, n, k, m, epi
 
 
 u = torch.empty(M, 3072, device=dev, dtype=torch.bfloat16)
 cm = torch.rand(3072, device=dev) + 0.5
 res32 = torch.randn(M, 768, device=dev)
+MC = 16 * 7999
+zc = torch.empty(MC, 512, device=dev, dtype=torch.bfloat16)
+cmc = torch.rand(512, device=dev) + 0.5
+dmc = torch.zeros(512, device=dev)
+CONV = [
+    case("conv2 dgrad k=3 odd rows (gelu bwd)", 512, 512, m=MC, act=K.ACT_GELU_BWD, aux_in=zc, colmask=cmc,
+         colsum_aux=dmc),
+    case("conv3 dgrad k=3 odd rows (gelu bwd)", 512, 512, m=16 * 3999, act=K.ACT_GELU_BWD, aux_in=zc, colmask=cmc,
+         colsum_aux=dmc),
+    case("conv2 dgrad k=3 even rows (gelu bwd)", 512, 1024, m=MC, act=K.ACT_GELU_BWD, aux_in=zc, colmask=cmc,
+         colsum_aux=dmc),
+    case("conv1 dgrad k=3 odd rows (no epilogue)", 512, 512, m=16 * 15999),
+]
 CASES = [
     case("ffn1 fwd student (gelu, gelu' factor, mask, dropout)", 3072, 768, act=K.ACT_GELU, pre_out=u, colmask=cm,
          dropout_p=0.1, seed=3, flags=K.GEMM_PRE_DGK, bias=True),
@@ -34,17 +49,19 @@ CASES = [
     case("ffn1 dgrad", 768, 3072),
     case("qkv dgrad", 768, 2304),
 ]
+if os.environ.get("DPH_AB_SET") == "conv":
+    CASES = CONV
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 5
 kinds = sys.argv[2:] or ["auto", "15", "16", "13", "12", "14"]
 data = {}
-for name, n, k, epi in CASES:
-    A, B = bf(M, k), bf(n, k)
+for name, n, k, m, epi in CASES:
+    A, B = bf(m, k), bf(n, k)
     odt = torch.float32 if epi.get("c_dtype") == K.OUT_F32 else torch.bfloat16
-    C = torch.empty(M, n, device=dev, dtype=odt)
+    C = torch.empty(m, n, device=dev, dtype=odt)
     kw = dict(epi)
     if kw.pop("bias", False):
         kw["bias"] = torch.randn(n, device=dev)
-    data[name] = (A, B, C, n, k, kw)
+    data[name] = (A, B, C, m, n, k, kw)
 
 
 def run(name, kind, iters=20):
@@ -52,8 +69,8 @@ def run(name, kind, iters=20):
         os.environ.pop("DPH_PP_FORCE", None)
     else:
         os.environ["DPH_PP_FORCE"] = kind
-    A, B, C, n, k, kw = data[name]
-    f = lambda: K.gemm(K.dense(A), K.dense(B), K.dense(C), M, n, k, a_kcontig=True, b_kcontig=True, **kw)  # noqa
+    A, B, C, m, n, k, kw = data[name]
+    f = lambda: K.gemm(K.dense(A), K.dense(B), K.dense(C), m, n, k, a_kcontig=True, b_kcontig=True, **kw)  # noqa
     f()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
@@ -70,9 +87,9 @@ for _ in range(rounds):
         for kd in kinds:
             res.setdefault((name, kd), []).append(run(name, kd))
 os.environ.pop("DPH_PP_FORCE", None)
-for name, n, k, _e in CASES:
-    fl = 2.0 * M * n * k
+for name, n, k, m, _e in CASES:
+    fl = 2.0 * m * n * k
     row = " | ".join(f"{kd} {statistics.median(res[(name, kd)]):6.1f}" for kd in kinds)
     best = min(kinds, key=lambda kd: statistics.median(res[(name, kd)]))
-    print(f"{name:52s} {M}x{n}x{k}: {row}  (best {best}: "
+    print(f"{name:52s} {m}x{n}x{k}: {row}  (best {best}: "
           f"{fl / statistics.median(res[(name, best)]) / 1e6:5.0f} TF/s)", flush=True)
