@@ -1432,7 +1432,8 @@ class PosConvFn(torch.autograd.Function):
             dh = dh if dh.dtype == F32 else dh.float()
             call("dph_branch_bwd_f32", ptr(dh), ptr(ds0), 0, M, D, cfg["p"], ctx.seed, None, None, 0, None, None,
                  None, _s())
-        dz = torch.empty_like(ds0)
+        # (+64 elements of slack: the weight gradient below reads 64 columns from group g's first one, see there)
+        dz = torch.empty(M * D + 64, dtype=BF16, device=dev)[:M * D].view(M, D)
         call("dph_gelu_mask_bwd", ptr(ds0), ptr(z), None, ptr(dz), None, M, D, _s())
         db, _ = go.buf(p_bias)
         call("dph_colsum", ptr(dz), ptr(db), M, D, *colsum_ws(M, D, dev), _s())
@@ -1447,14 +1448,19 @@ class PosConvFn(torch.autograd.Function):
         K.gemm(K.mat(dzg, Cg, z_inner=Tp2 * Cg), K.mat(wt, Kk * Cg, z_div=G, z_outer=0, z_inner=Cg * Kk * Cg),
                K.mat(dx, D, z_div=G, z_outer=T * D, z_inner=Cg), T, Cg, Kk * Cg, a_kcontig=True, b_kcontig=True,
                batch=B * G, residual=ds0)
-        # weight gradient in GEMM image layout [G][Cg_out][K*Cg_in]
+        # weight gradient in GEMM image layout [G][Cg_out][K*Cg_in].  The ping-pong (mn, mn) kernel takes M >= 64:
+        # a group's Cg = 48 output channels run as Mp = 64 GEMM rows (the 16 extra read the next group's dz columns
+        # -- or the slack past the last row -- and land in rows that are dropped); DPH_POSCONV_MP=0 keeps M = Cg on the
+        # register-staged kernel (A/B)
         Tp = P + T + Q
-        dimg = torch.empty(G, Cg, Kk * Cg, dtype=F32, device=dev)
+        Mp = 64 if (Cg < 64 and Cg % 8 == 0 and os.environ.get("DPH_POSCONV_MP", "1") != "0") else Cg
+        dimg_p = torch.empty(G, Mp, Kk * Cg, dtype=F32, device=dev)
         A = K.mat(dz, D, z_inner=Cg)
         Bm = K.mat(xg, Cg, rows_per_batch=T, batch_stride=G * Tp * Cg, z_inner=Tp * Cg)
-        splits = K.choose_splits(Cg, Kk * Cg, B * T, batch=G)
-        ws = K.gemm(A, Bm, K.mat(dimg, Kk * Cg, z_inner=Cg * Kk * Cg), Cg, Kk * Cg, B * T, a_kcontig=False,
+        splits = K.choose_splits(Mp, Kk * Cg, B * T, batch=G)
+        ws = K.gemm(A, Bm, K.mat(dimg_p, Kk * Cg, z_inner=Mp * Kk * Cg), Mp, Kk * Cg, B * T, a_kcontig=False,
                     b_kcontig=False, c_dtype=K.OUT_F32, batch=G, splits=splits, device=dev)
+        dimg = dimg_p[:, :Cg].contiguous() if Mp != Cg else dimg_p
         dg = torch.empty_like(norm)
         dv = torch.empty_like(wv)
         wn_ws = _weight_norm_ws(D * Cg, Kk, dev)

@@ -361,6 +361,33 @@ def test_posconv_vs_oracle():
         assert e < 5e-2, (n, e)
 
 
+@pytest.mark.parametrize("B,T", [(2, 150), (3, 499)])
+def test_posconv_wgrad_padded_rows_match(B, T, monkeypatch):
+    """The positional conv's weight gradient with each 48-channel group run as 64 GEMM rows on the ping-pong
+    (mn, mn) kernel (the extra rows read the next group's dz columns and are dropped) against the 48-row GEMM on
+    the register-staged kernel (DPH_POSCONV_MP=0): same sums, other split / summation order (fp32)."""
+    cfg = _cfg(1)
+    m, _ = _model(cfg, seed=3)
+    tr = m.encoder.transformer.train()
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(B, T, 768, generator=g).to(torch.bfloat16).to(DEV)
+    gh = torch.randn(B, T, 768, generator=g).to(torch.bfloat16).to(DEV)
+    grads = {}
+    for mp in ("0", "1"):
+        monkeypatch.setenv("DPH_POSCONV_MP", mp)
+        tr.zero_grad(set_to_none=True)
+        xg = x.clone().requires_grad_(True)
+        tr._preprocess(xg).backward(gh)
+        grads[mp] = {n: prm.grad.detach().float().clone() for n, prm in tr.named_parameters()
+                     if n.startswith("pos_conv_embed") and prm.grad is not None}
+        grads[mp]["x"] = xg.grad.detach().float().clone()
+    assert grads["0"].keys() == grads["1"].keys() and len(grads["1"]) >= 3
+    for n in grads["0"]:
+        a, b = grads["0"][n], grads["1"][n]
+        assert torch.isfinite(b).all(), n
+        assert (a - b).norm() <= 1e-5 * a.norm() + 1e-12, (n, float((a - b).norm() / a.norm()))
+
+
 def test_feature_projection_vs_oracle():
     cfg = _cfg(1)
     m, sd = _model(cfg, seed=3)
