@@ -2719,6 +2719,15 @@ struct PpwPlan {
 // (~4 TB/s) and that launch.  Each split keeps at least eight K-tiles.  The 128 x 192 and 128 x 128 tiles run two
 // blocks per CU here (<= 128 VGPRs, <= 80 KB LDS).  Long-K (conv) shapes: 128 x 192 tiles and ~48 K-tiles per
 // split (up to 32 splits).  Sweep behind both rules: profiles/r3_s9_wgrad_sweep.txt (tools/wgrad_sweep.py).
+// DPH_PPW_LONGK=0: the round-3 long-K rule (128 x 192, ~48 K-tiles per split) for the conv weight gradients (A/B)
+static bool long_k_one_round() {
+  static const bool on = [] {
+    const char* e = getenv("DPH_PPW_LONGK");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 static PpwPlan ppw_plan(int64_t M, int64_t N, int64_t K, int64_t batch, int want_splits) {
   struct Opt { int kind, bm, bn, per_cu; double tf; };
   static const Opt opts[] = {{12, 256, 256, 1, 1514.0}, {15, 128, 192, 2, 1282.0}, {13, 128, 256, 1, 1221.0},
@@ -2741,7 +2750,15 @@ static PpwPlan ppw_plan(int64_t M, int64_t N, int64_t K, int64_t batch, int want
       if (kct < 2 || cdiv(nkt, kct) != s || nkt - (s - 1) * kct < 2) continue;
       if (want_splits == 0 && kct < MIN_KT && s > 1) continue;
       double t;
-      if (nkt >= 768 && want_splits == 0) {
+      const int64_t tiles256 = cdiv(M, (int64_t)256) * cdiv(N, (int64_t)256) * batch;
+      if (nkt >= 384 && tiles256 <= 32 && want_splits == 0 && long_k_one_round()) {
+        // long K over few output tiles (the conv extractor's weight gradients, 512 x k*512 over B*L frames): ONE round
+        // of 256 x 256 (tile, split) blocks over the CUs -- 12 tiles x 21 splits: conv1-4 447 / 236 / 129 / 74 us
+        // against 529 / 286 / 134 / 82 us on the 128 x 192 / ~48-K-tile rule below (profiles/r4_s40_wgrad_sweep.txt);
+        // the nearest feasible split count on that tile, other tiles only as a fallback
+        const int64_t s1 = std::max<int64_t>(1, std::min<int64_t>(32, cus / tiles256));
+        t = (double)(s > s1 ? s - s1 : s1 - s) + (o.kind == 12 ? 0.0 : 1000.0);
+      } else if (nkt >= 768 && want_splits == 0) {
         // long K: the measured optimum sits at ~48 K-tiles per split on 128 x 192 (conv1 / conv2 at 32 splits)
         if (o.kind != 15) continue;
         t = kct > 48 ? (double)(kct - 48) : (double)(48 - kct);
