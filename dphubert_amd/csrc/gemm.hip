@@ -2728,6 +2728,15 @@ static bool long_k_one_round() {
   return on;
 }
 
+// DPH_PPW_GSPLIT=0: the grouped weight gradients on the rounds model alone (A/B)
+static bool grouped_two_splits() {
+  static const bool on = [] {
+    const char* e = getenv("DPH_PPW_GSPLIT");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 static PpwPlan ppw_plan(int64_t M, int64_t N, int64_t K, int64_t batch, int want_splits) {
   struct Opt { int kind, bm, bn, per_cu; double tf; };
   static const Opt opts[] = {{12, 256, 256, 1, 1514.0}, {15, 128, 192, 2, 1282.0}, {13, 128, 256, 1, 1221.0},
@@ -2758,6 +2767,12 @@ static PpwPlan ppw_plan(int64_t M, int64_t N, int64_t K, int64_t batch, int want
         // the nearest feasible split count on that tile, other tiles only as a fallback
         const int64_t s1 = std::max<int64_t>(1, std::min<int64_t>(32, cus / tiles256));
         t = (double)(s > s1 ? s - s1 : s1 - s) + (o.kind == 12 ? 0.0 : 1000.0);
+      } else if (batch > 1 && M >= 256 && N >= 256 && tiles256 * 2 <= cus * 3 && nkt >= 32 && want_splits == 0 &&
+                 grouped_two_splits()) {
+        // grouped weight gradients (n layers' dW of one shape per launch) whose 256 x 256 tiles fill at most 1.5
+        // rounds: two K-splits on that tile -- n = 12 QKV (1.27 rounds) 550 -> 478 us, out-proj (0.42) 194 -> 170 us
+        // (profiles/r4_s42_wgrad_group_sweep.txt; FFN1 / FFN2 at 1.69 rounds stay on one split)
+        t = (o.kind == 12 && s == 2) ? 0.0 : 1000.0 + (double)s;
       } else if (nkt >= 768 && want_splits == 0) {
         // long K: the measured optimum sits at ~48 K-tiles per split on 128 x 192 (conv1 / conv2 at 32 splits)
         if (o.kind != 15) continue;

@@ -142,7 +142,10 @@ def tracks_eager_report(eager, gr, le, lg):
     within the spread of the others, wherever its cluster -- and must sit within 4x the largest eager-vs-eager
     difference:
       * losses: that, plus 1e-3 relative (a stale or missing op in the replay moves the loss by > 1e-2);
-      * each parameter: that, or 5e-3 (1-D biases 1e-2: cancellation-heavy column sums); k_proj.bias is left out
+      * each parameter, against ITS nearest eager run (the branches of different parameters' cancellation-dominated
+        sums fall independently: the run nearest over the whole vector can sit in another cluster for one
+        HardConcrete log_alpha -- r4_s44: 0.0123 against 4 x 0.00227 for layer 1's FFN log_alpha, the whole vector
+        5.95e-5 inside its bound): that, or 5e-3 (1-D biases 1e-2: cancellation-heavy column sums); k_proj.bias is left out
         (its gradient is exactly zero by softmax shift invariance, so Adam turns the atomic-order noise of that
         zero into +-lr steps);
       * the whole parameter vector: that, or 1e-4.  The eager runs themselves split into branches ~1e-5 and
@@ -163,7 +166,7 @@ def tracks_eager_report(eager, gr, le, lg):
             ok = False
             lines.append(f"loss step {s_}: graph {b} eager {vals}")
     for n in names:
-        e = rel_l2(pg[n].detach().cpu(), pe[near][n].detach().cpu())
+        e = min(rel_l2(pg[n].detach().cpu(), d[n].detach().cpu()) for d in pe)
         base = max(rel_l2(pe[i][n].detach().cpu(), pe[j][n].detach().cpu()) for i, j in pairs)
         if not e < max(1e-2 if pg[n].dim() == 1 else 5e-3, 4 * base):
             ok = False
