@@ -135,13 +135,15 @@ def cpu_baseline(batch: int = 2, warmup: int = 3, steps: int = 5, seconds: float
 
 
 def pmc_traffic(args):
-    """HBM bytes per launch of every GEMM variant from rocprofv3 PMC counters.
+    """HBM bytes of every GEMM, attention and conv0 kernel variant from rocprofv3 PMC counters.
 
     Two child runs of this script (1 warm-up + 1 step, same workload), one counter per pass
     (FETCH_SIZE and WRITE_SIZE do not fit one TCC pass), started before this process touches the
     GPU.  gfx950 corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE is in KiB and reports
     half the bytes of wide coalesced reads -> bytes = 2 * 1024 * FETCH_SIZE; WRITE_SIZE is exact
-    for 16-B stores -> bytes = 1024 * WRITE_SIZE.  Returns {kernel name: bytes per launch}.
+    for 16-B stores -> bytes = 1024 * WRITE_SIZE.  Returns {kernel name: [total bytes, launches]}
+    (launches of the FETCH pass; both passes run the same launches).  DPH_BENCH_PMC_DIR: keep the
+    counter CSVs there (profiles/ evidence of the traffic figures).
     """
     exe = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
     if not os.path.exists(exe):
@@ -151,7 +153,8 @@ def pmc_traffic(args):
     with tempfile.TemporaryDirectory(dir="/tmp") as td:
         for counter, scale in (("FETCH_SIZE", 2 * 1024.0), ("WRITE_SIZE", 1024.0)):
             d = os.path.join(td, counter)
-            cmd = [exe, "--pmc", counter, "--kernel-include-regex", "gemm_kernel", "-f", "csv", "-d", d, "-o", "run",
+            cmd = [exe, "--pmc", counter, "--kernel-include-regex", "gemm_kernel|attn_|conv0_", "-f", "csv", "-d", d,
+                   "-o", "run",
                    "--", sys.executable, os.path.join(here, "bench.py"), "--steps", "1", "--warmup", "1",
                    "--no-cpu-baseline", "--no-roofline", "--traffic", "off", "--graphs", "off", "--batch", str(args.batch),
                    "--seconds", str(args.seconds), "--model", args.model, "--student", args.student]
@@ -164,6 +167,10 @@ def pmc_traffic(args):
                      if f.endswith("counter_collection.csv")]
             if not files:
                 raise RuntimeError(f"rocprofv3 {counter}: no counter_collection.csv")
+            keep = os.environ.get("DPH_BENCH_PMC_DIR")
+            if keep:
+                os.makedirs(keep, exist_ok=True)
+                shutil.copy(files[0], os.path.join(keep, f"pmc_{counter}.csv"))
             sums = {}
             for row in csv.DictReader(open(files[0])):
                 if row["Counter_Name"] != counter:
@@ -172,8 +179,33 @@ def pmc_traffic(args):
                 v[0] += float(row["Counter_Value"]) * scale
                 v[1] += 1
             for k, (tot, n) in sums.items():
-                out[k] = out.get(k, 0.0) + tot / n
-    return out
+                o = out.setdefault(k, [0.0, 0])
+                o[0] += tot / n          # mean bytes per launch of this counter ...
+                o[1] = max(o[1], n)
+    return {k: [b * n, n] for k, (b, n) in out.items()}   # ... -> total bytes over the launches
+
+
+# rocprof kernel-name fragments of the launches behind each kernel_table span (kernels.SPAN_WORK labels)
+SPAN_KERNELS = {
+    "attn_fwd_drop": ["attn_fwd32v2_kernel<true>"], "attn_fwd": ["attn_fwd32v2_kernel<false>"],
+    "attn_bwd_drop": ["attn_bwd_kernel<true"], "attn_bwd": ["attn_bwd_kernel<false"],
+    "conv0_gn_fwd": ["conv0_gram_part_kernel", "conv0_gram_reduce", "conv0_apply_kernel<true"],
+    "conv0_gn_bwd": ["conv0_gram_part_kernel", "conv0_gram_reduce", "conv0_gn_bwd_kernel", "conv0_bwd_finalize"],
+}
+
+
+def traffic_per_launch(traffic, frags):
+    """PMC bytes per launch summed over the kernels a span launches (each fragment: launch-weighted over every
+    template variant whose rocprof name contains it)."""
+    if not traffic:
+        return None
+    tot = 0.0
+    for fr in frags:
+        hits = [v for k, v in traffic.items() if fr in k]
+        if not hits:
+            return None
+        tot += sum(b for b, _ in hits) / sum(n for _, n in hits)
+    return tot
 
 
 def check_step(loss: float, terms, main_loss):
@@ -316,6 +348,20 @@ def main():
     torch.cuda.synchronize()
     graphed = trainer._graph is not None
     log(f"step mode: {'HIP graph replay' if graphed else 'eager'}")
+    ddp_plan = None
+    if world > 1:
+        # the data-parallel plan of this run: buckets, the weight-gradient group planned on the MAX frame
+        # count over the ranks, and the modelled window (compute end vs last collective end, ms from the start of
+        # the encoder backward) at the assumed xGMI ring rate
+        red = trainer.reducer
+        plan = trainer.wgrad_plan or {"group": trainer.wgrad_group}
+        ddp_plan = {"buckets": len(red.flat), "bucket_mb": [round(f.numel() * f.element_size() / 2 ** 20, 1)
+                                                            for f in red.flat],
+                    "grad_comm": args.grad_comm, "wgrad_group": plan.get("group"), "frames": plan.get("frames"),
+                    "assumed_bus_gbps": plan.get("bus_gbps"),
+                    "modelled_compute_end_ms": round(plan["timeline_ms"][0], 3) if "timeline_ms" in plan else None,
+                    "modelled_comm_end_ms": round(plan["timeline_ms"][1], 3) if "timeline_ms" in plan else None}
+        log(f"ddp plan: {json.dumps(ddp_plan)}")
     # GEMM launches of the LAST timed step are bracketed by HIP events on their launch stream (an
     # event marker costs ~3 us of GPU time, so bracketing every step would tax the headline number).
     # With graphs, that step replays a second capture of the same step whose GEMMs carry event nodes.
@@ -398,6 +444,8 @@ def main():
         "peak_hbm_gib": round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 2),
         "step_mode": "hip_graph" if graphed else "eager",
     }
+    if ddp_plan is not None:
+        out["ddp_plan"] = ddp_plan
     if prof is not None and not in_loop:
         torch.cuda.synchronize()
         saved, trainer._graphs = trainer._graphs, {}      # one eager step with the profiler on
@@ -428,8 +476,10 @@ def main():
         all_fl = sum(v["flops"] for v in summ.values())
         tr = None
         if traffic:
+            # launch-weighted over EVERY template variant of the dominant kernel (the algorithmic bytes below
+            # average all of its launches too)
             hits = [v for k, v in traffic.items() if name in k]
-            tr = round(hits[0]) if hits else None
+            tr = round(sum(b for b, _ in hits) / sum(n for _, n in hits)) if hits else None
         alg_b = d["bytes"] / d["launches"]
         out["roofline"] = {"bound": "mfma", "kernel": name, "achieved": round(achieved, 1),
                            "peak": MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / MFMA_PEAK_TFLOPS, 4),
@@ -453,11 +503,35 @@ def main():
                 ach, peak, unit = per / avg_s / 1e12, MFMA_PEAK_TFLOPS, "TFLOP/s"
             else:
                 ach, peak, unit = per / avg_s / 1e9, HBM_PEAK_GBPS, "GB/s"
-            table.append({"kernel": label, "bound": "mfma" if d["unit"] == "flop" else "hbm",
-                          "launches_per_step": d["launches"], "avg_launch_us": round(avg_s * 1e6, 2),
-                          "work_per_launch": per, "work_unit": d["unit"], "achieved": round(ach, 1), "peak": peak,
-                          "unit": unit, "frac": round(ach / peak, 4), "ms_per_step": round(d["ms"], 3)})
+            row = {"kernel": label, "bound": "mfma" if d["unit"] == "flop" else "hbm",
+                   "launches_per_step": d["launches"], "avg_launch_us": round(avg_s * 1e6, 2),
+                   "work_per_launch": per, "work_unit": d["unit"], "achieved": round(ach, 1), "peak": peak,
+                   "unit": unit, "frac": round(ach / peak, 4), "ms_per_step": round(d["ms"], 3)}
+            if label in SPAN_KERNELS:
+                tb = traffic_per_launch(traffic, SPAN_KERNELS[label])
+                row["pmc_bytes_per_launch"] = round(tb) if tb else None
+                if tb and d["unit"] == "byte":
+                    row["traffic_ratio"] = round(tb / per, 3)
+            table.append(row)
         out["kernel_table"] = table
+        # north_star's bar: MFMA utilisation of masked attention + FFN over the same profiled step -- the algorithmic
+        # FLOPs of every attention launch (forward Q K^T + P V, backward 2.5x) and of every FFN GEMM (FFN1 / FFN2
+        # forward of teacher and student, their input and weight gradients) over the summed event-timed durations
+        spans = prof.span_summary()
+        attn = [v for k, v in spans.items() if k.startswith("attn_")]
+        ffn = prof.role_summary().get("ffn")
+        a_ms, a_fl = sum(v["ms"] for v in attn), sum(v["work"] for v in attn)
+        f_ms, f_fl = (ffn["ms"], ffn["flops"]) if ffn else (0.0, 0.0)
+        if a_ms + f_ms > 0:
+            util = (a_fl + f_fl) / ((a_ms + f_ms) / 1e3) / 1e12 / MFMA_PEAK_TFLOPS
+            out["mfma_util_attn_ffn"] = round(util, 4)
+            out["mfma_util_detail"] = {
+                "attention": {"ms_per_step": round(a_ms, 3), "gflop": round(a_fl / 1e9, 1),
+                              "util": round(a_fl / (a_ms / 1e3) / 1e12 / MFMA_PEAK_TFLOPS, 4) if a_ms else None},
+                "ffn_gemms": {"ms_per_step": round(f_ms, 3), "gflop": round(f_fl / 1e9, 1),
+                              "launches": ffn["launches"] if ffn else 0,
+                              "util": round(f_fl / (f_ms / 1e3) / 1e12 / MFMA_PEAK_TFLOPS, 4) if f_ms else None},
+                "peak_tflops": MFMA_PEAK_TFLOPS, "timed_on": prof_mode}
     if batches is not None:
         shapes = [tuple(b[0].shape) for b in batches[args.warmup:]]
         out["config"]["batch_shapes"] = [f"{bb}x{ss / 16000:.2f}s" for bb, ss in shapes]

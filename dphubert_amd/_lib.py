@@ -67,6 +67,8 @@ S = vp  # hipStream_t
 
 _SIGS = {
     "dph_abi_version": ([], C.c_int),
+    "dph_set_deterministic": ([C.c_int], C.c_int),
+    "dph_get_deterministic": ([], C.c_int),
     "dph_gemm": ([C.POINTER(DphGemmArgs), S], C.c_int),
     "dph_gemm_mn_plan": ([i64, i64, i64, i64], C.c_int),
     "dph_gemm_grouped": ([C.POINTER(DphGemmArgs), C.POINTER(DphGemmGroup), S], C.c_int),
@@ -93,22 +95,28 @@ _SIGS = {
     "dph_layernorm_bwd_workspace": ([i64, i64], i64),
     "dph_attention_fwd": ([vp, vp, vp, vp, vp, vp, i64, i64, i64, f32, f32, u64, vp, S], C.c_int),
     "dph_attention_keep_bytes": ([i64, i64, i64], i64),
-    "dph_attention_bwd_prep": ([vp, vp, vp, vp, vp, i64, i64, i64, S], C.c_int),
+    "dph_attention_bwd_prep": ([vp, vp, vp, vp, vp, i64, i64, i64, vp, i64, S], C.c_int),
+    "dph_attention_bwd_prep_workspace": ([i64, i64, i64], i64),
     "dph_attention_bwd": ([vp, vp, vp, vp, vp, vp, vp, i64, i64, i64, f32, f32, u64, vp, S], C.c_int),
     "dph_attention_fwd_relpos": ([vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, i64, f32, f32, u64, vp, S], C.c_int),
-    "dph_attention_bwd_relpos": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, i64, f32, f32, u64, vp, S],
-                                 C.c_int),
+    "dph_attention_bwd_relpos": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, i64, f32, f32, u64, vp, vp,
+                                  i64, S], C.c_int),
+    "dph_attention_bwd_relpos_workspace": ([i64, i64, i64], i64),
     "dph_relpos_table": ([vp, vp, vp, vp, i64, i64, i64, i64, i64, S], C.c_int),
     "dph_relpos_table_bwd": ([vp, vp, vp, i64, i64, i64, i64, i64, S], C.c_int),
     "dph_wavlm_gate_fwd": ([vp, i64, vp, vp, vp, vp, vp, i64, i64, i64, i64, S], C.c_int),
-    "dph_wavlm_gate_bwd": ([vp, i64, vp, vp, vp, vp, vp, vp, i64, vp, vp, vp, vp, i64, i64, i64, i64, S], C.c_int),
+    "dph_wavlm_gate_bwd": ([vp, i64, vp, vp, vp, vp, vp, vp, i64, vp, vp, vp, vp, i64, i64, i64, i64, i64, S],
+                           C.c_int),
+    "dph_wavlm_gate_bwd_workspace": ([i64, i64, i64], i64),
     "dph_conv0_gn_fwd": ([vp, i64, i64, vp, i64, i64, i64, vp, vp, vp, vp, vp, vp, vp, i64, S], C.c_int),
-    "dph_conv0_gn_bwd_workspace": ([i64, i64], i64),
+    "dph_conv0_gn_bwd_workspace": ([i64, i64, i64], i64),
+    "dph_conv0_bwd_workspace": ([i64, i64, i64], i64),
     "dph_conv0_gn_bwd": ([vp, i64, i64, vp, i64, i64, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, S],
                          C.c_int),
     "dph_conv0_fwd": ([vp, i64, i64, vp, vp, i64, i64, i64, vp, S], C.c_int),
-    "dph_col2im_gelu_bwd": ([vp, i64, i64, i64, i64, i64, i64, vp, vp, vp, vp, S], C.c_int),
-    "dph_gelu_mask_bwd": ([vp, vp, vp, vp, vp, i64, i64, S], C.c_int),
+    "dph_col2im_gelu_bwd": ([vp, i64, i64, i64, i64, i64, i64, vp, vp, vp, vp, vp, i64, S], C.c_int),
+    "dph_gelu_mask_bwd": ([vp, vp, vp, vp, vp, i64, i64, vp, i64, S], C.c_int),
+    "dph_rowblock_workspace": ([i64, i64], i64),
     "dph_regroup_pad": ([vp, vp, i64, i64, i64, i64, i64, i64, S], C.c_int),
     "dph_weight_norm_fwd": ([vp, vp, i64, i64, i64, i64, vp, vp, vp, vp, vp, i64, S], C.c_int),
     "dph_weight_norm_bwd": ([vp, vp, vp, vp, i64, i64, i64, i64, vp, vp, vp, i64, S], C.c_int),
@@ -117,18 +125,18 @@ _SIGS = {
     "dph_cast_bf16_multi": ([vp, i64, S], C.c_int),
     "dph_copy_f32_multi": ([vp, i64, i64, S], C.c_int),
     "dph_conv_lengths": ([vp, vp, i64, i64, vp, vp, S], C.c_int),
-    "dph_conv0_bwd": ([vp, i64, i64, i64, i64, i64, vp, vp, vp, S], C.c_int),
+    "dph_conv0_bwd": ([vp, i64, i64, i64, i64, i64, vp, vp, vp, vp, i64, S], C.c_int),
     "dph_gelu_mask_fwd": ([vp, vp, vp, i64, i64, S], C.c_int),
     "dph_layernorm_gelu_fwd": ([vp, C.c_int, vp, vp, vp, vp, vp, vp, vp, i64, i64, f32, S], C.c_int),
     "dph_layernorm_bwd_x32": ([vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, vp, i64, S], C.c_int),
     "dph_transpose_bf16_multi": ([vp, i64, S], C.c_int),
     "dph_layernorm_fwd_x32": ([vp, vp, vp, vp, vp, vp, i64, i64, f32, S], C.c_int),
     "dph_layernorm_bwd_res32": ([vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, vp, vp, i64, S], C.c_int),
-    "dph_branch_bwd_f32": ([vp, vp, C.c_int, i64, i64, f32, u64, vp, vp, i64, vp, vp, vp, S], C.c_int),
+    "dph_branch_bwd_f32": ([vp, vp, C.c_int, i64, i64, f32, u64, vp, vp, i64, vp, vp, vp, vp, i64, S], C.c_int),
     "dph_conv_weight_pack": ([vp, vp, i64, i64, i64, i64, i64, S], C.c_int),
     "dph_conv_weight_unpack_grad": ([vp, vp, i64, i64, i64, i64, C.c_int, S], C.c_int),
     "dph_add_bf16": ([vp, vp, vp, i64, S], C.c_int),
-    "dph_branch_bwd": ([vp, vp, i64, i64, f32, u64, vp, vp, i64, vp, vp, vp, S], C.c_int),
+    "dph_branch_bwd": ([vp, vp, i64, i64, f32, u64, vp, vp, i64, vp, vp, vp, vp, i64, S], C.c_int),
     "dph_distill_loss_fwd": ([vp, vp, i64, i64, i64, i64, f32, f32, f32, C.c_int, vp, vp, vp, S], C.c_int),
     "dph_distill_loss_bwd": ([vp, vp, vp, vp, i64, i64, i64, i64, f32, f32, f32, C.c_int, vp, S], C.c_int),
     "dph_distill_loss_fwd_ex": ([vp, vp, C.c_uint32, i64, i64, i64, i64, f32, f32, f32, C.c_int, vp, vp, vp, S],
@@ -158,8 +166,9 @@ _lib = None
 # include/dphubert_hip.h layout (3: dph_adamw_step_dev, dph_set_rng_epoch; 4: dph_event_*; 5: LN bwd / colsum
 # workspaces; 12: dph_hc_bank_fwd / dph_hc_bank_bwd; 15: dph_gemm_mn_plan; 16: DphGemmArgs.dyn_ext, dph_ffn_compact + gathers / scatters;
 # 19: DPH_GEMM_RESID_F32, dph_layernorm_fwd_x32 / _bwd_res32, dph_branch_bwd_f32, dph_distill_loss_*_ex: the fp32
-# pre-norm residual stream)
-ABI_VERSION = 19
+# pre-norm residual stream; 20: deterministic mode -- dph_set_deterministic / dph_get_deterministic and the workspaces
+# of the fixed-order reductions: attention prep / relpos backward, WavLM gate, conv0, GELU-mask and branch backward)
+ABI_VERSION = 20
 
 
 class DphError(RuntimeError):
@@ -197,6 +206,17 @@ def lib():
 
 def exported_symbols():
     return ["dph_last_error", "dph_gemm_variant"] + list(_SIGS)
+
+
+def set_deterministic(on: bool = True) -> None:
+    """Process-wide deterministic mode of the kernel library (include/dphubert_hip.h): fixed-order cross-block
+    reductions instead of float atomics, so repeated runs of a step (eager or replayed) are bitwise identical.
+    Set it before capturing a HIP graph (a captured graph keeps the kernels it recorded)."""
+    check(lib().dph_set_deterministic(1 if on else 0), "dph_set_deterministic")
+
+
+def deterministic() -> bool:
+    return bool(lib().dph_get_deterministic())
 
 
 def check(rc: int, what: str = ""):

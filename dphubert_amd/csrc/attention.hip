@@ -83,6 +83,9 @@ struct RelBias {
   const float* gate;   // [B][H][T]
   float* dgate;        // [B][H][T]
   float* dtab;         // [H][2T-1], accumulated
+  // deterministic mode: per-wave LDS histograms and each dQ block's diagonal sums as one row of this slab
+  // [B][H][query blocks][T + RB - 1], added into dtab in a fixed order by relpos_dtab_reduce (NULL: float atomics)
+  float* dtab_part;
 };
 
 // clamped diagonal index: rows / keys past T (masked to 0 probability) read a valid entry
@@ -849,7 +852,8 @@ __global__ void __launch_bounds__(256) attn_bwd_prep_kernel(const bf16_t* __rest
                                                             const float* __restrict__ ou,
                                                             const float* __restrict__ head_mask,
                                                             float* __restrict__ Dv, float* __restrict__ dhm,
-                                                            int64_t B, int64_t T, int64_t H) {
+                                                            int64_t B, int64_t T, int64_t H,
+                                                            float* __restrict__ part) {
   __shared__ float red[4];
   const int64_t h = blockIdx.y;
   const int64_t bt = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -882,7 +886,12 @@ __global__ void __launch_bounds__(256) attn_bwd_prep_kernel(const bf16_t* __rest
   float s = wave_sum(rd);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
-  if (threadIdx.x == 0) atomicAdd(dhm + h, red[0] + red[1] + red[2] + red[3]);
+  if (threadIdx.x == 0) {
+    const float t = red[0] + red[1] + red[2] + red[3];
+    // deterministic mode: slab [row block][H], summed in row-block order after the launch
+    if (part) part[(int64_t)blockIdx.x * H + h] = t;
+    else atomicAdd(dhm + h, t);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1184,8 +1193,12 @@ __device__ __forceinline__ void attn_bwd_dq_body(const bf16_t* __restrict__ qkv,
 #pragma unroll
     for (int d = 0; d < 4; ++d) dq[u][d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   }
-  float* hist = dyn;
-  float* tw = dyn + (T32 + RB - 1);
+  // deterministic mode: one histogram per wave (a wave's LDS adds run in program order, its lanes' addresses in
+  // one add are distinct), summed in wave order at the end
+  const int HW = T32 + RB - 1;
+  const bool det_h = BIAS && rb.dtab_part != nullptr;
+  float* hist = dyn + (det_h ? wave * HW : 0);
+  float* tw = dyn + (det_h ? 4 : 1) * HW;
   const int qb0 = bx * RB;
   const int toff = T32 - 1 - (qb0 + RB - 1);
   float gq[NG], dg[NG];
@@ -1195,7 +1208,7 @@ __device__ __forceinline__ void attn_bwd_dq_body(const bf16_t* __restrict__ qkv,
     dg[u] = 0.f;
   }
   if constexpr (BIAS) {
-    for (int i = tid; i < T32 + RB - 1; i += 256) hist[i] = 0.f;   // ordered before use by the first barrier
+    for (int i = tid; i < (det_h ? 4 : 1) * HW; i += 256) dyn[i] = 0.f;   // ordered before use by the first barrier
     stage_tab_window(tw, rb.tab + h * (2 * T - 1), toff, T32);
   }
 
@@ -1365,12 +1378,17 @@ __device__ __forceinline__ void attn_bwd_dq_body(const bf16_t* __restrict__ qkv,
       if (g == 0 && qme[u] < T) rb.dgate[(b * H + h) * T + qme[u]] = v;
     }
     __syncthreads();   // all histogram adds of the block are done
-    float* dt = rb.dtab + h * (2 * T - 1);
-    const int off = T32 - 1 - (qb0 + RB - 1);   // global diagonal index of hist[0]
-    for (int i = tid; i < T32 + RB - 1; i += 256) {
-      const int gi = i + off;
-      const float v = hist[i];
-      if (gi >= 0 && gi < 2 * T32 - 1 && v != 0.f) atomicAdd(dt + gi, v);
+    if (det_h) {
+      float* prow = rb.dtab_part + (((int64_t)b * H + h) * cdiv(T, (int64_t)RB) + bx) * HW;
+      for (int i = tid; i < HW; i += 256) prow[i] = ((dyn[i] + dyn[HW + i]) + dyn[2 * HW + i]) + dyn[3 * HW + i];
+    } else {
+      float* dt = rb.dtab + h * (2 * T - 1);
+      const int off = T32 - 1 - (qb0 + RB - 1);   // global diagonal index of hist[0]
+      for (int i = tid; i < T32 + RB - 1; i += 256) {
+        const int gi = i + off;
+        const float v = hist[i];
+        if (gi >= 0 && gi < 2 * T32 - 1 && v != 0.f) atomicAdd(dt + gi, v);
+      }
     }
   }
 #pragma unroll
@@ -1428,6 +1446,23 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_kernel(const bf16_t* __restri
                                        keep_in, (int)blockIdx.x, blockIdx.y, mode == 0 ? z - nbz : z);
 }
 
+// deterministic mode: dtab[h][gi] += the dQ blocks' diagonal sums (relpos dtab_part slab) over (b, query block) in
+// order; one thread per (h, diagonal)
+__global__ void __launch_bounds__(256) relpos_dtab_reduce(const float* __restrict__ part, int64_t B, int64_t H,
+                                                          int64_t T, float* __restrict__ dtab) {
+  const int64_t R = 2 * T - 1, HW = T + RB - 1, nqb = cdiv(T, (int64_t)RB);
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= H * R) return;
+  const int64_t h = i / R, gi = i % R;
+  float s = 0.f;
+  for (int64_t b = 0; b < B; ++b)
+    for (int64_t bx = 0; bx < nqb; ++bx) {
+      const int64_t j = gi - (T - 1 - (bx * RB + RB - 1));
+      if (j >= 0 && j < HW) s += part[((b * H + h) * nqb + bx) * HW + j];
+    }
+  dtab[i] += s;
+}
+
 }  // namespace
 }  // namespace dph
 
@@ -1471,18 +1506,20 @@ void launch_bwd_k(dim3 grid, hipStream_t stream, const void* qkv, const void* do
                   const float* Dvec, void* dqkv, const int64_t* key_len, AttnShape sh, float scale, float p,
                   uint64_t seed, RelBias rb, const void* keep) {
   const size_t tw_bytes = BIAS ? (size_t)(sh.T + RB - 1) * sizeof(float) : 0;
+  // dynamic LDS: the table window + one diagonal histogram (four, per wave, in deterministic mode)
+  const size_t dyn_bytes = (rb.dtab_part != nullptr ? 5 : 2) * tw_bytes;
   const char* e = getenv("DPH_ATTN_SPLIT");
   const int nbz = (int)grid.z;
   if (e && e[0] == '1') {
     for (int mode = 1; mode <= 2; ++mode)
-      hipLaunchKernelGGL((attn_bwd_kernel<DROP, BIAS, KEEP>), grid, dim3(256), 2 * tw_bytes, stream,
+      hipLaunchKernelGGL((attn_bwd_kernel<DROP, BIAS, KEEP>), grid, dim3(256), dyn_bytes, stream,
                          reinterpret_cast<const bf16_t*>(qkv), reinterpret_cast<const bf16_t*>(dom), hm, lse, Dvec,
                          reinterpret_cast<bf16_t*>(dqkv), key_len, sh, scale, p, seed, rb,
                          reinterpret_cast<const uint16_t*>(keep), nbz, mode);
     return;
   }
   const dim3 g2(grid.x, grid.y, 2 * grid.z);
-  hipLaunchKernelGGL((attn_bwd_kernel<DROP, BIAS, KEEP>), g2, dim3(256), 2 * tw_bytes, stream,
+  hipLaunchKernelGGL((attn_bwd_kernel<DROP, BIAS, KEEP>), g2, dim3(256), dyn_bytes, stream,
                      reinterpret_cast<const bf16_t*>(qkv), reinterpret_cast<const bf16_t*>(dom), hm, lse, Dvec,
                      reinterpret_cast<bf16_t*>(dqkv), key_len, sh, scale, p, seed, rb,
                      reinterpret_cast<const uint16_t*>(keep), nbz, 0);
@@ -1560,13 +1597,22 @@ extern "C" int dph_attention_fwd_relpos(const void* qkv, void* o_unmasked, void*
                        RelBias{rel_tab, gate, nullptr, nullptr}, keep_bits, stream);
 }
 
+extern "C" int64_t dph_attention_bwd_prep_workspace(int64_t B, int64_t T, int64_t H) {
+  return cdiv(B * T, 256) * H * 4;
+}
+
 extern "C" int dph_attention_bwd_prep(const void* do_masked, const void* o_unmasked, const float* head_mask,
-                                      float* Dvec, float* dhead_mask, int64_t B, int64_t T, int64_t H,
-                                      hipStream_t stream) {
+                                      float* Dvec, float* dhead_mask, int64_t B, int64_t T, int64_t H, float* ws,
+                                      int64_t ws_bytes, hipStream_t stream) {
   DPH_REQUIRE(do_masked && o_unmasked && Dvec && B > 0 && T > 0 && H > 0, "dph_attention_bwd_prep: bad args");
+  const bool det = dhead_mask && deterministic();
+  DPH_REQUIRE(!det || (ws && ws_bytes >= dph_attention_bwd_prep_workspace(B, T, H)),
+              "dph_attention_bwd_prep: deterministic mode needs dph_attention_bwd_prep_workspace bytes");
   dim3 grid((unsigned)cdiv(B * T, 256), (unsigned)H);
   hipLaunchKernelGGL(attn_bwd_prep_kernel, grid, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(do_masked),
-                     reinterpret_cast<const float*>(o_unmasked), head_mask, Dvec, dhead_mask, B, T, H);
+                     reinterpret_cast<const float*>(o_unmasked), head_mask, Dvec, dhead_mask, B, T, H,
+                     det ? ws : nullptr);
+  if (det) slab_reduce_cols(ws, grid.x, H, H, dhead_mask, nullptr, nullptr, stream);
   return check_launch("dph_attention_bwd_prep");
 }
 
@@ -1579,14 +1625,26 @@ extern "C" int dph_attention_bwd(const void* qkv, const void* do_masked, const f
                        RelBias{nullptr, nullptr, nullptr, nullptr}, keep_bits, stream);
 }
 
+// deterministic mode: the dQ blocks' diagonal-sum slab [B][H][ceil(T/128)][T + 127] fp32
+extern "C" int64_t dph_attention_bwd_relpos_workspace(int64_t B, int64_t T, int64_t H) {
+  return B * H * cdiv(T, (int64_t)RB) * (T + RB - 1) * 4;
+}
+
 extern "C" int dph_attention_bwd_relpos(const void* qkv, const void* do_masked, const float* head_mask,
                                         const float* lse, const float* Dvec, void* dqkv, const int64_t* key_len,
                                         const float* rel_tab, const float* gate, float* dgate, float* drel_tab,
                                         int64_t B, int64_t T, int64_t H, float scale, float dropout_p, uint64_t seed,
-                                        const void* keep_bits, hipStream_t stream) {
+                                        const void* keep_bits, float* ws, int64_t ws_bytes, hipStream_t stream) {
   DPH_REQUIRE(qkv && do_masked && lse && Dvec && dqkv && rel_tab && gate && dgate && drel_tab && B > 0 && T > 0 &&
                   T <= 3584 && H > 0,
               "dph_attention_bwd_relpos: bad args (T <= 3584: two [T+127] fp32 LDS windows + 34 KB of tiles)");
-  return attention_bwd(qkv, do_masked, head_mask, lse, Dvec, dqkv, key_len, B, T, H, scale, dropout_p, seed,
-                       RelBias{rel_tab, gate, dgate, drel_tab}, keep_bits, stream);
+  const bool det = deterministic();
+  DPH_REQUIRE(!det || (ws && ws_bytes >= dph_attention_bwd_relpos_workspace(B, T, H)),
+              "dph_attention_bwd_relpos: deterministic mode needs dph_attention_bwd_relpos_workspace bytes");
+  const int rc = attention_bwd(qkv, do_masked, head_mask, lse, Dvec, dqkv, key_len, B, T, H, scale, dropout_p, seed,
+                               RelBias{rel_tab, gate, dgate, drel_tab, det ? ws : nullptr}, keep_bits, stream);
+  if (rc || !det) return rc;
+  hipLaunchKernelGGL(relpos_dtab_reduce, dim3((unsigned)cdiv(H * (2 * T - 1), 256)), dim3(256), 0, stream, ws, B, H, T,
+                     drel_tab);
+  return check_launch("dph_attention_bwd_relpos dtab reduce");
 }

@@ -24,6 +24,14 @@ namespace dph {
 
 void set_error(const char* fmt, ...);
 int check_launch(const char* what);
+// deterministic mode (runtime.hip, dph_set_deterministic): fixed-order cross-block reductions instead of float atomics
+bool deterministic();
+// norm.hip: o_q[c] += sum_r ws[r][q * seg + c] over the column segments q of a [nrows][ncols] fp32 partial slab (NULL
+// outputs skipped); fixed order in deterministic mode, row groups + one atomic per column per group otherwise
+void slab_reduce_cols(const float* ws, int64_t nrows, int64_t ncols, int64_t seg, float* o0, float* o1, float* o2,
+                      hipStream_t stream);
+// norm.hip: out[0] += sum of n partials, in order (one wave)
+void sdot_reduce(const float* part, int64_t n, float* out, hipStream_t stream);
 
 #define DPH_REQUIRE(cond, ...)              \
   do {                                      \
@@ -214,6 +222,39 @@ __device__ __forceinline__ float sum_partials_wave(const float* __restrict__ par
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
   return s;
+}
+
+// Deterministic-mode column reduction (dph_set_deterministic): a block of 32 x DET_PH threads sums 32 columns of a
+// [nrows][ld] fp32 partial slab over ALL its rows in a fixed order -- thread (column tx, phase ph) takes rows ph,
+// ph + DET_PH, ... into four chains (added in chain order), the DET_PH phase totals are added in phase order -- so the
+// result does not depend on scheduling.  `p` points at row 0 of the thread's column (NULL: 0).  Every thread of the
+// block must call it (it synchronises); the total is returned to the threads with ph == 0.
+constexpr int DET_PH = 32;
+__device__ __forceinline__ float det_column_total(const float* __restrict__ p, int64_t nrows, int64_t ld,
+                                                  float (*red)[33]) {
+  const int tx = threadIdx.x & 31, ph = threadIdx.x >> 5;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (p) {
+    int64_t r = ph;
+    for (; r + 3 * DET_PH < nrows; r += 4 * DET_PH) {
+      s0 += p[r * ld];
+      s1 += p[(r + DET_PH) * ld];
+      s2 += p[(r + 2 * DET_PH) * ld];
+      s3 += p[(r + 3 * DET_PH) * ld];
+    }
+    if (r < nrows) s0 += p[r * ld];
+    if (r + DET_PH < nrows) s1 += p[(r + DET_PH) * ld];
+    if (r + 2 * DET_PH < nrows) s2 += p[(r + 2 * DET_PH) * ld];
+  }
+  red[ph][tx] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  float t = 0.f;
+  if (ph == 0) {
+#pragma unroll 8
+    for (int i = 0; i < DET_PH; ++i) t += red[i][tx];
+  }
+  __syncthreads();
+  return t;
 }
 }  // namespace
 

@@ -21,7 +21,7 @@ __global__ void __launch_bounds__(256) gelu_mask_bwd_kernel(const bf16_t* __rest
                                                             const bf16_t* __restrict__ z_pre,
                                                             const float* __restrict__ mask, bf16_t* __restrict__ out,
                                                             float* __restrict__ dmask, int64_t rows,
-                                                            int64_t rows_per_block) {
+                                                            int64_t rows_per_block, float* __restrict__ part) {
   __shared__ float red[4][512];
   const int tx = threadIdx.x & 63;
   const int ty = threadIdx.x >> 6;
@@ -83,7 +83,11 @@ __global__ void __launch_bounds__(256) gelu_mask_bwd_kernel(const bf16_t* __rest
   __syncthreads();
   for (int c = threadIdx.x; c < 512; c += 256) {
     const int64_t col = (int64_t)blockIdx.x * 512 + c;
-    if (col < C) atomicAdd(dmask + col, red[0][c] + red[1][c] + red[2][c] + red[3][c]);
+    if (col >= C) continue;
+    const float t = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+    // deterministic mode: the block's partial row of the [grid.y][C] slab (summed in order after the launch)
+    if (part) part[(int64_t)blockIdx.y * C + col] = t;
+    else atomicAdd(dmask + col, t);
   }
 }
 
@@ -168,7 +172,8 @@ __global__ void __launch_bounds__(256) branch_bwd_kernel(const DyT* __restrict__
                                                          const float* __restrict__ smask,
                                                          const int64_t* __restrict__ row_len, int64_t len_rows,
                                                          float* __restrict__ colsum, const bf16_t* __restrict__ pre,
-                                                         float* __restrict__ sdot, int64_t rows_per_block) {
+                                                         float* __restrict__ sdot, int64_t rows_per_block,
+                                                         float* __restrict__ part) {
   seed = epoch_seed(seed);   // per-step RNG epoch (graph replays)
   __shared__ float red[4][512];
   __shared__ float sred[4];
@@ -222,45 +227,90 @@ __global__ void __launch_bounds__(256) branch_bwd_kernel(const DyT* __restrict__
   sd = wave_sum(sd);
   if (tx == 0) sred[ty] = sd;
   __syncthreads();
+  // deterministic mode (part != NULL): the block's column partials as row blockIdx.y of a [grid.y][cols] slab and its
+  // sdot partial after the slab (index y * grid.x + x), both summed in order after the launch
   if (colsum) {
     for (int c = threadIdx.x; c < 512; c += 256) {
       const int64_t col = (int64_t)blockIdx.x * 512 + c;
-      if (col < cols) atomicAdd(colsum + col, red[0][c] + red[1][c] + red[2][c] + red[3][c]);
+      if (col >= cols) continue;
+      const float t = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+      if (part) part[(int64_t)blockIdx.y * cols + col] = t;
+      else atomicAdd(colsum + col, t);
     }
   }
-  if (sdot && threadIdx.x == 0) atomicAdd(sdot, sred[0] + sred[1] + sred[2] + sred[3]);
+  if (sdot && threadIdx.x == 0) {
+    const float t = sred[0] + sred[1] + sred[2] + sred[3];
+    if (part) part[(int64_t)gridDim.y * cols + (int64_t)blockIdx.y * gridDim.x + blockIdx.x] = t;
+    else atomicAdd(sdot, t);
+  }
 }
 
 int64_t rows_per_block_for(int64_t rows) { return std::max<int64_t>(16, cdiv(cdiv(rows, 4096), 4) * 4); }
+// deterministic mode: at most ~512 row blocks (the fixed-order slab reduction then sums <= 512 rows per column)
+int64_t rows_per_block_det(int64_t rows) {
+  return std::max<int64_t>(rows_per_block_for(rows), cdiv(cdiv(rows, 512), 4) * 4);
+}
 
 }  // namespace
 }  // namespace dph
 
 using namespace dph;
 
+// Workspace (bytes) of the row-block column reductions below (dph_col2im_gelu_bwd / dph_gelu_mask_bwd over rows x C,
+// dph_branch_bwd(_f32) over rows x cols): the per-row-block partial slab + sdot partials of deterministic mode
+extern "C" int64_t dph_rowblock_workspace(int64_t rows, int64_t cols) {
+  if (rows <= 0 || cols <= 0) return 0;
+  const int64_t nrb = cdiv(rows, rows_per_block_det(rows));
+  return (nrb * cols + nrb * cdiv(cols, 512)) * 4;
+}
+
+namespace {
+// deterministic mode needs the workspace whenever a column sum / sdot is requested
+int rowblock_plan(int64_t rows, int64_t cols, bool sums, float* ws, int64_t ws_bytes, int64_t& rpb, float*& part,
+                  const char* who) {
+  part = nullptr;
+  rpb = rows_per_block_for(rows);
+  if (sums && deterministic()) {
+    DPH_REQUIRE(ws && ws_bytes >= dph_rowblock_workspace(rows, cols),
+                "%s: deterministic mode needs dph_rowblock_workspace(rows, cols) bytes of workspace", who);
+    rpb = rows_per_block_det(rows);
+    part = ws;
+  }
+  return DPH_OK;
+}
+}  // namespace
+
 extern "C" int dph_col2im_gelu_bwd(const void* dcols, int64_t B, int64_t Lout, int64_t Lin, int64_t C, int64_t k,
-                                   int64_t s, const void* z_pre, const float* mask, void* out, float* dmask,
-                                   hipStream_t stream) {
+                                   int64_t s, const void* z_pre, const float* mask, void* out, float* dmask, float* ws,
+                                   int64_t ws_bytes, hipStream_t stream) {
   DPH_REQUIRE(dcols && out && B > 0 && Lout > 0 && Lin >= Lout && C > 0 && k > 0 && s > 0,
               "dph_col2im_gelu_bwd: bad args");
   DPH_REQUIRE(!dmask || z_pre, "dph_col2im_gelu_bwd: dmask needs z_pre");
   const int64_t rows = B * Lin;
-  const int64_t rpb = rows_per_block_for(rows);
-  dim3 grid((unsigned)cdiv(C, 512), (unsigned)cdiv(rows, rpb));
+  int64_t rpb;
+  float* part;
+  if (int rc = rowblock_plan(rows, C, dmask != nullptr, ws, ws_bytes, rpb, part, "dph_col2im_gelu_bwd")) return rc;
+  const int64_t nrb = cdiv(rows, rpb);
+  dim3 grid((unsigned)cdiv(C, 512), (unsigned)nrb);
   hipLaunchKernelGGL(gelu_mask_bwd_kernel<true>, grid, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(dcols),
                      Lout, Lin, C, (int)k, (int)s, reinterpret_cast<const bf16_t*>(z_pre), mask,
-                     reinterpret_cast<bf16_t*>(out), dmask, rows, rpb);
+                     reinterpret_cast<bf16_t*>(out), dmask, rows, rpb, part);
+  if (part) slab_reduce_cols(part, nrb, C, C, dmask, nullptr, nullptr, stream);
   return check_launch("dph_col2im_gelu_bwd");
 }
 
 extern "C" int dph_gelu_mask_bwd(const void* dy, const void* z_pre, const float* mask, void* out, float* dmask,
-                                 int64_t rows, int64_t C, hipStream_t stream) {
+                                 int64_t rows, int64_t C, float* ws, int64_t ws_bytes, hipStream_t stream) {
   DPH_REQUIRE(dy && z_pre && out && rows > 0 && C > 0, "dph_gelu_mask_bwd: bad args");
-  const int64_t rpb = rows_per_block_for(rows);
-  dim3 grid((unsigned)cdiv(C, 512), (unsigned)cdiv(rows, rpb));
+  int64_t rpb;
+  float* part;
+  if (int rc = rowblock_plan(rows, C, dmask != nullptr, ws, ws_bytes, rpb, part, "dph_gelu_mask_bwd")) return rc;
+  const int64_t nrb = cdiv(rows, rpb);
+  dim3 grid((unsigned)cdiv(C, 512), (unsigned)nrb);
   hipLaunchKernelGGL(gelu_mask_bwd_kernel<false>, grid, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(dy),
                      (int64_t)1, (int64_t)1, C, 1, 1, reinterpret_cast<const bf16_t*>(z_pre), mask,
-                     reinterpret_cast<bf16_t*>(out), dmask, rows, rpb);
+                     reinterpret_cast<bf16_t*>(out), dmask, rows, rpb, part);
+  if (part) slab_reduce_cols(part, nrb, C, C, dmask, nullptr, nullptr, stream);
   return check_launch("dph_gelu_mask_bwd");
 }
 
@@ -518,33 +568,44 @@ extern "C" int dph_add_bf16(const void* a, const void* b, void* out, int64_t n, 
 
 extern "C" int dph_branch_bwd(const void* dy, void* out, int64_t rows, int64_t cols, float p, uint64_t seed,
                               const float* smask, const int64_t* row_len, int64_t len_rows, float* colsum,
-                              const void* pre, float* sdot, hipStream_t stream) {
+                              const void* pre, float* sdot, float* ws, int64_t ws_bytes, hipStream_t stream) {
   DPH_REQUIRE(dy && out && rows > 0 && cols > 0, "dph_branch_bwd: bad args");
   DPH_REQUIRE(!row_len || len_rows > 0, "dph_branch_bwd: row_len needs len_rows");
   DPH_REQUIRE(!sdot || pre, "dph_branch_bwd: sdot needs pre");
-  const int64_t rpb = rows_per_block_for(rows);
-  dim3 grid((unsigned)cdiv(cols, 512), (unsigned)cdiv(rows, rpb));
+  int64_t rpb;
+  float* part;
+  if (int rc = rowblock_plan(rows, cols, colsum || sdot, ws, ws_bytes, rpb, part, "dph_branch_bwd")) return rc;
+  const int64_t nrb = cdiv(rows, rpb);
+  dim3 grid((unsigned)cdiv(cols, 512), (unsigned)nrb);
   hipLaunchKernelGGL((branch_bwd_kernel<bf16_t, bf16_t>), grid, dim3(256), 0, stream,
                      reinterpret_cast<const bf16_t*>(dy), reinterpret_cast<bf16_t*>(out), rows, cols, p, seed, smask,
-                     row_len, len_rows, colsum, reinterpret_cast<const bf16_t*>(pre), sdot, rpb);
+                     row_len, len_rows, colsum, reinterpret_cast<const bf16_t*>(pre), sdot, rpb, part);
+  if (part && colsum) slab_reduce_cols(part, nrb, cols, cols, colsum, nullptr, nullptr, stream);
+  if (part && sdot) sdot_reduce(part + nrb * cols, nrb * (int64_t)grid.x, sdot, stream);
   return check_launch("dph_branch_bwd");
 }
 
 extern "C" int dph_branch_bwd_f32(const float* dy, void* out, int out_f32, int64_t rows, int64_t cols, float p,
                                   uint64_t seed, const float* smask, const int64_t* row_len, int64_t len_rows,
-                                  float* colsum, const void* pre, float* sdot, hipStream_t stream) {
+                                  float* colsum, const void* pre, float* sdot, float* ws, int64_t ws_bytes,
+                                  hipStream_t stream) {
   DPH_REQUIRE(dy && out && rows > 0 && cols > 0, "dph_branch_bwd_f32: bad args");
   DPH_REQUIRE(!row_len || len_rows > 0, "dph_branch_bwd_f32: row_len needs len_rows");
   DPH_REQUIRE(!sdot || pre, "dph_branch_bwd_f32: sdot needs pre");
-  const int64_t rpb = rows_per_block_for(rows);
-  dim3 grid((unsigned)cdiv(cols, 512), (unsigned)cdiv(rows, rpb));
+  int64_t rpb;
+  float* part;
+  if (int rc = rowblock_plan(rows, cols, colsum || sdot, ws, ws_bytes, rpb, part, "dph_branch_bwd_f32")) return rc;
+  const int64_t nrb = cdiv(rows, rpb);
+  dim3 grid((unsigned)cdiv(cols, 512), (unsigned)nrb);
   if (out_f32)
     hipLaunchKernelGGL((branch_bwd_kernel<float, float>), grid, dim3(256), 0, stream, dy,
                        reinterpret_cast<float*>(out), rows, cols, p, seed, smask, row_len, len_rows, colsum,
-                       reinterpret_cast<const bf16_t*>(pre), sdot, rpb);
+                       reinterpret_cast<const bf16_t*>(pre), sdot, rpb, part);
   else
     hipLaunchKernelGGL((branch_bwd_kernel<float, bf16_t>), grid, dim3(256), 0, stream, dy,
                        reinterpret_cast<bf16_t*>(out), rows, cols, p, seed, smask, row_len, len_rows, colsum,
-                       reinterpret_cast<const bf16_t*>(pre), sdot, rpb);
+                       reinterpret_cast<const bf16_t*>(pre), sdot, rpb, part);
+  if (part && colsum) slab_reduce_cols(part, nrb, cols, cols, colsum, nullptr, nullptr, stream);
+  if (part && sdot) sdot_reduce(part + nrb * cols, nrb * (int64_t)grid.x, sdot, stream);
   return check_launch("dph_branch_bwd_f32");
 }

@@ -199,7 +199,7 @@ __global__ void __launch_bounds__(256) conv0_gn_bwd_kernel(const float* __restri
                                                            const float* __restrict__ mean,
                                                            const float* __restrict__ rstd,
                                                            const bf16_t* __restrict__ dy, float* __restrict__ sums,
-                                                           int rows) {
+                                                           int rows, float* __restrict__ part) {
   __shared__ float xs[BWD_ROWS * S0 + K0];
   __shared__ float red[256 * CPT];
   const int64_t b = blockIdx.y;
@@ -338,7 +338,23 @@ __global__ void __launch_bounds__(256) conv0_gn_bwd_kernel(const float* __restri
         // acc q: 0-9 sum dg' x_j, 10 sum dg', 11 sum dg' xh, 14 sum dy GELU(g) (12, 13 unused) -> the 15 sums
         // conv0_bwd_finalize reads: P_j = ga mk (0-9), A = ga mk S1, Bv = ga mk T2, dgamma = mk T2,
         // dbeta = mk S1, dmask
-        if (c < p.C && q != 12 && q != 13) {
+        if (c < p.C && q != 12 && q != 13 && part) {
+          // deterministic mode: this block's 15 sums as its own slab entry, added in time-block order by
+          // conv0_part_reduce
+          const float gm = ga[i] * mk[i];
+          float* o = part + ((b * gridDim.x + blockIdx.x) * p.C + c) * NQ;
+          if (q < 10) {
+            o[q] = gm * s;
+          } else if (q == 10) {
+            o[10] = gm * s;
+            o[13] = mk[i] * s;
+          } else if (q == 11) {
+            o[11] = gm * s;
+            o[12] = mk[i] * s;
+          } else {
+            o[14] = s;
+          }
+        } else if (c < p.C && q != 12 && q != 13) {
           const float gm = ga[i] * mk[i];
           float* o = sums + (b * p.C + c) * NQ;
           if (q < 10) {
@@ -365,7 +381,7 @@ __global__ void __launch_bounds__(256) conv0_gn_bwd_kernel(const float* __restri
 template <int CPT>
 __global__ void __launch_bounds__(256) conv0_plain_bwd_kernel(const float* __restrict__ wave, Conv0 p,
                                                               const bf16_t* __restrict__ dz, float* __restrict__ dw,
-                                                              float* __restrict__ dbias) {
+                                                              float* __restrict__ dbias, float* __restrict__ part) {
   constexpr int NA = K0 + 1;
   __shared__ float xs[BWD_ROWS * S0 + K0];
   __shared__ float red[256 * CPT];
@@ -413,7 +429,10 @@ __global__ void __launch_bounds__(256) conv0_plain_bwd_kernel(const float* __res
         float sm = 0.f;
         for (int r = 0; r < L.rpp; ++r) sm += red[(r * L.tpr + (tid % L.tpr)) * CPT + i];
         const int64_t c = c0 + i;
-        if (c < p.C) {
+        if (c < p.C && part) {
+          // deterministic mode: this block's entry of the [b][time block][C][11] slab (conv0_plain_part_reduce)
+          part[((b * gridDim.x + blockIdx.x) * p.C + c) * NA + q] = sm;
+        } else if (c < p.C) {
           if (q < K0) atomicAdd(dw + c * K0 + q, sm);
           else if (dbias) atomicAdd(dbias + c, sm);
         }
@@ -505,6 +524,48 @@ __global__ void __launch_bounds__(256) conv0_gram_reduce(const double* __restric
     mean[b * p.C + c] = (float)m;
     rstd[b * p.C + c] = (float)(1.0 / sqrt(var + (double)eps));
   }
+}
+
+// deterministic mode: sums[b][c][q] = the time blocks' partials of utterance b added in block order (four chains)
+__global__ void __launch_bounds__(256) conv0_part_reduce(const float* __restrict__ part, int64_t nblk, int64_t per_b,
+                                                         int64_t B, float* __restrict__ sums) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= B * per_b) return;
+  const int64_t b = i / per_b, j = i % per_b;
+  const float* p = part + b * nblk * per_b + j;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int64_t k = 0;
+  for (; k + 3 < nblk; k += 4) {
+    s0 += p[k * per_b];
+    s1 += p[(k + 1) * per_b];
+    s2 += p[(k + 2) * per_b];
+    s3 += p[(k + 3) * per_b];
+  }
+  for (; k < nblk; ++k) s0 += p[k * per_b];
+  sums[i] = (s0 + s1) + (s2 + s3);
+}
+
+// deterministic mode of the plain conv0 backward: dw[c][j] / dbias[c] += the [b][time block][C][11] partials summed
+// over (b, time block) in order, one thread per (c, q)
+__global__ void __launch_bounds__(256) conv0_plain_part_reduce(const float* __restrict__ part, int64_t nbt, int64_t C,
+                                                               float* __restrict__ dw, float* __restrict__ dbias) {
+  constexpr int NA = K0 + 1;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= C * NA) return;
+  const int64_t c = i / NA, q = i % NA;
+  const float* p = part + i;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int64_t k = 0;
+  for (; k + 3 < nbt; k += 4) {
+    s0 += p[k * C * NA];
+    s1 += p[(k + 1) * C * NA];
+    s2 += p[(k + 2) * C * NA];
+    s3 += p[(k + 3) * C * NA];
+  }
+  for (; k < nbt; ++k) s0 += p[k * C * NA];
+  const float t = (s0 + s1) + (s2 + s3);
+  if (q < K0) dw[c * K0 + q] += t;
+  else if (dbias) dbias[c] += t;
 }
 
 // one thread per channel: combine the per-(b,c) sums into dw[c][j], dgamma, dbeta, dmask (accumulate)
@@ -681,8 +742,16 @@ extern "C" int dph_conv0_fwd(const float* wave, int64_t B, int64_t S, const floa
   return check_launch("dph_conv0_fwd");
 }
 
+// workspace (bytes) of dph_conv0_bwd: the per-(utterance, time block) partial slab of deterministic mode
+extern "C" int64_t dph_conv0_bwd_workspace(int64_t B, int64_t S, int64_t C) {
+  if (B <= 0 || S < K0 || C <= 0) return 0;
+  const int64_t L0 = (S - K0) / S0 + 1;
+  return B * cdiv(L0, (int64_t)BWD_ROWS) * C * (K0 + 1) * 4;
+}
+
 extern "C" int dph_conv0_bwd(const float* wave, int64_t B, int64_t S, int64_t C, int64_t k0, int64_t s0,
-                             const void* dz, float* dw, float* dbias, hipStream_t stream) {
+                             const void* dz, float* dw, float* dbias, float* ws, int64_t ws_bytes,
+                             hipStream_t stream) {
   DPH_REQUIRE(wave && dz && dw, "dph_conv0_bwd: null pointer");
   if (k0 != K0 || s0 != S0) {
     set_error("dph_conv0_bwd: conv0 kernel/stride (%lld,%lld) unsupported (only (10,5))", (long long)k0,
@@ -690,14 +759,27 @@ extern "C" int dph_conv0_bwd(const float* wave, int64_t B, int64_t S, int64_t C,
     return DPH_EUNSUPPORTED;
   }
   DPH_REQUIRE(S >= K0 && C <= 1024, "dph_conv0_bwd: unsupported (C > 1024)");
+  const bool det = deterministic();
+  DPH_REQUIRE(!det || (ws && ws_bytes >= dph_conv0_bwd_workspace(B, S, C)),
+              "dph_conv0_bwd: deterministic mode needs dph_conv0_bwd_workspace(B, S, C) bytes of workspace");
   Conv0 p = make_conv0(B, S, C);
-  hipLaunchKernelGGL(conv0_plain_bwd_kernel<4>, dim3((unsigned)cdiv(p.L0, BWD_ROWS), (unsigned)B), dim3(256), 0,
-                     stream, wave, p, reinterpret_cast<const bf16_t*>(dz), dw, dbias);
+  const int64_t nblk = cdiv(p.L0, (int64_t)BWD_ROWS);
+  hipLaunchKernelGGL(conv0_plain_bwd_kernel<4>, dim3((unsigned)nblk, (unsigned)B), dim3(256), 0,
+                     stream, wave, p, reinterpret_cast<const bf16_t*>(dz), dw, dbias, det ? ws : nullptr);
+  if (det)
+    hipLaunchKernelGGL(conv0_plain_part_reduce, dim3((unsigned)cdiv(C * (K0 + 1), 256)), dim3(256), 0, stream, ws,
+                       B * nblk, C, dw, dbias);
   return check_launch("dph_conv0_bwd");
 }
 
-extern "C" int64_t dph_conv0_gn_bwd_workspace(int64_t B, int64_t C) {
-  return cdiv(B * C * NQ * 4, 64) * 64 + B * NG * 8 + B * GRAM_CHUNKS * NG * 8;
+// (the smallest GroupNorm-backward time block is BWD_ROWS / 2 rows: DPH_C0B_VARIANT=3)
+static int64_t conv0_gn_part_floats(int64_t B, int64_t S, int64_t C) {
+  const int64_t L0 = S >= K0 ? (S - K0) / S0 + 1 : 0;
+  return B * cdiv(L0, (int64_t)(BWD_ROWS / 2)) * C * NQ;
+}
+
+extern "C" int64_t dph_conv0_gn_bwd_workspace(int64_t B, int64_t S, int64_t C) {
+  return cdiv(B * C * NQ * 4, 64) * 64 + B * NG * 8 + B * GRAM_CHUNKS * NG * 8 + conv0_gn_part_floats(B, S, C) * 4;
 }
 
 extern "C" int dph_conv0_gn_bwd(const float* wave, int64_t B, int64_t S, const float* w, int64_t C, int64_t k0,
@@ -711,14 +793,17 @@ extern "C" int dph_conv0_gn_bwd(const float* wave, int64_t B, int64_t S, const f
     return DPH_EUNSUPPORTED;
   }
   DPH_REQUIRE(S >= K0 && C <= 1024, "dph_conv0_gn_bwd: unsupported (C > 1024)");   // 256 threads x 4 channels
-  DPH_REQUIRE(ws_bytes >= dph_conv0_gn_bwd_workspace(B, C), "dph_conv0_gn_bwd: workspace too small (%lld < %lld)",
-              (long long)ws_bytes, (long long)dph_conv0_gn_bwd_workspace(B, C));
+  DPH_REQUIRE(ws_bytes >= dph_conv0_gn_bwd_workspace(B, S, C), "dph_conv0_gn_bwd: workspace too small (%lld < %lld)",
+              (long long)ws_bytes, (long long)dph_conv0_gn_bwd_workspace(B, S, C));
   Conv0 p = make_conv0(B, S, C);
   float* sums = ws;
   const int64_t sums_bytes = cdiv(B * C * NQ * 4, 64) * 64;
   double* gram = reinterpret_cast<double*>(reinterpret_cast<char*>(ws) + sums_bytes);
   double* gpart = gram + B * NG;
-  zero_async(ws, sums_bytes, stream);
+  // deterministic mode: per-(utterance, time block) partials after the Gram partials, reduced in order into sums
+  const bool det = deterministic();
+  float* part = det ? reinterpret_cast<float*>(gpart + B * GRAM_CHUNKS * NG) : nullptr;
+  if (!det) zero_async(ws, sums_bytes, stream);
   hipLaunchKernelGGL(conv0_gram_part_kernel, dim3(GRAM_CHUNKS, (unsigned)B), dim3(256), 0, stream, wave, p, gpart);
   hipLaunchKernelGGL(conv0_gram_reduce, dim3((unsigned)B), dim3(256), 0, stream, gpart, w, p, gram, (float*)nullptr,
                      (float*)nullptr, 0.f);
@@ -734,19 +819,22 @@ extern "C" int dph_conv0_gn_bwd(const float* wave, int64_t B, int64_t S, const f
   const bool vec = C % 4 == 0;
   if (var == 1 && C <= 512 && vec)
     hipLaunchKernelGGL((conv0_gn_bwd_kernel<2, 4, true>), grid, dim3(256), 0, stream, wave, w, p, gamma, beta, mask, mean,
-                       rstd, dyb, sums, rows);
+                       rstd, dyb, sums, rows, part);
   else if (var == 1 && C <= 512)
     hipLaunchKernelGGL((conv0_gn_bwd_kernel<2, 4, false>), grid, dim3(256), 0, stream, wave, w, p, gamma, beta, mask, mean,
-                       rstd, dyb, sums, rows);
+                       rstd, dyb, sums, rows, part);
   else if (var == 2)
     hipLaunchKernelGGL((conv0_gn_bwd_kernel<4, 1, false>), grid, dim3(256), 0, stream, wave, w, p, gamma, beta, mask, mean,
-                       rstd, dyb, sums, rows);
+                       rstd, dyb, sums, rows, part);
   else if (vec)
     hipLaunchKernelGGL((conv0_gn_bwd_kernel<4, 4, true>), grid, dim3(256), 0, stream, wave, w, p, gamma, beta, mask,
-                       mean, rstd, dyb, sums, rows);
+                       mean, rstd, dyb, sums, rows, part);
   else
     hipLaunchKernelGGL((conv0_gn_bwd_kernel<4, 4, false>), grid, dim3(256), 0, stream, wave, w, p, gamma, beta, mask,
-                       mean, rstd, dyb, sums, rows);
+                       mean, rstd, dyb, sums, rows, part);
+  if (det)
+    hipLaunchKernelGGL(conv0_part_reduce, dim3((unsigned)cdiv(B * C * NQ, 256)), dim3(256), 0, stream, part,
+                       (int64_t)grid.x, C * NQ, B, sums);
   hipLaunchKernelGGL(conv0_bwd_finalize, dim3((unsigned)cdiv(C, 64)), dim3(64), 0, stream, sums, gram, w, mean, rstd,
                      p, dw, dgamma, dbeta, dmask);
   return check_launch("dph_conv0_gn_bwd");

@@ -38,6 +38,9 @@ namespace dph {
 namespace {
 constexpr int BM = 128;
 constexpr int BN = 128;
+// internal DphGemmArgs.flags bit set by dph_gemm: column sums go to a workspace slab of per-tile / per-wave partial
+// rows (see the epilogues) instead of float atomics
+constexpr int64_t GEMM_COLSUM_SLAB = (int64_t)1 << 20;
 constexpr int BK = 64;
 constexpr int NTHREADS = 256;                 // 4 waves: 2 (M) x 2 (N), each a 64x64 output tile
 constexpr int CHUNKS = (128 * BK / 8) / NTHREADS;   // 16-B chunks per thread per operand tile
@@ -705,8 +708,17 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(const DphGemmArgs a, int64_
           so += red[(w * 2 + 0) * 128 + tid];
           sx += red[(w * 2 + 1) * 128 + tid];
         }
-        if (a.colsum_out && n < csn) atomicAdd(a.colsum_out + voff + n, so);
-        if (a.colsum_aux && n < csn) atomicAdd(a.colsum_aux + voff + n, sx);
+        if (a.flags & GEMM_COLSUM_SLAB) {
+          // one slab row per 128-row M tile (dph_gemm sums the slab in a fixed order: deterministic mode)
+          float* wo = reinterpret_cast<float*>(a.workspace) + (m0 / BM) * a.N;
+          if (n < csn) {
+            wo[n] = so;
+            wo[cdiv(a.M, (int64_t)BM) * a.N + n] = sx;
+          }
+        } else {
+          if (a.colsum_out && n < csn) atomicAdd(a.colsum_out + voff + n, so);
+          if (a.colsum_aux && n < csn) atomicAdd(a.colsum_aux + voff + n, sx);
+        }
       }
     }
   }
@@ -758,7 +770,7 @@ constexpr int ACT_GELU_DGKPRE = 16;
 // workspace slab [2][cdiv(M, WTM)][N] (summed by colsum_slab_reduce_kernel) instead of one same-address float
 // atomic per column per wave (126 -- 2000 adders per address on the FFN / conv input-gradient GEMMs: the
 // atomics, not the MFMAs or the GELU', set those launches' time)
-constexpr int64_t GEMM_COLSUM_SLAB = (int64_t)1 << 20;
+// (GEMM_COLSUM_SLAB: defined at the top of the file)
 // internal flags bit set by dph_gemm / dph_gemm_grouped on ppw launches with gridDim.z > 1 (problems / split-K
 // slices): the XCD-aware tile order runs over the whole (z, tile) space, so each XCD takes a contiguous range
 // of one slice's / problem's tiles (their shared operand panels stay in that XCD's L2).  DPH_PPW_ZMAP=0: per-z order
@@ -850,6 +862,13 @@ using Flat = Cfg<128, 256, 64, 64>;
 // 128 x 256 tiles for 256 CUs (74 % of the chip busy, each CU a full 32 K-output tile); 192 x 128 gives
 // 252 tiles of 24 K outputs (98 % busy, 25 % less work on the critical CU)
 using Tri = Cfg<192, 128, 96, 64>;
+
+// the ring kernel finishes a tile in the register epilogue (direct_epi: per-wave column-sum slab rows of WTM) when
+// the config allows it and the args do (splits == 1 && direct_epi_ok), else in the LDS-staged one (rows of BM)
+template <class C>
+constexpr bool direct_cfg() {
+  return DPH_DIRECT_EPI && (C::FM * C::FN <= 16 || C::NW == 4) && C::WPE <= 3;
+}
 
 // s_waitcnt vmcnt(n * DMA): at most n slices' DMAs still in flight
 template <int DMA, int n>
@@ -1518,7 +1537,7 @@ __global__ void __launch_bounds__(C::NT, C::WPE) ring_gemm_kernel(const DphGemmA
   };
   // (not the 256 x 256 tile: its 128 accumulators leave no room for the epilogue inputs; not the 8-wave
   // 128 x 128 tile: at 4 waves per SIMD its 128-VGPR budget spilled 50 registers)
-  if constexpr (DPH_DIRECT_EPI && (C::FM * C::FN <= 16 || C::NW == 4) && C::WPE <= 3) {
+  if constexpr (ring::direct_cfg<C>()) {
     if (a.splits == 1 && ring::direct_epi_ok(a)) {
       DPH_TSTAMP(sA);
       sB = sA;
@@ -1653,8 +1672,17 @@ __global__ void __launch_bounds__(C::NT, C::WPE) ring_gemm_kernel(const DphGemmA
           so += red[(w * 2 + 0) * C::BN + tid];
           sx += red[(w * 2 + 1) * C::BN + tid];
         }
-        if (a.colsum_out && n < csn) atomicAdd(a.colsum_out + voff + n, so);
-        if (a.colsum_aux && n < csn) atomicAdd(a.colsum_aux + voff + n, sx);
+        if (a.flags & GEMM_COLSUM_SLAB) {
+          // one slab row per BM-row M tile (summed in a fixed order by colsum_slab_reduce_kernel)
+          float* wo = reinterpret_cast<float*>(a.workspace) + (m0 / C::BM) * a.N;
+          if (n < csn) {
+            wo[n] = so;
+            wo[cdiv(a.M, (int64_t)C::BM) * a.N + n] = sx;
+          }
+        } else {
+          if (a.colsum_out && n < csn) atomicAdd(a.colsum_out + voff + n, so);
+          if (a.colsum_aux && n < csn) atomicAdd(a.colsum_aux + voff + n, sx);
+        }
       }
     }
   }
@@ -3124,58 +3152,70 @@ extern "C" int dph_gemm(const DphGemmArgs* args, hipStream_t stream) {
               "dph_gemm: device-side extents (dyn_ext) need a ping-pong layout (k-contiguous A and B, K %% 64 == 0, dense "
               "aligned C) or the (mn, mn) weight-gradient plan: M=%lld N=%lld K=%lld", (long long)a.M, (long long)a.N,
               (long long)a.K);
+  // Column sums (bias / mask gradients of the GELU-backward epilogues) go through a workspace slab of per-tile (or
+  // per-wave) partial rows when the caller passed one (kernels.py does for batch 1), summed after the GEMM by
+  // colsum_slab_reduce_kernel: in row groups with one float atomic per column per group, or -- deterministic mode --
+  // by one group in a fixed order.  The slab row granularity is the epilogue's: per wave (WTM rows) in the register
+  // epilogues, per M tile (BM rows) in the LDS-staged ones.
+  const bool want_cs = (a.colsum_out || a.colsum_aux) != 0;
+  int64_t slot_rows = 0;
+  if (want_cs) {
+    auto ring_rows = [&](int64_t bm, int64_t wtm, bool dcfg) { return (dcfg && ring::direct_epi_ok(a)) ? wtm : bm; };
+    switch (kind) {
+      case 12: case 14: slot_rows = 128; break;            // ping-pong register epilogues: per wave
+      case 13: case 15: case 16: slot_rows = 64; break;
+      case 10: slot_rows = ring_rows(ring::Tri::BM, ring::Tri::WTM, ring::direct_cfg<ring::Tri>()); break;
+      case 8: slot_rows = ring_rows(ring::Flat::BM, ring::Flat::WTM, ring::direct_cfg<ring::Flat>()); break;
+      case 7: slot_rows = ring_rows(ring::Wide::BM, ring::Wide::WTM, ring::direct_cfg<ring::Wide>()); break;
+      case 5: case 6: slot_rows = ring_rows(ring::Mid8::BM, ring::Mid8::WTM, ring::direct_cfg<ring::Mid8>()); break;
+      case 4: slot_rows = ring_rows(ring::Half::BM, ring::Half::WTM, ring::direct_cfg<ring::Half>()); break;
+      case 3: slot_rows = ring_rows(ring::Tall::BM, ring::Tall::WTM, ring::direct_cfg<ring::Tall>()); break;
+      case 2: slot_rows = ring_rows(ring::Big::BM, ring::Big::WTM, ring::direct_cfg<ring::Big>()); break;
+      case 1: slot_rows = ring_rows(ring::Mid::BM, ring::Mid::WTM, ring::direct_cfg<ring::Mid>()); break;
+      default: slot_rows = BM; break;                      // register-staged kernel: per 128-row M tile
+    }
+  }
+  const int64_t nslots = want_cs ? cdiv(a.M, slot_rows) : 0;
+  const bool slab = want_cs && a.batch == 1 && a.workspace && a.workspace_bytes >= 2 * nslots * a.N * 4;
+  DPH_REQUIRE(!want_cs || slab || !deterministic(),
+              "dph_gemm: deterministic mode needs the column-sum workspace (batch 1, >= 2 * cdiv(M, 64) * N fp32)");
+  DphGemmArgs b = a;
+  if (slab) b.flags |= GEMM_COLSUM_SLAB;
   if (kind >= 12 && kind <= 16) {
     DPH_REQUIRE(cdiv(a.M, 128) < 65536 && a.batch < 65536, "dph_gemm: grid too large");
-    // column sums through a workspace slab when the caller passed one (kernels.py does for splits == 1)
-    const int64_t wtm = (kind == 12 || kind == 14) ? 128 : 64;
-    const int64_t nslots = cdiv(a.M, wtm);
-    DphGemmArgs b = a;
-    const bool slab = (a.colsum_out || a.colsum_aux) && a.batch == 1 && a.workspace &&
-                      a.workspace_bytes >= 2 * nslots * a.N * 4;
-    if (slab) b.flags |= GEMM_COLSUM_SLAB;
     if (kind == 12) launch_pp<pp::P256>(b, stream);
     else if (kind == 13) launch_pp<pp::P128x256>(b, stream);
     else if (kind == 14) launch_pp<pp::P256x128>(b, stream);
     else if (kind == 15) launch_pp<pp::P128x192>(b, stream);
     else launch_pp<pp::P128>(b, stream);
-    if (slab) {
-      int rc = check_launch("dph_gemm");
-      if (rc) return rc;
-      const int64_t csn = std::min<int64_t>(a.colsum_n > 0 ? a.colsum_n : a.N, a.N);
-      // (>= 16 slab rows per group: a few hundred blocks even at N = 768, each thread's rows in flight together)
-      const unsigned groups = (unsigned)std::max<int64_t>(1, std::min<int64_t>(32, cdiv(nslots, 16)));
-      hipLaunchKernelGGL(colsum_slab_reduce_kernel, dim3((unsigned)cdiv(csn, 64), groups), dim3(256), 0, stream,
-                         reinterpret_cast<const float*>(a.workspace), nslots, a.N, csn, a.colsum_out, a.colsum_aux);
-      return check_launch("dph_gemm colsum reduce");
-    }
   } else if (kind == 10) {
     DPH_REQUIRE(cdiv(a.M, ring::Tri::BM) < 65536 && a.batch * a.splits < 65536, "dph_gemm: grid too large");
-    if (!launch_ring_persist<ring::Tri>(a, stream)) launch_ring<ring::Tri, false>(a, kchunk, stream);
+    if (!launch_ring_persist<ring::Tri>(b, stream)) launch_ring<ring::Tri, false>(b, kchunk, stream);
   } else if (kind == 8) {
     DPH_REQUIRE(cdiv(a.M, ring::Flat::BM) < 65536 && a.batch * a.splits < 65536, "dph_gemm: grid too large");
-    if (!launch_ring_persist<ring::Flat>(a, stream)) launch_ring<ring::Flat, false>(a, kchunk, stream);
+    if (!launch_ring_persist<ring::Flat>(b, stream)) launch_ring<ring::Flat, false>(b, kchunk, stream);
   } else if (kind == 7) {
     DPH_REQUIRE(cdiv(a.M, ring::Wide::BM) < 65536 && a.batch * a.splits < 65536, "dph_gemm: grid too large");
-    if (!launch_ring_persist<ring::Wide>(a, stream)) launch_ring<ring::Wide, false>(a, kchunk, stream);
+    if (!launch_ring_persist<ring::Wide>(b, stream)) launch_ring<ring::Wide, false>(b, kchunk, stream);
   } else if (kind == 6) {
     DPH_REQUIRE(cdiv(a.M, ring::Mid8::BM) < 65536 && a.batch * a.splits < 65536, "dph_gemm: grid too large");
-    launch_ring<ring::Mid8, true>(a, kchunk, stream);
+    launch_ring<ring::Mid8, true>(b, kchunk, stream);
   } else if (kind == 5) {
     DPH_REQUIRE(cdiv(a.M, ring::Mid8::BM) < 65536 && a.batch * a.splits < 65536, "dph_gemm: grid too large");
-    launch_ring<ring::Mid8, false>(a, kchunk, stream);
+    launch_ring<ring::Mid8, false>(b, kchunk, stream);
   } else if (kind == 4) {
     DPH_REQUIRE(cdiv(a.M, ring::Half::BM) < 65536 && a.batch * a.splits < 65536, "dph_gemm: grid too large");
-    launch_ring<ring::Half, false>(a, kchunk, stream);
+    launch_ring<ring::Half, false>(b, kchunk, stream);
   } else if (kind == 3) {
     DPH_REQUIRE(cdiv(a.M, ring::Tall::BM) < 65536 && a.batch * a.splits < 65536, "dph_gemm: grid too large");
-    launch_ring<ring::Tall, false>(a, kchunk, stream);
+    launch_ring<ring::Tall, false>(b, kchunk, stream);
   } else if (kind == 2) {
     DPH_REQUIRE(cdiv(a.M, ring::Big::BM) < 65536 && a.batch * a.splits < 65536, "dph_gemm: grid too large");
-    launch_ring<ring::Big, false>(a, kchunk, stream);
+    launch_ring<ring::Big, false>(b, kchunk, stream);
   } else if (kind == 1) {
     DPH_REQUIRE(cdiv(a.M, ring::Mid::BM) < 65536 && a.batch * a.splits < 65536, "dph_gemm: grid too large");
-    if (a.a_kcontig && a.b_kcontig) launch_ring<ring::Mid, false>(a, kchunk, stream);
-    else launch_ring<ring::Mid, true>(a, kchunk, stream);
+    if (a.a_kcontig && a.b_kcontig) launch_ring<ring::Mid, false>(b, kchunk, stream);
+    else launch_ring<ring::Mid, true>(b, kchunk, stream);
   } else {
   dim3 grid((unsigned)cdiv(a.N, BN), (unsigned)cdiv(a.M, BM), (unsigned)(a.batch * a.splits));
   DPH_REQUIRE(grid.y < 65536 && grid.z < 65536, "dph_gemm: grid too large");
@@ -3193,27 +3233,37 @@ extern "C" int dph_gemm(const DphGemmArgs* args, hipStream_t stream) {
   }
   if (small_nt(kchunk) == 512) {
     if (a.a_kcontig && a.b_kcontig)
-      hipLaunchKernelGGL((gemm_kernel<true, true, 512>), grid, dim3(512), 0, stream, a, kchunk, cnt);
+      hipLaunchKernelGGL((gemm_kernel<true, true, 512>), grid, dim3(512), 0, stream, b, kchunk, cnt);
     else if (a.a_kcontig && !a.b_kcontig)
-      hipLaunchKernelGGL((gemm_kernel<true, false, 512>), grid, dim3(512), 0, stream, a, kchunk, cnt);
+      hipLaunchKernelGGL((gemm_kernel<true, false, 512>), grid, dim3(512), 0, stream, b, kchunk, cnt);
     else if (!a.a_kcontig && a.b_kcontig)
-      hipLaunchKernelGGL((gemm_kernel<false, true, 512>), grid, dim3(512), 0, stream, a, kchunk, cnt);
+      hipLaunchKernelGGL((gemm_kernel<false, true, 512>), grid, dim3(512), 0, stream, b, kchunk, cnt);
     else
-      hipLaunchKernelGGL((gemm_kernel<false, false, 512>), grid, dim3(512), 0, stream, a, kchunk, cnt);
+      hipLaunchKernelGGL((gemm_kernel<false, false, 512>), grid, dim3(512), 0, stream, b, kchunk, cnt);
   } else {
   if (a.a_kcontig && a.b_kcontig)
-    hipLaunchKernelGGL((gemm_kernel<true, true>), grid, dim3(NTHREADS), 0, stream, a, kchunk, cnt);
+    hipLaunchKernelGGL((gemm_kernel<true, true>), grid, dim3(NTHREADS), 0, stream, b, kchunk, cnt);
   else if (a.a_kcontig && !a.b_kcontig)
-    hipLaunchKernelGGL((gemm_kernel<true, false>), grid, dim3(NTHREADS), 0, stream, a, kchunk, cnt);
+    hipLaunchKernelGGL((gemm_kernel<true, false>), grid, dim3(NTHREADS), 0, stream, b, kchunk, cnt);
   else if (!a.a_kcontig && a.b_kcontig)
-    hipLaunchKernelGGL((gemm_kernel<false, true>), grid, dim3(NTHREADS), 0, stream, a, kchunk, cnt);
+    hipLaunchKernelGGL((gemm_kernel<false, true>), grid, dim3(NTHREADS), 0, stream, b, kchunk, cnt);
   else
-    hipLaunchKernelGGL((gemm_kernel<false, false>), grid, dim3(NTHREADS), 0, stream, a, kchunk, cnt);
+    hipLaunchKernelGGL((gemm_kernel<false, false>), grid, dim3(NTHREADS), 0, stream, b, kchunk, cnt);
   }
   if (cnt != nullptr) return check_launch("dph_gemm");
   }
   int rc = check_launch("dph_gemm");
   if (rc) return rc;
+  if (slab) {
+    const int64_t csn = std::min<int64_t>(a.colsum_n > 0 ? a.colsum_n : a.N, a.N);
+    // (>= 16 slab rows per group: a few hundred blocks even at N = 768, each thread's rows in flight together;
+    // deterministic mode: one group, each column summed in a fixed order)
+    const unsigned groups =
+        deterministic() ? 1u : (unsigned)std::max<int64_t>(1, std::min<int64_t>(32, cdiv(nslots, 16)));
+    hipLaunchKernelGGL(colsum_slab_reduce_kernel, dim3((unsigned)cdiv(csn, 64), groups), dim3(256), 0, stream,
+                       reinterpret_cast<const float*>(a.workspace), nslots, a.N, csn, a.colsum_out, a.colsum_aux);
+    return check_launch("dph_gemm colsum reduce");
+  }
   if (a.splits > 1) {
     const int64_t work = a.M * cdiv(a.N, 8);
     dim3 g2((unsigned)cdiv(work, 256), 1, (unsigned)a.batch);

@@ -166,7 +166,8 @@ __global__ void __launch_bounds__(64 * LN_BWD_WAVES) ln_bwd_kernel(
     DT* __restrict__ dx, float* __restrict__ dgamma, float* __restrict__ dbeta, int64_t rows, int D, int ld,
     float drop_p, uint64_t seed, bf16_t* __restrict__ branch, float branch_p, uint64_t branch_seed,
     const float* __restrict__ branch_smask, float* __restrict__ branch_colsum, const bf16_t* __restrict__ branch_pre,
-    float* __restrict__ branch_sdot, const DT* __restrict__ dx_add, float* __restrict__ ws) {
+    float* __restrict__ branch_sdot, const DT* __restrict__ dx_add, float* __restrict__ ws,
+    float* __restrict__ sdot_part) {
   seed = epoch_seed(seed); branch_seed = epoch_seed(branch_seed);   // per-step RNG epoch (graph replays)
   __shared__ float4 red[LN_BWD_WAVES][NV * 64];
   const int lane = threadIdx.x & 63;
@@ -296,7 +297,9 @@ __global__ void __launch_bounds__(64 * LN_BWD_WAVES) ln_bwd_kernel(
     if (threadIdx.x == 0) {
       float t = 0.f;
       for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += sdot_s[w];
-      atomicAdd(branch_sdot, t);
+      // deterministic mode: the block's partial, summed in block order by sdot_reduce_kernel
+      if (sdot_part) sdot_part[blockIdx.x] = t;
+      else atomicAdd(branch_sdot, t);
     }
   }
 }
@@ -428,6 +431,43 @@ __global__ void __launch_bounds__(256) colprod_kernel(const bf16_t* __restrict__
   }
 }
 
+// deterministic mode: the same contraction with every column's rows in a fixed order, one block per 32 columns (thread
+// (column, phase) takes rows phase, phase + DET_PH, ... in four chains, the phases added in order; no atomics)
+__global__ void __launch_bounds__(32 * DET_PH) colprod_det_kernel(const bf16_t* __restrict__ a, int64_t lda,
+                                                                  const float* __restrict__ b, int64_t ldb,
+                                                                  const float* __restrict__ colmask,
+                                                                  float* __restrict__ out, int64_t R, int64_t N) {
+  __shared__ float red[DET_PH][33];
+  const int tx = threadIdx.x & 31, ph = threadIdx.x >> 5;
+  const int64_t col = (int64_t)blockIdx.x * 32 + tx;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (col < N) {
+    int64_t r = ph;
+    for (; r + 3 * DET_PH < R; r += 4 * DET_PH) {
+      s0 = fmaf(bf2f(a[r * lda + col]), b[r * ldb + col], s0);
+      s1 = fmaf(bf2f(a[(r + DET_PH) * lda + col]), b[(r + DET_PH) * ldb + col], s1);
+      s2 = fmaf(bf2f(a[(r + 2 * DET_PH) * lda + col]), b[(r + 2 * DET_PH) * ldb + col], s2);
+      s3 = fmaf(bf2f(a[(r + 3 * DET_PH) * lda + col]), b[(r + 3 * DET_PH) * ldb + col], s3);
+    }
+    if (r < R) s0 = fmaf(bf2f(a[r * lda + col]), b[r * ldb + col], s0);
+    if (r + DET_PH < R) s1 = fmaf(bf2f(a[(r + DET_PH) * lda + col]), b[(r + DET_PH) * ldb + col], s1);
+    if (r + 2 * DET_PH < R) s2 = fmaf(bf2f(a[(r + 2 * DET_PH) * lda + col]), b[(r + 2 * DET_PH) * ldb + col], s2);
+  }
+  red[ph][tx] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (ph == 0 && col < N) {
+    float t = 0.f;
+#pragma unroll 8
+    for (int i = 0; i < DET_PH; ++i) t += red[i][tx];
+    float sc = 1.f;
+    if (colmask) {
+      const float m = colmask[col];
+      sc = m != 0.f ? 1.0f / m : 0.f;
+    }
+    out[col] += sc * t;
+  }
+}
+
 // out_q[c] += sum_r ws[r][q * seg + c] for the (up to 3) column segments q of width seg (null outputs
 // skipped).  Block = 64 columns x 4 row phases over one of gridDim.y row groups; one atomic per column
 // per group (a handful of adders per address).
@@ -464,6 +504,36 @@ __global__ void __launch_bounds__(256) slab_reduce_kernel(const float* __restric
 // row groups of a slab reduction: >= 32 rows (8 per thread phase) per group, up to 32 groups (one atomic per column
 // per group)
 int64_t slab_groups(int64_t nrows) { return std::max<int64_t>(1, std::min<int64_t>(32, cdiv(nrows, 32))); }
+
+// deterministic mode: the same sums with every column's rows added in a fixed order by one block (32 columns each)
+__global__ void __launch_bounds__(32 * DET_PH) slab_reduce_det_kernel(const float* __restrict__ ws, int64_t nrows,
+                                                                      int64_t ncols, int64_t seg, float* __restrict__ o0,
+                                                                      float* __restrict__ o1, float* __restrict__ o2) {
+  __shared__ float red[DET_PH][33];
+  const int64_t col = (int64_t)blockIdx.x * 32 + (threadIdx.x & 31);
+  const int q = col < ncols ? (int)(col / seg) : 0;
+  float* out = q == 0 ? o0 : (q == 1 ? o1 : o2);
+  const bool live = col < ncols && out != nullptr;
+  const float t = det_column_total(live ? ws + col : nullptr, nrows, ncols, red);
+  if ((threadIdx.x >> 5) == 0 && live) out[col - (int64_t)q * seg] += t;
+}
+
+// out[0] += sum of n per-block partials, in block order (one wave)
+__global__ void __launch_bounds__(64) sdot_reduce_kernel(const float* __restrict__ part, int64_t n,
+                                                         float* __restrict__ out) {
+  const float s = sum_partials_wave(part, n, 1);
+  if (threadIdx.x == 0) out[0] += s;
+}
+
+void slab_reduce_launch(const float* ws, int64_t nrows, int64_t ncols, int64_t seg, float* o0, float* o1, float* o2,
+                        hipStream_t stream) {
+  if (deterministic())
+    hipLaunchKernelGGL(slab_reduce_det_kernel, dim3((unsigned)cdiv(ncols, 32)), dim3(32 * DET_PH), 0, stream, ws,
+                       nrows, ncols, seg, o0, o1, o2);
+  else
+    hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)cdiv(ncols, 64), (unsigned)slab_groups(nrows)), dim3(256), 0,
+                       stream, ws, nrows, ncols, seg, o0, o1, o2);
+}
 
 int64_t colsum_rpb(int64_t rows) { return std::max<int64_t>(64, cdiv(cdiv(rows, 8192), 4) * 4); }
 
@@ -571,7 +641,7 @@ __global__ void __launch_bounds__(512) ln_bwd16_kernel(
     float* __restrict__ dgamma, float* __restrict__ dbeta, int64_t rows, bf16_t* __restrict__ branch, float branch_p,
     uint64_t branch_seed, const float* __restrict__ branch_smask, float* __restrict__ branch_colsum,
     const bf16_t* __restrict__ branch_pre, float* __restrict__ branch_sdot, const DT* __restrict__ dx_add,
-    float* __restrict__ ws) {
+    float* __restrict__ ws, float* __restrict__ sdot_part) {
   constexpr int NC = NE / 8;
   constexpr int D = NE * 32;
   static_assert(LN_BWD_WAVES == 8 && LN_BWD_RPW == 2, "ln_bwd16: the slab layout assumes 16 rows per block");
@@ -715,12 +785,23 @@ __global__ void __launch_bounds__(512) ln_bwd16_kernel(
     if (threadIdx.x == 0) {
       float t = 0.f;
       for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += sdot_s[w];
-      atomicAdd(branch_sdot, t);
+      // deterministic mode: the block's partial, summed in block order by sdot_reduce_kernel
+      if (sdot_part) sdot_part[blockIdx.x] = t;
+      else atomicAdd(branch_sdot, t);
     }
   }
 }
 
 }  // namespace
+
+// (shared with the other translation units: common.h)
+void slab_reduce_cols(const float* ws, int64_t nrows, int64_t ncols, int64_t seg, float* o0, float* o1, float* o2,
+                      hipStream_t stream) {
+  slab_reduce_launch(ws, nrows, ncols, seg, o0, o1, o2, stream);
+}
+void sdot_reduce(const float* part, int64_t n, float* out, hipStream_t stream) {
+  hipLaunchKernelGGL(sdot_reduce_kernel, dim3(1), dim3(64), 0, stream, part, n, out);
+}
 }  // namespace dph
 
 using namespace dph;
@@ -798,7 +879,9 @@ extern "C" int dph_layernorm_fwd(const void* x, const float* xscale, const float
 }
 
 extern "C" int64_t dph_layernorm_bwd_workspace(int64_t rows, int64_t D) {
-  return cdiv(rows, (int64_t)LN_BWD_WAVES * LN_BWD_RPW) * 3 * D * 4;
+  // per-block slab rows [nblk][3][D] + the per-block branch_sdot partials of deterministic mode [nblk]
+  const int64_t nblk = cdiv(rows, (int64_t)LN_BWD_WAVES * LN_BWD_RPW);
+  return nblk * (3 * D + 1) * 4;
 }
 
 namespace {
@@ -821,7 +904,7 @@ void ln_bwd16_f32x(const void* dy, const float* x, const float* gamma, const flo
 #define LN_BWD16F_LAUNCH(NE)                                                                                     \
   hipLaunchKernelGGL((ln_bwd16_kernel<NE, float, DT>), grid, dim3(512), 0, stream, dyb, x, gamma, mean, rstd, dx,  \
                      dgamma, dbeta, rows, (bf16_t*)nullptr, 0.f, (uint64_t)0, (const float*)nullptr,              \
-                     (float*)nullptr, (const bf16_t*)nullptr, (float*)nullptr, dx_add, ws)
+                     (float*)nullptr, (const bf16_t*)nullptr, (float*)nullptr, dx_add, ws, (float*)nullptr)
   switch (D / 256) {
     case 1: LN_BWD16F_LAUNCH(8); break;
     case 2: LN_BWD16F_LAUNCH(16); break;
@@ -845,10 +928,12 @@ extern "C" int dph_layernorm_bwd_ld(const void* dy, const void* x, const float* 
   DPH_REQUIRE(!branch_sdot || branch_pre, "dph_layernorm_bwd: branch_sdot needs branch_pre");
   DPH_REQUIRE(!(branch_colsum || branch_sdot) || branch, "dph_layernorm_bwd: branch sums need branch output");
   const bool sums = dgamma || dbeta || branch_colsum;
-  DPH_REQUIRE(!sums || (ws && ws_bytes >= dph_layernorm_bwd_workspace(rows, D)),
+  const bool det_sdot = branch_sdot && deterministic();
+  DPH_REQUIRE(!(sums || det_sdot) || (ws && ws_bytes >= dph_layernorm_bwd_workspace(rows, D)),
               "dph_layernorm_bwd: workspace too small (%lld < %lld bytes)", (long long)ws_bytes,
               (long long)dph_layernorm_bwd_workspace(rows, D));
   const dim3 grid((unsigned)cdiv(rows, LN_BWD_WAVES * LN_BWD_RPW));
+  float* sdot_part = det_sdot ? ws + (int64_t)grid.x * 3 * D : nullptr;
   static const bool ln16 = [] {
     const char* e = getenv("DPH_LN_BWD16");
     return !(e && e[0] == '0');
@@ -863,7 +948,7 @@ extern "C" int dph_layernorm_bwd_ld(const void* dy, const void* x, const float* 
   hipLaunchKernelGGL(ln_bwd16_kernel<NE>, grid, dim3(512), 0, stream, dyb, xb, gamma, mean, rstd,                 \
                      reinterpret_cast<bf16_t*>(dx), dgamma, dbeta, rows, reinterpret_cast<bf16_t*>(branch), branch_p, \
                      branch_seed, branch_smask, branch_colsum, reinterpret_cast<const bf16_t*>(branch_pre),           \
-                     branch_sdot, reinterpret_cast<const bf16_t*>(dx_add), ws)
+                     branch_sdot, reinterpret_cast<const bf16_t*>(dx_add), ws, sdot_part)
     switch (D / 256) {
       case 1: LN_BWD16_LAUNCH(8); break;
       case 2: LN_BWD16_LAUNCH(16); break;
@@ -878,7 +963,7 @@ extern "C" int dph_layernorm_bwd_ld(const void* dy, const void* x, const float* 
                      rstd, reinterpret_cast<bf16_t*>(dx), dgamma, dbeta, rows, (int)D, (int)ld, dropout_p, seed,  \
                      reinterpret_cast<bf16_t*>(branch), branch_p, branch_seed, branch_smask, branch_colsum,       \
                      reinterpret_cast<const bf16_t*>(branch_pre), branch_sdot, reinterpret_cast<const bf16_t*>(dx_add), \
-                     ws)
+                     ws, sdot_part)
   switch (cdiv(ld, 256)) {
     case 1: LN_BWD_LAUNCH(1); break;
     case 2: LN_BWD_LAUNCH(2); break;
@@ -887,11 +972,8 @@ extern "C" int dph_layernorm_bwd_ld(const void* dy, const void* x, const float* 
   }
 #undef LN_BWD_LAUNCH
   }
-  if (sums) {
-    const int64_t nblk = grid.x;
-    hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)cdiv(3 * D, 64), (unsigned)slab_groups(nblk)), dim3(256),
-                       0, stream, ws, nblk, 3 * D, D, dgamma, dbeta, branch_colsum);
-  }
+  if (sums) slab_reduce_launch(ws, grid.x, 3 * D, D, dgamma, dbeta, branch_colsum, stream);
+  if (det_sdot) hipLaunchKernelGGL(sdot_reduce_kernel, dim3(1), dim3(64), 0, stream, sdot_part, (int64_t)grid.x, branch_sdot);
   return check_launch("dph_layernorm_bwd");
 }
 
@@ -916,7 +998,7 @@ extern "C" int dph_layernorm_bwd_x32(const void* dy, const float* x, const float
                      reinterpret_cast<const bf16_t*>(dy), x, (const float*)nullptr, gamma, mean, rstd,           \
                      reinterpret_cast<bf16_t*>(dx), dgamma, dbeta, rows, (int)D, (int)D, 0.f, (uint64_t)0,        \
                      (bf16_t*)nullptr, 0.f, (uint64_t)0, (const float*)nullptr, (float*)nullptr,                  \
-                     (const bf16_t*)nullptr, (float*)nullptr, (const bf16_t*)nullptr, ws)
+                     (const bf16_t*)nullptr, (float*)nullptr, (const bf16_t*)nullptr, ws, (float*)nullptr)
   switch (cdiv(D, 256)) {
     case 1: LN_BWD32_LAUNCH(1); break;
     case 2: LN_BWD32_LAUNCH(2); break;
@@ -925,11 +1007,7 @@ extern "C" int dph_layernorm_bwd_x32(const void* dy, const float* x, const float
   }
 #undef LN_BWD32_LAUNCH
   }
-  if (sums) {
-    const int64_t nblk = grid.x;
-    hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)cdiv(3 * D, 64), (unsigned)slab_groups(nblk)), dim3(256),
-                       0, stream, ws, nblk, 3 * D, D, dgamma, dbeta, (float*)nullptr);
-  }
+  if (sums) slab_reduce_launch(ws, grid.x, 3 * D, D, dgamma, dbeta, nullptr, stream);
   return check_launch("dph_layernorm_bwd_x32");
 }
 
@@ -985,7 +1063,8 @@ extern "C" int dph_layernorm_bwd_res32(const void* dy, const float* x, const flo
   hipLaunchKernelGGL((ln_bwd_kernel<NV, float, float>), grid, dim3(64 * LN_BWD_WAVES), 0, stream,                \
                      reinterpret_cast<const bf16_t*>(dy), x, (const float*)nullptr, gamma, mean, rstd, dx, dgamma, \
                      dbeta, rows, (int)D, (int)D, 0.f, (uint64_t)0, (bf16_t*)nullptr, 0.f, (uint64_t)0,           \
-                     (const float*)nullptr, (float*)nullptr, (const bf16_t*)nullptr, (float*)nullptr, dx_add, ws)
+                     (const float*)nullptr, (float*)nullptr, (const bf16_t*)nullptr, (float*)nullptr, dx_add, ws,      \
+                     (float*)nullptr)
   switch (cdiv(D, 256)) {
     case 1: LN_BWDR_LAUNCH(1); break;
     case 2: LN_BWDR_LAUNCH(2); break;
@@ -994,11 +1073,7 @@ extern "C" int dph_layernorm_bwd_res32(const void* dy, const float* x, const flo
   }
 #undef LN_BWDR_LAUNCH
   }
-  if (sums) {
-    const int64_t nblk = grid.x;
-    hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)cdiv(3 * D, 64), (unsigned)slab_groups(nblk)), dim3(256),
-                       0, stream, ws, nblk, 3 * D, D, dgamma, dbeta, (float*)nullptr);
-  }
+  if (sums) slab_reduce_launch(ws, grid.x, 3 * D, D, dgamma, dbeta, nullptr, stream);
   return check_launch("dph_layernorm_bwd_res32");
 }
 
@@ -1023,6 +1098,11 @@ extern "C" int dph_layernorm_bwd(const void* dy, const void* x, const float* xsc
 extern "C" int dph_colprod(const void* a, int64_t lda, const float* b, int64_t ldb, const float* colmask, float* out,
                            int64_t R, int64_t N, hipStream_t stream) {
   DPH_REQUIRE(a && b && out && R > 0 && N > 0 && lda >= N && ldb >= N, "dph_colprod: bad args");
+  if (deterministic()) {
+    hipLaunchKernelGGL(colprod_det_kernel, dim3((unsigned)cdiv(N, 32)), dim3(32 * DET_PH), 0, stream,
+                       reinterpret_cast<const bf16_t*>(a), lda, b, ldb, colmask, out, R, N);
+    return check_launch("dph_colprod");
+  }
   const int64_t rpb = 32;
   dim3 grid((unsigned)cdiv(N, 512), (unsigned)cdiv(R, rpb));
   hipLaunchKernelGGL(colprod_kernel, grid, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(a), lda, b, ldb,
@@ -1043,8 +1123,7 @@ extern "C" int dph_colsum(const void* x, float* out, int64_t rows, int64_t cols,
   dim3 grid((unsigned)cdiv(cols, 512), (unsigned)nrb);
   hipLaunchKernelGGL(colsum_kernel, grid, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(x), ws, rows, cols,
                      rpb);
-  hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)cdiv(cols, 64), (unsigned)slab_groups(nrb)), dim3(256), 0,
-                     stream, ws, nrb, cols, cols, out, (float*)nullptr, (float*)nullptr);
+  slab_reduce_launch(ws, nrb, cols, cols, out, nullptr, nullptr, stream);
   return check_launch("dph_colsum");
 }
 
@@ -1062,7 +1141,6 @@ extern "C" int dph_colsum3(const void* x, float* out0, float* out1, float* out2,
   dim3 grid((unsigned)cdiv(cols, 512), (unsigned)nrb);
   hipLaunchKernelGGL(colsum_kernel, grid, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(x), ws, rows, cols,
                      rpb);
-  hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)cdiv(cols, 64), (unsigned)slab_groups(nrb)), dim3(256), 0,
-                     stream, ws, nrb, cols, seg, out0, out1, out2);
+  slab_reduce_launch(ws, nrb, cols, seg, out0, out1, out2, stream);
   return check_launch("dph_colsum3");
 }

@@ -57,6 +57,25 @@ __global__ void relpos_table_bwd_kernel(const float* __restrict__ dtab, const in
   atomicAdd(dembed + (int64_t)bk * Htot + hh, v);
 }
 
+// deterministic mode: the diagonals r of one bucket form ONE contiguous run (the bucket is monotone in |k - q| on
+// each side of the main diagonal, and the two sides use disjoint bucket ranges), so the thread at a run's first
+// diagonal sums the run in order and is the only writer of its embedding entry
+__global__ void relpos_table_bwd_det_kernel(const float* __restrict__ dtab, const int64_t* __restrict__ heads,
+                                            float* __restrict__ dembed, int T, int H, int Htot, int num_buckets,
+                                            int max_distance, float log_ratio) {
+  const int R = 2 * T - 1;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= R * H) return;
+  const int h = i / R, r = i % R;
+  const int bk = relpos_bucket(r - (T - 1), num_buckets, max_distance, log_ratio);
+  if (r > 0 && relpos_bucket(r - 1 - (T - 1), num_buckets, max_distance, log_ratio) == bk) return;
+  float acc = 0.f;
+  for (int j = r; j < R && relpos_bucket(j - (T - 1), num_buckets, max_distance, log_ratio) == bk; ++j)
+    acc += dtab[h * R + j];
+  const int hh = heads ? (int)heads[h] : h;
+  dembed[(int64_t)bk * Htot + hh] += acc;
+}
+
 constexpr int HDG = 64;   // gate head dim
 
 struct GateArgs {
@@ -131,7 +150,7 @@ __global__ void __launch_bounds__(256) wavlm_gate_fwd_kernel(GateArgs a, float* 
 __global__ void __launch_bounds__(256) wavlm_gate_bwd_kernel(GateArgs a, const float* __restrict__ dgate,
                                                              bf16_t* __restrict__ dx, int64_t lddx,
                                                              float* __restrict__ dz_out, float* __restrict__ db,
-                                                             float* __restrict__ dconst) {
+                                                             float* __restrict__ dconst, float* __restrict__ dc_out) {
   __shared__ __attribute__((aligned(16))) float w_s[2 * HDG + 4];
   __shared__ float dc_s[64];   // per-block dconst partials (total heads <= 64)
   load_group_weights(a, w_s);
@@ -157,6 +176,7 @@ __global__ void __launch_bounds__(256) wavlm_gate_bwd_kernel(GateArgs a, const f
     dzb = dgb * gb * (1.f - gb);
     dz_out[i * 2] = dza;
     dz_out[i * 2 + 1] = dzb;
+    if (dc_out) dc_out[i] = dc;
     // dx[d] += dza wa[d] + dzb wb[d]  (read-modify-write of this head's 64 bf16; heads of a row are disjoint)
     bf16_t* xp = dx + bt * lddx + (int64_t)hh * HDG;
 #pragma unroll
@@ -173,6 +193,8 @@ __global__ void __launch_bounds__(256) wavlm_gate_bwd_kernel(GateArgs a, const f
       *reinterpret_cast<uint4*>(xp + k) = make_uint4(wv[0], wv[1], wv[2], wv[3]);
     }
   }
+  // deterministic mode (dc_out): db / dconst are summed in a fixed order by the weight-gradient / finish kernels
+  if (dc_out) return;
   // db[j] = sum dz_j (j < 4: dza, else dzb): wave sums -> one atomic pair per block; dconst[hh] += dc
   __shared__ float red[2][4];
   const float sa = wave_sum(dza), sb = wave_sum(dzb);
@@ -192,7 +214,8 @@ __global__ void __launch_bounds__(256) wavlm_gate_bwd_kernel(GateArgs a, const f
 // backward, pass 2: dW[j][d] = sum_n dz[n][j/4] x[n][d]; block = 256 rows n, thread (jg = t>>6 in {0..3}, d = t&63)
 // sums a quarter of the rows for both groups, LDS-combined, then atomics (db rows 1-3, 5-7 copied at the end).
 __global__ void __launch_bounds__(256) wavlm_gate_wgrad_kernel(GateArgs a, const float* __restrict__ dz,
-                                                               float* __restrict__ dw) {
+                                                               float* __restrict__ dw, const float* __restrict__ dc,
+                                                               float* __restrict__ part2) {
   __shared__ float red[4][2][HDG];
   const int d = threadIdx.x & 63;
   const int part = threadIdx.x >> 6;
@@ -216,6 +239,57 @@ __global__ void __launch_bounds__(256) wavlm_gate_wgrad_kernel(GateArgs a, const
     // the 4 logits of a group share the same gradient: one partial row per group and block (no atomics: ~1500
     // blocks' atomics on 128 addresses serialised), summed over blocks by wavlm_gate_finish_kernel
     dw[((int64_t)blockIdx.x * 2 + part) * HDG + d] = red[0][part][d] + red[1][part][d] + red[2][part][d] + red[3][part][d];
+  }
+  if (part2) {
+    // deterministic mode: this block's dconst per total head (thread t < 64) and the two group sums of dz
+    // (threads 64, 65) over its 256 rows in row order -> part2[block][66]
+    const int t = threadIdx.x;
+    if (t < 66) {
+      float acc = 0.f;
+      for (int r = 0; r < 256; ++r) {
+        const int64_t n = n0 + r;
+        if (n >= N) break;
+        if (t < 64) {
+          const int h = (int)(n % a.H);
+          const int hh = a.heads ? (int)a.heads[h] : h;
+          if (hh == t) acc += dc[n];
+        } else {
+          acc += dz[n * 2 + (t - 64)];
+        }
+      }
+      part2[(int64_t)blockIdx.x * 66 + t] = acc;
+    }
+  }
+}
+
+// deterministic mode: the per-block partial rows summed in block order (det_column_total) -- blocks 0..3: the 128
+// dW group columns (each added to its group's 4 rows); blocks 4..6: part2's 66 columns (dconst per head, then the
+// two db group sums, each added to its group's 4 bias entries)
+__global__ void __launch_bounds__(32 * DET_PH) wavlm_gate_finish_det_kernel(float* __restrict__ dw, float* __restrict__ db,
+                                                                           float* __restrict__ dconst,
+                                                                           const float* __restrict__ part,
+                                                                           const float* __restrict__ part2, int nblk) {
+  __shared__ float red[DET_PH][33];
+  const int tx = threadIdx.x & 31, ph = threadIdx.x >> 5;
+  if (blockIdx.x < 4) {
+    const int col = blockIdx.x * 32 + tx;   // (group, d) = (col / 64, col % 64)
+    const float t = det_column_total(part + col, nblk, 2 * HDG, red);
+    if (ph == 0) {
+      const int grp = col / HDG, d = col % HDG;
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) dw[(grp * 4 + jj) * HDG + d] += t;
+    }
+  } else {
+    const int col = (blockIdx.x - 4) * 32 + tx;
+    const float t = det_column_total(col < 66 ? part2 + col : nullptr, nblk, 66, red);
+    if (ph == 0 && col < 66) {
+      if (col < 64) {
+        if (t != 0.f) dconst[col] += t;     // (heads past Htot have no rows: their sum is 0 and is not written)
+      } else {
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) db[(col - 64) * 4 + jj] += t;
+      }
+    }
   }
 }
 
@@ -267,9 +341,14 @@ extern "C" int dph_relpos_table_bwd(const float* dtab, const int64_t* heads, flo
                   max_distance > num_buckets / 4,
               "dph_relpos_table_bwd: bad args");
   const int n = (int)((2 * T - 1) * H);
-  hipLaunchKernelGGL(relpos_table_bwd_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, stream, dtab, heads, dembed,
-                     (int)T, (int)H, (int)Htot, (int)num_buckets, (int)max_distance,
-                     relpos_log_ratio(num_buckets, max_distance));
+  if (deterministic())
+    hipLaunchKernelGGL(relpos_table_bwd_det_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, stream, dtab, heads,
+                       dembed, (int)T, (int)H, (int)Htot, (int)num_buckets, (int)max_distance,
+                       relpos_log_ratio(num_buckets, max_distance));
+  else
+    hipLaunchKernelGGL(relpos_table_bwd_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, stream, dtab, heads,
+                       dembed, (int)T, (int)H, (int)Htot, (int)num_buckets, (int)max_distance,
+                       relpos_log_ratio(num_buckets, max_distance));
   return check_launch("dph_relpos_table_bwd");
 }
 
@@ -283,26 +362,41 @@ extern "C" int dph_wavlm_gate_fwd(const void* x, int64_t ldx, const float* w, co
   return check_launch("dph_wavlm_gate_fwd");
 }
 
-// dx (bf16, ld lddx) is ADDED to; dw [8][64], db [8], dconst [Htot] accumulate;
-// ws = 2*N + 8 + 128*ceil(N/256) floats, N = B*T*H
+// workspace (bytes) of dph_wavlm_gate_bwd, either mode: dz [N][2], dc [N], db0 [8], the per-block dW group rows
+// [nblk][2][64] and (deterministic mode) the per-block dconst / db rows [nblk][66]; N = B*T*H, nblk = ceil(N / 256)
+extern "C" int64_t dph_wavlm_gate_bwd_workspace(int64_t B, int64_t T, int64_t H) {
+  const int64_t N = B * T * H, nblk = cdiv(N, 256);
+  return (3 * N + 8 + nblk * (2 * HDG + 66)) * 4;
+}
+
+// dx (bf16, ld lddx) is ADDED to; dw [8][64], db [8], dconst [Htot] accumulate
 extern "C" int dph_wavlm_gate_bwd(const void* x, int64_t ldx, const float* w, const float* bias, const float* gconst,
                                   const int64_t* heads, const float* dgate, void* dx, int64_t lddx, float* dw,
-                                  float* db, float* dconst, float* ws, int64_t B, int64_t T, int64_t H,
-                                  int64_t head_dim, hipStream_t stream) {
+                                  float* db, float* dconst, float* ws, int64_t ws_bytes, int64_t B, int64_t T,
+                                  int64_t H, int64_t head_dim, hipStream_t stream) {
   DPH_REQUIRE(x && w && bias && gconst && dgate && dx && dw && db && dconst && ws && B > 0 && T > 0 && H > 0 &&
                   head_dim == HDG && ldx % 8 == 0 && lddx % 8 == 0 && ldx / HDG <= 64,
               "dph_wavlm_gate_bwd: bad args (head_dim 64, <= 64 heads)");
+  DPH_REQUIRE(ws_bytes >= dph_wavlm_gate_bwd_workspace(B, T, H), "dph_wavlm_gate_bwd: workspace too small");
   GateArgs a{reinterpret_cast<const bf16_t*>(x), ldx, w, bias, gconst, heads, B, T, H};
   const int64_t N = B * T * H;
   const int nblk = (int)cdiv(N, 256);
+  const bool det = deterministic();
   float* dz = ws;
-  float* db0 = ws + 2 * N;          // [8] (entries 0 and 4 used)
+  float* dc = ws + 2 * N;           // [N] (deterministic mode)
+  float* db0 = dc + N;              // [8] (entries 0 and 4 used)
   float* part = db0 + 8;            // [nblk][2][64] per-block group rows of dW
-  zero_async(db0, 8 * sizeof(float), stream);
+  float* part2 = part + (int64_t)nblk * 2 * HDG;   // [nblk][66] (deterministic mode)
+  if (!det) zero_async(db0, 8 * sizeof(float), stream);
   hipLaunchKernelGGL(wavlm_gate_bwd_kernel, dim3((unsigned)cdiv(N, 256)), dim3(256), 0, stream, a, dgate,
-                     reinterpret_cast<bf16_t*>(dx), lddx, dz, db0, dconst);
-  hipLaunchKernelGGL(wavlm_gate_wgrad_kernel, dim3((unsigned)nblk), dim3(256), 0, stream, a, dz, part);
-  hipLaunchKernelGGL(wavlm_gate_finish_kernel, dim3((unsigned)cdiv(nblk, FIN_CHUNK)), dim3(128), 0, stream, dw, db,
-                     part, nblk, db0);
+                     reinterpret_cast<bf16_t*>(dx), lddx, dz, db0, dconst, det ? dc : nullptr);
+  hipLaunchKernelGGL(wavlm_gate_wgrad_kernel, dim3((unsigned)nblk), dim3(256), 0, stream, a, dz, part,
+                     (const float*)dc, det ? part2 : nullptr);
+  if (det)
+    hipLaunchKernelGGL(wavlm_gate_finish_det_kernel, dim3(7), dim3(32 * DET_PH), 0, stream, dw, db, dconst, part,
+                       part2, nblk);
+  else
+    hipLaunchKernelGGL(wavlm_gate_finish_kernel, dim3((unsigned)cdiv(nblk, FIN_CHUNK)), dim3(128), 0, stream, dw, db,
+                       part, nblk, db0);
   return check_launch("dph_wavlm_gate_bwd");
 }

@@ -3,6 +3,7 @@
 
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 namespace dph {
 namespace {
@@ -31,10 +32,32 @@ int check_launch(const char* what) {
   }
   return DPH_OK;
 }
+
+// ---- deterministic mode ----------------------------------------------------------------------
+// Process-wide switch read by the launch code of every kernel that reduces float partials across blocks
+// (bias / LayerNorm-affine column sums, mask gradients, conv0 sums, head-mask sums, WavLM diagonal sums): on, they
+// write per-block partial slabs summed in a fixed order instead of same-address float atomics, so two runs of a
+// step (eager or a HIP-graph replay) give bitwise identical gradients.  Initial value: DPH_DETERMINISTIC (default
+// on); set before a graph capture (a captured graph keeps the kernels it recorded).
+namespace {
+int g_det = -1;
+}
+bool deterministic() {
+  if (g_det < 0) {
+    const char* e = getenv("DPH_DETERMINISTIC");
+    g_det = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_det != 0;
+}
 }  // namespace dph
 
 extern "C" const char* dph_last_error(void) { return dph::g_err; }
-extern "C" int dph_abi_version(void) { return 19; }
+extern "C" int dph_abi_version(void) { return 20; }
+extern "C" int dph_set_deterministic(int on) {
+  dph::g_det = on ? 1 : 0;
+  return DPH_OK;
+}
+extern "C" int dph_get_deterministic(void) { return dph::deterministic() ? 1 : 0; }
 
 // Point every kernel's RNG epoch at the device word `epoch` (uint64, device memory) on the current
 // device, or detach it (NULL: seeds are used as passed).  Not stream-ordered: call outside any

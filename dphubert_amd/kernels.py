@@ -103,6 +103,34 @@ SPAN_WORK = {
 }
 SPAN_HINT = {}
 
+# GEMM role tag (bench.py's mfma_util_attn_ffn: north_star's utilisation bar over masked attention + FFN): the
+# GEMMs launched inside a ``role("ffn")`` block -- FFN1 / FFN2 forward, their input and weight gradients -- are
+# recorded with that role by the LaunchProfiler
+ROLE = [None]
+
+
+class role:
+    def __init__(self, name):
+        self.name = name
+
+    def __enter__(self):
+        self.prev, ROLE[0] = ROLE[0], self.name
+        return self
+
+    def __exit__(self, *exc):
+        ROLE[0] = self.prev
+
+
+def tagged(name):
+    """Decorator: run the function inside ``role(name)``."""
+    def deco(fn):
+        def wrap(*a, **kw):
+            with role(name):
+                return fn(*a, **kw)
+        wrap.__name__, wrap.__doc__ = fn.__name__, fn.__doc__
+        return wrap
+    return deco
+
 
 class LaunchProfiler:
     """Brackets every GEMM launch with HIP events on the launch stream (used by bench.py to
@@ -160,10 +188,23 @@ class LaunchProfiler:
             d["work"] += work
         return out
 
+    def role_summary(self):
+        """{role: {launches, ms, flops}} of the GEMM launches recorded inside a ``role`` block."""
+        torch.cuda.synchronize()
+        out = {}
+        for name, flops, e0, e1, byt, rl in self.records:
+            if rl is None:
+                continue
+            d = out.setdefault(rl, {"launches": 0, "ms": 0.0, "flops": 0.0})
+            d["launches"] += 1
+            d["ms"] += e0.elapsed_time(e1)
+            d["flops"] += flops
+        return out
+
     def summary(self):
         torch.cuda.synchronize()
         out = {}
-        for name, flops, e0, e1, byt in self.records:
+        for name, flops, e0, e1, byt, _rl in self.records:
             ms = e0.elapsed_time(e1)
             d = out.setdefault(name, {"launches": 0, "ms": 0.0, "flops": 0.0, "bytes": 0.0})
             d["launches"] += 1
@@ -244,7 +285,7 @@ def gemm(A: DphMat, B: DphMat, Cm: DphMat, M: int, N: int, K: int, *, a_kcontig:
         for t, rw in ((pre_out, 1), (aux_in, 1), (residual, 1)):
             if t is not None:
                 byt += rw * batch * M * N * t.element_size()
-        prof.records.append((name, 2.0 * M * N * K * batch, e0, e1, byt))
+        prof.records.append((name, 2.0 * M * N * K * batch, e0, e1, byt, ROLE[0]))
     return ws  # keep alive until the stream consumes it (caching allocator is stream-ordered)
 
 
@@ -384,5 +425,5 @@ def linear_wgrad_grouped(items: Sequence, accumulate: bool = True) -> Optional[t
         name = _variant(args)
         if prof.by_shape:
             name = f"{name} grouped M={N} N={K} K={M} b={n} s={splits}"
-        prof.records.append((name, 2.0 * M * N * K * n, e0, e1, n * (2.0 * (M * N + M * K) + 8.0 * N * K)))
+        prof.records.append((name, 2.0 * M * N * K * n, e0, e1, n * (2.0 * (M * N + M * K) + 8.0 * N * K), ROLE[0]))
     return ws

@@ -60,6 +60,12 @@ def colsum_ws(rows: int, cols: int, dev):
     return _ws(_lib.lib().dph_colsum_workspace(rows, cols), dev)
 
 
+def rb_ws(rows: int, cols: int, dev):
+    """Workspace of the per-row-block column reductions (GELU-mask / branch backward): their fixed-order partial
+    slab in deterministic mode (include/dphubert_hip.h dph_rowblock_workspace)."""
+    return _ws(_lib.lib().dph_rowblock_workspace(rows, cols), dev)
+
+
 # ---------------------------------------------------------------------------
 # counter-based seeds (dropout / HardConcrete noise)
 # ---------------------------------------------------------------------------
@@ -485,7 +491,7 @@ class grouped_wgrads:
                 self.queues = {}
 
     def add(self, dy, x, dw, params, post=None):
-        key = (tuple(dy.shape), tuple(x.shape), dy.device)
+        key = (tuple(dy.shape), tuple(x.shape), dy.device, K.ROLE[0])
         items = self.queues.setdefault(key, [])
         for p in params:
             p._dph_hold = True
@@ -500,7 +506,7 @@ class grouped_wgrads:
         # (DPH_WGRAD_STREAM=1 with DPH_WGRAD_SCOPE=group / all), beside the rest of the backward
         side_ok = all(post is None for *_, post in items)
         ins = [t for dy, x, *_ in items for t in (dy, x)]
-        with wgrad_side(*ins, enable=side_ok, scope="group"):
+        with wgrad_side(*ins, enable=side_ok, scope="group"), K.role(key[3]):
             ws = K.linear_wgrad_grouped([(dy, x, dw) for dy, x, dw, _, _ in items], accumulate=True)
             del ws
             for *_, params, post in items:
@@ -1043,7 +1049,7 @@ class FrontendFn(torch.autograd.Function):
         dz = torch.empty_like(dy)
         dm_raw = zeros_f32(Op, dev)
         call("dph_gelu_mask_bwd", ptr(dy), ptr(ctx.zs[-1]), ptr(ctx.cms[-1]), ptr(dz), ptr(dm_raw), B * Ls[-1], Op,
-             _s())
+             *rb_ws(B * Ls[-1], Op, dev), _s())
         if masks[-1] is not None:
             g_m[-1] = dm_raw[:O] * dummy
         keep = []
@@ -1083,10 +1089,10 @@ class FrontendFn(torch.autograd.Function):
                 nxt = torch.empty(B * Ls[i - 1], Cinp, dtype=BF16, device=dev)
                 if i > 1:
                     call("dph_col2im_gelu_bwd", ptr(dcols), B, Ls[i], Ls[i - 1], Cinp, k, s, ptr(ctx.zs[i - 1]),
-                         ptr(ctx.cms[i - 1]), ptr(nxt), ptr(dmk), _s())
+                         ptr(ctx.cms[i - 1]), ptr(nxt), ptr(dmk), *rb_ws(B * Ls[i - 1], Cinp, dev), _s())
                 else:
                     call("dph_col2im_gelu_bwd", ptr(dcols), B, Ls[i], Ls[i - 1], Cinp, k, s, None, None, ptr(nxt),
-                         None, _s())
+                         None, None, 0, _s())
             if i > 1 and masks[i - 1] is not None:
                 g_m[i - 1] = dmk[:Cin]
             dz = nxt
@@ -1103,7 +1109,7 @@ class FrontendFn(torch.autograd.Function):
             dw0, dgw, dgb = zeros_f32((C0p,) + tuple(ws_[0].shape[1:]), dev), zeros_f32(C0p, dev), zeros_f32(C0p, dev)
             go.bufs[id(pws[0])], go.bufs[id(pgn_w)], go.bufs[id(pgn_b)] = dw0[:C0], dgw[:C0], dgb[:C0]
         dm0 = zeros_f32(C0p, dev) if masks[0] is not None else None
-        wsb = torch.empty((_lib.lib().dph_conv0_gn_bwd_workspace(B, C0p) + 3) // 4, dtype=F32, device=dev)
+        wsb = torch.empty((_lib.lib().dph_conv0_gn_bwd_workspace(B, S, C0p) + 3) // 4, dtype=F32, device=dev)
         call("dph_conv0_gn_bwd", ptr(wave), B, S, ptr(w0), C0p, k0, s0, ptr(g0), ptr(b0), ptr(m0),
              ptr(mean), ptr(rstd), ptr(dz), ptr(dw0), ptr(dgw), ptr(dgb), ptr(dm0), ptr(wsb), wsb.numel() * 4, _s())
         g_m[0] = dm0[:C0] if dm0 is not None else None
@@ -1203,7 +1209,7 @@ class FrontendLNFn(torch.autograd.Function):
         dh = torch.empty(rows, C, dtype=BF16, device=dev)
         dm = zeros_f32(C, dev)
         call("dph_gelu_mask_bwd", ptr(dy.contiguous()), ptr(ctx.hs[-1]), ptr(ctx.cms[-1]), ptr(dh), ptr(dm), rows, C,
-             _s())
+             *rb_ws(rows, C, dev), _s())
         if ctx.has_mask[-1]:
             g_m[-1] = dm * dummy
         keep = []
@@ -1227,7 +1233,8 @@ class FrontendLNFn(torch.autograd.Function):
                 call("dph_colsum", ptr(dz), ptr(dbias), rows, C, *colsum_ws(rows, C, dev), _s())
             if i == 0:
                 dw, direct = go.buf(w)
-                call("dph_conv0_bwd", ptr(wave), B, S, C, k, s, ptr(dz), ptr(dw), None, _s())
+                call("dph_conv0_bwd", ptr(wave), B, S, C, k, s, ptr(dz), ptr(dw), None,
+                     *_ws(_lib.lib().dph_conv0_bwd_workspace(B, S, C), dev), _s())
                 break
             Cin = layers[i - 1][0]
             dwp = torch.empty(C, k * Cin, dtype=F32, device=dev)
@@ -1253,7 +1260,7 @@ class FrontendLNFn(torch.autograd.Function):
                            b_kcontig=False)
                 dh = torch.empty(B * Ls[i - 1], Cin, dtype=BF16, device=dev)
                 call("dph_col2im_gelu_bwd", ptr(dcols), B, Ls[i], Ls[i - 1], Cin, k, s, ptr(ctx.hs[i - 1]),
-                     ptr(ctx.cms[i - 1]), ptr(dh), ptr(dmk), _s())
+                     ptr(ctx.cms[i - 1]), ptr(dh), ptr(dmk), *rb_ws(B * Ls[i - 1], Cin, dev), _s())
             if ctx.has_mask[i - 1]:
                 g_m[i - 1] = dmk
         # the conv0 weight gradient went through dph_conv0_bwd, which accumulates (needs a zeroed
@@ -1303,7 +1310,7 @@ class FeatureProjectionFn(torch.autograd.Function):
         db, _ = go.buf(p_b)
         lens = cfg["lengths"]
         call("dph_branch_bwd", ptr(dout), ptr(dpre), M, D, cfg["p"], ctx.seed, None, ptr(lens),
-             cfg["T"] if lens is not None else 0, ptr(db), None, None, _s())
+             cfg["T"] if lens is not None else 0, ptr(db), None, None, *rb_ws(M, D, dev), _s())
         dw, direct = go.buf(p_w, zero=False)
         ws = K.linear_wgrad(dpre, xn, dw, accumulate=direct, k_in=C)
         dxn = K.linear_dgrad(dpre, img, w_t=t_image(img))
@@ -1400,7 +1407,7 @@ class PosConvFn(torch.autograd.Function):
         elif cfg["p"] > 0:   # pre-norm Transformer (components.py:1283 flag): no LayerNorm here, dropout only
             h = torch.empty(M, D, dtype=F32, device=dev)
             call("dph_branch_bwd_f32", ptr(s0), ptr(h), 1, M, D, cfg["p"], seed, None, None, 0, None, None, None,
-                 _s())
+                 None, 0, _s())
         else:
             h = s0
         if need:
@@ -1431,10 +1438,10 @@ class PosConvFn(torch.autograd.Function):
         else:   # (the fp32 residual stream's gradient)
             dh = dh if dh.dtype == F32 else dh.float()
             call("dph_branch_bwd_f32", ptr(dh), ptr(ds0), 0, M, D, cfg["p"], ctx.seed, None, None, 0, None, None,
-                 None, _s())
+                 None, None, 0, _s())
         # (+64 elements of slack: the weight gradient below reads 64 columns from group g's first one, see there)
         dz = torch.empty(M * D + 64, dtype=BF16, device=dev)[:M * D].view(M, D)
-        call("dph_gelu_mask_bwd", ptr(ds0), ptr(z), None, ptr(dz), None, M, D, _s())
+        call("dph_gelu_mask_bwd", ptr(ds0), ptr(z), None, ptr(dz), None, M, D, None, 0, _s())
         db, _ = go.buf(p_bias)
         call("dph_colsum", ptr(dz), ptr(db), M, D, *colsum_ws(M, D, dev), _s())
         # input gradient: transposed conv = same batched GEMM over a re-padded dz with flipped weights
@@ -1524,6 +1531,7 @@ def _ffn_interm_bwd(dy, sv, db1, dmask, cfg, F_):
 
 
 
+@K.tagged("ffn")
 def _ffn_forward(cfg, xin, w1, b1, w2, b2, im, lmf, resid, need, sv):
     """FeedForward (components.py:726-748) + dropout + layer mask + residual: resid + drop(FFN(xin)) * lmf.
 
@@ -1583,6 +1591,7 @@ def _ffn_forward(cfg, xin, w1, b1, w2, b2, im, lmf, resid, need, sv):
     return out
 
 
+@K.tagged("ffn")
 def _ffn_backward(cfg, sv, dy, xin, pr, go, dmask, residual=None):
     """Backward of _ffn_forward from dy = d(FFN2 output) (after the output dropout / layer mask): the W2 / b1 / W1
     gradients into ``go``'s buffers, the intermediate-mask gradient into ``dmask`` [F] (None: no intermediate mask,
@@ -1782,7 +1791,7 @@ class EncoderLayerFn(torch.autograd.Function):
             db2, _ = go.buf(pr["b2"])
             g["lmf"] = z(1) if has_lmf else None
             call("dph_branch_bwd_f32", ptr(dout), ptr(dy), 0, M, D, cfg["p_drop"], sv["seed_o"], ptr(lmf), None, 0,
-                 ptr(db2), ptr(sv["y_pre"]) if has_lmf else None, ptr(g["lmf"]), _s())
+                 ptr(db2), ptr(sv["y_pre"]) if has_lmf else None, ptr(g["lmf"]), *rb_ws(M, D, dev), _s())
             F_ = sv["F"]
             g["im"] = z(F_) if has_im else None
             dxn2 = _ffn_backward(cfg, sv, dy, xn2, pr, go, g["im"])
@@ -1799,13 +1808,14 @@ class EncoderLayerFn(torch.autograd.Function):
             dbo, _ = go.buf(pr["bo"])
             g["lma"] = z(1) if has_lma else None
             call("dph_branch_bwd_f32", ptr(ds1), ptr(da), 0, M, D, cfg["p_drop"], sv["seed_d"], ptr(lma), None, 0,
-                 ptr(dbo), ptr(sv["a_pre"]) if has_lma else None, ptr(g["lma"]), _s())
+                 ptr(dbo), ptr(sv["a_pre"]) if has_lma else None, ptr(g["lma"]), *rb_ws(M, D, dev), _s())
             dwo, direct = go.buf(pr["wo"], zero=False)
             k3 = _layer_wgrad(da, sv["o_m"], dwo, direct, (pr["wo"],))
             do_m = K.linear_dgrad(da, sv["Wo"], w_t=t_image(sv["Wo"]))
             Dvec = torch.empty(B * H * T, dtype=F32, device=dev)
             g["hm"] = z(H) if has_hm else None
-            call("dph_attention_bwd_prep", ptr(do_m), ptr(sv["o_u"]), ptr(hm), ptr(Dvec), ptr(g["hm"]), B, T, H, _s())
+            call("dph_attention_bwd_prep", ptr(do_m), ptr(sv["o_u"]), ptr(hm), ptr(Dvec), ptr(g["hm"]), B, T, H,
+                 *_ws(_lib.lib().dph_attention_bwd_prep_workspace(B, T, H), dev), _s())
             dqkv = torch.empty_like(sv["qkv"])
             wl_g = EncoderLayerFn._attention_bwd(ctx, cfg, sv, do_m, hm, Dvec, dqkv)
             dbqkv, _ = go.buf(pr["bq"], pr["bk"], pr["bv"])
@@ -1870,7 +1880,8 @@ class EncoderLayerFn(torch.autograd.Function):
         dtab = torch.zeros(wl["rel_tab"].shape, dtype=F32, device=dev)
         call("dph_attention_bwd_relpos", ptr(sv["qkv"]), ptr(do_m), ptr(hm), ptr(sv["lse"]), ptr(Dvec), ptr(dqkv),
              ptr(cfg["lengths"]), ptr(wl["rel_tab"]), ptr(sv["gate"]), ptr(dgate), ptr(dtab), B, T, H,
-             cfg["head_dim"] ** -0.5, cfg["p_attn"], sv["seed_a"], ptr(getattr(ctx, "attn_keep", None)), _s())
+             cfg["head_dim"] ** -0.5, cfg["p_attn"], sv["seed_a"], ptr(getattr(ctx, "attn_keep", None)),
+             *_ws(_lib.lib().dph_attention_bwd_relpos_workspace(B, T, H), dev), _s())
         return dgate, dtab
 
     @staticmethod
@@ -1885,10 +1896,10 @@ class EncoderLayerFn(torch.autograd.Function):
         dgb, _ = go.buf(wl["gb"])
         dgc, _ = go.buf(wl["gc"])
         N = B * T * H
-        ws = torch.empty(2 * N + 8 + 128 * ((N + 255) // 256), dtype=F32, device=dx_att.device)
+        ws = torch.empty(_lib.lib().dph_wavlm_gate_bwd_workspace(B, T, H) // 4, dtype=F32, device=dx_att.device)
         call("dph_wavlm_gate_bwd", ptr(x_att), x_att.shape[1], ptr(wl["gw"]), ptr(wl["gb"]), ptr(wl["gc"]),
              ptr(wl["heads"]), ptr(dgate), ptr(dx_att), dx_att.shape[1], ptr(dgw), ptr(dgb), ptr(dgc), ptr(ws),
-             B, T, H, 64, _s())
+             ws.numel() * 4, B, T, H, 64, _s())
         wl["dtab"] = dtab
 
     @staticmethod
@@ -1949,7 +1960,8 @@ class EncoderLayerFn(torch.autograd.Function):
             do_m = K.linear_dgrad(da, sv["Wo"], w_t=t_image(sv["Wo"]))
             Dvec = torch.empty(B * H * T, dtype=F32, device=dev)
             g["hm"] = z(H) if has_hm else None
-            call("dph_attention_bwd_prep", ptr(do_m), ptr(sv["o_u"]), ptr(hm), ptr(Dvec), ptr(g["hm"]), B, T, H, _s())
+            call("dph_attention_bwd_prep", ptr(do_m), ptr(sv["o_u"]), ptr(hm), ptr(Dvec), ptr(g["hm"]), B, T, H,
+                 *_ws(_lib.lib().dph_attention_bwd_prep_workspace(B, T, H), dev), _s())
             dqkv = torch.empty_like(sv["qkv"])
             wl_g = EncoderLayerFn._attention_bwd(ctx, cfg, sv, do_m, hm, Dvec, dqkv)
             dbqkv, _ = go.buf(pr["bq"], pr["bk"], pr["bv"])
@@ -2061,7 +2073,7 @@ class DistillProjLossFn(torch.autograd.Function):
         db = [go.buf(pw[2 * p + 1])[0] for p in range(P)]
         if ctx.pre is not None:
             # through the heads' GELU: dz = ds * gelu'(pre), in place
-            call("dph_gelu_mask_bwd", ptr(ds), ptr(ctx.pre), None, ptr(ds), None, L * M, Dt, _s())
+            call("dph_gelu_mask_bwd", ptr(ds), ptr(ctx.pre), None, ptr(ds), None, L * M, Dt, None, 0, _s())
             ctx.pre = None
         # predlayer: every head reads the same (last) hidden state -> one chained input gradient
         shared = cfg.get("shared_input", False)

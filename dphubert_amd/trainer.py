@@ -22,6 +22,7 @@ import warnings
 from typing import List, Optional
 
 import torch
+import torch.distributed as dist
 import torch.nn as nn
 
 from . import ops
@@ -438,9 +439,20 @@ class Trainer:
         verify_replicas(self.module, process_group=self.reducer.group)
 
     def _plan(self, batch):
-        """World size > 1: the weight-gradient group from the step's frames (B x ~S / 320) and the bucket layout."""
+        """World size > 1: the weight-gradient group from the step's frames (B x ~S / 320) and the bucket layout.
+
+        Every rank must plan the SAME group: the group decides when the held-back encoder weight gradients land,
+        hence the order in which buckets become ready and their collectives are issued; ranks issuing buckets in
+        different orders would pair different buffers in one all-reduce (a hang, or gradients summed across the
+        wrong buckets).  The bucketed train loader gives each rank its own padded length, so the plan runs on the
+        largest frame count over the ranks (one MAX all-reduce of a scalar, once)."""
         self._plan_group = False
         frames = batch[0].shape[0] * batch[0].shape[1] / 320.0
+        if self.reducer.world > 1 and dist.is_initialized():
+            dev = batch[0].device if self.reducer.backend == "nccl" else torch.device("cpu")
+            t = torch.tensor([frames], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.reducer.group)
+            frames = float(t.item())
         proj = list(self.module.distill_linear_projs.parameters())
         bus = float(os.environ.get("DPH_XGMI_BUS_GBPS", XGMI_BUS_GBPS))
         cb = 2 if self.reducer.comm_dtype == torch.bfloat16 else 4

@@ -34,6 +34,17 @@ extern "C" {
 const char* dph_last_error(void);
 int dph_abi_version(void);
 
+/* Deterministic mode (process-wide, read at launch time; initial value from the environment variable
+ * DPH_DETERMINISTIC, default on): every reduction of float partials across blocks -- bias / LayerNorm-affine
+ * column sums, mask gradients, conv0 GroupNorm sums, head-mask sums, WavLM relative-position sums -- writes
+ * per-block partials to its workspace and sums them in a fixed order, so repeated runs of a step (eager or a
+ * HIP-graph replay) produce bitwise identical gradients (the reproducibility contract of the reference's
+ * pl.seed_everything, distill.py:30).  Off: same-address float atomics (last-bit run-to-run noise).  A captured
+ * graph keeps the kernels it recorded: set the mode before capturing.  The entry points that take a workspace
+ * size it with their *_workspace function for either mode. */
+int dph_set_deterministic(int on);
+int dph_get_deterministic(void);
+
 /* ------------------------------------------------------------------------ *
  * Generic bf16 MFMA GEMM with fused epilogues.
  *   C[z][m][n] = epi( alpha * sum_k A[z][m][k] * B[z][k][n] )
@@ -90,12 +101,13 @@ typedef struct DphGemmArgs {
   void* pre_out;          /* bf16, pre-activation (after bias)                */
   const void* aux_in;     /* bf16, GELU_BWD pre-activation input              */
   const void* residual;   /* bf16, added last                                 */
-  float* colsum_out;      /* [N] fp32 atomics: column sums of the stored value */
-  float* colsum_aux;      /* [N] fp32 atomics: GELU_BWD mask gradient          */
+  float* colsum_out;      /* [N] += column sums of the stored value              */
+  float* colsum_aux;      /* [N] += GELU_BWD mask gradient                        */
   const int64_t* row_len; /* zero rows with (m % len_rows) >= row_len[m / len_rows] */
   int64_t len_rows;
   int64_t drop_row_offset;/* dropout element index = (drop_row_offset + m)*N + n (per batch z adds z*M*N) */
-  void* workspace;        /* split-K partials                                  */
+  void* workspace;        /* split-K partials; with column sums (batch 1): >= 2*ceil(M/64)*N fp32 of
+                           * per-tile partial rows, summed after the GEMM (required in deterministic mode) */
   int64_t workspace_bytes;
   int64_t colsum_n;       /* column sums only for n < colsum_n (0: all N); padded-width operands */
   int64_t flags;          /* DPH_GEMM_* bits below                                */
@@ -200,7 +212,8 @@ int dph_layernorm_bwd(const void* dy, const void* x, const float* xscale, const 
                       const float* branch_smask, float* branch_colsum, const void* branch_pre,
                       float* branch_sdot, float* ws, int64_t ws_bytes, hipStream_t stream);
 /* workspace (bytes) of dph_layernorm_bwd(_ld): per-block column-partial slab, reduced by a second
- * kernel (same-address atomics from hundreds of blocks serialise at the memory side) */
+ * kernel (same-address atomics from hundreds of blocks serialise at the memory side), + the per-block
+ * branch_sdot partials of deterministic mode */
 int64_t dph_layernorm_bwd_workspace(int64_t rows, int64_t D);
 
 /* the same over rows of stride ld >= D (ld % 4 == 0): columns [D, ld) are row padding (pruned
@@ -263,9 +276,12 @@ int dph_attention_fwd(const void* qkv, void* o_unmasked, void* o_masked, float* 
  * the backward reads them instead of re-hashing (NULL on both sides: regenerated from (seed, element)) */
 int64_t dph_attention_keep_bytes(int64_t B, int64_t T, int64_t H);
 /* backward prep: rowdot[b][h][t] = sum_d do_m*o_u (o_u fp32) ; D = head_mask*rowdot ;
- * dhead_mask[h] += sum rowdot */
+ * dhead_mask[h] += sum rowdot.  ws (deterministic mode with dhead_mask): the per-row-block head sums,
+ * dph_attention_bwd_prep_workspace(B, T, H) bytes (may be NULL otherwise) */
+int64_t dph_attention_bwd_prep_workspace(int64_t B, int64_t T, int64_t H);
 int dph_attention_bwd_prep(const void* do_masked, const void* o_unmasked, const float* head_mask, float* Dvec,
-                           float* dhead_mask, int64_t B, int64_t T, int64_t H, hipStream_t stream);
+                           float* dhead_mask, int64_t B, int64_t T, int64_t H, float* ws, int64_t ws_bytes,
+                           hipStream_t stream);
 /* dq|dk|dv into dqkv [B*T][3*H*64] (bf16) */
 int dph_attention_bwd(const void* qkv, const void* do_masked, const float* head_mask, const float* lse,
                       const float* Dvec, void* dqkv, const int64_t* key_len, int64_t B, int64_t T, int64_t H,
@@ -286,11 +302,14 @@ int dph_attention_fwd_relpos(const void* qkv, void* o_unmasked, void* o_masked, 
                              int64_t H, float scale, float dropout_p, uint64_t seed, void* keep_bits,
                              hipStream_t stream);
 /* its backward: dqkv as dph_attention_bwd, plus dgate [B][H][T] (written) = sum_k dS*rel_tab and
- * drel_tab [H][2T-1] (ACCUMULATED, zero it first) = diagonal sums of dS*gate */
+ * drel_tab [H][2T-1] (ACCUMULATED, zero it first) = diagonal sums of dS*gate.  ws (deterministic mode): the
+ * per-query-block diagonal sums, dph_attention_bwd_relpos_workspace(B, T, H) bytes (may be NULL otherwise) */
+int64_t dph_attention_bwd_relpos_workspace(int64_t B, int64_t T, int64_t H);
 int dph_attention_bwd_relpos(const void* qkv, const void* do_masked, const float* head_mask, const float* lse,
                              const float* Dvec, void* dqkv, const int64_t* key_len, const float* rel_tab,
                              const float* gate, float* dgate, float* drel_tab, int64_t B, int64_t T, int64_t H,
-                             float scale, float dropout_p, uint64_t seed, const void* keep_bits, hipStream_t stream);
+                             float scale, float dropout_p, uint64_t seed, const void* keep_bits, float* ws,
+                             int64_t ws_bytes, hipStream_t stream);
 /* rel_tab[h][r] = embed[bucket(r-(T-1))][heads[h]] (embed [num_buckets][Htot] fp32; heads [H] int64 or NULL =
  * identity); buckets [2T-1] int64 (optional) receives the bucket index table; either output may be NULL */
 int dph_relpos_table(const float* embed, const int64_t* heads, float* rel_tab, int64_t* buckets, int64_t T,
@@ -304,10 +323,11 @@ int dph_wavlm_gate_fwd(const void* x, int64_t ldx, const float* w, const float* 
                        const int64_t* heads, float* gate, int64_t B, int64_t T, int64_t H, int64_t head_dim,
                        hipStream_t stream);
 /* its backward: dx (bf16, ld lddx) += the gate's input gradient; dw [8][64], db [8], dconst [Htot] ACCUMULATE;
- * ws: 2*N + 8 + 128*ceil(N/256) floats, N = B*T*H */
+ * ws: dph_wavlm_gate_bwd_workspace(B, T, H) bytes */
+int64_t dph_wavlm_gate_bwd_workspace(int64_t B, int64_t T, int64_t H);
 int dph_wavlm_gate_bwd(const void* x, int64_t ldx, const float* w, const float* bias, const float* gconst,
                        const int64_t* heads, const float* dgate, void* dx, int64_t lddx, float* dw, float* db,
-                       float* dconst, float* ws, int64_t B, int64_t T, int64_t H, int64_t head_dim,
+                       float* dconst, float* ws, int64_t ws_bytes, int64_t B, int64_t T, int64_t H, int64_t head_dim,
                        hipStream_t stream);
 
 /* ------------------------------------------------------------------------ *
@@ -320,8 +340,9 @@ int dph_wavlm_gate_bwd(const void* x, int64_t ldx, const float* w, const float* 
 int dph_conv0_gn_fwd(const float* wave, int64_t B, int64_t S, const float* w, int64_t C, int64_t k0, int64_t s0,
                      const float* gamma, const float* beta, const float* mask, void* y, float* mean, float* rstd,
                      float* ws, int64_t ws_bytes, hipStream_t stream);
-/* backward scratch: per-(b,c) partial sums (fp32) + per-utterance waveform Gram matrix (fp64) */
-int64_t dph_conv0_gn_bwd_workspace(int64_t B, int64_t C);
+/* backward scratch: per-(b,c) partial sums (fp32) + per-utterance waveform Gram matrix (fp64) + (deterministic
+ * mode) the per-(utterance, time block) partials, reduced in block order */
+int64_t dph_conv0_gn_bwd_workspace(int64_t B, int64_t S, int64_t C);
 int dph_conv0_gn_bwd(const float* wave, int64_t B, int64_t S, const float* w, int64_t C, int64_t k0, int64_t s0,
                      const float* gamma, const float* beta, const float* mask, const float* mean, const float* rstd,
                      const void* dy, float* dw, float* dgamma, float* dbeta, float* dmask, float* ws,
@@ -331,21 +352,28 @@ int dph_conv0_fwd(const float* wave, int64_t B, int64_t S, const float* w, const
                   int64_t k0, int64_t s0, void* y, hipStream_t stream);
 
 /* its backward (dz = gradient of the conv0 output, LN/GELU/mask backward already applied):
- * dw[c][j] += sum dz[b][t][c] * x[b][s0*t+j], dbias[c] += sum dz (dbias may be NULL); accumulates */
+ * dw[c][j] += sum dz[b][t][c] * x[b][s0*t+j], dbias[c] += sum dz (dbias may be NULL); accumulates.
+ * ws (deterministic mode): dph_conv0_bwd_workspace(B, S, C) bytes of per-(utterance, time block) partials */
+int64_t dph_conv0_bwd_workspace(int64_t B, int64_t S, int64_t C);
 int dph_conv0_bwd(const float* wave, int64_t B, int64_t S, int64_t C, int64_t k0, int64_t s0, const void* dz,
-                  float* dw, float* dbias, hipStream_t stream);
+                  float* dw, float* dbias, float* ws, int64_t ws_bytes, hipStream_t stream);
 /* y = GELU(h) * mask[c] on a dense bf16 [rows][C] tensor (C % 8 == 0; mask may be NULL):
  * layer_norm-mode conv layers after their LayerNorm (components.py:110-114) */
 int dph_gelu_mask_fwd(const void* h, const float* mask, void* y, int64_t rows, int64_t C, hipStream_t stream);
 
 /* Fused col2im + GELU/mask backward for a strided conv layer (k, s):
  * dy_in[b][t'][c] = sum_{t,j: s*t+j==t'} dcols[b][t][j*C+c]; then, if z_pre != NULL,
- * out = dy_in*mask[c]*gelu'(z_pre), dmask[c] += dy_in*gelu(z_pre); else out = dy_in. */
+ * out = dy_in*mask[c]*gelu'(z_pre), dmask[c] += dy_in*gelu(z_pre); else out = dy_in.
+ * ws (deterministic mode with dmask): dph_rowblock_workspace(B * Lin, C) bytes (may be NULL otherwise) */
 int dph_col2im_gelu_bwd(const void* dcols, int64_t B, int64_t Lout, int64_t Lin, int64_t C, int64_t k, int64_t s,
-                        const void* z_pre, const float* mask, void* out, float* dmask, hipStream_t stream);
-/* GELU/mask backward on a dense [rows][C] tensor (no col2im) */
+                        const void* z_pre, const float* mask, void* out, float* dmask, float* ws, int64_t ws_bytes,
+                        hipStream_t stream);
+/* GELU/mask backward on a dense [rows][C] tensor (no col2im); ws as above: dph_rowblock_workspace(rows, C) */
 int dph_gelu_mask_bwd(const void* dy, const void* z_pre, const float* mask, void* out, float* dmask, int64_t rows,
-                      int64_t C, hipStream_t stream);
+                      int64_t C, float* ws, int64_t ws_bytes, hipStream_t stream);
+/* workspace (bytes) of the per-row-block column reductions (dph_col2im_gelu_bwd, dph_gelu_mask_bwd,
+ * dph_branch_bwd(_f32)) in deterministic mode */
+int64_t dph_rowblock_workspace(int64_t rows, int64_t cols);
 
 /* pos-conv layout helpers: x [B][T][G*Cg] bf16 -> xg [B][G][pad_front + T + pad_back][Cg] zero-padded */
 int dph_regroup_pad(const void* x, void* xg, int64_t B, int64_t T, int64_t G, int64_t Cg, int64_t pad_front,
@@ -390,15 +418,16 @@ int dph_conv_weight_unpack_grad(const float* g, float* dst, int64_t O, int64_t C
                                 hipStream_t stream);
 /* residual-branch gradient: out = dy*drop(p,seed)*(*smask), padded rows zeroed
  * ((m % len_rows) >= row_len[m/len_rows]); colsum += out; sdot += sum(dy*drop*pre).
+ * ws (deterministic mode with colsum / sdot): dph_rowblock_workspace(rows, cols) bytes.
  * Backward of components.py:273,845 (dropout), :432-434,:744-746 (layer masks), :980 (pad zeroing). */
 int dph_branch_bwd(const void* dy, void* out, int64_t rows, int64_t cols, float p, uint64_t seed, const float* smask,
-                   const int64_t* row_len, int64_t len_rows, float* colsum, const void* pre, float* sdot,
-                   hipStream_t stream);
+                   const int64_t* row_len, int64_t len_rows, float* colsum, const void* pre, float* sdot, float* ws,
+                   int64_t ws_bytes, hipStream_t stream);
 /* the same with an fp32 dy (the pre-norm residual stream's gradient); out is bf16, or fp32 when out_f32 (the
  * pre-norm pos-conv output's dropout, components.py:891, forward) */
 int dph_branch_bwd_f32(const float* dy, void* out, int out_f32, int64_t rows, int64_t cols, float p, uint64_t seed,
                        const float* smask, const int64_t* row_len, int64_t len_rows, float* colsum, const void* pre,
-                       float* sdot, hipStream_t stream);
+                       float* sdot, float* ws, int64_t ws_bytes, hipStream_t stream);
 /* bf16 -> f32 copy / accumulate helpers */
 int dph_add_bf16(const void* a, const void* b, void* out, int64_t n, hipStream_t stream);
 

@@ -382,3 +382,115 @@ def test_wgrad_group_plan_and_bucket_order():
         assert ends[g] <= min(ends.values()) + 1e-9, (bus, g, ends)
         picks[bus] = g
     assert picks[20.0] <= picks[150.0], picks
+
+
+def _plan_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ.pop("DPH_XGMI_BUS_GBPS", None)
+    os.environ.pop("DPH_WGRAD_GROUP", None)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from dphubert_amd.synthetic import HUBERT_BASE_CONFIG
+        from dphubert_amd import trainer as T
+        dm = T.build_distill_module(HUBERT_BASE_CONFIG, distill_layers="0.4,8,12")
+        tr = T.Trainer(dm, clip_norm=10.0)
+        # the bucketed loader hands every rank its own padded length: 16 x 10 s here, 3 x 2 s there
+        B, S = (16, 160000) if rank == 0 else (3, 32000)
+        local = T.plan_wgrad_group(dm.student_model, tr.reducer.buckets, world, B * S / 320.0, T.XGMI_BUS_GBPS, 4,
+                                   list(dm.distill_linear_projs.parameters()))
+        tr._plan((torch.zeros(B, S), None))
+        ready, _, t_end = T.grad_ready_times(dm.student_model, tr.wgrad_plan["frames"], tr.wgrad_group,
+                                             list(dm.distill_linear_projs.parameters()))
+        order = sorted(range(len(tr.reducer.buckets)),
+                       key=lambda bi: (max(ready.get(id(p), t_end) for p in tr.reducer.buckets[bi]), bi))
+        q.put((rank, local, tr.wgrad_group, tr.wgrad_plan["frames"], order))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_wgrad_group_plan_identical_across_ranks():
+    """ranks with different padded lengths must plan the same weight-gradient group -- it
+    decides when the held-back encoder gradients land and so the order of the bucket collectives.  The plan runs on
+    the MAX frame count over the ranks: the group, the frames it was planned on and the predicted bucket launch
+    order agree on both ranks, although each rank's own frames would have picked different groups."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_plan_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict((r, (loc, g, f, o)) for r, loc, g, f, o in (q.get(timeout=300) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0][0] != res[1][0], f"precondition: local plans should differ ({res})"
+    assert res[0][1] == res[1][1] == res[0][0], res       # rank 0 has the larger batch: its plan wins
+    assert res[0][2] == res[1][2] == 16 * 160000 / 320.0
+    assert res[0][3] == res[1][3]
+
+
+def _capture_count_worker(rank, world, port, accum, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from dphubert_amd import ops
+        ops.K.linear_wgrad_grouped = _cpu_grouped
+        net = Net(sink="defer")
+        red = GradReducer(list(net.parameters()), bucket_mb=1e-4, groups=net.groups())
+        calls = []
+        orig = dist.all_reduce
+
+        def counting(t, *a, **kw):
+            calls.append(t.data_ptr())
+            return orig(t, *a, **kw)
+
+        dist.all_reduce = counting
+        per_micro = []
+        for step in range(2):                       # two optimizer steps
+            for m in range(accum):
+                zero, final = m == 0, m + 1 == accum
+                n0 = len(calls)
+                # the body Trainer._gpu_step records into the (zero, final) graph: prepare, backward inside
+                # grouped_wgrads, and on the final micro-step finish() (what the captured graph replays)
+                red.prepare(zero=zero, sync=final)
+                with ops.grouped_wgrads(2):
+                    (net(_inputs(rank, m)) / accum).backward()
+                if final:
+                    red.finish()
+                per_micro.append((step, m, calls[n0:]))
+        dist.all_reduce = orig
+        flat = [f.data_ptr() for f in red.flat]
+        q.put((rank, [(s, m, [flat.index(c) for c in cs]) for s, m, cs in per_micro], len(red.flat)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("accum", [1, 3])
+def test_reducer_collectives_once_per_optimizer_step(accum):
+    """The body of each captured micro-step graph (Trainer._gpu_step: reducer.prepare(zero, sync=final), the
+    backward inside ops.grouped_wgrads, finish() on the final micro-step) issues every bucket's collective exactly
+    once per optimizer step -- none on the non-final micro-steps of gradient accumulation (run_large.sh:54), each
+    bucket once on the final one, in the same order on both ranks -- so the graph replay of that body does too."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_capture_count_worker, args=(r, world, port, accum, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict((r, (pm, nb)) for r, pm, nb in (q.get(timeout=120) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        pm, nb = res[r]
+        assert nb > 1
+        for step, m, buckets in pm:
+            if m + 1 < accum:
+                assert buckets == [], (r, step, m, buckets)
+            else:
+                assert sorted(buckets) == list(range(nb)), (r, step, m, buckets)
+    assert res[0][0] == res[1][0]

@@ -1,10 +1,12 @@
 """Whole-step HIP-graph replay (trainer.Trainer(graphs=True)) against eager steps, and the
 optimizer -> bf16 GEMM image hand-off.
 
-Deterministic configuration (dropout 0, HardConcrete noise injected as device tensors) so that eager
-and replayed steps compute the same math; the remaining differences are fp32 atomics in weight/bias
-gradient reductions (~1e-6 relative).  A short LR schedule (warmup 2, max 10 updates) makes every
-step use a different learning rate, so the device-resident AdamW hyper-parameters are exercised.
+Deterministic configuration (dropout 0, HardConcrete noise injected as device tensors) in the kernel library's
+deterministic mode (include/dphubert_hip.h dph_set_deterministic: every cross-block float reduction in a fixed
+order, no float atomics), so eager and replayed steps compute the same math in the same order: a replayed
+trajectory must equal the eager one BITWISE -- every loss, every parameter after every optimizer step -- and two
+eager runs must equal each other.  A short LR schedule (warmup 2, max 10 updates) makes every step use a different
+learning rate, so the device-resident AdamW hyper-parameters are exercised.
 """
 
 import copy
@@ -102,16 +104,23 @@ def test_optimizer_updates_reach_gemm_images():
         assert torch.equal(a, b)
 
 
+@pytest.fixture(autouse=True)
+def _deterministic():
+    from dphubert_amd import _lib
+    prev = _lib.deterministic()
+    _lib.set_deterministic(True)
+    yield
+    _lib.set_deterministic(prev)
+
+
 @pytest.mark.parametrize("family,accum", [("hubert", 1), ("wavlm", 1), ("large", 1), ("hubert", 3), ("large", 2)])
 def test_graph_replay_matches_eager(family, accum):
-    """Replayed steps track eager steps as closely as two eager runs track each other (the only
-    run-to-run difference is the fp32 atomic order of gradient reductions, which AdamW's
-    normalisation amplifies on tiny gradients).  accum > 1: first / middle / final micro-step graphs
-    (run_large.sh:54 --accum_grad 3)."""
+    """Replayed steps equal eager steps bitwise (deterministic mode); accum > 1: first / middle / final micro-step
+    graphs (run_large.sh:54 --accum_grad 3)."""
     from dphubert_amd.trainer import Trainer
     batch = _batch()
-    # four eager runs sample the run-to-run spread (tracks_eager_report)
-    eager = [Trainer(_module(family=family), clip_norm=10.0, accum_grad=accum) for _ in range(4)]
+    # two eager runs (run-to-run determinism) and the graph run
+    eager = [Trainer(_module(family=family), clip_norm=10.0, accum_grad=accum) for _ in range(2)]
     gr = Trainer(_module(family=family), clip_norm=10.0, graphs=True, graph_warmup=1, accum_grad=accum)
     le = [[] for _ in eager]
     lg = []
@@ -125,74 +134,49 @@ def test_graph_replay_matches_eager(family, accum):
     assert len(gr._graphs) == min(accum, 3), sorted(gr._graphs)
     assert ea.module.global_step == gr.module.global_step == 1 + 5   # _module() starts at global_step 1
     assert len(set(round(x, 6) for x in lg)) > 1, "replayed steps did not train"
-    _assert_tracks_eager(eager, gr, le, lg)
+    _assert_bitwise(eager, gr, le, lg)
     # the graph replays follow the LR schedule: optimizer and scheduler state agree
     assert ea.optimizer._step == gr.optimizer._step
     for g1, g2 in zip(ea.optimizer.param_groups, gr.optimizer.param_groups):
         assert g1["lr"] == g2["lr"]
 
 
-def tracks_eager_report(eager, gr, le, lg):
-    """Does the graph trainer track the eager ones?  Returns (ok, report lines).
-
-    The eager runs sample the run-to-run spread (fp32 atomic order in gradient reductions, amplified by AdamW on
-    tiny gradients; it is not Gaussian: at a step where some gradient is a cancellation-dominated sum the runs
-    split into two or three clusters, tools/graph_diag.py, profiles/r4_graph_diag_rccl.txt).  The replay is
-    compared with the NEAREST eager run (whole-vector distance) -- one more draw from the same distribution lies
-    within the spread of the others, wherever its cluster -- and must sit within 4x the largest eager-vs-eager
-    difference:
-      * losses: that, plus 1e-3 relative (a stale or missing op in the replay moves the loss by > 1e-2);
-      * each parameter, against ITS nearest eager run (the branches of different parameters' cancellation-dominated
-        sums fall independently: the run nearest over the whole vector can sit in another cluster for one
-        HardConcrete log_alpha -- r4_s44: 0.0123 against 4 x 0.00227 for layer 1's FFN log_alpha, the whole vector
-        5.95e-5 inside its bound): that, or 5e-3 (1-D biases 1e-2: cancellation-heavy column sums); k_proj.bias is left out
-        (its gradient is exactly zero by softmax shift invariance, so Adam turns the atomic-order noise of that
-        zero into +-lr steps);
-      * the whole parameter vector: that, or 1e-4.  The eager runs themselves split into branches ~1e-5 and
-        ~5.4e-5 apart in this configuration (profiles/r4_s25_graph_flake.txt: tools/graph_flake_probe.py, six trials in
-        one process), so four eager runs that all took one branch cannot bound a replay that took the other (r4_s23:
-        5.38e-5 against 4 x 1.21e-5); a stale or missing op in the replay moves the whole vector by > 1e-3."""
-    pe = [dict(t.module.named_parameters()) for t in eager]
-    pg = dict(gr.module.named_parameters())
-    names = [n for n, p in gr.module.named_parameters() if p.requires_grad and not n.endswith("k_proj.bias")]
-    cat = lambda d: torch.cat([d[n].detach().float().flatten().cpu() for n in names])  # noqa: E731
-    vg, ve = cat(pg), [cat(d) for d in pe]
-    pairs = [(i, j) for i in range(len(eager)) for j in range(i + 1, len(eager))]
-    near = min(range(len(eager)), key=lambda i: rel_l2(vg, ve[i]))
+def bitwise_report(eager, gr, le, lg):
+    """Deterministic mode: every eager run and the graph run must produce the same losses and the same parameters
+    bit for bit (every parameter, k_proj.bias included).  Returns (ok, report lines naming each difference)."""
     ok, lines = True, []
-    for s_, b in enumerate(lg):
-        vals = [l[s_] for l in le]
-        if not abs(vals[near] - b) <= 1e-3 * max(1.0, abs(b)) + 4 * (max(vals) - min(vals)):
+    for i, l in enumerate(le[1:], 1):
+        if l != le[0]:
             ok = False
-            lines.append(f"loss step {s_}: graph {b} eager {vals}")
-    for n in names:
-        e = min(rel_l2(pg[n].detach().cpu(), d[n].detach().cpu()) for d in pe)
-        base = max(rel_l2(pe[i][n].detach().cpu(), pe[j][n].detach().cpu()) for i, j in pairs)
-        if not e < max(1e-2 if pg[n].dim() == 1 else 5e-3, 4 * base):
-            ok = False
-            lines.append(f"param {n}: graph-vs-eager {e:.3g} eager spread {base:.3g}")
-    e_all = rel_l2(vg, ve[near])
-    base_all = max(rel_l2(ve[i], ve[j]) for i, j in pairs)
-    ok &= e_all < max(1e-4, 4 * base_all)
-    lines.append(f"whole vector: graph vs nearest eager run ({near}) {e_all:.3g}, largest eager-vs-eager "
-                 f"{base_all:.3g}, eager runs to run 0 {[round(rel_l2(v, ve[0]), 8) for v in ve[1:]]}")
+            lines.append(f"eager run {i} losses {l} != eager run 0 {le[0]}")
+    if lg != le[0]:
+        ok = False
+        lines.append(f"graph losses {lg} != eager {le[0]}")
+    pg = dict(gr.module.named_parameters())
+    for i, t in enumerate(eager):
+        for n, p in t.module.named_parameters():
+            if not torch.equal(p.detach(), pg[n].detach()):
+                ok = False
+                d = (p.detach().float() - pg[n].detach().float()).abs().max().item()
+                lines.append(f"param {n}: eager run {i} vs graph max |diff| {d:.3g}")
+    lines.append(f"{sum(1 for _ in pg)} parameters x {len(eager) + 1} runs compared bitwise; losses {lg}")
     return ok, lines
 
 
-def _assert_tracks_eager(eager, gr, le, lg):
-    ok, lines = tracks_eager_report(eager, gr, le, lg)
-    assert ok, "\n".join(lines + [f"eager losses {le}", f"graph losses {lg}"])
+def _assert_bitwise(eager, gr, le, lg):
+    ok, lines = bitwise_report(eager, gr, le, lg)
+    assert ok, "\n".join(lines[:40])
 
 
 def test_ffn_compaction_switch_under_graphs():
     """A gate whose expected zero fraction crosses Trainer.FFN_COMPACT_MIN_ZERO at a re-evaluation step under graph
     replay (a prune.py run toward 0.75 sparsity reaches it): the stale graphs are dropped, that optimizer step runs
     eagerly in the packed FFN layout, the next one recaptures -- and the trajectory tracks eager trainers making the
-    same switch (losses and every parameter within 4x the eager-vs-eager spread)."""
+    same switch bitwise (deterministic mode)."""
     from dphubert_amd.trainer import Trainer
     batch = _batch()
     mk = lambda graphs: Trainer(_module(), clip_norm=10.0, graphs=graphs, graph_warmup=1)  # noqa: E731
-    eager = [mk(False) for _ in range(4)]
+    eager = [mk(False) for _ in range(2)]
     gr = mk(True)
     for t in eager + [gr]:
         t.FFN_COMPACT_EVERY = 3          # decisions at global steps 1, 4, 7 (_module() starts at 1)
@@ -217,7 +201,7 @@ def test_ffn_compaction_switch_under_graphs():
     hc = gr.module.student_model.encoder.transformer.layers[0].feed_forward.hard_concrete_for_intermediate
     assert getattr(hc, "dph_compact", False), "the gate did not switch to the packed FFN"
     assert gr._graph is not None, "no graph recaptured after the switch"
-    _assert_tracks_eager(eager, gr, le, lg)
+    _assert_bitwise(eager, gr, le, lg)
 
 
 def test_profiled_graph_survives_grouped_fallback(monkeypatch):
@@ -311,3 +295,66 @@ def test_grouped_wgrads_match_per_layer(monkeypatch):
         assert not any(getattr(p, "_dph_hold", False) for p in tr.reducer.params)
     assert calls == [2, 2, 2, 2], calls     # FFN w2, FFN w1, out-proj, qkv: both layers each
     assert rel_l2(res[1], res[0]) < 1e-4
+
+
+@pytest.mark.parametrize("family", ["hubert", "wavlm", "large"])
+def test_deterministic_mode_matches_atomic_reductions(family):
+    """The fixed-order reductions of deterministic mode (LayerNorm-affine / bias column sums, mask gradients, conv0
+    sums, head-mask sums, the WavLM diagonal and gate sums) against the float-atomic ones: one step's gradients agree
+    to fp32 summation-order noise (whole gradient vector rel-L2 < 1e-5), and deterministic mode repeats bitwise."""
+    from dphubert_amd import _lib
+    from dphubert_amd.ddp import GradReducer
+    batch = _batch()
+    grads = []
+    for det in (True, False, True):
+        _lib.set_deterministic(det)
+        dm = _module(family=family)
+        red = GradReducer([p for p in dm.parameters() if p.requires_grad])
+        red.prepare()
+        loss = dm._step(batch, 0, "train")
+        loss.backward()
+        red.finish()
+        torch.cuda.synchronize()
+        grads.append(torch.cat([f.detach().float().cpu() for f in red.flat]))
+        red.remove()
+    assert torch.equal(grads[0], grads[2]), "deterministic mode did not repeat bitwise"
+    assert rel_l2(grads[1], grads[0]) < 1e-5, rel_l2(grads[1], grads[0])
+
+
+@pytest.mark.parametrize("group", [1, 2])
+def test_ffn_mask_grad_colprod_matches_epilogue(monkeypatch, group):
+    """the FFN intermediate-mask gradient from the FFN2 weight gradient (dph_colprod: sum_o W2[o][n]
+    dW2[o][n] / mask_n, the default) against the f-reading DGK epilogue (DPH_FFN_COLPROD=0), ungrouped and grouped
+    weight gradients, over two accumulated micro-batches (the second one takes the epilogue either way: its bucket
+    is no longer fresh), with intermediate masks exactly 0, near 0 and near 1."""
+    from dphubert_amd import ops
+    from dphubert_amd.ddp import GradReducer
+    batch = _batch()
+    res = []
+    for colprod in (True, False):
+        monkeypatch.setattr(ops, "_FFN_COLPROD", colprod)
+        dm = _module()
+        g = torch.Generator().manual_seed(3)
+        for name, mod in dm.student_model.named_modules():
+            if name.endswith("hard_concrete_for_intermediate"):
+                n = mod.log_alpha.numel()
+                u = torch.rand(n, generator=g) * 0.98 + 0.01
+                u[: n // 4] = 1e-4            # sampled below 0: clamped to exactly 0 (hardconcrete.py:99)
+                u[n // 4: n // 2] = 0.9999     # near 1
+                mod.set_noise(u.to(DEV))
+        red = GradReducer([p for p in dm.parameters() if p.requires_grad])
+        grads = []
+        for micro in range(2):
+            red.prepare(zero=micro == 0, sync=micro == 1)
+            with ops.grouped_wgrads(group):
+                (dm._step(batch, 0, "train") / 2).backward()
+            torch.cuda.synchronize()
+            grads.append({n: p.grad.detach().clone().cpu() for n, p in dm.student_model.named_parameters()
+                          if n.endswith("hard_concrete_for_intermediate.log_alpha")})
+        red.finish()
+        red.remove()
+        res.append(grads)
+    for micro in range(2):
+        for n, a in res[0][micro].items():
+            b = res[1][micro][n]
+            assert rel_l2(a, b) < 1e-4, (micro, n, rel_l2(a, b))

@@ -14,6 +14,13 @@ import torch.nn.functional as F
 from helpers import rel_l2, seeded_sd
 from oracle import hubert_ref as ref
 
+
+def prep_ws(B, T, H):
+    """(pointer, bytes) of the attention-prep head-sum workspace (deterministic mode)."""
+    from dphubert_amd import _lib
+    from dphubert_amd.ops import _ws
+    return _ws(_lib.lib().dph_attention_bwd_prep_workspace(B, T, H), DEV)
+
 pytestmark = pytest.mark.gpu
 
 DEV = "cuda"
@@ -84,7 +91,7 @@ def test_attention_kernel_vs_torch(fwd, T, short, amp, zero_head, monkeypatch):
     om_ref.backward(g.float())
     Dv = torch.empty(B * H * T, device=DEV)
     dhm = torch.zeros(H, device=DEV)
-    call("dph_attention_bwd_prep", ptr(g), ptr(o_u), ptr(hm), ptr(Dv), ptr(dhm), B, T, H, s)
+    call("dph_attention_bwd_prep", ptr(g), ptr(o_u), ptr(hm), ptr(Dv), ptr(dhm), B, T, H, *prep_ws(B, T, H), s)
     dqkv = torch.empty_like(qkv)
     call("dph_attention_bwd", ptr(qkv), ptr(g), ptr(hm), ptr(lse), ptr(Dv), ptr(dqkv), ptr(lens), B, T, H, 0.125,
          0.0, 0, None, s)
@@ -122,7 +129,7 @@ def test_attention_backward_vs_fp64_on_same_inputs(sharp):
     lse = torch.empty(B * H * T, device=DEV)
     call("dph_attention_fwd", ptr(qkv), ptr(o_u), ptr(o_m), ptr(lse), None, None, B, T, H, 0.125, 0.0, 0, None, s)
     Dv = torch.empty(B * H * T, device=DEV)
-    call("dph_attention_bwd_prep", ptr(g), ptr(o_u), None, ptr(Dv), None, B, T, H, s)
+    call("dph_attention_bwd_prep", ptr(g), ptr(o_u), None, ptr(Dv), None, B, T, H, None, 0, s)
     dqkv = torch.empty_like(qkv)
     call("dph_attention_bwd", ptr(qkv), ptr(g), None, ptr(lse), ptr(Dv), ptr(dqkv), None, B, T, H, 0.125, 0.0, 0, None, s)
     x = qkv.double().clone().requires_grad_(True)
@@ -169,7 +176,7 @@ def test_attention_dropout_consistency():
     # gradient of sum(o * g) wrt v must equal P_drop^T g ; check via the value path:
     g = torch.randn(B * T, D, device=DEV).to(torch.bfloat16)
     Dv = torch.empty(B * H * T, device=DEV)
-    call("dph_attention_bwd_prep", ptr(g), ptr(o1), None, ptr(Dv), None, B, T, H, s)
+    call("dph_attention_bwd_prep", ptr(g), ptr(o1), None, ptr(Dv), None, B, T, H, None, 0, s)
     dqkv = torch.empty_like(qkv)
     call("dph_attention_bwd", ptr(qkv), ptr(g), None, ptr(lse), ptr(Dv), ptr(dqkv), None, B, T, H, 0.125, 0.3, 77, None, s)
     # o is linear in v: sum(o*g) = sum(v * dv) exactly (up to bf16 rounding)
@@ -204,7 +211,7 @@ def test_attention_stored_keep_bits_match_rehash(T, lens):
         call("dph_attention_fwd", ptr(qkv), ptr(o_u), ptr(o_m), ptr(lse), ptr(hm), ptr(ln), B, T, H, 0.125, 0.1, 99,
              ptr(kb), s)
         Dv = torch.empty(B * H * T, device=DEV)
-        call("dph_attention_bwd_prep", ptr(g), ptr(o_u), ptr(hm), ptr(Dv), None, B, T, H, s)
+        call("dph_attention_bwd_prep", ptr(g), ptr(o_u), ptr(hm), ptr(Dv), None, B, T, H, None, 0, s)
         dqkv = torch.empty_like(qkv)
         call("dph_attention_bwd", ptr(qkv), ptr(g), ptr(hm), ptr(lse), ptr(Dv), ptr(dqkv), ptr(ln), B, T, H, 0.125,
              0.1, 99, ptr(kb), s)
@@ -501,7 +508,7 @@ def _conv0_gn(wave, w, C, gamma, beta, mask, dy=None):
         return y
     dw = torch.zeros(C, 10, device=DEV)
     dg, db, dm = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
-    wsb = torch.empty((_lib.lib().dph_conv0_gn_bwd_workspace(B, C) + 3) // 4, device=DEV)
+    wsb = torch.empty((_lib.lib().dph_conv0_gn_bwd_workspace(B, S, C) + 3) // 4, device=DEV)
     call("dph_conv0_gn_bwd", ptr(wave), B, S, ptr(w), C, 10, 5, ptr(gamma), ptr(beta), ptr(mask), ptr(mean),
          ptr(rstd), ptr(dy), ptr(dw), ptr(dg), ptr(db), ptr(dm), ptr(wsb), wsb.numel() * 4, st)
     torch.cuda.synchronize()
@@ -594,7 +601,7 @@ def test_attention_bwd_merged_grid_matches_split(T, lens, p, monkeypatch):
     kb = keep if p > 0 else None
     call("dph_attention_fwd", ptr(qkv), ptr(o_u), ptr(o_m), ptr(lse), ptr(hm), ptr(ln), B, T, H, 0.125, p, 5, ptr(kb), s)
     Dv = torch.empty(B * H * T, device=DEV)
-    call("dph_attention_bwd_prep", ptr(g), ptr(o_u), ptr(hm), ptr(Dv), None, B, T, H, s)
+    call("dph_attention_bwd_prep", ptr(g), ptr(o_u), ptr(hm), ptr(Dv), None, B, T, H, None, 0, s)
     outs = []
     for split in ("0", "1"):
         monkeypatch.setenv("DPH_ATTN_SPLIT", split)

@@ -7,6 +7,11 @@ sys.path.insert(0, __import__("os").path.join(__import__("os").path.dirname(__im
                                               ".."))
 from dphubert_amd import _lib  # noqa: E402
 from dphubert_amd._lib import call, ptr  # noqa: E402
+from dphubert_amd.ops import _ws  # noqa: E402
+
+
+def prep_ws(B, T, H):
+    return _ws(_lib.lib().dph_attention_bwd_prep_workspace(B, T, H), "cuda")
 
 B, T, H = 16, 499, 12
 D = H * 64
@@ -41,7 +46,7 @@ keep = torch.empty(_lib.lib().dph_attention_keep_bytes(B, T, H) // 8, dtype=torc
 for p, kb in ((0.0, None), (0.1, None), (0.1, keep)):
     fwd = lambda: call("dph_attention_fwd", ptr(qkv), ptr(o_u), ptr(o_m), ptr(lse), ptr(hm), ptr(lens), B, T, H,  # noqa
                        0.125, p, 7, ptr(kb), s)
-    prep = lambda: call("dph_attention_bwd_prep", ptr(g), ptr(o_u), ptr(hm), ptr(Dv), ptr(dhm), B, T, H, s)  # noqa
+    prep = lambda: call("dph_attention_bwd_prep", ptr(g), ptr(o_u), ptr(hm), ptr(Dv), ptr(dhm), B, T, H, *prep_ws(B, T, H), s)  # noqa
     bwd = lambda: call("dph_attention_bwd", ptr(qkv), ptr(g), ptr(hm), ptr(lse), ptr(Dv), ptr(dqkv), ptr(lens),  # noqa
                        B, T, H, 0.125, p, 7, ptr(kb), s)
     tf, tp, tb = timeit(fwd), timeit(prep), timeit(bwd)

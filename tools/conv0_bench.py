@@ -27,7 +27,7 @@ mean = torch.empty(B * C, device=dev)
 rstd = torch.empty(B * C, device=dev)
 ws_f = torch.empty(B * 16 * 65 * 2, device=dev)
 dy = (torch.randn(B, L0, C, device=dev) * 0.01).to(torch.bfloat16)
-wsb = torch.empty(_lib.lib().dph_conv0_gn_bwd_workspace(B, C) // 4 + 64, device=dev)
+wsb = torch.empty(_lib.lib().dph_conv0_gn_bwd_workspace(B, S, C) // 4 + 64, device=dev)
 dw = torch.zeros(C, 10, device=dev)
 dg, db, dm = (torch.zeros(C, device=dev) for _ in range(3))
 

@@ -2,7 +2,7 @@
 
 Single process, world_size 1 over RCCL ("nccl" backend), GradReducer forced on so every bucket
 goes through a real RCCL all-reduce (AVG) launched from the backward hooks during capture.
-Compares 4 replayed optimizer steps with 4 eager steps of an identical module.
+Compares 4 replayed optimizer steps with 4 eager steps of an identical module, bitwise (deterministic mode).
 Run on the GPU box:  python tools/graph_rccl_probe.py [--comm fp32|bf16] [--accum N] [--port P]
 (tests/test_graph_gpu.py::test_graph_replay_with_rccl_allreduce runs it as a subprocess)
 """
@@ -27,11 +27,13 @@ def main():
     os.environ["MASTER_PORT"] = args.port
     torch.cuda.set_device(0)
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
-    from test_graph_gpu import _batch, _module, tracks_eager_report
+    from test_graph_gpu import _batch, _module, bitwise_report
+    from dphubert_amd import _lib
     from dphubert_amd.trainer import Trainer
+    _lib.set_deterministic(True)
     batch = _batch()
     gd = torch.bfloat16 if args.comm == "bf16" else torch.float32
-    eager = [Trainer(_module(), clip_norm=10.0, accum_grad=args.accum, grad_dtype=gd) for _ in range(4)]
+    eager = [Trainer(_module(), clip_norm=10.0, accum_grad=args.accum, grad_dtype=gd) for _ in range(2)]
     gr = Trainer(_module(), clip_norm=10.0, graphs=True, graph_warmup=1, accum_grad=args.accum, grad_dtype=gd)
     for t in eager + [gr]:
         t.reducer.force_enable()
@@ -46,8 +48,8 @@ def main():
     print("reducer buckets:", len(gr.reducer.buckets), "comm dtype:", gr.reducer.comm_dtype)
     print("eager losses  ", le)
     print("graph losses  ", lg)
-    # the criteria of tests/test_graph_gpu.py::test_graph_replay_matches_eager (tracks_eager_report)
-    ok, lines = tracks_eager_report(eager, gr, le, lg)
+    # the criteria of tests/test_graph_gpu.py::test_graph_replay_matches_eager: bitwise equal
+    ok, lines = bitwise_report(eager, gr, le, lg)
     ok &= gr._graph is not None
     print("\n".join(lines))
     dist.destroy_process_group()
