@@ -187,7 +187,7 @@ def pmc_traffic(args):
 
 # rocprof kernel-name fragments of the launches behind each kernel_table span (kernels.SPAN_WORK labels)
 SPAN_KERNELS = {
-    "attn_fwd_drop": ["attn_fwd32v2_kernel<true>"], "attn_fwd": ["attn_fwd32v2_kernel<false>"],
+    "attn_fwd_drop": ["attn_fwd32v2_kernel<true"], "attn_fwd": ["attn_fwd32v2_kernel<false"],
     "attn_bwd_drop": ["attn_bwd_kernel<true"], "attn_bwd": ["attn_bwd_kernel<false"],
     "conv0_gn_fwd": ["conv0_gram_part_kernel", "conv0_gram_reduce", "conv0_apply_kernel<true"],
     "conv0_gn_bwd": ["conv0_gram_part_kernel", "conv0_gram_reduce", "conv0_gn_bwd_kernel", "conv0_bwd_finalize"],

@@ -641,7 +641,11 @@ __global__ void __launch_bounds__(256, 2) attn_fwd32_kernel(const bf16_t* __rest
 // Same arithmetic per score as attn_fwd32_kernel; keep bits in the same layout (tiles past the key length
 // are not written: their probabilities are 0 and the backward multiplies whatever it reads there by 0).
 // ---------------------------------------------------------------------------
-template <bool DROP>
+// STAGE: the epilogue goes through LDS (the K / V tiles' space, free after the loop's last barrier): each wave writes
+// its 32 x 64 normalised O rows there and re-reads them row-contiguous, so every global store instruction writes
+// whole rows (o_u: 4 rows of 256 B, o_m: 4 rows of 128 B per wave instruction) instead of 16-B / 8-B pieces of 32
+// rows (the store tail of a one-round grid: guide T21, MI355X_MICROARCH 'attention epilogue store tail')
+template <bool DROP, bool STAGE>
 __global__ void __launch_bounds__(256, 3) attn_fwd32v2_kernel(const bf16_t* __restrict__ qkv, float* __restrict__ o_u,
                                                              bf16_t* __restrict__ o_m, float* __restrict__ lse,
                                                              const float* __restrict__ head_mask,
@@ -827,9 +831,48 @@ __global__ void __launch_bounds__(256, 3) attn_fwd32v2_kernel(const bf16_t* __re
   for (; kt < nfull; ++kt) body(kt, std::integral_constant<bool, false>());
   for (; kt < ntile; ++kt) body(kt, std::integral_constant<bool, true>());
 
-  if (q >= T32) return;
   const float hm = head_mask ? head_mask[h] : 1.0f;
   const float inv_l = inv_keep / l_run;
+  if constexpr (STAGE) {
+    // (every wave passed the last tile's barrier: the 32 KB of K / V buffers are free; 4 waves x 32 rows x 68
+    // floats = 34 KB would not fit, so each wave stages its rows in two halves of 16 rows)
+    constexpr int OST = 68;                              // padded row (floats)
+    float* ob = reinterpret_cast<float*>(smem) + wave * (16 * OST);
+    const int r = lane & 31;
+    const int qb = (int)blockIdx.x * RB + wave * 32;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      if ((r >> 4) == half) {
+#pragma unroll
+        for (int d = 0; d < 2; ++d)
+#pragma unroll
+          for (int rq = 0; rq < 4; ++rq) {
+            const int col = 32 * d + 8 * rq + 4 * hi;
+            *reinterpret_cast<float4*>(ob + (r & 15) * OST + col) =
+                make_float4(oacc[d][4 * rq] * inv_l, oacc[d][4 * rq + 1] * inv_l, oacc[d][4 * rq + 2] * inv_l,
+                            oacc[d][4 * rq + 3] * inv_l);
+          }
+      }
+      __syncthreads();
+      // 16 lanes per row (16 B each), 4 rows per wave instruction
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int rr = 4 * i + (lane >> 4);
+        const int cc = (lane & 15) * 4;
+        const int qr = qb + 16 * half + rr;
+        const float4 v = *reinterpret_cast<const float4*>(ob + rr * OST + cc);
+        if (qr < T32) {
+          const int64_t ob2 = ((int64_t)b * T32 + qr) * (H * HD) + h * HD + cc;
+          if (o_u) *reinterpret_cast<float4*>(o_u + ob2) = v;
+          *reinterpret_cast<uint2*>(o_m + ob2) = make_uint2(pack2bf(v.x * hm, v.y * hm), pack2bf(v.z * hm, v.w * hm));
+        }
+      }
+      if (half == 0) __syncthreads();
+    }
+    if (hi == 0 && lse && q < T32) lse[(int64_t)(b * H + h) * T32 + q] = m_run + __logf(l_run);
+    return;
+  }
+  if (q >= T32) return;
   const int64_t obase = ((int64_t)b * T32 + q) * (H * HD) + h * HD;
 #pragma unroll
   for (int d = 0; d < 2; ++d)
@@ -1484,9 +1527,21 @@ void launch_fwd(dim3 grid, hipStream_t stream, const void* qkv, void* o_u, void*
                 const int64_t* key_len, AttnShape sh, float scale, float p, uint64_t seed, RelBias rb, void* keep) {
   const int mode = BIAS ? 0 : fwd32_mode();
   if (mode == 2) {
-    hipLaunchKernelGGL((attn_fwd32v2_kernel<DROP>), grid, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(qkv),
-                       reinterpret_cast<float*>(o_u), reinterpret_cast<bf16_t*>(o_m), lse, hm, key_len, sh, scale, p,
-                       seed, reinterpret_cast<uint16_t*>(keep));
+    // DPH_ATTN_EPI=0: the per-lane scattered epilogue stores (A/B)
+    static const bool staged = [] {
+      const char* e = getenv("DPH_ATTN_EPI");
+      return !(e && e[0] == '0');
+    }();
+    if (staged)
+      hipLaunchKernelGGL((attn_fwd32v2_kernel<DROP, true>), grid, dim3(256), 0, stream,
+                         reinterpret_cast<const bf16_t*>(qkv), reinterpret_cast<float*>(o_u),
+                         reinterpret_cast<bf16_t*>(o_m), lse, hm, key_len, sh, scale, p, seed,
+                         reinterpret_cast<uint16_t*>(keep));
+    else
+      hipLaunchKernelGGL((attn_fwd32v2_kernel<DROP, false>), grid, dim3(256), 0, stream,
+                         reinterpret_cast<const bf16_t*>(qkv), reinterpret_cast<float*>(o_u),
+                         reinterpret_cast<bf16_t*>(o_m), lse, hm, key_len, sh, scale, p, seed,
+                         reinterpret_cast<uint16_t*>(keep));
     return;
   }
   if (mode == 1) {

@@ -219,16 +219,25 @@ def bf16_sensitivity(exact, emulated):
 
 
 def run_step(tcfg, scfg, distill_layers_str, B, S, units, lambdas, global_step, seed=0, lengths=None,
-             full=False, cos_type="raw", l2=0.0, distill_mode="layer2layer", sens=True):
+             full=False, cos_type="raw", l2=0.0, distill_mode="layer2layer", sens=True, whole=None):
     """Run the reference DistillModule._step + backward; return a fixture dict (plus, with ``sens``, the bf16
-    sensitivity of every checked quantity from a second run under Bf16Emulation with the same noise)."""
+    sensitivity of every checked quantity from a second run under Bf16Emulation with the same noise).
+
+    ``whole``: a predicate on student parameter names whose gradients are stored WHOLE (bf16 values plus their
+    exact fp32 norm, and their bf16-emulation sensitivity as a whole-tensor rel-L2)."""
     if sens:
         kw = dict(seed=seed, lengths=lengths, full=full, cos_type=cos_type, l2=l2, distill_mode=distill_mode,
-                  sens=False)
+                  sens=False, whole=whole)
         fx = run_step(tcfg, scfg, distill_layers_str, B, S, units, lambdas, global_step, **kw)
         with Bf16Emulation():
             em = run_step(tcfg, scfg, distill_layers_str, B, S, units, lambdas, global_step, **kw)
         fx["sens"] = bf16_sensitivity(fx, em)
+        if whole is not None:
+            rl2 = lambda a, b: ((a.double() - b.double()).norm() / b.double().norm().clamp_min(1e-30)).item()  # noqa
+            fx["sens"]["whole"] = {n: rl2(em["whole_f32"][n], g) for n, g in fx["whole_f32"].items()}
+            fx["whole_grads"] = {n: g.to(torch.bfloat16) for n, g in fx["whole_f32"].items()}
+            fx["whole_norms"] = {n: g.double().norm().item() for n, g in fx["whole_f32"].items()}
+            del fx["whole_f32"]
         return fx
     scfg = dict(scfg, **units_flags(units))
     teacher, tsd = seeded_model(tcfg, seed)
@@ -317,6 +326,9 @@ def run_step(tcfg, scfg, distill_layers_str, B, S, units, lambdas, global_step, 
         fx["lambda_grads"] = [dm.lambda1.grad.detach().clone(), dm.lambda2.grad.detach().clone()]
     if full:
         fx["student_hiddens"] = cap["h"]
+    if whole is not None:
+        fx["whole_f32"] = {n: p.grad.detach().clone() for n, p in student.named_parameters()
+                           if p.grad is not None and whole(n)}
     return fx
 
 
@@ -520,6 +532,28 @@ def gen_base12():
                     units="conv,head,interm", lambdas=(0.0, 0.0), global_step=5000)
 
 
+def _g14_whole(n):
+    """The parameters g14 stores whole gradients of: the last two encoder layers' attention projections, the last
+    layer's feed-forward and LayerNorms, and the conv frontend's first and last two layers + GroupNorm and the
+    feature projection (the rest of the frontend is ~3 M more parameters; every other gradient keeps its 64-sample
+    checksum)."""
+    if "log_alpha" in n:
+        return False
+    if n.startswith("encoder.transformer.layers.11."):
+        return True
+    if n.startswith("encoder.transformer.layers.10.attention.") and "hard_concrete" not in n:
+        return True
+    return n.startswith(("feature_extractor.conv_layers.0.", "feature_extractor.conv_layers.5.",
+                         "feature_extractor.conv_layers.6.", "encoder.feature_projection."))
+
+
+def gen_base12_whole():
+    """G14: G3's configuration (full Base 12 layers, 1 x 10 s, distill layers 0.4,8,12) with whole gradients of the
+    _g14_whole parameters (bf16 values + fp32 norms + bf16-emulation sensitivity per tensor)."""
+    return run_step(no_dropout(HUBERT_BASE_CONFIG), no_dropout(HUBERT_BASE_CONFIG), "0.4,8,12", B=1, S=160000,
+                    units="conv,head,interm", lambdas=(0.0, 0.0), global_step=5000, whole=_g14_whole)
+
+
 def gen_large():
     """G10: Large dimensions, 2 layers, one utterance at lightning.py:313's max_len 250000 samples (T = 781) and a
     shorter padded one, all of conv,head,interm, regulariser active (checksums only: full hiddens are 6 MB each)."""
@@ -555,7 +589,7 @@ def gen_predlayer():
 def main():
     only = [a[len("--only="):] for a in sys.argv[1:] if a.startswith("--only=")]
     extra = {"g10_large.pt": gen_large, "g11_large_lnext.pt": gen_large_ln, "g12_predlayer.pt": gen_predlayer,
-             "g3_base12.pt": gen_base12, "g13_large24.pt": gen_large24}
+             "g3_base12.pt": gen_base12, "g13_large24.pt": gen_large24, "g14_base12_whole.pt": gen_base12_whole}
     if only:
         OUT.mkdir(parents=True, exist_ok=True)
         torch.set_num_threads(8)
