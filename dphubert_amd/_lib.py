@@ -34,9 +34,7 @@ class DphGemmArgs(C.Structure):
                 ("alpha", f32), ("dropout_p", f32), ("seed", u64), ("bias", vp), ("colmask", vp), ("smask", vp),
                 ("vec_z_inner", i64), ("pre_out", vp), ("aux_in", vp), ("residual", vp), ("colsum_out", vp),
                 ("colsum_aux", vp), ("row_len", vp), ("len_rows", i64), ("drop_row_offset", i64),
-                ("workspace", vp), ("workspace_bytes", i64), ("colsum_n", i64), ("flags", i64), ("dyn_ext", vp),
-                ("ln_gamma", vp), ("ln_beta", vp), ("ln_out", vp), ("ln_mean", vp), ("ln_rstd", vp),
-                ("ln_tickets", vp)]
+                ("workspace", vp), ("workspace_bytes", i64), ("colsum_n", i64), ("flags", i64), ("dyn_ext", vp)]
 
 
 GEMM_GROUP_MAX = 16
@@ -169,9 +167,8 @@ _lib = None
 # workspaces; 12: dph_hc_bank_fwd / dph_hc_bank_bwd; 15: dph_gemm_mn_plan; 16: DphGemmArgs.dyn_ext, dph_ffn_compact + gathers / scatters;
 # 19: DPH_GEMM_RESID_F32, dph_layernorm_fwd_x32 / _bwd_res32, dph_branch_bwd_f32, dph_distill_loss_*_ex: the fp32
 # pre-norm residual stream; 20: deterministic mode -- dph_set_deterministic / dph_get_deterministic and the workspaces
-# of the fixed-order reductions: attention prep / relpos backward, WavLM gate, conv0, GELU-mask and branch backward;
-# 21: DphGemmArgs.ln_* + DPH_GEMM_LN_TAIL, the post-norm LayerNorm fused into the producing GEMM)
-ABI_VERSION = 21
+# of the fixed-order reductions: attention prep / relpos backward, WavLM gate, conv0, GELU-mask and branch backward)
+ABI_VERSION = 20
 
 
 class DphError(RuntimeError):

@@ -1971,107 +1971,7 @@ __device__ __forceinline__ bf16x8_t hfrag(const char* ht, int rb, int s, int lan
   return *reinterpret_cast<const bf16x8_t*>(ht + row * 128 + phys * 16);
 }
 
-// DPH_GEMM_LN_TAIL (N = 768): the post-norm LayerNorm of the row strip [m0, m0 + BM) -- components.py:853 / :856,
-// nn.LayerNorm(768) of the GEMM output just stored (bias + dropout + residual applied) -- by the LAST of the strip's
-// gridDim.x column tiles to finish, inside the same launch (no separate LayerNorm launch, its launch gap and its
-// one-round load / store bursts).  Publication (MI355X_MICROARCH hand-off table, row 1): every wave's stores drained,
-// a barrier, one lane's agent-scope release + s_waitcnt + agent-scope ticket add; the lane whose add returns
-// gridDim.x - 1 acquires, re-arms the ticket to 0 and the block reads the strip after a barrier.  The arithmetic is
-// norm.hip's ln_fwd16_kernel's (half a wave per row, 8 elements per 16-B access, the same sum orders): the result
-// equals the stand-alone LayerNorm bit for bit.
-template <class C>
-__device__ __forceinline__ void ln_tail(const DphGemmArgs& a, int64_t m0, int lane, int wave) {
-  constexpr int NE = 24, NC = NE / 8, D = NE * 32;   // N == 768 (checked on the host)
-  __shared__ unsigned last_s;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int64_t tm = m0 / C::BM;
-    const unsigned old = __hip_atomic_fetch_add(a.ln_tickets + tm, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const bool last = old == gridDim.x - 1;
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      a.ln_tickets[tm] = 0u;
-    }
-    last_s = last ? 1u : 0u;
-  }
-  __syncthreads();
-  if (last_s == 0u) return;
-  const bf16_t* X = reinterpret_cast<const bf16_t*>(a.C.ptr);
-  bf16_t* Y = reinterpret_cast<bf16_t*>(a.ln_out);
-  const int64_t m1 = min<int64_t>(m0 + C::BM, a.M);
-  const int hl = lane & 31;
-  float ga[NC][8], be[NC][8];
-#pragma unroll
-  for (int c = 0; c < NC; ++c) {
-    const int col = (c * 32 + hl) * 8;
-    const float4 g0 = *reinterpret_cast<const float4*>(a.ln_gamma + col), g1 = *reinterpret_cast<const float4*>(a.ln_gamma + col + 4);
-    const float4 b0 = *reinterpret_cast<const float4*>(a.ln_beta + col), b1 = *reinterpret_cast<const float4*>(a.ln_beta + col + 4);
-    ga[c][0] = g0.x; ga[c][1] = g0.y; ga[c][2] = g0.z; ga[c][3] = g0.w;
-    ga[c][4] = g1.x; ga[c][5] = g1.y; ga[c][6] = g1.z; ga[c][7] = g1.w;
-    be[c][0] = b0.x; be[c][1] = b0.y; be[c][2] = b0.z; be[c][3] = b0.w;
-    be[c][4] = b1.x; be[c][5] = b1.y; be[c][6] = b1.z; be[c][7] = b1.w;
-  }
-#pragma unroll 1
-  for (int64_t r0 = m0; r0 < m1; r0 += 2 * C::NW) {
-    const int64_t row = r0 + 2 * wave + (lane >> 5);
-    const bool ok = row < m1;
-    float v[NC][8];
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      if (ok) {
-        const uint4 r = *reinterpret_cast<const uint4*>(X + row * D + (c * 32 + hl) * 8);
-        const uint32_t w[4] = {r.x, r.y, r.z, r.w};
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          v[c][2 * i] = __uint_as_float(w[i] << 16);
-          v[c][2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
-        }
-      } else {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) v[c][i] = 0.f;
-      }
-    }
-    float sm = 0.f;
-#pragma unroll
-    for (int c = 0; c < NC; ++c)
-#pragma unroll
-      for (int i = 0; i < 8; ++i) sm += v[c][i];
-#pragma unroll
-    for (int o = 16; o > 0; o >>= 1) sm += __shfl_xor(sm, o, 64);
-    const float mean = sm * (1.0f / (float)D);
-    float q = 0.f;
-#pragma unroll
-    for (int c = 0; c < NC; ++c)
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const float d = v[c][i] - mean;
-        q += d * d;
-      }
-#pragma unroll
-    for (int o = 16; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
-    const float rstd = rsqrtf(q * (1.0f / (float)D) + 1e-5f);
-    if (ok) {
-#pragma unroll
-      for (int c = 0; c < NC; ++c) {
-        float o[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) o[i] = (v[c][i] - mean) * rstd * ga[c][i] + be[c][i];
-        *reinterpret_cast<uint4*>(Y + row * D + (c * 32 + hl) * 8) =
-            make_uint4(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]), pack2bf(o[4], o[5]), pack2bf(o[6], o[7]));
-      }
-      if (hl == 0) {
-        a.ln_mean[row] = mean;
-        a.ln_rstd[row] = rstd;
-      }
-    }
-  }
-}
-
-template <class C, int ACT, bool DROP, bool LNT = false>
+template <class C, int ACT, bool DROP>
 __global__ void __launch_bounds__(C::NT, C::WPE) pp_gemm_kernel(const DphGemmArgs a) {
   __shared__ __attribute__((aligned(1024))) char smem[C::LDS];
   const int tid = threadIdx.x;
@@ -2299,7 +2199,6 @@ __global__ void __launch_bounds__(C::NT, C::WPE) pp_gemm_kernel(const DphGemmArg
   }
   if (wr == 0) bar();            // pairs with group 1's extra barrier
   ring::direct_epi_t<C, ACT, DROP, true>(a, z, m0 + wr * C::WTM, n0 + wc * C::WTN, lane, acc);
-  if constexpr (LNT) ln_tail<C>(a, m0, lane, wave);
 }
 }  // namespace pp
 
@@ -2711,6 +2610,23 @@ __global__ void __launch_bounds__(256) colsum_slab_reduce_kernel(const float* __
   if (ty == 0 && col < csn) {
     if (out) atomicAdd(out + col, red[0][0][tx] + red[0][1][tx] + red[0][2][tx] + red[0][3][tx]);
     if (aux) atomicAdd(aux + col, red[1][0][tx] + red[1][1][tx] + red[1][2][tx] + red[1][3][tx]);
+  }
+}
+
+// deterministic mode: the same sums, every column's slab rows added in a fixed order by one block of 32 columns x
+// DET_PH row phases (det_column_total); out and aux each get one writer per column
+__global__ void __launch_bounds__(32 * DET_PH) colsum_slab_reduce_det_kernel(const float* __restrict__ slab,
+                                                                             int64_t nrows, int64_t ncols, int64_t csn,
+                                                                             float* __restrict__ out,
+                                                                             float* __restrict__ aux) {
+  __shared__ float red[DET_PH][33];
+  const int64_t col = (int64_t)blockIdx.x * 32 + (threadIdx.x & 31);
+  const bool live = col < csn;
+  const float so = det_column_total(live && out ? slab + col : nullptr, nrows, ncols, red);
+  const float sa = det_column_total(live && aux ? slab + nrows * ncols + col : nullptr, nrows, ncols, red);
+  if ((threadIdx.x >> 5) == 0 && live) {
+    if (out) out[col] += so;
+    if (aux) aux[col] += sa;
   }
 }
 
@@ -3145,24 +3061,10 @@ static void launch_pp(const DphGemmArgs& a, hipStream_t stream) {
   } else if (a.act == DPH_ACT_GELU_BWD) {
     if (drop) hipLaunchKernelGGL((pp::pp_gemm_kernel<Cf, DPH_ACT_GELU_BWD, true>), g, b, 0, stream, a);
     else hipLaunchKernelGGL((pp::pp_gemm_kernel<Cf, DPH_ACT_GELU_BWD, false>), g, b, 0, stream, a);
-  } else if (a.flags & DPH_GEMM_LN_TAIL) {
-    // (the host took the LayerNorm tail only where ln_tail_ok holds)
-    if (drop) hipLaunchKernelGGL((pp::pp_gemm_kernel<Cf, DPH_ACT_NONE, true, true>), g, b, 0, stream, a);
-    else hipLaunchKernelGGL((pp::pp_gemm_kernel<Cf, DPH_ACT_NONE, false, true>), g, b, 0, stream, a);
   } else {
     if (drop) hipLaunchKernelGGL((pp::pp_gemm_kernel<Cf, DPH_ACT_NONE, true>), g, b, 0, stream, a);
     else hipLaunchKernelGGL((pp::pp_gemm_kernel<Cf, DPH_ACT_NONE, false>), g, b, 0, stream, a);
   }
-}
-
-// the fused LayerNorm tail applies: a ping-pong tile, N == 768, dense bf16 C without a batched row layout, no
-// split-K / batch / device extents, every LN pointer given and 16-B aligned
-static bool ln_tail_ok(const DphGemmArgs& a, int kind) {
-  auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
-  return kind >= 12 && kind <= 16 && a.N == 768 && a.act == DPH_ACT_NONE && a.c_dtype == DPH_OUT_BF16 &&
-         a.C.row_stride == a.N && a.C.rows_per_batch == 0 && a.batch == 1 && a.splits == 1 && !a.dyn_ext &&
-         a.ln_gamma && a.ln_beta && a.ln_out && a.ln_mean && a.ln_rstd && a.ln_tickets && al(a.C.ptr) &&
-         al(a.ln_out) && al(a.ln_gamma) && al(a.ln_beta);
 }
 
 // CU count of the current device (persistent grids)
@@ -3302,10 +3204,6 @@ extern "C" int dph_gemm(const DphGemmArgs* args, hipStream_t stream) {
               "> 1 only with shared output vectors, vec_z_inner 0)");
   DphGemmArgs b = a;
   if (slab) b.flags |= GEMM_COLSUM_SLAB;
-  // the post-norm LayerNorm tail: fused where it applies, else the stand-alone LayerNorm after the GEMM (below)
-  const bool want_ln = (a.flags & DPH_GEMM_LN_TAIL) != 0;
-  const bool ln_fused = want_ln && ln_tail_ok(a, kind);
-  if (want_ln && !ln_fused) b.flags &= ~(int64_t)DPH_GEMM_LN_TAIL;
   if (kind >= 12 && kind <= 16) {
     DPH_REQUIRE(cdiv(a.M, 128) < 65536 && a.batch < 65536, "dph_gemm: grid too large");
     if (kind == 12) launch_pp<pp::P256>(b, stream);
@@ -3379,22 +3277,18 @@ extern "C" int dph_gemm(const DphGemmArgs* args, hipStream_t stream) {
   }
   int rc = check_launch("dph_gemm");
   if (rc) return rc;
-  if (want_ln && !ln_fused) {
-    DPH_REQUIRE(a.c_dtype == DPH_OUT_BF16 && a.C.row_stride == a.N && a.batch == 1 && a.ln_gamma && a.ln_beta &&
-                    a.ln_out && a.ln_mean && a.ln_rstd,
-                "dph_gemm: DPH_GEMM_LN_TAIL needs a dense bf16 C of batch 1 and every ln_* pointer");
-    rc = dph_layernorm_fwd(a.C.ptr, nullptr, a.ln_gamma, a.ln_beta, a.ln_out, a.ln_mean, a.ln_rstd, a.M, a.N, 1e-5f,
-                           0.f, 0, stream);
-    if (rc) return rc;
-  }
   if (slab) {
     const int64_t csn = std::min<int64_t>(a.colsum_n > 0 ? a.colsum_n : a.N, a.N);
     // (>= 16 slab rows per group: a few hundred blocks even at N = 768, each thread's rows in flight together;
-    // deterministic mode: one group, each column summed in a fixed order)
-    const unsigned groups =
-        deterministic() ? 1u : (unsigned)std::max<int64_t>(1, std::min<int64_t>(32, cdiv(nslots, 16)));
-    hipLaunchKernelGGL(colsum_slab_reduce_kernel, dim3((unsigned)cdiv(csn, 64), groups), dim3(256), 0, stream,
-                       reinterpret_cast<const float*>(a.workspace), nslots, a.N, csn, a.colsum_out, a.colsum_aux);
+    // deterministic mode: each column's rows in a fixed order)
+    if (deterministic()) {
+      hipLaunchKernelGGL(colsum_slab_reduce_det_kernel, dim3((unsigned)cdiv(csn, 32)), dim3(32 * DET_PH), 0, stream,
+                         reinterpret_cast<const float*>(a.workspace), nslots, a.N, csn, a.colsum_out, a.colsum_aux);
+    } else {
+      const unsigned groups = (unsigned)std::max<int64_t>(1, std::min<int64_t>(32, cdiv(nslots, 16)));
+      hipLaunchKernelGGL(colsum_slab_reduce_kernel, dim3((unsigned)cdiv(csn, 64), groups), dim3(256), 0, stream,
+                         reinterpret_cast<const float*>(a.workspace), nslots, a.N, csn, a.colsum_out, a.colsum_aux);
+    }
     return check_launch("dph_gemm colsum reduce");
   }
   if (a.splits > 1) {

@@ -222,20 +222,7 @@ def _variant(args):
 GEMM_NO_PERSIST = 1            # DphGemmArgs.flags (include/dphubert_hip.h)
 GEMM_PRE_DGK = 2               # ACT_GELU: pre_out stores gelu'(pre)*colmask*keep/(1-p) (ACT_GELU_BWD_DGK's aux)
 GEMM_RESID_F32 = 4             # the residual is fp32 (the pre-norm residual stream); set from the tensor's dtype
-GEMM_LN_TAIL = 8               # the post-norm LayerNorm of the output fused into the GEMM (DphGemmArgs.ln_*)
 _SHARED_GPU = [0]
-_TICKETS = {}
-
-
-def ln_tickets(device) -> torch.Tensor:
-    """The LayerNorm tail's row-strip tickets of the CURRENT stream (include/dphubert_hip.h DPH_GEMM_LN_TAIL: zeroed
-    once here, every launch leaves them zero; two launches running at once on different streams must not share
-    them).  65 536 strips = 8.4 M rows at 128 rows per strip."""
-    key = (str(device), torch.cuda.current_stream(device).cuda_stream)
-    t = _TICKETS.get(key)
-    if t is None:
-        t = _TICKETS[key] = torch.zeros(65536, dtype=torch.int32, device=device)
-    return t
 
 
 class shared_gpu:
@@ -254,15 +241,8 @@ def gemm(A: DphMat, B: DphMat, Cm: DphMat, M: int, N: int, K: int, *, a_kcontig:
          c_dtype: int = OUT_BF16, act: int = ACT_NONE, alpha: float = 1.0, batch: int = 1, splits: int = 1,
          bias=None, colmask=None, smask=None, vec_z_inner: int = 0, pre_out=None, aux_in=None, residual=None,
          colsum_out=None, colsum_aux=None, row_len=None, len_rows: int = 0, dropout_p: float = 0.0, seed: int = 0,
-         drop_row_offset: int = 0, colsum_n: int = 0, device=None, flags: int = 0, dyn=None, ln=None):
-    """``dyn``: (int32 device tensor, offset) of a {m, n, k} device-side extent triplet (DphGemmArgs.dyn_ext).
-    ``ln``: (gamma, beta, out, mean, rstd) -- the post-norm LayerNorm of the output in the same launch
-    (DPH_GEMM_LN_TAIL; dph_gemm falls back to the stand-alone LayerNorm where the fused tail does not apply)."""
-    if ln is not None:
-        if M > 65536 * 128:
-            raise ValueError("ln tail: more row strips than tickets")
-        flags |= GEMM_LN_TAIL
-        tick = ln_tickets(Cm_device(ln[2]))
+         drop_row_offset: int = 0, colsum_n: int = 0, device=None, flags: int = 0, dyn=None):
+    """``dyn``: (int32 device tensor, offset) of a {m, n, k} device-side extent triplet (DphGemmArgs.dyn_ext)."""
     if residual is not None and residual.dtype == F32:
         flags |= GEMM_RESID_F32
     ws = None
@@ -285,9 +265,7 @@ def gemm(A: DphMat, B: DphMat, Cm: DphMat, M: int, N: int, K: int, *, a_kcontig:
                        ptr(pre_out), ptr(aux_in), ptr(residual), ptr(colsum_out), ptr(colsum_aux), ptr(row_len),
                        len_rows, drop_row_offset, ptr(ws), ws_bytes, colsum_n,
                        flags | (GEMM_NO_PERSIST if _SHARED_GPU[0] else 0),
-                       (dyn[0].data_ptr() + 4 * dyn[1]) if dyn is not None else None,
-                       *((ptr(ln[0]), ptr(ln[1]), ptr(ln[2]), ptr(ln[3]), ptr(ln[4]), ptr(tick)) if ln is not None
-                         else (None,) * 6))
+                       (dyn[0].data_ptr() + 4 * dyn[1]) if dyn is not None else None)
     prof = LaunchProfiler.active
     if prof is not None:
         e0, e1 = prof.event(), prof.event()
@@ -295,7 +273,7 @@ def gemm(A: DphMat, B: DphMat, Cm: DphMat, M: int, N: int, K: int, *, a_kcontig:
     call("dph_gemm", C.byref(args), _stream())
     if prof is not None:
         e1.record()
-        name = _variant(args) + (" +ln_tail" if ln is not None else "")
+        name = _variant(args)
         if prof.by_shape:
             al = min((x & -x) if x else 1 << 20 for x in (Cm.ptr or 0, ptr(pre_out) or 0, ptr(aux_in) or 0,
                                                             ptr(residual) or 0, ptr(bias) or 0))
@@ -334,7 +312,7 @@ def choose_splits(M: int, N: int, K: int, batch: int = 1, target_blocks: int = 5
 
 def linear_fwd(x: torch.Tensor, w_bf16: torch.Tensor, bias: Optional[torch.Tensor] = None, *, out=None,
                out_dtype=BF16, act=ACT_NONE, pre_out=None, colmask=None, smask=None, residual=None,
-               dropout_p=0.0, seed=0, row_len=None, len_rows=0, colsum_out=None, pre_dgk=False, dyn=None, ln=None):
+               dropout_p=0.0, seed=0, row_len=None, len_rows=0, colsum_out=None, pre_dgk=False, dyn=None):
     """y = epi(x @ w^T + b); x [M,K] bf16, w [N,K] bf16 (nn.Linear layout).
 
     ``pre_dgk`` (act=ACT_GELU): pre_out receives gelu'(pre)*colmask*keep/(1-p), the aux input of the matching
@@ -351,7 +329,7 @@ def linear_fwd(x: torch.Tensor, w_bf16: torch.Tensor, bias: Optional[torch.Tenso
     gemm(dense(x), dense(w_bf16), dense(out), M, N, K, a_kcontig=True, b_kcontig=True, c_dtype=c_dtype, act=act,
          bias=bias, colmask=colmask, smask=smask, pre_out=pre_out, residual=residual, dropout_p=dropout_p,
          seed=seed, row_len=row_len, len_rows=len_rows, colsum_out=colsum_out,
-         flags=GEMM_PRE_DGK if pre_dgk else 0, dyn=dyn, ln=ln)
+         flags=GEMM_PRE_DGK if pre_dgk else 0, dyn=dyn)
     return out
 
 

@@ -567,8 +567,6 @@ def _bucket_fresh(p) -> bool:
 # instead of re-reading the forward's f in the FFN2 input-gradient epilogue; DPH_FFN_COLPROD=0 keeps the epilogue
 _FFN_COLPROD = os.environ.get("DPH_FFN_COLPROD", "1") != "0"
 _TEACHER_OU = os.environ.get("DPH_TEACHER_OU", "0") == "1"   # A/B: the no-grad attention forward writes o_u / lse
-# the post-norm LayerNorms in the out-projection / FFN2 GEMM launches (DPH_GEMM_LN_TAIL); DPH_LN_TAIL=0: stand-alone
-_LN_TAIL = os.environ.get("DPH_LN_TAIL", "1") != "0"
 
 
 # ---------------------------------------------------------------------------
@@ -1534,7 +1532,7 @@ def _ffn_interm_bwd(dy, sv, db1, dmask, cfg, F_):
 
 
 @K.tagged("ffn")
-def _ffn_forward(cfg, xin, w1, b1, w2, b2, im, lmf, resid, need, sv, ln=None):
+def _ffn_forward(cfg, xin, w1, b1, w2, b2, im, lmf, resid, need, sv):
     """FeedForward (components.py:726-748) + dropout + layer mask + residual: resid + drop(FFN(xin)) * lmf.
 
     Training with sampled intermediate masks (``im``, HardConcrete interm units): the units whose mask is exactly
@@ -1580,15 +1578,14 @@ def _ffn_forward(cfg, xin, w1, b1, w2, b2, im, lmf, resid, need, sv, ln=None):
         f = K.linear_fwd(xin, W1g, b1g, act=K.ACT_GELU, pre_out=u, colmask=mg, dropout_p=cfg["p_interm"],
                          seed=seed_i, pre_dgk=True, dyn=(ext, 0))
         out = K.linear_fwd(f, W2g, b2, smask=lmf, residual=resid, dropout_p=cfg["p_drop"], seed=seed_o,
-                           pre_out=y_pre, dyn=(ext, 3), ln=ln)
+                           pre_out=y_pre, dyn=(ext, 3))
         sv.update(W1=W1, W2=W2, W1g=W1g, W2g=W2g, W1gT=W1gT, W2gT=W2gT, idx=idx, ext=ext, Fc=Fc, u=u, f=f,
                   y_pre=y_pre, seed_i=seed_i, seed_o=seed_o, F=F_, imp=mg, dgk=True, compact=True)
         return out
     u = torch.empty(M, Fp, dtype=BF16, device=dev) if need else None
     f = K.linear_fwd(xin, W1, b1p, act=K.ACT_GELU, pre_out=u, colmask=imp, dropout_p=cfg["p_interm"],
                      seed=seed_i, pre_dgk=dgk)
-    out = K.linear_fwd(f, W2, b2, smask=lmf, residual=resid, dropout_p=cfg["p_drop"], seed=seed_o, pre_out=y_pre,
-                       ln=ln)
+    out = K.linear_fwd(f, W2, b2, smask=lmf, residual=resid, dropout_p=cfg["p_drop"], seed=seed_o, pre_out=y_pre)
     sv.update(W1=W1, W2=W2, u=u, f=f, y_pre=y_pre, seed_i=seed_i, seed_o=seed_o, F=F_, imp=imp, dgk=dgk,
               compact=False)
     return out
@@ -1683,32 +1680,26 @@ class EncoderLayerFn(torch.autograd.Function):
             Wo = bf16_image(wo)
             seed_d = SEEDS.next() if cfg["p_drop"] > 0 else 0
             a_pre = torch.empty(M, D, dtype=BF16, device=dev) if (need and lma is not None) else None
-        h1 = torch.empty_like(h)
-        mu1 = torch.empty(M, dtype=F32, device=dev)
-        rs1 = torch.empty(M, dtype=F32, device=dev)
-        if use_att:
-            # the post-norm LayerNorm (components.py:853) rides in the out-projection GEMM's launch (DPH_GEMM_LN_TAIL)
             s1 = K.linear_fwd(o_m, Wo, bo, smask=lma, residual=h, dropout_p=cfg["p_drop"], seed=seed_d,
-                              pre_out=a_pre, ln=(ln1_w, ln1_b, h1, mu1, rs1) if _LN_TAIL else None)
+                              pre_out=a_pre)
             sv.update(Wqkv=Wqkv, qkv=qkv, o_u=o_u, o_m=o_m, lse=lse, Wo=Wo, a_pre=a_pre, seed_a=seed_a, seed_d=seed_d)
         else:
             s1 = h
-        if not (use_att and _LN_TAIL):
-            call("dph_layernorm_fwd", ptr(s1), None, ptr(ln1_w), ptr(ln1_b), ptr(h1), ptr(mu1), ptr(rs1), M, D, 1e-5,
-                 0.0, 0, _s())
+        h1 = torch.empty_like(h)
+        mu1 = torch.empty(M, dtype=F32, device=dev)
+        rs1 = torch.empty(M, dtype=F32, device=dev)
+        call("dph_layernorm_fwd", ptr(s1), None, ptr(ln1_w), ptr(ln1_b), ptr(h1), ptr(mu1), ptr(rs1), M, D, 1e-5, 0.0,
+             0, _s())
         # ---------------- feed-forward block ----------------
+        if use_ff:
+            s2 = _ffn_forward(cfg, h1, w1, b1, w2, b2, im, lmf, h1, need, sv)
+        else:
+            s2 = h1
         out = torch.empty_like(h)
         mu2 = torch.empty(M, dtype=F32, device=dev)
         rs2 = torch.empty(M, dtype=F32, device=dev)
-        if use_ff:
-            # (components.py:856's LayerNorm in the FFN2 GEMM's launch)
-            s2 = _ffn_forward(cfg, h1, w1, b1, w2, b2, im, lmf, h1, need, sv,
-                              ln=(ln2_w, ln2_b, out, mu2, rs2) if _LN_TAIL else None)
-        else:
-            s2 = h1
-        if not (use_ff and _LN_TAIL):
-            call("dph_layernorm_fwd", ptr(s2), None, ptr(ln2_w), ptr(ln2_b), ptr(out), ptr(mu2), ptr(rs2), M, D, 1e-5,
-                 0.0, 0, _s())
+        call("dph_layernorm_fwd", ptr(s2), None, ptr(ln2_w), ptr(ln2_b), ptr(out), ptr(mu2), ptr(rs2), M, D, 1e-5,
+             0.0, 0, _s())
         if need:
             ctx.cfg = cfg
             ctx.sv = sv

@@ -116,19 +116,6 @@ typedef struct DphGemmArgs {
    * packed active units (dph_ffn_compact) read the active count this way inside a captured step graph.
    * Ping-pong kernels only (pp_gemm_kernel: m / n / k, ppw_gemm_kernel: m / n); NULL = static.            */
   const int32_t* dyn_ext;
-  /* DPH_GEMM_LN_TAIL: the post-norm LayerNorm of the stored output (components.py:853, :856: the out-projection /
-   * FFN2 output + residual, then nn.LayerNorm over the N columns, eps 1e-5) inside the same launch: the last of a
-   * row strip's column tiles to finish normalises the strip -> ln_out (bf16, row stride N), ln_mean / ln_rstd [M].
-   * ln_tickets: >= ceil(M / 128) uint32 of caller-owned device memory, zero before the first use and left zero by
-   * every launch (one buffer per stream: two launches running at once must not share it).  Taken by the ping-pong
-   * kernels when N == 768, C is dense bf16 and neither split-K, batching nor dyn_ext is in use; otherwise dph_gemm
-   * runs the stand-alone LayerNorm after the GEMM (same arithmetic, same result). */
-  const float* ln_gamma;
-  const float* ln_beta;
-  void* ln_out;
-  float* ln_mean;
-  float* ln_rstd;
-  uint32_t* ln_tickets;
 } DphGemmArgs;
 
 /* flags: one tile per block even where the persistent ring grid applies -- for GEMMs that share the
@@ -142,8 +129,6 @@ typedef struct DphGemmArgs {
  * the layers (components.py:846, :850), whose 2 x L bf16 roundings would otherwise accumulate.  Forward epilogues
  * only (not with DPH_ACT_GELU_BWD / _DGK). */
 #define DPH_GEMM_RESID_F32 4
-/* the fused post-norm LayerNorm tail (DphGemmArgs.ln_*) */
-#define DPH_GEMM_LN_TAIL 8
 
 int dph_gemm(const DphGemmArgs* args, hipStream_t stream);
 /* Grouped (mn, mn) weight gradients: n <= DPH_GEMM_GROUP_MAX independent dW_i (+)= dY_i^T X_i of ONE shape in one

@@ -383,42 +383,3 @@ def test_gelu_dgk_pair_matches_recompute(p):
     live = cm != 0
     close(ca1[live], ca0[live], 2e-2)
     assert torch.count_nonzero(ca1[~live]) == 0
-
-
-@pytest.mark.parametrize("M,K,drop", [(7984, 768, 0.0), (7984, 3072, 0.1), (300, 768, 0.0), (129, 1536, 0.0)])
-def test_ln_tail_matches_standalone_layernorm(M, K, drop):
-    """DPH_GEMM_LN_TAIL (the post-norm LayerNorm of components.py:853 / :856 in the out-projection / FFN2 GEMM's
-    launch, by the last column tile of each row strip) against the same GEMM followed by the stand-alone
-    dph_layernorm_fwd: the GEMM output, the normalised rows and the saved mean / rstd are bitwise equal, and a second
-    launch on the same tickets (left zero by the first) gives the same again."""
-    from dphubert_amd import _lib
-    from dphubert_amd._lib import call, ptr
-    K_ = _k()
-    DEV = "cuda"
-    N = 768
-    g = torch.Generator(device="cpu").manual_seed(M + K)
-    x = (torch.randn(M, K, generator=g) * 0.5).to(DEV, torch.bfloat16)
-    w = (torch.randn(N, K, generator=g) / K ** 0.5).to(DEV, torch.bfloat16)
-    b = torch.randn(N, generator=g).to(DEV)
-    res = torch.randn(M, N, generator=g).to(DEV, torch.bfloat16)
-    gam = (1 + 0.1 * torch.randn(N, generator=g)).to(DEV)
-    bet = (0.1 * torch.randn(N, generator=g)).to(DEV)
-    outs = []
-    for fused in (True, False, True):
-        y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
-        mu = torch.empty(M, device=DEV)
-        rs = torch.empty(M, device=DEV)
-        if fused:
-            s = K_.linear_fwd(x, w, b, residual=res, dropout_p=drop, seed=5, ln=(gam, bet, y, mu, rs))
-        else:
-            s = K_.linear_fwd(x, w, b, residual=res, dropout_p=drop, seed=5)
-            call("dph_layernorm_fwd", ptr(s), None, ptr(gam), ptr(bet), ptr(y), ptr(mu), ptr(rs), M, N, 1e-5, 0.0, 0,
-                 _lib.stream_ptr())
-        torch.cuda.synchronize()
-        outs.append((s, y, mu, rs))
-    for i in (1, 2):
-        for a_, b_ in zip(outs[0], outs[i]):
-            assert torch.equal(a_, b_)
-    assert int(K_.ln_tickets(x.device).abs().sum()) == 0
-    ref = torch.nn.functional.layer_norm(outs[0][0].float(), (N,), gam, bet, 1e-5)
-    assert (outs[0][1].float() - ref).abs().max().item() < 0.05

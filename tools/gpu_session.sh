@@ -27,7 +27,7 @@ for s in $STEPS; do
       rc=$?; echo "bench rc=$rc"; cat "$OUT/bench.json"
       if [ $rc -ne 0 ]; then tail -20 "$OUT/bench.log"; exit $rc; fi ;;
     prof)
-      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run -- \
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/prof" -o run -- \
         python -u bench.py --steps 8 --warmup 3 --no-cpu-baseline --traffic off > "$OUT/prof_bench.json" 2> "$OUT/prof.log"
       rc=$?; echo "prof rc=$rc"
       if [ $rc -ne 0 ]; then tail -20 "$OUT/prof.log"; exit $rc; fi
