@@ -186,7 +186,7 @@ static_assert(RB == RBW, "table window width");
 // one basic block (runtime `if`s split it and kept hipcc from overlapping one query group's
 // softmax with the other group's MFMAs).
 // ---------------------------------------------------------------------------
-template <bool DROP, bool BIAS>
+template <bool DROP, bool BIAS, bool PREC>
 __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(const bf16_t* __restrict__ qkv, float* __restrict__ o_u,
                                                           bf16_t* __restrict__ o_m, float* __restrict__ lse,
                                                           const float* __restrict__ head_mask,
@@ -344,10 +344,19 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(const bf16_t* __restri
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
           const bf16x8_t pf = pack_frag(sacc[u][2 * kk], sacc[u][2 * kk + 1]);
+          bf16x8_t pl;   // PREC: residuals p - bf16(p) (see launch_fwd)
+          if constexpr (PREC) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              pl[j] = (__bf16)(sacc[u][2 * kk][j] - (float)pf[j]);
+              pl[4 + j] = (__bf16)(sacc[u][2 * kk + 1][j] - (float)pf[4 + j]);
+            }
+          }
 #pragma unroll
           for (int d = 0; d < 4; ++d) {
             const bf16x8_t vf = tr_frag(V_, 32 * kk + 4 * g, 32 * kk + 16 + 4 * g, 16 * d, lane);
             oacc[u][d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf, oacc[u][d], 0, 0, 0);
+            if constexpr (PREC) oacc[u][d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pl, oacc[u][d], 0, 0, 0);
           }
         }
       }
@@ -645,7 +654,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd32_kernel(const bf16_t* __rest
 // its 32 x 64 normalised O rows there and re-reads them row-contiguous, so every global store instruction writes
 // whole rows (o_u: 4 rows of 256 B, o_m: 4 rows of 128 B per wave instruction) instead of 16-B / 8-B pieces of 32
 // rows (the store tail of a one-round grid: guide T21, MI355X_MICROARCH 'attention epilogue store tail')
-template <bool DROP, bool STAGE>
+template <bool DROP, bool STAGE, bool PREC>
 __global__ void __launch_bounds__(256, 3) attn_fwd32v2_kernel(const bf16_t* __restrict__ qkv, float* __restrict__ o_u,
                                                              bf16_t* __restrict__ o_m, float* __restrict__ lse,
                                                              const float* __restrict__ head_mask,
@@ -776,6 +785,7 @@ __global__ void __launch_bounds__(256, 3) attn_fwd32v2_kernel(const bf16_t* __re
     // bits < thr, and its arithmetic shift by 15 is the half's drop mask.  Three packed-16 ops and two bitops
     // per PAIR instead of an extract / compare / select / bit-insert per score.
     uint32_t pw[2][4][2];
+    uint32_t pl[2][4][2];        // PREC: bf16 residual words p - bf16(p)
     uint32_t kd[2] = {0u, 0u};   // DROP bits of the rq-even / rq-odd stored words: even key low half, odd high
 #pragma unroll
     for (int k2 = 0; k2 < 2; ++k2)
@@ -791,10 +801,14 @@ __global__ void __launch_bounds__(256, 3) attn_fwd32v2_kernel(const bf16_t* __re
 #pragma unroll
         for (int pi = 0; pi < 2; ++pi) {
           uint32_t w = pack2bf(pv[2 * pi], pv[2 * pi + 1]);
+          if constexpr (PREC)
+            pl[k2][rq][pi] = pack2bf(pv[2 * pi] - __uint_as_float(w << 16),
+                                     pv[2 * pi + 1] - __uint_as_float(w & 0xffff0000u));
           if constexpr (DROP) {
             const uint32_t hsh = attn_hash32(mix, hrow + (uint32_t)((kb + 32 * k2 + 8 * rq) >> 1) + pi);
             const uint32_t m = drop_mask2(hsh, thr2);
             w &= ~m;
+            if constexpr (PREC) pl[k2][rq][pi] &= ~m;
             const int bt = 4 * (2 * k2 + (rq >> 1)) + 2 * pi;
             kd[rq & 1] |= m & ((1u << bt) | (1u << (17 + bt)));
           }
@@ -822,6 +836,10 @@ __global__ void __launch_bounds__(256, 3) attn_fwd32v2_kernel(const bf16_t* __re
         for (int d = 0; d < 2; ++d) {
           const bf16x8_t vf = tr_frag_v(V_, base, base + 8, 32 * d + 16 * ((lane >> 4) & 1), lane);
           oacc[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, oacc[d], 0, 0, 0);
+          if constexpr (PREC) {
+            const uint4 lq = make_uint4(pl[k2][2 * e][0], pl[k2][2 * e][1], pl[k2][2 * e + 1][0], pl[k2][2 * e + 1][1]);
+            oacc[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, __builtin_bit_cast(bf16x8_t, lq), oacc[d], 0, 0, 0);
+          }
         }
       }
     if (more) store_kv(cur ^ 1);
@@ -889,7 +907,7 @@ __global__ void __launch_bounds__(256, 3) attn_fwd32v2_kernel(const bf16_t* __re
 }
 
 // ---------------------------------------------------------------------------
-// backward prep: rowdot[b][h][t] = sum_d dO_m * O_u ; D = hm * rowdot ; dhm[h] += sum rowdot
+// backward prep: rowdot[b][h][t] = sum_d dO_m * O_u ; D = sum_d bf16(hm * dO_m) * O_u ; dhm[h] += sum rowdot
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) attn_bwd_prep_kernel(const bf16_t* __restrict__ dom,
                                                             const float* __restrict__ ou,
@@ -900,7 +918,7 @@ __global__ void __launch_bounds__(256) attn_bwd_prep_kernel(const bf16_t* __rest
   __shared__ float red[4];
   const int64_t h = blockIdx.y;
   const int64_t bt = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  float rd = 0.f;
+  float rd = 0.f, rs = 0.f;   // rowdot(dO_m, O_u) (head-mask gradient) / rowdot(dO', O_u) (D)
   const float hmh = head_mask ? head_mask[h] : 1.0f;
   if (bt < B * T && hmh == 0.f) {
     // skipped head (attn_fwd32_kernel): its unmasked output was never written
@@ -917,13 +935,20 @@ __global__ void __launch_bounds__(256) attn_bwd_prep_kernel(const bf16_t* __rest
       uint32_t wa[4] = {va.x, va.y, va.z, va.w};
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        rd += __uint_as_float(wa[q] << 16) * wc[2 * q];
-        rd += __uint_as_float(wa[q] & 0xffff0000u) * wc[2 * q + 1];
+        const float a0 = __uint_as_float(wa[q] << 16), a1 = __uint_as_float(wa[q] & 0xffff0000u);
+        rd += a0 * wc[2 * q];
+        rd += a1 * wc[2 * q + 1];
+        // D against the dO' = bf16(hm * dO_m) the dK / dV and dQ kernels multiply V by (scale_bf16x8): D must equal
+        // sum_j P_j dP_j for THOSE dP_j, or dS = P (dP - D) keeps a row sum of (hm dO_m - dO') . O, which the
+        // O-weighted key sums of dQ / dK then multiply by the keys' common component (a 0.99 head mask put the
+        // 12-layer fixture's last-layer dW_q off by 50 %)
+        const uint32_t sw = pack2bf(a0 * hmh, a1 * hmh);
+        rs += __uint_as_float(sw << 16) * wc[2 * q];
+        rs += __uint_as_float(sw & 0xffff0000u) * wc[2 * q + 1];
       }
     }
     const int64_t bb = bt / T, t = bt % T;
-    const float hm = head_mask ? head_mask[h] : 1.0f;
-    Dv[(bb * H + h) * T + t] = rd * hm;
+    Dv[(bb * H + h) * T + t] = rs;
   }
   if (!dhm) return;
   float s = wave_sum(rd);
@@ -1526,22 +1551,31 @@ template <bool DROP, bool BIAS>
 void launch_fwd(dim3 grid, hipStream_t stream, const void* qkv, void* o_u, void* o_m, float* lse, const float* hm,
                 const int64_t* key_len, AttnShape sh, float scale, float p, uint64_t seed, RelBias rb, void* keep) {
   const int mode = BIAS ? 0 : fwd32_mode();
+  static const bool prec_env = [] {
+    const char* e = getenv("DPH_ATTN_PREC");
+    return !(e && e[0] == '0');
+  }();
+  const bool prec = prec_env && o_u != nullptr;
   if (mode == 2) {
-    // DPH_ATTN_EPI=0: the per-lane scattered epilogue stores (A/B)
+    // DPH_ATTN_EPI=0: the per-lane scattered epilogue stores (A/B).  PREC (a forward whose O_u feeds a backward,
+    // unless DPH_ATTN_PREC=0): O accumulates P as bf16(P) + bf16(P - bf16(P)), so D = dO . O_u equals
+    // sum_j P_j dP_j to ~2^-17 and dS = P (dP - D) keeps its row sums near zero on saturated rows
     static const bool staged = [] {
       const char* e = getenv("DPH_ATTN_EPI");
       return !(e && e[0] == '0');
     }();
-    if (staged)
-      hipLaunchKernelGGL((attn_fwd32v2_kernel<DROP, true>), grid, dim3(256), 0, stream,
-                         reinterpret_cast<const bf16_t*>(qkv), reinterpret_cast<float*>(o_u),
-                         reinterpret_cast<bf16_t*>(o_m), lse, hm, key_len, sh, scale, p, seed,
-                         reinterpret_cast<uint16_t*>(keep));
-    else
-      hipLaunchKernelGGL((attn_fwd32v2_kernel<DROP, false>), grid, dim3(256), 0, stream,
-                         reinterpret_cast<const bf16_t*>(qkv), reinterpret_cast<float*>(o_u),
-                         reinterpret_cast<bf16_t*>(o_m), lse, hm, key_len, sh, scale, p, seed,
-                         reinterpret_cast<uint16_t*>(keep));
+    auto go = [&](auto kern) {
+      hipLaunchKernelGGL(kern, grid, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(qkv),
+                         reinterpret_cast<float*>(o_u), reinterpret_cast<bf16_t*>(o_m), lse, hm, key_len, sh, scale,
+                         p, seed, reinterpret_cast<uint16_t*>(keep));
+    };
+    if (staged) {
+      if (prec) go(attn_fwd32v2_kernel<DROP, true, true>);
+      else go(attn_fwd32v2_kernel<DROP, true, false>);
+    } else {
+      if (prec) go(attn_fwd32v2_kernel<DROP, false, true>);
+      else go(attn_fwd32v2_kernel<DROP, false, false>);
+    }
     return;
   }
   if (mode == 1) {
@@ -1551,9 +1585,13 @@ void launch_fwd(dim3 grid, hipStream_t stream, const void* qkv, void* o_u, void*
     return;
   }
   const size_t tw_bytes = BIAS ? (size_t)(sh.T + RB - 1) * sizeof(float) : 0;
-  hipLaunchKernelGGL((attn_fwd_kernel<DROP, BIAS>), grid, dim3(256), tw_bytes, stream, reinterpret_cast<const bf16_t*>(qkv),
-                     reinterpret_cast<float*>(o_u), reinterpret_cast<bf16_t*>(o_m), lse, hm, key_len, sh, scale, p,
-                     seed, rb, reinterpret_cast<uint16_t*>(keep));
+  auto go16 = [&](auto kern) {
+    hipLaunchKernelGGL(kern, grid, dim3(256), tw_bytes, stream, reinterpret_cast<const bf16_t*>(qkv),
+                       reinterpret_cast<float*>(o_u), reinterpret_cast<bf16_t*>(o_m), lse, hm, key_len, sh, scale, p,
+                       seed, rb, reinterpret_cast<uint16_t*>(keep));
+  };
+  if (prec) go16(attn_fwd_kernel<DROP, BIAS, true>);
+  else go16(attn_fwd_kernel<DROP, BIAS, false>);
 }
 
 template <bool DROP, bool BIAS, bool KEEP>

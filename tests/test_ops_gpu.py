@@ -108,46 +108,69 @@ def test_attention_kernel_vs_torch(fwd, T, short, amp, zero_head, monkeypatch):
     assert torch.count_nonzero(dqkv.float().view(B * T, 3, D)[:, :, ~live[0]]) == 0
 
 
-@pytest.mark.parametrize("sharp", [1.0, 16.0])
-def test_attention_backward_vs_fp64_on_same_inputs(sharp):
-    """The attention backward against fp64 torch on the SAME bf16 q/k/v/dO (isolates the kernel's arithmetic from
-    upstream bf16 drift).  sharp = 6 scales q so the softmax is nearly one-hot (the regime of the deep layers of the
-    12-layer fixture, where dS = P (dP - D) cancels to a tiny value): the fp32 O the forward saves keeps D consistent
-    with sum_j P_j dP_j, so dQ / dK stay within a few bf16 ulps."""
+@pytest.mark.parametrize("regime", ["plain", "sharp", "collapsed"])
+def test_attention_backward_vs_fp64_on_same_inputs(regime):
+    """The attention backward against fp64 torch on the SAME bf16 q/k/v/dO and head mask (isolates the kernel's
+    arithmetic from upstream bf16 drift).  sharp: q x 16, the softmax nearly one-hot (dS = P (dP - D) cancels to a
+    tiny value).  collapsed: the regime of the 12-layer fixture's last layer (tools/attn_probe.py) -- every frame's
+    q / k / v is one large common vector (norm ~27) plus a ~1 % deviation, so attention is near uniform and dQ / dK are
+    small differences of large key / value sums -- with head masks 0.9933 and 1.  There D must be the row dot of O
+    with the SAME bf16(hm dO_m) the kernels multiply V by, and O must carry P to ~2^-17 (bf16 hi + lo parts): with
+    D from the unrounded hm dO_m the masked head's dQ was off by 100 %, with a bf16-P O by 33 %.  What remains is the
+    floor of a bf16 dS MFMA operand (its rounding leaves each dS row a nonzero sum that dQ multiplies by the keys'
+    common component: ~14 % of this dQ, while dW_q = dQ^T X stays within 1e-3 -- tools/attn_probe.py), so each part
+    is held to 1e-2 + 1.25 x that floor, computed here in fp64."""
     from dphubert_amd import _lib
     from dphubert_amd._lib import call, ptr
     torch.manual_seed(4)
     B, T, H = 2, 499, 2
     D = H * 64
-    qkv = torch.randn(B * T, 3 * D, device=DEV)
-    qkv[:, :D] *= sharp
+    if regime == "collapsed":
+        common = torch.randn(1, 3 * D, device=DEV) * 3.4
+        qkv = common + 0.04 * torch.randn(B * T, 3 * D, device=DEV)
+        hm = torch.tensor([0.9933, 1.0], device=DEV)
+    else:
+        qkv = torch.randn(B * T, 3 * D, device=DEV)
+        if regime == "sharp":
+            qkv[:, :D] *= 16.0
+        hm = torch.ones(H, device=DEV)
     qkv = qkv.to(torch.bfloat16)
     g = torch.randn(B * T, D, device=DEV).to(torch.bfloat16)
     s = _lib.stream_ptr()
     o_u = torch.empty(B * T, D, device=DEV, dtype=torch.float32)
     o_m = torch.empty(B * T, D, device=DEV, dtype=torch.bfloat16)
     lse = torch.empty(B * H * T, device=DEV)
-    call("dph_attention_fwd", ptr(qkv), ptr(o_u), ptr(o_m), ptr(lse), None, None, B, T, H, 0.125, 0.0, 0, None, s)
+    call("dph_attention_fwd", ptr(qkv), ptr(o_u), ptr(o_m), ptr(lse), ptr(hm), None, B, T, H, 0.125, 0.0, 0, None, s)
     Dv = torch.empty(B * H * T, device=DEV)
-    call("dph_attention_bwd_prep", ptr(g), ptr(o_u), None, ptr(Dv), None, B, T, H, None, 0, s)
+    dhm = torch.zeros(H, device=DEV)
+    call("dph_attention_bwd_prep", ptr(g), ptr(o_u), ptr(hm), ptr(Dv), ptr(dhm), B, T, H, *prep_ws(B, T, H), s)
     dqkv = torch.empty_like(qkv)
-    call("dph_attention_bwd", ptr(qkv), ptr(g), None, ptr(lse), ptr(Dv), ptr(dqkv), None, B, T, H, 0.125, 0.0, 0, None, s)
+    call("dph_attention_bwd", ptr(qkv), ptr(g), ptr(hm), ptr(lse), ptr(Dv), ptr(dqkv), None, B, T, H, 0.125, 0.0, 0,
+         None, s)
     x = qkv.double().clone().requires_grad_(True)
     q, k, v = x.view(B, T, 3, H, 64).permute(2, 0, 3, 1, 4)
     w = (0.125 * q) @ k.transpose(-1, -2)
     p = torch.softmax(w - w.max(-1, keepdim=True)[0], -1)
-    o = (p @ v).permute(0, 2, 1, 3).reshape(B * T, D)
-    o.backward(g.double())
+    o = (p @ v) * hm.double().view(1, H, 1, 1)
+    o.permute(0, 2, 1, 3).reshape(B * T, D).backward(g.double())
     torch.cuda.synchronize()
-    assert rel_l2(o_u.double(), o.detach()) < 5e-3
-    if sharp > 1:
+    assert rel_l2(o_u.double(), (p @ v).detach().permute(0, 2, 1, 3).reshape(B * T, D)) < 5e-3
+    if regime == "sharp":
         assert p.max(-1)[0].mean().item() > 0.8      # really saturated
+    if regime == "collapsed":
+        assert p.max(-1)[0].mean().item() < 3.0 / T  # really near uniform
+    with torch.no_grad():   # the bf16-dS floor: the exact dS rounded to bf16, contracted in fp64
+        do = g.double().view(B, T, H, 64).permute(0, 2, 1, 3) * hm.double().view(1, H, 1, 1)
+        dS = p * (do @ v.transpose(-1, -2) - (do * (p @ v)).sum(-1, keepdim=True))
+        dSb = dS.to(torch.bfloat16).double()
+        floor = [rel_l2(0.125 * dSb @ k, 0.125 * dS @ k), rel_l2(0.125 * dSb.transpose(-1, -2) @ q,
+                                                                 0.125 * dS.transpose(-1, -2) @ q), 0.0]
     for part in range(3):
         a = dqkv.double().view(B * T, 3, D)[:, part]
         b = x.grad.view(B * T, 3, D)[:, part]
         e = rel_l2(a, b)
-        print(f"sharp {sharp} part {part}: rel-L2 {e:.3g}")
-        assert e < 1e-2, (part, e)
+        print(f"{regime} part {part}: rel-L2 {e:.3g} (bf16-dS floor {floor[part]:.3g})")
+        assert e < 1e-2 + 1.25 * floor[part], (part, e, floor[part])
 
 
 def test_attention_dropout_consistency():
