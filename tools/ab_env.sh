@@ -1,17 +1,22 @@
 #!/bin/bash
-# A/B of environment switches on the default bench line, one bench process per arm, same box:
-#   bash tools/ab_env.sh TAG "ENV=1 OTHER=2" "ENV=0" ...   (an empty string = the default arm)
-#   BENCH_ARGS="--model large" picks another configuration
-set -o pipefail
-TAG=$1; shift
-R=${GRAFT_REPO_ROOT:-$(pwd)}
-O=$R/gpurun_out/$TAG
-mkdir -p "$O"
-cd "$R" || exit 1
-i=0
-for ARM in "$@"; do
-  i=$((i+1))
-  env $ARM timeout -k 10 200 python -u bench.py $BENCH_ARGS --steps 20 --warmup 3 --no-cpu-baseline --traffic off --no-roofline \
-    > "$O/ab_$i.json" 2> "$O/ab_$i.err" || { echo "arm $i ($ARM) failed"; tail -5 "$O/ab_$i.err"; exit 1; }
-  echo "arm $i [$ARM]: $(python3 -c "import json,sys; d=json.load(open('$O/ab_$i.json')); print(d['ms_per_step'], 'ms', d['value'], 'audio-s/s')")"
+# Same-box A/B of environment switches on the default bench step (no CPU baseline, no PMC passes), variants
+# interleaved over REPS rounds so box drift hits them alike.  Usage (from the repo root, through gpurun):
+#   tools/ab_env.sh OUTFILE REPS "ENV=a ENV2=b" "ENV=c" ...
+# Each variant's bench line is appended to OUTFILE with its env prefix; a step that fails ends the run.
+set -u
+OUT=${1:?usage: tools/ab_env.sh OUTFILE REPS VARIANT...}
+REPS=${2:?}
+shift 2
+mkdir -p "$(dirname "$OUT")"
+export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
+for r in $(seq 1 "$REPS"); do
+  for v in "$@"; do
+    line=$(env $v timeout -k 10 300 python -u bench.py --steps 30 --warmup 3 --no-cpu-baseline --traffic off \
+           2> /tmp/ab_err.log)
+    rc=$?
+    if [ $rc -ne 0 ]; then echo "variant [$v] rc=$rc"; tail -20 /tmp/ab_err.log; exit $rc; fi
+    ms=$(python -c "import json,sys; print(json.loads(sys.argv[1])['ms_per_step'])" "$line")
+    echo "round $r [$v] ${ms} ms/step" | tee -a "$OUT.txt"
+    echo "[$v] $line" >> "$OUT.jsonl"
+  done
 done
