@@ -261,8 +261,8 @@ def bucketed_batches(n: int, seconds_per_batch: float, rank: int, dev):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=None,
                     help="utterances per GPU per micro-batch (default: 16 = run.sh's 160 s per GPU; 8 for --student "
                          "pruned = 640 s over 8 GPUs, SURVEY 8(d) config 4; 6 for --model large = run_large.sh's 60 s)")

@@ -69,6 +69,9 @@ _SIGS = {
     "dph_abi_version": ([], C.c_int),
     "dph_set_deterministic": ([C.c_int], C.c_int),
     "dph_get_deterministic": ([], C.c_int),
+    "dph_defer_reductions": ([C.c_int], C.c_int),
+    "dph_flush_reductions": ([S], C.c_int),
+    "dph_deferred_reductions": ([], i64),
     "dph_gemm": ([C.POINTER(DphGemmArgs), S], C.c_int),
     "dph_gemm_mn_plan": ([i64, i64, i64, i64], C.c_int),
     "dph_gemm_grouped": ([C.POINTER(DphGemmArgs), C.POINTER(DphGemmGroup), S], C.c_int),
@@ -167,8 +170,9 @@ _lib = None
 # workspaces; 12: dph_hc_bank_fwd / dph_hc_bank_bwd; 15: dph_gemm_mn_plan; 16: DphGemmArgs.dyn_ext, dph_ffn_compact + gathers / scatters;
 # 19: DPH_GEMM_RESID_F32, dph_layernorm_fwd_x32 / _bwd_res32, dph_branch_bwd_f32, dph_distill_loss_*_ex: the fp32
 # pre-norm residual stream; 20: deterministic mode -- dph_set_deterministic / dph_get_deterministic and the workspaces
-# of the fixed-order reductions: attention prep / relpos backward, WavLM gate, conv0, GELU-mask and branch backward)
-ABI_VERSION = 20
+# of the fixed-order reductions: attention prep / relpos backward, WavLM gate, conv0, GELU-mask and branch backward;
+# 21: deferred column reductions -- dph_defer_reductions / dph_flush_reductions / dph_deferred_reductions)
+ABI_VERSION = 21
 
 
 class DphError(RuntimeError):

@@ -26,6 +26,10 @@ void set_error(const char* fmt, ...);
 int check_launch(const char* what);
 // deterministic mode (runtime.hip, dph_set_deterministic): fixed-order cross-block reductions instead of float atomics
 bool deterministic();
+// deferred fixed-order column reductions (runtime.hip, dph_defer_reductions): while deferring, a slab reduction
+// out[j] += sum_r ws[r * ld + j] (j < n) is queued by colred_push and launched with the rest by dph_flush_reductions
+bool colred_deferring();
+void colred_push(const float* ws, int64_t nrows, int64_t ld, int64_t n, float* out, hipStream_t stream);
 // norm.hip: o_q[c] += sum_r ws[r][q * seg + c] over the column segments q of a [nrows][ncols] fp32 partial slab (NULL
 // outputs skipped); fixed order in deterministic mode, row groups + one atomic per column per group otherwise
 void slab_reduce_cols(const float* ws, int64_t nrows, int64_t ncols, int64_t seg, float* o0, float* o1, float* o2,

@@ -3281,7 +3281,11 @@ extern "C" int dph_gemm(const DphGemmArgs* args, hipStream_t stream) {
     const int64_t csn = std::min<int64_t>(a.colsum_n > 0 ? a.colsum_n : a.N, a.N);
     // (>= 16 slab rows per group: a few hundred blocks even at N = 768, each thread's rows in flight together;
     // deterministic mode: each column's rows in a fixed order)
-    if (deterministic()) {
+    if (colred_deferring()) {
+      const float* sl = reinterpret_cast<const float*>(a.workspace);
+      colred_push(sl, nslots, a.N, csn, a.colsum_out, stream);
+      colred_push(sl + nslots * a.N, nslots, a.N, csn, a.colsum_aux, stream);
+    } else if (deterministic()) {
       hipLaunchKernelGGL(colsum_slab_reduce_det_kernel, dim3((unsigned)cdiv(csn, 32)), dim3(32 * DET_PH), 0, stream,
                          reinterpret_cast<const float*>(a.workspace), nslots, a.N, csn, a.colsum_out, a.colsum_aux);
     } else {

@@ -527,6 +527,12 @@ __global__ void __launch_bounds__(64) sdot_reduce_kernel(const float* __restrict
 
 void slab_reduce_launch(const float* ws, int64_t nrows, int64_t ncols, int64_t seg, float* o0, float* o1, float* o2,
                         hipStream_t stream) {
+  if (colred_deferring()) {
+    float* outs[3] = {o0, o1, o2};
+    for (int q = 0; q < 3 && q * seg < ncols; ++q)
+      colred_push(ws + q * seg, nrows, ncols, std::min<int64_t>(seg, ncols - q * seg), outs[q], stream);
+    return;
+  }
   if (deterministic())
     hipLaunchKernelGGL(slab_reduce_det_kernel, dim3((unsigned)cdiv(ncols, 32)), dim3(32 * DET_PH), 0, stream, ws,
                        nrows, ncols, seg, o0, o1, o2);
@@ -590,6 +596,17 @@ __global__ void __launch_bounds__(256) ln_fwd16_kernel(const XT* __restrict__ x,
       for (int i = 0; i < 8; ++i) v[c][i] = 0.f;
     }
   }
+  // gamma / beta issued with the row loads (after the statistics they were one more dependent load latency of a
+  // one-round grid)
+  float4 gb[NC][4];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int col = (c * 32 + hl) * 8;
+    gb[c][0] = *reinterpret_cast<const float4*>(gamma + col);
+    gb[c][1] = *reinterpret_cast<const float4*>(gamma + col + 4);
+    gb[c][2] = *reinterpret_cast<const float4*>(beta + col);
+    gb[c][3] = *reinterpret_cast<const float4*>(beta + col + 4);
+  }
   float s = 0.f;
 #pragma unroll
   for (int c = 0; c < NC; ++c)
@@ -613,8 +630,7 @@ __global__ void __launch_bounds__(256) ln_fwd16_kernel(const XT* __restrict__ x,
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
     const int col = (c * 32 + hl) * 8;
-    const float4 g0 = *reinterpret_cast<const float4*>(gamma + col), g1 = *reinterpret_cast<const float4*>(gamma + col + 4);
-    const float4 b0 = *reinterpret_cast<const float4*>(beta + col), b1 = *reinterpret_cast<const float4*>(beta + col + 4);
+    const float4 g0 = gb[c][0], g1 = gb[c][1], b0 = gb[c][2], b1 = gb[c][3];
     const float ga[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
     const float be[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
     float o[8];
@@ -653,6 +669,8 @@ __global__ void __launch_bounds__(512) ln_bwd16_kernel(
   const int64_t row = ((int64_t)blockIdx.x * 8 + wave) * 2 + (lane >> 5);
   const bool ok = row < rows;
   float xh[NC][8], g[NC][8], dyv[NC][8], ga[NC][8];
+  const float mean = ok ? mean_in[row] : 0.f;
+  const float rstd = ok ? rstd_in[row] : 0.f;
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
     const int64_t off = row * D + (c * 32 + hl) * 8;
@@ -664,15 +682,19 @@ __global__ void __launch_bounds__(512) ln_bwd16_kernel(
       for (int i = 0; i < 8; ++i) xh[c][i] = dyv[c][i] = 0.f;
     }
   }
-  const float mean = ok ? mean_in[row] : 0.f;
-  const float rstd = ok ? rstd_in[row] : 0.f;
+  float4 gq[NC][2];   // gamma, issued with the row loads
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int col = (c * 32 + hl) * 8;
+    gq[c][0] = *reinterpret_cast<const float4*>(gamma + col);
+    gq[c][1] = *reinterpret_cast<const float4*>(gamma + col + 4);
+  }
   const float binv_keep = branch_p > 0.f ? 1.f / (1.f - branch_p) : 1.f;
   const float bsm = branch_smask ? *branch_smask : 1.0f;
   float s1 = 0.f, s2 = 0.f;
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
-    const int col = (c * 32 + hl) * 8;
-    const float4 g0 = *reinterpret_cast<const float4*>(gamma + col), g1 = *reinterpret_cast<const float4*>(gamma + col + 4);
+    const float4 g0 = gq[c][0], g1 = gq[c][1];
     ga[c][0] = g0.x; ga[c][1] = g0.y; ga[c][2] = g0.z; ga[c][3] = g0.w;
     ga[c][4] = g1.x; ga[c][5] = g1.y; ga[c][6] = g1.z; ga[c][7] = g1.w;
 #pragma unroll

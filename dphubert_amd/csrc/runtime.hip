@@ -5,6 +5,8 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <vector>
+
 namespace dph {
 namespace {
 thread_local char g_err[1024] = {0};
@@ -49,10 +51,95 @@ bool deterministic() {
   }
   return g_det != 0;
 }
+
+// ---- deferred column reductions (deterministic mode) -------------------------------------------
+// Between dph_defer_reductions(1) and (0) the fixed-order partial-slab column reductions (LayerNorm affine / branch
+// bias gradients, dph_colsum*, GEMM epilogue column sums) are queued instead of launched -- each is a ~4 us launch
+// of a 32-column x DET_PH-phase grid -- and dph_flush_reductions launches the queue as ONE grid (up to RED_MAXP
+// problems per launch), each problem summed exactly as its own launch would (det_column_total), so the results are
+// bitwise those of the immediate launches.  The caller keeps every queued slab alive and its outputs unread until
+// the flush; two queued problems never write overlapping outputs (an overlapping one flushes the queue first).
+namespace {
+struct ColRed {
+  const float* ws;   // row 0 of the problem's first column
+  float* out;        // out[j] += sum_r ws[r * ld + j], j < n
+  int32_t nrows, ld, n, pad;
+};
+constexpr int RED_MAXP = 96;
+struct ColRedBatch {
+  int32_t np;
+  int32_t pre[RED_MAXP + 1];   // first 32-column block of each problem
+  ColRed p[RED_MAXP];
+};
+static_assert(sizeof(ColRedBatch) <= 4096, "kernel argument limit");
+
+__global__ void __launch_bounds__(32 * DET_PH) colred_batch_kernel(const ColRedBatch b) {
+  __shared__ float red[DET_PH][33];
+  const int bx = (int)blockIdx.x;
+  int k = 0;
+  while (k + 1 < b.np && b.pre[k + 1] <= bx) ++k;
+  const float* ws = b.p[k].ws;
+  float* out = b.p[k].out;
+  const int64_t col = (int64_t)(bx - b.pre[k]) * 32 + (threadIdx.x & 31);
+  const bool live = col < b.p[k].n;
+  const float t = det_column_total(live ? ws + col : nullptr, b.p[k].nrows, b.p[k].ld, red);
+  if ((threadIdx.x >> 5) == 0 && live) out[col] += t;
+}
+
+bool g_defer = false;
+std::vector<ColRed> g_redq;
+hipStream_t g_redq_stream = nullptr;
+
+int flush_redq() {
+  size_t i = 0;
+  while (i < g_redq.size()) {
+    ColRedBatch b{};
+    int blocks = 0;
+    while (i < g_redq.size() && b.np < RED_MAXP) {
+      b.pre[b.np] = blocks;
+      b.p[b.np] = g_redq[i++];
+      blocks += (int)cdiv(b.p[b.np].n, 32);
+      ++b.np;
+    }
+    b.pre[b.np] = blocks;
+    hipLaunchKernelGGL(colred_batch_kernel, dim3((unsigned)blocks), dim3(32 * DET_PH), 0, g_redq_stream, b);
+    const int rc = check_launch("dph_flush_reductions");
+    if (rc != DPH_OK) {
+      g_redq.clear();
+      return rc;
+    }
+  }
+  g_redq.clear();
+  return DPH_OK;
+}
+}  // namespace
+
+bool colred_deferring() { return g_defer && deterministic(); }
+
+void colred_push(const float* ws, int64_t nrows, int64_t ld, int64_t n, float* out, hipStream_t stream) {
+  if (n <= 0 || out == nullptr) return;
+  bool clash = !g_redq.empty() && stream != g_redq_stream;
+  for (const ColRed& q : g_redq)
+    if (out < q.out + q.n && q.out < out + n) clash = true;
+  if (clash) flush_redq();
+  g_redq.push_back(ColRed{ws, out, (int32_t)nrows, (int32_t)ld, (int32_t)n, 0});
+  g_redq_stream = stream;
+}
 }  // namespace dph
 
+extern "C" int dph_defer_reductions(int on) {
+  dph::g_defer = on != 0;
+  return DPH_OK;
+}
+extern "C" int64_t dph_deferred_reductions(void) { return (int64_t)dph::g_redq.size(); }
+extern "C" int dph_flush_reductions(hipStream_t stream) {
+  if (dph::g_redq.empty()) return DPH_OK;
+  DPH_REQUIRE(stream == dph::g_redq_stream, "dph_flush_reductions: the queued reductions were issued on another stream");
+  return dph::flush_redq();
+}
+
 extern "C" const char* dph_last_error(void) { return dph::g_err; }
-extern "C" int dph_abi_version(void) { return 20; }
+extern "C" int dph_abi_version(void) { return 21; }
 extern "C" int dph_set_deterministic(int on) {
   dph::g_det = on ? 1 : 0;
   return DPH_OK;

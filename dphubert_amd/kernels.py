@@ -237,6 +237,11 @@ class shared_gpu:
         _SHARED_GPU[0] -= 1
 
 
+# ops.deferred_reductions: while set, the list that keeps every column-sum workspace alive until the queued
+# reductions that read it are flushed
+KEEP_WS = [None]
+
+
 def gemm(A: DphMat, B: DphMat, Cm: DphMat, M: int, N: int, K: int, *, a_kcontig: bool, b_kcontig: bool,
          c_dtype: int = OUT_BF16, act: int = ACT_NONE, alpha: float = 1.0, batch: int = 1, splits: int = 1,
          bias=None, colmask=None, smask=None, vec_z_inner: int = 0, pre_out=None, aux_in=None, residual=None,
@@ -260,6 +265,8 @@ def gemm(A: DphMat, B: DphMat, Cm: DphMat, M: int, N: int, K: int, *, a_kcontig:
         n_el = 2 * batch * ((M + 63) // 64) * N
         ws_bytes = n_el * 4
         ws = torch.empty(n_el, dtype=F32, device=device or Cm_device(colsum_out, colsum_aux))
+        if KEEP_WS[0] is not None:
+            KEEP_WS[0].append(ws)
     args = DphGemmArgs(M, N, K, batch, splits, int(a_kcontig), int(b_kcontig), A, B, Cm, c_dtype, act, alpha,
                        dropout_p, seed & 0xFFFFFFFFFFFFFFFF, ptr(bias), ptr(colmask), ptr(smask), vec_z_inner,
                        ptr(pre_out), ptr(aux_in), ptr(residual), ptr(colsum_out), ptr(colsum_aux), ptr(row_len),

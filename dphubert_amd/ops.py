@@ -47,8 +47,12 @@ def _s():
 
 def _ws(nbytes: int, dev):
     """Scratch for a column-partial slab (stream-ordered caching allocator: the block is reused only
-    by work queued after the kernel that consumes it)."""
+    by work queued after the kernel that consumes it -- inside a deferred_reductions block the slab is kept
+    alive until the block's flush, which is then that consumer)."""
     t = torch.empty(max(int(nbytes), 4) // 4, dtype=F32, device=dev)
+    keep = K.KEEP_WS[0]
+    if keep is not None:
+        keep.append(t)
     return ptr(t), t.numel() * 4
 
 
@@ -525,7 +529,89 @@ def _flush_wgrads_hook(grad):
     q = _WGRAD_DEFER[0]
     if q is not None:
         q.flush()
+    r = _RED_DEFER[0]
+    if r is not None:
+        r.close()
     return None
+
+
+# ---------------------------------------------------------------------------
+# deferred column reductions (Trainer: one backward = one deferred_reductions block)
+# ---------------------------------------------------------------------------
+# In deterministic mode each bias / LayerNorm-affine gradient is a per-block partial slab summed in a fixed order
+# by its own small grid (~4-5 us each, ~50 per encoder backward).  Inside a deferred_reductions block the ones whose
+# outputs are bucket-sink gradients (nothing in the backward reads them) are queued by the library
+# (dph_defer_reductions) and launched together when the encoder backward ends (the flush of the encoder-input hook,
+# next to the grouped weight gradients) -- one grid per 96 reductions, bitwise the same sums.  Their parameters are
+# held back from the reducer until then, and their slabs kept alive.
+_RED_DEFER = [None]
+
+
+class deferred_reductions:
+    """Queue the sink-bound column reductions of one backward (see above); close() / exit flush them."""
+
+    def __init__(self, enable: bool = True):
+        self.enable = bool(enable) and os.environ.get("DPH_DEFER_RED", "1") != "0" and _lib.deterministic()
+        self.keep, self.pending = [], []
+        self.open = False
+
+    def __enter__(self):
+        if self.enable:
+            self.prev, _RED_DEFER[0] = _RED_DEFER[0], self
+            self.prev_keep, K.KEEP_WS[0] = K.KEEP_WS[0], self.keep
+            self.open = True
+        return self
+
+    def arm(self, go, ok: bool):
+        """Context of one library call whose column reductions may be queued (``ok``: all their outputs are
+        bucket sinks)."""
+        return _Armed(self if (self.open and ok) else None, go)
+
+    def close(self):
+        """Launch the queued reductions, then release their parameters to the reducer; later calls run as usual."""
+        if not self.open:
+            return
+        self.open = False
+        K.KEEP_WS[0] = self.prev_keep
+        call("dph_flush_reductions", _s())
+        pend, self.pending = self.pending, []
+        for p in pend:
+            p._dph_sink_ready(p)
+        self.keep = []
+
+    def __exit__(self, exc_type, *exc):
+        if self.enable:
+            _RED_DEFER[0] = self.prev
+            if exc_type is None:
+                self.close()
+            else:
+                self.open = False
+                K.KEEP_WS[0] = self.prev_keep
+                _lib.lib().dph_defer_reductions(0)
+
+
+class _Armed:
+    def __init__(self, scope, go):
+        self.scope, self.go = scope, go
+
+    def __enter__(self):
+        if self.scope is not None:
+            _lib.lib().dph_defer_reductions(1)
+            self.go.deferred = self.scope
+        return self
+
+    def __exit__(self, *exc):
+        if self.scope is not None:
+            _lib.lib().dph_defer_reductions(0)
+
+
+def _defer_red(go, *outs_direct):
+    """Arm reduction deferral for the next library call when a deferred_reductions block is open and every output
+    of its column reductions is a bucket sink (``outs_direct``: the GradOut ``direct`` flags)."""
+    r = _RED_DEFER[0]
+    if r is None:
+        return _Armed(None, go)
+    return r.arm(go, all(outs_direct))
 
 
 def mark_encoder_input(x: torch.Tensor) -> torch.Tensor:
@@ -603,6 +689,7 @@ class GradOut:
         self.sunk = set()
         self.sunk_params = []
         self.bufs = {}
+        self.deferred = None     # the deferred_reductions block that queued reductions into these buffers
 
     def buf(self, *params, zero: bool = True):
         t = _sink_view(params)
@@ -631,6 +718,10 @@ class GradOut:
             red = getattr(self.sunk_params[0]._dph_sink_ready, "__self__", None)
             if red is not None and red.enabled and red.sync:
                 torch.cuda.current_stream().wait_stream(side)   # the bucket's collective reads these gradients
+        d = self.deferred
+        if d is not None and d.open:
+            d.pending.extend(self.sunk_params)     # complete only once the queued reductions are flushed
+            return
         for p in self.sunk_params:
             p._dph_sink_ready(p)
 
@@ -1376,13 +1467,23 @@ class PosConvFn(torch.autograd.Function):
         Kk = wv.shape[2]
         Cg = D // G
         dev = x.device
-        # weight norm -> bf16 GEMM images (forward and flipped/transposed for dgrad)
-        norm = torch.empty(Kk, dtype=F32, device=dev)
-        wk = torch.empty(G, Cg, Kk * Cg, dtype=BF16, device=dev)
-        wt = torch.empty(G, Cg, Kk * Cg, dtype=BF16, device=dev)
-        wn_ws = _weight_norm_ws(D * Cg, Kk, dev)
-        call("dph_weight_norm_fwd", ptr(wg), ptr(wv), D, Cg, Kk, G, None, ptr(norm), ptr(wk), ptr(wt), ptr(wn_ws),
-             wn_ws.numel() * 4, _s())
+        # weight norm -> bf16 GEMM images (forward and flipped/transposed for dgrad).  A frozen model's (the
+        # teacher's: no gradient, parameters without requires_grad) forward image is computed once per weight
+        # version and reused: the step graph then carries no weight-norm launches for it
+        frozen = not cfg["need_grad"] and not wg.requires_grad and not wv.requires_grad
+        key = (wg.data_ptr(), wg._version, wv.data_ptr(), wv._version, G, Kk)
+        hit = getattr(wv, "_dph_wn_img", None) if frozen else None
+        if hit is not None and hit[0] == key:
+            norm, wk, wt = hit[1], hit[2], None
+        else:
+            norm = torch.empty(Kk, dtype=F32, device=dev)
+            wk = torch.empty(G, Cg, Kk * Cg, dtype=BF16, device=dev)
+            wt = None if frozen else torch.empty(G, Cg, Kk * Cg, dtype=BF16, device=dev)
+            wn_ws = _weight_norm_ws(D * Cg, Kk, dev)
+            call("dph_weight_norm_fwd", ptr(wg), ptr(wv), D, Cg, Kk, G, None, ptr(norm), ptr(wk), ptr(wt),
+                 ptr(wn_ws), wn_ws.numel() * 4, _s())
+            if frozen and not torch.cuda.is_current_stream_capturing():
+                wv._dph_wn_img = (key, norm, wk)
         P = Kk // 2
         Q = Kk - 1 - P
         Tp = P + T + Q
@@ -1632,8 +1733,10 @@ def _ffn_backward(cfg, sv, dy, xin, pr, go, dmask, residual=None):
         post = lambda: call("dph_colprod", ptr(W2i), W2i.shape[1], ptr(dw2), F_, ptr(imp), ptr(dmask), D, F_,  # noqa
                             _s())
     k1 = _layer_wgrad(dy, sv["f"], dw2, direct, (pr["w2"],), post=post, k_in=F_)
-    db1, _ = go.buf(pr["b1"])
-    du = _ffn_interm_bwd(dy, sv, db1, None if colprod else dmask, cfg, F_)
+    db1, db1d = go.buf(pr["b1"])
+    dmk = None if colprod else dmask
+    with _defer_red(go, db1d, dmk is None):     # (the mask gradient feeds autograd: never queued)
+        du = _ffn_interm_bwd(dy, sv, db1, dmk, cfg, F_)
     dw1, direct = go.buf(pr["w1"], zero=False)
     k2 = _layer_wgrad(du, xin, dw1, direct, (pr["w1"],), n_out=F_)
     dx = K.linear_dgrad(du, sv["W1"], w_t=t_image(sv["W1"]), residual=residual)
@@ -1927,34 +2030,37 @@ class EncoderLayerFn(torch.autograd.Function):
         g = {}
         # ---- LN2 backward (+ FFN branch gradient) ----
         ds2 = torch.empty_like(dout)
-        dln2w, _ = go.buf(pr["ln2_w"])
-        dln2b, _ = go.buf(pr["ln2_b"])
+        dln2w, d2w = go.buf(pr["ln2_w"])
+        dln2b, d2b = go.buf(pr["ln2_b"])
         if use_ff:
             dy = torch.empty_like(dout)
-            db2, _ = go.buf(pr["b2"])
+            db2, dd2 = go.buf(pr["b2"])
             g["lmf"] = z(1) if has_lmf else None
-            call("dph_layernorm_bwd", ptr(dout), ptr(s2), None, ptr(ln2_w), ptr(mu2), ptr(rs2), ptr(ds2),
-                 ptr(dln2w), ptr(dln2b), M, D, 0.0, 0, ptr(dy), cfg["p_drop"], sv["seed_o"], ptr(lmf), ptr(db2),
-                 ptr(sv["y_pre"]), ptr(g["lmf"]), *ln_ws(M, D, dev), _s())
+            with _defer_red(go, d2w, d2b, dd2):
+                call("dph_layernorm_bwd", ptr(dout), ptr(s2), None, ptr(ln2_w), ptr(mu2), ptr(rs2), ptr(ds2),
+                     ptr(dln2w), ptr(dln2b), M, D, 0.0, 0, ptr(dy), cfg["p_drop"], sv["seed_o"], ptr(lmf), ptr(db2),
+                     ptr(sv["y_pre"]), ptr(g["lmf"]), *ln_ws(M, D, dev), _s())
             F_ = sv["F"]
             g["im"] = z(F_) if has_im else None
             dh1 = _ffn_backward(cfg, sv, dy, h1, pr, go, g["im"], residual=ds2)
         else:
-            call("dph_layernorm_bwd", ptr(dout), ptr(s2), None, ptr(ln2_w), ptr(mu2), ptr(rs2), ptr(ds2),
-                 ptr(dln2w), ptr(dln2b), M, D, 0.0, 0, None, 0.0, 0, None, None, None, None, *ln_ws(M, D, dev),
-                 _s())
+            with _defer_red(go, d2w, d2b):
+                call("dph_layernorm_bwd", ptr(dout), ptr(s2), None, ptr(ln2_w), ptr(mu2), ptr(rs2), ptr(ds2),
+                     ptr(dln2w), ptr(dln2b), M, D, 0.0, 0, None, 0.0, 0, None, None, None, None, *ln_ws(M, D, dev),
+                     _s())
             dh1 = ds2
         # ---- LN1 backward (+ attention branch gradient) ----
         ds1 = torch.empty_like(dout)
-        dln1w, _ = go.buf(pr["ln1_w"])
-        dln1b, _ = go.buf(pr["ln1_b"])
+        dln1w, d1w = go.buf(pr["ln1_w"])
+        dln1b, d1b = go.buf(pr["ln1_b"])
         if use_att:
             da = torch.empty_like(dout)
-            dbo, _ = go.buf(pr["bo"])
+            dbo, ddo = go.buf(pr["bo"])
             g["lma"] = z(1) if has_lma else None
-            call("dph_layernorm_bwd", ptr(dh1), ptr(s1), None, ptr(ln1_w), ptr(mu1), ptr(rs1), ptr(ds1),
-                 ptr(dln1w), ptr(dln1b), M, D, 0.0, 0, ptr(da), cfg["p_drop"], sv["seed_d"], ptr(lma), ptr(dbo),
-                 ptr(sv["a_pre"]), ptr(g["lma"]), *ln_ws(M, D, dev), _s())
+            with _defer_red(go, d1w, d1b, ddo):
+                call("dph_layernorm_bwd", ptr(dh1), ptr(s1), None, ptr(ln1_w), ptr(mu1), ptr(rs1), ptr(ds1),
+                     ptr(dln1w), ptr(dln1b), M, D, 0.0, 0, ptr(da), cfg["p_drop"], sv["seed_d"], ptr(lma), ptr(dbo),
+                     ptr(sv["a_pre"]), ptr(g["lma"]), *ln_ws(M, D, dev), _s())
             dwo, direct = go.buf(pr["wo"], zero=False)
             k3 = _layer_wgrad(da, sv["o_m"], dwo, direct, (pr["wo"],))
             do_m = K.linear_dgrad(da, sv["Wo"], w_t=t_image(sv["Wo"]))
@@ -1964,17 +2070,19 @@ class EncoderLayerFn(torch.autograd.Function):
                  *_ws(_lib.lib().dph_attention_bwd_prep_workspace(B, T, H), dev), _s())
             dqkv = torch.empty_like(sv["qkv"])
             wl_g = EncoderLayerFn._attention_bwd(ctx, cfg, sv, do_m, hm, Dvec, dqkv)
-            dbqkv, _ = go.buf(pr["bq"], pr["bk"], pr["bv"])
-            _qkv_bias_grad(dqkv, dbqkv, M, dev)
+            dbqkv, dqb = go.buf(pr["bq"], pr["bk"], pr["bv"])
+            with _defer_red(go, dqb):
+                _qkv_bias_grad(dqkv, dbqkv, M, dev)
             dwqkv, direct = go.buf(pr["wq"], pr["wk"], pr["wv"], zero=False)
             k4 = _layer_wgrad(dqkv, h, dwqkv, direct, (pr["wq"], pr["wk"], pr["wv"]))
             dh = K.linear_dgrad(dqkv, sv["Wqkv"], w_t=t_image(sv["Wqkv"]), residual=ds1)
             EncoderLayerFn._gate_bwd(ctx, cfg, h, dh, wl_g, go)
             del k3, k4
         else:
-            call("dph_layernorm_bwd", ptr(dh1), ptr(s1), None, ptr(ln1_w), ptr(mu1), ptr(rs1), ptr(ds1),
-                 ptr(dln1w), ptr(dln1b), M, D, 0.0, 0, None, 0.0, 0, None, None, None, None, *ln_ws(M, D, dev),
-                 _s())
+            with _defer_red(go, d1w, d1b):
+                call("dph_layernorm_bwd", ptr(dh1), ptr(s1), None, ptr(ln1_w), ptr(mu1), ptr(rs1), ptr(ds1),
+                     ptr(dln1w), ptr(dln1b), M, D, 0.0, 0, None, 0.0, 0, None, None, None, None, *ln_ws(M, D, dev),
+                     _s())
             dh = ds1
         go.done()
         order = ["wq", "wk", "wv", "bq", "bk", "bv", "wo", "bo", "ln1_w", "ln1_b", "w1", "b1", "w2", "b2", "ln2_w",
@@ -2070,7 +2178,9 @@ class DistillProjLossFn(torch.autograd.Function):
         go = GradOut(dev)
         pw = ctx.params
         dW = [go.buf(pw[2 * p])[0] for p in range(P)]
-        db = [go.buf(pw[2 * p + 1])[0] for p in range(P)]
+        dbs = [go.buf(pw[2 * p + 1]) for p in range(P)]
+        db = [t for t, _ in dbs]
+        db_direct = [d for _, d in dbs]
         if ctx.pre is not None:
             # through the heads' GELU: dz = ds * gelu'(pre), in place
             call("dph_gelu_mask_bwd", ptr(ds), ptr(ctx.pre), None, ptr(ds), None, L * M, Dt, None, 0, _s())
@@ -2083,7 +2193,8 @@ class DistillProjLossFn(torch.autograd.Function):
         for l in range(L):
             p = cfg["proj_index"][l]
             keep.append(K.linear_wgrad(ds[l], sh[l], dW[p], accumulate=True))
-            call("dph_colsum", ptr(ds[l]), ptr(db[p]), M, Dt, *colsum_ws(M, Dt, dev), _s())
+            with _defer_red(go, db_direct[p]):
+                call("dph_colsum", ptr(ds[l]), ptr(db[p]), M, Dt, *colsum_ws(M, Dt, dev), _s())
             o = torch.empty(M, Ds, dtype=F32, device=dev) if ctx.in_f32[l] else None
             if shared:
                 acc = K.linear_dgrad(ds[l], imgs[p], w_t=t_image(imgs[p]), residual=acc, out=o if acc is None else None)

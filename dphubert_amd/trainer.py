@@ -321,7 +321,7 @@ class Trainer:
             if torch.cuda.is_current_stream_capturing():
                 raise RuntimeError("Trainer: the backward seed must exist before a graph capture")
             seed = self._grad_seed = torch.full((), 1.0 / self.accum_grad, dtype=loss.dtype, device=loss.device)
-        with ops.wgrad_overlap(self._wgrad_stream), ops.grouped_wgrads(self.wgrad_group):
+        with ops.wgrad_overlap(self._wgrad_stream), ops.grouped_wgrads(self.wgrad_group), ops.deferred_reductions():
             loss.backward(seed)
         if final:
             self.reducer.finish()

@@ -45,6 +45,18 @@ int dph_abi_version(void);
 int dph_set_deterministic(int on);
 int dph_get_deterministic(void);
 
+/* Deferred column reductions (deterministic mode only; ABI 21).  Between dph_defer_reductions(1) and
+ * dph_defer_reductions(0), the fixed-order partial-slab column sums that dph_layernorm_bwd*, dph_colsum /
+ * dph_colsum3, the rowblock reductions and dph_gemm's column-sum epilogues would launch as their own small grid
+ * are queued instead; dph_flush_reductions launches the queue as one grid per 96 problems, each problem summed
+ * in the same fixed order as its own launch (bitwise identical results).  The caller keeps every queued
+ * workspace alive and the queued outputs unread until the flush, which must be issued on the stream the
+ * reductions were queued on.  Queued problems whose outputs overlap are flushed in queue order (an overlapping
+ * enqueue flushes the queue first).  dph_deferred_reductions: the queue length. */
+int dph_defer_reductions(int on);
+int dph_flush_reductions(hipStream_t stream);
+int64_t dph_deferred_reductions(void);
+
 /* ------------------------------------------------------------------------ *
  * Generic bf16 MFMA GEMM with fused epilogues.
  *   C[z][m][n] = epi( alpha * sum_k A[z][m][k] * B[z][k][n] )

@@ -12,6 +12,7 @@
 #   wgrad   -- tools/wgrad_ab.py (weight-gradient GEMMs: ppw plan vs the register-staged kernel)
 #   pmcattn -- rocprofv3 --pmc passes over the attention kernels (tools/attn_bench.py)
 #   pmcgemm -- the same over the dominant GEMM shape (7984 x 3072 x 768, tools/gemm_one.py)
+#   pmcgemmx -- PMC of the 128 x 192 tile (FFN2 shape, 8192^3) and the 256 x 256 tile (8192^3)
 #   pmcconv0 -- the same over the conv0 GroupNorm kernels (tools/conv0_bench.py)
 # Every GPU step runs under its own timeout; the first failing step ends the script.
 set -o pipefail
@@ -76,6 +77,12 @@ for P in $PHASES; do
       pmc_run pmcattn attn python3 "$R/tools/attn_bench.py" || exit 1 ;;
     pmcgemm)
       pmc_run pmcgemm gemm python3 "$R/tools/gemm_one.py" 7984 3072 768 5 || exit 1 ;;
+    pmcgemmx)
+      # the 128 x 192 tile on the FFN2 projection shape and on 8192^3, the 256 x 256 tile on 8192^3
+      for cfg in "15 7984 768 3072" "15 8192 8192 8192" "12 8192 8192 8192"; do
+        set -- $cfg
+        (export DPH_PP_FORCE=$1; pmc_run "pmcgemm_$1_$2x$3x$4" gemm python3 "$R/tools/gemm_one.py" $2 $3 $4 5) || exit 1
+      done ;;
     pmcconv0)
       pmc_run pmcconv0 conv0 python3 "$R/tools/conv0_bench.py" 0 3 || exit 1 ;;
     *) echo "unknown phase $P"; exit 2 ;;
