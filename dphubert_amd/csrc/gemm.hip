@@ -1974,6 +1974,9 @@ __device__ __forceinline__ bf16x8_t hfrag(const char* ht, int rb, int s, int lan
 template <class C, int ACT, bool DROP>
 __global__ void __launch_bounds__(C::NT, C::WPE) pp_gemm_kernel(const DphGemmArgs a) {
   __shared__ __attribute__((aligned(1024))) char smem[C::LDS];
+  unsigned long long st0 = 0, st1 = 0, st2 = 0, st3 = 0;
+  (void)st0; (void)st1; (void)st2; (void)st3;
+  DPH_TSTAMP(st0);
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -2113,6 +2116,7 @@ __global__ void __launch_bounds__(C::NT, C::WPE) pp_gemm_kernel(const DphGemmArg
   st_b0(1);
   vm_wait<G>();
   bar();
+  DPH_TSTAMP(st1);
   if (wr == 1) bar();            // group 1 runs one interval behind group 0
   int u = 0;
 #pragma unroll 1
@@ -2198,7 +2202,21 @@ __global__ void __launch_bounds__(C::NT, C::WPE) pp_gemm_kernel(const DphGemmArg
     bar();
   }
   if (wr == 0) bar();            // pairs with group 1's extra barrier
+  DPH_TSTAMP(st2);
   ring::direct_epi_t<C, ACT, DROP, true>(a, z, m0 + wr * C::WTM, n0 + wc * C::WTN, lane, acc);
+  if (DPH_STAMP) {
+    // diagnostic build only (tools/stamp_pp.py): per-block stamps into the workspace, written by lane 0 of wave 0
+    __syncthreads();
+    DPH_TSTAMP(st3);
+    if (tid == 0) {
+      unsigned hw, xcc;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+      unsigned long long* o = reinterpret_cast<unsigned long long*>(a.workspace) +
+                              8 * ((int64_t)blockIdx.y * gridDim.x + blockIdx.x);
+      o[0] = st0; o[1] = st1; o[2] = st2; o[3] = st3; o[4] = hw; o[5] = xcc;
+    }
+  }
 }
 }  // namespace pp
 

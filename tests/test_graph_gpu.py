@@ -358,3 +358,35 @@ def test_ffn_mask_grad_colprod_matches_epilogue(monkeypatch, group):
         for n, a in res[0][micro].items():
             b = res[1][micro][n]
             assert rel_l2(a, b) < 1e-4, (micro, n, rel_l2(a, b))
+
+
+@pytest.mark.parametrize("accum", [1, 2])
+def test_deferred_reductions_match_immediate(monkeypatch, accum):
+    """ops.deferred_reductions (the sink-bound bias / LayerNorm-affine column reductions queued by the library and
+    launched as one grid at the encoder-end flush) against immediate launches: the same gradient buckets BITWISE
+    (each queued problem is summed in the fixed order of its own launch), reductions really queued, and no
+    parameter left held back from the reducer."""
+    from dphubert_amd import _lib, ops
+    from dphubert_amd.trainer import Trainer
+    batch = _batch()
+    queued = []
+    orig = ops.deferred_reductions.close
+
+    def spy(self):
+        if self.open:
+            queued.append(_lib.lib().dph_deferred_reductions())
+        return orig(self)
+
+    monkeypatch.setattr(ops.deferred_reductions, "close", spy)
+    res = []
+    for on in ("0", "1"):
+        monkeypatch.setenv("DPH_DEFER_RED", on)
+        tr = Trainer(_module(), clip_norm=10.0, accum_grad=accum)
+        for _ in range(accum):
+            tr.step(batch)
+        torch.cuda.synchronize()
+        res.append(torch.cat([f.detach().float().cpu() for f in tr.reducer.flat]))
+        assert not any(getattr(p, "_dph_hold", False) for p in tr.reducer.params)
+        assert _lib.lib().dph_deferred_reductions() == 0
+    assert queued and max(queued) >= 8, queued
+    assert torch.equal(res[0], res[1])

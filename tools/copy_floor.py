@@ -61,7 +61,25 @@ def ln_bwd_lm():
          ptr(br), 0.1, 7, ptr(sm), ptr(bcs), ptr(pre), ptr(sd), ptr(wsb), wsb.numel() * 4, _lib.stream_ptr())
 
 
+def ln_bwd_plain():
+    call("dph_layernorm_bwd", ptr(dy), ptr(x), None, ptr(w), ptr(mu), ptr(rs), ptr(dx), ptr(dg), ptr(db), M, D, 0.0, 0,
+         None, 0.0, 0, None, None, None, None, ptr(wsb), wsb.numel() * 4, _lib.stream_ptr())
+
+
+def ln_bwd_p0():
+    call("dph_layernorm_bwd", ptr(dy), ptr(x), None, ptr(w), ptr(mu), ptr(rs), ptr(dx), ptr(dg), ptr(db), M, D, 0.0, 0,
+         ptr(br), 0.0, 7, None, ptr(bcs), None, None, ptr(wsb), wsb.numel() * 4, _lib.stream_ptr())
+
+
+def ln_bwd_nocol():
+    call("dph_layernorm_bwd", ptr(dy), ptr(x), None, ptr(w), ptr(mu), ptr(rs), ptr(dx), None, None, M, D, 0.0, 0,
+         ptr(br), 0.1, 7, None, None, None, None, ptr(wsb), wsb.numel() * 4, _lib.stream_ptr())
+
+
 for name, f, byt in (
+        ("layernorm bwd plain", ln_bwd_plain, 3 * M * D * 2),
+        ("layernorm bwd (+branch p=0)", ln_bwd_p0, 4 * M * D * 2),
+        ("layernorm bwd (+branch, no colsums)", ln_bwd_nocol, 4 * M * D * 2),
         ("layernorm bwd (+branch)", ln_bwd, 5 * M * D * 2),
         ("layernorm bwd (+layer mask)", ln_bwd_lm, 6 * M * D * 2),
         ("copy bf16 12 MB -> 12 MB", lambda: y.copy_(x), 2 * M * D * 2),
