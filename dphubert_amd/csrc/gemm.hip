@@ -1944,6 +1944,10 @@ struct Cfg {
   // two blocks per CU only for the small tiles (the 128 x 192 GELU epilogues spilled at the 128-VGPR cap)
   static constexpr int MINB = (LDS <= 80 * 1024 && FM * FN <= 8) ? 2 : 1;
   static constexpr int WPE = MINB * 2;                                  // waves per SIMD
+  // the A-lo fragments of K-tile u + 1 read in K-tile u's last interval (pp_gemm_kernel): taken where it measured
+  // faster -- the 256-row tiles (8192^3 on 256 x 256: 2382 -> 2124 cycles per K-tile) and 128 x 128; the 128 x 192
+  // projection shapes ran 2-3 % slower with it (tools/stamp_pp.py, profiles/r5_pp_loop_stamps.txt)
+  static constexpr bool SPLITA = BM_ == 256 || (BM_ == 128 && BN_ == 128);
   static_assert(FM % 2 == 0 && FN >= 2 && RA % 64 == 0 && G < 16, "pp tile geometry");
 };
 using P256 = Cfg<256, 256>;
@@ -1971,6 +1975,14 @@ __device__ __forceinline__ bf16x8_t hfrag(const char* ht, int rb, int s, int lan
   return *reinterpret_cast<const bf16x8_t*>(ht + row * 128 + phys * 16);
 }
 
+#ifndef DPH_PP_ABL
+#define DPH_PP_ABL 0   // diagnostic builds only (tools/stamp_pp.py): 1 = no main-loop DMAs, 2 = no main-loop MFMAs,
+#endif              // 3 = no main-loop LDS reads, 4 = no main-loop barriers, 5 = reads + barriers only, 6 = MFMAs +
+                    // barriers only (timing ablations: the results are garbage)
+#define PP_ABL_DMA (DPH_PP_ABL == 1 || DPH_PP_ABL == 5 || DPH_PP_ABL == 6)
+#define PP_ABL_MFMA (DPH_PP_ABL == 2 || DPH_PP_ABL == 5)
+#define PP_ABL_READ (DPH_PP_ABL == 3 || DPH_PP_ABL == 6)
+#define PP_ABL_BAR (DPH_PP_ABL == 4)
 template <class C, int ACT, bool DROP>
 __global__ void __launch_bounds__(C::NT, C::WPE) pp_gemm_kernel(const DphGemmArgs a) {
   __shared__ __attribute__((aligned(1024))) char smem[C::LDS];
@@ -2039,19 +2051,25 @@ __global__ void __launch_bounds__(C::NT, C::WPE) pp_gemm_kernel(const DphGemmArg
     ob1[jj] = (uint32_t)(row_addr32(a.B, (uint32_t)min<int64_t>(n0 + tcol, a.N - 1)) + lc * 8);
   }
   auto buf = [&](int u) -> char* { return smem + (u & 1) * C::BUF; };
+  // (DPH_PP_ABL == 1: DMAs past the prologue's two K-tiles are not issued -- a timing ablation on stale operands)
+  auto dma_on = [&](int u) { return !PP_ABL_DMA || u < 2; };
   auto st_alo = [&](int u) {
+    if (!dma_on(u)) return;
 #pragma unroll
     for (int jj = 0; jj < C::GA; ++jj) ring::dma16(Ab + oal[jj] + (int64_t)u * BK, buf(u) + C::O_ALO + (jj * 8 + wave) * 1024);
   };
   auto st_ahi = [&](int u) {
+    if (!dma_on(u)) return;
 #pragma unroll
     for (int jj = 0; jj < C::GA; ++jj) ring::dma16(Ab + oah[jj] + (int64_t)u * BK, buf(u) + C::O_AHI + (jj * 8 + wave) * 1024);
   };
   auto st_b0 = [&](int u) {
+    if (!dma_on(u)) return;
 #pragma unroll
     for (int jj = 0; jj < C::GB0; ++jj) ring::dma16(Bb + ob0[jj] + (int64_t)u * BK, buf(u) + C::O_B0 + (jj * 8 + wave) * 1024);
   };
   auto st_b1 = [&](int u) {
+    if (!dma_on(u)) return;
 #pragma unroll
     for (int jj = 0; jj < C::GB1; ++jj) ring::dma16(Bb + ob1[jj] + (int64_t)u * BK, buf(u) + C::O_B1 + (jj * 8 + wave) * 1024);
   };
@@ -2061,28 +2079,37 @@ __global__ void __launch_bounds__(C::NT, C::WPE) pp_gemm_kernel(const DphGemmArg
   for (int i = 0; i < C::FM; ++i)
 #pragma unroll
     for (int j = 0; j < C::FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  bf16x8_t fa[C::FM2][2], fb0[C::FN0][2], fb1[C::FN1][2];
+  // A fragments of the tile's low and high row halves in separate registers: the low half of K-tile u + 1 is read
+  // during K-tile u's last (A-high x B-n0) interval -- its half-tile landed two intervals earlier -- so every
+  // interval carries at most FM2 * 2 or FN0 * 2 fragment reads (4 / 2 / 4 / 4 on the 128 x 192 tile instead of
+  // 8 / 2 / 4 / 0, whose 8-read interval left the next MFMA cluster waiting on its LDS reads)
+  bf16x8_t falo[C::FM2][2] = {}, fa_hi_[C::FM2][2] = {}, fb0[C::FN0][2] = {}, fb1[C::FN1][2] = {};
+  bf16x8_t (&fahi)[C::FM2][2] = C::SPLITA ? fa_hi_ : falo;   // one A fragment set where the split is not taken
 
-  auto rd_a = [&](const char* ht) {
+  auto rd_a = [&](const char* ht, bf16x8_t (&fa)[C::FM2][2]) {
+    if (PP_ABL_READ) return;
 #pragma unroll
     for (int i = 0; i < C::FM2; ++i)
 #pragma unroll
       for (int s = 0; s < 2; ++s) fa[i][s] = hfrag(ht, wr * HA + 16 * i, s, lane);
   };
   auto rd_b0 = [&](const char* bu) {
+    if (PP_ABL_READ) return;
 #pragma unroll
     for (int j = 0; j < C::FN0; ++j)
 #pragma unroll
       for (int s = 0; s < 2; ++s) fb0[j][s] = hfrag(bu + C::O_B0, wc * 16 * C::FN0 + 16 * j, s, lane);
   };
   auto rd_b1 = [&](const char* bu) {
+    if (PP_ABL_READ) return;
 #pragma unroll
     for (int j = 0; j < C::FN1; ++j)
 #pragma unroll
       for (int s = 0; s < 2; ++s) fb1[j][s] = hfrag(bu + C::O_B1, wc * 16 * C::FN1 + 16 * j, s, lane);
   };
-  // MFMA cluster: rows [i0, i0 + FM2) x the given B fragment set
-  auto mm0 = [&](int i0) {
+  // MFMA cluster: rows [i0, i0 + FM2) (fragments fa) x the given B fragment set
+  auto mm0 = [&](int i0, const bf16x8_t (&fa)[C::FM2][2]) {
+    if (PP_ABL_MFMA) return;
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int s = 0; s < 2; ++s)
@@ -2093,7 +2120,8 @@ __global__ void __launch_bounds__(C::NT, C::WPE) pp_gemm_kernel(const DphGemmArg
           acc[i0 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb0[j][s], fa[i][s], acc[i0 + i][j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
   };
-  auto mm1 = [&](int i0) {
+  auto mm1 = [&](int i0, const bf16x8_t (&fa)[C::FM2][2]) {
+    if (PP_ABL_MFMA) return;
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int s = 0; s < 2; ++s)
@@ -2106,6 +2134,9 @@ __global__ void __launch_bounds__(C::NT, C::WPE) pp_gemm_kernel(const DphGemmArg
     __builtin_amdgcn_s_setprio(0);
   };
   constexpr int G = C::G;
+  auto lbar = [&]() {
+    if (!PP_ABL_BAR) bar();
+  };
   // prologue: the half-tiles of "phases" -6 .. -1 (A-lo(0), B-n0(0), B-n1(0), A-hi(0), A-lo(1), B-n0(1)),
   // then wait for A-lo(0) and B-n0(0)
   st_alo(0);
@@ -2117,6 +2148,7 @@ __global__ void __launch_bounds__(C::NT, C::WPE) pp_gemm_kernel(const DphGemmArg
   vm_wait<G>();
   bar();
   DPH_TSTAMP(st1);
+  if constexpr (C::SPLITA) rd_a(buf(0) + C::O_ALO, falo);
   if (wr == 1) bar();            // group 1 runs one interval behind group 0
   int u = 0;
 #pragma unroll 1
@@ -2124,38 +2156,39 @@ __global__ void __launch_bounds__(C::NT, C::WPE) pp_gemm_kernel(const DphGemmArg
     const char* bu = buf(u);
     // j = 0
     rd_b0(bu);
-    rd_a(bu + C::O_ALO);
+    if constexpr (!C::SPLITA) rd_a(bu + C::O_ALO, falo);
     st_b1(u + 1);
     vm_wait<G>();
-    bar();
+    lbar();
     lgkm0();
     __builtin_amdgcn_sched_barrier(0);
-    mm0(0);
-    bar();
+    mm0(0, falo);
+    lbar();
     // j = 1
     rd_b1(bu);
     st_ahi(u + 1);
     vm_wait<G>();
-    bar();
+    lbar();
     lgkm0();
     __builtin_amdgcn_sched_barrier(0);
-    mm1(0);
-    bar();
+    mm1(0, falo);
+    lbar();
     // j = 2
-    rd_a(bu + C::O_AHI);
+    rd_a(bu + C::O_AHI, fahi);
     st_alo(u + 2);
     vm_wait<G>();
-    bar();
+    lbar();
     lgkm0();
     __builtin_amdgcn_sched_barrier(0);
-    mm1(C::FM2);
-    bar();
-    // j = 3
+    mm1(C::FM2, fahi);
+    lbar();
+    // j = 3 (A-lo(u + 1): landed by the vm_wait of j = 2, visible after its barrier; not waited for here)
+    if constexpr (C::SPLITA) rd_a(buf(u + 1) + C::O_ALO, falo);
     st_b0(u + 2);
     vm_wait<G>();
-    bar();
-    mm0(C::FM2);
-    bar();
+    lbar();
+    mm0(C::FM2, fahi);
+    lbar();
   }
   // the last two K-tiles: nothing staged past nk - 1, the counted waits drain
 #pragma unroll
@@ -2163,18 +2196,18 @@ __global__ void __launch_bounds__(C::NT, C::WPE) pp_gemm_kernel(const DphGemmArg
     const bool second_last = t == 0;
     const char* bu = buf(u);
     rd_b0(bu);
-    rd_a(bu + C::O_ALO);
+    if constexpr (!C::SPLITA) rd_a(bu + C::O_ALO, falo);
     if (second_last) {
       st_b1(u + 1);
       vm_wait<G>();
     } else {
       vm_wait<C::GA>();
     }
-    bar();
+    lbar();
     lgkm0();
     __builtin_amdgcn_sched_barrier(0);
-    mm0(0);
-    bar();
+    mm0(0, falo);
+    lbar();
     rd_b1(bu);
     if (second_last) {
       st_ahi(u + 1);
@@ -2182,24 +2215,28 @@ __global__ void __launch_bounds__(C::NT, C::WPE) pp_gemm_kernel(const DphGemmArg
     } else {
       vm_wait<0>();
     }
-    bar();
+    lbar();
     lgkm0();
     __builtin_amdgcn_sched_barrier(0);
-    mm1(0);
-    bar();
-    rd_a(bu + C::O_AHI);
+    mm1(0, falo);
+    lbar();
+    rd_a(bu + C::O_AHI, fahi);
     if (second_last) vm_wait<G - C::GA>();
     else vm_wait<0>();
-    bar();
+    lbar();
     lgkm0();
     __builtin_amdgcn_sched_barrier(0);
-    mm1(C::FM2);
-    bar();
-    if (second_last) vm_wait<C::GB1 + C::GA>();
-    else vm_wait<0>();
-    bar();
-    mm0(C::FM2);
-    bar();
+    mm1(C::FM2, fahi);
+    lbar();
+    if (second_last) {
+      if constexpr (C::SPLITA) rd_a(buf(u + 1) + C::O_ALO, falo);   // (landed by the j = 2 wait above)
+      vm_wait<C::GB1 + C::GA>();
+    } else {
+      vm_wait<0>();
+    }
+    lbar();
+    mm0(C::FM2, fahi);
+    lbar();
   }
   if (wr == 0) bar();            // pairs with group 1's extra barrier
   DPH_TSTAMP(st2);
@@ -2433,18 +2470,21 @@ __global__ void __launch_bounds__(C::NT, C::WPE) ppw_gemm_kernel(const DphGemmAr
   for (int j = 0; j < C::FN1; ++j) ob1[j] = tfrag_off<C::RB1>(wc * 16 * C::FN1 + 16 * j, lane);
 
   auto rd_a = [&](const char* ht) {
+    if (PP_ABL_READ) return;
 #pragma unroll
     for (int i = 0; i < C::FM2; ++i)
 #pragma unroll
       for (int s = 0; s < 2; ++s) fa[i][s] = tfrag<C::RA>(ht, oa[i], s);
   };
   auto rd_b0 = [&](const char* bu) {
+    if (PP_ABL_READ) return;
 #pragma unroll
     for (int j = 0; j < C::FN0; ++j)
 #pragma unroll
       for (int s = 0; s < 2; ++s) fb0[j][s] = tfrag<C::RB0>(bu + C::O_B0, ob0[j], s);
   };
   auto rd_b1 = [&](const char* bu) {
+    if (PP_ABL_READ) return;
 #pragma unroll
     for (int j = 0; j < C::FN1; ++j)
 #pragma unroll
@@ -2461,6 +2501,7 @@ __global__ void __launch_bounds__(C::NT, C::WPE) ppw_gemm_kernel(const DphGemmAr
     }
   };
   auto mm0 = [&](int i0) {
+    if (PP_ABL_MFMA) return;
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int s = 0; s < 2; ++s)
@@ -2472,6 +2513,7 @@ __global__ void __launch_bounds__(C::NT, C::WPE) ppw_gemm_kernel(const DphGemmAr
     __builtin_amdgcn_s_setprio(0);
   };
   auto mm1 = [&](int i0) {
+    if (PP_ABL_MFMA) return;
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int s = 0; s < 2; ++s)

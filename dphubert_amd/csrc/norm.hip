@@ -662,7 +662,7 @@ __global__ void __launch_bounds__(512) ln_bwd16_kernel(
   constexpr int D = NE * 32;
   static_assert(LN_BWD_WAVES == 8 && LN_BWD_RPW == 2, "ln_bwd16: the slab layout assumes 16 rows per block");
   branch_seed = epoch_seed(branch_seed);
-  __shared__ float4 red[8][NC * 32][2];
+  __shared__ float4 red[3][8][NC * 32][2];
   const int lane = threadIdx.x & 63;
   const int hl = lane & 31;
   const int wave = threadIdx.x >> 6;
@@ -765,13 +765,13 @@ __global__ void __launch_bounds__(512) ln_bwd16_kernel(
             make_uint4(pack2bf(bo[0], bo[1]), pack2bf(bo[2], bo[3]), pack2bf(bo[4], bo[5]), pack2bf(bo[6], bo[7]));
     }
   }
-  // column partials of this row: dgamma = dy * xh, dbeta = dy, branch colsum = bo (rows past `rows` are zero)
+  // column partials of this row: dgamma = dy * xh, dbeta = dy, branch colsum = bo (rows past `rows` are zero), all
+  // three staged in ONE LDS pass (one pair of barriers instead of three)
   float* wrow = ws + (int64_t)blockIdx.x * 3 * D;
+  const bool want[3] = {dgamma != nullptr, dbeta != nullptr, branch_colsum != nullptr};
 #pragma unroll
   for (int q = 0; q < 3; ++q) {
-    const bool want = q == 0 ? dgamma != nullptr : (q == 1 ? dbeta != nullptr : branch_colsum != nullptr);
-    if (!want) continue;
-    __syncthreads();
+    if (!want[q]) continue;
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
       float t[8];
@@ -781,22 +781,24 @@ __global__ void __launch_bounds__(512) ln_bwd16_kernel(
         t[i] = vq + __shfl_xor(vq, 32, 64);
       }
       if (lane < 32) {
-        red[wave][c * 32 + hl][0] = make_float4(t[0], t[1], t[2], t[3]);
-        red[wave][c * 32 + hl][1] = make_float4(t[4], t[5], t[6], t[7]);
+        red[q][wave][c * 32 + hl][0] = make_float4(t[0], t[1], t[2], t[3]);
+        red[q][wave][c * 32 + hl][1] = make_float4(t[4], t[5], t[6], t[7]);
       }
     }
-    __syncthreads();
-    for (int j = threadIdx.x; j < NC * 32 * 2; j += 512) {
-      const int cj = j >> 1, hh = j & 1;
-      float4 acc = red[0][cj][hh];
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < 3 * NC * 32 * 2; j += 512) {
+    const int q = j / (NC * 32 * 2), jj = j % (NC * 32 * 2);
+    if (!want[q]) continue;
+    const int cj = jj >> 1, hh = jj & 1;
+    float4 acc = red[q][0][cj][hh];
 #pragma unroll
-      for (int w = 1; w < 8; ++w) {
-        const float4 u = red[w][cj][hh];
-        acc.x += u.x; acc.y += u.y; acc.z += u.z; acc.w += u.w;
-      }
-      // (cj = c * 32 + hl owns columns (c * 32 + hl) * 8 .. + 7; hh picks the half)
-      *reinterpret_cast<float4*>(wrow + q * D + cj * 8 + hh * 4) = acc;
+    for (int w = 1; w < 8; ++w) {
+      const float4 u = red[q][w][cj][hh];
+      acc.x += u.x; acc.y += u.y; acc.z += u.z; acc.w += u.w;
     }
+    // (cj = c * 32 + hl owns columns (c * 32 + hl) * 8 .. + 7; hh picks the half)
+    *reinterpret_cast<float4*>(wrow + q * D + cj * 8 + hh * 4) = acc;
   }
   if (branch_sdot) {
     // one same-address atomic per BLOCK (per wave: 66 us for a 7984 x 768 launch, profiles/r4_s28_ln_ab.txt)

@@ -1,6 +1,7 @@
 """Per-block timeline of the ping-pong GEMM (pp_gemm_kernel) from s_memtime stamps (diagnostic build, DPH_STAMP=1).
 
-  python tools/stamp_pp.py build                       # ab/stamp_pp.so (build container)
+  python tools/stamp_pp.py build [-DDPH_PP_ABL=1|2]    # ab/stamp_pp[1|2].so (build container; 1: no main-loop
+                                                       # DMAs, 2: no main-loop MFMAs -- timing ablations)
   DPH_LIB_PATH=ab/stamp_pp.so DPH_PP_FORCE=15 python tools/stamp_pp.py time M N K [resid]   (GPU box)
 
 Stamps per block: start, prologue landed (first K-tiles in LDS), main loop done, epilogue done (after a block
@@ -21,11 +22,14 @@ if sys.argv[1] == "build":
     b.build()
     objs = [o for o in (REPO / "dphubert_amd" / "csrc" / "build").glob("*.o") if o.stem != "gemm"]
     (REPO / "ab").mkdir(exist_ok=True)
-    obj = REPO / "ab" / "gemm_stamp_pp.o"
-    subprocess.run([b.HIPCC] + b.FLAGS + ["-DDPH_STAMP=1", "-c", str(b.CSRC / "gemm.hip"), "-o", str(obj)], check=True)
-    subprocess.run([b.HIPCC, f"--offload-arch={b.ARCH}", "-shared", "-fPIC", "-o", str(REPO / "ab" / "stamp_pp.so"),
-                    str(obj)] + [str(o) for o in objs], check=True)
-    print("built ab/stamp_pp.so")
+    extra = sys.argv[2:]          # e.g. -DDPH_PP_ABL=1 ; output ab/stamp_pp<suffix>.so
+    suffix = "".join(x.split("=")[-1] for x in extra)
+    obj = REPO / "ab" / f"gemm_stamp_pp{suffix}.o"
+    subprocess.run([b.HIPCC] + b.FLAGS + ["-DDPH_STAMP=1"] + extra + ["-c", str(b.CSRC / "gemm.hip"), "-o", str(obj)],
+                   check=True)
+    subprocess.run([b.HIPCC, f"--offload-arch={b.ARCH}", "-shared", "-fPIC", "-o",
+                    str(REPO / "ab" / f"stamp_pp{suffix}.so"), str(obj)] + [str(o) for o in objs], check=True)
+    print(f"built ab/stamp_pp{suffix}.so")
 else:
     import os
 
