@@ -612,14 +612,42 @@ __global__ void conv0_bwd_finalize(const float* __restrict__ sums, const double*
 // forward pass is bitwise reproducible): x [R][K] (R = Cout*Cin_g)
 //   stage 1: part[blk][j] = sum_{r in blk} a[r][j]*b[r][j]
 //   stage 2: out[j] = sum_blk part[blk][j]  (fixed order)
-__global__ void tap_dot_partial_kernel(const float* __restrict__ a, const float* __restrict__ bb, int64_t R,
-                                       int64_t K, float* __restrict__ part, int64_t rows_per_block) {
+// 256 threads: with K <= 256, PH = 256 / K row phases per tap (thread (phase, tap) takes rows r0 + phase, + PH, ...
+// into four chains, loads of four rows in flight), the phases added in order through LDS -- a fixed order, so
+// deterministic.  (The round-4 form, one thread per tap walking its 64 rows one dependent load after the other
+// over 128-thread blocks, ran 30 us for the positional conv's 19 MB.)
+__global__ void __launch_bounds__(256) tap_dot_partial_kernel(const float* __restrict__ a,
+                                                              const float* __restrict__ bb, int64_t R, int64_t K,
+                                                              float* __restrict__ part, int64_t rows_per_block) {
+  __shared__ float red[256];
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
   const int64_t r1 = min(R, r0 + rows_per_block);
-  for (int64_t j = threadIdx.x; j < K; j += blockDim.x) {
-    float s = 0.f;
-    for (int64_t r = r0; r < r1; ++r) s = fmaf(a[r * K + j], bb[r * K + j], s);
-    part[(int64_t)blockIdx.x * K + j] = s;
+  const int PH = K <= 256 ? (int)(256 / K) : 1;
+  const int ph = (int)(threadIdx.x / (K <= 256 ? K : 256));
+  for (int64_t j = threadIdx.x % (K <= 256 ? K : 256); j < K; j += 256) {
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    int64_t r = r0 + ph;
+    if (ph < PH) {
+      for (; r + 3 * PH < r1; r += 4 * PH) {
+        s0 = fmaf(a[r * K + j], bb[r * K + j], s0);
+        s1 = fmaf(a[(r + PH) * K + j], bb[(r + PH) * K + j], s1);
+        s2 = fmaf(a[(r + 2 * PH) * K + j], bb[(r + 2 * PH) * K + j], s2);
+        s3 = fmaf(a[(r + 3 * PH) * K + j], bb[(r + 3 * PH) * K + j], s3);
+      }
+      for (; r < r1; r += PH) s0 = fmaf(a[r * K + j], bb[r * K + j], s0);
+    }
+    const float s = (s0 + s1) + (s2 + s3);
+    if (PH == 1) {
+      part[(int64_t)blockIdx.x * K + j] = s;
+    } else {
+      red[threadIdx.x] = s;
+      __syncthreads();
+      if (ph == 0) {
+        float t = 0.f;
+        for (int q = 0; q < PH; ++q) t += red[q * K + j];
+        part[(int64_t)blockIdx.x * K + j] = t;
+      }
+    }
   }
 }
 
@@ -847,7 +875,7 @@ static int tap_dot(const float* a, const float* b, int64_t R, int64_t K, float* 
   const int64_t nblk = cdiv(R, TAP_ROWS);
   DPH_REQUIRE(ws && ws_bytes >= nblk * K * 4, "weight norm: workspace too small (%lld bytes needed)",
               (long long)(nblk * K * 4));
-  hipLaunchKernelGGL(tap_dot_partial_kernel, dim3((unsigned)nblk), dim3(128), 0, stream, a, b, R, K, ws, TAP_ROWS);
+  hipLaunchKernelGGL(tap_dot_partial_kernel, dim3((unsigned)nblk), dim3(256), 0, stream, a, b, R, K, ws, TAP_ROWS);
   hipLaunchKernelGGL(tap_dot_finalize_kernel, dim3((unsigned)K), dim3(256), 0, stream, ws, nblk, K, out);
   return DPH_OK;
 }
