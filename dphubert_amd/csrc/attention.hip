@@ -50,17 +50,11 @@ __device__ __forceinline__ bf16x8_t tr_frag(const char* lds, int r0, int r1, int
   return __builtin_bit_cast(bf16x8_t, v);
 }
 
+// (one v_cvt_pk_bf16_f32 per element pair; element-wise casts came out as packs of mismatched pairs plus
+// v_alignbit / v_pk_mov shuffles)
 __device__ __forceinline__ bf16x8_t pack_frag(const f32x4_t& a, const f32x4_t& b) {
-  bf16x8_t r;
-  r[0] = (__bf16)a[0];
-  r[1] = (__bf16)a[1];
-  r[2] = (__bf16)a[2];
-  r[3] = (__bf16)a[3];
-  r[4] = (__bf16)b[0];
-  r[5] = (__bf16)b[1];
-  r[6] = (__bf16)b[2];
-  r[7] = (__bf16)b[3];
-  return r;
+  return __builtin_bit_cast(bf16x8_t, make_uint4(pack2bf(a[0], a[1]), pack2bf(a[2], a[3]), pack2bf(b[0], b[1]),
+                                                 pack2bf(b[2], b[3])));
 }
 
 __device__ __forceinline__ uint4 scale_bf16x8(uint4 v, float s) {
@@ -139,6 +133,25 @@ constexpr float L2E = 1.4426950408889634f;
 
 __device__ __forceinline__ float attn_keep(uint32_t bits, bool odd_key, uint32_t thr, float inv_keep) {
   return ((odd_key ? (bits >> 16) : (bits & 0xffffu)) >= thr) ? inv_keep : 0.f;
+}
+
+// (the select form: the WavLM dQ body, where the asm form's constant-bit SGPRs pushed the kernel into spills)
+__device__ __forceinline__ float keep_scale_x(uint32_t word, int bit, float inv_keep) {
+  return ((word >> bit) & 1u) ? inv_keep : 0.f;
+}
+// stored keep bit `bit` of `word` -> inv_keep (kept) or 0 (dropped): the bit sign-extended (v_bfe_i32) masks
+// inv_keep's bits -- two VALU ops instead of an and / compare / select.  In asm: for a constant bit the compiler
+// turns the builtin's bfe + and back into and / compare / select.  keep_scale: bit per lane (VGPR); keep_scale_u:
+// bit uniform (SGPR, s_mov'd constants in the unrolled dQ loop).
+__device__ __forceinline__ float keep_scale(uint32_t word, int bit, float inv_keep) {
+  uint32_t r;
+  asm("v_bfe_i32 %0, %1, %2, 1\n\tv_and_b32 %0, %3, %0" : "=&v"(r) : "v"(word), "v"(bit), "s"(inv_keep));
+  return __uint_as_float(r);
+}
+__device__ __forceinline__ float keep_scale_u(uint32_t word, int bit, float inv_keep) {
+  uint32_t r;
+  asm("v_bfe_i32 %0, %1, %2, 1\n\tv_and_b32 %0, %3, %0" : "=&v"(r) : "v"(word), "s"(bit), "s"(inv_keep));
+  return __uint_as_float(r);
 }
 
 // stage a [rows][64] bf16 tile (rows from row0, clamped to T) from column block col0 into LDS.
@@ -992,17 +1005,28 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const bf16_t* __restrict__ qkv
   const uint32_t thr = drop_thr(drop_p);
   const uint64_t half_tp = (uint64_t)(T + 1) >> 1;
   const bool odd_key = (lane & 1) != 0;     // key parity (k0 is a multiple of 16)
+  // A power-of-two softmax scale (64-wide heads: 1/8) is folded out of the staged Q tiles: S = Q K^T unscaled,
+  // its scale applied in the exp2 argument (L2E * scale) or the bias fma, dK = scale * dS^T Q at the store.  Each
+  // of these is exact (a power-of-two factor commutes with every rounding), so the results are bitwise those of
+  // staging bf16(scale * Q) -- without the per-tile unpack / multiply / repack of every Q element.
+  const bool fold = (__float_as_uint(scale) & 0x807fffffu) == 0u && scale != 0.f;
+  const float s_mul = fold ? scale : 1.f;          // applied to S (exp2 argument / bias fma) and to dK
+  const float q_scale = fold ? 1.f : scale;        // applied to the staged Q tile
+  const float l2s = L2E * s_mul;
   int64_t kme[NG];
   bool kpad[NG], kout[NG];   // key padded (masked -1e4) / past T
   const int T32 = (int)T;
   float kmask[NG];   // additive key mask in log2 units (-1e4 * log2 e on padded keys)
+  bool anypad = false;
 #pragma unroll
   for (int u = 0; u < NG; ++u) {
     kme[u] = k0 + 16 * u + (lane & 15);
     kpad[u] = kme[u] >= klen;
     kout[u] = kme[u] >= T;
     kmask[u] = kpad[u] ? -10000.0f * L2E : 0.f;
+    anypad = anypad || kpad[u];
   }
+  const bool wpad = __any(anypad);   // wave-uniform
 
   // K[key = lane&15][hd 32ks+8g+j], V[...]: B operands of S = Q' K^T and dP = dO V^T
   bf16x8_t kf[NG][2], vf[NG][2];
@@ -1031,7 +1055,10 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const bf16_t* __restrict__ qkv
   float* lse_s = reinterpret_cast<float*>(smem + 4 * TB);        // [2][32]
   float* dv_s = reinterpret_cast<float*>(smem + 4 * TB + 2 * QT_BWD * 4);
   float* g_s = reinterpret_cast<float*>(smem + 4 * TB + 4 * QT_BWD * 4);   // [2][32] gates (BIAS)
-  uint32_t* kw_s = reinterpret_cast<uint32_t*>(smem + 4 * TB + 6 * QT_BWD * 4);   // [2][2][32][2] keep words
+  // keep words [2 bufs][2 key tiles][2 halves][32 query rows]: the 4 consecutive query rows a lane's MFMA layout
+  // holds for one key are one 16-B read (a word per row and (row, half) pair as [2][32][2] cost one ds_read_b32 and
+  // two address ops per score)
+  uint32_t* kw_s = reinterpret_cast<uint32_t*>(smem + 4 * TB + 6 * QT_BWD * 4);
   const int nkt = (int)cdiv(T, KT);
   constexpr bool use_keep = DROP && KEEP;   // KEEP: read the forward's stored keep bits (else re-hash)
   // this lane's key inside its 64-key tile: word half and bit of the stored keep word (forward layout)
@@ -1057,11 +1084,11 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const bf16_t* __restrict__ qkv
   float lse_r = 0.f, dv_r = 0.f, g_r = 0.f;
   uint2 kw_r = make_uint2(0u, 0u);
   auto load_tiles = [&](int qt) {
-    stage_load<QT_BWD, true>(rq, rowbase + h * HD, (int64_t)qt * QT_BWD, T, RS, scale, tid);
+    stage_load<QT_BWD, true>(rq, rowbase + h * HD, (int64_t)qt * QT_BWD, T, RS, q_scale, tid);
     stage_load<QT_BWD, true>(ro, dobase, (int64_t)qt * QT_BWD, T, H * HD, hm, tid);
     if (tid < QT_BWD) {
       const int64_t q = (int64_t)qt * QT_BWD + tid;
-      lse_r = q < T ? lse[(b * H + h) * T + q] * L2E : 0.f;   // log2 units
+      lse_r = q < T ? -(lse[(b * H + h) * T + q] * L2E) : 0.f;   // -lse, log2 units
       dv_r = q < T ? Dv[(b * H + h) * T + q] : 0.f;
       if constexpr (BIAS) g_r = q < T ? rb.gate[(b * H + h) * T + q] : 0.f;
     }
@@ -1085,7 +1112,8 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const bf16_t* __restrict__ qkv
     }
     if (use_keep && tid >= 64 && tid < 128) {
       const int r = tid & 31, lt = (tid >> 5) & 1;
-      *reinterpret_cast<uint2*>(kw_s + ((buf * 2 + lt) * QT_BWD + r) * 2) = kw_r;
+      kw_s[((buf * 2 + lt) * 2 + 0) * QT_BWD + r] = kw_r.x;
+      kw_s[((buf * 2 + lt) * 2 + 1) * QT_BWD + r] = kw_r.y;
     }
   };
   load_tiles(0);
@@ -1118,11 +1146,18 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const bf16_t* __restrict__ qkv
       }
     }
     bf16x8_t pzf[NG], dsf[NG];
+    // PAD: this wave holds padded keys (>= klen; the -1e4 key mask joins the exp2 argument's constant).  Without
+    // them the constant is the staged -lse itself, no add per score.
+    auto softmax_bwd = [&](auto pad_c) {
+    constexpr bool PAD = decltype(pad_c)::value || BIAS;
 #pragma unroll
     for (int u = 0; u < NG; ++u) {
       f32x4_t pz[2], ds[2];
 #pragma unroll
       for (int w = 0; w < 2; ++w) {
+        uint4 kwv = make_uint4(0u, 0u, 0u, 0u);
+        if constexpr (use_keep)
+          kwv = *reinterpret_cast<const uint4*>(kw_s + ((cur * 2 + kt_loc[u]) * 2 + khalf[u]) * QT_BWD + 16 * w + 4 * g);
         uint32_t hb[4] = {0u, 0u, 0u, 0u};
         if constexpr (DROP) {
           if constexpr (!use_keep) {
@@ -1142,21 +1177,27 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const bf16_t* __restrict__ qkv
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int ql = 16 * w + 4 * g + i;
-          float sv = sacc[u][w][i];
-          if constexpr (BIAS) sv += g_s[cur * QT_BWD + ql] * tw[rel_idx((int)kme[u], qt * QT_BWD + ql, T32) - toff];
+          float sv = sacc[u][w][i];   // unscaled when fold
+          float p;
           // padded keys (>= klen) get the -1e4 of the key mask; keys past T and queries past T have zero K / V / Q /
           // dO / D rows, so their p never reaches a stored dK / dV row or a nonzero product
-          const float p = __builtin_amdgcn_exp2f(fmaf(sv, L2E, kmask[u] - lse_s[cur * QT_BWD + ql]));
+          const float nl = lse_s[cur * QT_BWD + ql];   // -lse (log2 units)
+          const float c = PAD ? kmask[u] + nl : nl;
+          if constexpr (BIAS) {
+            sv = fmaf(sv, s_mul, g_s[cur * QT_BWD + ql] * tw[rel_idx((int)kme[u], qt * QT_BWD + ql, T32) - toff]);
+            p = __builtin_amdgcn_exp2f(fmaf(sv, L2E, c));
+          } else {
+            p = __builtin_amdgcn_exp2f(fmaf(sv, l2s, c));
+          }
           float z = 1.f;
           if constexpr (DROP) {
-            bool keep;
             if constexpr (use_keep) {
-              const uint32_t wd = kw_s[((cur * 2 + kt_loc[u]) * QT_BWD + ql) * 2 + khalf[u]];
-              keep = ((wd >> kbit[u]) & 1u) != 0u;
+              // the keep bit sign-extended to an all-ones / zero mask over inv_keep's bits: z in {inv_keep, 0}
+              const uint32_t wd = (&kwv.x)[i];
+              z = keep_scale(wd, kbit[u], inv_keep);
             } else {
-              keep = attn_keep(hb[i], odd_key, thr, 1.f) != 0.f;
+              z = attn_keep(hb[i], odd_key, thr, 1.f) != 0.f ? inv_keep : 0.f;
             }
-            z = keep ? inv_keep : 0.f;
           }
           pz[w][i] = p * z;
           ds[w][i] = p * (pacc[u][w][i] * z - dv_s[cur * QT_BWD + ql]);
@@ -1165,6 +1206,9 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const bf16_t* __restrict__ qkv
       pzf[u] = pack_frag(pz[0], pz[1]);
       dsf[u] = pack_frag(ds[0], ds[1]);
     }
+    };
+    if (BIAS || wpad) softmax_bwd(std::integral_constant<bool, true>());
+    else softmax_bwd(std::integral_constant<bool, false>());
     // dV[key][d] += sum_q PZ[q][key] dO'[q][d] ; dK[key][d] += sum_q dS[q][key] Q'[q][d]
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
@@ -1192,7 +1236,7 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const bf16_t* __restrict__ qkv
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int d = 0; d < 4; ++d)
-          st[(16 * u + 4 * g + i) * HD + 16 * d + (lane & 15)] = f2bf(tsel == 0 ? dk[u][d][i] : dv[u][d][i]);
+          st[(16 * u + 4 * g + i) * HD + 16 * d + (lane & 15)] = f2bf(tsel == 0 ? dk[u][d][i] * s_mul : dv[u][d][i]);
     __syncthreads();
 #pragma unroll
     for (int ps = 0; ps < 16 * NG / 8; ++ps) {
@@ -1358,10 +1402,8 @@ __device__ __forceinline__ void attn_bwd_dq_body(const bf16_t* __restrict__ qkv,
             if constexpr (MASKED) p = (key >= T32 || qout[u]) ? 0.f : p;
             float z = 1.f;
             if constexpr (DROP) {
-              bool keep;
-              if constexpr (KEEP) keep = ((kw[u] >> (4 * s + i)) & 1u) != 0u;
-              else keep = attn_keep(hb[i >> 1], i & 1, thr, 1.f) != 0.f;
-              z = keep ? inv_keep : 0.f;
+              if constexpr (KEEP) z = BIAS ? keep_scale_x(kw[u], 4 * s + i, inv_keep) : keep_scale_u(kw[u], 4 * s + i, inv_keep);
+              else z = attn_keep(hb[i >> 1], i & 1, thr, 1.f) != 0.f ? inv_keep : 0.f;
             }
             const float dsv = p * (pa[u][i] * z - my_D[u]);
             ds[u][s][i] = dsv;
