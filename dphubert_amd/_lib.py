@@ -171,8 +171,9 @@ _lib = None
 # 19: DPH_GEMM_RESID_F32, dph_layernorm_fwd_x32 / _bwd_res32, dph_branch_bwd_f32, dph_distill_loss_*_ex: the fp32
 # pre-norm residual stream; 20: deterministic mode -- dph_set_deterministic / dph_get_deterministic and the workspaces
 # of the fixed-order reductions: attention prep / relpos backward, WavLM gate, conv0, GELU-mask and branch backward;
-# 21: deferred column reductions -- dph_defer_reductions / dph_flush_reductions / dph_deferred_reductions)
-ABI_VERSION = 21
+# 21: deferred column reductions -- dph_defer_reductions / dph_flush_reductions / dph_deferred_reductions;
+# 22: dph_attention_bwd_prep's D is the rowdot of dO_m itself, the head mask applied to dq / dk / dv in fp32)
+ABI_VERSION = 22
 
 
 class DphError(RuntimeError):

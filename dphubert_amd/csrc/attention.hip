@@ -920,7 +920,7 @@ __global__ void __launch_bounds__(256, 3) attn_fwd32v2_kernel(const bf16_t* __re
 }
 
 // ---------------------------------------------------------------------------
-// backward prep: rowdot[b][h][t] = sum_d dO_m * O_u ; D = sum_d bf16(hm * dO_m) * O_u ; dhm[h] += sum rowdot
+// backward prep: D[b][h][t] = rowdot = sum_d dO_m * O_u ; dhm[h] += sum rowdot
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) attn_bwd_prep_kernel(const bf16_t* __restrict__ dom,
                                                             const float* __restrict__ ou,
@@ -931,7 +931,7 @@ __global__ void __launch_bounds__(256) attn_bwd_prep_kernel(const bf16_t* __rest
   __shared__ float red[4];
   const int64_t h = blockIdx.y;
   const int64_t bt = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  float rd = 0.f, rs = 0.f;   // rowdot(dO_m, O_u) (head-mask gradient) / rowdot(dO', O_u) (D)
+  float rd = 0.f;   // rowdot(dO_m, O_u): D and the head-mask gradient
   const float hmh = head_mask ? head_mask[h] : 1.0f;
   if (bt < B * T && hmh == 0.f) {
     // skipped head (attn_fwd32_kernel): its unmasked output was never written
@@ -951,17 +951,15 @@ __global__ void __launch_bounds__(256) attn_bwd_prep_kernel(const bf16_t* __rest
         const float a0 = __uint_as_float(wa[q] << 16), a1 = __uint_as_float(wa[q] & 0xffff0000u);
         rd += a0 * wc[2 * q];
         rd += a1 * wc[2 * q + 1];
-        // D against the dO' = bf16(hm * dO_m) the dK / dV and dQ kernels multiply V by (scale_bf16x8): D must equal
-        // sum_j P_j dP_j for THOSE dP_j, or dS = P (dP - D) keeps a row sum of (hm dO_m - dO') . O, which the
-        // O-weighted key sums of dQ / dK then multiply by the keys' common component (a 0.99 head mask put the
-        // 12-layer fixture's last-layer dW_q off by 50 %)
-        const uint32_t sw = pack2bf(a0 * hmh, a1 * hmh);
-        rs += __uint_as_float(sw << 16) * wc[2 * q];
-        rs += __uint_as_float(sw & 0xffff0000u) * wc[2 * q + 1];
       }
     }
+    // D = rowdot(dO_m, O_u): the dK / dV and dQ kernels form dP from the same bf16 dO_m (the head mask factors
+    // out of dP, D and dS and is applied to their fp32 outputs), so D = sum_j P_j dP_j holds for THOSE dP_j --
+    // with a D from another rounding of dO than dP's, dS = P (dP - D) keeps a row sum that the O-weighted key
+    // sums of dQ / dK multiply by the keys' common component (a 0.99 head mask put the 12-layer fixture's
+    // last-layer dW_q off by 50 % before round 5)
     const int64_t bb = bt / T, t = bt % T;
-    Dv[(bb * H + h) * T + t] = rs;
+    Dv[(bb * H + h) * T + t] = rd;
   }
   if (!dhm) return;
   float s = wave_sum(rd);
@@ -1013,6 +1011,9 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const bf16_t* __restrict__ qkv
   const float s_mul = fold ? scale : 1.f;          // applied to S (exp2 argument / bias fma) and to dK
   const float q_scale = fold ? 1.f : scale;        // applied to the staged Q tile
   const float l2s = L2E * s_mul;
+  // the head mask factors out: dP, D (dph_attention_bwd_prep) and dS are formed from dO_m itself and dK, dV are
+  // multiplied by hm in fp32 at the store (no per-tile rounding of hm * dO_m to bf16)
+  const float dk_mul = s_mul * hm;
   int64_t kme[NG];
   bool kpad[NG], kout[NG];   // key padded (masked -1e4) / past T
   const int T32 = (int)T;
@@ -1085,7 +1086,7 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const bf16_t* __restrict__ qkv
   uint2 kw_r = make_uint2(0u, 0u);
   auto load_tiles = [&](int qt) {
     stage_load<QT_BWD, true>(rq, rowbase + h * HD, (int64_t)qt * QT_BWD, T, RS, q_scale, tid);
-    stage_load<QT_BWD, true>(ro, dobase, (int64_t)qt * QT_BWD, T, H * HD, hm, tid);
+    stage_load<QT_BWD, true>(ro, dobase, (int64_t)qt * QT_BWD, T, H * HD, 1.0f, tid);   // dO_m as is
     if (tid < QT_BWD) {
       const int64_t q = (int64_t)qt * QT_BWD + tid;
       lse_r = q < T ? -(lse[(b * H + h) * T + q] * L2E) : 0.f;   // -lse, log2 units
@@ -1236,7 +1237,7 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const bf16_t* __restrict__ qkv
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int d = 0; d < 4; ++d)
-          st[(16 * u + 4 * g + i) * HD + 16 * d + (lane & 15)] = f2bf(tsel == 0 ? dk[u][d][i] * s_mul : dv[u][d][i]);
+          st[(16 * u + 4 * g + i) * HD + 16 * d + (lane & 15)] = f2bf(tsel == 0 ? dk[u][d][i] * dk_mul : dv[u][d][i] * hm);
     __syncthreads();
 #pragma unroll
     for (int ps = 0; ps < 16 * NG / 8; ++ps) {
@@ -1276,6 +1277,7 @@ __device__ __forceinline__ void attn_bwd_dq_body(const bf16_t* __restrict__ qkv,
   const bf16_t* rowbase = qkv + b * T * RS;
   const int64_t klen = key_len ? key_len[b] : T;
   const float hm = head_mask ? head_mask[h] : 1.0f;
+  const float dq_mul = scale * hm;   // dQ = scale * hm * dS_m K (dS_m from dO_m)
   const float inv_keep = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
   int64_t qme[NG];
   uint64_t hrow[NG];
@@ -1298,7 +1300,7 @@ __device__ __forceinline__ void attn_bwd_dq_body(const bf16_t* __restrict__ qkv,
         c = *reinterpret_cast<const uint4*>(dom + (b * T + qme[u]) * (H * HD) + h * HD + ks * 32 + 8 * g);
       }
       qf[u][ks] = __builtin_bit_cast(bf16x8_t, scale_bf16x8(x, scale));
-      of[u][ks] = __builtin_bit_cast(bf16x8_t, scale_bf16x8(c, hm));
+      of[u][ks] = __builtin_bit_cast(bf16x8_t, c);   // dO_m: hm is applied to dQ (and the bias gradients) at the end
     }
     my_lse[u] = qme[u] < T ? lse[(b * H + h) * T + qme[u]] * L2E : 0.f;   // log2 units: p = 2^(s log2e - lse')
     my_D[u] = qme[u] < T ? Dv[(b * H + h) * T + qme[u]] : 0.f;
@@ -1485,19 +1487,19 @@ __device__ __forceinline__ void attn_bwd_dq_body(const bf16_t* __restrict__ qkv,
       float v = dg[u];
       v += __shfl_xor(v, 16, 64);
       v += __shfl_xor(v, 32, 64);
-      if (g == 0 && qme[u] < T) rb.dgate[(b * H + h) * T + qme[u]] = v;
+      if (g == 0 && qme[u] < T) rb.dgate[(b * H + h) * T + qme[u]] = v * hm;
     }
     __syncthreads();   // all histogram adds of the block are done
     if (det_h) {
       float* prow = rb.dtab_part + (((int64_t)b * H + h) * cdiv(T, (int64_t)RB) + bx) * HW;
-      for (int i = tid; i < HW; i += 256) prow[i] = ((dyn[i] + dyn[HW + i]) + dyn[2 * HW + i]) + dyn[3 * HW + i];
+      for (int i = tid; i < HW; i += 256) prow[i] = (((dyn[i] + dyn[HW + i]) + dyn[2 * HW + i]) + dyn[3 * HW + i]) * hm;
     } else {
       float* dt = rb.dtab + h * (2 * T - 1);
       const int off = T32 - 1 - (qb0 + RB - 1);   // global diagonal index of hist[0]
       for (int i = tid; i < T32 + RB - 1; i += 256) {
         const int gi = i + off;
         const float v = hist[i];
-        if (gi >= 0 && gi < 2 * T32 - 1 && v != 0.f) atomicAdd(dt + gi, v);
+        if (gi >= 0 && gi < 2 * T32 - 1 && v != 0.f) atomicAdd(dt + gi, v * hm);
       }
     }
   }
@@ -1508,8 +1510,8 @@ __device__ __forceinline__ void attn_bwd_dq_body(const bf16_t* __restrict__ qkv,
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
       const int col = 16 * d + 4 * g;
-      *reinterpret_cast<uint2*>(rowp + col) = make_uint2(pack2bf(dq[u][d][0] * scale, dq[u][d][1] * scale),
-                                                         pack2bf(dq[u][d][2] * scale, dq[u][d][3] * scale));
+      *reinterpret_cast<uint2*>(rowp + col) = make_uint2(pack2bf(dq[u][d][0] * dq_mul, dq[u][d][1] * dq_mul),
+                                                         pack2bf(dq[u][d][2] * dq_mul, dq[u][d][3] * dq_mul));
     }
   }
 }

@@ -287,8 +287,9 @@ int dph_attention_fwd(const void* qkv, void* o_unmasked, void* o_masked, float* 
  * stores its dropout keep decisions (1 bit per probability, uint16 per (row, 64-key tile, lane group)) and
  * the backward reads them instead of re-hashing (NULL on both sides: regenerated from (seed, element)) */
 int64_t dph_attention_keep_bytes(int64_t B, int64_t T, int64_t H);
-/* backward prep: rowdot[b][h][t] = sum_d do_m*o_u (o_u fp32) ; D = head_mask*rowdot ;
- * dhead_mask[h] += sum rowdot.  ws (deterministic mode with dhead_mask): the per-row-block head sums,
+/* backward prep: D[b][h][t] = rowdot = sum_d do_m*o_u (o_u fp32) ; dhead_mask[h] += sum rowdot.
+ * (ABI 22: D is the rowdot of do_m itself -- dph_attention_bwd forms dP and dS from do_m and applies head_mask
+ * to dq / dk / dv in fp32 -- where ABI <= 21 took the rowdot of bf16(head_mask * do_m).)  ws (deterministic mode with dhead_mask): the per-row-block head sums,
  * dph_attention_bwd_prep_workspace(B, T, H) bytes (may be NULL otherwise) */
 int64_t dph_attention_bwd_prep_workspace(int64_t B, int64_t T, int64_t H);
 int dph_attention_bwd_prep(const void* do_masked, const void* o_unmasked, const float* head_mask, float* Dvec,
