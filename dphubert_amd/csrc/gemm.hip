@@ -1917,7 +1917,8 @@ __global__ void __launch_bounds__(C::NT, C::WPE) ring_persist_kernel(const DphGe
 // Phase j of K-tile u (buffer u & 1) reads / multiplies:
 //   j=0: read A-lo, B-n0 -> MFMA A-lo x B-n0      j=1: read B-n1 -> A-lo x B-n1
 //   j=2: read A-hi       -> A-hi x B-n1           j=3: (no reads)  A-hi x B-n0 (B-n0 kept since j=0)
-// and issues ONE half-tile: j=0 B-n1(u+1), j=1 A-hi(u+1), j=2 A-lo(u+2), j=3 B-n0(u+2).  With the two
+// and issues ONE half-tile: j=0 B-n1(u+1), j=1 A-hi(u+1), j=2 A-lo(u+2), j=3 B-n0(u+2) (Cfg::B0PF: j=2 B-n0(u+2),
+// j=3 A-lo(u+2), and B-n0(u+1) read in j=3 into a second register set instead of at j=0 of u+1).  With the two
 // groups one interval apart, a stage may overwrite a half-tile two phases after its last read (WAR) and a
 // half-tile may be read one phase after the wait that retires it (RAW); the issue order above gives every
 // half-tile exactly that and keeps four half-tiles (G DMAs per thread = one K-tile) in flight across the
@@ -1948,7 +1949,19 @@ struct Cfg {
   // faster -- the 256-row tiles (8192^3 on 256 x 256: 2382 -> 2124 cycles per K-tile) and 128 x 128; the 128 x 192
   // projection shapes ran 2-3 % slower with it (tools/stamp_pp.py, profiles/r5_pp_loop_stamps.txt)
   static constexpr bool SPLITA = BM_ == 256 || (BM_ == 128 && BN_ == 128);
+  // the next K-tile's B-n0 fragments read in the last interval (pp_gemm_kernel): the PF variant below
+  static constexpr bool B0PF = false;
+  struct PF;
   static_assert(FM % 2 == 0 && FN >= 2 && RA % 64 == 0 && G < 16, "pp tile geometry");
+};
+// Cfg::PF: the B-n0 prefetch schedule of pp_gemm_kernel (tiles without the A-lo split).  Taken for ONE-ROUND
+// grids: their K-tile loop is the whole launch (7984 x 768 x 3072 on 128 x 192: 44.8 -> 40.3 us), while on
+// multi-round grids its extra registers (126 -> 202 VGPRs) keep the second block off the CU (QKV forward
+// 35.1 -> 40.0 us, profiles/r5_pp_b0pf_ab.txt)
+template <int BM_, int BN_>
+struct Cfg<BM_, BN_>::PF : Cfg<BM_, BN_> {
+  static_assert(!Cfg<BM_, BN_>::SPLITA, "B-n0 prefetch: tiles without the A-lo split");
+  static constexpr bool B0PF = true;
 };
 using P256 = Cfg<256, 256>;
 using P128x256 = Cfg<128, 256>;
@@ -2083,8 +2096,12 @@ __global__ void __launch_bounds__(C::NT, C::WPE) pp_gemm_kernel(const DphGemmArg
   // during K-tile u's last (A-high x B-n0) interval -- its half-tile landed two intervals earlier -- so every
   // interval carries at most FM2 * 2 or FN0 * 2 fragment reads (4 / 2 / 4 / 4 on the 128 x 192 tile instead of
   // 8 / 2 / 4 / 0, whose 8-read interval left the next MFMA cluster waiting on its LDS reads)
-  bf16x8_t falo[C::FM2][2] = {}, fa_hi_[C::FM2][2] = {}, fb0[C::FN0][2] = {}, fb1[C::FN1][2] = {};
+  bf16x8_t falo[C::FM2][2] = {}, fa_hi_[C::FM2][2] = {}, fb0x[C::FN0][2] = {}, fb0y[C::FN0][2] = {}, fb1[C::FN1][2] = {};
   bf16x8_t (&fahi)[C::FM2][2] = C::SPLITA ? fa_hi_ : falo;   // one A fragment set where the split is not taken
+  // Cfg::B0PF: the B-n0 fragments of K-tile u + 1 are read in K-tile u's last interval, beside its A-hi x B-n0
+  // cluster (two register sets, alternating per K-tile): its half-tile landed by that interval's counted wait
+  // (issued one K-tile earlier), so no wait moves -- the 8-read first interval of a K-tile becomes a 4-read one
+  constexpr bool B0PF = C::B0PF;
 
   auto rd_a = [&](const char* ht, bf16x8_t (&fa)[C::FM2][2]) {
     if (PP_ABL_READ) return;
@@ -2093,7 +2110,7 @@ __global__ void __launch_bounds__(C::NT, C::WPE) pp_gemm_kernel(const DphGemmArg
 #pragma unroll
       for (int s = 0; s < 2; ++s) fa[i][s] = hfrag(ht, wr * HA + 16 * i, s, lane);
   };
-  auto rd_b0 = [&](const char* bu) {
+  auto rd_b0 = [&](const char* bu, bf16x8_t (&fb0)[C::FN0][2]) {
     if (PP_ABL_READ) return;
 #pragma unroll
     for (int j = 0; j < C::FN0; ++j)
@@ -2108,7 +2125,7 @@ __global__ void __launch_bounds__(C::NT, C::WPE) pp_gemm_kernel(const DphGemmArg
       for (int s = 0; s < 2; ++s) fb1[j][s] = hfrag(bu + C::O_B1, wc * 16 * C::FN1 + 16 * j, s, lane);
   };
   // MFMA cluster: rows [i0, i0 + FM2) (fragments fa) x the given B fragment set
-  auto mm0 = [&](int i0, const bf16x8_t (&fa)[C::FM2][2]) {
+  auto mm0 = [&](int i0, const bf16x8_t (&fa)[C::FM2][2], const bf16x8_t (&fb0)[C::FN0][2]) {
     if (PP_ABL_MFMA) return;
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -2139,30 +2156,39 @@ __global__ void __launch_bounds__(C::NT, C::WPE) pp_gemm_kernel(const DphGemmArg
   };
   // prologue: the half-tiles of "phases" -6 .. -1 (A-lo(0), B-n0(0), B-n1(0), A-hi(0), A-lo(1), B-n0(1)),
   // then wait for A-lo(0) and B-n0(0)
-  st_alo(0);
-  st_b0(0);
-  st_b1(0);
-  st_ahi(0);
-  st_alo(1);
-  st_b0(1);
+  if constexpr (B0PF) {   // (B-n0 staged before A-lo: see kstep)
+    st_b0(0);
+    st_alo(0);
+    st_b1(0);
+    st_ahi(0);
+    st_b0(1);
+    st_alo(1);
+  } else {
+    st_alo(0);
+    st_b0(0);
+    st_b1(0);
+    st_ahi(0);
+    st_alo(1);
+    st_b0(1);
+  }
   vm_wait<G>();
   bar();
   DPH_TSTAMP(st1);
   if constexpr (C::SPLITA) rd_a(buf(0) + C::O_ALO, falo);
+  if constexpr (B0PF) rd_b0(buf(0), fb0x);
   if (wr == 1) bar();            // group 1 runs one interval behind group 0
-  int u = 0;
-#pragma unroll 1
-  for (; u + 2 < nk; ++u) {
+  // one K-tile of the main loop; fbc: this tile's B-n0 fragments, fbn: the next tile's (B0PF)
+  auto kstep = [&](int u, bf16x8_t (&fbc)[C::FN0][2], bf16x8_t (&fbn)[C::FN0][2]) {
     const char* bu = buf(u);
     // j = 0
-    rd_b0(bu);
+    if constexpr (!B0PF) rd_b0(bu, fbc);
     if constexpr (!C::SPLITA) rd_a(bu + C::O_ALO, falo);
     st_b1(u + 1);
     vm_wait<G>();
     lbar();
     lgkm0();
     __builtin_amdgcn_sched_barrier(0);
-    mm0(0, falo);
+    mm0(0, falo, fbc);
     lbar();
     // j = 1
     rd_b1(bu);
@@ -2173,70 +2199,108 @@ __global__ void __launch_bounds__(C::NT, C::WPE) pp_gemm_kernel(const DphGemmArg
     __builtin_amdgcn_sched_barrier(0);
     mm1(0, falo);
     lbar();
-    // j = 2
+    // j = 2 (B0PF: B-n0(u + 2) here and A-lo(u + 2) at j = 3, so that B-n0(u + 1) is retired by THIS wait -- in
+    // both wave groups by the barrier after group 0's j = 3 wait, where group 0 reads it)
     rd_a(bu + C::O_AHI, fahi);
-    st_alo(u + 2);
+    if constexpr (B0PF) st_b0(u + 2);
+    else st_alo(u + 2);
     vm_wait<G>();
     lbar();
     lgkm0();
     __builtin_amdgcn_sched_barrier(0);
     mm1(C::FM2, fahi);
     lbar();
-    // j = 3 (A-lo(u + 1): landed by the vm_wait of j = 2, visible after its barrier; not waited for here)
+    // j = 3 (SPLITA: A-lo(u + 1) landed by the vm_wait of j = 2, visible after its barrier; not waited for here.
+    // B0PF: B-n0(u + 1), issued at j = 2 of K-tile u - 1, retired by both groups' j = 2 waits: group 0 reads it
+    // after the barrier that pairs its j = 3 wait with group 1's j = 2 wait, group 1 one interval later)
     if constexpr (C::SPLITA) rd_a(buf(u + 1) + C::O_ALO, falo);
-    st_b0(u + 2);
+    if constexpr (B0PF) st_alo(u + 2);
+    else st_b0(u + 2);
     vm_wait<G>();
     lbar();
-    mm0(C::FM2, fahi);
+    if constexpr (B0PF) {
+      rd_b0(buf(u + 1), fbn);
+      __builtin_amdgcn_sched_barrier(0);   // (issued ahead of the cluster, not sunk below it)
+    }
+    mm0(C::FM2, fahi, fbc);
     lbar();
-  }
+  };
   // the last two K-tiles: nothing staged past nk - 1, the counted waits drain
+  auto tail = [&](int u, bf16x8_t (&fbc)[C::FN0][2], bf16x8_t (&fbn)[C::FN0][2]) {
 #pragma unroll
-  for (int t = 0; t < 2; ++t, ++u) {
-    const bool second_last = t == 0;
-    const char* bu = buf(u);
-    rd_b0(bu);
-    if constexpr (!C::SPLITA) rd_a(bu + C::O_ALO, falo);
-    if (second_last) {
-      st_b1(u + 1);
-      vm_wait<G>();
-    } else {
-      vm_wait<C::GA>();
+    for (int t = 0; t < 2; ++t, ++u) {
+      const bool second_last = t == 0;
+      const char* bu = buf(u);
+      bf16x8_t (&fb)[C::FN0][2] = (B0PF && t == 1) ? fbn : fbc;
+      if constexpr (!B0PF) rd_b0(bu, fb);
+      if constexpr (!C::SPLITA) rd_a(bu + C::O_ALO, falo);
+      if (second_last) {
+        st_b1(u + 1);
+        vm_wait<G>();
+      } else {
+        vm_wait<C::GA>();
+      }
+      lbar();
+      lgkm0();
+      __builtin_amdgcn_sched_barrier(0);
+      mm0(0, falo, fb);
+      lbar();
+      rd_b1(bu);
+      if (second_last) {
+        st_ahi(u + 1);
+        vm_wait<G>();
+      } else {
+        vm_wait<0>();
+      }
+      lbar();
+      lgkm0();
+      __builtin_amdgcn_sched_barrier(0);
+      mm1(0, falo);
+      lbar();
+      rd_a(bu + C::O_AHI, fahi);
+      if (second_last) {
+        if constexpr (B0PF) vm_wait<C::GB1 + C::GA>();   // B-n0(u + 1) and A-lo(u + 1) retired
+        else vm_wait<G - C::GA>();
+      } else {
+        vm_wait<0>();
+      }
+      lbar();
+      lgkm0();
+      __builtin_amdgcn_sched_barrier(0);
+      mm1(C::FM2, fahi);
+      lbar();
+      if (second_last) {
+        if constexpr (C::SPLITA) rd_a(buf(u + 1) + C::O_ALO, falo);   // (landed by the j = 2 wait above)
+        vm_wait<C::GB1 + C::GA>();   // (B-n0(u + 1), issued one K-tile earlier, is done)
+      } else {
+        vm_wait<0>();
+      }
+      lbar();
+      if (B0PF && second_last) {
+        rd_b0(buf(u + 1), fbn);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      mm0(C::FM2, fahi, fb);
+      lbar();
     }
-    lbar();
-    lgkm0();
-    __builtin_amdgcn_sched_barrier(0);
-    mm0(0, falo);
-    lbar();
-    rd_b1(bu);
-    if (second_last) {
-      st_ahi(u + 1);
-      vm_wait<G>();
-    } else {
-      vm_wait<0>();
+  };
+  int u = 0;
+  if constexpr (B0PF) {
+#pragma unroll 1
+    for (; u + 3 < nk; u += 2) {
+      kstep(u, fb0x, fb0y);
+      kstep(u + 1, fb0y, fb0x);
     }
-    lbar();
-    lgkm0();
-    __builtin_amdgcn_sched_barrier(0);
-    mm1(0, falo);
-    lbar();
-    rd_a(bu + C::O_AHI, fahi);
-    if (second_last) vm_wait<G - C::GA>();
-    else vm_wait<0>();
-    lbar();
-    lgkm0();
-    __builtin_amdgcn_sched_barrier(0);
-    mm1(C::FM2, fahi);
-    lbar();
-    if (second_last) {
-      if constexpr (C::SPLITA) rd_a(buf(u + 1) + C::O_ALO, falo);   // (landed by the j = 2 wait above)
-      vm_wait<C::GB1 + C::GA>();
+    if (u + 2 < nk) {
+      kstep(u, fb0x, fb0y);
+      tail(u + 1, fb0y, fb0x);
     } else {
-      vm_wait<0>();
+      tail(u, fb0x, fb0y);
     }
-    lbar();
-    mm0(C::FM2, fahi);
-    lbar();
+  } else {
+#pragma unroll 1
+    for (; u + 2 < nk; ++u) kstep(u, fb0x, fb0x);
+    tail(u, fb0x, fb0x);
   }
   if (wr == 0) bar();            // pairs with group 1's extra barrier
   DPH_TSTAMP(st2);
@@ -2776,6 +2840,12 @@ static bool pp_enabled() {
 // tile's measured rate (8192^3 random bf16, tools/gemm_ab.py: 256x256 1514, 128x192 1282, 128x256 1221,
 // 256x128 1211, 128x128 1178 TFLOP/s; a 128x128 block shares its CU with a second one).  Picks 256x256 for the
 // many-round conv GEMMs and 128x192 for the M = B*T projections (756 / 252 tiles = whole rounds on 256 CUs).
+// DPH_PP_B0PF=0: one-round 128 x 192 grids on the plain schedule too (A/B and the bitwise test; read per call)
+static bool pp_b0pf() {
+  const char* e = getenv("DPH_PP_B0PF");
+  return !(e && e[0] == '0');
+}
+
 static int pp_pick(const DphGemmArgs& a) {
   struct Opt { int kind, bm, bn, per_cu; double tf; };
   static const Opt opts[] = {{12, 256, 256, 1, 1514.0}, {15, 128, 192, 1, 1282.0}, {13, 128, 256, 1, 1221.0},
@@ -3269,8 +3339,12 @@ extern "C" int dph_gemm(const DphGemmArgs* args, hipStream_t stream) {
     if (kind == 12) launch_pp<pp::P256>(b, stream);
     else if (kind == 13) launch_pp<pp::P128x256>(b, stream);
     else if (kind == 14) launch_pp<pp::P256x128>(b, stream);
-    else if (kind == 15) launch_pp<pp::P128x192>(b, stream);
-    else launch_pp<pp::P128>(b, stream);
+    else if (kind == 15) {
+      if (pp_b0pf() && cdiv(a.M, 128) * cdiv(a.N, 192) * a.batch <= num_cus()) launch_pp<pp::P128x192::PF>(b, stream);
+      else launch_pp<pp::P128x192>(b, stream);
+    } else {
+      launch_pp<pp::P128>(b, stream);
+    }
   } else if (kind == 10) {
     DPH_REQUIRE(cdiv(a.M, ring::Tri::BM) < 65536 && a.batch * a.splits < 65536, "dph_gemm: grid too large");
     if (!launch_ring_persist<ring::Tri>(b, stream)) launch_ring<ring::Tri, false>(b, kchunk, stream);

@@ -10,7 +10,7 @@ torch.manual_seed(0)
 
 
 @pytest.fixture(autouse=True, params=["small", "mid", "big", "wide", "flat", "flat-np", "tall", "half", "mid8",
-                                     "mid8mn", "tri", "tri-np", "pp256", "pp128x256", "pp256x128", "pp128x192", "pp128", "ppw"])
+                                     "mid8mn", "tri", "tri-np", "pp256", "pp128x256", "pp256x128", "pp128x192", "pp128x192-nopf", "pp128", "ppw"])
 def gemm_path(request, monkeypatch):
     """Run every test on each GEMM path: the 128x128 register-staged kernel and the 128x128 /
     256x256 / 256x128 / 128x256 / 256x64 / 192x128 LDS-DMA ring kernels (taken where their constraints hold: both operands
@@ -19,6 +19,9 @@ def gemm_path(request, monkeypatch):
     if path.endswith("-np"):            # one tile per block instead of the persistent grid
         monkeypatch.setenv("DPH_GEMM_PERSIST", "0")
         path = path[:-3]
+    if path.endswith("-nopf"):          # one-round 128 x 192 grids on the plain schedule (no B-n0 prefetch)
+        monkeypatch.setenv("DPH_PP_B0PF", "0")
+        path = path[:-5]
     monkeypatch.setenv("DPH_GEMM_PATH", path)
     return request.param
 
@@ -383,3 +386,22 @@ def test_gelu_dgk_pair_matches_recompute(p):
     live = cm != 0
     close(ca1[live], ca0[live], 2e-2)
     assert torch.count_nonzero(ca1[~live]) == 0
+
+
+@pytest.mark.parametrize("M,N,K", [(7984, 768, 3072), (7984, 768, 768), (1000, 264, 512)])
+def test_pp_b0_prefetch_bitwise(gemm_path, monkeypatch, M, N, K):
+    """The B-n0 prefetch schedule of the one-round 128 x 192 ping-pong grids (pp::Cfg::PF) issues the same MFMAs in
+    the same order into every accumulator as the plain schedule: bitwise equal outputs (residual epilogue)."""
+    if gemm_path != "pp128x192":
+        pytest.skip("one tile path is enough")
+    K_ = _k()
+    A, B, R = rnd(M, K), rnd(N, K, scale=0.05), rnd(M, N)
+    outs = []
+    for pf in ("1", "0"):
+        monkeypatch.setenv("DPH_PP_B0PF", pf)
+        C = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        K_.gemm(K_.dense(A), K_.dense(B), K_.dense(C), M, N, K, a_kcontig=True, b_kcontig=True, residual=R)
+        torch.cuda.synchronize()
+        outs.append(C)
+    assert torch.equal(outs[0].view(torch.int16), outs[1].view(torch.int16))
+    close(outs[0], A.float() @ B.float().t() + R.float())
