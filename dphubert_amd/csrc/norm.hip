@@ -346,9 +346,12 @@ __global__ void __launch_bounds__(1024) wave_norm_kernel(const float* __restrict
 }
 
 // column partial sums of x [rows][cols] bf16: block (blockIdx.x: 512-column chunk, blockIdx.y: range of
-// rows_per_block rows) = 64 x 4 threads, 8 columns per thread -> ws[blockIdx.y][cols]
+// rows_per_block rows) = 64 x 4 threads, 8 columns per thread -> ws[blockIdx.y][cols].  ld: x's row stride;
+// logical column c reads physical column c + (c >= skip0 ? skipn : 0) (dph_colsum3 without its middle segment:
+// the q / v bias gradients read 2/3 of the fused dqkv rows, skip0 and skipn multiples of 8)
 __global__ void __launch_bounds__(256) colsum_kernel(const bf16_t* __restrict__ x, float* __restrict__ ws,
-                                                     int64_t rows, int64_t cols, int64_t rows_per_block) {
+                                                     int64_t rows, int64_t cols, int64_t rows_per_block, int64_t ld,
+                                                     int64_t skip0, int64_t skipn) {
   __shared__ float red[4][512];
   const int tx = threadIdx.x & 63;
   const int ty = threadIdx.x >> 6;
@@ -356,9 +359,11 @@ __global__ void __launch_bounds__(256) colsum_kernel(const bf16_t* __restrict__ 
   const int64_t r0 = (int64_t)blockIdx.y * rows_per_block;
   const int64_t r1 = min(rows, r0 + rows_per_block);
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  const bool vec = (c0 + 8 <= cols) && (cols % 8 == 0);
+  const bool vec = (c0 + 8 <= cols) && (cols % 8 == 0) && (ld % 8 == 0);
+  const int64_t pc0 = c0 + (c0 >= skip0 ? skipn : 0);
+#pragma unroll 4
   for (int64_t r = r0 + ty; r < r1; r += 4) {
-    const bf16_t* p = x + r * cols + c0;
+    const bf16_t* p = x + r * ld + pc0;
     if (vec) {
       uint4 raw = *reinterpret_cast<const uint4*>(p);
       uint32_t w[4] = {raw.x, raw.y, raw.z, raw.w};
@@ -1146,7 +1151,7 @@ extern "C" int dph_colsum(const void* x, float* out, int64_t rows, int64_t cols,
   const int64_t nrb = cdiv(rows, rpb);
   dim3 grid((unsigned)cdiv(cols, 512), (unsigned)nrb);
   hipLaunchKernelGGL(colsum_kernel, grid, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(x), ws, rows, cols,
-                     rpb);
+                     rpb, cols, cols, (int64_t)0);
   slab_reduce_launch(ws, nrb, cols, cols, out, nullptr, nullptr, stream);
   return check_launch("dph_colsum");
 }
@@ -1162,9 +1167,17 @@ extern "C" int dph_colsum3(const void* x, float* out0, float* out1, float* out2,
   DPH_REQUIRE(ws && ws_bytes >= dph_colsum_workspace(rows, cols), "dph_colsum3: workspace too small");
   const int64_t rpb = colsum_rpb(rows);
   const int64_t nrb = cdiv(rows, rpb);
+  if (out1 == nullptr && out0 && out2 && seg % 8 == 0) {
+    // the middle segment skipped: only the outer two are read (the slab holds [seg | seg])
+    dim3 grid2((unsigned)cdiv(2 * seg, 512), (unsigned)nrb);
+    hipLaunchKernelGGL(colsum_kernel, grid2, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(x), ws, rows,
+                       2 * seg, rpb, cols, seg, seg);
+    slab_reduce_launch(ws, nrb, 2 * seg, seg, out0, out2, nullptr, stream);
+    return check_launch("dph_colsum3");
+  }
   dim3 grid((unsigned)cdiv(cols, 512), (unsigned)nrb);
   hipLaunchKernelGGL(colsum_kernel, grid, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(x), ws, rows, cols,
-                     rpb);
+                     rpb, cols, cols, (int64_t)0);
   slab_reduce_launch(ws, nrb, cols, seg, out0, out1, out2, stream);
   return check_launch("dph_colsum3");
 }

@@ -685,3 +685,25 @@ def test_ffn_compaction_matches_full_width(monkeypatch, pre_norm):
             assert a.norm().item() == 0.0, n
             continue
         assert (a - b).norm().item() / den < 2e-2, (n, (a - b).norm().item() / den)
+
+
+@pytest.mark.parametrize("skip_k", [True, False])
+def test_colsum3_segments(skip_k):
+    """dph_colsum3 (the fused q/k/v bias gradients): with the k output NULL only the q and v segments are read
+    (column-remapped slab), with it every segment -- each against a float64 column sum of the same bf16 rows."""
+    from dphubert_amd import _lib
+    from dphubert_amd._lib import call, ptr
+    from dphubert_amd.ops import colsum_ws
+    M, seg = 7984, 768
+    g = torch.Generator(device="cpu").manual_seed(3)
+    x = torch.randn(M, 3 * seg, generator=g).to(torch.bfloat16).to(DEV)
+    outs = [torch.full((seg,), 0.5, device=DEV) for _ in range(3)]
+    call("dph_colsum3", ptr(x), ptr(outs[0]), None if skip_k else ptr(outs[1]), ptr(outs[2]), M, seg,
+         *colsum_ws(M, 3 * seg, DEV), _lib.stream_ptr())
+    torch.cuda.synchronize()
+    want = x.double().sum(0).view(3, seg).cpu() + 0.5
+    for i in range(3):
+        if skip_k and i == 1:
+            assert torch.equal(outs[1].cpu(), torch.full((seg,), 0.5))   # untouched
+            continue
+        torch.testing.assert_close(outs[i].double().cpu(), want[i], rtol=0, atol=2e-3)
