@@ -380,6 +380,11 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    # host-side accounting of the timed loop: the step-scalar ring blocks the host once it runs RING steps ahead
+    # of the GPU (stepstate.StepScalars), so the loop's host time minus that blocked time is the enqueue cost
+    scal = trainer._bind_scalars(dev)
+    scal.wait_s = 0.0
+    trainer.host_s = {"upload": 0.0, "replay": 0.0, "replays": 0}
     t0 = time.perf_counter()
     in_loop = prof is not None and prof_mode != "eager step right after the timed region (same kernels)"
     last_final = (args.steps // args.accum) * args.accum - 1    # the last micro-step that ends an optimizer step
@@ -404,7 +409,14 @@ def main():
     ms = dt / args.steps * 1e3
     audio_s = world * audio_timed            # (every rank processes the same amount: shapes per rank differ)
     value = audio_s / dt
-    log(f"host enqueue {t_host / args.steps * 1e3:.2f} ms/step")
+    host = {"host_loop_ms": round(t_host / args.steps * 1e3, 3),
+            "host_blocked_ms": round(scal.wait_s / args.steps * 1e3, 3),
+            "host_enqueue_ms": round((t_host - scal.wait_s) / args.steps * 1e3, 3),
+            "host_replay_ms": round(trainer.host_s["replay"] / max(1, trainer.host_s["replays"]) * 1e3, 3),
+            "host_upload_ms": round((trainer.host_s["upload"] - scal.wait_s) / args.steps * 1e3, 3)}
+    log(f"host loop {host['host_loop_ms']:.2f} ms/step = enqueue {host['host_enqueue_ms']:.2f} "
+        f"(hipGraphLaunch {host['host_replay_ms']:.2f}, scalar upload {host['host_upload_ms']:.3f}) + blocked on the "
+        f"step-scalar ring {host['host_blocked_ms']:.2f}")
     log(f"loss {loss.item():.5f}  step {ms:.2f} ms  {value:.1f} audio-s/s  "
         f"({flop_utt * args.batch / (ms / 1e3) / 1e12:.0f} TFLOP/s algorithmic/GPU)")
     terms = {k: (float(v.float().sum()) if torch.is_tensor(v) else v)
@@ -443,6 +455,7 @@ def main():
                    "lengths": args.lengths, "masks": args.masks},
         "peak_hbm_gib": round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 2),
         "step_mode": "hip_graph" if graphed else "eager",
+        "host": host,
     }
     if ddp_plan is not None:
         out["ddp_plan"] = ddp_plan

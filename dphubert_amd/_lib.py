@@ -72,6 +72,8 @@ _SIGS = {
     "dph_defer_reductions": ([C.c_int], C.c_int),
     "dph_flush_reductions": ([S], C.c_int),
     "dph_deferred_reductions": ([], i64),
+    "dph_discard_reductions": ([], i64),
+    "dph_reductions_pushed": ([], i64),
     "dph_gemm": ([C.POINTER(DphGemmArgs), S], C.c_int),
     "dph_gemm_mn_plan": ([i64, i64, i64, i64], C.c_int),
     "dph_gemm_grouped": ([C.POINTER(DphGemmArgs), C.POINTER(DphGemmGroup), S], C.c_int),
@@ -172,8 +174,9 @@ _lib = None
 # pre-norm residual stream; 20: deterministic mode -- dph_set_deterministic / dph_get_deterministic and the workspaces
 # of the fixed-order reductions: attention prep / relpos backward, WavLM gate, conv0, GELU-mask and branch backward;
 # 21: deferred column reductions -- dph_defer_reductions / dph_flush_reductions / dph_deferred_reductions;
-# 22: dph_attention_bwd_prep's D is the rowdot of dO_m itself, the head mask applied to dq / dk / dv in fp32)
-ABI_VERSION = 22
+# 22: dph_attention_bwd_prep's D is the rowdot of dO_m itself, the head mask applied to dq / dk / dv in fp32;
+# 23: dph_discard_reductions / dph_reductions_pushed, queue-flush launch errors propagated by every column reduction)
+ABI_VERSION = 23
 
 
 class DphError(RuntimeError):
@@ -245,8 +248,25 @@ def ptr(t):
 CALL_HOOK = [None]
 
 
+# Tracing (SURVEY 5 "Tracing / profiling"): with DPH_TRACE=1 (or set_trace(True)) every C-ABI call runs inside a
+# torch.profiler.record_function range named after the entry point, so a torch.profiler / Kineto trace shows which
+# library call enqueued each HIP kernel next to the reference's module names.  Off by default: a range costs a few
+# microseconds of host time per call (there are ~600 calls in an eager step).  Inside a HIP-graph capture the ranges
+# mark the capture, not the replays.
+TRACE = [os.environ.get("DPH_TRACE", "0") == "1"]
+
+
+def set_trace(on: bool) -> bool:
+    prev, TRACE[0] = TRACE[0], bool(on)
+    return prev
+
+
 def call(name: str, *args):
     fn = getattr(lib(), name)
     hook = CALL_HOOK[0]
-    rc = hook(name, fn, args) if hook is not None else fn(*args)
+    if TRACE[0]:
+        with torch.profiler.record_function(f"dph::{name}"):
+            rc = hook(name, fn, args) if hook is not None else fn(*args)
+    else:
+        rc = hook(name, fn, args) if hook is not None else fn(*args)
     check(rc, name)

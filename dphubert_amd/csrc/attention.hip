@@ -1749,7 +1749,7 @@ extern "C" int dph_attention_bwd_prep(const void* do_masked, const void* o_unmas
   hipLaunchKernelGGL(attn_bwd_prep_kernel, grid, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(do_masked),
                      reinterpret_cast<const float*>(o_unmasked), head_mask, Dvec, dhead_mask, B, T, H,
                      det ? ws : nullptr);
-  if (det) slab_reduce_cols(ws, grid.x, H, H, dhead_mask, nullptr, nullptr, stream);
+  if (det) DPH_TRY(slab_reduce_cols(ws, grid.x, H, H, dhead_mask, nullptr, nullptr, stream));
   return check_launch("dph_attention_bwd_prep");
 }
 

@@ -29,13 +29,20 @@ bool deterministic();
 // deferred fixed-order column reductions (runtime.hip, dph_defer_reductions): while deferring, a slab reduction
 // out[j] += sum_r ws[r * ld + j] (j < n) is queued by colred_push and launched with the rest by dph_flush_reductions
 bool colred_deferring();
-void colred_push(const float* ws, int64_t nrows, int64_t ld, int64_t n, float* out, hipStream_t stream);
+int colred_push(const float* ws, int64_t nrows, int64_t ld, int64_t n, float* out, hipStream_t stream);
 // norm.hip: o_q[c] += sum_r ws[r][q * seg + c] over the column segments q of a [nrows][ncols] fp32 partial slab (NULL
 // outputs skipped); fixed order in deterministic mode, row groups + one atomic per column per group otherwise
-void slab_reduce_cols(const float* ws, int64_t nrows, int64_t ncols, int64_t seg, float* o0, float* o1, float* o2,
+int slab_reduce_cols(const float* ws, int64_t nrows, int64_t ncols, int64_t seg, float* o0, float* o1, float* o2,
                       hipStream_t stream);
 // norm.hip: out[0] += sum of n partials, in order (one wave)
 void sdot_reduce(const float* part, int64_t n, float* out, hipStream_t stream);
+
+// propagate a non-OK DPH_* code from a host-side helper (its error text is already set)
+#define DPH_TRY(expr)                       \
+  do {                                      \
+    const int dph_try_rc_ = (expr);         \
+    if (dph_try_rc_ != DPH_OK) return dph_try_rc_; \
+  } while (0)
 
 #define DPH_REQUIRE(cond, ...)              \
   do {                                      \

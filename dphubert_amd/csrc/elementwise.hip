@@ -295,7 +295,7 @@ extern "C" int dph_col2im_gelu_bwd(const void* dcols, int64_t B, int64_t Lout, i
   hipLaunchKernelGGL(gelu_mask_bwd_kernel<true>, grid, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(dcols),
                      Lout, Lin, C, (int)k, (int)s, reinterpret_cast<const bf16_t*>(z_pre), mask,
                      reinterpret_cast<bf16_t*>(out), dmask, rows, rpb, part);
-  if (part) slab_reduce_cols(part, nrb, C, C, dmask, nullptr, nullptr, stream);
+  if (part) DPH_TRY(slab_reduce_cols(part, nrb, C, C, dmask, nullptr, nullptr, stream));
   return check_launch("dph_col2im_gelu_bwd");
 }
 
@@ -310,7 +310,7 @@ extern "C" int dph_gelu_mask_bwd(const void* dy, const void* z_pre, const float*
   hipLaunchKernelGGL(gelu_mask_bwd_kernel<false>, grid, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(dy),
                      (int64_t)1, (int64_t)1, C, 1, 1, reinterpret_cast<const bf16_t*>(z_pre), mask,
                      reinterpret_cast<bf16_t*>(out), dmask, rows, rpb, part);
-  if (part) slab_reduce_cols(part, nrb, C, C, dmask, nullptr, nullptr, stream);
+  if (part) DPH_TRY(slab_reduce_cols(part, nrb, C, C, dmask, nullptr, nullptr, stream));
   return check_launch("dph_gelu_mask_bwd");
 }
 
@@ -580,7 +580,7 @@ extern "C" int dph_branch_bwd(const void* dy, void* out, int64_t rows, int64_t c
   hipLaunchKernelGGL((branch_bwd_kernel<bf16_t, bf16_t>), grid, dim3(256), 0, stream,
                      reinterpret_cast<const bf16_t*>(dy), reinterpret_cast<bf16_t*>(out), rows, cols, p, seed, smask,
                      row_len, len_rows, colsum, reinterpret_cast<const bf16_t*>(pre), sdot, rpb, part);
-  if (part && colsum) slab_reduce_cols(part, nrb, cols, cols, colsum, nullptr, nullptr, stream);
+  if (part && colsum) DPH_TRY(slab_reduce_cols(part, nrb, cols, cols, colsum, nullptr, nullptr, stream));
   if (part && sdot) sdot_reduce(part + nrb * cols, nrb * (int64_t)grid.x, sdot, stream);
   return check_launch("dph_branch_bwd");
 }
@@ -605,7 +605,7 @@ extern "C" int dph_branch_bwd_f32(const float* dy, void* out, int out_f32, int64
     hipLaunchKernelGGL((branch_bwd_kernel<float, bf16_t>), grid, dim3(256), 0, stream, dy,
                        reinterpret_cast<bf16_t*>(out), rows, cols, p, seed, smask, row_len, len_rows, colsum,
                        reinterpret_cast<const bf16_t*>(pre), sdot, rpb, part);
-  if (part && colsum) slab_reduce_cols(part, nrb, cols, cols, colsum, nullptr, nullptr, stream);
+  if (part && colsum) DPH_TRY(slab_reduce_cols(part, nrb, cols, cols, colsum, nullptr, nullptr, stream));
   if (part && sdot) sdot_reduce(part + nrb * cols, nrb * (int64_t)grid.x, sdot, stream);
   return check_launch("dph_branch_bwd_f32");
 }

@@ -3417,8 +3417,8 @@ extern "C" int dph_gemm(const DphGemmArgs* args, hipStream_t stream) {
     // deterministic mode: each column's rows in a fixed order)
     if (colred_deferring()) {
       const float* sl = reinterpret_cast<const float*>(a.workspace);
-      colred_push(sl, nslots, a.N, csn, a.colsum_out, stream);
-      colred_push(sl + nslots * a.N, nslots, a.N, csn, a.colsum_aux, stream);
+      DPH_TRY(colred_push(sl, nslots, a.N, csn, a.colsum_out, stream));
+      DPH_TRY(colred_push(sl + nslots * a.N, nslots, a.N, csn, a.colsum_aux, stream));
     } else if (deterministic()) {
       hipLaunchKernelGGL(colsum_slab_reduce_det_kernel, dim3((unsigned)cdiv(csn, 32)), dim3(32 * DET_PH), 0, stream,
                          reinterpret_cast<const float*>(a.workspace), nslots, a.N, csn, a.colsum_out, a.colsum_aux);

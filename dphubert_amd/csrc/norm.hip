@@ -530,13 +530,15 @@ __global__ void __launch_bounds__(64) sdot_reduce_kernel(const float* __restrict
   if (threadIdx.x == 0) out[0] += s;
 }
 
-void slab_reduce_launch(const float* ws, int64_t nrows, int64_t ncols, int64_t seg, float* o0, float* o1, float* o2,
-                        hipStream_t stream) {
+int slab_reduce_launch(const float* ws, int64_t nrows, int64_t ncols, int64_t seg, float* o0, float* o1, float* o2,
+                       hipStream_t stream) {
   if (colred_deferring()) {
     float* outs[3] = {o0, o1, o2};
-    for (int q = 0; q < 3 && q * seg < ncols; ++q)
-      colred_push(ws + q * seg, nrows, ncols, std::min<int64_t>(seg, ncols - q * seg), outs[q], stream);
-    return;
+    for (int q = 0; q < 3 && q * seg < ncols; ++q) {
+      const int rc = colred_push(ws + q * seg, nrows, ncols, std::min<int64_t>(seg, ncols - q * seg), outs[q], stream);
+      if (rc != DPH_OK) return rc;
+    }
+    return DPH_OK;
   }
   if (deterministic())
     hipLaunchKernelGGL(slab_reduce_det_kernel, dim3((unsigned)cdiv(ncols, 32)), dim3(32 * DET_PH), 0, stream, ws,
@@ -544,6 +546,7 @@ void slab_reduce_launch(const float* ws, int64_t nrows, int64_t ncols, int64_t s
   else
     hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)cdiv(ncols, 64), (unsigned)slab_groups(nrows)), dim3(256), 0,
                        stream, ws, nrows, ncols, seg, o0, o1, o2);
+  return DPH_OK;
 }
 
 int64_t colsum_rpb(int64_t rows) { return std::max<int64_t>(64, cdiv(cdiv(rows, 8192), 4) * 4); }
@@ -824,9 +827,9 @@ __global__ void __launch_bounds__(512) ln_bwd16_kernel(
 }  // namespace
 
 // (shared with the other translation units: common.h)
-void slab_reduce_cols(const float* ws, int64_t nrows, int64_t ncols, int64_t seg, float* o0, float* o1, float* o2,
-                      hipStream_t stream) {
-  slab_reduce_launch(ws, nrows, ncols, seg, o0, o1, o2, stream);
+int slab_reduce_cols(const float* ws, int64_t nrows, int64_t ncols, int64_t seg, float* o0, float* o1, float* o2,
+                     hipStream_t stream) {
+  return slab_reduce_launch(ws, nrows, ncols, seg, o0, o1, o2, stream);
 }
 void sdot_reduce(const float* part, int64_t n, float* out, hipStream_t stream) {
   hipLaunchKernelGGL(sdot_reduce_kernel, dim3(1), dim3(64), 0, stream, part, n, out);
@@ -1001,7 +1004,7 @@ extern "C" int dph_layernorm_bwd_ld(const void* dy, const void* x, const float* 
   }
 #undef LN_BWD_LAUNCH
   }
-  if (sums) slab_reduce_launch(ws, grid.x, 3 * D, D, dgamma, dbeta, branch_colsum, stream);
+  if (sums) DPH_TRY(slab_reduce_launch(ws, grid.x, 3 * D, D, dgamma, dbeta, branch_colsum, stream));
   if (det_sdot) hipLaunchKernelGGL(sdot_reduce_kernel, dim3(1), dim3(64), 0, stream, sdot_part, (int64_t)grid.x, branch_sdot);
   return check_launch("dph_layernorm_bwd");
 }
@@ -1036,7 +1039,7 @@ extern "C" int dph_layernorm_bwd_x32(const void* dy, const float* x, const float
   }
 #undef LN_BWD32_LAUNCH
   }
-  if (sums) slab_reduce_launch(ws, grid.x, 3 * D, D, dgamma, dbeta, nullptr, stream);
+  if (sums) DPH_TRY(slab_reduce_launch(ws, grid.x, 3 * D, D, dgamma, dbeta, nullptr, stream));
   return check_launch("dph_layernorm_bwd_x32");
 }
 
@@ -1102,7 +1105,7 @@ extern "C" int dph_layernorm_bwd_res32(const void* dy, const float* x, const flo
   }
 #undef LN_BWDR_LAUNCH
   }
-  if (sums) slab_reduce_launch(ws, grid.x, 3 * D, D, dgamma, dbeta, nullptr, stream);
+  if (sums) DPH_TRY(slab_reduce_launch(ws, grid.x, 3 * D, D, dgamma, dbeta, nullptr, stream));
   return check_launch("dph_layernorm_bwd_res32");
 }
 
@@ -1152,7 +1155,7 @@ extern "C" int dph_colsum(const void* x, float* out, int64_t rows, int64_t cols,
   dim3 grid((unsigned)cdiv(cols, 512), (unsigned)nrb);
   hipLaunchKernelGGL(colsum_kernel, grid, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(x), ws, rows, cols,
                      rpb, cols, cols, (int64_t)0);
-  slab_reduce_launch(ws, nrb, cols, cols, out, nullptr, nullptr, stream);
+  DPH_TRY(slab_reduce_launch(ws, nrb, cols, cols, out, nullptr, nullptr, stream));
   return check_launch("dph_colsum");
 }
 
@@ -1172,12 +1175,12 @@ extern "C" int dph_colsum3(const void* x, float* out0, float* out1, float* out2,
     dim3 grid2((unsigned)cdiv(2 * seg, 512), (unsigned)nrb);
     hipLaunchKernelGGL(colsum_kernel, grid2, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(x), ws, rows,
                        2 * seg, rpb, cols, seg, seg);
-    slab_reduce_launch(ws, nrb, 2 * seg, seg, out0, out2, nullptr, stream);
+    DPH_TRY(slab_reduce_launch(ws, nrb, 2 * seg, seg, out0, out2, nullptr, stream));
     return check_launch("dph_colsum3");
   }
   dim3 grid((unsigned)cdiv(cols, 512), (unsigned)nrb);
   hipLaunchKernelGGL(colsum_kernel, grid, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(x), ws, rows, cols,
                      rpb, cols, cols, (int64_t)0);
-  slab_reduce_launch(ws, nrb, cols, seg, out0, out1, out2, stream);
+  DPH_TRY(slab_reduce_launch(ws, nrb, cols, seg, out0, out1, out2, stream));
   return check_launch("dph_colsum3");
 }

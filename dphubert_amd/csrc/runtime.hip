@@ -88,6 +88,7 @@ __global__ void __launch_bounds__(32 * DET_PH) colred_batch_kernel(const ColRedB
 
 bool g_defer = false;
 std::vector<ColRed> g_redq;
+int64_t g_redq_pushed = 0;   // every problem ever queued (dph_reductions_pushed)
 hipStream_t g_redq_stream = nullptr;
 
 int flush_redq() {
@@ -116,14 +117,21 @@ int flush_redq() {
 
 bool colred_deferring() { return g_defer && deterministic(); }
 
-void colred_push(const float* ws, int64_t nrows, int64_t ld, int64_t n, float* out, hipStream_t stream) {
-  if (n <= 0 || out == nullptr) return;
+// (a queue flushed on a clash that fails to launch is dropped: its error code is returned, and the caller passes it
+// on, so the reductions it held are never silently lost)
+int colred_push(const float* ws, int64_t nrows, int64_t ld, int64_t n, float* out, hipStream_t stream) {
+  if (n <= 0 || out == nullptr) return DPH_OK;
   bool clash = !g_redq.empty() && stream != g_redq_stream;
   for (const ColRed& q : g_redq)
     if (out < q.out + q.n && q.out < out + n) clash = true;
-  if (clash) flush_redq();
+  if (clash) {
+    const int rc = flush_redq();
+    if (rc != DPH_OK) return rc;
+  }
   g_redq.push_back(ColRed{ws, out, (int32_t)nrows, (int32_t)ld, (int32_t)n, 0});
   g_redq_stream = stream;
+  ++g_redq_pushed;
+  return DPH_OK;
 }
 }  // namespace dph
 
@@ -132,6 +140,15 @@ extern "C" int dph_defer_reductions(int on) {
   return DPH_OK;
 }
 extern "C" int64_t dph_deferred_reductions(void) { return (int64_t)dph::g_redq.size(); }
+extern "C" int64_t dph_reductions_pushed(void) { return dph::g_redq_pushed; }
+// Drop the queued reductions without launching them (the error path of a deferred block: their slabs may no longer
+// be alive, so launching them would read freed memory and add garbage into the sinks).  Returns how many were dropped.
+extern "C" int64_t dph_discard_reductions(void) {
+  const int64_t n = (int64_t)dph::g_redq.size();
+  dph::g_redq.clear();
+  dph::g_redq_stream = nullptr;
+  return n;
+}
 extern "C" int dph_flush_reductions(hipStream_t stream) {
   if (dph::g_redq.empty()) return DPH_OK;
   DPH_REQUIRE(stream == dph::g_redq_stream, "dph_flush_reductions: the queued reductions were issued on another stream");
@@ -139,7 +156,7 @@ extern "C" int dph_flush_reductions(hipStream_t stream) {
 }
 
 extern "C" const char* dph_last_error(void) { return dph::g_err; }
-extern "C" int dph_abi_version(void) { return 22; }
+extern "C" int dph_abi_version(void) { return 23; }
 extern "C" int dph_set_deterministic(int on) {
   dph::g_det = on ? 1 : 0;
   return DPH_OK;

@@ -240,6 +240,8 @@ class shared_gpu:
 # ops.deferred_reductions: while set, the list that keeps every column-sum workspace alive until the queued
 # reductions that read it are flushed
 KEEP_WS = [None]
+# True inside an armed deferral scope (ops._Armed): only then can a call's slab be queued, so only then is it kept
+ARMED = [False]
 
 
 def gemm(A: DphMat, B: DphMat, Cm: DphMat, M: int, N: int, K: int, *, a_kcontig: bool, b_kcontig: bool,
@@ -265,7 +267,7 @@ def gemm(A: DphMat, B: DphMat, Cm: DphMat, M: int, N: int, K: int, *, a_kcontig:
         n_el = 2 * batch * ((M + 63) // 64) * N
         ws_bytes = n_el * 4
         ws = torch.empty(n_el, dtype=F32, device=device or Cm_device(colsum_out, colsum_aux))
-        if KEEP_WS[0] is not None:
+        if KEEP_WS[0] is not None and ARMED[0]:
             KEEP_WS[0].append(ws)
     args = DphGemmArgs(M, N, K, batch, splits, int(a_kcontig), int(b_kcontig), A, B, Cm, c_dtype, act, alpha,
                        dropout_p, seed & 0xFFFFFFFFFFFFFFFF, ptr(bias), ptr(colmask), ptr(smask), vec_z_inner,
@@ -422,7 +424,11 @@ def linear_wgrad_grouped(items: Sequence, accumulate: bool = True) -> Optional[t
     if prof is not None:
         e0, e1 = prof.event(), prof.event()   # (owned by the profiler: e0 is recorded even if the launch falls back)
         e0.record()
-    rc = _lib.lib().dph_gemm_grouped(C.byref(args), C.byref(grp), _stream())
+    if _lib.TRACE[0]:
+        with torch.profiler.record_function("dph::dph_gemm_grouped"):
+            rc = _lib.lib().dph_gemm_grouped(C.byref(args), C.byref(grp), _stream())
+    else:
+        rc = _lib.lib().dph_gemm_grouped(C.byref(args), C.byref(grp), _stream())
     if rc == EUNSUPPORTED:
         for dy, x, dw in items:
             linear_wgrad(dy, x, dw, accumulate=accumulate)

@@ -51,7 +51,7 @@ def _ws(nbytes: int, dev):
     alive until the block's flush, which is then that consumer)."""
     t = torch.empty(max(int(nbytes), 4) // 4, dtype=F32, device=dev)
     keep = K.KEEP_WS[0]
-    if keep is not None:
+    if keep is not None and K.ARMED[0]:
         keep.append(t)
     return ptr(t), t.numel() * 4
 
@@ -557,6 +557,9 @@ class deferred_reductions:
 
     def __enter__(self):
         if self.enable:
+            left = int(_lib.lib().dph_deferred_reductions())
+            if left:
+                raise RuntimeError(f"deferred_reductions: {left} column reductions left queued by an earlier block")
             self.prev, _RED_DEFER[0] = _RED_DEFER[0], self
             self.prev_keep, K.KEEP_WS[0] = K.KEEP_WS[0], self.keep
             self.open = True
@@ -585,9 +588,15 @@ class deferred_reductions:
             if exc_type is None:
                 self.close()
             else:
+                # the block failed (e.g. a graph capture that raised): the queued problems refer to slabs this block
+                # no longer keeps and to sinks whose step is abandoned -- drop them unlaunched, so that no later flush
+                # adds them into the next step's gradients
                 self.open = False
                 K.KEEP_WS[0] = self.prev_keep
+                K.ARMED[0] = False
                 _lib.lib().dph_defer_reductions(0)
+                _lib.lib().dph_discard_reductions()
+                self.pending, self.keep = [], []
 
 
 class _Armed:
@@ -596,13 +605,21 @@ class _Armed:
 
     def __enter__(self):
         if self.scope is not None:
-            _lib.lib().dph_defer_reductions(1)
+            L = _lib.lib()
+            L.dph_defer_reductions(1)
+            K.ARMED[0] = True
+            self.pushed0, self.keep0 = int(L.dph_reductions_pushed()), len(self.scope.keep)
             self.go.deferred = self.scope
         return self
 
     def __exit__(self, *exc):
         if self.scope is not None:
-            _lib.lib().dph_defer_reductions(0)
+            L = _lib.lib()
+            L.dph_defer_reductions(0)
+            K.ARMED[0] = False
+            if int(L.dph_reductions_pushed()) == self.pushed0:
+                # nothing queued by this call (its reductions ran immediately): its slabs need not outlive it
+                del self.scope.keep[self.keep0:]
 
 
 def _defer_red(go, *outs_direct):

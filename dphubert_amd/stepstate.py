@@ -16,6 +16,7 @@ to it for the life of the process.
 """
 
 import ctypes as C
+import time
 from typing import Dict, Optional, Sequence
 
 import torch
@@ -40,6 +41,10 @@ class StepScalars:
         self.events: list = [None] * RING
         self.k = 0
         self.epoch = 0
+        # host seconds spent blocked on the ring (a slot whose copy of RING steps ago has not run yet): with
+        # graph replay the host runs at most RING steps ahead of the GPU, so a loop's host time minus this is the
+        # host's own enqueue cost (bench.py host_enqueue_ms)
+        self.wait_s = 0.0
         with torch.cuda.device(device):
             call("dph_set_rng_epoch", self.dev.data_ptr() + OFF_EPOCH)
 
@@ -62,8 +67,10 @@ class StepScalars:
             self.epoch += 1
         i = self.k % RING
         self.k += 1
-        if self.events[i] is not None:
+        if self.events[i] is not None and not self.events[i].query():
+            t0 = time.perf_counter()
             self.events[i].synchronize()        # the copy that last read this pinned slot is done
+            self.wait_s += time.perf_counter() - t0
         h = self.host[i]
         base = h.data_ptr()
         C.c_uint64.from_address(base + OFF_EPOCH).value = self.epoch & 0xFFFFFFFFFFFFFFFF

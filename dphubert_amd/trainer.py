@@ -18,6 +18,7 @@ reference schedule exactly while the host does ~50 us of work per step instead o
 
 import copy
 import os
+import time
 import warnings
 from typing import List, Optional
 
@@ -247,6 +248,8 @@ class Trainer:
         self.graphs = bool(graphs)
         self.graph_warmup = max(1, int(graph_warmup))
         self._n_eager = 0                # eager OPTIMIZER steps so far
+        # host seconds in the step-scalar upload and in hipGraphLaunch (bench.py host_enqueue_ms)
+        self.host_s = {"upload": 0.0, "replay": 0.0, "replays": 0}
         self._graphs = {}                # (zero, final) -> (graph, static loss)
         self._pool = None
         self._prof_graph = None
@@ -482,7 +485,9 @@ class Trainer:
         zero = self._micro == 0
         final = self._micro + 1 == self.accum_grad
         adam_step = self.optimizer.begin_step() if final else self.optimizer._step + 1
+        t_up = time.perf_counter()
         self._upload(dev, adam_step)
+        self.host_s["upload"] += time.perf_counter() - t_up
         loss = None
         if self.graphs and self._n_eager >= self.graph_warmup and m.global_step >= self._eager_until:
             self._set_static(batch)
@@ -502,7 +507,10 @@ class Trainer:
                     g, loss = self._prof_graph, self._prof_loss
                 else:
                     g, loss = self._graphs[key]
+                t_rp = time.perf_counter()
                 g.replay()
+                self.host_s["replay"] += time.perf_counter() - t_rp
+                self.host_s["replays"] += 1
                 m.logged = dict(self._logged_of[id(g)])
         if loss is None:
             loss = self._gpu_step(batch, zero, final)

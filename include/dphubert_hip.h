@@ -52,10 +52,15 @@ int dph_get_deterministic(void);
  * in the same fixed order as its own launch (bitwise identical results).  The caller keeps every queued
  * workspace alive and the queued outputs unread until the flush, which must be issued on the stream the
  * reductions were queued on.  Queued problems whose outputs overlap are flushed in queue order (an overlapping
- * enqueue flushes the queue first).  dph_deferred_reductions: the queue length. */
+ * enqueue flushes the queue first).  dph_deferred_reductions: the queue length.
+ * ABI 23: dph_discard_reductions drops the queue without launching it (the error path of a deferred block, whose
+ * slabs may already be freed) and returns how many were dropped; dph_reductions_pushed counts every problem ever
+ * queued (a caller keeps a call's slab alive only when that call queued something). */
 int dph_defer_reductions(int on);
 int dph_flush_reductions(hipStream_t stream);
 int64_t dph_deferred_reductions(void);
+int64_t dph_discard_reductions(void);
+int64_t dph_reductions_pushed(void);
 
 /* ------------------------------------------------------------------------ *
  * Generic bf16 MFMA GEMM with fused epilogues.

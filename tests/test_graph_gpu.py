@@ -390,3 +390,39 @@ def test_deferred_reductions_match_immediate(monkeypatch, accum):
         assert _lib.lib().dph_deferred_reductions() == 0
     assert queued and max(queued) >= 8, queued
     assert torch.equal(res[0], res[1])
+
+
+def test_deferred_block_error_discards_queue(monkeypatch):
+    """A deferred_reductions block left by an exception (e.g. a HIP-graph capture that raised: trainer.py falls back
+    to eager steps) drops its queued reductions unlaunched: their slabs are no longer kept and their sinks belong to
+    an abandoned step.  The next step's gradient buckets must equal an immediate-mode step BITWISE (a stale queue
+    flushed into them would add the abandoned step's partial sums)."""
+    from dphubert_amd import _lib, ops
+    from dphubert_amd import kernels as K
+    from dphubert_amd.trainer import Trainer
+    batch = _batch()
+    seen = []
+
+    def boom(grad):
+        seen.append(int(_lib.lib().dph_deferred_reductions()))
+        raise RuntimeError("injected failure inside the deferred block")
+
+    monkeypatch.setenv("DPH_DEFER_RED", "1")
+    tr = Trainer(_module(), clip_norm=10.0)
+    monkeypatch.setattr(ops, "_flush_wgrads_hook", boom)
+    with pytest.raises(RuntimeError, match="injected failure"):
+        tr.step(batch)
+    monkeypatch.undo()
+    assert seen and seen[0] > 0, seen                       # reductions were queued when the block failed
+    assert _lib.lib().dph_deferred_reductions() == 0        # ... and dropped, not left for a later flush
+    assert not K.ARMED[0] and K.KEEP_WS[0] is None
+    tr._micro = 0
+    tr.step(batch)                                          # same weights: the failed step updated nothing
+    torch.cuda.synchronize()
+    got = torch.cat([f.detach().float().cpu() for f in tr.reducer.flat])
+    monkeypatch.setenv("DPH_DEFER_RED", "0")
+    ref = Trainer(_module(), clip_norm=10.0)
+    ref.step(batch)
+    torch.cuda.synchronize()
+    want = torch.cat([f.detach().float().cpu() for f in ref.reducer.flat])
+    assert torch.equal(got, want)

@@ -89,7 +89,7 @@ def test_library_loads_and_exports_every_symbol():
     import re
     from pathlib import Path
     hdr = (Path(__file__).resolve().parents[1] / "include" / "dphubert_hip.h").read_text()
-    declared = set(re.findall(r"^\s*(?:const char\*|int)\s+(dph_\w+)\s*\(", hdr, re.M))
+    declared = set(re.findall(r"^\s*(?:const char\*|int|int64_t)\s+(dph_\w+)\s*\(", hdr, re.M))
     assert declared, "no declarations parsed"
     for name in declared:
         assert hasattr(L, name), name
@@ -109,3 +109,33 @@ def test_no_cpu_fallback():
     m = wav2vec2_model(**copy.deepcopy(HUBERT_BASE_CONFIG))
     with pytest.raises(ValueError):
         m.extract_features(torch.zeros(2, 16000))     # CPU tensors are rejected, never computed on the host
+
+
+def test_trace_ranges_name_each_abi_call():
+    """DPH_TRACE / _lib.set_trace: every C-ABI call runs inside a torch.profiler.record_function range named after
+    its entry point (SURVEY 5 tracing); off by default.  Host-only entry points, so no GPU is needed."""
+    from torch.profiler import ProfilerActivity, profile
+    from dphubert_amd import _lib
+    prev = _lib.set_trace(True)
+    det = _lib.deterministic()
+    try:
+        with profile(activities=[ProfilerActivity.CPU]) as prof:
+            _lib.call("dph_set_deterministic", 1)
+            _lib.call("dph_defer_reductions", 0)
+    finally:
+        _lib.set_trace(prev)
+        _lib.set_deterministic(det)
+    names = {e.name for e in prof.events()}
+    assert {"dph::dph_set_deterministic", "dph::dph_defer_reductions"} <= names, sorted(names)[:20]
+    with profile(activities=[ProfilerActivity.CPU]) as prof:
+        _lib.call("dph_defer_reductions", 0)
+    assert not any(e.name.startswith("dph::") for e in prof.events())
+
+
+def test_discard_reductions_host_only():
+    """dph_discard_reductions (ABI 23) empties the deferred-reduction queue without launching anything."""
+    from dphubert_amd import _lib
+    L = _lib.lib()
+    assert L.dph_deferred_reductions() == 0
+    assert L.dph_discard_reductions() == 0
+    assert L.dph_reductions_pushed() >= 0
