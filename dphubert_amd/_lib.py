@@ -34,7 +34,8 @@ class DphGemmArgs(C.Structure):
                 ("alpha", f32), ("dropout_p", f32), ("seed", u64), ("bias", vp), ("colmask", vp), ("smask", vp),
                 ("vec_z_inner", i64), ("pre_out", vp), ("aux_in", vp), ("residual", vp), ("colsum_out", vp),
                 ("colsum_aux", vp), ("row_len", vp), ("len_rows", i64), ("drop_row_offset", i64),
-                ("workspace", vp), ("workspace_bytes", i64), ("colsum_n", i64), ("flags", i64), ("dyn_ext", vp)]
+                ("workspace", vp), ("workspace_bytes", i64), ("colsum_n", i64), ("flags", i64), ("dyn_ext", vp),
+                ("sk_ws", vp), ("sk_ws_bytes", i64), ("sk_flags", vp), ("sk_nflags", i64)]
 
 
 GEMM_GROUP_MAX = 16
@@ -73,6 +74,7 @@ _SIGS = {
     "dph_flush_reductions": ([S], C.c_int),
     "dph_deferred_reductions": ([], i64),
     "dph_discard_reductions": ([], i64),
+    "dph_gemm_sk_plan": ([C.POINTER(DphGemmArgs), C.POINTER(i64), C.POINTER(i64)], C.c_int),
     "dph_reductions_pushed": ([], i64),
     "dph_gemm": ([C.POINTER(DphGemmArgs), S], C.c_int),
     "dph_gemm_mn_plan": ([i64, i64, i64, i64], C.c_int),
@@ -175,7 +177,8 @@ _lib = None
 # of the fixed-order reductions: attention prep / relpos backward, WavLM gate, conv0, GELU-mask and branch backward;
 # 21: deferred column reductions -- dph_defer_reductions / dph_flush_reductions / dph_deferred_reductions;
 # 22: dph_attention_bwd_prep's D is the rowdot of dO_m itself, the head mask applied to dq / dk / dv in fp32;
-# 23: dph_discard_reductions / dph_reductions_pushed, queue-flush launch errors propagated by every column reduction)
+# 23: dph_discard_reductions / dph_reductions_pushed, queue-flush launch errors propagated by every column reduction;
+#     DphGemmArgs.sk_* + dph_gemm_sk_plan: the persistent stream-K 256 x 256 GEMM)
 ABI_VERSION = 23
 
 

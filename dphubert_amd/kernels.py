@@ -244,6 +244,23 @@ KEEP_WS = [None]
 ARMED = [False]
 
 
+def _sk_scratch(args, dev):
+    """Stream-K route (dph_gemm_sk_plan): the fp32 partial-tile buffer (stream-ordered caching allocator: reused only
+    by work queued after this GEMM) and the hand-off flags, which must be zero at launch -- a fresh slice of the zero
+    arena (ops.zeros_f32: re-zeroed by the graph's fill node on every replay; the teacher's side stream has its own
+    arena).  Returns the tensors to keep alive until the launch is enqueued (None: not taken)."""
+    nb, nf = C.c_int64(0), C.c_int64(0)
+    if not _lib.lib().dph_gemm_sk_plan(C.byref(args), C.byref(nb), C.byref(nf)):
+        return None
+    from . import ops
+    dev = dev if dev is not None else "cuda"
+    ws = torch.empty(nb.value // 4, dtype=torch.float32, device=dev)
+    fl = ops.zeros_f32(int(nf.value), dev)
+    args.sk_ws, args.sk_ws_bytes = ws.data_ptr(), nb.value
+    args.sk_flags, args.sk_nflags = fl.data_ptr(), nf.value
+    return ws, fl
+
+
 def gemm(A: DphMat, B: DphMat, Cm: DphMat, M: int, N: int, K: int, *, a_kcontig: bool, b_kcontig: bool,
          c_dtype: int = OUT_BF16, act: int = ACT_NONE, alpha: float = 1.0, batch: int = 1, splits: int = 1,
          bias=None, colmask=None, smask=None, vec_z_inner: int = 0, pre_out=None, aux_in=None, residual=None,
@@ -275,11 +292,13 @@ def gemm(A: DphMat, B: DphMat, Cm: DphMat, M: int, N: int, K: int, *, a_kcontig:
                        len_rows, drop_row_offset, ptr(ws), ws_bytes, colsum_n,
                        flags | (GEMM_NO_PERSIST if _SHARED_GPU[0] else 0),
                        (dyn[0].data_ptr() + 4 * dyn[1]) if dyn is not None else None)
+    sk_keep = _sk_scratch(args, device or Cm_device(colsum_out, colsum_aux))
     prof = LaunchProfiler.active
     if prof is not None:
         e0, e1 = prof.event(), prof.event()
         e0.record()
     call("dph_gemm", C.byref(args), _stream())
+    del sk_keep
     if prof is not None:
         e1.record()
         name = _variant(args)

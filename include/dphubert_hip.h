@@ -133,6 +133,13 @@ typedef struct DphGemmArgs {
    * packed active units (dph_ffn_compact) read the active count this way inside a captured step graph.
    * Ping-pong kernels only (pp_gemm_kernel: m / n / k, ppw_gemm_kernel: m / n); NULL = static.            */
   const int32_t* dyn_ext;
+  /* stream-K scratch (ABI 23; sized by dph_gemm_sk_plan): sk_ws = fp32 partial tiles (sk_ws_bytes), sk_flags =
+   * sk_nflags int32 hand-off flags that must be ZERO at launch (the library never resets them: give each call
+   * fresh zeros).  NULL sk_ws: the stream-K kernel is not used for this call.                              */
+  void* sk_ws;
+  int64_t sk_ws_bytes;
+  int32_t* sk_flags;
+  int64_t sk_nflags;
 } DphGemmArgs;
 
 /* flags: one tile per block even where the persistent ring grid applies -- for GEMMs that share the
@@ -148,6 +155,11 @@ typedef struct DphGemmArgs {
 #define DPH_GEMM_RESID_F32 4
 
 int dph_gemm(const DphGemmArgs* args, hipStream_t stream);
+/* Stream-K route (ABI 23): 1 when dph_gemm would run these args (sk_* fields ignored) on the persistent stream-K
+ * 256 x 256 ping-pong kernel -- the M = B*T projections with N >= 2048 (QKV forward, FFN1 forward, FFN2 input
+ * gradient: components.py:406-408, :733-741) -- and then the partial-tile bytes and zeroed flags it needs; 0 otherwise
+ * (DPH_GEMM_SK=0 turns the route off). */
+int dph_gemm_sk_plan(const DphGemmArgs* args, int64_t* ws_bytes, int64_t* nflags);
 /* Grouped (mn, mn) weight gradients: n <= DPH_GEMM_GROUP_MAX independent dW_i (+)= dY_i^T X_i of ONE shape in one
  * launch (grid batch z = problem i, operand i at a[i] / b[i] / c[i]).  ``args`` describes every problem: batch == n,
  * splits = dph_gemm_mn_plan(M, N, K, n) with the workspace sized for n problems, A / B / C ptr ignored, their

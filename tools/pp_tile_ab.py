@@ -52,7 +52,7 @@ CASES = [
 if os.environ.get("DPH_AB_SET") == "conv":
     CASES = CONV
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 5
-kinds = sys.argv[2:] or ["auto", "15", "16", "13", "12", "14"]
+kinds = sys.argv[2:] or ["auto", "sk0", "skall", "15", "16", "12"]
 data = {}
 for name, n, k, m, epi in CASES:
     A, B = bf(m, k), bf(n, k)
@@ -64,18 +64,42 @@ for name, n, k, m, epi in CASES:
     data[name] = (A, B, C, m, n, k, kw)
 
 
+GRAPHS = {}
+
+
 def run(name, kind, iters=20):
-    if kind == "auto":
-        os.environ.pop("DPH_PP_FORCE", None)
-    else:
+    """kind: "auto" (the library's routing), "sk0" / "skall" (DPH_GEMM_SK=0 / =all, tiles by the library's pick), or
+    a ping-pong tile id forced with the stream-K route off.  The iters launches are captured once into a HIP graph
+    and replayed (host launch cost out of the measurement)."""
+    from dphubert_amd import ops
+    os.environ.pop("DPH_PP_FORCE", None)
+    os.environ.pop("DPH_GEMM_SK", None)
+    if kind == "sk0":
+        os.environ["DPH_GEMM_SK"] = "0"
+    elif kind == "skall":
+        os.environ["DPH_GEMM_SK"] = "all"
+    elif kind != "auto":
         os.environ["DPH_PP_FORCE"] = kind
+        os.environ["DPH_GEMM_SK"] = "0"
     A, B, C, m, n, k, kw = data[name]
     f = lambda: K.gemm(K.dense(A), K.dense(B), K.dense(C), m, n, k, a_kcontig=True, b_kcontig=True, **kw)  # noqa
-    f()
+    g = GRAPHS.get((name, kind))
+    if g is None:
+        f()
+        torch.cuda.synchronize()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        g = torch.cuda.CUDAGraph()
+        ops.reset_zero_arena()
+        with torch.cuda.graph(g, stream=s):
+            for _ in range(iters):
+                f()
+        ops.reset_zero_arena()
+        GRAPHS[(name, kind)] = g
+        g.replay()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
-    for _ in range(iters):
-        f()
+    g.replay()
     e1.record()
     torch.cuda.synchronize()
     return e0.elapsed_time(e1) / iters * 1e3
@@ -87,6 +111,7 @@ for _ in range(rounds):
         for kd in kinds:
             res.setdefault((name, kd), []).append(run(name, kd))
 os.environ.pop("DPH_PP_FORCE", None)
+os.environ.pop("DPH_GEMM_SK", None)
 for name, n, k, m, _e in CASES:
     fl = 2.0 * m * n * k
     row = " | ".join(f"{kd} {statistics.median(res[(name, kd)]):6.1f}" for kd in kinds)
