@@ -73,6 +73,15 @@ __global__ void __launch_bounds__(C::NT, C::WPE) sk_gemm_kernel(const DphGemmArg
   // (lofs: this lane's byte offset inside a partial slot -- accumulator s of wave w at ((w * NACC + s) * 64 + lane)
   // * 16, so each store / load instruction moves one contiguous KB)
   unsigned long long st1 = 0;
+  // DPH_STAMP diagnostic build (tools/stamp_sk.py): per logical block 16 int64 slots in a.workspace -- [0] start,
+  // per segment s < 5: [1 + 3s] main loop entry (after a head piece's wait), [2 + 3s] loop done, [3 + 3s] segment done
+  int nseg = 0;
+  unsigned long long stv = 0;
+  auto stamp = [&](int slot) {
+    DPH_TSTAMP(stv);
+    if (DPH_STAMP && tid == 0 && slot < 16) reinterpret_cast<unsigned long long*>(a.workspace)[b * 16 + slot] = stv;
+  };
+  stamp(0);
 #pragma unroll 1
   while (it < end) {
     // (lane made opaque per segment: keeps the compiler from hoisting lane-derived DMA offsets and epilogue
@@ -119,12 +128,14 @@ __global__ void __launch_bounds__(C::NT, C::WPE) sk_gemm_kernel(const DphGemmArg
 #pragma unroll
         for (int j = 0; j < C::FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
     }
+    stamp(1 + 3 * nseg);
     const bf16_t* Ab = reinterpret_cast<const bf16_t*>(a.A.ptr) + (int64_t)k0 * pp::BK;
     const bf16_t* Bb = reinterpret_cast<const bf16_t*>(a.B.ptr) + (int64_t)k0 * pp::BK;
     pp::mainloop<C>(a, Ab, Bb, m0, n0, k1 - k0, acc, smem, wave, lane, st1);
     // (compiler-only memory barrier: the epilogue's bias / mask / input loads must not be hoisted above the main loop,
     // where their registers would be live beside the fragments and accumulators)
     asm volatile("" ::: "memory");
+    stamp(2 + 3 * nseg);
     if (k0 > 0) {
       // tail piece -> slot b (write-through), drained by every wave, then the flag
       const auto rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<float*>(a.sk_ws) + (int64_t)b * TILE_F,
@@ -141,6 +152,8 @@ __global__ void __launch_bounds__(C::NT, C::WPE) sk_gemm_kernel(const DphGemmArg
     } else {
       ring::direct_epi_t<C, ACT, DROP, true>(a, 0, m0 + wr * C::WTM, n0 + wc * C::WTN, lane, acc);
     }
+    stamp(3 + 3 * nseg);
+    ++nseg;
     it += k1 - k0;
   }
 }
@@ -150,10 +163,16 @@ __global__ void __launch_bounds__(C::NT, C::WPE) sk_gemm_kernel(const DphGemmArg
 // ---- host side (declared in gemm_core.h; called by dph_gemm / dph_gemm_sk_plan in gemm.hip) ----
 // The stream-K route: k-contiguous operands on the ping-pong layout (pp_ok), one batch, no split-K / device-side
 // extents, K a multiple of 128 (an even K-tile count), a wide N (>= 2048: the shapes above), at least one 256 x 256
-// tile per block pair; DPH_GEMM_SK=0 turns it off (A/B; read per call).
+// tile per block pair.  OFF by default -- DPH_GEMM_SK=1 (plain epilogues) / all (every epilogue) turn it on, read
+// per call: on the step's shapes it measured slower than the tile kernels (QKV forward 53.0 vs 39.8 us, teacher FFN1
+// 76.5 vs 57.1 us, profiles/r6_sk_ab.txt).  The stamps (tools/stamp_sk.py, profiles/r6_sk_stamps.txt) show why: at
+// one 8-wave block per CU nothing overlaps a 256 x 256 epilogue (11 k ticks plain, 20 k with GELU, every block
+// bursting its stores at the same two phase points) nor a segment's prologue fill (12 K-tiles take 36.6 k ticks
+// against 28-30 k in a long loop), and a head piece waits / loads 256 KB of fp32 partial (entry gap up to 16 k).
+// The two-blocks-per-CU 128 x 128 / 128 x 192 tiles hide their epilogue VALU and stores under the other block's MFMAs.
 bool sk_plan(const DphGemmArgs& a, int cus, SkPlan* out) {
   const char* e = getenv("DPH_GEMM_SK");
-  if (e && e[0] == '0') return false;
+  if (!e || e[0] == '0') return false;
   if (a.batch != 1 || a.splits != 1 || a.dyn_ext || a.K % 128 != 0 || a.K < 256 || a.N < 2048) return false;
   if (!(a.act == DPH_ACT_NONE || a.act == DPH_ACT_GELU || a.act == DPH_ACT_GELU_BWD_DGK)) return false;
   // the epilogues whose working set beside 128 accumulator registers spills (dropout, the stored GELU' factor, the
@@ -169,12 +188,14 @@ bool sk_plan(const DphGemmArgs& a, int cus, SkPlan* out) {
   const int64_t tiles = (int64_t)p.ntm * p.ntn;
   if (tiles >= ((int64_t)1 << 24)) return false;
   p.half = tiles * p.nk / 2;
-  int64_t nb = std::min<int64_t>(cus, p.half);
+  // every block's range spans at least nk + 2 K-tiles (ranges are 2 * (floor((b+1) h / n) - floor(b h / n)) >=
+  // 2 * floor(h / n)), so a tile is cut at most once: one tail piece per head piece (the kernel's hand-off is
+  // one-to-one).  The QKV shape (288 tiles x 12 K-tiles) therefore runs on 240 blocks rather than 256.
+  int64_t nb = std::min<int64_t>({(int64_t)cus, p.half, p.half / (p.nk / 2 + 1)});
   if (nb >= 8) nb &= ~(int64_t)7;
+  if (nb < 1) return false;
   p.nblk = (int32_t)nb;
-  // every block's range spans at least nk + 2 K-tiles (its pieces are even-aligned), so a tile is cut at most once:
-  // one tail piece per head piece (the kernel's hand-off is one-to-one)
-  if (2 * p.half / p.nblk < p.nk + 2) return false;
+  if (p.half / p.nblk < p.nk / 2 + 1) return false;
   *out = p;
   return true;
 }

@@ -7,6 +7,7 @@ inside the library.
 """
 
 import ctypes as C
+import os
 from typing import Optional, Sequence
 
 import torch
@@ -249,6 +250,8 @@ def _sk_scratch(args, dev):
     by work queued after this GEMM) and the hand-off flags, which must be zero at launch -- a fresh slice of the zero
     arena (ops.zeros_f32: re-zeroed by the graph's fill node on every replay; the teacher's side stream has its own
     arena).  Returns the tensors to keep alive until the launch is enqueued (None: not taken)."""
+    if os.environ.get("DPH_GEMM_SK", "0")[:1] in ("", "0"):   # (opt-in route: no planning call per GEMM otherwise)
+        return None
     nb, nf = C.c_int64(0), C.c_int64(0)
     if not _lib.lib().dph_gemm_sk_plan(C.byref(args), C.byref(nb), C.byref(nf)):
         return None

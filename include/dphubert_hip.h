@@ -158,7 +158,7 @@ int dph_gemm(const DphGemmArgs* args, hipStream_t stream);
 /* Stream-K route (ABI 23): 1 when dph_gemm would run these args (sk_* fields ignored) on the persistent stream-K
  * 256 x 256 ping-pong kernel -- the M = B*T projections with N >= 2048 (QKV forward, FFN1 forward, FFN2 input
  * gradient: components.py:406-408, :733-741) -- and then the partial-tile bytes and zeroed flags it needs; 0 otherwise
- * (DPH_GEMM_SK=0 turns the route off). */
+ * (off unless DPH_GEMM_SK=1 / all: measured slower than the tile kernels on the step's shapes, gemm_sk.hip). */
 int dph_gemm_sk_plan(const DphGemmArgs* args, int64_t* ws_bytes, int64_t* nflags);
 /* Grouped (mn, mn) weight gradients: n <= DPH_GEMM_GROUP_MAX independent dW_i (+)= dY_i^T X_i of ONE shape in one
  * launch (grid batch z = problem i, operand i at a[i] / b[i] / c[i]).  ``args`` describes every problem: batch == n,
