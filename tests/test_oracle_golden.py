@@ -126,6 +126,21 @@ def test_base12_g3():
     _check_step(fx, out, tol_loss=2e-5, tol_ck=5e-4)
 
 
+def test_large_whole_g15():
+    """g15 (4 pre-norm Large layers, T = 781): the oracle's WHOLE gradients of the stored tensors against the
+    reference's (stored in bf16: rel-L2 <= 1e-2 covers their rounding), loss terms and checksums as every step."""
+    fx = load_golden("g15_large4_whole.pt")
+    out = _run_fixture(fx)
+    _check_step(fx, out, tol_loss=2e-5, tol_ck=5e-4)
+    assert len(fx["whole_grads"]) >= 20
+    for n, w in fx["whole_grads"].items():
+        if n.endswith("k_proj.bias"):
+            continue
+        g = out["grads"][n]
+        assert rel_l2(g, w.float()) < 1e-2, (n, rel_l2(g, w.float()))
+        assert abs(g.double().norm().item() - fx["whole_norms"][n]) <= 1e-4 * fx["whole_norms"][n], n
+
+
 def test_oracle_pruned_forward_matches_reference():
     """The oracle restatement on the reference's pruned architecture (ragged widths) -- g4."""
     import copy as _copy

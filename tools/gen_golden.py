@@ -578,6 +578,29 @@ def gen_large24():
                     global_step=5000)
 
 
+def _g15_whole(n):
+    """g15's whole-gradient set: layer 0's attention projections, every parameter of the last (4th) layer, the
+    transformer's closing LayerNorm (pre-norm), conv0 / conv5 / conv6 + GroupNorm and the feature projection."""
+    if "log_alpha" in n or "hard_concrete" in n:
+        return False
+    if n.startswith(("encoder.transformer.layers.3.", "encoder.transformer.layer_norm.")):
+        return True
+    if n.startswith("encoder.transformer.layers.0.attention."):
+        return True
+    return n.startswith(("feature_extractor.conv_layers.0.", "feature_extractor.conv_layers.5.",
+                         "feature_extractor.conv_layers.6.", "encoder.feature_projection."))
+
+
+def gen_large_whole():
+    """G15: pre-norm Large width (D 1024, 16 heads, FFN 4096, normalize_waveform, group_norm extractor), 4 layers, one
+    utterance at lightning.py:313's max_len 250000 samples (T = 781), distill layers 0.2,4, conv,head,interm with the
+    regulariser active; whole gradients of the _g15_whole parameters (bf16 values + fp32 norms + bf16-emulation
+    sensitivity per tensor), checked like g14 (components.py:848-850 pre-norm, model.py:96-103)."""
+    cfg = large_cfg(4)
+    return run_step(cfg, cfg, "0.2,4", B=1, S=250000, units="conv,head,interm", lambdas=(0.2, 0.1),
+                    global_step=5000, whole=_g15_whole)
+
+
 def gen_predlayer():
     """G12: predlayer distill mode (distill.py:100-107, lightning.py:259-260) on the 2-layer Base shape, three
     heads (distill layers 0,1,2) on the last hidden state, padded batch, regulariser active."""
@@ -589,7 +612,8 @@ def gen_predlayer():
 def main():
     only = [a[len("--only="):] for a in sys.argv[1:] if a.startswith("--only=")]
     extra = {"g10_large.pt": gen_large, "g11_large_lnext.pt": gen_large_ln, "g12_predlayer.pt": gen_predlayer,
-             "g3_base12.pt": gen_base12, "g13_large24.pt": gen_large24, "g14_base12_whole.pt": gen_base12_whole}
+             "g3_base12.pt": gen_base12, "g13_large24.pt": gen_large24, "g14_base12_whole.pt": gen_base12_whole,
+             "g15_large4_whole.pt": gen_large_whole}
     if only:
         OUT.mkdir(parents=True, exist_ok=True)
         torch.set_num_threads(8)
