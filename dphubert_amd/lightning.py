@@ -179,6 +179,23 @@ class DistillModule(nn.Module):
             return self.target_sparsity
         return self.target_sparsity * (self.global_step / self.sparsity_warmup_updates)
 
+    # ---- the step in three phases (trainer.Trainer captures them as separate HIP graphs) -------------------------
+    def teacher_layers(self, waveforms, lengths):
+        """The frozen teacher's distilled hidden states (no autograd) on the current stream."""
+        with torch.no_grad():
+            teacher_hiddens, _ = self.teacher_model.extract_features(waveforms, lengths)
+            return [teacher_hiddens[idx] for idx in self.distill_layers]
+
+    def student_layers(self, waveforms, lengths):
+        """The student's hidden states the distill loss reads, per distilled layer."""
+        student_hiddens, _ = self.student_model.extract_features(waveforms, lengths)
+        if self.distill_mode == "layer2layer":
+            return [student_hiddens[idx] for idx in self.distill_layers]
+        if self.distill_mode == "predlayer":
+            # lightning.py:259-260: every head projects the LAST student hidden state
+            return [student_hiddens[-1]] * len(self.distill_layers)
+        raise ValueError(f"Invalid distill mode: {self.distill_mode}")
+
     def _step(self, batch, batch_idx, mode):
         waveforms, lengths = batch
         self.teacher_model.eval()
@@ -193,7 +210,7 @@ class DistillModule(nn.Module):
             if after:
                 main = torch.cuda.current_stream()
                 side.wait_stream(main)
-                student_hiddens, student_lengths = self.student_model.extract_features(waveforms, lengths)
+                s_layers = self.student_layers(waveforms, lengths)
             if side is not None:
                 # the frozen teacher runs on its own HIP stream, concurrently with the student forward: its
                 # kernels fill the CUs the student's GEMM tile rounds and latency-bound launches leave idle
@@ -201,26 +218,20 @@ class DistillModule(nn.Module):
                 main = torch.cuda.current_stream()
                 if not after:
                     side.wait_stream(main)
-                with torch.cuda.stream(side), torch.no_grad(), ops.private_zero_arena(self._teacher_arena):
-                    teacher_hiddens, teacher_lengths = self.teacher_model.extract_features(waveforms, lengths)
-                    t_layers = [teacher_hiddens[idx] for idx in self.distill_layers]
+                with torch.cuda.stream(side), ops.private_zero_arena(self._teacher_arena):
+                    t_layers = self.teacher_layers(waveforms, lengths)
             else:
-                with torch.no_grad():
-                    teacher_hiddens, teacher_lengths = self.teacher_model.extract_features(waveforms, lengths)
-                    t_layers = [teacher_hiddens[idx] for idx in self.distill_layers]
+                t_layers = self.teacher_layers(waveforms, lengths)
             if not after:
-                student_hiddens, student_lengths = self.student_model.extract_features(waveforms, lengths)
+                s_layers = self.student_layers(waveforms, lengths)
         if side is not None:
             main.wait_stream(side)
             for t in t_layers:
                 t.record_stream(main)
-        if self.distill_mode == "layer2layer":
-            s_layers = [student_hiddens[idx] for idx in self.distill_layers]
-        elif self.distill_mode == "predlayer":
-            # lightning.py:259-260: every head projects the LAST student hidden state
-            s_layers = [student_hiddens[-1]] * len(self.distill_layers)
-        else:
-            raise ValueError(f"Invalid distill mode: {self.distill_mode}")
+        return self.loss_from_layers(s_layers, t_layers, mode)
+
+    def loss_from_layers(self, s_layers, t_layers, mode):
+        """Projections + DistillLoss + the sparsity Lagrangian on the phases' hidden states; logs the terms."""
         B, T, Ds = s_layers[0].shape
         cfg = dict(self.distill_loss.cfg(), L=len(s_layers), P=len(self._proj_uniq), B=B, T=T,
                    proj_index=self._proj_index)

@@ -250,8 +250,15 @@ class Trainer:
         self._n_eager = 0                # eager OPTIMIZER steps so far
         # host seconds in the step-scalar upload and in hipGraphLaunch (bench.py host_enqueue_ms)
         self.host_s = {"upload": 0.0, "replay": 0.0, "replays": 0}
-        self._graphs = {}                # (zero, final) -> (graph, static loss)
+        self._graphs = {}                # (zero, final) -> (graph, static loss) or, split, ((graph A, graph B), loss)
         self._pool = None
+        # split capture (DPH_GRAPH_SPLIT, default on with the teacher stream): the teacher forward is its own graph
+        # replayed on the side stream, the student step two graphs on the main stream (A: forward, B: loss +
+        # backward + all-reduce + AdamW) joined by a host-issued stream wait between them.  One graph with the
+        # fork / join inside made hipGraphLaunch cost 5.9-11.3 ms of host time per step (its parallel branches are
+        # launched node by node) against 0.3 ms for a single-stream graph (profiles/r6_s1_host_enqueue_ab.txt)
+        self._split = os.environ.get("DPH_GRAPH_SPLIT", "1") != "0"
+        self._tgraph = None              # (teacher graph, its static distilled hiddens, its private pool)
         self._prof_graph = None
         self._static = None
         self._prof_loss = None
@@ -318,6 +325,10 @@ class Trainer:
         m = self.module
         self.reducer.prepare(zero=zero, sync=final)
         loss = m.training_step(batch, 0)
+        self._backward_and_update(loss, final)
+        return loss
+
+    def _backward_and_update(self, loss, final: bool):
         # backward seeded with a persistent 1/accum_grad scalar: no ones_like fill / division launch per step
         seed = getattr(self, "_grad_seed", None)
         if seed is None or seed.device != loss.device:
@@ -329,7 +340,6 @@ class Trainer:
         if final:
             self.reducer.finish()
             self.optimizer.launch()
-        return loss
 
     def _capture(self, zero: bool, final: bool, prof=None):
         """Record one (micro-)step into a HIP graph (nothing executes during capture)."""
@@ -360,6 +370,50 @@ class Trainer:
         # the logged terms of this graph are the tensors its capture wrote: a replay of THIS graph refreshes them
         self._logged_of[id(g)] = dict(self.module.logged)
         return g, loss
+
+    def _capture_split(self, zero: bool, final: bool):
+        """Split capture (see __init__): the teacher graph once (its own memory pool: it replays concurrently with
+        graph A), then graphs A and B of this (zero, final) kind in the shared pool, A before B (replay order)."""
+        m = self.module
+        side = m.teacher_stream
+        from . import kernels as K
+        ops.reset_zero_arena()
+        try:
+            if self._tgraph is None:
+                m.teacher_model.eval()
+                gt = torch.cuda.CUDAGraph()
+                side.wait_stream(torch.cuda.current_stream())
+                with K.shared_gpu(), ops.private_zero_arena(m._teacher_arena), \
+                        torch.cuda.graph(gt, stream=side, capture_error_mode="thread_local"):
+                    t_layers = m.teacher_layers(*self._static)
+                torch.cuda.current_stream().wait_stream(side)
+                self._tgraph = (gt, t_layers, gt.pool())
+            t_layers = self._tgraph[1]
+            ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            with torch.cuda.graph(ga, pool=self._pool, capture_error_mode="thread_local"):
+                self.reducer.prepare(zero=zero, sync=final)
+                with K.shared_gpu():
+                    s_layers = m.student_layers(*self._static)
+            if self._pool is None:
+                self._pool = ga.pool()
+            with torch.cuda.graph(gb, pool=self._pool, capture_error_mode="thread_local"):
+                loss = m.loss_from_layers(s_layers, t_layers, "train")
+                self._backward_and_update(loss, final)
+        finally:
+            ops.reset_zero_arena()
+        self._logged_of[id(gb)] = dict(m.logged)
+        return (ga, gb), loss
+
+    def _replay_split(self, graphs):
+        ga, gb = graphs
+        main, side = torch.cuda.current_stream(), self.module.teacher_stream
+        side.wait_stream(main)          # this step's static input is written; the last step's loss has read t_layers
+        with torch.cuda.stream(side):
+            self._tgraph[0].replay()
+        ga.replay()
+        main.wait_stream(side)
+        gb.replay()
+        return gb
 
     def _set_static(self, batch):
         wave, lengths = batch
@@ -431,6 +485,7 @@ class Trainer:
         capture into the stale pool handle trips the caching allocator (use_count assert); the next capture
         starts a new one."""
         self._graphs = {}
+        self._tgraph = None
         self._prof_graph = None
         self._prof_loss = None
         self._logged_of = {}
@@ -492,9 +547,10 @@ class Trainer:
         if self.graphs and self._n_eager >= self.graph_warmup and m.global_step >= self._eager_until:
             self._set_static(batch)
             key = (zero, final)
+            split = self._split and m.teacher_stream is not None
             if key not in self._graphs:
                 try:
-                    self._graphs[key] = self._capture(zero, final)
+                    self._graphs[key] = self._capture_split(zero, final) if split else self._capture(zero, final)
                 except Exception as e:  # noqa: BLE001 -- uncapturable op: stay eager
                     warnings.warn(f"HIP graph capture failed, running eagerly: {e!r}")
                     self.graphs = False
@@ -508,7 +564,10 @@ class Trainer:
                 else:
                     g, loss = self._graphs[key]
                 t_rp = time.perf_counter()
-                g.replay()
+                if isinstance(g, tuple):
+                    g = self._replay_split(g)
+                else:
+                    g.replay()
                 self.host_s["replay"] += time.perf_counter() - t_rp
                 self.host_s["replays"] += 1
                 m.logged = dict(self._logged_of[id(g)])
