@@ -2161,6 +2161,18 @@ static bool pp_b0pf() {
   return !(e && e[0] == '0');
 }
 
+// Multi-round 128 x 192 grids with the plain epilogue (no activation, no dropout: the QKV forward, 756 tiles) on the
+// two-blocks-per-CU build (Cfg::M2, <= 128 VGPRs, 20 B of epilogue spill): one block's prologue / epilogue runs
+// beside the other's main loop -- QKV forward 41.9 -> 36.1 us (profiles/r6_m2_ab.txt).  The GELU / dropout epilogues
+// spill 36-172 B per lane at that cap and measured slower (FFN1 / FFN2-DGK: +3-24 %): they keep one block per CU.
+// DPH_PP_M2=0 keeps every 128 x 192 grid on the one-block build, =1 forces M2 for all of them (A/B, read per call).
+static bool pp_m2(const DphGemmArgs& a) {
+  const char* e = getenv("DPH_PP_M2");
+  if (e && e[0] == '0') return false;
+  if (e && e[0] == '1') return true;
+  return a.act == DPH_ACT_NONE && a.dropout_p <= 0.f && !(a.flags & DPH_GEMM_PRE_DGK);
+}
+
 static int pp_pick(const DphGemmArgs& a) {
   struct Opt { int kind, bm, bn, per_cu; double tf; };
   static const Opt opts[] = {{12, 256, 256, 1, 1514.0}, {15, 128, 192, 1, 1282.0}, {13, 128, 256, 1, 1221.0},
@@ -2680,6 +2692,7 @@ extern "C" int dph_gemm(const DphGemmArgs* args, hipStream_t stream) {
     else if (kind == 14) launch_pp<pp::P256x128>(b, stream);
     else if (kind == 15) {
       if (pp_b0pf() && cdiv(a.M, 128) * cdiv(a.N, 192) * a.batch <= num_cus()) launch_pp<pp::P128x192::PF>(b, stream);
+      else if (pp_m2(a)) launch_pp<pp::P128x192::M2>(b, stream);
       else launch_pp<pp::P128x192>(b, stream);
     } else {
       launch_pp<pp::P128>(b, stream);

@@ -398,6 +398,7 @@ struct Cfg {
   // the next K-tile's B-n0 fragments read in the last interval (pp_gemm_kernel): the PF variant below
   static constexpr bool B0PF = false;
   struct PF;
+  struct M2;
   static_assert(FM % 2 == 0 && FN >= 2 && RA % 64 == 0 && G < 16, "pp tile geometry");
 };
 // Cfg::PF: the B-n0 prefetch schedule of pp_gemm_kernel (tiles without the A-lo split).  Taken for ONE-ROUND
@@ -408,6 +409,14 @@ template <int BM_, int BN_>
 struct Cfg<BM_, BN_>::PF : Cfg<BM_, BN_> {
   static_assert(!Cfg<BM_, BN_>::SPLITA, "B-n0 prefetch: tiles without the A-lo split");
   static constexpr bool B0PF = true;
+};
+// Cfg::M2: two blocks per CU (4 waves per SIMD: <= 128 VGPRs) for a tile that otherwise gets one -- the 128 x 192
+// tile on multi-round grids, so one block's prologue / epilogue overlaps the other's main loop (A/B: DPH_PP_M2)
+template <int BM_, int BN_>
+struct Cfg<BM_, BN_>::M2 : Cfg<BM_, BN_> {
+  static_assert(Cfg<BM_, BN_>::LDS <= 80 * 1024, "two blocks per CU: LDS");
+  static constexpr int MINB = 2;
+  static constexpr int WPE = 4;
 };
 using P256 = Cfg<256, 256>;
 using P128x256 = Cfg<128, 256>;

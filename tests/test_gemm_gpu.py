@@ -405,3 +405,26 @@ def test_pp_b0_prefetch_bitwise(gemm_path, monkeypatch, M, N, K):
         outs.append(C)
     assert torch.equal(outs[0].view(torch.int16), outs[1].view(torch.int16))
     close(outs[0], A.float() @ B.float().t() + R.float())
+
+
+@pytest.mark.parametrize("M,N,K,act", [(7984, 2304, 768, "none"), (2000, 2304, 768, "none"), (7984, 3072, 768, "gelu")])
+def test_pp_two_blocks_per_cu_bitwise(gemm_path, monkeypatch, M, N, K, act):
+    """Multi-round 128 x 192 grids on the two-blocks-per-CU build (pp::Cfg::M2: the QKV forward's default) run the same
+    main loop and epilogue as the one-block build: bitwise equal outputs, forced onto either build (DPH_PP_M2)."""
+    if gemm_path != "pp128x192":
+        pytest.skip("one tile path is enough")
+    K_ = _k()
+    A, B = rnd(M, K), rnd(N, K, scale=0.05)
+    bias = torch.randn(N, device="cuda")
+    kw = dict(act=K_.ACT_GELU, bias=bias) if act == "gelu" else dict(bias=bias)
+    outs = []
+    monkeypatch.setenv("DPH_PP_FORCE", "15")
+    for m2 in ("1", "0"):
+        monkeypatch.setenv("DPH_PP_M2", m2)
+        C = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        K_.gemm(K_.dense(A), K_.dense(B), K_.dense(C), M, N, K, a_kcontig=True, b_kcontig=True, **kw)
+        torch.cuda.synchronize()
+        outs.append(C)
+    assert torch.equal(outs[0].view(torch.int16), outs[1].view(torch.int16))
+    ref = A.float() @ B.float().t() + bias
+    close(outs[0], torch.nn.functional.gelu(ref) if act == "gelu" else ref)

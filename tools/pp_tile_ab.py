@@ -74,7 +74,11 @@ def run(name, kind, iters=20):
     from dphubert_amd import ops
     os.environ.pop("DPH_PP_FORCE", None)
     os.environ.pop("DPH_GEMM_SK", None)
-    if kind == "sk0":
+    os.environ.pop("DPH_PP_M2", None)
+    if kind == "m2":          # the 128 x 192 tile on its two-blocks-per-CU build (Cfg::M2)
+        os.environ["DPH_PP_M2"] = "1"
+        os.environ["DPH_PP_FORCE"] = "15"
+    elif kind == "sk0":
         os.environ["DPH_GEMM_SK"] = "0"
     elif kind == "skall":
         os.environ["DPH_GEMM_SK"] = "all"
@@ -112,6 +116,7 @@ for _ in range(rounds):
             res.setdefault((name, kd), []).append(run(name, kd))
 os.environ.pop("DPH_PP_FORCE", None)
 os.environ.pop("DPH_GEMM_SK", None)
+os.environ.pop("DPH_PP_M2", None)
 for name, n, k, m, _e in CASES:
     fl = 2.0 * m * n * k
     row = " | ".join(f"{kd} {statistics.median(res[(name, kd)]):6.1f}" for kd in kinds)
