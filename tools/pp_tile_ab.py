@@ -49,13 +49,24 @@ CASES = [
     case("ffn1 dgrad", 768, 3072),
     case("qkv dgrad", 768, 2304),
 ]
+# conv extractor forward (implicit GEMM over overlapping row windows, GELU + stored pre-activation: ops.FrontendFn)
+CONVF = []
+for li, (lin, lout, kk, st) in enumerate([(31999, 15999, 3, 2), (15999, 7999, 3, 2), (7999, 3999, 3, 2)], start=1):
+    xin = bf(16 * lin, 512)
+    CONVF.append((f"conv{li} fwd k={kk} (gelu, pre)", 512, kk * 512, 16 * lout,
+                  dict(act=K.ACT_GELU, pre=True, win=(xin, st * 512, lout, lin * 512))))
 if os.environ.get("DPH_AB_SET") == "conv":
     CASES = CONV
+elif os.environ.get("DPH_AB_SET") == "convf":
+    CASES = CONVF
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 5
 kinds = sys.argv[2:] or ["auto", "sk0", "skall", "15", "16", "12"]
 data = {}
 for name, n, k, m, epi in CASES:
-    A, B = bf(m, k), bf(n, k)
+    win = epi.pop("win", None)
+    if epi.pop("pre", False):
+        epi["pre_out"] = torch.empty(m, n, device=dev, dtype=torch.bfloat16)
+    A, B = (win if win is not None else bf(m, k)), bf(n, k)
     odt = torch.float32 if epi.get("c_dtype") == K.OUT_F32 else torch.bfloat16
     C = torch.empty(m, n, device=dev, dtype=odt)
     kw = dict(epi)
@@ -86,7 +97,9 @@ def run(name, kind, iters=20):
         os.environ["DPH_PP_FORCE"] = kind
         os.environ["DPH_GEMM_SK"] = "0"
     A, B, C, m, n, k, kw = data[name]
-    f = lambda: K.gemm(K.dense(A), K.dense(B), K.dense(C), m, n, k, a_kcontig=True, b_kcontig=True, **kw)  # noqa
+    Am = (K.mat(A[0], row_stride=A[1], rows_per_batch=A[2], batch_stride=A[3]) if isinstance(A, tuple)
+          else K.dense(A))
+    f = lambda: K.gemm(Am, K.dense(B), K.dense(C), m, n, k, a_kcontig=True, b_kcontig=True, **kw)  # noqa
     g = GRAPHS.get((name, kind))
     if g is None:
         f()
