@@ -428,3 +428,4 @@ def test_pp_two_blocks_per_cu_bitwise(gemm_path, monkeypatch, M, N, K, act):
     assert torch.equal(outs[0].view(torch.int16), outs[1].view(torch.int16))
     ref = A.float() @ B.float().t() + bias
     close(outs[0], torch.nn.functional.gelu(ref) if act == "gelu" else ref)
+

@@ -46,6 +46,10 @@ CASES = [
     case("qkv fwd", 2304, 768, bias=True),
     case("ffn2 fwd (fp32 residual)", 768, 3072, residual=res32, c_dtype=K.OUT_F32, bias=True),
     case("oproj fwd (fp32 residual)", 768, 768, residual=res32, c_dtype=K.OUT_F32, bias=True),
+    case("oproj fwd (bf16 residual, post-norm)", 768, 768, residual=torch.empty(M, 768, device=dev,
+                                                                                dtype=torch.bfloat16), bias=True),
+    case("ffn2 fwd (bf16 residual, post-norm)", 768, 3072, residual=torch.empty(M, 768, device=dev,
+                                                                                dtype=torch.bfloat16), bias=True),
     case("ffn1 dgrad", 768, 3072),
     case("qkv dgrad", 768, 2304),
 ]
