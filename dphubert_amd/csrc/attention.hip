@@ -1774,7 +1774,8 @@ extern "C" int dph_attention_bwd_relpos(const void* qkv, const void* do_masked, 
                                         const void* keep_bits, float* ws, int64_t ws_bytes, hipStream_t stream) {
   DPH_REQUIRE(qkv && do_masked && lse && Dvec && dqkv && rel_tab && gate && dgate && drel_tab && B > 0 && T > 0 &&
                   T <= 3584 && H > 0,
-              "dph_attention_bwd_relpos: bad args (T <= 3584: two [T+127] fp32 LDS windows + 34 KB of tiles)");
+              "dph_attention_bwd_relpos: bad args (T <= 3584: the [T+127] fp32 table window, in deterministic mode plus four "
+              "per-wave [T+127] diagonal histograms -- <= 74 KB of dynamic LDS beside 34 KB of tiles)");
   const bool det = deterministic();
   DPH_REQUIRE(!det || (ws && ws_bytes >= dph_attention_bwd_relpos_workspace(B, T, H)),
               "dph_attention_bwd_relpos: deterministic mode needs dph_attention_bwd_relpos_workspace bytes");

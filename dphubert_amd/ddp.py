@@ -171,7 +171,10 @@ class GradReducer:
     def _ready(self, p):
         # (_dph_hold: the parameter's gradient GEMM is queued in an ops.grouped_wgrads block, which notifies again
         # once it has landed)
-        if not self.sync or id(p) in self._seen or getattr(p, "_dph_hold", False):
+        # (_dph_defer_hold: its bias / LayerNorm-affine column reduction is queued in an ops.deferred_reductions block,
+        # which notifies once the flush has written it)
+        if not self.sync or id(p) in self._seen or getattr(p, "_dph_hold", False) or \
+                getattr(p, "_dph_defer_hold", False):
             return
         self._seen.add(id(p))
         bi = self.bucket_of[id(p)]

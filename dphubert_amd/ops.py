@@ -579,6 +579,8 @@ class deferred_reductions:
         call("dph_flush_reductions", _s())
         pend, self.pending = self.pending, []
         for p in pend:
+            p._dph_defer_hold = False
+        for p in pend:
             p._dph_sink_ready(p)
         self.keep = []
 
@@ -596,6 +598,8 @@ class deferred_reductions:
                 K.ARMED[0] = False
                 _lib.lib().dph_defer_reductions(0)
                 _lib.lib().dph_discard_reductions()
+                for p in self.pending:
+                    p._dph_defer_hold = False
                 self.pending, self.keep = [], []
 
 
@@ -737,7 +741,13 @@ class GradOut:
                 torch.cuda.current_stream().wait_stream(side)   # the bucket's collective reads these gradients
         d = self.deferred
         if d is not None and d.open:
-            d.pending.extend(self.sunk_params)     # complete only once the queued reductions are flushed
+            # complete only once the queued reductions are flushed: held from the reducer until then (the autograd
+            # post-accumulate hook of these parameters fires right after this backward returns and would otherwise
+            # count them ready -- a bucket holding only such parameters was all-reduced before the flush wrote
+            # them, tests/test_ddp_trainer_gpu.py with 8 MB buckets)
+            for p in self.sunk_params:
+                p._dph_defer_hold = True
+            d.pending.extend(self.sunk_params)
             return
         for p in self.sunk_params:
             p._dph_sink_ready(p)
@@ -1476,6 +1486,18 @@ class LayerNormFn(torch.autograd.Function):
         return dx, dw, db
 
 
+def invalidate_weight_norm_cache(module: torch.nn.Module) -> int:
+    """Drop the cached positional-conv weight-norm images of a frozen module (PosConvFn): needed after writing its
+    weights in a way that does not bump their version counters (``.data`` writes).  Returns how many were dropped.
+    Captured HIP graphs that replayed a cached image must be recaptured too (Trainer._drop_graphs)."""
+    n = 0
+    for p in module.parameters():
+        if getattr(p, "_dph_wn_img", None) is not None:
+            p._dph_wn_img = None
+            n += 1
+    return n
+
+
 class PosConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, wg, wv, bias, ln_w, ln_b, cfg):
@@ -1486,7 +1508,11 @@ class PosConvFn(torch.autograd.Function):
         dev = x.device
         # weight norm -> bf16 GEMM images (forward and flipped/transposed for dgrad).  A frozen model's (the
         # teacher's: no gradient, parameters without requires_grad) forward image is computed once per weight
-        # version and reused: the step graph then carries no weight-norm launches for it
+        # version and reused: the step graph then carries no weight-norm launches for it.  ASSUMPTION: a frozen
+        # weight changes only through ops that bump its version (load_state_dict, copy_, the DDP broadcast); an
+        # in-place write through .data or an alias with its own version counter does not -- call
+        # invalidate_weight_norm_cache(module) after one.  A graph captured after a cache hit replays the cached
+        # image (it does not re-read wg / wv).
         frozen = not cfg["need_grad"] and not wg.requires_grad and not wv.requires_grad
         key = (wg.data_ptr(), wg._version, wv.data_ptr(), wv._version, G, Kk)
         hit = getattr(wv, "_dph_wn_img", None) if frozen else None

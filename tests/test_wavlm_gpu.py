@@ -132,3 +132,51 @@ def test_pruned_wavlm_forward_vs_reference():
     for h, g in zip(hs, fx["pruned_hiddens"]):
         e = rel_l2(h.float().cpu(), g)
         assert e < 1e-2, e
+
+
+@pytest.mark.parametrize("T", [3584, 3000])
+def test_relpos_backward_long_T_deterministic(T):
+    """The relative-position attention backward at its largest supported length (T = 3584: the [T+127] table
+    window plus, in deterministic mode, four per-wave diagonal histograms in LDS): deterministic mode runs and
+    agrees with the atomic mode (dqkv, dgate, drel_tab rel-L2 <= 1e-4) -- the LDS footprint limit of
+    dph_attention_bwd_relpos."""
+    import ctypes as C
+    from dphubert_amd import _lib
+    from dphubert_amd._lib import call, stream_ptr
+    B, H = 1, 2
+    g = torch.Generator(device="cuda").manual_seed(3)
+    qkv = (torch.randn(B * T, 3 * H * 64, device="cuda", generator=g) * 0.5).to(torch.bfloat16)
+    tab = torch.randn(H, 2 * T - 1, device="cuda", generator=g) * 0.1
+    gate = torch.rand(B, H, T, device="cuda", generator=g)
+    o_u = torch.empty(B * T, H * 64, device="cuda")
+    o_m = torch.empty(B * T, H * 64, device="cuda", dtype=torch.bfloat16)
+    lse = torch.empty(B * H * T, device="cuda")
+    ptr = lambda t: C.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+    call("dph_attention_fwd_relpos", ptr(qkv), ptr(o_u), ptr(o_m), ptr(lse), None, None, ptr(tab), ptr(gate),
+         B, T, H, 0.125, 0.0, 0, None, stream_ptr())
+    do = (torch.randn(B * T, H * 64, device="cuda", generator=g) * 0.1).to(torch.bfloat16)
+    D = torch.empty(B * H * T, device="cuda")
+    dhm = torch.zeros(H, device="cuda")
+    pws = torch.empty(max(1, _lib.lib().dph_attention_bwd_prep_workspace(B, T, H) // 4 + 1), device="cuda")
+    call("dph_attention_bwd_prep", ptr(do), ptr(o_u), None, ptr(D), ptr(dhm), B, T, H, ptr(pws), pws.numel() * 4,
+         stream_ptr())
+    res = {}
+    prev = _lib.lib().dph_get_deterministic()
+    try:
+        for det in (1, 0):
+            _lib.lib().dph_set_deterministic(det)
+            dqkv = torch.empty_like(qkv)
+            dgate = torch.empty_like(gate)
+            dtab = torch.zeros_like(tab)
+            nws = _lib.lib().dph_attention_bwd_relpos_workspace(B, T, H)
+            ws = torch.empty(nws // 4 + 1, device="cuda")
+            call("dph_attention_bwd_relpos", ptr(qkv), ptr(do), None, ptr(lse), ptr(D), ptr(dqkv), None, ptr(tab),
+                 ptr(gate), ptr(dgate), ptr(dtab), B, T, H, 0.125, 0.0, 0, None, ptr(ws), ws.numel() * 4,
+                 stream_ptr())
+            torch.cuda.synchronize()
+            res[det] = (dqkv.float(), dgate, dtab)
+    finally:
+        _lib.lib().dph_set_deterministic(prev)
+    for a, b in zip(res[1], res[0]):
+        assert torch.isfinite(a).all()
+        assert rel_l2(a.cpu(), b.cpu()) <= 1e-4, rel_l2(a.cpu(), b.cpu())
