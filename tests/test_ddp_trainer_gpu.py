@@ -2,7 +2,8 @@
 twin of the RCCL AVG path), each rank with its own bucketed batch length (audio_dataset.py:145-217): the reduced
 gradients equal the mean of the ranks' local gradients, the bucket collectives launch in the same order on both
 ranks, and the parameters stay bitwise identical across ranks after every optimizer step (distill.py:41 strategy
-"ddp").  Runs tools/ddp_trainer_probe.py in a child process (its own process group and spawned ranks)."""
+"ddp"); with gradient accumulation (run_large.sh's --accum_grad) and bf16 bucket payloads too.  Runs
+tools/ddp_trainer_probe.py in a child process (its own process group and spawned ranks)."""
 import os
 import socket
 import subprocess
@@ -14,13 +15,15 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def test_trainer_ws2_different_bucket_lengths():
+@pytest.mark.parametrize("accum,comm", [(1, "fp32"), (3, "fp32"), (1, "bf16")])
+def test_trainer_ws2_different_bucket_lengths(accum, comm):
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     root = Path(__file__).resolve().parents[1]
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
-    r = subprocess.run([sys.executable, str(root / "tools" / "ddp_trainer_probe.py"), "--port", str(port)],
+    r = subprocess.run([sys.executable, str(root / "tools" / "ddp_trainer_probe.py"), "--port", str(port),
+                        "--accum", str(accum), "--comm", comm],
                        capture_output=True, text=True, timeout=300, env=env, cwd=str(root))
     out = r.stdout + r.stderr
     print(r.stdout)
