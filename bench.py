@@ -306,10 +306,19 @@ def main():
             traffic = pmc_traffic(args)
         except Exception as e:  # noqa: BLE001 -- traffic is informational
             traffic_err = repr(e)[:300]
+    # DPH_BENCH_BACKEND=gloo (rehearsal of the N > 1 path on one GPU: every rank on device LOCAL_RANK % count, gloo
+    # collectives, eager steps -- gloo collectives cannot be captured); the scaling runs use the default, nccl = RCCL
+    backend = os.environ.get("DPH_BENCH_BACKEND", "nccl")
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if backend == "gloo":
+            local_rank %= torch.cuda.device_count()
+            args.graphs = "off"
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if backend == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
