@@ -15,8 +15,19 @@
 // Weight norm (components.py:306, dim=2): w = g * v / ||v||_(dims 0,1).
 #include "common.h"
 
+#ifndef DPH_C0_ABL
+#define DPH_C0_ABL 0   // diagnostic builds only: 1 = conv0 GELU / GELU' replaced by a cheap stand-in (timing ablation)
+#endif
+
 namespace dph {
 namespace {
+#if DPH_C0_ABL
+__device__ __forceinline__ float c0_gelu(float x) { return x * 0.5f; }
+__device__ __forceinline__ void c0_gelu_and_grad(float x, float& g, float& d) { g = 0.5f * x; d = 0.5f; }
+#else
+__device__ __forceinline__ float c0_gelu(float x) { return gelu_f(x); }
+__device__ __forceinline__ void c0_gelu_and_grad(float x, float& g, float& d) { gelu_and_grad(x, g, d); }
+#endif
 
 // conv0 of every wav2vec2 / HuBERT / WavLM config is (512, 10, 5): compile-time taps and stride let
 // each thread keep a sliding window of the waveform in registers (k0 = 2*s0: consecutive rows share
@@ -134,7 +145,7 @@ __global__ void __launch_bounds__(256) conv0_apply_kernel(const float* __restric
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
       const float v = fmaf(o[i], sc[i], sh[i]);
-      o[i] = GN ? gelu_f(v) * mk[i] : v;
+      o[i] = GN ? c0_gelu(v) * mk[i] : v;
     }
     bf16_t* yp = y + ((b * p.L0) + t0 + t) * p.C + c0;
     if (VEC) {
@@ -251,8 +262,8 @@ __global__ void __launch_bounds__(256) conv0_gn_bwd_kernel(const float* __restri
         const f32x2_t xh = (v - f32x2_t{mu[i0], mu[i1]}) * f32x2_t{rs[i0], rs[i1]};
         const f32x2_t g = __builtin_elementwise_fma(f32x2_t{ga[i0], ga[i1]}, xh, f32x2_t{be[i0], be[i1]});
         float gl0, gd0, gl1, gd1;
-        gelu_and_grad(g.x, gl0, gd0);
-        gelu_and_grad(g.y, gl1, gd1);
+        c0_gelu_and_grad(g.x, gl0, gd0);
+        c0_gelu_and_grad(g.y, gl1, gd1);
         const f32x2_t cu = {d[i0], d[i1]};
         // dg' = dy GELU'(g): the channel's mask and gamma are factored out of every sum (applied per block)
         const f32x2_t dgp = cu * f32x2_t{gd0, gd1};
@@ -270,7 +281,7 @@ __global__ void __launch_bounds__(256) conv0_gn_bwd_kernel(const float* __restri
         const float xh = (v[i] - mu[i]) * rs[i];
         const float g = fmaf(ga[i], xh, be[i]);
         float gl, gd;
-        gelu_and_grad(g, gl, gd);
+        c0_gelu_and_grad(g, gl, gd);
         const float dgp = d[i] * gd;
 #pragma unroll
         for (int j = 0; j < K0; ++j) acc[i][j] = fmaf(dgp, x[j], acc[i][j]);
