@@ -105,10 +105,15 @@ _SIGS = {
     "dph_attention_bwd_prep": ([vp, vp, vp, vp, vp, i64, i64, i64, vp, i64, S], C.c_int),
     "dph_attention_bwd_prep_workspace": ([i64, i64, i64], i64),
     "dph_attention_bwd": ([vp, vp, vp, vp, vp, vp, vp, i64, i64, i64, f32, f32, u64, vp, S], C.c_int),
+    "dph_attention_bwd_qv": ([vp, vp, vp, vp, vp, vp, vp, i64, i64, i64, f32, f32, u64, vp, vp, vp, vp, i64, S],
+                             C.c_int),
+    "dph_attention_bwd_qv_workspace": ([i64, i64, i64], i64),
     "dph_attention_fwd_relpos": ([vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, i64, f32, f32, u64, vp, S], C.c_int),
     "dph_attention_bwd_relpos": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, i64, f32, f32, u64, vp, vp,
                                   i64, S], C.c_int),
     "dph_attention_bwd_relpos_workspace": ([i64, i64, i64], i64),
+    "dph_attention_bwd_relpos_qv": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, i64, f32, f32, u64, vp, vp,
+                                     i64, vp, vp, vp, i64, S], C.c_int),
     "dph_relpos_table": ([vp, vp, vp, vp, i64, i64, i64, i64, i64, S], C.c_int),
     "dph_relpos_table_bwd": ([vp, vp, vp, i64, i64, i64, i64, i64, S], C.c_int),
     "dph_wavlm_gate_fwd": ([vp, i64, vp, vp, vp, vp, vp, i64, i64, i64, i64, S], C.c_int),
@@ -178,8 +183,10 @@ _lib = None
 # 21: deferred column reductions -- dph_defer_reductions / dph_flush_reductions / dph_deferred_reductions;
 # 22: dph_attention_bwd_prep's D is the rowdot of dO_m itself, the head mask applied to dq / dk / dv in fp32;
 # 23: dph_discard_reductions / dph_reductions_pushed, queue-flush launch errors propagated by every column reduction;
-#     DphGemmArgs.sk_* + dph_gemm_sk_plan: the persistent stream-K 256 x 256 GEMM)
-ABI_VERSION = 23
+#     DphGemmArgs.sk_* + dph_gemm_sk_plan: the persistent stream-K 256 x 256 GEMM;
+# 24: dph_attention_bwd_qv / dph_attention_bwd_relpos_qv + dph_attention_bwd_qv_workspace: the q / v bias
+#     gradients summed inside the attention backward)
+ABI_VERSION = 24
 
 
 class DphError(RuntimeError):

@@ -983,7 +983,8 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const bf16_t* __restrict__ qkv
                                                   const float* __restrict__ Dv, bf16_t* __restrict__ dqkv,
                                                   const int64_t* __restrict__ key_len, AttnShape sh, float scale,
                                                   float drop_p, uint64_t seed, RelBias rb,
-                                                  const uint16_t* __restrict__ keep_in, int bx, int64_t h, int64_t b) {
+                                                  const uint16_t* __restrict__ keep_in, float* __restrict__ bpart,
+                                                  int bx, int64_t h, int64_t b) {
   seed = epoch_seed(seed);   // per-step RNG epoch (graph replays)
   const uint32_t mix = seed_mix(seed);
   constexpr int TB = QT_BWD * 128;   // 4096 B per tile
@@ -1224,6 +1225,28 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const bf16_t* __restrict__ qkv
     if (more) store_tiles(cur ^ 1, qt + 1);
     __syncthreads();
   }
+  if (bpart != nullptr) {
+    // v_proj bias gradient (the column sums of dV, components.py:365 v_proj): this wave's partial over its keys
+    // < T, in a fixed order (keys in-lane, then the four lane groups g), into its row of the [waves][2 * H * 64]
+    // slab (q half | v half) that the host reduces over the rows -- no second pass over dqkv
+    float cs[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      cs[d] = 0.f;
+#pragma unroll
+      for (int u = 0; u < NG; ++u)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (k0 + 16 * u + 4 * g + i < T) cs[d] += dv[u][d][i];
+      cs[d] += __shfl_xor(cs[d], 16, 64);
+      cs[d] += __shfl_xor(cs[d], 32, 64);
+    }
+    if (g == 0) {
+      float* row = bpart + (((int64_t)b * gridDim.x + bx) * 4 + wave) * (2 * H * HD) + (H + h) * HD;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) row[16 * d + (lane & 15)] = cs[d] * hm;
+    }
+  }
   // lane holds dK[key = k0 + 16u + 4g + i][d = 16dd + (lane&15)]: stage the wave's [32 keys][64] bf16
   // tile in LDS and store whole 128-B key rows with 16-B stores (4 per lane per tensor instead of 32
   // scattered 2-byte stores)
@@ -1260,7 +1283,8 @@ __device__ __forceinline__ void attn_bwd_dq_body(const bf16_t* __restrict__ qkv,
                                                  const float* __restrict__ Dv, bf16_t* __restrict__ dqkv,
                                                  const int64_t* __restrict__ key_len, AttnShape sh, float scale,
                                                  float drop_p, uint64_t seed, RelBias rb,
-                                                 const uint16_t* __restrict__ keep_in, int bx, int64_t h, int64_t b) {
+                                                 const uint16_t* __restrict__ keep_in, float* __restrict__ bpart,
+                                                 int bx, int64_t h, int64_t b) {
   extern __shared__ float dyn[];   // BIAS: hist [T + RB - 1] (diagonal sums of dS * gate) | table window [T + RB - 1]
   seed = epoch_seed(seed);   // per-step RNG epoch (graph replays)
   const uint32_t mix = seed_mix(seed);
@@ -1503,6 +1527,28 @@ __device__ __forceinline__ void attn_bwd_dq_body(const bf16_t* __restrict__ qkv,
       }
     }
   }
+  if (bpart != nullptr) {
+    // q_proj bias gradient (the column sums of dQ): lane holds dQ[q0 + 16u + (lane&15)][16d + 4g + j]; summed over
+    // u in-lane, then over the 16 row lanes, in a fixed order (rows past T hold exactly 0 and are skipped anyway)
+    f32x4_t cs[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      cs[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < NG; ++u)
+        if (qme[u] < T) cs[d] += dq[u][d];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int m = 1; m < 16; m <<= 1) cs[d][j] += __shfl_xor(cs[d][j], m, 64);
+    }
+    if ((lane & 15) == 0) {
+      float* row = bpart + (((int64_t)b * gridDim.x + bx) * 4 + wave) * (2 * H * HD) + h * HD;
+#pragma unroll
+      for (int d = 0; d < 4; ++d)
+        *reinterpret_cast<f32x4_t*>(row + 16 * d + 4 * g) = cs[d] * dq_mul;
+    }
+  }
 #pragma unroll
   for (int u = 0; u < NG; ++u) {
     if (qme[u] >= T) continue;
@@ -1530,8 +1576,8 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_kernel(const bf16_t* __restri
                                                        const float* __restrict__ lse, const float* __restrict__ Dv,
                                                        bf16_t* __restrict__ dqkv, const int64_t* __restrict__ key_len,
                                                        AttnShape sh, float scale, float drop_p, uint64_t seed,
-                                                       RelBias rb, const uint16_t* __restrict__ keep_in, int nbz,
-                                                       int mode) {
+                                                       RelBias rb, const uint16_t* __restrict__ keep_in,
+                                                       float* __restrict__ bpart, int nbz, int mode) {
   const int z = (int)blockIdx.z;
   const bool kv = mode == 1 || (mode == 0 && z < nbz);
   if constexpr (!BIAS) {
@@ -1547,15 +1593,19 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_kernel(const bf16_t* __restri
         if (r < T)
           *reinterpret_cast<uint4*>(dqkv + (b * T + r) * RS + (sel * H + h) * HD + (c & 7) * 8) = make_uint4(0, 0, 0, 0);
       }
+      if (bpart != nullptr) {   // this head's q (dQ blocks) / v (dK/dV blocks) bias partials: 4 wave rows x 64
+        const int w = threadIdx.x >> 6, c = threadIdx.x & 63;
+        bpart[(((int64_t)b * gridDim.x + blockIdx.x) * 4 + w) * (2 * H * HD) + ((kv ? H : 0) + h) * HD + c] = 0.f;
+      }
       return;
     }
   }
   if (kv)
     attn_bwd_dkv_body<DROP, BIAS, KEEP>(qkv, dom, head_mask, lse, Dv, dqkv, key_len, sh, scale, drop_p, seed, rb,
-                                        keep_in, (int)blockIdx.x, blockIdx.y, z);
+                                        keep_in, bpart, (int)blockIdx.x, blockIdx.y, z);
   else
     attn_bwd_dq_body<DROP, BIAS, KEEP>(qkv, dom, head_mask, lse, Dv, dqkv, key_len, sh, scale, drop_p, seed, rb,
-                                       keep_in, (int)blockIdx.x, blockIdx.y, mode == 0 ? z - nbz : z);
+                                       keep_in, bpart, (int)blockIdx.x, blockIdx.y, mode == 0 ? z - nbz : z);
 }
 
 // deterministic mode: dtab[h][gi] += the dQ blocks' diagonal sums (relpos dtab_part slab) over (b, query block) in
@@ -1641,7 +1691,7 @@ void launch_fwd(dim3 grid, hipStream_t stream, const void* qkv, void* o_u, void*
 template <bool DROP, bool BIAS, bool KEEP>
 void launch_bwd_k(dim3 grid, hipStream_t stream, const void* qkv, const void* dom, const float* hm, const float* lse,
                   const float* Dvec, void* dqkv, const int64_t* key_len, AttnShape sh, float scale, float p,
-                  uint64_t seed, RelBias rb, const void* keep) {
+                  uint64_t seed, RelBias rb, const void* keep, float* bpart) {
   const size_t tw_bytes = BIAS ? (size_t)(sh.T + RB - 1) * sizeof(float) : 0;
   // dynamic LDS: the table window + one diagonal histogram (four, per wave, in deterministic mode)
   const size_t dyn_bytes = (rb.dtab_part != nullptr ? 5 : 2) * tw_bytes;
@@ -1652,24 +1702,26 @@ void launch_bwd_k(dim3 grid, hipStream_t stream, const void* qkv, const void* do
       hipLaunchKernelGGL((attn_bwd_kernel<DROP, BIAS, KEEP>), grid, dim3(256), dyn_bytes, stream,
                          reinterpret_cast<const bf16_t*>(qkv), reinterpret_cast<const bf16_t*>(dom), hm, lse, Dvec,
                          reinterpret_cast<bf16_t*>(dqkv), key_len, sh, scale, p, seed, rb,
-                         reinterpret_cast<const uint16_t*>(keep), nbz, mode);
+                         reinterpret_cast<const uint16_t*>(keep), bpart, nbz, mode);
     return;
   }
   const dim3 g2(grid.x, grid.y, 2 * grid.z);
   hipLaunchKernelGGL((attn_bwd_kernel<DROP, BIAS, KEEP>), g2, dim3(256), dyn_bytes, stream,
                      reinterpret_cast<const bf16_t*>(qkv), reinterpret_cast<const bf16_t*>(dom), hm, lse, Dvec,
                      reinterpret_cast<bf16_t*>(dqkv), key_len, sh, scale, p, seed, rb,
-                     reinterpret_cast<const uint16_t*>(keep), nbz, 0);
+                     reinterpret_cast<const uint16_t*>(keep), bpart, nbz, 0);
 }
 
 template <bool DROP, bool BIAS>
 void launch_bwd(dim3 grid, hipStream_t stream, const void* qkv, const void* dom, const float* hm, const float* lse,
                 const float* Dvec, void* dqkv, const int64_t* key_len, AttnShape sh, float scale, float p,
-                uint64_t seed, RelBias rb, const void* keep) {
+                uint64_t seed, RelBias rb, const void* keep, float* bpart) {
   if (DROP && keep != nullptr)
-    launch_bwd_k<DROP, BIAS, true>(grid, stream, qkv, dom, hm, lse, Dvec, dqkv, key_len, sh, scale, p, seed, rb, keep);
+    launch_bwd_k<DROP, BIAS, true>(grid, stream, qkv, dom, hm, lse, Dvec, dqkv, key_len, sh, scale, p, seed, rb, keep,
+                                   bpart);
   else
-    launch_bwd_k<DROP, BIAS, false>(grid, stream, qkv, dom, hm, lse, Dvec, dqkv, key_len, sh, scale, p, seed, rb, keep);
+    launch_bwd_k<DROP, BIAS, false>(grid, stream, qkv, dom, hm, lse, Dvec, dqkv, key_len, sh, scale, p, seed, rb, keep,
+                                    bpart);
 }
 
 }  // namespace
@@ -1699,21 +1751,32 @@ static int attention_fwd(const void* qkv, void* o_unmasked, void* o_masked, floa
 
 static int attention_bwd(const void* qkv, const void* do_masked, const float* head_mask, const float* lse,
                          const float* Dvec, void* dqkv, const int64_t* key_len, int64_t B, int64_t T, int64_t H,
-                         float scale, float dropout_p, uint64_t seed, RelBias rb, const void* keep, hipStream_t stream) {
+                         float scale, float dropout_p, uint64_t seed, RelBias rb, const void* keep, hipStream_t stream,
+                         float* dbq = nullptr, float* dbv = nullptr, float* bws = nullptr) {
   AttnShape sh{B, T, H, 3 * H * HD};
   dim3 grid((unsigned)cdiv(T, RB), (unsigned)H, (unsigned)B);
   const bool bias = rb.tab != nullptr;
+  float* bpart = dbq != nullptr ? bws : nullptr;
   DPH_REQUIRE(dropout_p <= 0.f || pairs_fit(B, T, H), "dph_attention_bwd: B*H*T*ceil(T/2) >= 2^32 dropout pairs");
   DPH_REQUIRE(keep == nullptr || (reinterpret_cast<uintptr_t>(keep) & 7) == 0, "dph_attention_bwd: keep bits not 8-B aligned");
   DPH_REQUIRE(2 * B < 65536 && H < 65536, "dph_attention_bwd: grid too large (B=%lld H=%lld)", (long long)B, (long long)H);
   if (dropout_p > 0.f) {
-    if (bias) launch_bwd<true, true>(grid, stream, qkv, do_masked, head_mask, lse, Dvec, dqkv, key_len, sh, scale, dropout_p, seed, rb, keep);
-    else launch_bwd<true, false>(grid, stream, qkv, do_masked, head_mask, lse, Dvec, dqkv, key_len, sh, scale, dropout_p, seed, rb, keep);
+    if (bias) launch_bwd<true, true>(grid, stream, qkv, do_masked, head_mask, lse, Dvec, dqkv, key_len, sh, scale, dropout_p, seed, rb, keep, bpart);
+    else launch_bwd<true, false>(grid, stream, qkv, do_masked, head_mask, lse, Dvec, dqkv, key_len, sh, scale, dropout_p, seed, rb, keep, bpart);
   } else {
-    if (bias) launch_bwd<false, true>(grid, stream, qkv, do_masked, head_mask, lse, Dvec, dqkv, key_len, sh, scale, dropout_p, seed, rb, nullptr);
-    else launch_bwd<false, false>(grid, stream, qkv, do_masked, head_mask, lse, Dvec, dqkv, key_len, sh, scale, dropout_p, seed, rb, nullptr);
+    if (bias) launch_bwd<false, true>(grid, stream, qkv, do_masked, head_mask, lse, Dvec, dqkv, key_len, sh, scale, dropout_p, seed, rb, nullptr, bpart);
+    else launch_bwd<false, false>(grid, stream, qkv, do_masked, head_mask, lse, Dvec, dqkv, key_len, sh, scale, dropout_p, seed, rb, nullptr, bpart);
   }
+  DPH_TRY(check_launch("dph_attention_bwd"));
+  // q / v bias gradients: the wave-row slab summed over its rows in order (queued in a deferred-reduction block)
+  if (bpart != nullptr) DPH_TRY(slab_reduce_cols(bpart, B * grid.x * 4, 2 * H * HD, H * HD, dbq, dbv, nullptr, stream));
   return check_launch("dph_attention_bwd");
+}
+
+// the q / v bias-gradient slab of dph_attention_bwd_qv / dph_attention_bwd_relpos_qv: one fp32 row of [q | v] columns
+// (2 * H * 64) per wave of the backward grid (B * ceil(T / 128) * 4 rows)
+extern "C" int64_t dph_attention_bwd_qv_workspace(int64_t B, int64_t T, int64_t H) {
+  return B * cdiv(T, (int64_t)RB) * 4 * 2 * H * HD * 4;
 }
 
 extern "C" int dph_attention_fwd(const void* qkv, void* o_unmasked, void* o_masked, float* lse,
@@ -1762,16 +1825,28 @@ extern "C" int dph_attention_bwd(const void* qkv, const void* do_masked, const f
                        RelBias{nullptr, nullptr, nullptr, nullptr}, keep_bits, stream);
 }
 
+extern "C" int dph_attention_bwd_qv(const void* qkv, const void* do_masked, const float* head_mask, const float* lse,
+                                    const float* Dvec, void* dqkv, const int64_t* key_len, int64_t B, int64_t T,
+                                    int64_t H, float scale, float dropout_p, uint64_t seed, const void* keep_bits,
+                                    float* dbq, float* dbv, float* ws, int64_t ws_bytes, hipStream_t stream) {
+  DPH_REQUIRE(qkv && do_masked && lse && Dvec && dqkv && dbq && dbv && B > 0 && T > 0 && H > 0,
+              "dph_attention_bwd_qv: bad args");
+  DPH_REQUIRE(ws && ws_bytes >= dph_attention_bwd_qv_workspace(B, T, H) && (reinterpret_cast<uintptr_t>(ws) & 15) == 0,
+              "dph_attention_bwd_qv: needs dph_attention_bwd_qv_workspace bytes (16-B aligned)");
+  return attention_bwd(qkv, do_masked, head_mask, lse, Dvec, dqkv, key_len, B, T, H, scale, dropout_p, seed,
+                       RelBias{nullptr, nullptr, nullptr, nullptr}, keep_bits, stream, dbq, dbv, ws);
+}
+
 // deterministic mode: the dQ blocks' diagonal-sum slab [B][H][ceil(T/128)][T + 127] fp32
 extern "C" int64_t dph_attention_bwd_relpos_workspace(int64_t B, int64_t T, int64_t H) {
   return B * H * cdiv(T, (int64_t)RB) * (T + RB - 1) * 4;
 }
 
-extern "C" int dph_attention_bwd_relpos(const void* qkv, const void* do_masked, const float* head_mask,
-                                        const float* lse, const float* Dvec, void* dqkv, const int64_t* key_len,
-                                        const float* rel_tab, const float* gate, float* dgate, float* drel_tab,
-                                        int64_t B, int64_t T, int64_t H, float scale, float dropout_p, uint64_t seed,
-                                        const void* keep_bits, float* ws, int64_t ws_bytes, hipStream_t stream) {
+static int attention_bwd_relpos(const void* qkv, const void* do_masked, const float* head_mask, const float* lse,
+                                const float* Dvec, void* dqkv, const int64_t* key_len, const float* rel_tab,
+                                const float* gate, float* dgate, float* drel_tab, int64_t B, int64_t T, int64_t H,
+                                float scale, float dropout_p, uint64_t seed, const void* keep_bits, float* ws,
+                                int64_t ws_bytes, hipStream_t stream, float* dbq, float* dbv, float* bws) {
   DPH_REQUIRE(qkv && do_masked && lse && Dvec && dqkv && rel_tab && gate && dgate && drel_tab && B > 0 && T > 0 &&
                   T <= 3584 && H > 0,
               "dph_attention_bwd_relpos: bad args (T <= 3584: the [T+127] fp32 table window, in deterministic mode plus four "
@@ -1780,9 +1855,34 @@ extern "C" int dph_attention_bwd_relpos(const void* qkv, const void* do_masked, 
   DPH_REQUIRE(!det || (ws && ws_bytes >= dph_attention_bwd_relpos_workspace(B, T, H)),
               "dph_attention_bwd_relpos: deterministic mode needs dph_attention_bwd_relpos_workspace bytes");
   const int rc = attention_bwd(qkv, do_masked, head_mask, lse, Dvec, dqkv, key_len, B, T, H, scale, dropout_p, seed,
-                               RelBias{rel_tab, gate, dgate, drel_tab, det ? ws : nullptr}, keep_bits, stream);
+                               RelBias{rel_tab, gate, dgate, drel_tab, det ? ws : nullptr}, keep_bits, stream, dbq,
+                               dbv, bws);
   if (rc || !det) return rc;
   hipLaunchKernelGGL(relpos_dtab_reduce, dim3((unsigned)cdiv(H * (2 * T - 1), 256)), dim3(256), 0, stream, ws, B, H, T,
                      drel_tab);
   return check_launch("dph_attention_bwd_relpos dtab reduce");
+}
+
+extern "C" int dph_attention_bwd_relpos(const void* qkv, const void* do_masked, const float* head_mask,
+                                        const float* lse, const float* Dvec, void* dqkv, const int64_t* key_len,
+                                        const float* rel_tab, const float* gate, float* dgate, float* drel_tab,
+                                        int64_t B, int64_t T, int64_t H, float scale, float dropout_p, uint64_t seed,
+                                        const void* keep_bits, float* ws, int64_t ws_bytes, hipStream_t stream) {
+  return attention_bwd_relpos(qkv, do_masked, head_mask, lse, Dvec, dqkv, key_len, rel_tab, gate, dgate, drel_tab, B,
+                              T, H, scale, dropout_p, seed, keep_bits, ws, ws_bytes, stream, nullptr, nullptr,
+                              nullptr);
+}
+
+extern "C" int dph_attention_bwd_relpos_qv(const void* qkv, const void* do_masked, const float* head_mask,
+                                           const float* lse, const float* Dvec, void* dqkv, const int64_t* key_len,
+                                           const float* rel_tab, const float* gate, float* dgate, float* drel_tab,
+                                           int64_t B, int64_t T, int64_t H, float scale, float dropout_p,
+                                           uint64_t seed, const void* keep_bits, float* ws, int64_t ws_bytes,
+                                           float* dbq, float* dbv, float* bws, int64_t bws_bytes,
+                                           hipStream_t stream) {
+  DPH_REQUIRE(dbq && dbv && bws && bws_bytes >= dph_attention_bwd_qv_workspace(B, T, H) &&
+                  (reinterpret_cast<uintptr_t>(bws) & 15) == 0,
+              "dph_attention_bwd_relpos_qv: needs dph_attention_bwd_qv_workspace bytes (16-B aligned)");
+  return attention_bwd_relpos(qkv, do_masked, head_mask, lse, Dvec, dqkv, key_len, rel_tab, gate, dgate, drel_tab, B,
+                              T, H, scale, dropout_p, seed, keep_bits, ws, ws_bytes, stream, dbq, dbv, bws);
 }

@@ -156,7 +156,7 @@ extern "C" int dph_flush_reductions(hipStream_t stream) {
 }
 
 extern "C" const char* dph_last_error(void) { return dph::g_err; }
-extern "C" int dph_abi_version(void) { return 23; }
+extern "C" int dph_abi_version(void) { return 24; }
 extern "C" int dph_set_deterministic(int on) {
   dph::g_det = on ? 1 : 0;
   return DPH_OK;

@@ -763,6 +763,9 @@ def _dev(t):
 # unchanged either way).  DPH_KBIAS_GRAD=1 computes the column sum of dK as the reference does (checkpoint-matching
 # runs; its values are noise and are not parity-pinned).
 _KBIAS_GRAD = os.environ.get("DPH_KBIAS_GRAD", "0") == "1"
+# DPH_ATTN_QV=0: the q / v bias gradients as a separate column-sum pass over dqkv (dph_colsum3) instead of inside the
+# attention backward (A/B timing)
+_ATTN_QV = os.environ.get("DPH_ATTN_QV", "1") != "0"
 
 
 def _qkv_bias_grad(dqkv, dbqkv, M, dev):
@@ -1963,9 +1966,8 @@ class EncoderLayerFn(torch.autograd.Function):
             call("dph_attention_bwd_prep", ptr(do_m), ptr(sv["o_u"]), ptr(hm), ptr(Dvec), ptr(g["hm"]), B, T, H,
                  *_ws(_lib.lib().dph_attention_bwd_prep_workspace(B, T, H), dev), _s())
             dqkv = torch.empty_like(sv["qkv"])
-            wl_g = EncoderLayerFn._attention_bwd(ctx, cfg, sv, do_m, hm, Dvec, dqkv)
             dbqkv, _ = go.buf(pr["bq"], pr["bk"], pr["bv"])
-            _qkv_bias_grad(dqkv, dbqkv, M, dev)
+            wl_g = EncoderLayerFn._attention_bwd(ctx, cfg, sv, do_m, hm, Dvec, dqkv, dbqkv)
             dwqkv, direct = go.buf(pr["wq"], pr["wk"], pr["wv"], zero=False)
             k4 = _layer_wgrad(dqkv, xn1, dwqkv, direct, (pr["wq"], pr["wk"], pr["wv"]))
             dxn1 = K.linear_dgrad(dqkv, sv["Wqkv"], w_t=t_image(sv["Wqkv"]))
@@ -2013,21 +2015,45 @@ class EncoderLayerFn(torch.autograd.Function):
         return gate
 
     @staticmethod
-    def _attention_bwd(ctx, cfg, sv, do_m, hm, Dvec, dqkv):
+    def _attention_bwd(ctx, cfg, sv, do_m, hm, Dvec, dqkv, dbqkv):
+        """dq | dk | dv into dqkv, and the q / v bias gradients added into dbqkv's [bq | bk | bv] (summed inside the
+        backward kernels: dph_attention_bwd_qv; DPH_KBIAS_GRAD=1 -- the k bias as well -- or DPH_ATTN_QV=0 takes the
+        plain backward and the separate column sums of dqkv)."""
         B, T, H = cfg["B"], cfg["T"], cfg["H"]
         wl = ctx.wl
-        if wl is None:
-            call("dph_attention_bwd", ptr(sv["qkv"]), ptr(do_m), ptr(hm), ptr(sv["lse"]), ptr(Dvec), ptr(dqkv),
-                 ptr(cfg["lengths"]), B, T, H, cfg["head_dim"] ** -0.5, cfg["p_attn"], sv["seed_a"],
-                 ptr(getattr(ctx, "attn_keep", None)), _s())
-            return None
         dev = dqkv.device
+        M = B * T
+        fused = _ATTN_QV and not _KBIAS_GRAD
+        L = _lib.lib()
+        # one scratch block for the relpos slab (WavLM, deterministic mode) and the q / v bias slab: two _ws calls
+        # would hand out the same freed block twice (the caching allocator reuses it for the second request)
+        rws = L.dph_attention_bwd_relpos_workspace(B, T, H) if wl is not None else 0
+        rws = (rws + 255) // 256 * 256
+        qvb = L.dph_attention_bwd_qv_workspace(B, T, H) if fused else 0
+        wsp, _ = _ws(rws + qvb, dev)
+        if fused:
+            Dh = dqkv.shape[1] // 3
+            base = dbqkv.data_ptr()
+            qv = (base, base + 8 * Dh, wsp + rws, qvb)
+        if wl is None:
+            args = (ptr(sv["qkv"]), ptr(do_m), ptr(hm), ptr(sv["lse"]), ptr(Dvec), ptr(dqkv), ptr(cfg["lengths"]), B, T,
+                    H, cfg["head_dim"] ** -0.5, cfg["p_attn"], sv["seed_a"], ptr(getattr(ctx, "attn_keep", None)))
+            if fused:
+                call("dph_attention_bwd_qv", *args, *qv, _s())
+            else:
+                call("dph_attention_bwd", *args, _s())
+                _qkv_bias_grad(dqkv, dbqkv, M, dev)
+            return None
         dgate = torch.empty(B * H * T, dtype=F32, device=dev)
         dtab = torch.zeros(wl["rel_tab"].shape, dtype=F32, device=dev)
-        call("dph_attention_bwd_relpos", ptr(sv["qkv"]), ptr(do_m), ptr(hm), ptr(sv["lse"]), ptr(Dvec), ptr(dqkv),
-             ptr(cfg["lengths"]), ptr(wl["rel_tab"]), ptr(sv["gate"]), ptr(dgate), ptr(dtab), B, T, H,
-             cfg["head_dim"] ** -0.5, cfg["p_attn"], sv["seed_a"], ptr(getattr(ctx, "attn_keep", None)),
-             *_ws(_lib.lib().dph_attention_bwd_relpos_workspace(B, T, H), dev), _s())
+        args = (ptr(sv["qkv"]), ptr(do_m), ptr(hm), ptr(sv["lse"]), ptr(Dvec), ptr(dqkv), ptr(cfg["lengths"]),
+                ptr(wl["rel_tab"]), ptr(sv["gate"]), ptr(dgate), ptr(dtab), B, T, H, cfg["head_dim"] ** -0.5,
+                cfg["p_attn"], sv["seed_a"], ptr(getattr(ctx, "attn_keep", None)), wsp, rws)
+        if fused:
+            call("dph_attention_bwd_relpos_qv", *args, *qv, _s())
+        else:
+            call("dph_attention_bwd_relpos", *args, _s())
+            _qkv_bias_grad(dqkv, dbqkv, M, dev)
         return dgate, dtab
 
     @staticmethod
@@ -2112,10 +2138,9 @@ class EncoderLayerFn(torch.autograd.Function):
             call("dph_attention_bwd_prep", ptr(do_m), ptr(sv["o_u"]), ptr(hm), ptr(Dvec), ptr(g["hm"]), B, T, H,
                  *_ws(_lib.lib().dph_attention_bwd_prep_workspace(B, T, H), dev), _s())
             dqkv = torch.empty_like(sv["qkv"])
-            wl_g = EncoderLayerFn._attention_bwd(ctx, cfg, sv, do_m, hm, Dvec, dqkv)
             dbqkv, dqb = go.buf(pr["bq"], pr["bk"], pr["bv"])
             with _defer_red(go, dqb):
-                _qkv_bias_grad(dqkv, dbqkv, M, dev)
+                wl_g = EncoderLayerFn._attention_bwd(ctx, cfg, sv, do_m, hm, Dvec, dqkv, dbqkv)
             dwqkv, direct = go.buf(pr["wq"], pr["wk"], pr["wv"], zero=False)
             k4 = _layer_wgrad(dqkv, h, dwqkv, direct, (pr["wq"], pr["wk"], pr["wv"]))
             dh = K.linear_dgrad(dqkv, sv["Wqkv"], w_t=t_image(sv["Wqkv"]), residual=ds1)

@@ -316,6 +316,18 @@ int dph_attention_bwd_prep(const void* do_masked, const void* o_unmasked, const 
 int dph_attention_bwd(const void* qkv, const void* do_masked, const float* head_mask, const float* lse,
                       const float* Dvec, void* dqkv, const int64_t* key_len, int64_t B, int64_t T, int64_t H,
                       float scale, float dropout_p, uint64_t seed, const void* keep_bits, hipStream_t stream);
+/* ABI 24: dph_attention_bwd plus the q_proj / v_proj bias gradients (replaces the reference's autograd column sums
+ * of the q / v projection output gradients: components.py:365-366 v_proj / q_proj, nn.Linear(bias=True)):
+ * dbq[H*64], dbv[H*64] (ACCUMULATED) += the column sums of dQ / dV in fp32 (before dqkv's bf16 rounding; padded keys
+ * < T included as in dqkv, rows >= T excluded), summed by each backward wave over its 32 rows in a fixed order into
+ * ws (16-B aligned, dph_attention_bwd_qv_workspace(B, T, H) bytes = one [q | v] fp32 row per wave) and reduced
+ * over the rows in order (inside a dph_defer_reductions block: queued).  The k_proj bias gradient is exactly zero
+ * (softmax shift invariance) and is not produced. */
+int64_t dph_attention_bwd_qv_workspace(int64_t B, int64_t T, int64_t H);
+int dph_attention_bwd_qv(const void* qkv, const void* do_masked, const float* head_mask, const float* lse,
+                         const float* Dvec, void* dqkv, const int64_t* key_len, int64_t B, int64_t T, int64_t H,
+                         float scale, float dropout_p, uint64_t seed, const void* keep_bits, float* dbq, float* dbv,
+                         float* ws, int64_t ws_bytes, hipStream_t stream);
 
 /* ------------------------------------------------------------------------ *
  * WavLM gated relative-position bias (WavLMSelfAttention, components.py:486-659).
@@ -340,6 +352,13 @@ int dph_attention_bwd_relpos(const void* qkv, const void* do_masked, const float
                              const float* gate, float* dgate, float* drel_tab, int64_t B, int64_t T, int64_t H,
                              float scale, float dropout_p, uint64_t seed, const void* keep_bits, float* ws,
                              int64_t ws_bytes, hipStream_t stream);
+/* ABI 24: dph_attention_bwd_relpos plus dbq / dbv as dph_attention_bwd_qv (bws: its workspace) */
+int dph_attention_bwd_relpos_qv(const void* qkv, const void* do_masked, const float* head_mask, const float* lse,
+                                const float* Dvec, void* dqkv, const int64_t* key_len, const float* rel_tab,
+                                const float* gate, float* dgate, float* drel_tab, int64_t B, int64_t T, int64_t H,
+                                float scale, float dropout_p, uint64_t seed, const void* keep_bits, float* ws,
+                                int64_t ws_bytes, float* dbq, float* dbv, float* bws, int64_t bws_bytes,
+                                hipStream_t stream);
 /* rel_tab[h][r] = embed[bucket(r-(T-1))][heads[h]] (embed [num_buckets][Htot] fp32; heads [H] int64 or NULL =
  * identity); buckets [2T-1] int64 (optional) receives the bucket index table; either output may be NULL */
 int dph_relpos_table(const float* embed, const int64_t* heads, float* rel_tab, int64_t* buckets, int64_t T,

@@ -707,3 +707,95 @@ def test_colsum3_segments(skip_k):
             assert torch.equal(outs[1].cpu(), torch.full((seg,), 0.5))   # untouched
             continue
         torch.testing.assert_close(outs[i].double().cpu(), want[i], rtol=0, atol=2e-3)
+
+
+@pytest.mark.parametrize("T,lens,p,zero_head,relpos,split", [
+    (499, None, 0.1, False, False, "0"),      # the distill shape (B = 16): several rounds of blocks
+    (499, None, 0.0, True, False, "0"),       # an exactly-zero head: the blocks' early-return path writes its rows
+    (131, [131, 97], 0.1, False, False, "0"),  # padded keys, T not a multiple of 128 (waves past T)
+    (131, [131, 97], 0.1, False, False, "1"),  # the dK/dV and dQ bodies as two launches
+    (200, [200, 150], 0.1, False, True, "0"),  # WavLM gated relative-position bias
+])
+def test_attention_bwd_qv_bias_sums(T, lens, p, zero_head, relpos, split, monkeypatch):
+    """dph_attention_bwd_qv / dph_attention_bwd_relpos_qv (ABI 24): dqkv bitwise that of the plain backward; dbq / dbv
+    (accumulated) = the column sums of dQ / dV -- summed in fp32 before dqkv's bf16 rounding, so against the float64
+    column sums of the stored bf16 rows they differ by at most the rounding of each element (2^-9 relative, bound
+    2^-8 * sum |x| per column); the k bias slot is never written; repeated and deferred (queued, flushed) runs are
+    bitwise equal."""
+    from dphubert_amd import _lib
+    from dphubert_amd._lib import call, ptr
+    monkeypatch.setenv("DPH_ATTN_SPLIT", split)
+    torch.manual_seed(9)
+    B, H = 16 if lens is None else 2, 12
+    D = H * 64
+    L = _lib.lib()
+    qkv = (torch.randn(B * T, 3 * D, device=DEV) * 0.5).to(torch.bfloat16)
+    g = torch.randn(B * T, D, device=DEV).to(torch.bfloat16)
+    hm = torch.rand(H, device=DEV) + 0.1
+    if zero_head:
+        hm[3] = 0.0
+    ln = torch.tensor(lens, device=DEV, dtype=torch.int64) if lens else None
+    s = _lib.stream_ptr()
+    keep = torch.zeros(L.dph_attention_keep_bytes(B, T, H) // 8, dtype=torch.int64, device=DEV) if p > 0 else None
+    o_u = torch.empty(B * T, D, device=DEV, dtype=torch.float32)
+    o_m = torch.empty(B * T, D, device=DEV, dtype=torch.bfloat16)
+    lse = torch.empty(B * H * T, device=DEV)
+    if relpos:
+        tab = torch.randn(H, 2 * T - 1, device=DEV) * 0.5
+        gate = torch.rand(B * H * T, device=DEV) * 2.0
+        call("dph_attention_fwd_relpos", ptr(qkv), ptr(o_u), ptr(o_m), ptr(lse), ptr(hm), ptr(ln), ptr(tab), ptr(gate),
+             B, T, H, 0.125, p, 5, ptr(keep), s)
+    else:
+        call("dph_attention_fwd", ptr(qkv), ptr(o_u), ptr(o_m), ptr(lse), ptr(hm), ptr(ln), B, T, H, 0.125, p, 5,
+             ptr(keep), s)
+    Dv = torch.empty(B * H * T, device=DEV)
+    call("dph_attention_bwd_prep", ptr(g), ptr(o_u), ptr(hm), ptr(Dv), None, B, T, H, None, 0, s)
+
+    def run(qv, defer=False):
+        dqkv = torch.full_like(qkv, float("nan"))
+        db = torch.full((3, D), 0.5, device=DEV)
+        com = (ptr(qkv), ptr(g), ptr(hm), ptr(lse), ptr(Dv), ptr(dqkv), ptr(ln))
+        # (separate live tensors: two _ws calls in a row can return the same freed block)
+        wsq_t = torch.empty(L.dph_attention_bwd_qv_workspace(B, T, H) // 4, device=DEV)
+        wsq = (ptr(wsq_t), wsq_t.numel() * 4)
+        if relpos:
+            dgate = torch.empty(B * H * T, device=DEV)
+            dtab = torch.zeros(H, 2 * T - 1, device=DEV)
+            wsr = torch.empty(L.dph_attention_bwd_relpos_workspace(B, T, H) // 4, device=DEV)
+            args = com + (ptr(tab), ptr(gate), ptr(dgate), ptr(dtab), B, T, H, 0.125, p, 5, ptr(keep), ptr(wsr),
+                          wsr.numel() * 4)
+        else:
+            args = com + (B, T, H, 0.125, p, 5, ptr(keep))
+        if defer:
+            L.dph_defer_reductions(1)
+        name = "dph_attention_bwd_relpos" if relpos else "dph_attention_bwd"
+        if qv:
+            call(name + "_qv", *args, ptr(db[0]), ptr(db[2]), *wsq, s)
+        else:
+            call(name, *args, s)
+        if defer:
+            L.dph_defer_reductions(0)
+            assert int(L.dph_reductions_pushed()) > 0
+            call("dph_flush_reductions", s)
+        torch.cuda.synchronize()
+        return dqkv, db.cpu()
+
+    d0, _ = run(False)
+    d1, db1 = run(True)
+    d2, db2 = run(True)
+    assert torch.isfinite(d0.float()).all()
+    assert torch.equal(d0, d1)
+    assert torch.equal(db1, db2)
+    x = d0.double().cpu().view(B * T, 3, D)
+    want = x.sum(0) + 0.5
+    bound = x.abs().sum(0) * 2.0 ** -8 + 1e-4
+    for i in (0, 2):
+        err = (db1[i].double() - want[i]).abs()
+        assert (err <= bound[i]).all(), (i, (err / bound[i]).max().item())
+    assert torch.equal(db1[1], torch.full((D,), 0.5))
+    if zero_head:
+        assert torch.equal(db1[0, 3 * 64:4 * 64], torch.full((64,), 0.5))
+        assert torch.equal(db1[2, 3 * 64:4 * 64], torch.full((64,), 0.5))
+    if L.dph_get_deterministic():
+        d3, db3 = run(True, defer=True)
+        assert torch.equal(d3, d0) and torch.equal(db3, db1)
