@@ -45,14 +45,23 @@ def _s():
     return _lib.stream_ptr()
 
 
-def _ws(nbytes: int, dev):
-    """Scratch for a column-partial slab (stream-ordered caching allocator: the block is reused only
-    by work queued after the kernel that consumes it -- inside a deferred_reductions block the slab is kept
-    alive until the block's flush, which is then that consumer)."""
+def _ws_t(nbytes: int, dev):
+    """Scratch tensor for a column-partial slab (inside an armed deferred_reductions call it is kept alive until
+    the block's flush)."""
     t = torch.empty(max(int(nbytes), 4) // 4, dtype=F32, device=dev)
     keep = K.KEEP_WS[0]
     if keep is not None and K.ARMED[0]:
         keep.append(t)
+    return t
+
+
+def _ws(nbytes: int, dev):
+    """Scratch for a column-partial slab, as (pointer, bytes) for the NEXT library call (stream-ordered caching
+    allocator: the block is reused only by work queued after the kernel that consumes it -- inside a
+    deferred_reductions block the slab is kept alive until the block's flush, which is then that consumer).  The
+    tensor itself is released at once: no other allocation may come between this and the call that uses it (it
+    could be handed the same block) -- hold a ``_ws_t`` tensor instead where one must."""
+    t = _ws_t(nbytes, dev)
     return ptr(t), t.numel() * 4
 
 
@@ -2025,12 +2034,13 @@ class EncoderLayerFn(torch.autograd.Function):
         M = B * T
         fused = _ATTN_QV and not _KBIAS_GRAD
         L = _lib.lib()
-        # one scratch block for the relpos slab (WavLM, deterministic mode) and the q / v bias slab: two _ws calls
-        # would hand out the same freed block twice (the caching allocator reuses it for the second request)
+        # one scratch tensor, held until the call, for the relpos slab (WavLM, deterministic mode) and the q / v bias
+        # slab (a released _ws block would be handed out again to the dgate / dtab allocations below)
         rws = L.dph_attention_bwd_relpos_workspace(B, T, H) if wl is not None else 0
         rws = (rws + 255) // 256 * 256
         qvb = L.dph_attention_bwd_qv_workspace(B, T, H) if fused else 0
-        wsp, _ = _ws(rws + qvb, dev)
+        wst = _ws_t(rws + qvb, dev)
+        wsp = ptr(wst)
         if fused:
             Dh = dqkv.shape[1] // 3
             base = dbqkv.data_ptr()
@@ -2054,6 +2064,7 @@ class EncoderLayerFn(torch.autograd.Function):
         else:
             call("dph_attention_bwd_relpos", *args, _s())
             _qkv_bias_grad(dqkv, dbqkv, M, dev)
+        del wst
         return dgate, dtab
 
     @staticmethod

@@ -799,3 +799,35 @@ def test_attention_bwd_qv_bias_sums(T, lens, p, zero_head, relpos, split, monkey
     if L.dph_get_deterministic():
         d3, db3 = run(True, defer=True)
         assert torch.equal(d3, d0) and torch.equal(db3, db1)
+
+
+@pytest.mark.parametrize("B,T,H", [(16, 499, 12), (3, 131, 16), (2, 77, 5), (1, 33, 40)])
+def test_attention_bwd_prep_rowdot(B, T, H):
+    """dph_attention_bwd_prep: D[b][h][t] = rowdot(dO_m, O_u) and dhead_mask[h] += sum_(b,t) D against float64 on
+    the same bf16 / fp32 inputs, with an exactly-zero head (its D is 0, O_u never read), pruned head counts (8-lane
+    groups not filling a wave) and H > 32 (one row per block); repeated runs bitwise equal."""
+    from dphubert_amd import _lib
+    from dphubert_amd._lib import call, ptr
+    torch.manual_seed(11)
+    D = H * 64
+    g = torch.randn(B * T, D, device=DEV).to(torch.bfloat16)
+    o_u = torch.randn(B * T, D, device=DEV)
+    hm = torch.rand(H, device=DEV) + 0.1
+    hm[H // 2] = 0.0
+    o_u.view(B * T, H, 64)[:, H // 2] = float("nan")   # a skipped head's O_u is never written
+    s = _lib.stream_ptr()
+    outs = []
+    for _ in range(2):
+        Dv = torch.full((B * H * T,), float("nan"), device=DEV)
+        dhm = torch.full((H,), 0.25, device=DEV)
+        call("dph_attention_bwd_prep", ptr(g), ptr(o_u), ptr(hm), ptr(Dv), ptr(dhm), B, T, H, *prep_ws(B, T, H), s)
+        torch.cuda.synchronize()
+        outs.append((Dv.cpu(), dhm.cpu()))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    ou = o_u.double().cpu().view(B, T, H, 64).clone()
+    ou[:, :, H // 2] = 0.0
+    want = (g.double().cpu().view(B, T, H, 64) * ou).sum(-1).permute(0, 2, 1).reshape(-1)   # [B][H][T]
+    Dv, dhm = outs[0]
+    torch.testing.assert_close(Dv.double(), want, rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(dhm.double(), want.view(B, H, T).sum((0, 2)) + 0.25, rtol=1e-5, atol=1e-2)
+    assert torch.equal(Dv.view(B, H, T)[:, H // 2], torch.zeros(B, T))
