@@ -220,8 +220,12 @@ def test_model_step_passes_stored_keep_bits(monkeypatch):
     real = ops.call
 
     def spy(name, *args):
-        if name in ("dph_attention_fwd", "dph_attention_bwd"):
-            seen.append((name, args[-2]))
+        # (keep_bits: argument 12 of the forward, 13 of the backward -- dph_attention_bwd_qv, ABI 24, appends the
+        # q / v bias outputs after it)
+        if name == "dph_attention_fwd":
+            seen.append((name, args[12]))
+        elif name in ("dph_attention_bwd", "dph_attention_bwd_qv"):
+            seen.append(("dph_attention_bwd", args[13]))
         return real(name, *args)
     monkeypatch.setattr(ops, "call", spy)
     wave = torch.randn(2, 16000, device=DEV) * 0.1
