@@ -659,7 +659,7 @@ __global__ void __launch_bounds__(256) ln_fwd16_kernel(const XT* __restrict__ x,
 // per-block slab row ws[block][3][D] for slab_reduce.  The two halves of a wave (two rows, same columns) combine
 // their column partials with one lane ^ 32 exchange before the cross-wave LDS sum.
 template <int NE, typename XT = bf16_t, typename DT = bf16_t>
-__global__ void __launch_bounds__(512) ln_bwd16_kernel(
+__global__ void __launch_bounds__(512, 4) ln_bwd16_kernel(
     const bf16_t* __restrict__ dy, const XT* __restrict__ x, const float* __restrict__ gamma,
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in, DT* __restrict__ dx,
     float* __restrict__ dgamma, float* __restrict__ dbeta, int64_t rows, bf16_t* __restrict__ branch, float branch_p,
@@ -697,6 +697,16 @@ __global__ void __launch_bounds__(512) ln_bwd16_kernel(
     gq[c][0] = *reinterpret_cast<const float4*>(gamma + col);
     gq[c][1] = *reinterpret_cast<const float4*>(gamma + col + 4);
   }
+  // the branch's pre-mask output (layer-mask gradient dot), also issued with the row loads: read after the dx
+  // stores it was a second dependent HBM round trip per row
+  // (post-norm bf16 rows only: the fp32 residual-stream variants have no registers to spare)
+  constexpr bool EARLY_PRE = std::is_same<XT, bf16_t>::value && std::is_same<DT, bf16_t>::value;
+  uint4 prer[NC];
+  const bool want_pre = branch != nullptr && branch_sdot != nullptr && ok;
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+    prer[c] = (EARLY_PRE && want_pre) ? *reinterpret_cast<const uint4*>(branch_pre + row * D + (c * 32 + hl) * 8)
+                                      : make_uint4(0u, 0u, 0u, 0u);
   const float binv_keep = branch_p > 0.f ? 1.f / (1.f - branch_p) : 1.f;
   const float bsm = branch_smask ? *branch_smask : 1.0f;
   float s1 = 0.f, s2 = 0.f;
@@ -745,7 +755,7 @@ __global__ void __launch_bounds__(512) ln_bwd16_kernel(
     if (branch) {
       float pre[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, z[8], bo[8];
       if (branch_sdot && ok) {
-        const uint4 rp = *reinterpret_cast<const uint4*>(branch_pre + row * D + col);
+        const uint4 rp = EARLY_PRE ? prer[c] : *reinterpret_cast<const uint4*>(branch_pre + row * D + col);
         const uint32_t wp[4] = {rp.x, rp.y, rp.z, rp.w};
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
