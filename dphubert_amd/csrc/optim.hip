@@ -32,7 +32,10 @@ __global__ void __launch_bounds__(256) sumsq_kernel(const DphTensorSlot* __restr
                                                     const int64_t* __restrict__ cstart, int64_t n_chunks,
                                                     float* __restrict__ out) {
   __shared__ float red[4];
-  float s = 0.f;
+  // four independent accumulators: a full chunk's eight float4 loads per thread are issued four at a time (one
+  // dependent add chain and one load per trip ran the 382 MB read at ~5.4 TB/s)
+  float s = 0.f, sa = 0.f, sb = 0.f, sc = 0.f;
+  auto sq = [](float4 v) { return v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w; };
   for (int64_t c = blockIdx.x; c < n_chunks; c += gridDim.x) {
     const DphTensorSlot sl = slots[cslot[c]];
     if (!sl.grad) continue;
@@ -42,14 +45,20 @@ __global__ void __launch_bounds__(256) sumsq_kernel(const DphTensorSlot* __restr
     if ((reinterpret_cast<uintptr_t>(sl.grad + s0) & 15) == 0) {
       const int64_t n4 = (s1 - s0) >> 2;
       const float4* g4 = reinterpret_cast<const float4*>(sl.grad + s0);
-      for (int64_t j = threadIdx.x; j < n4; j += 256) {
-        const float4 v = g4[j];
-        s += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+      int64_t j = threadIdx.x;
+      for (; j + 768 < n4; j += 1024) {
+        const float4 v0 = g4[j], v1 = g4[j + 256], v2 = g4[j + 512], v3 = g4[j + 768];
+        s += sq(v0);
+        sa += sq(v1);
+        sb += sq(v2);
+        sc += sq(v3);
       }
+      for (; j < n4; j += 256) s += sq(g4[j]);
       i = s0 + 4 * n4;
     }
     for (i += threadIdx.x; i < s1; i += 256) s += sl.grad[i] * sl.grad[i];
   }
+  s = (s + sa) + (sb + sc);
   s = wave_sum(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
@@ -105,6 +114,8 @@ __global__ void __launch_bounds__(256) adamw_kernel(const DphTensorSlot* __restr
     float4* p4 = reinterpret_cast<float4*>(sl.param + s0);
     float4* m4 = reinterpret_cast<float4*>(sl.exp_avg + s0);
     float4* v4 = reinterpret_cast<float4*>(sl.exp_avg_sq + s0);
+    // (two quads per trip -- eight loads before the first store -- measured slower: 84 VGPRs, 5 waves per SIMD,
+    // 467 -> 532 us per step for the 95 M-parameter student, profiles/r6_optim_ab.txt)
     for (int64_t j = threadIdx.x; j < n4; j += 256) {
       float4 g = g4[j], p = p4[j], m = m4[j], v = v4[j];
       upd(g.x, p.x, m.x, v.x, g.x);
